@@ -1,0 +1,202 @@
+// BN254 prime-field arithmetic (Fp and Fr), 8 x 32-bit limbs, Montgomery form.
+//
+// CDNA4 mapping: every limb product is one `v_mad_u64_u32` (32x32+64 -> 64);
+// the no-carry CIOS variant is valid because both moduli have top word
+// 0x30644e72 < 2^31-1, so the (m*p + t) accumulator never needs a 9th limb.
+// One thread owns one field element (8 VGPRs); kernels are thread-per-item.
+//
+// The same inline functions are compiled for the host (CPU batch path used by
+// the control plane and the CPU test-suite) and for gfx950 device kernels.
+// Replaces kyber's bn256 gfP (reference: lib/suite.go:10, external kyber).
+#pragma once
+#include <cstdint>
+#include <hip/hip_runtime.h>
+#include "constants.h"
+
+#define DX_HD __host__ __device__ __forceinline__
+#define DX_NI __host__ __device__ __noinline__ inline
+// The Montgomery multiply is force-inlined into device code (register
+// allocation across a whole Fp2/Fp6 product) but kept out-of-line on the host,
+// where x86 instruction selection of thousands of unrolled 64-bit MACs would
+// otherwise dominate build time.
+#ifdef __HIP_DEVICE_COMPILE__
+#define DX_MUL DX_HD
+#else
+#define DX_MUL __host__ __device__ __noinline__ inline
+#endif
+
+namespace dx {
+
+DX_HD uint32_t addc32(uint32_t a, uint32_t b, uint32_t &carry) {
+  uint64_t s = (uint64_t)a + b + carry;
+  carry = (uint32_t)(s >> 32);
+  return (uint32_t)s;
+}
+DX_HD uint32_t subb32(uint32_t a, uint32_t b, uint32_t &borrow) {
+  uint64_t d = (uint64_t)a - b - borrow;
+  borrow = (uint32_t)(d >> 63);
+  return (uint32_t)d;
+}
+
+template <class PR>
+struct FieldT {
+  uint32_t v[8];
+
+  static DX_HD FieldT zero() {
+    FieldT r;
+#pragma unroll
+    for (int i = 0; i < 8; i++) r.v[i] = 0;
+    return r;
+  }
+  static DX_HD FieldT one() {
+    FieldT r;
+#pragma unroll
+    for (int i = 0; i < 8; i++) r.v[i] = PR::ONE[i];
+    return r;
+  }
+  static DX_HD FieldT from_limbs(const uint32_t *p) {
+    FieldT r;
+#pragma unroll
+    for (int i = 0; i < 8; i++) r.v[i] = p[i];
+    return r;
+  }
+  DX_HD bool is_zero() const {
+    uint32_t acc = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) acc |= v[i];
+    return acc == 0;
+  }
+  DX_HD bool operator==(const FieldT &o) const {
+    uint32_t acc = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) acc |= v[i] ^ o.v[i];
+    return acc == 0;
+  }
+  DX_HD bool operator!=(const FieldT &o) const { return !(*this == o); }
+};
+
+// r = a if borrow==0 after t-MOD else t (i.e. conditional subtract of the modulus)
+template <class PR>
+DX_HD void cond_sub_mod(uint32_t *t) {
+  uint32_t s[8];
+  uint32_t borrow = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) s[i] = subb32(t[i], PR::MOD[i], borrow);
+  // borrow==1 -> t < MOD -> keep t
+#pragma unroll
+  for (int i = 0; i < 8; i++) t[i] = borrow ? t[i] : s[i];
+}
+
+template <class PR>
+DX_HD FieldT<PR> fadd(const FieldT<PR> &a, const FieldT<PR> &b) {
+  FieldT<PR> r;
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = addc32(a.v[i], b.v[i], c);
+  cond_sub_mod<PR>(r.v);
+  return r;
+}
+
+template <class PR>
+DX_HD FieldT<PR> fsub(const FieldT<PR> &a, const FieldT<PR> &b) {
+  FieldT<PR> r;
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = subb32(a.v[i], b.v[i], br);
+  uint32_t mask = 0u - br;
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = addc32(r.v[i], PR::MOD[i] & mask, c);
+  return r;
+}
+
+template <class PR>
+DX_HD FieldT<PR> fneg(const FieldT<PR> &a) {
+  return fsub(FieldT<PR>::zero(), a);
+}
+
+template <class PR>
+DX_HD FieldT<PR> fdbl(const FieldT<PR> &a) {
+  return fadd(a, a);
+}
+
+// Montgomery multiplication, no-carry CIOS. a*b*2^-256 mod MOD.
+template <class PR>
+DX_MUL FieldT<PR> fmul(const FieldT<PR> &a, const FieldT<PR> &b) {
+  uint32_t t[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) t[j] = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint32_t bi = b.v[i];
+    uint64_t x = (uint64_t)a.v[0] * bi + t[0];
+    uint32_t A = (uint32_t)(x >> 32);
+    uint32_t t0 = (uint32_t)x;
+    uint32_t m = t0 * PR::INV;
+    uint64_t y = (uint64_t)m * PR::MOD[0] + t0;
+    uint32_t C = (uint32_t)(y >> 32);
+#pragma unroll
+    for (int j = 1; j < 8; j++) {
+      x = (uint64_t)a.v[j] * bi + t[j] + A;
+      A = (uint32_t)(x >> 32);
+      y = (uint64_t)m * PR::MOD[j] + (uint32_t)x + C;
+      C = (uint32_t)(y >> 32);
+      t[j - 1] = (uint32_t)y;
+    }
+    t[7] = C + A;
+  }
+  cond_sub_mod<PR>(t);
+  FieldT<PR> r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = t[i];
+  return r;
+}
+
+template <class PR>
+DX_HD FieldT<PR> fsqr(const FieldT<PR> &a) {
+  return fmul(a, a);
+}
+
+// a^e for a little-endian 8-limb exponent (square-and-multiply, MSB first).
+template <class PR>
+DX_NI FieldT<PR> fpow(const FieldT<PR> &a, const uint32_t *e) {
+  FieldT<PR> r = FieldT<PR>::one();
+  for (int i = 7; i >= 0; i--) {
+    for (int b = 31; b >= 0; b--) {
+      r = fsqr(r);
+      if ((e[i] >> b) & 1u) r = fmul(r, a);
+    }
+  }
+  return r;
+}
+
+template <class PR>
+DX_HD FieldT<PR> finv(const FieldT<PR> &a) {
+  return fpow(a, PR::MODM2);
+}
+
+// canonical integer (limbs, little endian) <-> Montgomery
+template <class PR>
+DX_HD FieldT<PR> to_mont(const FieldT<PR> &a) {
+  return fmul(a, FieldT<PR>::from_limbs(PR::R2));
+}
+template <class PR>
+DX_HD FieldT<PR> from_mont(const FieldT<PR> &a) {
+  FieldT<PR> one = FieldT<PR>::zero();
+  one.v[0] = 1;
+  return fmul(a, one);
+}
+
+// Reduce an arbitrary 256-bit integer (little-endian limbs) below MOD.
+// Inputs are < 2^256 < 6*MOD, so at most 5 subtractions are needed.
+template <class PR>
+DX_HD FieldT<PR> reduce_256(const uint32_t *x) {
+  FieldT<PR> r = FieldT<PR>::from_limbs(x);
+  for (int k = 0; k < 5; k++) cond_sub_mod<PR>(r.v);
+  return r;
+}
+
+using Fp = FieldT<FpParams>;
+using Fr = FieldT<FrParams>;
+
+}  // namespace dx

@@ -1,0 +1,209 @@
+// Field, G1 and ElGamal batch ops (K1-K5, K9 of SURVEY §2.3): unlynx EncryptIntGetR,
+// IntToPoint, CipherVector.Add, DecryptIntWithNeg (BSGS).
+// C ABI consumed by drynx_amd/native (ctypes).  Every entry point takes
+// (on_gpu, stream): on_gpu launches a gfx950 kernel on that HIP stream (torch's
+// current stream), otherwise the same functor runs on the host thread pool.
+#include "common.h"
+
+extern "C" {
+// ---------------------------------------------------------------- field utils
+int dx_fp_to_mont(int on_gpu, void *stream, const uint32_t *in, uint32_t *out, int64_t n) {
+  auto op = [=] __host__ __device__(int64_t i) { at<Fp>(out, i) = to_mont(at<Fp>(in, i)); };
+  return run(on_gpu, stream, n, op, false, "fp_to_mont");
+}
+int dx_fp_from_mont(int on_gpu, void *stream, const uint32_t *in, uint32_t *out, int64_t n) {
+  auto op = [=] __host__ __device__(int64_t i) { at<Fp>(out, i) = from_mont(at<Fp>(in, i)); };
+  return run(on_gpu, stream, n, op, false, "fp_from_mont");
+}
+
+// Fr arithmetic on canonical scalars. op: 0 add, 1 sub, 2 mul, 3 neg(a), 4 inv(a), 5 reduce(a)
+int dx_fr_arith(int on_gpu, void *stream, int opc, const uint32_t *a, const uint32_t *b, uint32_t *out, int64_t n,
+                int b_bcast) {
+  auto op = [=] __host__ __device__(int64_t i) {
+    Fr x = reduce_256<FrParams>(a + 8 * i);
+    Fr y = b ? reduce_256<FrParams>(b + 8 * (b_bcast ? 0 : i)) : Fr::zero();
+    Fr r;
+    switch (opc) {
+      case 0: r = fadd(x, y); break;
+      case 1: r = fsub(x, y); break;
+      case 2: r = from_mont(fmul(to_mont(x), to_mont(y))); break;
+      case 3: r = fneg(x); break;
+      case 4: r = from_mont(finv(to_mont(x))); break;
+      default: r = x; break;
+    }
+    at<Fr>(out, i) = r;
+  };
+  return run(on_gpu, stream, n, op, false, "fr_arith");
+}
+
+// ---------------------------------------------------------------- G1
+int dx_g1_fb_table(int on_gpu, void *stream, const uint32_t *base_aff, uint32_t *table) {
+  auto op = [=] __host__ __device__(int64_t i) {
+    int w = (int)(i >> 8), d = (int)(i & 255);
+    uint32_t k[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    // k = d << (8w)
+    int bit = 8 * w;
+    uint64_t v = (uint64_t)d << (bit & 31);
+    k[bit >> 5] = (uint32_t)v;
+    if ((bit >> 5) + 1 < 8) k[(bit >> 5) + 1] = (uint32_t)(v >> 32);
+    G1J p = G1J::from_aff(at<G1A>(base_aff, 0));
+    at<G1A>(table, i) = d ? to_affine(scalar_mul(p, k)) : G1A::inf();
+  };
+  return run(on_gpu, stream, 32 * 256, op, true, "g1_fb_table");
+}
+
+int dx_g1_fb_mul(int on_gpu, void *stream, const uint32_t *table, const uint32_t *scalars, uint32_t *out, int64_t n) {
+  auto op = [=] __host__ __device__(int64_t i) {
+    at<G1J>(out, i) = fixed_base_mul(reinterpret_cast<const G1A *>(table), scalars + 8 * i);
+  };
+  return run(on_gpu, stream, n, op, true, "g1_fb_mul");
+}
+
+// m * base for signed 64-bit m (unlynx IntToPoint).
+int dx_g1_fb_mul_i64(int on_gpu, void *stream, const uint32_t *table, const int64_t *m, uint32_t *out, int64_t n) {
+  auto op = [=] __host__ __device__(int64_t i) {
+    uint32_t k[8];
+    bool ng;
+    signed_to_scalar(m[i], k, ng);
+    G1J r = fixed_base_mul(reinterpret_cast<const G1A *>(table), k);
+    at<G1J>(out, i) = ng ? jneg(r) : r;
+  };
+  return run(on_gpu, stream, n, op, true, "g1_fb_mul_i64");
+}
+
+// Variable base: out[i] = k[i] * P[i or 0]
+int dx_g1_mul(int on_gpu, void *stream, const uint32_t *pts_jac, const uint32_t *scalars, uint32_t *out, int64_t n,
+              int pt_bcast, int k_bcast) {
+  auto op = [=] __host__ __device__(int64_t i) {
+    at<G1J>(out, i) = scalar_mul(at<G1J>(pts_jac, pt_bcast ? 0 : i), scalars + 8 * (k_bcast ? 0 : i));
+  };
+  return run(on_gpu, stream, n, op, true, "g1_mul");
+}
+
+// out = a +/- b (b may be broadcast)
+int dx_g1_add(int on_gpu, void *stream, const uint32_t *a, const uint32_t *b, uint32_t *out, int64_t n, int subtract,
+              int b_bcast) {
+  auto op = [=] __host__ __device__(int64_t i) {
+    G1J q = at<G1J>(b, b_bcast ? 0 : i);
+    if (subtract) q = jneg(q);
+    at<G1J>(out, i) = jadd(at<G1J>(a, i), q);
+  };
+  return run(on_gpu, stream, n, op, false, "g1_add");
+}
+
+int dx_g1_to_affine(int on_gpu, void *stream, const uint32_t *jac, uint32_t *aff, int64_t n) {
+  auto op = [=] __host__ __device__(int64_t i) { at<G1A>(aff, i) = to_affine(at<G1J>(jac, i)); };
+  return run(on_gpu, stream, n, op, true, "g1_to_affine");
+}
+
+int dx_g1_from_affine(int on_gpu, void *stream, const uint32_t *aff, uint32_t *jac, int64_t n) {
+  auto op = [=] __host__ __device__(int64_t i) { at<G1J>(jac, i) = G1J::from_aff(at<G1A>(aff, i)); };
+  return run(on_gpu, stream, n, op, false, "g1_from_affine");
+}
+
+int dx_g1_eq(int on_gpu, void *stream, const uint32_t *a, const uint32_t *b, uint8_t *out, int64_t n) {
+  auto op = [=] __host__ __device__(int64_t i) { out[i] = jeq(at<G1J>(a, i), at<G1J>(b, i)) ? 1 : 0; };
+  return run(on_gpu, stream, n, op, false, "g1_eq");
+}
+
+int dx_g1_on_curve(int on_gpu, void *stream, const uint32_t *aff, uint8_t *out, int64_t n) {
+  auto op = [=] __host__ __device__(int64_t i) { out[i] = on_curve(at<G1A>(aff, i)) ? 1 : 0; };
+  return run(on_gpu, stream, n, op, false, "g1_on_curve");
+}
+
+// Partial sums over axis 0 of in[n_items][n_groups] (Jacobian):
+// out[c][g] = sum_{i in chunk c} in[i][g], chunk = `chunk` items.
+int dx_g1_sum_chunks(int on_gpu, void *stream, const uint32_t *in, uint32_t *out, int64_t n_items, int64_t n_groups,
+                     int64_t chunk) {
+  int64_t n_chunks = (n_items + chunk - 1) / chunk;
+  auto op = [=] __host__ __device__(int64_t t) {
+    int64_t c = t / n_groups, g = t % n_groups;
+    int64_t s = c * chunk, e = s + chunk < n_items ? s + chunk : n_items;
+    G1J acc = G1J::inf();
+    for (int64_t i = s; i < e; i++) acc = jadd(acc, at<G1J>(in, i * n_groups + g));
+    at<G1J>(out, t) = acc;
+  };
+  return run(on_gpu, stream, n_chunks * n_groups, op, true, "g1_sum_chunks");
+}
+
+// ---------------------------------------------------------------- ElGamal
+// K = r*B, C = m*B + r*P  (unlynx EncryptIntGetR with caller-provided r)
+int dx_elgamal_encrypt(int on_gpu, void *stream, const uint32_t *tabB, const uint32_t *tabP, const int64_t *m,
+                       const uint32_t *r, uint32_t *outK, uint32_t *outC, int64_t n) {
+  auto op = [=] __host__ __device__(int64_t i) {
+    const G1A *TB = reinterpret_cast<const G1A *>(tabB);
+    const G1A *TP = reinterpret_cast<const G1A *>(tabP);
+    uint32_t k[8];
+    bool ng;
+    signed_to_scalar(m[i], k, ng);
+    G1J mB = fixed_base_mul(TB, k);
+    if (ng) mB = jneg(mB);
+    at<G1J>(outK, i) = fixed_base_mul(TB, r + 8 * i);
+    at<G1J>(outC, i) = jadd(mB, fixed_base_mul(TP, r + 8 * i));
+  };
+  return run(on_gpu, stream, n, op, true, "elgamal_encrypt");
+}
+
+// ---------------------------------------------------------------- BSGS dlog
+// Open-addressing table (cap = power of two): keys[] u64 (0 = empty), vals[] i32.
+int dx_bsgs_build(int on_gpu, void *stream, const uint32_t *tabB, int64_t m_baby, uint64_t *keys, int32_t *vals,
+                  int64_t cap) {
+  auto op = [=] __host__ __device__(int64_t j) {
+    uint32_t k[8] = {(uint32_t)j, (uint32_t)((uint64_t)j >> 32), 0, 0, 0, 0, 0, 0};
+    G1A a = to_affine(fixed_base_mul(reinterpret_cast<const G1A *>(tabB), k));
+    uint64_t key = j == 0 ? 1ull : point_key(a);  // j==0: infinity, handled by the solver
+    if (j == 0) return;
+    uint64_t h = mix64(key) & (uint64_t)(cap - 1);
+    int32_t val = (int32_t)((j << 1) | (a.y.v[0] & 1u));  // y parity disambiguates +/-j
+    for (int64_t probe = 0; probe < cap; probe++) {
+      uint64_t old;
+      if (cas64(&keys[h], 0ull, key, old) || old == key) {
+        vals[h] = val;
+        return;
+      }
+      h = (h + 1) & (uint64_t)(cap - 1);
+    }
+  };
+  return run(on_gpu, stream, m_baby, op, true, "bsgs_build");
+}
+
+// For each target T_i (affine, = m_i*B + offset*B with m_i + offset in [0, m_baby*n_giant)),
+// find m = j + g*m_baby with T - g*(m_baby*B) = +/- j*B. Outputs value-offset.
+int dx_bsgs_solve(int on_gpu, void *stream, const uint32_t *targets_jac, const uint32_t *giant_aff, const uint64_t *keys,
+                  const int32_t *vals, int64_t cap, int64_t m_baby, int64_t n_giant, int64_t offset, int64_t *out,
+                  uint8_t *found, int64_t n) {
+  auto op = [=] __host__ __device__(int64_t i) {
+    G1J cur = at<G1J>(targets_jac, i);
+    G1A gneg = aneg(at<G1A>(giant_aff, 0));
+    found[i] = 0;
+    out[i] = 0;
+    for (int64_t g = 0; g < n_giant; g++) {
+      if (cur.is_inf()) {
+        out[i] = g * m_baby - offset;
+        found[i] = 1;
+        return;
+      }
+      G1A a = to_affine(cur);
+      uint64_t key = point_key(a);
+      uint64_t h = mix64(key) & (uint64_t)(cap - 1);
+      for (int64_t probe = 0; probe < cap; probe++) {
+        uint64_t kk = keys[h];
+        if (kk == 0) break;
+        if (kk == key) {
+          int64_t j = vals[h] >> 1;
+          bool same = (uint32_t)(vals[h] & 1) == (a.y.v[0] & 1u);
+          out[i] = g * m_baby + (same ? j : -j) - offset;
+          found[i] = 1;
+          return;
+        }
+        h = (h + 1) & (uint64_t)(cap - 1);
+      }
+      cur = jadd_mixed(cur, gneg);
+    }
+  };
+  return run(on_gpu, stream, n, op, true, "bsgs_solve");
+}
+
+
+int dx_version() { return 1; }
+}  // extern "C"

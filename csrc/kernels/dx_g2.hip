@@ -1,0 +1,48 @@
+// G2 batch ops (K6): BB-signature setup and range-proof V_ij = v_ij * A_{i,phi_j}
+// (lib/range/range_proof.go:259-288,392).
+// C ABI consumed by drynx_amd/native (ctypes).  Every entry point takes
+// (on_gpu, stream): on_gpu launches a gfx950 kernel on that HIP stream (torch's
+// current stream), otherwise the same functor runs on the host thread pool.
+#include "common.h"
+
+extern "C" {
+// ---------------------------------------------------------------- G2
+int dx_g2_fb_table(int on_gpu, void *stream, const uint32_t *base_aff, uint32_t *table) {
+  auto op = [=] __host__ __device__(int64_t i) {
+    int w = (int)(i >> 8), d = (int)(i & 255);
+    uint32_t k[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    int bit = 8 * w;
+    uint64_t v = (uint64_t)d << (bit & 31);
+    k[bit >> 5] = (uint32_t)v;
+    if ((bit >> 5) + 1 < 8) k[(bit >> 5) + 1] = (uint32_t)(v >> 32);
+    G2J p = G2J::from_aff(at<G2A>(base_aff, 0));
+    at<G2A>(table, i) = d ? to_affine(scalar_mul(p, k)) : G2A::inf();
+  };
+  return run(on_gpu, stream, 32 * 256, op, true, "g2_fb_table");
+}
+
+// out[i] = k[i] * base, table chosen per item from tables[tab_idx[i]] (tab_idx may be null -> table 0)
+int dx_g2_fb_mul(int on_gpu, void *stream, const uint32_t *tables, const int32_t *tab_idx, const uint32_t *scalars,
+                 uint32_t *out_aff, int64_t n) {
+  auto op = [=] __host__ __device__(int64_t i) {
+    const G2A *T = reinterpret_cast<const G2A *>(tables) + (int64_t)(tab_idx ? tab_idx[i] : 0) * 8192;
+    at<G2A>(out_aff, i) = to_affine(fixed_base_mul(T, scalars + 8 * i));
+  };
+  return run(on_gpu, stream, n, op, true, "g2_fb_mul");
+}
+
+int dx_g2_mul(int on_gpu, void *stream, const uint32_t *pts_aff, const uint32_t *scalars, uint32_t *out_aff, int64_t n,
+              int pt_bcast) {
+  auto op = [=] __host__ __device__(int64_t i) {
+    G2J p = G2J::from_aff(at<G2A>(pts_aff, pt_bcast ? 0 : i));
+    at<G2A>(out_aff, i) = to_affine(scalar_mul(p, scalars + 8 * i));
+  };
+  return run(on_gpu, stream, n, op, true, "g2_mul");
+}
+
+int dx_g2_on_curve(int on_gpu, void *stream, const uint32_t *aff, uint8_t *out, int64_t n) {
+  auto op = [=] __host__ __device__(int64_t i) { out[i] = on_curve(at<G2A>(aff, i)) ? 1 : 0; };
+  return run(on_gpu, stream, n, op, false, "g2_on_curve");
+}
+
+}  // extern "C"

@@ -1,0 +1,82 @@
+// Pairing / GT batch ops (K7, K8): kyber bn256 Pair + GT arithmetic used by
+// lib/range/range_proof.go:396-397 (prove) and :540-546 (verify).
+// C ABI consumed by drynx_amd/native (ctypes).  Every entry point takes
+// (on_gpu, stream): on_gpu launches a gfx950 kernel on that HIP stream (torch's
+// current stream), otherwise the same functor runs on the host thread pool.
+#include "common.h"
+
+extern "C" {
+// ---------------------------------------------------------------- pairing / GT
+int dx_miller_loop(int on_gpu, void *stream, const uint32_t *P_aff, const uint32_t *Q_aff, uint32_t *out, int64_t n) {
+  auto op = [=] __host__ __device__(int64_t i) { at<Fp12>(out, i) = miller_loop(at<G1A>(P_aff, i), at<G2A>(Q_aff, i)); };
+  return run(on_gpu, stream, n, op, true, "miller_loop");
+}
+
+int dx_final_exp(int on_gpu, void *stream, const uint32_t *in, uint32_t *out, int64_t n) {
+  auto op = [=] __host__ __device__(int64_t i) { at<Fp12>(out, i) = final_exp(at<Fp12>(in, i)); };
+  return run(on_gpu, stream, n, op, true, "final_exp");
+}
+
+int dx_pairing(int on_gpu, void *stream, const uint32_t *P_aff, const uint32_t *Q_aff, uint32_t *out, int64_t n) {
+  auto op = [=] __host__ __device__(int64_t i) { at<Fp12>(out, i) = pairing(at<G1A>(P_aff, i), at<G2A>(Q_aff, i)); };
+  return run(on_gpu, stream, n, op, true, "pairing");
+}
+
+int dx_gt_mul(int on_gpu, void *stream, const uint32_t *a, const uint32_t *b, uint32_t *out, int64_t n) {
+  auto op = [=] __host__ __device__(int64_t i) { at<Fp12>(out, i) = mul(at<Fp12>(a, i), at<Fp12>(b, i)); };
+  return run(on_gpu, stream, n, op, true, "gt_mul");
+}
+
+int dx_gt_pow(int on_gpu, void *stream, const uint32_t *a, const uint32_t *scalars, uint32_t *out, int64_t n,
+              int a_bcast) {
+  auto op = [=] __host__ __device__(int64_t i) {
+    at<Fp12>(out, i) = gt_pow(at<Fp12>(a, a_bcast ? 0 : i), scalars + 8 * i);
+  };
+  return run(on_gpu, stream, n, op, true, "gt_pow");
+}
+
+int dx_gt_eq(int on_gpu, void *stream, const uint32_t *a, const uint32_t *b, uint8_t *out, int64_t n) {
+  auto op = [=] __host__ __device__(int64_t i) { out[i] = at<Fp12>(a, i) == at<Fp12>(b, i) ? 1 : 0; };
+  return run(on_gpu, stream, n, op, false, "gt_eq");
+}
+
+// comb table for fixed-base GT exponentiation (32 x 256 entries of Fp12)
+int dx_gt_fb_table(int on_gpu, void *stream, const uint32_t *base, uint32_t *table, int64_t n_bases) {
+  auto op = [=] __host__ __device__(int64_t t) {
+    int64_t b = t / 8192, i = t % 8192;
+    int w = (int)(i >> 8), d = (int)(i & 255);
+    uint32_t k[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    int bit = 8 * w;
+    uint64_t v = (uint64_t)d << (bit & 31);
+    k[bit >> 5] = (uint32_t)v;
+    if ((bit >> 5) + 1 < 8) k[(bit >> 5) + 1] = (uint32_t)(v >> 32);
+    at<Fp12>(table, t) = gt_pow(at<Fp12>(base, b), k);
+  };
+  return run(on_gpu, stream, n_bases * 8192, op, true, "gt_fb_table");
+}
+
+int dx_gt_fb_pow(int on_gpu, void *stream, const uint32_t *tables, const int32_t *tab_idx, const uint32_t *scalars,
+                 uint32_t *out, int64_t n) {
+  auto op = [=] __host__ __device__(int64_t i) {
+    const Fp12 *T = reinterpret_cast<const Fp12 *>(tables) + (int64_t)(tab_idx ? tab_idx[i] : 0) * 8192;
+    at<Fp12>(out, i) = gt_fixed_pow(T, scalars + 8 * i);
+  };
+  return run(on_gpu, stream, n, op, true, "gt_fb_pow");
+}
+
+// product over axis 0 chunks of in[n_items][n_groups] Fp12 (same scheme as g1_sum_chunks)
+int dx_gt_prod_chunks(int on_gpu, void *stream, const uint32_t *in, uint32_t *out, int64_t n_items, int64_t n_groups,
+                      int64_t chunk) {
+  int64_t n_chunks = (n_items + chunk - 1) / chunk;
+  auto op = [=] __host__ __device__(int64_t t) {
+    int64_t c = t / n_groups, g = t % n_groups;
+    int64_t s = c * chunk, e = s + chunk < n_items ? s + chunk : n_items;
+    Fp12 acc = Fp12::one();
+    for (int64_t i = s; i < e; i++) acc = mul(acc, at<Fp12>(in, i * n_groups + g));
+    at<Fp12>(out, t) = acc;
+  };
+  return run(on_gpu, stream, n_chunks * n_groups, op, true, "gt_prod_chunks");
+}
+
+
+}  // extern "C"

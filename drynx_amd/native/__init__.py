@@ -1,0 +1,413 @@
+"""ctypes binding of the in-tree native library (csrc/ -> libdrynx_native.so).
+
+Every op takes torch tensors.  If the tensors live on a GPU the gfx950 kernel
+is launched on torch's current HIP stream; otherwise the same functor runs on
+the host thread pool inside the library.  There is no pure-Python fallback for
+any op: if the library is missing the import fails loudly (and on a GPU box the
+driver can see exactly which .so was loaded).
+
+Tensor conventions (all int32 tensors carrying raw u32 limbs, little endian):
+  Fp / scalar : [..., 8]
+  G1 affine   : [..., 16]   (x, y) Montgomery, infinity = zeros
+  G1 Jacobian : [..., 24]
+  G2 affine   : [..., 32]
+  Fp12 (GT)   : [..., 96]
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libdrynx_native.so")
+
+_lib = None
+
+
+def _load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        if os.environ.get("DRYNX_AUTOBUILD", "1") == "1":
+            from . import build as _b
+
+            _b.build()
+        else:
+            raise ImportError(f"{LIB_PATH} missing: run `python -m drynx_amd.native.build`")
+    _lib = ctypes.CDLL(LIB_PATH)
+    _declare(_lib)
+    return _lib
+
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_L = ctypes.c_int64
+_U64 = ctypes.c_uint64
+
+_SIGS = {
+    "dx_fp_to_mont": [_I, _P, _P, _P, _L],
+    "dx_fp_from_mont": [_I, _P, _P, _P, _L],
+    "dx_fr_arith": [_I, _P, _I, _P, _P, _P, _L, _I],
+    "dx_g1_fb_table": [_I, _P, _P, _P],
+    "dx_g1_fb_mul": [_I, _P, _P, _P, _P, _L],
+    "dx_g1_fb_mul_i64": [_I, _P, _P, _P, _P, _L],
+    "dx_g1_mul": [_I, _P, _P, _P, _P, _L, _I, _I],
+    "dx_g1_add": [_I, _P, _P, _P, _P, _L, _I, _I],
+    "dx_g1_to_affine": [_I, _P, _P, _P, _L],
+    "dx_g1_from_affine": [_I, _P, _P, _P, _L],
+    "dx_g1_eq": [_I, _P, _P, _P, _P, _L],
+    "dx_g1_on_curve": [_I, _P, _P, _P, _L],
+    "dx_g1_sum_chunks": [_I, _P, _P, _P, _L, _L, _L],
+    "dx_elgamal_encrypt": [_I, _P, _P, _P, _P, _P, _P, _P, _L],
+    "dx_bsgs_build": [_I, _P, _P, _L, _P, _P, _L],
+    "dx_bsgs_solve": [_I, _P, _P, _P, _P, _P, _L, _L, _L, _L, _P, _P, _L],
+    "dx_g2_fb_table": [_I, _P, _P, _P],
+    "dx_g2_fb_mul": [_I, _P, _P, _P, _P, _P, _L],
+    "dx_g2_mul": [_I, _P, _P, _P, _P, _L, _I],
+    "dx_g2_on_curve": [_I, _P, _P, _P, _L],
+    "dx_miller_loop": [_I, _P, _P, _P, _P, _L],
+    "dx_final_exp": [_I, _P, _P, _P, _L],
+    "dx_pairing": [_I, _P, _P, _P, _P, _L],
+    "dx_gt_mul": [_I, _P, _P, _P, _P, _L],
+    "dx_gt_pow": [_I, _P, _P, _P, _P, _L, _I],
+    "dx_gt_eq": [_I, _P, _P, _P, _P, _L],
+    "dx_gt_fb_table": [_I, _P, _P, _P, _L],
+    "dx_gt_fb_pow": [_I, _P, _P, _P, _P, _P, _L],
+    "dx_gt_prod_chunks": [_I, _P, _P, _P, _L, _L, _L],
+    "dx_version": [],
+}
+
+
+def _declare(lib):
+    for name, args in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = ctypes.c_int
+
+
+def lib():
+    return _load()
+
+
+def loaded_path() -> str:
+    _load()
+    return LIB_PATH
+
+
+# ----------------------------------------------------------------------------- helpers
+def _ptr(t: torch.Tensor | None):
+    if t is None:
+        return None
+    assert t.is_contiguous(), "native ops need contiguous tensors"
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _ctx(*ts):
+    dev = None
+    for t in ts:
+        if t is not None:
+            dev = t.device
+            break
+    for t in ts:
+        if t is not None and t.device != dev:
+            raise ValueError(f"native op mixes devices {dev} and {t.device}")
+    if dev is not None and dev.type == "cuda":
+        return 1, ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    return 0, None
+
+
+def _call(name, *args):
+    rc = getattr(_load(), name)(*args)
+    if rc != 0:
+        raise RuntimeError(f"native op {name} failed (rc={rc})")
+
+
+def _rows(t: torch.Tensor, width: int) -> int:
+    assert t.dtype == torch.int32 and t.shape[-1] == width, (t.dtype, t.shape, width)
+    return t.numel() // width
+
+
+def empty_like_rows(ref: torch.Tensor, n: int, width: int) -> torch.Tensor:
+    return torch.empty((n, width), dtype=torch.int32, device=ref.device)
+
+
+# ----------------------------------------------------------------------------- field
+def fp_to_mont(x: torch.Tensor) -> torch.Tensor:
+    out = torch.empty_like(x)
+    g, s = _ctx(x)
+    _call("dx_fp_to_mont", g, s, _ptr(x), _ptr(out), _rows(x, 8))
+    return out
+
+
+def fp_from_mont(x: torch.Tensor) -> torch.Tensor:
+    out = torch.empty_like(x)
+    g, s = _ctx(x)
+    _call("dx_fp_from_mont", g, s, _ptr(x), _ptr(out), _rows(x, 8))
+    return out
+
+
+FR_ADD, FR_SUB, FR_MUL, FR_NEG, FR_INV, FR_REDUCE = range(6)
+
+
+def fr_arith(op: int, a: torch.Tensor, b: torch.Tensor | None = None) -> torch.Tensor:
+    n = _rows(a, 8)
+    out = torch.empty_like(a)
+    bb = b.contiguous() if b is not None else None
+    bcast = 1 if (bb is not None and bb.numel() == 8 and n != 1) else 0
+    g, s = _ctx(a, bb)
+    _call("dx_fr_arith", g, s, op, _ptr(a), _ptr(bb), _ptr(out), n, bcast)
+    return out
+
+
+# ----------------------------------------------------------------------------- G1
+def g1_fb_table(base_aff: torch.Tensor) -> torch.Tensor:
+    assert base_aff.numel() == 16
+    table = torch.empty((32 * 256, 16), dtype=torch.int32, device=base_aff.device)
+    g, s = _ctx(base_aff)
+    _call("dx_g1_fb_table", g, s, _ptr(base_aff.contiguous()), _ptr(table))
+    return table
+
+
+def g1_fb_mul(table: torch.Tensor, scalars: torch.Tensor) -> torch.Tensor:
+    n = _rows(scalars, 8)
+    out = torch.empty((n, 24), dtype=torch.int32, device=scalars.device)
+    g, s = _ctx(table, scalars)
+    _call("dx_g1_fb_mul", g, s, _ptr(table), _ptr(scalars), _ptr(out), n)
+    return out
+
+
+def g1_fb_mul_i64(table: torch.Tensor, m: torch.Tensor) -> torch.Tensor:
+    assert m.dtype == torch.int64
+    n = m.numel()
+    out = torch.empty((n, 24), dtype=torch.int32, device=m.device)
+    g, s = _ctx(table, m)
+    _call("dx_g1_fb_mul_i64", g, s, _ptr(table), _ptr(m.contiguous()), _ptr(out), n)
+    return out
+
+
+def g1_mul(pts_jac: torch.Tensor, scalars: torch.Tensor) -> torch.Tensor:
+    np_ = _rows(pts_jac, 24)
+    nk = _rows(scalars, 8)
+    n = max(np_, nk)
+    assert np_ in (1, n) and nk in (1, n)
+    out = torch.empty((n, 24), dtype=torch.int32, device=scalars.device)
+    g, s = _ctx(pts_jac, scalars)
+    _call("dx_g1_mul", g, s, _ptr(pts_jac), _ptr(scalars), _ptr(out), n, int(np_ == 1 and n > 1), int(nk == 1 and n > 1))
+    return out
+
+
+def g1_add(a: torch.Tensor, b: torch.Tensor, subtract: bool = False) -> torch.Tensor:
+    n = _rows(a, 24)
+    nb = _rows(b, 24)
+    assert nb in (1, n)
+    out = torch.empty((n, 24), dtype=torch.int32, device=a.device)
+    g, s = _ctx(a, b)
+    _call("dx_g1_add", g, s, _ptr(a), _ptr(b), _ptr(out), n, int(subtract), int(nb == 1 and n > 1))
+    return out
+
+
+def g1_to_affine(jac: torch.Tensor) -> torch.Tensor:
+    n = _rows(jac, 24)
+    out = torch.empty((n, 16), dtype=torch.int32, device=jac.device)
+    g, s = _ctx(jac)
+    _call("dx_g1_to_affine", g, s, _ptr(jac), _ptr(out), n)
+    return out
+
+
+def g1_from_affine(aff: torch.Tensor) -> torch.Tensor:
+    n = _rows(aff, 16)
+    out = torch.empty((n, 24), dtype=torch.int32, device=aff.device)
+    g, s = _ctx(aff)
+    _call("dx_g1_from_affine", g, s, _ptr(aff), _ptr(out), n)
+    return out
+
+
+def g1_eq(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    n = _rows(a, 24)
+    assert _rows(b, 24) == n
+    out = torch.empty((n,), dtype=torch.uint8, device=a.device)
+    g, s = _ctx(a, b)
+    _call("dx_g1_eq", g, s, _ptr(a), _ptr(b), _ptr(out), n)
+    return out
+
+
+def g1_on_curve(aff: torch.Tensor) -> torch.Tensor:
+    n = _rows(aff, 16)
+    out = torch.empty((n,), dtype=torch.uint8, device=aff.device)
+    g, s = _ctx(aff)
+    _call("dx_g1_on_curve", g, s, _ptr(aff), _ptr(out), n)
+    return out
+
+
+def g1_sum(x: torch.Tensor, chunk: int = 64) -> torch.Tensor:
+    """Sum over axis 0 of x[n_items, n_groups, 24] (Jacobian) -> [n_groups, 24].
+
+    Multi-pass chunked reduction: each pass has n_groups * ceil(items/chunk)
+    independent threads, so wide vectors and deep reductions both fill the GPU.
+    """
+    assert x.dim() == 3 and x.shape[-1] == 24
+    n_items, n_groups = x.shape[0], x.shape[1]
+    cur = x.contiguous()
+    if n_items == 0:
+        from ..crypto.bn254 import g1_infinity_jac
+
+        return g1_infinity_jac(n_groups, x.device)
+    while n_items > 1:
+        ch = max(2, min(chunk, n_items)) if n_groups >= 4096 else max(2, min(8, n_items))
+        n_chunks = (n_items + ch - 1) // ch
+        out = torch.empty((n_chunks, n_groups, 24), dtype=torch.int32, device=x.device)
+        g, s = _ctx(cur)
+        _call("dx_g1_sum_chunks", g, s, _ptr(cur), _ptr(out), n_items, n_groups, ch)
+        cur, n_items = out, n_chunks
+    return cur[0]
+
+
+# ----------------------------------------------------------------------------- ElGamal
+def elgamal_encrypt(tabB, tabP, m: torch.Tensor, r: torch.Tensor):
+    n = m.numel()
+    assert m.dtype == torch.int64 and _rows(r, 8) == n
+    K = torch.empty((n, 24), dtype=torch.int32, device=m.device)
+    C = torch.empty((n, 24), dtype=torch.int32, device=m.device)
+    g, s = _ctx(tabB, tabP, m, r)
+    _call("dx_elgamal_encrypt", g, s, _ptr(tabB), _ptr(tabP), _ptr(m.contiguous()), _ptr(r), _ptr(K), _ptr(C), n)
+    return K, C
+
+
+def bsgs_build(tabB: torch.Tensor, m_baby: int, cap: int):
+    assert cap & (cap - 1) == 0 and cap >= 2 * m_baby
+    keys = torch.zeros((cap,), dtype=torch.int64, device=tabB.device)
+    vals = torch.zeros((cap,), dtype=torch.int32, device=tabB.device)
+    g, s = _ctx(tabB)
+    _call("dx_bsgs_build", g, s, _ptr(tabB), m_baby, _ptr(keys), _ptr(vals), cap)
+    return keys, vals
+
+
+def bsgs_solve(targets_jac, giant_aff, keys, vals, m_baby: int, n_giant: int, offset: int):
+    n = _rows(targets_jac, 24)
+    out = torch.empty((n,), dtype=torch.int64, device=targets_jac.device)
+    found = torch.empty((n,), dtype=torch.uint8, device=targets_jac.device)
+    g, s = _ctx(targets_jac, giant_aff, keys, vals)
+    _call("dx_bsgs_solve", g, s, _ptr(targets_jac), _ptr(giant_aff), _ptr(keys), _ptr(vals), keys.numel(), m_baby,
+          n_giant, offset, _ptr(out), _ptr(found), n)
+    return out, found
+
+
+# ----------------------------------------------------------------------------- G2
+def g2_fb_table(base_aff: torch.Tensor) -> torch.Tensor:
+    assert base_aff.numel() == 32
+    table = torch.empty((32 * 256, 32), dtype=torch.int32, device=base_aff.device)
+    g, s = _ctx(base_aff)
+    _call("dx_g2_fb_table", g, s, _ptr(base_aff.contiguous()), _ptr(table))
+    return table
+
+
+def g2_fb_mul(tables: torch.Tensor, scalars: torch.Tensor, tab_idx: torch.Tensor | None = None) -> torch.Tensor:
+    n = _rows(scalars, 8)
+    out = torch.empty((n, 32), dtype=torch.int32, device=scalars.device)
+    g, s = _ctx(tables, scalars, tab_idx)
+    _call("dx_g2_fb_mul", g, s, _ptr(tables), _ptr(tab_idx), _ptr(scalars), _ptr(out), n)
+    return out
+
+
+def g2_mul(pts_aff: torch.Tensor, scalars: torch.Tensor) -> torch.Tensor:
+    n = _rows(scalars, 8)
+    np_ = _rows(pts_aff, 32)
+    assert np_ in (1, n)
+    out = torch.empty((n, 32), dtype=torch.int32, device=scalars.device)
+    g, s = _ctx(pts_aff, scalars)
+    _call("dx_g2_mul", g, s, _ptr(pts_aff), _ptr(scalars), _ptr(out), n, int(np_ == 1 and n > 1))
+    return out
+
+
+def g2_on_curve(aff: torch.Tensor) -> torch.Tensor:
+    n = _rows(aff, 32)
+    out = torch.empty((n,), dtype=torch.uint8, device=aff.device)
+    g, s = _ctx(aff)
+    _call("dx_g2_on_curve", g, s, _ptr(aff), _ptr(out), n)
+    return out
+
+
+# ----------------------------------------------------------------------------- pairing / GT
+def miller_loop(P_aff: torch.Tensor, Q_aff: torch.Tensor) -> torch.Tensor:
+    n = _rows(P_aff, 16)
+    assert _rows(Q_aff, 32) == n
+    out = torch.empty((n, 96), dtype=torch.int32, device=P_aff.device)
+    g, s = _ctx(P_aff, Q_aff)
+    _call("dx_miller_loop", g, s, _ptr(P_aff), _ptr(Q_aff), _ptr(out), n)
+    return out
+
+
+def final_exp(f: torch.Tensor) -> torch.Tensor:
+    n = _rows(f, 96)
+    out = torch.empty_like(f)
+    g, s = _ctx(f)
+    _call("dx_final_exp", g, s, _ptr(f), _ptr(out), n)
+    return out
+
+
+def pairing(P_aff: torch.Tensor, Q_aff: torch.Tensor) -> torch.Tensor:
+    n = _rows(P_aff, 16)
+    assert _rows(Q_aff, 32) == n
+    out = torch.empty((n, 96), dtype=torch.int32, device=P_aff.device)
+    g, s = _ctx(P_aff, Q_aff)
+    _call("dx_pairing", g, s, _ptr(P_aff), _ptr(Q_aff), _ptr(out), n)
+    return out
+
+
+def gt_mul(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    n = _rows(a, 96)
+    out = torch.empty_like(a)
+    g, s = _ctx(a, b)
+    _call("dx_gt_mul", g, s, _ptr(a), _ptr(b), _ptr(out), n)
+    return out
+
+
+def gt_pow(a: torch.Tensor, scalars: torch.Tensor) -> torch.Tensor:
+    n = _rows(scalars, 8)
+    na = _rows(a, 96)
+    out = torch.empty((n, 96), dtype=torch.int32, device=a.device)
+    g, s = _ctx(a, scalars)
+    _call("dx_gt_pow", g, s, _ptr(a), _ptr(scalars), _ptr(out), n, int(na == 1 and n > 1))
+    return out
+
+
+def gt_eq(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    n = _rows(a, 96)
+    out = torch.empty((n,), dtype=torch.uint8, device=a.device)
+    g, s = _ctx(a, b)
+    _call("dx_gt_eq", g, s, _ptr(a), _ptr(b), _ptr(out), n)
+    return out
+
+
+def gt_fb_table(bases: torch.Tensor) -> torch.Tensor:
+    nb = _rows(bases, 96)
+    table = torch.empty((nb * 896, 96), dtype=torch.int32, device=bases.device)
+    g, s = _ctx(bases)
+    _call("dx_gt_fb_table", g, s, _ptr(bases.contiguous()), _ptr(table), nb)
+    return table
+
+
+def gt_fb_pow(tables: torch.Tensor, scalars: torch.Tensor, tab_idx: torch.Tensor | None = None) -> torch.Tensor:
+    n = _rows(scalars, 8)
+    out = torch.empty((n, 96), dtype=torch.int32, device=scalars.device)
+    g, s = _ctx(tables, scalars, tab_idx)
+    _call("dx_gt_fb_pow", g, s, _ptr(tables), _ptr(tab_idx), _ptr(scalars), _ptr(out), n)
+    return out
+
+
+def gt_prod(x: torch.Tensor, chunk: int = 16) -> torch.Tensor:
+    """Product over axis 0 of x[n_items, n_groups, 96] -> [n_groups, 96]."""
+    assert x.dim() == 3 and x.shape[-1] == 96
+    n_items, n_groups = x.shape[0], x.shape[1]
+    cur = x.contiguous()
+    while n_items > 1:
+        ch = max(2, min(chunk, n_items))
+        n_chunks = (n_items + ch - 1) // ch
+        out = torch.empty((n_chunks, n_groups, 96), dtype=torch.int32, device=x.device)
+        g, s = _ctx(cur)
+        _call("dx_gt_prod_chunks", g, s, _ptr(cur), _ptr(out), n_items, n_groups, ch)
+        cur, n_items = out, n_chunks
+    return cur[0]

@@ -1,0 +1,87 @@
+"""Build the in-tree native library ``libdrynx_native.so`` for gfx950.
+
+Each ``csrc/kernels/*.hip`` translation unit is compiled by ``hipcc
+--offload-arch=gfx950`` in parallel (one process per TU, bounded by a
+timeout) and linked into one shared object that lives next to this file, so
+it travels with the repo snapshot to the GPU box.  The library contains both
+the gfx950 device code and the host (CPU) path of every batched op.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import hashlib
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.abspath(os.path.join(HERE, "..", ".."))
+CSRC = os.path.join(ROOT, "csrc")
+LIB = os.path.join(HERE, "libdrynx_native.so")
+OBJDIR = os.path.join(ROOT, "build", "native")
+ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0] or "gfx950"
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result"]
+
+
+def _sources():
+    kdir = os.path.join(CSRC, "kernels")
+    return sorted(os.path.join(kdir, f) for f in os.listdir(kdir) if f.endswith(".hip"))
+
+
+def _headers():
+    out = []
+    for d in ("bn254", "kernels"):
+        p = os.path.join(CSRC, d)
+        out += sorted(os.path.join(p, f) for f in os.listdir(p) if f.endswith(".h"))
+    return out
+
+
+def _digest(paths):
+    h = hashlib.sha256()
+    for p in paths:
+        with open(p, "rb") as f:
+            h.update(p.encode() + f.read())
+    h.update(" ".join(FLAGS).encode())
+    return h.hexdigest()
+
+
+def _compile(src, hdr_digest):
+    os.makedirs(OBJDIR, exist_ok=True)
+    key = _digest([src]) + hdr_digest
+    obj = os.path.join(OBJDIR, os.path.basename(src) + ".o")
+    stamp = obj + ".stamp"
+    if os.path.exists(obj) and os.path.exists(stamp) and open(stamp).read() == key:
+        return obj
+    cmd = [HIPCC, *FLAGS, "-I", CSRC, "-c", src, "-o", obj]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=1800)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr[-4000:]}")
+    with open(stamp, "w") as f:
+        f.write(key)
+    return obj
+
+
+def build(force: bool = False, verbose: bool = True) -> str:
+    gen = os.path.join(ROOT, "tools", "gen_constants.py")
+    subprocess.run([sys.executable, gen], check=True)
+    srcs = _sources()
+    hdr_digest = _digest(_headers())
+    lib_stamp = LIB + ".stamp"
+    all_key = _digest(srcs) + hdr_digest
+    if not force and os.path.exists(LIB) and os.path.exists(lib_stamp) and open(lib_stamp).read() == all_key:
+        return LIB
+    workers = min(len(srcs), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4)), 16)
+    with cf.ThreadPoolExecutor(max_workers=workers) as ex:
+        objs = list(ex.map(lambda s: _compile(s, hdr_digest), srcs))
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs, "-lpthread"]
+    subprocess.run(cmd, check=True, timeout=600)
+    with open(lib_stamp, "w") as f:
+        f.write(all_key)
+    if verbose:
+        print(f"[drynx_amd] built {LIB}")
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)
