@@ -172,7 +172,9 @@ DX_NI Jac<F> scalar_mul(const Jac<F> &p, const uint32_t *k) {
   tab[1] = p;
   for (int i = 2; i < 16; i++) tab[i] = (i & 1) ? jadd(tab[i - 1], p) : jdbl(tab[i >> 1]);
   Jac<F> r = Jac<F>::inf();
-  for (int w = 63; w >= 0; w--) {
+  int top = 63;  // skip leading zero windows (short scalars: 64-bit batch-verification weights)
+  while (top > 0 && ((k[top >> 3] >> ((top & 7) * 4)) & 15u) == 0) top--;
+  for (int w = top; w >= 0; w--) {
     r = jdbl(jdbl(jdbl(jdbl(r))));
     uint32_t d = (k[w >> 3] >> ((w & 7) * 4)) & 15u;
     if (d) r = jadd(r, tab[d]);

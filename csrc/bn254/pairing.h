@@ -84,7 +84,9 @@ DX_NI Fp12 pairing(const G1A &P, const G2A &Q) { return final_exp(miller_loop(P,
 // GT exponentiation by a 256-bit scalar (cyclotomic squarings).
 DX_NI Fp12 gt_pow(const Fp12 &x, const uint32_t *k) {
   Fp12 r = Fp12::one();
-  for (int i = 255; i >= 0; i--) {
+  int top = 255;
+  while (top > 0 && ((k[top >> 5] >> (top & 31)) & 1u) == 0) top--;
+  for (int i = top; i >= 0; i--) {
     r = cyclotomic_sqr(r);
     if ((k[i >> 5] >> (i & 31)) & 1u) r = mul(r, x);
   }

@@ -1,0 +1,50 @@
+// Fused range-proof kernels (K15 prove, K16 batched verify).
+//
+// Reference: lib/range/range_proof.go.  Per value, digit j and server i the
+// prover publishes a_ij = e(-s_j B, V_ij) * e(t_j B, B2) (:396-397) and the
+// verifier checks a_ij == e(c y_i, V_ij) e(-Zphi_j B, V_ij) e(Zv_ij B, B2)
+// (:540-546) — 2 + 3 full pairings per (i, j) in the reference.
+//
+// Here:
+//   prove  : a_ij = FE(ML(-s_j B, V_ij)) * gT^{t_j}   (gT = e(B,B2) comb table)
+//   verify : all (p,i,j) of a list are folded with random 64-bit weights rho:
+//            FE(prod_pij ML(rho (Zphi_j B - c y_i), V_ij)) * prod_pij a_ij^rho
+//            == gT^{sum rho Zv}: ONE final exponentiation for the whole list.  One Miller loop per (p,i,j)
+//            instead of three pairings.
+// Item index: it = (p * S + i) * L + j.
+#include "common.h"
+
+extern "C" {
+
+// a[it] = FE(ML(negsB[p*L+j], V[it])) * gT^{t[p*L+j]}
+int dx_rp_prove_a(int on_gpu, void *stream, const uint32_t *negsB_aff, const uint32_t *V_aff, const uint32_t *t_sc,
+                  const uint32_t *gt_table, uint32_t *a_out, int64_t n_items, int S, int L) {
+  auto op = [=] __host__ __device__(int64_t it) {
+    int64_t j = it % L;
+    int64_t p = it / ((int64_t)S * L);
+    int64_t pj = p * L + j;
+    Fp12 f = final_exp(miller_loop(at<G1A>(negsB_aff, pj), at<G2A>(V_aff, it)));
+    Fp12 g = gt_fixed_pow(reinterpret_cast<const Fp12 *>(gt_table), t_sc + 8 * pj);
+    at<Fp12>(a_out, it) = mul(f, g);
+  };
+  return run(on_gpu, stream, n_items, op, true, "rp_prove_a");
+}
+
+// f[it] = ML(rho (ZB[p*L+j] - Y[p*S+i]), V[it]),  g[it] = a[it]^rho
+// (the final exponentiation applies to the Miller product only: a_ij is already in GT)
+int dx_rp_verify_items(int on_gpu, void *stream, const uint32_t *ZB_jac, const uint32_t *Y_jac, const uint32_t *rho,
+                       const uint32_t *V_aff, const uint32_t *a, uint32_t *f_out, uint32_t *g_out, int64_t n_items,
+                       int S, int L) {
+  auto op = [=] __host__ __device__(int64_t it) {
+    int64_t j = it % L;
+    int64_t pi = it / L;  // p*S + i
+    int64_t p = pi / S;
+    G1J T = jadd(at<G1J>(ZB_jac, p * L + j), jneg(at<G1J>(Y_jac, pi)));
+    G1A P = to_affine(scalar_mul(T, rho + 8 * it));
+    at<Fp12>(f_out, it) = miller_loop(P, at<G2A>(V_aff, it));
+    at<Fp12>(g_out, it) = gt_pow(at<Fp12>(a, it), rho + 8 * it);
+  };
+  return run(on_gpu, stream, n_items, op, true, "rp_verify_items");
+}
+
+}  // extern "C"

@@ -78,6 +78,9 @@ _SIGS = {
     "dx_gt_fb_pow": [_I, _P, _P, _P, _P, _P, _L],
     "dx_gt_prod_chunks": [_I, _P, _P, _P, _L, _L, _L],
     "dx_version": [],
+    "dx_lr_moments": [_P, _P, _P, _L, _I, _P, _I],
+    "dx_rp_prove_a": [_I, _P, _P, _P, _P, _P, _P, _L, _I, _I],
+    "dx_rp_verify_items": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _I],
 }
 
 
@@ -384,7 +387,7 @@ def gt_eq(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
 
 def gt_fb_table(bases: torch.Tensor) -> torch.Tensor:
     nb = _rows(bases, 96)
-    table = torch.empty((nb * 896, 96), dtype=torch.int32, device=bases.device)
+    table = torch.empty((nb * 8192, 96), dtype=torch.int32, device=bases.device)
     g, s = _ctx(bases)
     _call("dx_gt_fb_table", g, s, _ptr(bases.contiguous()), _ptr(table), nb)
     return table
@@ -411,3 +414,38 @@ def gt_prod(x: torch.Tensor, chunk: int = 16) -> torch.Tensor:
         _call("dx_gt_prod_chunks", g, s, _ptr(cur), _ptr(out), n_items, n_groups, ch)
         cur, n_items = out, n_chunks
     return cur[0]
+
+
+# ----------------------------------------------------------------------------- logistic-regression GEMM (K13)
+def lr_moments(X: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """sum_i w_i X_i X_i^T on the fp64-MFMA kernel (GPU tensors only)."""
+    assert X.is_cuda and X.dtype == torch.float64 and X.dim() == 2 and X.shape[1] <= 48
+    N, D = X.shape
+    steps = (N + 3) // 4
+    n_blocks = int(max(1, min(2048, (steps + 15) // 16)))
+    partial = torch.empty((n_blocks, 48, 48), dtype=torch.float64, device=X.device)
+    _, s = _ctx(X)
+    lib_ = _load()
+    rc = lib_.dx_lr_moments(s, _ptr(X), _ptr(w.to(torch.float64).contiguous()), N, D, _ptr(partial), n_blocks)
+    if rc != 0:
+        raise RuntimeError(f"dx_lr_moments failed rc={rc}")
+    return partial.sum(0)[:D, :D]
+
+
+# ----------------------------------------------------------------------------- range proofs (K15/K16)
+def rp_prove_a(negsB_aff, V_aff, t_sc, gt_table, S: int, L: int) -> torch.Tensor:
+    n = _rows(V_aff, 32)
+    out = torch.empty((n, 96), dtype=torch.int32, device=V_aff.device)
+    g, s = _ctx(negsB_aff, V_aff, t_sc, gt_table)
+    _call("dx_rp_prove_a", g, s, _ptr(negsB_aff), _ptr(V_aff), _ptr(t_sc), _ptr(gt_table), _ptr(out), n, S, L)
+    return out
+
+
+def rp_verify_items(ZB_jac, Y_jac, rho, V_aff, a, S: int, L: int):
+    n = _rows(V_aff, 32)
+    f = torch.empty((n, 96), dtype=torch.int32, device=V_aff.device)
+    gg = torch.empty((n, 96), dtype=torch.int32, device=V_aff.device)
+    g, s = _ctx(ZB_jac, Y_jac, rho, V_aff, a)
+    _call("dx_rp_verify_items", g, s, _ptr(ZB_jac), _ptr(Y_jac), _ptr(rho), _ptr(V_aff), _ptr(a), _ptr(f), _ptr(gg),
+          n, S, L)
+    return f, gg

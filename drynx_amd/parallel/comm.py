@@ -1,0 +1,201 @@
+"""Communication planes for the party runtime.
+
+The reference moves every protocol message over onet (TCP/protobuf between
+separate server processes).  Here parties are logical
+entities hosted by ranks (one rank per GPU) and the data plane is
+torch.distributed:
+
+* device tensors (ciphertext vectors, proof blobs) go over the ``nccl``
+  backend, which on ROCm is RCCL over xGMI;
+* small control messages (the SurveyQuery, bitmaps, acks) use
+  ``broadcast_object_list`` / ``all_gather_object`` on a gloo group.
+
+Point-to-point patterns used by the protocols:
+  - ``exchange``: personalised all-to-all (star gathers DP->CN, CN->root, proof
+    fan-out to VNs).  On RCCL this is ONE ``all_to_all_single`` whose per-peer
+    splits go straight over the 7 xGMI links (no ring hops); gloo has no
+    all-to-all so it falls back to all_gather of padded buffers.
+  - ``send/recv``: the DRO shuffle chain CN_i -> CN_{i+1}.
+RCCL cannot add BN254 points, so EC reductions are exchange + HIP reduce
+kernels (parallel/ec_collectives.py).
+"""
+from __future__ import annotations
+
+import os
+import pickle
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+
+class Comm:
+    rank: int = 0
+    world: int = 1
+    device: torch.device = torch.device("cpu")
+
+    def barrier(self):
+        pass
+
+    def broadcast_object(self, obj, src: int = 0):
+        return obj
+
+    def all_gather_object(self, obj) -> list:
+        return [obj]
+
+    def exchange(self, outgoing: dict) -> dict:
+        """outgoing: dst_rank -> int32 tensor (any shape, on self.device).
+        Returns src_rank -> flat int32 tensor received (only non-empty ones)."""
+        return {self.rank: outgoing[self.rank].reshape(-1)} if self.rank in outgoing else {}
+
+    def send(self, t: torch.Tensor, dst: int):
+        raise RuntimeError("single-process comm has no peers")
+
+    def recv(self, numel: int, src: int) -> torch.Tensor:
+        raise RuntimeError("single-process comm has no peers")
+
+    def exchange_bytes(self, outgoing: dict) -> dict:
+        """Like exchange but for python bytes payloads (proof blobs)."""
+        tens = {d: _bytes_to_i32(b, self.device) for d, b in outgoing.items()}
+        got = self.exchange(tens)
+        return {s: _i32_to_bytes(t) for s, t in got.items()}
+
+
+def _bytes_to_i32(b: bytes, device) -> torch.Tensor:
+    n = len(b)
+    pad = (-(n + 8)) % 4
+    raw = n.to_bytes(8, "little") + b + b"\x00" * pad
+    return torch.from_numpy(np.frombuffer(raw, dtype=np.int32).copy()).to(device)
+
+
+def _i32_to_bytes(t: torch.Tensor) -> bytes:
+    raw = t.detach().cpu().numpy().tobytes()
+    n = int.from_bytes(raw[:8], "little")
+    return raw[8: 8 + n]
+
+
+class LocalComm(Comm):
+    """World of one rank: every logical party lives in this process."""
+
+    def __init__(self, device="cpu"):
+        self.rank, self.world = 0, 1
+        self.device = torch.device(device)
+
+
+class DistComm(Comm):
+    """torch.distributed world; one rank per GPU (RCCL) or per CPU process (gloo)."""
+
+    def __init__(self, device=None):
+        assert dist.is_initialized(), "init_process_group first (see parallel.launch)"
+        self.rank = dist.get_rank()
+        self.world = dist.get_world_size()
+        self.backend = dist.get_backend()
+        if device is None:
+            if self.backend == "nccl":
+                device = torch.device("cuda", torch.cuda.current_device())
+            else:
+                device = torch.device("cpu")
+        self.device = torch.device(device)
+        # control plane: gloo group (CPU objects) even when the data plane is RCCL
+        self._ctrl = dist.new_group(backend="gloo") if self.backend == "nccl" else None
+
+    def barrier(self):
+        if self.backend == "nccl":
+            dist.barrier(group=self._ctrl)
+        else:
+            dist.barrier()
+
+    def broadcast_object(self, obj, src: int = 0):
+        lst = [obj]
+        dist.broadcast_object_list(lst, src=src, group=self._ctrl)
+        return lst[0]
+
+    def all_gather_object(self, obj) -> list:
+        out = [None] * self.world
+        dist.all_gather_object(out, obj, group=self._ctrl)
+        return out
+
+    def exchange(self, outgoing: dict) -> dict:
+        W = self.world
+        flat = {d: t.reshape(-1).to(torch.int32) for d, t in outgoing.items()}
+        sizes = torch.zeros(W, dtype=torch.int64)
+        for d, t in flat.items():
+            sizes[d] = t.numel()
+        if self.backend == "nccl":
+            send_sizes = sizes.to(self.device)
+            recv_sizes = torch.empty_like(send_sizes)
+            dist.all_to_all_single(recv_sizes, send_sizes)
+            recv_sizes = recv_sizes.cpu()
+            send = torch.cat([flat.get(d, torch.empty(0, dtype=torch.int32, device=self.device)) for d in range(W)])
+            if send.numel() == 0:
+                send = torch.empty(0, dtype=torch.int32, device=self.device)
+            recv = torch.empty(int(recv_sizes.sum()), dtype=torch.int32, device=self.device)
+            dist.all_to_all_single(recv, send.to(self.device), output_split_sizes=recv_sizes.tolist(),
+                                   input_split_sizes=sizes.tolist())
+            out, off = {}, 0
+            for s in range(W):
+                n = int(recv_sizes[s])
+                if n:
+                    out[s] = recv[off: off + n]
+                off += n
+            return out
+        # gloo: all_gather a [W, maxlen] matrix of padded per-destination payloads
+        all_sizes = [torch.zeros(W, dtype=torch.int64) for _ in range(W)]
+        dist.all_gather(all_sizes, sizes)
+        mat = torch.stack(all_sizes)  # [src, dst]
+        maxlen = int(mat.max()) if mat.numel() else 0
+        if maxlen == 0:
+            return {}
+        buf = torch.zeros((W, maxlen), dtype=torch.int32)
+        for d, t in flat.items():
+            buf[d, : t.numel()] = t.cpu()
+        gathered = [torch.zeros((W, maxlen), dtype=torch.int32) for _ in range(W)]
+        dist.all_gather(gathered, buf)
+        out = {}
+        for s in range(W):
+            n = int(mat[s, self.rank])
+            if n:
+                out[s] = gathered[s][self.rank, :n].to(self.device)
+        return out
+
+    def send(self, t: torch.Tensor, dst: int):
+        dist.send(t.contiguous(), dst)
+
+    def recv(self, numel: int, src: int) -> torch.Tensor:
+        t = torch.empty(numel, dtype=torch.int32, device=self.device)
+        dist.recv(t, src)
+        return t
+
+
+def make_comm(device=None) -> Comm:
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        return DistComm(device)
+    if device is None:
+        device = "cuda" if torch.cuda.is_available() else "cpu"
+    return LocalComm(device)
+
+
+def init_distributed(backend: str | None = None):
+    """Initialise torch.distributed from the torchrun env (RANK/WORLD_SIZE/MASTER_*)."""
+    if dist.is_initialized():
+        return
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world <= 1:
+        return
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    if backend == "nccl":
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        dist.init_process_group("gloo")
+
+
+def obj_to_bytes(obj) -> bytes:
+    return pickle.dumps(obj, protocol=pickle.HIGHEST_PROTOCOL)
+
+
+def bytes_to_obj(b: bytes):
+    # only ever applied to payloads produced by this framework's own ranks
+    return pickle.loads(b)

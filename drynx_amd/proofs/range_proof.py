@@ -1,0 +1,399 @@
+"""Pairing-based (Boneh–Boyen-signature, CCS08-style) range proofs, batched.
+
+Reference: lib/range/range_proof.go
+  * InitRangeProofSignature[Deterministic] (:249-288): CN key (x, y = xB) and
+    u signatures A_k = (x+k)^-1 B2.
+  * CreatePredicateRangeProofForAllServ (:320-407): prove that the ElGamal
+    commitment C = mB + rP hides m = sum_j phi_j u^j with digits phi_j < u.
+  * RangeProofVerification / RangeProofListVerification (:484-565).
+  * ToBytes/FromBytes (:72-246) — field sizes kept (Challenge/Zr/Zphi/Zv 32 B,
+    D 64 B, V 128 B, A 384 B, Commit 128 B).
+
+MI355X design (all lists of proofs are processed as ONE batch on the device):
+  prove : a_ij = FE(ML(-s_j B, V_ij)) * gT^{t_j} with a comb table for
+          gT = e(B, B2) (fused kernel dx_rp_prove_a); D = (sum u^j s_j) B +
+          (sum m_j) P by two fixed-base mults; all Fr arithmetic on device.
+  verify: D-check folded to c*C + Zr*P + (sum_j Zphi_j u^j)*B per proof, and
+          the l*S pairing equations of every proof in the list combined with
+          random 64-bit weights rho: one Miller loop per (proof, server,
+          digit) + ONE final exponentiation per list (dx_rp_verify_items).
+          The reference's AND over the list (:497-500) makes this exact up
+          to a 2^-64 soundness error.
+
+Extension (documented): ranges may carry a third element ``offset``; the
+proof then shows m + offset in [0, u^l) (signed values such as logistic-
+regression coefficients).  offset = 0 is the reference behaviour.
+"""
+from __future__ import annotations
+
+import hashlib
+import io
+import math
+import os
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from .. import native as nt
+from ..crypto import bn254 as bn
+from ..crypto import oracle as O
+from ..crypto.elgamal import CipherVector, pk_table
+from ..query import PublishSignatureBytes
+
+G2_LEN, G1_LEN, GT_LEN, SC_LEN = 128, 64, 384, 32
+
+
+# ----------------------------------------------------------------------------- setup (CN side)
+def init_range_proof_signature(u: int, secret: int | None = None, device="cpu") -> PublishSignatureBytes:
+    """A CN's input-validation key for one output column: y = x*B, A_k = (x+k)^-1 * B2."""
+    x = O.random_scalar() if secret is None else secret % O.R
+    y = O.g1_mul(x, O.G1_GEN)
+    inv = [pow((x + k) % O.R, -1, O.R) for k in range(u)]
+    A = nt.g2_fb_mul(bn.base2_table(device), bn.scalars_tensor(inv, device))
+    return PublishSignatureBytes(O.g1_to_bytes(y), bn.g2_aff_to_bytes(A).tobytes())
+
+
+def init_range_proof_signature_deterministic(u: int, device="cpu") -> PublishSignatureBytes:
+    """InitRangeProofSignatureDeterministic: x = 12 (range_proof.go:249)."""
+    return init_range_proof_signature(u, 12, device)
+
+
+class SigMaterial:
+    """Device-resident view of InputValidationSigs[cn][col]: y_{i,col} (G1) and
+    A_{i,col,k} (G2 affine), plus per-column Y = sum_i y_{i,col} bytes for the
+    Fiat–Shamir hash."""
+
+    def __init__(self, sigs, device="cpu"):
+        self.device = torch.device(device)
+        self.S = len(sigs)
+        self.n_cols = len(sigs[0]) if self.S else 0
+        self.u = [len(sigs[0][c].Signature) // G2_LEN for c in range(self.n_cols)]
+        self.umax = max(self.u) if self.u else 0
+        ys = []
+        A_bytes = np.zeros((self.S, self.n_cols, max(1, self.umax), G2_LEN), dtype=np.uint8)
+        for i in range(self.S):
+            for c in range(self.n_cols):
+                ys.append(O.g1_from_bytes(sigs[i][c].Public))
+                raw = np.frombuffer(sigs[i][c].Signature, dtype=np.uint8).reshape(-1, G2_LEN)
+                A_bytes[i, c, : raw.shape[0]] = raw
+        self.y_pts = ys  # index i*n_cols + c
+        self.y_jac = bn.g1_jac_tensor(ys, device) if ys else None
+        flat = A_bytes.reshape(-1, G2_LEN)
+        nz = flat.any(axis=1)
+        A = torch.zeros((flat.shape[0], 32), dtype=torch.int32, device=device)
+        if nz.any():
+            A[torch.from_numpy(np.nonzero(nz)[0]).to(device)] = bn.g2_aff_from_bytes(flat[nz], device, check=False)
+        self.A = A  # index (i*n_cols + c)*umax + k
+        self.Ysum_bytes = []
+        for c in range(self.n_cols):
+            acc = None
+            for i in range(self.S):
+                acc = O.g1_add(acc, ys[i * self.n_cols + c])
+            self.Ysum_bytes.append(O.g1_to_bytes(acc))
+
+
+_gt_cache: dict = {}
+
+
+def gt_generator_table(device="cpu"):
+    """gT = e(B, B2) and its comb table (3 MiB of HBM, cached per device)."""
+    key = str(torch.device(device))
+    if key not in _gt_cache:
+        gT = nt.pairing(bn.g1_generator_aff(device), bn.g2_generator_aff(device))
+        _gt_cache[key] = (gT, nt.gt_fb_table(gT))
+    return _gt_cache[key]
+
+
+# ----------------------------------------------------------------------------- proof list (columnar)
+@dataclass
+class RangeProofList:
+    """n proofs sharing (u, l, S).  Tensors on one device."""
+    u: int
+    l: int
+    S: int
+    offset: list
+    cols: list
+    commit: CipherVector          # n ciphertexts (Commit)
+    challenge: torch.Tensor = None  # [n, 8]
+    zr: torch.Tensor = None         # [n, 8]
+    D: torch.Tensor = None          # [n, 24] Jacobian
+    zphi: torch.Tensor = None       # [n*l, 8]
+    zv: torch.Tensor = None         # [n*S*l, 8]  index (p*S+i)*l+j
+    V: torch.Tensor = None          # [n*S*l, 32]
+    A: torch.Tensor = None          # [n*S*l, 96]
+
+    def __len__(self):
+        return len(self.commit)
+
+    @property
+    def has_rp(self) -> bool:
+        return not (self.u == 0 and self.l == 0)
+
+    # ------------------------------------------------------------- wire
+    def to_bytes(self) -> bytes:
+        """Columnar kyber-layout encoding of the list (all proofs share u,l,S)."""
+        n = len(self)
+        out = io.BytesIO()
+        hdr = np.array([n, self.u, self.l, self.S], dtype="<i8")
+        out.write(hdr.tobytes())
+        out.write(np.asarray(self.offset, dtype="<i8").tobytes())
+        out.write(np.asarray(self.cols, dtype="<i8").tobytes())
+        out.write(self.commit.to_bytes())
+        if self.has_rp and n:
+            out.write(bn.scalars_to_bytes(self.challenge).tobytes())
+            out.write(bn.scalars_to_bytes(self.zr).tobytes())
+            out.write(bn.g1_aff_to_bytes(nt.g1_to_affine(self.D)).tobytes())
+            out.write(bn.scalars_to_bytes(self.zv).tobytes())
+            out.write(bn.scalars_to_bytes(self.zphi).tobytes())
+            out.write(bn.g2_aff_to_bytes(self.V).tobytes())
+            out.write(bn.gt_to_bytes(self.A).tobytes())
+        return out.getvalue()
+
+    @staticmethod
+    def from_bytes(b: bytes, device="cpu") -> "RangeProofList":
+        mv = memoryview(b)
+        n, u, l, S = (int(v) for v in np.frombuffer(mv[:32], dtype="<i8"))
+        off = 32
+        offset = np.frombuffer(mv[off: off + 8 * n], dtype="<i8").tolist()
+        off += 8 * n
+        cols = np.frombuffer(mv[off: off + 8 * n], dtype="<i8").tolist()
+        off += 8 * n
+        commit = CipherVector.from_bytes(bytes(mv[off: off + 128 * n]), device)
+        off += 128 * n
+        rpl = RangeProofList(u, l, S, offset, cols, commit)
+        if rpl.has_rp and n:
+            def take(nbytes):
+                nonlocal off
+                chunk = bytes(mv[off: off + nbytes])
+                off += nbytes
+                return np.frombuffer(chunk, dtype=np.uint8)
+            rpl.challenge = bn.scalars_from_bytes(take(SC_LEN * n), device)
+            rpl.zr = bn.scalars_from_bytes(take(SC_LEN * n), device)
+            rpl.D = nt.g1_from_affine(bn.g1_aff_from_bytes(take(G1_LEN * n), device))
+            rpl.zv = bn.scalars_from_bytes(take(SC_LEN * n * S * l), device)
+            rpl.zphi = bn.scalars_from_bytes(take(SC_LEN * n * l), device)
+            rpl.V = bn.g2_aff_from_bytes(take(G2_LEN * n * S * l), device)
+            rpl.A = bn.gt_from_bytes(take(GT_LEN * n * S * l), device)
+        return rpl
+
+    def to(self, device) -> "RangeProofList":
+        mv = lambda t: None if t is None else t.to(device)  # noqa: E731
+        return RangeProofList(self.u, self.l, self.S, list(self.offset), list(self.cols), self.commit.to(device),
+                              mv(self.challenge), mv(self.zr), mv(self.D), mv(self.zphi), mv(self.zv), mv(self.V),
+                              mv(self.A))
+
+
+# ----------------------------------------------------------------------------- helpers
+def to_base(n: int, b: int, l: int) -> list:
+    """ToBase (range_proof.go:584): little-endian base-b digits, zero-padded to l.
+    Non-positive n gives all-zero digits (reference behaviour)."""
+    digits = []
+    while n > 0:
+        digits.append(n % b)
+        n //= b
+    while len(digits) < l:
+        digits.append(0)
+    return digits[:max(l, len(digits))]
+
+
+def _rep(t: torch.Tensor, k: int) -> torch.Tensor:
+    return t.repeat_interleave(k, dim=0).contiguous()
+
+
+def _fr_sum_rows(x: torch.Tensor, groups: int) -> torch.Tensor:
+    """x: [groups*m, 8] -> per-group Fr sum [groups, 8] (pairwise tree on device)."""
+    m = x.shape[0] // groups
+    cur = x.view(groups, m, 8)
+    while cur.shape[1] > 1:
+        if cur.shape[1] % 2:
+            pad = torch.zeros((groups, 1, 8), dtype=torch.int32, device=x.device)
+            cur = torch.cat([cur, pad], dim=1)
+        a = cur[:, 0::2].contiguous().view(-1, 8)
+        b = cur[:, 1::2].contiguous().view(-1, 8)
+        cur = nt.fr_arith(nt.FR_ADD, a, b).view(groups, -1, 8)
+    return cur[:, 0].contiguous()
+
+
+def _small_scalars(vals, device) -> torch.Tensor:
+    a = np.zeros((len(vals), 8), dtype=np.uint32)
+    v = np.asarray(vals, dtype=np.int64)
+    a[:, 0] = (v & 0xFFFFFFFF).astype(np.uint32)
+    a[:, 1] = ((v >> 32) & 0xFFFFFFFF).astype(np.uint32)
+    return bn.to_tensor(a, device)
+
+
+def _challenge_hash(C_aff_bytes: np.ndarray, ysum_bytes: list) -> list:
+    """c = SHA3-512(B || C || sum_i y_i) mod r (range_proof.go:350-374)."""
+    Bb = O.g1_to_bytes(O.G1_GEN)
+    out = []
+    for p in range(C_aff_bytes.shape[0]):
+        h = hashlib.sha3_512()
+        h.update(Bb)
+        h.update(C_aff_bytes[p].tobytes())
+        h.update(ysum_bytes[p])
+        out.append(int.from_bytes(h.digest(), "big") % O.R)
+    return out
+
+
+# ----------------------------------------------------------------------------- prove
+def create_range_proofs(batch, sigmat: SigMaterial, P_point, device=None) -> list:
+    """Batched CreatePredicateRangeProofForAllServ over a CreateProofBatch.
+    Returns a list of RangeProofList (one per distinct (u, l))."""
+    device = torch.device(device or batch.cv.device)
+    groups: dict = {}
+    for idx in range(len(batch)):
+        groups.setdefault((batch.u[idx], batch.l[idx]), []).append(idx)
+    out = []
+    for (u, l), idxs in groups.items():
+        sel = torch.tensor(idxs, dtype=torch.long, device=batch.cv.device)
+        cv = CipherVector(batch.cv.K[sel], batch.cv.C[sel])
+        vals = [batch.values[i] for i in idxs]
+        offs = [batch.offset[i] if batch.offset else 0 for i in idxs]
+        cols = [batch.sig_col[i] for i in idxs]
+        r = batch.r[sel].contiguous()
+        out.append(_prove_group(u, l, vals, offs, cols, r, cv.to(device), sigmat, P_point, device))
+    return out
+
+
+def _prove_group(u, l, vals, offs, cols, r, cv, sigmat, P_point, device) -> RangeProofList:
+    n = len(vals)
+    S = sigmat.S
+    rpl = RangeProofList(u, l, S, offs, cols, cv)
+    if u == 0 and l == 0:
+        return rpl
+    r = r.to(device)
+    tabB = bn.base_table(device)
+    tabP = pk_table(P_point, device).tabP
+    # digits of m + offset
+    phi = np.array([to_base(int(v) + int(o), u, l)[:l] for v, o in zip(vals, offs)], dtype=np.int64).reshape(n, l)
+    # Fiat–Shamir challenge per value
+    C_bytes = bn.g1_aff_to_bytes(nt.g1_to_affine(cv.C))
+    c_int = _challenge_hash(C_bytes, [sigmat.Ysum_bytes[c] for c in cols])
+    c = bn.scalars_tensor(c_int, device)
+    # randomness
+    s = bn.random_scalars(n * l, device)
+    t = bn.random_scalars(n * l, device)
+    m = bn.random_scalars(n * l, device)
+    v = bn.random_scalars(n * S * l, device)
+    # D = (sum_j u^j s_j) B + (sum_j m_j) P
+    uj = bn.scalars_tensor([pow(u, j, O.R) for j in range(l)] * n, device)
+    us = _fr_sum_rows(nt.fr_arith(nt.FR_MUL, s, uj), n)
+    msum = _fr_sum_rows(m, n)
+    D = nt.g1_add(nt.g1_fb_mul(tabB, us), nt.g1_fb_mul(tabP, msum))
+    # Zphi_j = s_j - c phi_j ; Zr = sum m - c r ; Zv_ij = t_j - c v_ij
+    phi_sc = _small_scalars(phi.reshape(-1), device)
+    zphi = nt.fr_arith(nt.FR_SUB, s, nt.fr_arith(nt.FR_MUL, _rep(c, l), phi_sc))
+    zr = nt.fr_arith(nt.FR_SUB, msum, nt.fr_arith(nt.FR_MUL, c, r))
+    t_rep = t.view(n, 1, l, 8).expand(n, S, l, 8).reshape(-1, 8).contiguous()
+    zv = nt.fr_arith(nt.FR_SUB, t_rep, nt.fr_arith(nt.FR_MUL, _rep(c, S * l), v))
+    # V_ij = v_ij * A_{i, col, phi_j}
+    cols_t = torch.tensor(cols, dtype=torch.long, device=device)
+    i_idx = torch.arange(S, device=device)
+    phi_t = torch.from_numpy(phi).to(device)
+    a_index = ((i_idx.view(1, S, 1) * sigmat.n_cols + cols_t.view(n, 1, 1)) * max(1, sigmat.umax)
+               + phi_t.view(n, 1, l)).reshape(-1)
+    A_sel = sigmat.A.to(device).index_select(0, a_index).contiguous()
+    V = nt.g2_mul(A_sel, v)
+    # a_ij = FE(ML(-s_j B, V_ij)) * gT^{t_j}
+    negsB = nt.g1_to_affine(nt.g1_fb_mul(tabB, nt.fr_arith(nt.FR_NEG, s)))
+    _, gt_tab = gt_generator_table(device)
+    A = nt.rp_prove_a(negsB, V, t, gt_tab, S, l)
+    rpl.challenge, rpl.zr, rpl.D, rpl.zphi, rpl.zv, rpl.V, rpl.A = c, zr, D, zphi, zv, V, A
+    return rpl
+
+
+# ----------------------------------------------------------------------------- verify
+def _rand64(n, device) -> torch.Tensor:
+    """Random 64-bit batch weights from the OS CSPRNG (unknown to the prover)."""
+    a = np.zeros((n, 8), dtype=np.uint32)
+    raw = np.frombuffer(os.urandom(8 * n), dtype="<u4").reshape(n, 2)
+    a[:, :2] = raw
+    a[:, 0] |= 1  # never zero
+    return bn.to_tensor(a, device)
+
+
+def verify_range_proof_list(rpl: RangeProofList, sigmat: SigMaterial, P_point, threshold: float = 1.0,
+                            device=None) -> bool:
+    """RangeProofListVerification: verifies the first ceil(threshold * n)
+    proofs of the list (reference sampling semantics) as ONE batch."""
+    if not rpl.has_rp:
+        return True
+    n_all = len(rpl)
+    k = int(math.ceil(threshold * n_all))
+    if k == 0:
+        return True
+    device = torch.device(device or rpl.commit.device)
+    r = rpl if k == n_all else _slice(rpl, k)
+    r = r.to(device)
+    n, l, S, u = k, r.l, r.S, r.u
+    if r.zphi.shape[0] != n * l or r.zv.shape[0] != n * S * l or r.V.shape[0] != n * S * l \
+            or r.A.shape[0] != n * S * l:
+        return False
+    tabB = bn.base_table(device)
+    tabP = pk_table(P_point, device).tabP
+    # --- D == c*C' + Zr*P + (sum_j Zphi_j u^j) B, C' = C + offset*B
+    Cp = r.commit.C
+    if any(r.offset):
+        Cp = nt.g1_add(Cp, nt.g1_fb_mul_i64(tabB, torch.tensor(r.offset, dtype=torch.int64, device=device)))
+    uj = bn.scalars_tensor([pow(u, j, O.R) for j in range(l)] * n, device)
+    z = _fr_sum_rows(nt.fr_arith(nt.FR_MUL, r.zphi, uj), n)
+    lhs = nt.g1_add(nt.g1_add(nt.g1_mul(Cp.contiguous(), r.challenge), nt.g1_fb_mul(tabP, r.zr)),
+                    nt.g1_fb_mul(tabB, z))
+    if not bool(nt.g1_eq(lhs, r.D).all()):
+        return False
+    # --- pairing equations, randomly combined
+    ZB = nt.g1_fb_mul(tabB, r.zphi)                                  # [n*l]
+    cols_t = torch.tensor(r.cols, dtype=torch.long, device=device)
+    y_idx = (torch.arange(S, device=device).view(1, S) * sigmat.n_cols + cols_t.view(n, 1)).reshape(-1)
+    Ysel = sigmat.y_jac.to(device).index_select(0, y_idx).contiguous()
+    Y = nt.g1_mul(Ysel, _rep(r.challenge, S))                         # [n*S]
+    rho = _rand64(n * S * l, device)
+    f, g = nt.rp_verify_items(ZB, Y, rho, r.V, r.A, S, l)            # [n*S*l, 96] each
+    F = nt.gt_prod(f.view(-1, 1, 96))
+    G = nt.gt_prod(g.view(-1, 1, 96))
+    lhs_gt = nt.gt_mul(nt.final_exp(F.view(1, 96)), G.view(1, 96))
+    e = _fr_sum_rows(nt.fr_arith(nt.FR_MUL, rho, r.zv), 1)           # sum rho Zv
+    _, gt_tab = gt_generator_table(device)
+    rhs_gt = nt.gt_fb_pow(gt_tab, e)
+    return bool(nt.gt_eq(lhs_gt, rhs_gt).all())
+
+
+def _slice(r: RangeProofList, k: int) -> RangeProofList:
+    l, S = r.l, r.S
+    return RangeProofList(r.u, l, S, r.offset[:k], r.cols[:k], r.commit[:k], r.challenge[:k], r.zr[:k], r.D[:k],
+                          r.zphi[: k * l], r.zv[: k * S * l], r.V[: k * S * l], r.A[: k * S * l])
+
+
+def verify_range_proof_single_reference(rpl: RangeProofList, p: int, sigmat: SigMaterial, P_point) -> bool:
+    """Unbatched, equation-by-equation check of proof p exactly as
+    range_proof.go:504-565 (3 pairings per (i, j)); used to cross-check the
+    batched verifier in tests."""
+    device = rpl.commit.device
+    n, l, S, u = len(rpl), rpl.l, rpl.S, rpl.u
+    c = bn.scalars_from_tensor(rpl.challenge[p: p + 1])[0]
+    zr = bn.scalars_from_tensor(rpl.zr[p: p + 1])[0]
+    zphi = bn.scalars_from_tensor(rpl.zphi[p * l:(p + 1) * l])
+    zv = bn.scalars_from_tensor(rpl.zv[p * S * l:(p + 1) * S * l])
+    Cpt = bn.g1_points_from_jac(rpl.commit.C[p: p + 1])[0]
+    Cpt = O.g1_add(Cpt, O.g1_mul_signed(rpl.offset[p], O.G1_GEN)) if rpl.offset[p] else Cpt
+    D = bn.g1_points_from_jac(rpl.D[p: p + 1])[0]
+    Dp = O.g1_add(O.g1_mul(c, Cpt), O.g1_mul(zr, P_point))
+    for j in range(l):
+        Dp = O.g1_add(Dp, O.g1_mul(zphi[j] * pow(u, j, O.R), O.G1_GEN))
+    if Dp != D:
+        return False
+    V = rpl.V[p * S * l:(p + 1) * S * l]
+    A = rpl.A[p * S * l:(p + 1) * S * l]
+    Pa, Qa = [], []
+    for i in range(S):
+        y = sigmat.y_pts[i * sigmat.n_cols + rpl.cols[p]]
+        for j in range(l):
+            Pa += [O.g1_mul(c, y), O.g1_mul((-zphi[j]) % O.R, O.G1_GEN), O.g1_mul(zv[i * l + j], O.G1_GEN)]
+            Qa += [i * l + j, i * l + j, None]
+    Vp = bn.g2_points_from_aff(V)
+    Qpts = [Vp[q] if q is not None else O.G2_GEN for q in Qa]
+    e = nt.pairing(bn.g1_aff_tensor(Pa, device), bn.g2_aff_tensor(Qpts, device))
+    e3 = e.view(-1, 3, 96)
+    prod = nt.gt_mul(nt.gt_mul(e3[:, 0].contiguous(), e3[:, 1].contiguous()), e3[:, 2].contiguous())
+    return bool(nt.gt_eq(prod, A.contiguous()).all())

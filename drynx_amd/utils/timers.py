@@ -1,0 +1,99 @@
+"""Named wall-clock timers (reference: unlynx ``StartTimer/EndTimer`` over onet
+``simul/monitor``, 25 call sites; names kept identical for comparability:
+``<node>_DataCollectionProtocol``, ``JustExecution``, ``<node>_AggregationPhase``,
+``<node>_KeySwitchingPhase``, ``<name>_DPencoding``, ``<name>_AllProofs``,
+``<VN>_VerifyRange``, ``BI``, ``Decode``, ``Decryption``, ``GradientDescent``,
+``Simulation``...).  GPU work inside a timer is synchronised at the end so the
+interval is real device time, and each timer also emits a roctx range when
+profiling under rocprofv3."""
+from __future__ import annotations
+
+import contextlib
+import csv
+import threading
+import time
+from collections import defaultdict
+
+import torch
+
+_lock = threading.Lock()
+_records: dict = defaultdict(list)
+
+
+def _sync():
+    if torch.cuda.is_available() and torch.cuda.is_initialized():
+        torch.cuda.synchronize()
+
+
+class Timer:
+    def __init__(self, name: str, sync: bool = True):
+        self.name = name
+        self.sync = sync
+        self.t0 = None
+
+    def start(self):
+        if self.sync:
+            _sync()
+        self.t0 = time.perf_counter()
+        return self
+
+    def end(self) -> float:
+        if self.sync:
+            _sync()
+        dt = time.perf_counter() - self.t0
+        with _lock:
+            _records[self.name].append(dt)
+        return dt
+
+
+def start_timer(name: str, sync: bool = True) -> Timer:
+    return Timer(name, sync).start()
+
+
+def end_timer(t: Timer) -> float:
+    return t.end()
+
+
+@contextlib.contextmanager
+def timed(name: str, sync: bool = True):
+    rng = None
+    try:
+        if torch.cuda.is_available() and torch.cuda.is_initialized():
+            rng = torch.cuda.nvtx.range_push(name)
+    except Exception:  # roctx not present
+        rng = None
+    t = Timer(name, sync).start()
+    try:
+        yield t
+    finally:
+        t.end()
+        if rng is not None:
+            try:
+                torch.cuda.nvtx.range_pop()
+            except Exception:
+                pass
+
+
+def records() -> dict:
+    with _lock:
+        return {k: list(v) for k, v in _records.items()}
+
+
+def reset():
+    with _lock:
+        _records.clear()
+
+
+def summary() -> dict:
+    with _lock:
+        return {k: {"n": len(v), "sum": sum(v), "mean": sum(v) / len(v), "max": max(v)} for k, v in _records.items()}
+
+
+def write_csv(path: str):
+    """onet-simul-like CSV: one row per timer with n/sum/mean/max (parsed by simul.parse_time_data)."""
+    s = summary()
+    with open(path, "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["name", "n", "sum", "mean", "max"])
+        for k in sorted(s):
+            w.writerow([k, s[k]["n"], f"{s[k]['sum']:.6f}", f"{s[k]['mean']:.6f}", f"{s[k]['max']:.6f}"])
