@@ -172,33 +172,62 @@ int dx_bsgs_build(int on_gpu, void *stream, const uint32_t *tabB, int64_t m_baby
 int dx_bsgs_solve(int on_gpu, void *stream, const uint32_t *targets_jac, const uint32_t *giant_aff, const uint64_t *keys,
                   const int32_t *vals, int64_t cap, int64_t m_baby, int64_t n_giant, int64_t offset, int64_t *out,
                   uint8_t *found, int64_t n) {
+  // Giant steps are taken CH at a time in Jacobian coordinates and normalised
+  // with ONE field inversion (Montgomery's simultaneous-inversion trick):
+  // ~20 Fp multiplications per giant step instead of ~300.
+  constexpr int CH = 8;
   auto op = [=] __host__ __device__(int64_t i) {
     G1J cur = at<G1J>(targets_jac, i);
     G1A gneg = aneg(at<G1A>(giant_aff, 0));
     found[i] = 0;
     out[i] = 0;
-    for (int64_t g = 0; g < n_giant; g++) {
-      if (cur.is_inf()) {
-        out[i] = g * m_baby - offset;
+    for (int64_t g0 = 0; g0 < n_giant; g0 += CH) {
+      G1J pts[CH];
+      Fp pre[CH];
+      Fp acc = Fp::one();
+      for (int c = 0; c < CH; c++) {
+        pts[c] = cur;
+        Fp z = cur.is_inf() ? Fp::one() : cur.z;
+        acc = fmul(acc, z);
+        pre[c] = acc;
+        cur = jadd_mixed(cur, gneg);
+      }
+      Fp inv = finv(acc);
+      int64_t best = -1;
+      int64_t best_val = 0;
+      for (int c = CH - 1; c >= 0; c--) {
+        Fp z = pts[c].is_inf() ? Fp::one() : pts[c].z;
+        Fp zi = c ? fmul(inv, pre[c - 1]) : inv;
+        inv = fmul(inv, z);
+        int64_t g = g0 + c;
+        if (g >= n_giant) continue;
+        if (pts[c].is_inf()) {
+          best = g;
+          best_val = g * m_baby - offset;
+          continue;
+        }
+        Fp zi2 = fsqr(zi);
+        G1A a = {fmul(pts[c].x, zi2), fmul(fmul(pts[c].y, zi2), zi)};
+        uint64_t key = point_key(a);
+        uint64_t h = mix64(key) & (uint64_t)(cap - 1);
+        for (int64_t probe = 0; probe < cap; probe++) {
+          uint64_t kk = keys[h];
+          if (kk == 0) break;
+          if (kk == key) {
+            int64_t j = vals[h] >> 1;
+            bool same = (uint32_t)(vals[h] & 1) == (a.y.v[0] & 1u);
+            best = g;
+            best_val = g * m_baby + (same ? j : -j) - offset;
+            break;
+          }
+          h = (h + 1) & (uint64_t)(cap - 1);
+        }
+      }
+      if (best >= 0) {
+        out[i] = best_val;
         found[i] = 1;
         return;
       }
-      G1A a = to_affine(cur);
-      uint64_t key = point_key(a);
-      uint64_t h = mix64(key) & (uint64_t)(cap - 1);
-      for (int64_t probe = 0; probe < cap; probe++) {
-        uint64_t kk = keys[h];
-        if (kk == 0) break;
-        if (kk == key) {
-          int64_t j = vals[h] >> 1;
-          bool same = (uint32_t)(vals[h] & 1) == (a.y.v[0] & 1u);
-          out[i] = g * m_baby + (same ? j : -j) - offset;
-          found[i] = 1;
-          return;
-        }
-        h = (h + 1) & (uint64_t)(cap - 1);
-      }
-      cur = jadd_mixed(cur, gneg);
     }
   };
   return run(on_gpu, stream, n, op, true, "bsgs_solve");

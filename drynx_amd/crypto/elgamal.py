@@ -242,5 +242,26 @@ def decryption_table(bound: int = 10000, device="cpu") -> DecryptionTable:
     return t
 
 
+def decrypt_auto(secret: int, cv: CipherVector, bound: int = 10000, max_bound: int = 1 << 44) -> torch.Tensor:
+    """Decrypt with a table that grows (x256) until every plaintext is found:
+    aggregates of 1e6-record logistic regressions exceed the reference's fixed
+    10000-entry table."""
+    M = decrypt_points(secret, cv)
+    out = torch.zeros(len(cv), dtype=torch.int64, device=cv.device)
+    todo = torch.arange(len(cv), device=cv.device)
+    b = max(1, int(bound))
+    while todo.numel():
+        t = decryption_table(b, cv.device)
+        T = nt.g1_add(M.index_select(0, todo).contiguous(), t.offset_pt)
+        vals, found = nt.bsgs_solve(T, t.giant, t.keys, t.vals, t.m_baby, t.n_giant, t.bound)
+        ok = found.bool()
+        out[todo[ok]] = vals[ok]
+        todo = todo[~ok]
+        if b >= max_bound and todo.numel():
+            raise ValueError(f"{todo.numel()} plaintexts beyond +/-{max_bound}")
+        b = min(b * 256, max_bound)
+    return out
+
+
 def decrypt_ints(secret: int, cv: CipherVector, bound: int = 10000) -> list[int]:
     return [int(v) for v in decryption_table(bound, cv.device).decrypt(secret, cv).cpu().tolist()]

@@ -1,0 +1,115 @@
+"""Embedded bucketed key-value store (bbolt equivalent) for verifying nodes.
+
+Reference: each VN opens bbolt at ``"db:"+ServerIdentity.ID``
+(services/service_skipchain.go:77-86) and writes with ``libdrynx.UpdateDB``
+(lib/structs.go:571-588: batch put, create bucket if missing).  Buckets:
+  surveyID/<type>  key surveyID/type/sender/differInfo/VN -> proof bytes
+  <VN address>     key surveyID/map                        -> bitmap
+  genesis          key genesis                             -> genesis block
+  mapping          key surveyID                            -> block hash
+Here: SQLite (WAL) with one (bucket, key) -> blob table; writes can be queued
+to a background writer thread so proof persistence never sits on the
+verification critical path (``flush`` joins them).
+"""
+from __future__ import annotations
+
+import os
+import queue
+import sqlite3
+import threading
+
+
+class Store:
+    def __init__(self, path: str):
+        self.path = path
+        d = os.path.dirname(os.path.abspath(path))
+        os.makedirs(d, exist_ok=True)
+        self._lock = threading.RLock()
+        self._db = sqlite3.connect(path, check_same_thread=False, isolation_level=None)
+        self._db.execute("PRAGMA journal_mode=WAL")
+        self._db.execute("PRAGMA synchronous=NORMAL")
+        self._db.execute("CREATE TABLE IF NOT EXISTS kv (bucket TEXT, key TEXT, value BLOB, PRIMARY KEY(bucket, key))")
+        self._q: queue.Queue = queue.Queue()
+        self._writer = None
+        self.closed = False
+
+    # ------------------------------------------------------------- sync API
+    def update(self, bucket: str, key: str, value: bytes):
+        """UpdateDB(db, bucket, key, value)."""
+        with self._lock:
+            self._db.execute("INSERT OR REPLACE INTO kv(bucket, key, value) VALUES (?,?,?)", (bucket, key, value))
+
+    def update_many(self, rows):
+        with self._lock:
+            self._db.execute("BEGIN")
+            self._db.executemany("INSERT OR REPLACE INTO kv(bucket, key, value) VALUES (?,?,?)", rows)
+            self._db.execute("COMMIT")
+
+    def get(self, bucket: str, key: str):
+        with self._lock:
+            r = self._db.execute("SELECT value FROM kv WHERE bucket=? AND key=?", (bucket, key)).fetchone()
+        return None if r is None else bytes(r[0])
+
+    def bucket(self, bucket: str) -> dict:
+        with self._lock:
+            rows = self._db.execute("SELECT key, value FROM kv WHERE bucket=? ORDER BY key", (bucket,)).fetchall()
+        return {k: bytes(v) for k, v in rows}
+
+    def buckets(self) -> list:
+        with self._lock:
+            return [r[0] for r in self._db.execute("SELECT DISTINCT bucket FROM kv ORDER BY bucket").fetchall()]
+
+    def cursor_prefix(self, bucket_prefix: str) -> dict:
+        with self._lock:
+            rows = self._db.execute("SELECT bucket, key, value FROM kv WHERE bucket LIKE ? ORDER BY bucket, key",
+                                    (bucket_prefix + "%",)).fetchall()
+        return {(b, k): bytes(v) for b, k, v in rows}
+
+    # ------------------------------------------------------------- async writer
+    def update_async(self, bucket: str, key: str, value: bytes):
+        if self._writer is None:
+            self._writer = threading.Thread(target=self._drain, daemon=True)
+            self._writer.start()
+        self._q.put((bucket, key, value))
+
+    def _drain(self):
+        while True:
+            item = self._q.get()
+            if item is None:
+                self._q.task_done()
+                return
+            batch = [item]
+            while True:
+                try:
+                    nxt = self._q.get_nowait()
+                except queue.Empty:
+                    break
+                if nxt is None:
+                    self._q.put(None)
+                    self._q.task_done()
+                    break
+                batch.append(nxt)
+            self.update_many(batch)
+            for _ in batch:
+                self._q.task_done()
+
+    def flush(self):
+        if self._writer is not None:
+            self._q.join()
+
+    def close(self, remove: bool = False):
+        """HandleCloseDB: close and optionally delete the file (service_skipchain.go:323-342)."""
+        self.flush()
+        if self._writer is not None:
+            self._q.put(None)
+            self._writer.join(timeout=5)
+            self._writer = None
+        with self._lock:
+            self._db.close()
+        self.closed = True
+        if remove:
+            for suf in ("", "-wal", "-shm"):
+                try:
+                    os.remove(self.path + suf)
+                except FileNotFoundError:
+                    pass

@@ -1,0 +1,172 @@
+"""Proof request envelopes, signature checks and sampled verification.
+
+Reference: lib/proof/structs_proofs.go — ``ProofRequest`` union of five request
+types (:35-104); each ``New*ProofRequest`` marshals the proof and Schnorr-signs
+it with the sender's key; ``VerifyProof`` checks the signature in parallel with
+a *sampled* verification and returns a bitmap code (:22-27):
+0 false, 1 true, 2 received-not-checked, 4 bad signature.
+
+Sampling: reference semantics is ``rand.Float64() <= Threshold`` per VN.
+Extension ``SurveyQuery.VerificationSharding = k > 0``: the VNs split the work
+deterministically so every request is verified by exactly k VNs (the others
+record code 2) — disjoint batched verification across GPUs with guaranteed
+coverage.
+"""
+from __future__ import annotations
+
+import hashlib
+import random
+from dataclasses import dataclass, field
+from typing import Any
+
+from ..utils import timers
+from ..utils.log import get_logger
+from . import aggregation_shuffle as ags
+from . import range_proof as rp
+from . import sigma
+
+log = get_logger("proofs")
+
+PROOF_FALSE, PROOF_TRUE, PROOF_RECEIVED, PROOF_FALSE_SIGN = 0, 1, 2, 4
+# order of QueryToProofsNbrs (structs.go:567) and the VN-side order (service_skipchain.go:57-63)
+QUERY_ORDER = ["range", "shuffle", "aggregation", "obfuscation", "keyswitch"]
+VN_ORDER = ["range", "aggregation", "obfuscation", "shuffle", "keyswitch"]
+TIMER = {"range": "VerifyRange", "aggregation": "VerifyAggregation", "obfuscation": "VerifyObfuscation",
+         "shuffle": "VerifyShuffle", "keyswitch": "VerifyKeySwitch"}
+
+
+@dataclass
+class ProofRequest:
+    kind: str
+    survey_id: str
+    sender_id: str
+    differ_info: str
+    data: bytes
+    signature: bytes
+    obj: Any = field(default=None, repr=False, compare=False)  # decoded proof (in-process fast path)
+
+    def base_key(self) -> str:
+        return f"{self.survey_id}/{self.kind}/{self.sender_id}/{self.differ_info}"
+
+    def key(self, vn_addr: str) -> str:
+        return f"{self.base_key()}/{vn_addr}"
+
+    def digest(self) -> bytes:
+        return hashlib.sha256(self.data).digest()
+
+    def to_wire(self) -> dict:
+        return {"kind": self.kind, "survey_id": self.survey_id, "sender_id": self.sender_id,
+                "differ_info": self.differ_info, "data": self.data, "signature": self.signature}
+
+    @staticmethod
+    def from_wire(d: dict) -> "ProofRequest":
+        return ProofRequest(d["kind"], d["survey_id"], d["sender_id"], d["differ_info"], d["data"], d["signature"])
+
+
+def range_bundle_to_bytes(rpls) -> bytes:
+    out = [len(rpls).to_bytes(8, "little")]
+    for r in rpls:
+        b = r.to_bytes()
+        out += [len(b).to_bytes(8, "little"), b]
+    return b"".join(out)
+
+
+def range_bundle_from_bytes(b: bytes, device="cpu") -> list:
+    n = int.from_bytes(b[:8], "little")
+    o, out = 8, []
+    for _ in range(n):
+        ln = int.from_bytes(b[o: o + 8], "little")
+        o += 8
+        out.append(rp.RangeProofList.from_bytes(b[o: o + ln], device))
+        o += ln
+    return out
+
+
+def new_proof_request(kind: str, proof, survey_id: str, sender_id: str, differ_info: str, secret: int) -> ProofRequest:
+    """New{Range,Aggregation,Obfuscation,Shuffle,KeySwitch}ProofRequest: marshal + Schnorr-sign."""
+    data = range_bundle_to_bytes(proof) if kind == "range" else proof.to_bytes()
+    sig = sigma.schnorr_sign(secret, hashlib.sha256(data).digest())
+    return ProofRequest(kind, survey_id, sender_id, differ_info, data, sig, obj=proof)
+
+
+def verify_signature(req: ProofRequest, public) -> bool:
+    """VerifyProofSignature (structs_proofs.go:498-505)."""
+    return sigma.schnorr_verify(public, req.digest(), req.signature)
+
+
+def should_verify(sq, req: ProofRequest, vn_index: int, n_vns: int) -> bool:
+    shard = int(getattr(sq, "VerificationSharding", 0) or 0)
+    if shard > 0 and n_vns > 0:
+        h = int.from_bytes(hashlib.sha256(req.base_key().encode()).digest()[:8], "little")
+        return (vn_index - h) % n_vns < shard
+    return random.random() <= sq.Threshold
+
+
+class VerifierCache:
+    """Per-survey device material a VN reuses across requests (signature
+    tables, collective key)."""
+
+    def __init__(self):
+        self._sig = {}
+
+    def sigmat(self, sq, device):
+        key = (sq.SurveyID, str(device))
+        if key not in self._sig:
+            self._sig[key] = rp.SigMaterial(sq.Query.IVSigs.InputValidationSigs, device)
+        return self._sig[key]
+
+
+def _ranges_ok(sq, rpl) -> bool:
+    rg = sq.Query.Ranges
+    for j, col in enumerate(rpl.cols):
+        r = rg[col] if col < len(rg) else None
+        if r is None or int(r[0]) != rpl.u or int(r[1]) != rpl.l:
+            return False
+        if (int(r[2]) if len(r) > 2 else 0) != int(rpl.offset[j]):
+            return False
+    return True
+
+
+def verify_content(req: ProofRequest, sq, device, cache: VerifierCache) -> bool:
+    P = sq.RosterServers.aggregate()
+    if req.kind == "range":
+        rpls = req.obj if req.obj is not None else range_bundle_from_bytes(req.data, device)
+        sigs = sq.Query.IVSigs.InputValidationSigs
+        for r in rpls:
+            if not r.has_rp:
+                continue
+            if sigs is None or not _ranges_ok(sq, r):
+                return False
+            if not rp.verify_range_proof_list(r, cache.sigmat(sq, device), P, sq.RangeProofThreshold, device):
+                return False
+        return True
+    if req.kind == "aggregation":
+        pr = req.obj if req.obj is not None else ags.AggregationProof.from_bytes(req.data, device)
+        return ags.aggregation_list_proof_verification(pr, sq.AggregationProofThreshold)
+    if req.kind == "obfuscation":
+        pr = req.obj if req.obj is not None else sigma.ObfuscationProof.from_bytes(req.data, device)
+        return sigma.obfuscation_list_proof_verification(pr, sq.ObfuscationProofThreshold)
+    if req.kind == "shuffle":
+        pr = req.obj if req.obj is not None else ags.ShuffleProof.from_bytes(req.data, device)
+        return ags.shuffle_proof_verification(pr, P)
+    if req.kind == "keyswitch":
+        pr = req.obj if req.obj is not None else sigma.KeySwitchProof.from_bytes(req.data, device)
+        if pr.X != sq.IDtoPublic.get(req.sender_id) or pr.Q != sq.ClientPubKey:
+            return False
+        return sigma.key_switch_list_proof_verification(pr, sq.KeySwitchingProofThreshold)
+    raise ValueError(req.kind)
+
+
+def verify_proof(req: ProofRequest, sq, vn_id: str, vn_index: int, n_vns: int, device, cache: VerifierCache) -> int:
+    """<Kind>ProofRequest.VerifyProof -> bitmap code."""
+    with timers.timed(f"{vn_id}_{TIMER[req.kind]}"):
+        if not verify_signature(req, sq.IDtoPublic.get(req.sender_id)):
+            return PROOF_FALSE_SIGN
+        if not should_verify(sq, req, vn_index, n_vns):
+            return PROOF_RECEIVED
+        try:
+            ok = verify_content(req, sq, device, cache)
+        except Exception as e:  # malformed proof bytes => false, never a crash of the VN
+            log.warning(f"{vn_id}: {req.kind} proof from {req.sender_id} rejected: {e}")
+            ok = False
+        return PROOF_TRUE if ok else PROOF_FALSE

@@ -1,0 +1,121 @@
+"""ProofCollection: every proof request reaches the verifying nodes, which
+verify (sampled), persist, fill their bitmaps and append a ledger block.
+
+Reference: protocols/proof_collection_protocol.go — star tree prover root +
+all VNs (:84-305): each VN verifies, stores the proof in bbolt
+(``storeProof`` :307-406; bucket surveyID/type, key
+surveyID/type/sender/differInfo/VN; shuffle proofs are not stored), updates
+the bitmap, decrements the expected count; when done it persists its bitmap
+(bucket <VN>, key surveyID/map) and forwards it to the root VN, which builds
+the DataBlock and appends the skipchain (services/service_skipchain.go:96-158).
+
+MI355X mapping: the per-proof star broadcasts collapse into one personalised
+exchange of all requests to the ranks hosting VNs (xGMI all-to-all); each VN
+verifies every request it is assigned as one device batch; bitmaps and the
+block travel on the control plane.
+"""
+from __future__ import annotations
+
+import json
+
+from ..ledger import skipchain as skc
+from ..parallel.comm import bytes_to_obj, obj_to_bytes
+from ..proofs import requests as prq
+from ..query import query_to_proofs_nbrs
+from ..utils import timers
+from ..utils.log import get_logger
+
+log = get_logger("proof_collection")
+
+
+def expected_counts(sq) -> dict:
+    """QueryToProofsNbrs reordered to the VN order (service_skipchain.go:57-63)."""
+    q = query_to_proofs_nbrs(sq)
+    return dict(zip(prq.QUERY_ORDER, q))
+
+
+def fan_out(ctx, sq, local_requests: list) -> list:
+    """All requests, on every rank that hosts a VN (others get nothing)."""
+    vn_ranks = sorted({ctx.cluster.by_id(si.id).rank for si in sq.Query.RosterVNs.list})
+    if ctx.comm.world == 1:
+        return list(local_requests)
+    payload = obj_to_bytes([r.to_wire() for r in local_requests])
+    got = ctx.comm.exchange_bytes({d: payload for d in vn_ranks})
+    out = []
+    for src in sorted(got):
+        if src == ctx.rank:
+            out += list(local_requests)  # keep decoded objects for locally produced proofs
+        else:
+            out += [prq.ProofRequest.from_wire(d) for d in bytes_to_obj(got[src])]
+    return out
+
+
+def verify_and_store(ctx, sq, vn, vn_index: int, n_vns: int, requests: list) -> dict:
+    store = ctx.store(vn.id)
+    bitmap = {}
+    counts = {k: 0 for k in prq.VN_ORDER}
+    for req in requests:
+        code = prq.verify_proof(req, sq, vn.id, vn_index, n_vns, ctx.device, ctx.verifier_cache)
+        key = req.key(vn.id)
+        bitmap[key] = code
+        counts[req.kind] += 1
+        if req.kind != "shuffle":  # storeProof skips shuffle proofs (proof_collection_protocol.go:318-331)
+            store.update_async(f"{sq.SurveyID}/{req.kind}", key, req.data)
+    exp = expected_counts(sq)
+    for k in prq.VN_ORDER:
+        if counts[k] != exp[k]:
+            log.warning(f"{vn.id}: received {counts[k]} {k} proofs, expected {exp[k]}")
+    store.update(vn.id, f"{sq.SurveyID}/map", json.dumps(bitmap, sort_keys=True).encode())
+    ctx.local_bitmaps[(sq.SurveyID, vn.id)] = bitmap
+    return bitmap
+
+
+def proof_collection(ctx, sq, local_requests: list):
+    """Returns the new SkipBlock (on every rank)."""
+    vns = [ctx.cluster.by_id(si.id) for si in sq.Query.RosterVNs.list]
+    with timers.timed("ProofFanOut"):
+        reqs = fan_out(ctx, sq, local_requests)
+    bitmaps = {}
+    with timers.timed("ProofVerification"):
+        for idx, vn in enumerate(vns):
+            if vn.rank == ctx.rank:
+                bitmaps[vn.id] = verify_and_store(ctx, sq, vn, idx, len(vns), reqs)
+    # bitmaps -> root VN (SharedBMChannel)
+    allbm = {}
+    for d in ctx.comm.all_gather_object(bitmaps):
+        allbm.update(d)
+    root = vns[0]
+    block = None
+    t = timers.start_timer("BI", sync=False)
+    if ctx.rank == root.rank:
+        merged = {}
+        for vn in vns:
+            merged.update(allbm.get(vn.id, {}))
+        data = skc.new_data_block(sq.SurveyID, merged, [v.identity() for v in vns])
+        block = skc.make_block(ctx.last_block, data, [v.identity() for v in vns])
+    block_bytes = ctx.comm.broadcast_object(block.to_bytes() if block is not None else None, src=root.rank)
+    block = skc.SkipBlock.from_bytes(block_bytes)
+    # every VN runs the bitmap verifier (verifyFuncBitmap) and signs the forward link
+    sigs = {}
+    for vn in vns:
+        if vn.rank == ctx.rank:
+            if skc.verify_bitmap(block, ctx.local_bitmaps.get((sq.SurveyID, vn.id), {}), vn.id):
+                skc.sign_block(block, vn.id, vn.keypair.secret)
+                sigs[vn.id] = block.ForwardSignatures[vn.id]
+            else:
+                log.warning(f"{vn.id} refused block for survey {sq.SurveyID}")
+    for d in ctx.comm.all_gather_object(sigs):
+        block.ForwardSignatures.update(d)
+    for vn in vns:
+        if vn.rank == ctx.rank:
+            st = ctx.store(vn.id)
+            st.flush()
+            raw = block.to_bytes()
+            st.update("skipchain", block.Hash, raw)
+            st.update("skipchain", "latest", raw)
+            if block.Index == 0:
+                st.update("genesis", "genesis", raw)
+            st.update("mapping", sq.SurveyID, block.Hash.encode())
+    ctx.last_block = block
+    timers.end_timer(t)
+    return block

@@ -163,6 +163,10 @@ class SurveyQuery:
     ObfuscationProofThreshold: float = 0.0
     RangeProofThreshold: float = 0.0
     KeySwitchingProofThreshold: float = 0.0
+    # extension: >0 -> each proof request is verified by exactly this many VNs
+    # (deterministic sharding of the verification work across GPUs); 0 -> the
+    # reference's random sampling with probability Threshold.
+    VerificationSharding: int = 0
 
     # -------------------------------------------------------------- helpers
     def all_dps(self):
@@ -237,6 +241,7 @@ def _survey_from_dict(d: dict) -> SurveyQuery:
         ObfuscationProofThreshold=d.get("ObfuscationProofThreshold", 0.0),
         RangeProofThreshold=d.get("RangeProofThreshold", 0.0),
         KeySwitchingProofThreshold=d.get("KeySwitchingProofThreshold", 0.0),
+        VerificationSharding=d.get("VerificationSharding", 0),
     )
 
 

@@ -1,0 +1,175 @@
+"""The Drynx node runtime (one instance per rank = per GPU).
+
+Reference: services/service.go (CN orchestration, ``HandleSurveyQuery`` :263,
+phases :711-868), services/service_data_provider.go (DP), and
+services/service_skipchain.go (VN + skipchain + bbolt getters).  The reference
+runs each party as its own onet server and wires phases with goroutines and
+channels (with known ordering fragility); here every rank runs
+the same explicit phase sequence (SPMD) with collective barriers between
+phases, hosting any number of logical CN/DP/VN parties:
+
+  broadcast query -> DRO noise shuffle -> DataCollection (+ range proofs)
+  -> CollectiveAggregation (+ aggregation proofs) -> [Obfuscation (+ proofs)]
+  -> KeySwitching (+ proofs) -> result to the querier
+  -> ProofCollection at the VNs -> skipchain block
+
+Timer names follow the reference.
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass, field
+
+import torch
+
+from ..crypto.elgamal import CipherVector
+from ..ledger.skipchain import SkipBlock
+from ..ledger.store import Store
+from ..parallel.comm import Comm, LocalComm
+from ..parallel.ec_collectives import KeyIndex
+from ..parallel.topology import Cluster
+from ..proofs import range_proof as rp
+from ..proofs import requests as prq
+from ..protocols import computing_nodes as cnp
+from ..protocols import data_collection as dcp
+from ..protocols import proof_collection as pcp
+from ..query import SurveyQuery, add_diff_p, check_parameters
+from ..utils import timers
+from ..utils.log import get_logger
+
+log = get_logger("service")
+
+
+@dataclass
+class SurveyResult:
+    survey_id: str
+    result: CipherVector | None            # key-switched ciphertexts, groups x NbrOutput (root rank)
+    n_groups: int
+    n_out: int
+    block: SkipBlock | None = None
+    clear_dp: dict = field(default_factory=dict)
+
+    def groups(self):
+        return [self.result[g * self.n_out:(g + 1) * self.n_out] for g in range(self.n_groups)]
+
+
+class DrynxNode:
+    """Per-rank runtime hosting the logical parties placed on this rank."""
+
+    def __init__(self, cluster: Cluster, comm: Comm | None = None, workdir: str = "./drynx_db", device=None,
+                 dp_data: dict | None = None, shuffle_proof_k: int = 40):
+        self.comm = comm or LocalComm(device or ("cuda" if torch.cuda.is_available() else "cpu"))
+        self.rank = self.comm.rank
+        self.device = torch.device(device) if device is not None else self.comm.device
+        self.cluster = cluster
+        self.key_index = KeyIndex([p.id for p in cluster.parties])
+        self.workdir = workdir
+        self.dp_data = dp_data or {}
+        self.shuffle_proof_k = shuffle_proof_k
+        self._stores: dict = {}
+        self.verifier_cache = prq.VerifierCache()
+        self.local_bitmaps: dict = {}
+        self.last_block: SkipBlock | None = None
+        self.surveys: dict = {}
+
+    # ------------------------------------------------------------------ VN storage
+    def store(self, vn_id: str) -> Store:
+        s = self._stores.get(vn_id)
+        if s is None or s.closed:
+            s = self._stores[vn_id] = Store(os.path.join(self.workdir, f"db_{vn_id}.sqlite"))
+        return s
+
+    # ------------------------------------------------------------------ main entry
+    def run_survey(self, sq: SurveyQuery | None) -> SurveyResult:
+        """Collective: every rank calls it; rank 0 passes the SurveyQuery."""
+        d = self.comm.broadcast_object(sq.to_dict() if sq is not None else None, src=0)
+        sq = SurveyQuery.from_dict(d)
+        self.surveys[sq.SurveyID] = sq
+        if self.rank == 0 and not check_parameters(sq, add_diff_p(sq.Query.DiffP)):
+            log.warning("query parameters failed CheckParameters; continuing as the reference does")
+        proofs: list = []
+        q = sq.Query
+        n_groups = len(dcp.all_possible_groups(q.DPDataGen.GroupByValues))
+        n_out = q.Operation.NbrOutput
+        t_exec = timers.start_timer("JustExecution")
+        noise = cnp.dro_phase(self, sq, proofs)
+        cn_sums, cn_inputs, dp_results = dcp.data_collection(self, sq)
+        if dp_results:
+            n_out = len(next(iter(dp_results.values()))["cv"]) // n_groups
+        n_out = max(self.comm.all_gather_object(n_out if dp_results else 0)) or n_out
+        n_rows = n_groups * n_out
+        agg = cnp.collective_aggregation(self, sq, cn_sums, cn_inputs, n_rows, proofs)
+        if q.Obfuscation:
+            agg = cnp.obfuscation(self, sq, agg, n_rows, proofs)
+        result = cnp.key_switching(self, sq, agg, n_groups, n_out, noise, proofs)
+        if q.CuttingFactor and result is not None:
+            # CN truncates the replicated response (service.go:760-761)
+            per = n_out // q.CuttingFactor
+            result = CipherVector.cat([result[g * n_out: g * n_out + per] for g in range(n_groups)])
+            n_out = per
+        timers.end_timer(t_exec)
+        # range proofs of the local DPs (generated off the query's critical path in the reference)
+        if q.Proofs:
+            self._range_proofs(sq, dp_results, proofs)
+        block = None
+        if q.Proofs and q.RosterVNs is not None and len(q.RosterVNs.list):
+            block = pcp.proof_collection(self, sq, proofs)
+        clear = {k: v["clear"] for k, v in dp_results.items()}
+        return SurveyResult(sq.SurveyID, result, n_groups, n_out, block, clear)
+
+    def _range_proofs(self, sq, dp_results: dict, proofs: list):
+        q = sq.Query
+        P = sq.RosterServers.aggregate()
+        for dp_id, res in dp_results.items():
+            dp = self.cluster.by_id(dp_id)
+            with timers.timed(f"{dp_id}_AllProofs"):
+                lists = []
+                if any(b is not None for b in res["proofs"]):
+                    sigmat = self.verifier_cache.sigmat(sq, self.device)
+                    for b in res["proofs"]:
+                        if b is not None and len(b):
+                            lists += rp.create_range_proofs(b, sigmat, P, self.device)
+                else:  # no range proofs (ranges 0): ship the commitments only (dcp.go:283-288)
+                    lists.append(rp.RangeProofList(0, 0, 0, [0] * len(res["cv"]), list(range(len(res["cv"]))),
+                                                   res["cv"]))
+                proofs.append(prq.new_proof_request("range", lists, sq.SurveyID, dp_id, "", dp.keypair.secret))
+
+    # ------------------------------------------------------------------ VN getters (api_skipchain.go)
+    def get_genesis(self, vn_id: str):
+        raw = self.store(vn_id).get("genesis", "genesis")
+        return SkipBlock.from_bytes(raw) if raw else None
+
+    def get_latest_block(self, vn_id: str):
+        raw = self.store(vn_id).get("skipchain", "latest")
+        return SkipBlock.from_bytes(raw) if raw else None
+
+    def get_block(self, vn_id: str, survey_id: str):
+        st = self.store(vn_id)
+        h = st.get("mapping", survey_id)
+        if h is None:
+            return None
+        raw = st.get("skipchain", h.decode())
+        return SkipBlock.from_bytes(raw) if raw else None
+
+    def get_proofs(self, vn_id: str, survey_id: str) -> dict:
+        st = self.store(vn_id)
+        st.flush()
+        out = {}
+        for kind in prq.VN_ORDER:
+            out.update(st.bucket(f"{survey_id}/{kind}"))
+        return out
+
+    def get_bitmap(self, vn_id: str, survey_id: str) -> dict:
+        import json
+
+        raw = self.store(vn_id).get(vn_id, f"{survey_id}/map")
+        return json.loads(raw) if raw else {}
+
+    def close_db(self, vn_id: str, remove: bool = False):
+        s = self._stores.pop(vn_id, None)
+        if s is not None:
+            s.close(remove)
+
+    def close(self, remove: bool = False):
+        for k in list(self._stores):
+            self.close_db(k, remove)
