@@ -110,9 +110,20 @@ class VerifierCache:
         self._sig = {}
 
     def sigmat(self, sq, device):
-        key = (sq.SurveyID, str(device))
+        """Keyed by a digest of the signature set, so repeated surveys over the
+        same CN input-validation keys reuse the device tables."""
+        sigs = sq.Query.IVSigs.InputValidationSigs
+        h = hashlib.sha256()
+        for row in sigs:
+            for s in row:
+                h.update(s.Public)
+                h.update(s.Signature[:128])
+                h.update(len(s.Signature).to_bytes(4, "little"))
+        key = (h.hexdigest(), len(sigs), len(sigs[0]) if sigs else 0, str(device))
         if key not in self._sig:
-            self._sig[key] = rp.SigMaterial(sq.Query.IVSigs.InputValidationSigs, device)
+            if len(self._sig) > 8:
+                self._sig.clear()
+            self._sig[key] = rp.SigMaterial(sigs, device)
         return self._sig[key]
 
 

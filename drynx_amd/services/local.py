@@ -36,12 +36,17 @@ def local_cluster(n_cns=3, n_dps=5, n_vns=3, comm: Comm | None = None, device=No
 def make_signatures(cluster, ranges, device="cpu", deterministic=False):
     """InputValidationSigs[cn][col]: one BB key + u signatures per (CN, output)."""
     out = []
+    det: dict = {}
     for _ in cluster.cns:
         row = []
         for r in ranges:
             u = int(r[0])
-            row.append(rp.init_range_proof_signature_deterministic(u, device) if deterministic
-                       else rp.init_range_proof_signature(u, None, device))
+            if deterministic:  # InitRangeProofSignatureDeterministic: identical keys (x = 12), computed once per u
+                if u not in det:
+                    det[u] = rp.init_range_proof_signature_deterministic(u, device)
+                row.append(det[u])
+            else:
+                row.append(rp.init_range_proof_signature(u, None, device))
         out.append(row)
     return out
 

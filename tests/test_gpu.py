@@ -1,0 +1,128 @@
+"""GPU (gfx950) kernels vs the host path / oracle.  Run with -m gpu on an MI355X."""
+import random
+
+import pytest
+import torch
+
+from drynx_amd import native as nt
+from drynx_amd.crypto import bn254 as bn
+from drynx_amd.crypto import oracle as O
+
+pytestmark = pytest.mark.gpu
+RNG = random.Random(11)
+
+
+def _both(fn, *cpu_args):
+    """Run fn on CPU and on GPU copies of the args; return (cpu, gpu->cpu)."""
+    dev = torch.device("cuda", 0)
+    c = fn(*cpu_args)
+    g = fn(*[a.to(dev) if isinstance(a, torch.Tensor) else a for a in cpu_args])
+    torch.cuda.synchronize()
+    return c, (g.cpu() if isinstance(g, torch.Tensor) else g)
+
+
+def test_native_loaded_on_gpu(gpu_device):
+    assert nt.lib().dx_version() == 1
+    assert nt.loaded_path().endswith("libdrynx_native.so")
+
+
+def test_g1_ops_gpu_match_cpu(gpu_device):
+    ks = bn.scalars_tensor([RNG.randrange(O.R) for _ in range(300)] + [0, 1, O.R - 1])
+    c, g = _both(lambda k: nt.g1_fb_mul(bn.base_table(k.device), k), ks)
+    assert torch.equal(nt.g1_to_affine(c), nt.g1_to_affine(g))
+    J = bn.g1_jac_tensor([O.g1_mul(5, O.G1_GEN)])
+    c, g = _both(lambda j, k: nt.g1_to_affine(nt.g1_mul(j, k)), J, ks)
+    assert torch.equal(c, g)
+    x = bn.g1_jac_tensor([O.g1_mul(i + 1, O.G1_GEN) for i in range(40)]).view(8, 5, 24)
+    c, g = _both(lambda t: nt.g1_to_affine(nt.g1_sum(t)), x)
+    assert torch.equal(c, g)
+
+
+def test_fr_and_codecs_gpu(gpu_device):
+    a = bn.scalars_tensor([RNG.randrange(O.R) for _ in range(100)])
+    b = bn.scalars_tensor([RNG.randrange(O.R) for _ in range(100)])
+    for op in (nt.FR_ADD, nt.FR_SUB, nt.FR_MUL):
+        c, g = _both(lambda x, y: nt.fr_arith(op, x, y), a, b)
+        assert torch.equal(c, g)
+    pts = [O.g1_mul(RNG.randrange(O.R), O.G1_GEN) for _ in range(10)]
+    t = bn.g1_aff_tensor(pts, gpu_device)
+    assert bytes(bn.g1_aff_to_bytes(t).tobytes()) == b"".join(O.g1_to_bytes(p) for p in pts)
+
+
+def test_pairing_gpu_matches_oracle(gpu_device):
+    P = [O.g1_mul(RNG.randrange(1, O.R), O.G1_GEN) for _ in range(64)]
+    Q = [O.g2_mul(RNG.randrange(1, O.R), O.G2_GEN) for _ in range(2)] * 32
+    Pt, Qt = bn.g1_aff_tensor(P), bn.g2_aff_tensor(Q)
+    c, g = _both(nt.pairing, Pt, Qt)
+    assert torch.equal(c, g)
+    assert bn.gt_from_tensor(g[:1])[0] == O.pairing(P[0], Q[0])
+    c, g = _both(lambda p, q: nt.final_exp(nt.miller_loop(p, q)), Pt[:8], Qt[:8])
+    assert torch.equal(c, g)
+
+
+def test_g2_and_gt_gpu(gpu_device):
+    ks = bn.scalars_tensor([RNG.randrange(O.R) for _ in range(64)])
+    c, g = _both(lambda k: nt.g2_fb_mul(bn.base2_table(k.device), k), ks)
+    assert torch.equal(c, g)
+    c, g = _both(lambda k: nt.g2_mul(bn.g2_generator_aff(k.device), k), ks)
+    assert torch.equal(c, g)
+    e = nt.pairing(bn.g1_generator_aff(), bn.g2_generator_aff())
+    c, g = _both(lambda t, k: nt.gt_pow(t, k), e, ks[:16].contiguous())
+    assert torch.equal(c, g)
+
+
+def test_elgamal_and_bsgs_gpu(gpu_device):
+    from drynx_amd.crypto import elgamal as eg
+
+    kp = eg.KeyPair.generate()
+    pk = eg.pk_table(kp.public, gpu_device)
+    vals = [RNG.randrange(-10**6, 10**6) for _ in range(500)]
+    cv, _ = eg.encrypt_ints(pk, vals)
+    assert eg.decryption_table(10**6, gpu_device).decrypt(kp.secret, cv).cpu().tolist() == vals
+    big = [10**9 + 7, -(10**9) + 3]
+    cv2, _ = eg.encrypt_ints(pk, big)
+    assert eg.decrypt_auto(kp.secret, cv2, 10000).cpu().tolist() == big
+
+
+def test_lr_moments_mfma_matches_fp64(gpu_device):
+    for N, D in [(1000, 45), (4099, 9), (123, 48)]:
+        X = torch.randn(N, D, dtype=torch.float64, device=gpu_device)
+        w = torch.randn(N, dtype=torch.float64, device=gpu_device)
+        ref = (X * w[:, None]).T @ X
+        got = nt.lr_moments(X, w)
+        assert torch.allclose(got, ref, rtol=1e-10, atol=1e-9), (got - ref).abs().max()
+
+
+def test_range_proofs_gpu(gpu_device):
+    from drynx_amd.crypto import elgamal as eg
+    from drynx_amd.ops.encoding import CreateProofBatch
+    from drynx_amd.proofs import range_proof as rp
+
+    S, u, l = 3, 16, 4
+    sigs = [[rp.init_range_proof_signature(u, device=gpu_device) for _ in range(4)] for _ in range(S)]
+    sm = rp.SigMaterial(sigs, gpu_device)
+    P = eg.aggregate_keys([eg.KeyPair.generate().public for _ in range(S)])
+    vals = [0, 1, 65535, 1234]
+    cv, r = eg.encrypt_ints(eg.pk_table(P, gpu_device), vals)
+    rpl = rp.create_range_proofs(CreateProofBatch(vals, r, cv, [u] * 4, [l] * 4, [0, 1, 2, 3], [0] * 4), sm, P,
+                                 gpu_device)[0]
+    assert rp.verify_range_proof_list(rpl, sm, P, 1.0, gpu_device)
+    assert rp.verify_range_proof_single_reference(rpl.to("cpu"), 2, rp.SigMaterial(sigs, "cpu"), P)
+    rpl.zv[3, 0] ^= 1
+    assert not rp.verify_range_proof_list(rpl, sm, P, 1.0, gpu_device)
+
+
+def test_survey_end_to_end_gpu(gpu_device, tmp_path):
+    from drynx_amd.services.api import DrynxClient
+    from drynx_amd.services.local import local_cluster, make_survey
+
+    cl, node = local_cluster(3, 4, 2, device=gpu_device, workdir=str(tmp_path))
+    client = DrynxClient(node, device=gpu_device)
+    sq = make_survey(client, cl, "variance", query_min=0, query_max=50, rows=100, proofs=1, ranges=[16, 4],
+                     sig_device=gpu_device)
+    _, vals, res = client.send_survey_query(sq)
+    tot = [sum(v[0][i] for v in res.clear_dp.values()) for i in range(3)]
+    m = tot[0] / tot[1]
+    assert abs(vals[0][0] - (tot[2] / tot[1] - m * m)) < 1e-9
+    assert set(res.block.data_block().Proofs.values()) == {1}
+    node.close(remove=True)

@@ -1,0 +1,109 @@
+"""Native (host path of the HIP library) vs the Python oracle, bit-exact."""
+import random
+
+import pytest
+import torch
+
+from drynx_amd import native as nt
+from drynx_amd.crypto import bn254 as bn
+from drynx_amd.crypto import oracle as O
+
+RNG = random.Random(7)
+SCALARS = [0, 1, 2, 3, 255, 256, 2**64 - 1, 2**64 + 5, O.R - 1, O.R - 2] + [RNG.randrange(O.R) for _ in range(6)]
+
+
+def test_fp_mont_roundtrip():
+    vals = [0, 1, O.P - 1, 123456789] + [RNG.randrange(O.P) for _ in range(4)]
+    t = bn.to_tensor(bn.ints_to_limbs(vals), "cpu")
+    m = nt.fp_to_mont(t)
+    assert bn.limbs_to_ints(bn.to_numpy(m)) == [bn.mont(v) for v in vals]
+    assert bn.limbs_to_ints(bn.to_numpy(nt.fp_from_mont(m))) == vals
+
+
+@pytest.mark.parametrize("op", ["add", "sub", "mul", "neg", "inv"])
+def test_fr_arith(op):
+    a = [RNG.randrange(1, O.R) for _ in range(8)]
+    b = [RNG.randrange(O.R) for _ in range(8)]
+    ta, tb = bn.scalars_tensor(a), bn.scalars_tensor(b)
+    code = {"add": nt.FR_ADD, "sub": nt.FR_SUB, "mul": nt.FR_MUL, "neg": nt.FR_NEG, "inv": nt.FR_INV}[op]
+    out = bn.scalars_from_tensor(nt.fr_arith(code, ta, tb if op in ("add", "sub", "mul") else None))
+    f = {"add": lambda x, y: (x + y) % O.R, "sub": lambda x, y: (x - y) % O.R, "mul": lambda x, y: x * y % O.R,
+         "neg": lambda x, y: (-x) % O.R, "inv": lambda x, y: pow(x, -1, O.R)}[op]
+    assert out == [f(x, y) for x, y in zip(a, b)]
+
+
+def test_g1_fixed_and_variable_base():
+    tab = bn.base_table()
+    fb = bn.g1_points_from_jac(nt.g1_fb_mul(tab, bn.scalars_tensor(SCALARS)))
+    vb = bn.g1_points_from_jac(nt.g1_mul(bn.g1_jac_tensor([O.G1_GEN]), bn.scalars_tensor(SCALARS)))
+    exp = [O.g1_mul(k, O.G1_GEN) for k in SCALARS]
+    assert fb == exp and vb == exp
+
+
+def test_g1_signed_and_group_law():
+    m = torch.tensor([0, 1, -1, 5, -5, 2**40], dtype=torch.int64)
+    got = bn.g1_points_from_jac(nt.g1_fb_mul_i64(bn.base_table(), m))
+    assert got == [O.g1_mul_signed(int(v), O.G1_GEN) for v in m]
+    a = bn.g1_jac_tensor([O.g1_mul(3, O.G1_GEN), O.G1_GEN, None, O.G1_GEN])
+    b = bn.g1_jac_tensor([O.g1_mul(4, O.G1_GEN), O.G1_GEN, O.G1_GEN, O.g1_neg(O.G1_GEN)])
+    s = bn.g1_points_from_jac(nt.g1_add(a, b))
+    assert s == [O.g1_mul(7, O.G1_GEN), O.g1_mul(2, O.G1_GEN), O.G1_GEN, None]
+    assert nt.g1_eq(a, a).all()
+
+
+def test_g1_sum_reduction():
+    pts = [O.g1_mul(k + 1, O.G1_GEN) for k in range(3 * 5)]
+    x = bn.g1_jac_tensor(pts).view(5, 3, 24)
+    got = bn.g1_points_from_jac(nt.g1_sum(x))
+    exp = [O.g1_mul(sum(k * 3 + g + 1 for k in range(5)), O.G1_GEN) for g in range(3)]
+    assert got == exp
+
+
+def test_g2_mults():
+    ks = SCALARS[:6]
+    fb = bn.g2_points_from_aff(nt.g2_fb_mul(bn.base2_table(), bn.scalars_tensor(ks)))
+    vb = bn.g2_points_from_aff(nt.g2_mul(bn.g2_generator_aff(), bn.scalars_tensor(ks)))
+    exp = [O.g2_mul(k, O.G2_GEN) for k in ks]
+    assert fb == exp and vb == exp
+
+
+def test_pairing_matches_oracle():
+    P = [O.G1_GEN, O.g1_mul(5, O.G1_GEN), None]
+    Q = [O.G2_GEN, O.g2_mul(3, O.G2_GEN), O.G2_GEN]
+    e = bn.gt_from_tensor(nt.pairing(bn.g1_aff_tensor(P), bn.g2_aff_tensor(Q)))
+    e0 = O.pairing(O.G1_GEN, O.G2_GEN)
+    assert e[0] == e0 and e[1] == e0 ** 15 and e[2] == O.Fp12.one()
+    ml = nt.miller_loop(bn.g1_aff_tensor(P[:1]), bn.g2_aff_tensor(Q[:1]))
+    assert bn.gt_from_tensor(nt.final_exp(ml))[0] == e0
+
+
+def test_gt_ops():
+    e0 = O.pairing(O.G1_GEN, O.G2_GEN)
+    t = bn.gt_tensor([e0])
+    ks = [0, 1, 7, 2**70 + 3, O.R - 1]
+    got = bn.gt_from_tensor(nt.gt_pow(t, bn.scalars_tensor(ks)))
+    assert got == [e0 ** k for k in ks]
+    tab = nt.gt_fb_table(t)
+    assert bn.gt_from_tensor(nt.gt_fb_pow(tab, bn.scalars_tensor(ks))) == got
+    sq = nt.gt_mul(t, t)
+    assert bn.gt_from_tensor(sq)[0] == e0 * e0
+    prod = nt.gt_prod(torch.stack([t, sq, t]).view(3, 1, 96))
+    assert bn.gt_from_tensor(prod)[0] == e0 ** 4
+
+
+def test_wire_codecs_match_oracle():
+    p = O.g1_mul(99, O.G1_GEN)
+    q = O.g2_mul(99, O.G2_GEN)
+    e = O.pairing(p, q)
+    assert bytes(bn.g1_aff_to_bytes(bn.g1_aff_tensor([p]))[0]) == O.g1_to_bytes(p)
+    assert bytes(bn.g2_aff_to_bytes(bn.g2_aff_tensor([q]))[0]) == O.g2_to_bytes(q)
+    assert bytes(bn.gt_to_bytes(bn.gt_tensor([e]))[0]) == O.gt_to_bytes(e)
+    assert bn.g1_points_from_aff(bn.g1_aff_from_bytes(O.g1_to_bytes(p))) == [p]
+    assert bn.g2_points_from_aff(bn.g2_aff_from_bytes(O.g2_to_bytes(q))) == [q]
+    with pytest.raises(ValueError):
+        bn.g1_aff_from_bytes(b"\x00" * 63 + b"\x05")
+
+
+def test_random_scalars_in_range():
+    s = bn.scalars_from_tensor(bn.random_scalars(500))
+    assert all(0 < v < O.R for v in s) and len(set(s)) == 500
