@@ -314,7 +314,7 @@ def decode(cv: eg.CipherVector, secret: int, operation: Operation, table: Option
             return [float(b != 0) for b in nz]
         return [float(b == 0) for b in nz]
     table = table or eg.decryption_table(10000, cv.device)
-    vals = _dec(table.decrypt(secret, cv).cpu().tolist())
+    vals = _dec(eg.decrypt_auto(secret, cv, table.bound).cpu().tolist())
     if name == "logistic regression":
         from ..models.logistic_regression import decode_logistic_regression_values
 

@@ -1,0 +1,75 @@
+"""lib/range/range_proof_test.go equivalents + batched-vs-reference checks."""
+import pytest
+
+from drynx_amd.crypto import elgamal as eg
+from drynx_amd.ops.encoding import CreateProofBatch
+from drynx_amd.proofs import range_proof as rp
+
+
+@pytest.fixture(scope="module")
+def setup():
+    S, u, l = 2, 4, 3
+    sigs = [[rp.init_range_proof_signature(u) for _ in range(3)] for _ in range(S)]
+    kps = [eg.KeyPair.generate() for _ in range(S)]
+    P = eg.aggregate_keys([k.public for k in kps])
+    return S, u, l, sigs, rp.SigMaterial(sigs), P, eg.pk_table(P)
+
+
+def _prove(setup, vals, offs=None):
+    S, u, l, sigs, sm, P, pk = setup
+    cv, r = eg.encrypt_ints(pk, vals)
+    n = len(vals)
+    b = CreateProofBatch(vals, r, cv, [u] * n, [l] * n, list(range(n)), offs or [0] * n)
+    return rp.create_range_proofs(b, sm, P)[0]
+
+
+def test_valid_proofs_verify_batched_and_reference(setup):
+    rpl = _prove(setup, [0, 17, 63])
+    sm, P = setup[4], setup[5]
+    assert rp.verify_range_proof_list(rpl, sm, P)
+    assert all(rp.verify_range_proof_single_reference(rpl, p, sm, P) for p in range(3))
+
+
+def test_out_of_range_fails(setup):
+    rpl = _prove(setup, [64])  # 4^3 = 64 is out of range
+    assert not rp.verify_range_proof_list(rpl, setup[4], setup[5])
+    assert not rp.verify_range_proof_single_reference(rpl, 0, setup[4], setup[5])
+
+
+@pytest.mark.parametrize("field", ["A", "V", "zv", "zphi", "zr", "challenge"])
+def test_tampering_detected(setup, field):
+    rpl = _prove(setup, [5, 6])
+    t = getattr(rpl, field)
+    t[-1, 3] ^= 4
+    assert not rp.verify_range_proof_list(rpl, setup[4], setup[5])
+
+
+def test_bytes_roundtrip_and_no_proof_case(setup):
+    rpl = _prove(setup, [1, 2])
+    back = rp.RangeProofList.from_bytes(rpl.to_bytes())
+    assert rp.verify_range_proof_list(back, setup[4], setup[5])
+    empty = rp.RangeProofList(0, 0, 0, [0], [0], rpl.commit[:1])
+    assert rp.verify_range_proof_list(empty, setup[4], setup[5])  # u = l = 0 -> true (range_proof.go:508)
+
+
+def test_threshold_checks_only_prefix(setup):
+    rpl = _prove(setup, [1, 64])  # second proof is bad
+    sm, P = setup[4], setup[5]
+    assert rp.verify_range_proof_list(rpl, sm, P, threshold=0.5)  # only the first ceil(0.5*2)=1
+    assert not rp.verify_range_proof_list(rpl, sm, P, threshold=1.0)
+
+
+def test_signed_offset_extension(setup):
+    rpl = _prove(setup, [-30, 31], offs=[32, 32])
+    assert rp.verify_range_proof_list(rpl, setup[4], setup[5])
+
+
+def test_to_base():
+    assert rp.to_base(13, 2, 6) == [1, 0, 1, 1, 0, 0]
+    assert rp.to_base(-5, 16, 3) == [0, 0, 0]  # reference: non-positive -> zeros
+
+
+def test_deterministic_signature():
+    a = rp.init_range_proof_signature_deterministic(3)
+    b = rp.init_range_proof_signature_deterministic(3)
+    assert a == b and len(a.Signature) == 3 * 128

@@ -1,0 +1,151 @@
+"""In-process multi-party surveys (the onet LocalTest analogue): every
+operation end to end, proofs + VNs + skipchain, getters, malicious parties."""
+import pytest
+import torch
+
+from drynx_amd.crypto import elgamal as eg
+from drynx_amd.ops import encoding as enc
+from drynx_amd.proofs import requests as prq
+from drynx_amd.query import QueryDiffP
+from drynx_amd.services.api import DrynxClient
+from drynx_amd.services.local import local_cluster, make_survey
+
+
+@pytest.fixture(scope="module")
+def env(tmp_path_factory):
+    cl, node = local_cluster(3, 5, 3, device="cpu", workdir=str(tmp_path_factory.mktemp("db")))
+    yield cl, node, DrynxClient(node)
+    node.close(remove=True)
+
+
+def _sum_clear(res, n):
+    return [sum(v[0][i] for v in res.clear_dp.values()) for i in range(n)]
+
+
+@pytest.mark.parametrize("op", ["sum", "mean", "variance", "cosim", "frequencyCount", "lin_reg", "MLeval"])
+def test_numeric_ops_match_clear(env, op):
+    cl, node, client = env
+    sq = make_survey(client, cl, op, query_min=0, query_max=6, rows=12, d=2)
+    _, vals, res = client.send_survey_query(sq)
+    n = sq.Query.Operation.NbrOutput
+    tot = _sum_clear(res, n)
+    exp = enc.decode_values(op, tot, sq.Query.Operation)
+    assert vals[0] == pytest.approx(exp, rel=1e-9, abs=1e-9)
+
+
+@pytest.mark.parametrize("op", ["min", "max", "bool_OR", "bool_AND", "union", "inter"])
+def test_boolean_ops(env, op):
+    cl, node, client = env
+    dp_data = {}
+    rows = [[2, 3, 5], [4, 5, 6], [3, 4, 5], [1, 5, 5], [5, 5, 2]]
+    for i, dp in enumerate(cl.dps):
+        dp_data[dp.id] = [torch.tensor(rows[i], dtype=torch.int64)]
+    node.dp_data = dp_data
+    try:
+        sq = make_survey(client, cl, op, query_min=0, query_max=6, rows=3)
+        _, vals, _ = client.send_survey_query(sq)
+    finally:
+        node.dp_data = {}
+    sets = [set(r) for r in rows]
+    exp = {"min": [1.0], "max": [6.0], "bool_OR": [1.0], "bool_AND": [0.0],
+           "union": [float(any(i in s for s in sets)) for i in range(7)],
+           "inter": [float(all(i in s for s in sets)) for i in range(7)]}[op]
+    assert vals[0] == exp
+
+
+def test_group_by_and_cutting_factor(env):
+    cl, node, client = env
+    sq = make_survey(client, cl, "mean", query_min=0, query_max=9, rows=10, group_by=(3, 2))
+    groups, vals, res = client.send_survey_query(sq)
+    assert len(groups) == 6 and all(v == vals[0] for v in vals)
+    sq = make_survey(client, cl, "sum", query_min=0, query_max=9, rows=10, cutting_factor=3)
+    _, vals, res = client.send_survey_query(sq)
+    assert vals[0][0] == sum(v[0][0] for v in res.clear_dp.values())
+
+
+def test_proofs_skipchain_and_getters(env):
+    cl, node, client = env
+    sq = make_survey(client, cl, "frequencyCount", query_min=0, query_max=3, rows=6, proofs=1, ranges=[2, 4])
+    _, vals, res = client.send_survey_query(sq)
+    assert vals[0] == [float(x) for x in _sum_clear(res, 4)]
+    b = res.block
+    codes = b.data_block().Proofs
+    assert set(codes.values()) == {prq.PROOF_TRUE}
+    assert len(codes) == 3 * (5 + 3 + 3)  # VNs x (range per DP + aggregation per CN + keyswitch per CN)
+    assert b.verify_signatures({p.id: p.public for p in cl.parties})
+    assert client.send_get_block("vn2", sq.SurveyID).Hash == b.Hash
+    assert client.send_get_latest_block("vn0").Hash == b.Hash
+    assert client.send_get_genesis("vn1") is not None
+    proofs = client.send_get_proofs("vn0", sq.SurveyID)
+    assert len(proofs) == 5 + 3 + 3 and all(k.endswith("/vn0") for k in proofs)
+    assert node.get_bitmap("vn1", sq.SurveyID) == {k: v for k, v in codes.items() if k.endswith("/vn1")}
+    # second survey appends a linked block
+    sq2 = make_survey(client, cl, "sum", query_min=0, query_max=3, rows=6, proofs=1, ranges=[2, 4])
+    _, _, res2 = client.send_survey_query(sq2)
+    assert res2.block.BackLink == b.Hash and res2.block.Index == b.Index + 1
+
+
+def test_obfuscation_and_diffp_with_proofs(env):
+    cl, node, client = env
+    node.shuffle_proof_k = 6
+    sq = make_survey(client, cl, "union", query_min=0, query_max=4, rows=4, proofs=1, ranges=[2, 1],
+                     obfuscation=True)
+    _, vals, res = client.send_survey_query(sq)
+    assert set(res.block.data_block().Proofs.values()) == {1}
+    dp = QueryDiffP(LapMean=0.0, LapScale=1.0, NoiseListSize=8, Quanta=1.0, Scale=1.0, Limit=3)
+    sq = make_survey(client, cl, "sum", query_min=0, query_max=4, rows=4, proofs=1, ranges=[16, 4], diffp=dp)
+    _, vals, res = client.send_survey_query(sq)
+    assert abs(vals[0][0] - sum(v[0][0] for v in res.clear_dp.values())) <= 3
+    kinds = {k.split("/")[1] for k in res.block.data_block().Proofs}
+    assert kinds == {"range", "aggregation", "keyswitch", "shuffle"}
+
+
+def test_malicious_dp_and_bad_signature_recorded(env, monkeypatch):
+    """Fault injection: a DP lying about its range and a forged
+    envelope signature show up as bitmap codes 0 and 4."""
+    cl, node, client = env
+    orig = node._range_proofs
+
+    def evil(sq, dp_results, proofs):
+        orig(sq, dp_results, proofs)
+        for r in proofs:
+            if r.kind == "range" and r.sender_id == "dp0":
+                r.obj[0].zv[0, 1] ^= 1  # corrupt after signing -> content false
+                r.data = prq.range_bundle_to_bytes(r.obj)
+                r.signature = __import__("drynx_amd.proofs.sigma", fromlist=["x"]).schnorr_sign(
+                    cl.by_id("dp0").keypair.secret, r.digest())
+            if r.kind == "range" and r.sender_id == "dp1":
+                r.signature = b"\x00" * 96
+    monkeypatch.setattr(node, "_range_proofs", evil)
+    sq = make_survey(client, cl, "sum", query_min=0, query_max=3, rows=4, proofs=1, ranges=[16, 2])
+    _, _, res = client.send_survey_query(sq)
+    codes = res.block.data_block().Proofs
+    assert {v for k, v in codes.items() if "/range/dp0/" in k} == {prq.PROOF_FALSE}
+    assert {v for k, v in codes.items() if "/range/dp1/" in k} == {prq.PROOF_FALSE_SIGN}
+    assert {v for k, v in codes.items() if "/range/dp2/" in k} == {prq.PROOF_TRUE}
+
+
+def test_sampled_verification_codes(env):
+    cl, node, client = env
+    sq = make_survey(client, cl, "sum", query_min=0, query_max=3, rows=4, proofs=1, ranges=[16, 2],
+                     verification_sharding=1)
+    _, _, res = client.send_survey_query(sq)
+    codes = res.block.data_block().Proofs
+    by_req = {}
+    for k, v in codes.items():
+        by_req.setdefault(k.rsplit("/", 1)[0], []).append(v)
+    for v in by_req.values():
+        assert sorted(v) == [1, 2, 2]  # exactly one VN verified each request
+
+
+def test_close_db(env, tmp_path):
+    cl, node = local_cluster(2, 2, 1, device="cpu", workdir=str(tmp_path))
+    client = DrynxClient(node)
+    sq = make_survey(client, cl, "sum", query_min=0, query_max=3, rows=4, proofs=1, ranges=[16, 2])
+    client.send_survey_query(sq)
+    import os
+
+    path = os.path.join(str(tmp_path), "db_vn0.sqlite")
+    assert os.path.exists(path)
+    client.send_close_db("vn0", remove=True)
+    assert not os.path.exists(path)

@@ -1,0 +1,84 @@
+"""Obfuscation (incl. the negative test of obfuscation_proof_test.go:30-31),
+key-switch, Schnorr, aggregation and shuffle proofs."""
+import torch
+
+from drynx_amd.crypto import bn254 as bn
+from drynx_amd.crypto import elgamal as eg
+from drynx_amd.crypto import oracle as O
+from drynx_amd.proofs import aggregation_shuffle as ags
+from drynx_amd.proofs import sigma
+
+
+def _cv(vals):
+    kp = eg.KeyPair.generate()
+    pk = eg.pk_table(kp.public)
+    return kp, pk, eg.encrypt_ints(pk, vals)[0]
+
+
+def test_schnorr():
+    x = O.random_scalar()
+    X = O.g1_mul(x, O.G1_GEN)
+    sig = sigma.schnorr_sign(x, b"msg")
+    assert len(sig) == 96 and sigma.schnorr_verify(X, b"msg", sig)
+    assert not sigma.schnorr_verify(X, b"msh", sig)
+    assert not sigma.schnorr_verify(O.g1_mul(2, X), b"msg", sig)
+
+
+def test_obfuscation_proof_positive_and_negative():
+    kp, pk, C = _cv([0, 3, 0, 9])
+    s = bn.random_scalars(4)
+    Co = C.mul_scalars(s)
+    pr = sigma.obfuscation_list_proof_creation(C, Co, s)
+    assert sigma.obfuscation_list_proof_verification(pr)
+    back = sigma.ObfuscationProof.from_bytes(pr.to_bytes())
+    assert sigma.obfuscation_list_proof_verification(back)
+    wrong = sigma.obfuscation_list_proof_creation(C, Co, bn.random_scalars(4))  # wrong scalar -> false
+    assert not sigma.obfuscation_list_proof_verification(wrong)
+    assert eg.decrypt_check_zero(kp.secret, Co).tolist() == [0, 1, 0, 1]
+
+
+def test_key_switch_share_and_proof():
+    xs = [O.random_scalar() for _ in range(3)]
+    P = eg.aggregate_keys([O.g1_mul(x, O.G1_GEN) for x in xs])
+    cv, _ = eg.encrypt_ints(eg.pk_table(P), [5, -7])
+    q = eg.KeyPair.generate()
+    Ks, Cs = [], []
+    for x in xs:
+        share, v = sigma.key_switch_share(x, cv.K, q.public)
+        pr = sigma.key_switch_list_proof_creation(x, O.g1_mul(x, O.G1_GEN), q.public, cv.K, share, v)
+        assert sigma.key_switch_list_proof_verification(pr)
+        assert sigma.key_switch_list_proof_verification(sigma.KeySwitchProof.from_bytes(pr.to_bytes()))
+        Ks.append(share)
+    tot = eg.CipherVector.sum(Ks)
+    switched = eg.CipherVector(tot.K, __import__("drynx_amd").native.g1_add(cv.C, tot.C))
+    assert eg.decrypt_ints(q.secret, switched) == [5, -7]
+    # a share computed with the wrong secret does not verify
+    share, v = sigma.key_switch_share(xs[0] + 1, cv.K, q.public)
+    bad = sigma.key_switch_list_proof_creation(xs[0], O.g1_mul(xs[0], O.G1_GEN), q.public, cv.K, share, v)
+    assert not sigma.key_switch_list_proof_verification(bad)
+
+
+def test_aggregation_proof():
+    kp, pk, a = _cv([1, 2])
+    b, _ = eg.encrypt_ints(pk, [3, 4])
+    pr = ags.aggregation_list_proof_creation([a, b], a.add(b))
+    assert ags.aggregation_list_proof_verification(pr)
+    assert ags.aggregation_list_proof_verification(ags.AggregationProof.from_bytes(pr.to_bytes()))
+    assert not ags.aggregation_list_proof_verification(ags.aggregation_list_proof_creation([a, b], a.add(a)))
+
+
+def test_shuffle_proof():
+    kp, pk, X = _cv([1, 2, 3, 4, 5])
+    Y, perm, rho = ags.shuffle_sequence(X, kp.public)
+    assert sorted(eg.decrypt_ints(kp.secret, Y)) == [1, 2, 3, 4, 5]
+    pr = ags.shuffle_proof_creation(X, Y, perm, rho, kp.public, k=12)
+    assert ags.shuffle_proof_verification(pr, kp.public)
+    assert ags.shuffle_proof_verification(ags.ShuffleProof.from_bytes(pr.to_bytes()), kp.public)
+    Z, _ = eg.encrypt_ints(pk, [1, 2, 3, 4, 6])  # not a shuffle of X
+    pr2 = ags.shuffle_proof_creation(X, Z, perm, rho, kp.public, k=12)
+    assert not ags.shuffle_proof_verification(pr2, kp.public)
+
+
+def test_noise_generation():
+    v = ags.generate_noise_values_scale(100, 0.0, 2.0, 1.0, 1.0, 10)
+    assert len(v) == 100 and max(abs(x) for x in v) <= 10 and v.count(0) > v.count(5)
