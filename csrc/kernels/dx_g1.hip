@@ -37,19 +37,31 @@ int dx_fr_arith(int on_gpu, void *stream, int opc, const uint32_t *a, const uint
 }
 
 // ---------------------------------------------------------------- G1
-int dx_g1_fb_table(int on_gpu, void *stream, const uint32_t *base_aff, uint32_t *table) {
-  auto op = [=] __host__ __device__(int64_t i) {
-    int w = (int)(i >> 8), d = (int)(i & 255);
-    uint32_t k[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    // k = d << (8w)
-    int bit = 8 * w;
-    uint64_t v = (uint64_t)d << (bit & 31);
-    k[bit >> 5] = (uint32_t)v;
-    if ((bit >> 5) + 1 < 8) k[(bit >> 5) + 1] = (uint32_t)(v >> 32);
-    G1J p = G1J::from_aff(at<G1A>(base_aff, 0));
-    at<G1A>(table, i) = d ? to_affine(scalar_mul(p, k)) : G1A::inf();
+// Comb tables for n_bases points: table[b][w*256+d] = d * 2^(8w) * base_b (affine).
+// Two phases: (1) one thread per base walks the 256 doublings 2^k * base into
+// `work` ([n_bases][256] Jacobian); (2) one thread per entry adds the <= 8
+// powers selected by the bits of d and normalises (~400 Fp mults per entry
+// instead of a 256-bit scalar multiplication).
+int dx_g1_fb_table(int on_gpu, void *stream, const uint32_t *bases_aff, uint32_t *work, uint32_t *table,
+                   int64_t n_bases) {
+  auto p1 = [=] __host__ __device__(int64_t b) {
+    G1J acc = G1J::from_aff(at<G1A>(bases_aff, b));
+    for (int k = 0; k < 256; k++) {
+      at<G1J>(work, b * 256 + k) = acc;
+      acc = jdbl(acc);
+    }
   };
-  return run(on_gpu, stream, 32 * 256, op, true, "g1_fb_table");
+  int rc = run(on_gpu, stream, n_bases, p1, true, "g1_fb_table_pow2");
+  if (rc) return rc;
+  auto p2 = [=] __host__ __device__(int64_t t) {
+    int64_t b = t / 8192, i = t % 8192;
+    int w = (int)(i >> 8), d = (int)(i & 255);
+    G1J acc = G1J::inf();
+    for (int bit = 0; bit < 8; bit++)
+      if ((d >> bit) & 1) acc = jadd(acc, at<G1J>(work, b * 256 + 8 * w + bit));
+    at<G1A>(table, t) = to_affine(acc);
+  };
+  return run(on_gpu, stream, n_bases * 8192, p2, true, "g1_fb_table");
 }
 
 int dx_g1_fb_mul(int on_gpu, void *stream, const uint32_t *table, const uint32_t *scalars, uint32_t *out, int64_t n) {

@@ -7,18 +7,27 @@
 
 extern "C" {
 // ---------------------------------------------------------------- G2
-int dx_g2_fb_table(int on_gpu, void *stream, const uint32_t *base_aff, uint32_t *table) {
-  auto op = [=] __host__ __device__(int64_t i) {
-    int w = (int)(i >> 8), d = (int)(i & 255);
-    uint32_t k[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    int bit = 8 * w;
-    uint64_t v = (uint64_t)d << (bit & 31);
-    k[bit >> 5] = (uint32_t)v;
-    if ((bit >> 5) + 1 < 8) k[(bit >> 5) + 1] = (uint32_t)(v >> 32);
-    G2J p = G2J::from_aff(at<G2A>(base_aff, 0));
-    at<G2A>(table, i) = d ? to_affine(scalar_mul(p, k)) : G2A::inf();
+// Same two-phase comb-table build as dx_g1_fb_table, over the twist.
+int dx_g2_fb_table(int on_gpu, void *stream, const uint32_t *bases_aff, uint32_t *work, uint32_t *table,
+                   int64_t n_bases) {
+  auto p1 = [=] __host__ __device__(int64_t b) {
+    G2J acc = G2J::from_aff(at<G2A>(bases_aff, b));
+    for (int k = 0; k < 256; k++) {
+      at<G2J>(work, b * 256 + k) = acc;
+      acc = jdbl(acc);
+    }
   };
-  return run(on_gpu, stream, 32 * 256, op, true, "g2_fb_table");
+  int rc = run(on_gpu, stream, n_bases, p1, true, "g2_fb_table_pow2");
+  if (rc) return rc;
+  auto p2 = [=] __host__ __device__(int64_t t) {
+    int64_t b = t / 8192, i = t % 8192;
+    int w = (int)(i >> 8), d = (int)(i & 255);
+    G2J acc = G2J::inf();
+    for (int bit = 0; bit < 8; bit++)
+      if ((d >> bit) & 1) acc = jadd(acc, at<G2J>(work, b * 256 + 8 * w + bit));
+    at<G2A>(table, t) = to_affine(acc);
+  };
+  return run(on_gpu, stream, n_bases * 8192, p2, true, "g2_fb_table");
 }
 
 // out[i] = k[i] * base, table chosen per item from tables[tab_idx[i]] (tab_idx may be null -> table 0)

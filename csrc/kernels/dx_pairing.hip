@@ -41,18 +41,27 @@ int dx_gt_eq(int on_gpu, void *stream, const uint32_t *a, const uint32_t *b, uin
 }
 
 // comb table for fixed-base GT exponentiation (32 x 256 entries of Fp12)
-int dx_gt_fb_table(int on_gpu, void *stream, const uint32_t *base, uint32_t *table, int64_t n_bases) {
-  auto op = [=] __host__ __device__(int64_t t) {
+// Two-phase comb table in GT: 256 cyclotomic squarings per base, then <= 7
+// Fp12 products per entry.
+int dx_gt_fb_table(int on_gpu, void *stream, const uint32_t *base, uint32_t *work, uint32_t *table, int64_t n_bases) {
+  auto p1 = [=] __host__ __device__(int64_t b) {
+    Fp12 acc = at<Fp12>(base, b);
+    for (int k = 0; k < 256; k++) {
+      at<Fp12>(work, b * 256 + k) = acc;
+      acc = cyclotomic_sqr(acc);
+    }
+  };
+  int rc = run(on_gpu, stream, n_bases, p1, true, "gt_fb_table_pow2");
+  if (rc) return rc;
+  auto p2 = [=] __host__ __device__(int64_t t) {
     int64_t b = t / 8192, i = t % 8192;
     int w = (int)(i >> 8), d = (int)(i & 255);
-    uint32_t k[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    int bit = 8 * w;
-    uint64_t v = (uint64_t)d << (bit & 31);
-    k[bit >> 5] = (uint32_t)v;
-    if ((bit >> 5) + 1 < 8) k[(bit >> 5) + 1] = (uint32_t)(v >> 32);
-    at<Fp12>(table, t) = gt_pow(at<Fp12>(base, b), k);
+    Fp12 acc = Fp12::one();
+    for (int bit = 0; bit < 8; bit++)
+      if ((d >> bit) & 1) acc = mul(acc, at<Fp12>(work, b * 256 + 8 * w + bit));
+    at<Fp12>(table, t) = acc;
   };
-  return run(on_gpu, stream, n_bases * 8192, op, true, "gt_fb_table");
+  return run(on_gpu, stream, n_bases * 8192, p2, true, "gt_fb_table");
 }
 
 int dx_gt_fb_pow(int on_gpu, void *stream, const uint32_t *tables, const int32_t *tab_idx, const uint32_t *scalars,

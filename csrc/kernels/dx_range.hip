@@ -30,6 +30,23 @@ int dx_rp_prove_a(int on_gpu, void *stream, const uint32_t *negsB_aff, const uin
   return run(on_gpu, stream, n_items, op, true, "rp_prove_a");
 }
 
+// Table-driven prover (no pairing per item): a[it] = g_phi^{e[it]} * gT^{t[p*L+j]}
+// with g_phi = e(B, A_phi) comb-tabled per distinct signature point
+// (gphi_tables[tab_idx[it]]) and e = -s_j v_ij computed on the device.
+int dx_rp_prove_a_tab(int on_gpu, void *stream, const uint32_t *gphi_tables, const int32_t *tab_idx,
+                      const uint32_t *e_sc, const uint32_t *t_sc, const uint32_t *gt_table, uint32_t *a_out,
+                      int64_t n_items, int S, int L) {
+  auto op = [=] __host__ __device__(int64_t it) {
+    int64_t j = it % L;
+    int64_t p = it / ((int64_t)S * L);
+    const Fp12 *T = reinterpret_cast<const Fp12 *>(gphi_tables) + (int64_t)tab_idx[it] * 8192;
+    Fp12 f = gt_fixed_pow(T, e_sc + 8 * it);
+    Fp12 g = gt_fixed_pow(reinterpret_cast<const Fp12 *>(gt_table), t_sc + 8 * (p * L + j));
+    at<Fp12>(a_out, it) = mul(f, g);
+  };
+  return run(on_gpu, stream, n_items, op, true, "rp_prove_a_tab");
+}
+
 // f[it] = ML(rho (ZB[p*L+j] - Y[p*S+i]), V[it]),  g[it] = a[it]^rho
 // (the final exponentiation applies to the Miller product only: a_ij is already in GT)
 int dx_rp_verify_items(int on_gpu, void *stream, const uint32_t *ZB_jac, const uint32_t *Y_jac, const uint32_t *rho,

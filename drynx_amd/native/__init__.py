@@ -51,7 +51,7 @@ _SIGS = {
     "dx_fp_to_mont": [_I, _P, _P, _P, _L],
     "dx_fp_from_mont": [_I, _P, _P, _P, _L],
     "dx_fr_arith": [_I, _P, _I, _P, _P, _P, _L, _I],
-    "dx_g1_fb_table": [_I, _P, _P, _P],
+    "dx_g1_fb_table": [_I, _P, _P, _P, _P, _L],
     "dx_g1_fb_mul": [_I, _P, _P, _P, _P, _L],
     "dx_g1_fb_mul_i64": [_I, _P, _P, _P, _P, _L],
     "dx_g1_mul": [_I, _P, _P, _P, _P, _L, _I, _I],
@@ -64,7 +64,7 @@ _SIGS = {
     "dx_elgamal_encrypt": [_I, _P, _P, _P, _P, _P, _P, _P, _L],
     "dx_bsgs_build": [_I, _P, _P, _L, _P, _P, _L],
     "dx_bsgs_solve": [_I, _P, _P, _P, _P, _P, _L, _L, _L, _L, _P, _P, _L],
-    "dx_g2_fb_table": [_I, _P, _P, _P],
+    "dx_g2_fb_table": [_I, _P, _P, _P, _P, _L],
     "dx_g2_fb_mul": [_I, _P, _P, _P, _P, _P, _L],
     "dx_g2_mul": [_I, _P, _P, _P, _P, _L, _I],
     "dx_g2_on_curve": [_I, _P, _P, _P, _L],
@@ -74,12 +74,13 @@ _SIGS = {
     "dx_gt_mul": [_I, _P, _P, _P, _P, _L],
     "dx_gt_pow": [_I, _P, _P, _P, _P, _L, _I],
     "dx_gt_eq": [_I, _P, _P, _P, _P, _L],
-    "dx_gt_fb_table": [_I, _P, _P, _P, _L],
+    "dx_gt_fb_table": [_I, _P, _P, _P, _P, _L],
     "dx_gt_fb_pow": [_I, _P, _P, _P, _P, _P, _L],
     "dx_gt_prod_chunks": [_I, _P, _P, _P, _L, _L, _L],
     "dx_version": [],
     "dx_lr_moments": [_P, _P, _P, _L, _I, _P, _I],
     "dx_rp_prove_a": [_I, _P, _P, _P, _P, _P, _P, _L, _I, _I],
+    "dx_rp_prove_a_tab": [_I, _P, _P, _P, _P, _P, _P, _P, _L, _I, _I],
     "dx_rp_verify_items": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _I],
 }
 
@@ -167,10 +168,13 @@ def fr_arith(op: int, a: torch.Tensor, b: torch.Tensor | None = None) -> torch.T
 
 # ----------------------------------------------------------------------------- G1
 def g1_fb_table(base_aff: torch.Tensor) -> torch.Tensor:
-    assert base_aff.numel() == 16
-    table = torch.empty((32 * 256, 16), dtype=torch.int32, device=base_aff.device)
-    g, s = _ctx(base_aff)
-    _call("dx_g1_fb_table", g, s, _ptr(base_aff.contiguous()), _ptr(table))
+    """Comb table(s) [n_bases*8192, 16] for one or more affine G1 bases."""
+    bases = base_aff.contiguous().view(-1, 16)
+    nb = bases.shape[0]
+    table = torch.empty((nb * 8192, 16), dtype=torch.int32, device=base_aff.device)
+    work = torch.empty((nb * 256, 24), dtype=torch.int32, device=base_aff.device)
+    g, s = _ctx(bases)
+    _call("dx_g1_fb_table", g, s, _ptr(bases), _ptr(work), _ptr(table), nb)
     return table
 
 
@@ -300,10 +304,13 @@ def bsgs_solve(targets_jac, giant_aff, keys, vals, m_baby: int, n_giant: int, of
 
 # ----------------------------------------------------------------------------- G2
 def g2_fb_table(base_aff: torch.Tensor) -> torch.Tensor:
-    assert base_aff.numel() == 32
-    table = torch.empty((32 * 256, 32), dtype=torch.int32, device=base_aff.device)
-    g, s = _ctx(base_aff)
-    _call("dx_g2_fb_table", g, s, _ptr(base_aff.contiguous()), _ptr(table))
+    """Comb table(s) [n_bases*8192, 32] for one or more affine G2 bases."""
+    bases = base_aff.contiguous().view(-1, 32)
+    nb = bases.shape[0]
+    table = torch.empty((nb * 8192, 32), dtype=torch.int32, device=base_aff.device)
+    work = torch.empty((nb * 256, 48), dtype=torch.int32, device=base_aff.device)
+    g, s = _ctx(bases)
+    _call("dx_g2_fb_table", g, s, _ptr(bases), _ptr(work), _ptr(table), nb)
     return table
 
 
@@ -388,8 +395,9 @@ def gt_eq(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
 def gt_fb_table(bases: torch.Tensor) -> torch.Tensor:
     nb = _rows(bases, 96)
     table = torch.empty((nb * 8192, 96), dtype=torch.int32, device=bases.device)
+    work = torch.empty((nb * 256, 96), dtype=torch.int32, device=bases.device)
     g, s = _ctx(bases)
-    _call("dx_gt_fb_table", g, s, _ptr(bases.contiguous()), _ptr(table), nb)
+    _call("dx_gt_fb_table", g, s, _ptr(bases.contiguous()), _ptr(work), _ptr(table), nb)
     return table
 
 
@@ -438,6 +446,15 @@ def rp_prove_a(negsB_aff, V_aff, t_sc, gt_table, S: int, L: int) -> torch.Tensor
     out = torch.empty((n, 96), dtype=torch.int32, device=V_aff.device)
     g, s = _ctx(negsB_aff, V_aff, t_sc, gt_table)
     _call("dx_rp_prove_a", g, s, _ptr(negsB_aff), _ptr(V_aff), _ptr(t_sc), _ptr(gt_table), _ptr(out), n, S, L)
+    return out
+
+
+def rp_prove_a_tab(gphi_tables, tab_idx, e_sc, t_sc, gt_table, S: int, L: int) -> torch.Tensor:
+    n = _rows(e_sc, 8)
+    out = torch.empty((n, 96), dtype=torch.int32, device=e_sc.device)
+    g, s = _ctx(gphi_tables, tab_idx, e_sc, t_sc, gt_table)
+    _call("dx_rp_prove_a_tab", g, s, _ptr(gphi_tables), _ptr(tab_idx), _ptr(e_sc), _ptr(t_sc), _ptr(gt_table),
+          _ptr(out), n, S, L)
     return out
 
 

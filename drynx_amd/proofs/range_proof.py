@@ -91,6 +91,43 @@ class SigMaterial:
             for i in range(self.S):
                 acc = O.g1_add(acc, ys[i * self.n_cols + c])
             self.Ysum_bytes.append(O.g1_to_bytes(acc))
+        # prover tables, keyed by the distinct signature point (deduplicated by value)
+        flat_u8 = A_bytes.reshape(-1, G2_LEN)
+        keys = [flat_u8[i].tobytes() for i in range(flat_u8.shape[0])]
+        first = {}
+        canon = []
+        for i, k in enumerate(keys):
+            canon.append(first.setdefault(k, i))
+        self.canon = torch.tensor(canon, dtype=torch.long)  # A index -> first index with the same point
+        self._ptab = {}
+
+    def prover_tables(self, a_idx: torch.Tensor, device):
+        """Comb tables (G2 for V = v*A, GT for e(B, A)) of the distinct signature
+        points used by a proof batch, cached for the lifetime of the signature
+        set.  Returns (g2_tables, gt_tables, slot[a_idx-position]) or None when
+        the distinct points exceed the memory budget (1 MiB + 3 MiB each; budget
+        ``DRYNX_PROVER_TABLE_MB``, default 8 GiB on a GPU / 96 MiB on the host)."""
+        dev = torch.device(device)
+        canon = self.canon.to(a_idx.device).index_select(0, a_idx)
+        uniq, inv = torch.unique(canon, return_inverse=True)
+        key = str(dev)
+        cache = self._ptab.setdefault(key, {"idx": [], "g2": None, "gt": None, "pos": {}})
+        missing = [int(u) for u in uniq.tolist() if int(u) not in cache["pos"]]
+        budget = int(os.environ.get("DRYNX_PROVER_TABLE_MB", 8192 if dev.type == "cuda" else 96)) << 20
+        if (len(cache["pos"]) + len(missing)) * (4 << 20) > budget:
+            return None
+        if missing:
+            pts = self.A.to(dev).index_select(0, torch.tensor(missing, dtype=torch.long, device=dev)).contiguous()
+            g2 = nt.g2_fb_table(pts)
+            gphi = nt.pairing(bn.g1_generator_aff(dev).expand(len(missing), 16).contiguous(), pts)
+            gt = nt.gt_fb_table(gphi)
+            cache["g2"] = g2 if cache["g2"] is None else torch.cat([cache["g2"], g2])
+            cache["gt"] = gt if cache["gt"] is None else torch.cat([cache["gt"], gt])
+            for m in missing:
+                cache["pos"][m] = len(cache["idx"])
+                cache["idx"].append(m)
+        slot_of_uniq = torch.tensor([cache["pos"][int(u)] for u in uniq.tolist()], dtype=torch.long, device=dev)
+        return cache["g2"], cache["gt"], slot_of_uniq.index_select(0, inv.to(dev))
 
 
 _gt_cache: dict = {}
@@ -293,12 +330,24 @@ def _prove_group(u, l, vals, offs, cols, r, cv, sigmat, P_point, device) -> Rang
     phi_t = torch.from_numpy(phi).to(device)
     a_index = ((i_idx.view(1, S, 1) * sigmat.n_cols + cols_t.view(n, 1, 1)) * max(1, sigmat.umax)
                + phi_t.view(n, 1, l)).reshape(-1)
-    A_sel = sigmat.A.to(device).index_select(0, a_index).contiguous()
-    V = nt.g2_mul(A_sel, v)
-    # a_ij = FE(ML(-s_j B, V_ij)) * gT^{t_j}
-    negsB = nt.g1_to_affine(nt.g1_fb_mul(tabB, nt.fr_arith(nt.FR_NEG, s)))
     _, gt_tab = gt_generator_table(device)
-    A = nt.rp_prove_a(negsB, V, t, gt_tab, S, l)
+    uniq, inv = torch.unique(a_index, return_inverse=True)
+    tabs = sigmat.prover_tables(uniq, device)
+    if tabs is not None:
+        # table-driven prover: V = v * A_phi (G2 comb), a = e(B,A_phi)^{-s v} * gT^t (GT combs) —
+        # no pairing and no final exponentiation per (value, server, digit)
+        g2_tabs, gphi_tabs, slot = tabs
+        tidx = slot.index_select(0, inv).to(torch.int32).contiguous()
+        V = nt.g2_fb_mul(g2_tabs, v, tidx)
+        negs_rep = nt.fr_arith(nt.FR_NEG, s).view(n, 1, l, 8).expand(n, S, l, 8).reshape(-1, 8).contiguous()
+        e = nt.fr_arith(nt.FR_MUL, negs_rep, v)
+        A = nt.rp_prove_a_tab(gphi_tabs, tidx, e, t, gt_tab, S, l)
+    else:
+        A_sel = sigmat.A.to(device).index_select(0, a_index).contiguous()
+        V = nt.g2_mul(A_sel, v)
+        # a_ij = FE(ML(-s_j B, V_ij)) * gT^{t_j}
+        negsB = nt.g1_to_affine(nt.g1_fb_mul(tabB, nt.fr_arith(nt.FR_NEG, s)))
+        A = nt.rp_prove_a(negsB, V, t, gt_tab, S, l)
     rpl.challenge, rpl.zr, rpl.D, rpl.zphi, rpl.zv, rpl.V, rpl.A = c, zr, D, zphi, zv, V, A
     return rpl
 
