@@ -118,7 +118,7 @@ def test_survey_end_to_end_gpu(gpu_device, tmp_path):
 
     cl, node = local_cluster(3, 4, 2, device=gpu_device, workdir=str(tmp_path))
     client = DrynxClient(node, device=gpu_device)
-    sq = make_survey(client, cl, "variance", query_min=0, query_max=50, rows=100, proofs=1, ranges=[16, 4],
+    sq = make_survey(client, cl, "variance", query_min=0, query_max=50, rows=100, proofs=1, ranges=[16, 5],
                      sig_device=gpu_device)
     _, vals, res = client.send_survey_query(sq)
     tot = [sum(v[0][i] for v in res.clear_dp.values()) for i in range(3)]
