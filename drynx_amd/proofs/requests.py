@@ -44,6 +44,7 @@ class ProofRequest:
     data: bytes
     signature: bytes
     obj: Any = field(default=None, repr=False, compare=False)  # decoded proof (in-process fast path)
+    data_digest: bytes = b""  # set for header-only copies (sharded verification: payload not shipped)
 
     def base_key(self) -> str:
         return f"{self.survey_id}/{self.kind}/{self.sender_id}/{self.differ_info}"
@@ -52,15 +53,28 @@ class ProofRequest:
         return f"{self.base_key()}/{vn_addr}"
 
     def digest(self) -> bytes:
-        return hashlib.sha256(self.data).digest()
+        if self.data_digest:
+            return self.data_digest
+        self.data_digest = hashlib.sha256(self.data).digest()
+        return self.data_digest
+
+    @property
+    def header_only(self) -> bool:
+        return not self.data and bool(self.data_digest)
+
+    def header(self) -> "ProofRequest":
+        return ProofRequest(self.kind, self.survey_id, self.sender_id, self.differ_info, b"", self.signature,
+                            None, self.digest())
 
     def to_wire(self) -> dict:
         return {"kind": self.kind, "survey_id": self.survey_id, "sender_id": self.sender_id,
-                "differ_info": self.differ_info, "data": self.data, "signature": self.signature}
+                "differ_info": self.differ_info, "data": self.data, "signature": self.signature,
+                "digest": self.data_digest if self.header_only else b""}
 
     @staticmethod
     def from_wire(d: dict) -> "ProofRequest":
-        return ProofRequest(d["kind"], d["survey_id"], d["sender_id"], d["differ_info"], d["data"], d["signature"])
+        return ProofRequest(d["kind"], d["survey_id"], d["sender_id"], d["differ_info"], d["data"], d["signature"],
+                            None, d.get("digest", b""))
 
 
 def range_bundle_to_bytes(rpls) -> bytes:
@@ -94,11 +108,19 @@ def verify_signature(req: ProofRequest, public) -> bool:
     return sigma.schnorr_verify(public, req.digest(), req.signature)
 
 
-def should_verify(sq, req: ProofRequest, vn_index: int, n_vns: int) -> bool:
+def assigned_vns(sq, req: ProofRequest, n_vns: int):
+    """Sharded mode: the VN indices that verify this request (None = every VN samples)."""
     shard = int(getattr(sq, "VerificationSharding", 0) or 0)
-    if shard > 0 and n_vns > 0:
-        h = int.from_bytes(hashlib.sha256(req.base_key().encode()).digest()[:8], "little")
-        return (vn_index - h) % n_vns < shard
+    if shard <= 0 or n_vns <= 0:
+        return None
+    h = int.from_bytes(hashlib.sha256(req.base_key().encode()).digest()[:8], "little")
+    return {(h + k) % n_vns for k in range(min(shard, n_vns))}
+
+
+def should_verify(sq, req: ProofRequest, vn_index: int, n_vns: int) -> bool:
+    a = assigned_vns(sq, req, n_vns)
+    if a is not None:
+        return vn_index in a
     return random.random() <= sq.Threshold
 
 

@@ -36,11 +36,19 @@ def expected_counts(sq) -> dict:
 
 def fan_out(ctx, sq, local_requests: list) -> list:
     """All requests, on every rank that hosts a VN (others get nothing)."""
-    vn_ranks = sorted({ctx.cluster.by_id(si.id).rank for si in sq.Query.RosterVNs.list})
+    vns = [ctx.cluster.by_id(si.id) for si in sq.Query.RosterVNs.list]
+    vn_ranks = sorted({v.rank for v in vns})
     if ctx.comm.world == 1:
         return list(local_requests)
-    payload = obj_to_bytes([r.to_wire() for r in local_requests])
-    got = ctx.comm.exchange_bytes({d: payload for d in vn_ranks})
+    # sharded verification: ship the payload only to ranks hosting an assigned
+    # VN; the others get the signed header (signature + digest) and record 2
+    per_rank = {d: [] for d in vn_ranks}
+    for r in local_requests:
+        assigned = prq.assigned_vns(sq, r, len(vns))
+        full_ranks = vn_ranks if assigned is None else {vns[i].rank for i in assigned}
+        for d in vn_ranks:
+            per_rank[d].append(r.to_wire() if d in full_ranks else r.header().to_wire())
+    got = ctx.comm.exchange_bytes({d: obj_to_bytes(per_rank[d]) for d in vn_ranks})
     out = []
     for src in sorted(got):
         if src == ctx.rank:
