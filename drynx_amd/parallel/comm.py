@@ -80,6 +80,8 @@ class LocalComm(Comm):
     def __init__(self, device="cpu"):
         self.rank, self.world = 0, 1
         self.device = torch.device(device)
+        if self.device.type == "cuda" and self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
 
 
 class DistComm(Comm):
@@ -171,7 +173,10 @@ def make_comm(device=None) -> Comm:
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
         return DistComm(device)
     if device is None:
-        device = "cuda" if torch.cuda.is_available() else "cpu"
+        device = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0"))) if torch.cuda.is_available() else "cpu"
+    device = torch.device(device)
+    if device.type == "cuda" and device.index is None:
+        device = torch.device("cuda", torch.cuda.current_device())
     return LocalComm(device)
 
 
