@@ -206,9 +206,12 @@ class DecryptionTable:
         self.device = torch.device(device)
         self.bound = int(bound)
         span = 2 * self.bound + 1
-        if max_baby is None:
-            max_baby = (1 << 22) if self.device.type == "cuda" else (1 << 15)
-        self.m_baby = max(2, min(int(math.isqrt(span)) + 1, max_baby))
+        if self.device.type == "cuda":
+            # HBM is plentiful: a baby table of up to 2^24 entries (~400 MB hash
+            # table, built once and cached) leaves few serial giant steps per value
+            self.m_baby = max(2, min(span + 1, max_baby or (1 << 24)))
+        else:
+            self.m_baby = max(2, min(int(math.isqrt(span)) + 1, max_baby or (1 << 15)))
         self.n_giant = (span + self.m_baby - 1) // self.m_baby + 1
         cap = 1
         while cap < 2 * self.m_baby:
