@@ -214,6 +214,46 @@ class RangeProofList:
             rpl.A = bn.gt_from_bytes(take(GT_LEN * n * S * l), device)
         return rpl
 
+    # ------------------------------------------------------------- raw (HBM-native) format
+    def pack(self) -> torch.Tensor:
+        """One int32 device tensor with every field as raw Montgomery limbs —
+        the intra-cluster format (RCCL payload, VN store); ``to_bytes`` is the
+        kyber-layout export."""
+        dev = self.commit.device
+        n, l, S = len(self), self.l, self.S
+        meta = torch.tensor([0x52505231, n, self.u, l, S], dtype=torch.int32)
+        offs = torch.tensor(self.offset, dtype=torch.int64).view(torch.int32) if n else torch.empty(0, dtype=torch.int32)
+        cols = torch.tensor(self.cols, dtype=torch.int32)
+        parts = [meta.to(dev), offs.to(dev), cols.to(dev), self.commit.K.reshape(-1), self.commit.C.reshape(-1)]
+        if self.has_rp and n:
+            parts += [t.reshape(-1) for t in (self.challenge, self.zr, self.D, self.zphi, self.zv, self.V, self.A)]
+        return torch.cat(parts)
+
+    @staticmethod
+    def unpack(t: torch.Tensor) -> "RangeProofList":
+        meta = t[:5].cpu().tolist()
+        assert meta[0] == 0x52505231, "not a packed RangeProofList"
+        n, u, l, S = meta[1:]
+        o = 5
+        offs = t[o: o + 2 * n].cpu().clone().view(torch.int64).tolist()
+        o += 2 * n
+        cols = t[o: o + n].cpu().tolist()
+        o += n
+
+        def take(rows, width):
+            nonlocal o
+            v = t[o: o + rows * width].view(rows, width)
+            o += rows * width
+            return v
+
+        commit = CipherVector(take(n, 24), take(n, 24))
+        rpl = RangeProofList(u, l, S, offs, cols, commit)
+        if rpl.has_rp and n:
+            rpl.challenge, rpl.zr, rpl.D = take(n, 8), take(n, 8), take(n, 24)
+            rpl.zphi, rpl.zv = take(n * l, 8), take(n * S * l, 8)
+            rpl.V, rpl.A = take(n * S * l, 32), take(n * S * l, 96)
+        return rpl
+
     def to(self, device) -> "RangeProofList":
         mv = lambda t: None if t is None else t.to(device)  # noqa: E731
         return RangeProofList(self.u, self.l, self.S, list(self.offset), list(self.cols), self.commit.to(device),

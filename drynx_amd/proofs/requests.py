@@ -19,6 +19,9 @@ import random
 from dataclasses import dataclass, field
 from typing import Any
 
+import numpy as np
+import torch
+
 from ..utils import timers
 from ..utils.log import get_logger
 from . import aggregation_shuffle as ags
@@ -77,23 +80,42 @@ class ProofRequest:
                             None, d.get("digest", b""))
 
 
+def range_bundle_pack(rpls) -> torch.Tensor:
+    """All range-proof lists of one DP response as ONE int32 device tensor:
+    [count, len_0, ..., len_{k-1}, packed_0, ..., packed_{k-1}]."""
+    packed = [r.pack() for r in rpls]
+    dev = packed[0].device if packed else torch.device("cpu")
+    hdr = torch.tensor([len(packed)] + [p.numel() for p in packed], dtype=torch.int32, device=dev)
+    return torch.cat([hdr] + packed)
+
+
+def range_bundle_unpack(t: torch.Tensor) -> list:
+    k = int(t[0])
+    sizes = t[1: 1 + k].cpu().tolist()
+    o, out = 1 + k, []
+    for s in sizes:
+        out.append(rp.RangeProofList.unpack(t[o: o + s]))
+        o += s
+    return out
+
+
 def range_bundle_to_bytes(rpls) -> bytes:
+    """Marshalled range-proof request payload (raw limb format, see RangeProofList.pack)."""
+    return range_bundle_pack(rpls).cpu().numpy().tobytes()
+
+
+def range_bundle_from_bytes(b: bytes, device="cpu") -> list:
+    t = torch.from_numpy(np.frombuffer(b, dtype=np.int32).copy()).to(device)
+    return range_bundle_unpack(t)
+
+
+def range_bundle_export_kyber(rpls) -> bytes:
+    """kyber-layout (reference ToBytes field order/sizes) export of a bundle."""
     out = [len(rpls).to_bytes(8, "little")]
     for r in rpls:
         b = r.to_bytes()
         out += [len(b).to_bytes(8, "little"), b]
     return b"".join(out)
-
-
-def range_bundle_from_bytes(b: bytes, device="cpu") -> list:
-    n = int.from_bytes(b[:8], "little")
-    o, out = 8, []
-    for _ in range(n):
-        ln = int.from_bytes(b[o: o + 8], "little")
-        o += 8
-        out.append(rp.RangeProofList.from_bytes(b[o: o + ln], device))
-        o += ln
-    return out
 
 
 def new_proof_request(kind: str, proof, survey_id: str, sender_id: str, differ_info: str, secret: int) -> ProofRequest:

@@ -18,6 +18,8 @@ from __future__ import annotations
 
 import json
 
+import torch
+
 from ..ledger import skipchain as skc
 from ..parallel.comm import bytes_to_obj, obj_to_bytes
 from ..proofs import requests as prq
@@ -42,19 +44,45 @@ def fan_out(ctx, sq, local_requests: list) -> list:
         return list(local_requests)
     # sharded verification: ship the payload only to ranks hosting an assigned
     # VN; the others get the signed header (signature + digest) and record 2
+    # range-proof payloads (tens of MB per DP) go as raw limb tensors over RCCL;
+    # envelopes and small proofs as pickled control messages
     per_rank = {d: [] for d in vn_ranks}
-    for r in local_requests:
+    per_rank_t = {d: [] for d in vn_ranks}
+    packed = {}
+    for idx, r in enumerate(local_requests):
         assigned = prq.assigned_vns(sq, r, len(vns))
         full_ranks = vn_ranks if assigned is None else {vns[i].rank for i in assigned}
         for d in vn_ranks:
-            per_rank[d].append(r.to_wire() if d in full_ranks else r.header().to_wire())
+            if d not in full_ranks:
+                per_rank[d].append(r.header().to_wire())
+            elif r.kind == "range" and r.obj is not None and d != ctx.rank:
+                if idx not in packed:
+                    packed[idx] = prq.range_bundle_pack(r.obj).to(ctx.device)
+                w = r.header().to_wire()
+                w["digest"], w["tensor"] = b"", packed[idx].numel()
+                per_rank[d].append(w)
+                per_rank_t[d].append(packed[idx])
+            else:
+                per_rank[d].append(r.to_wire())
     got = ctx.comm.exchange_bytes({d: obj_to_bytes(per_rank[d]) for d in vn_ranks})
+    tens = {d: torch.cat(per_rank_t[d]) for d in vn_ranks if per_rank_t[d]}
+    got_t = ctx.comm.exchange(tens)
     out = []
     for src in sorted(got):
         if src == ctx.rank:
             out += list(local_requests)  # keep decoded objects for locally produced proofs
-        else:
-            out += [prq.ProofRequest.from_wire(d) for d in bytes_to_obj(got[src])]
+            continue
+        off = 0
+        for w in bytes_to_obj(got[src]):
+            req = prq.ProofRequest.from_wire(w)
+            n = w.get("tensor")
+            if n:
+                t = got_t[src][off: off + n]
+                off += n
+                req.obj = prq.range_bundle_unpack(t)
+                req.data = t.cpu().numpy().tobytes()  # signed bytes: the VN checks the digest itself
+                req.data_digest = b""
+            out.append(req)
     return out
 
 
