@@ -79,6 +79,7 @@ _SIGS = {
     "dx_gt_prod_chunks": [_I, _P, _P, _P, _L, _L, _L],
     "dx_version": [],
     "dx_lr_moments": [_P, _P, _P, _L, _I, _P, _I],
+    "dx_g1_mul_fast": [_P, _P, _P, _P, _L, _I, _I],
     "dx_rp_prove_a": [_I, _P, _P, _P, _P, _P, _P, _L, _I, _I],
     "dx_rp_prove_a_tab": [_I, _P, _P, _P, _P, _P, _P, _P, _L, _I, _I],
     "dx_rp_verify_items": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _I],
@@ -202,6 +203,12 @@ def g1_mul(pts_jac: torch.Tensor, scalars: torch.Tensor) -> torch.Tensor:
     assert np_ in (1, n) and nk in (1, n)
     out = torch.empty((n, 24), dtype=torch.int32, device=scalars.device)
     g, s = _ctx(pts_jac, scalars)
+    if g:  # gfx950: register-resident kernel with the window table in LDS (dx_g1_varmul.hip)
+        rc = _load().dx_g1_mul_fast(s, _ptr(pts_jac), _ptr(scalars), _ptr(out), n, int(np_ == 1 and n > 1),
+                                    int(nk == 1 and n > 1))
+        if rc:
+            raise RuntimeError(f"dx_g1_mul_fast failed rc={rc}")
+        return out
     _call("dx_g1_mul", g, s, _ptr(pts_jac), _ptr(scalars), _ptr(out), n, int(np_ == 1 and n > 1), int(nk == 1 and n > 1))
     return out
 
