@@ -212,6 +212,61 @@ def verify_content(req: ProofRequest, sq, device, cache: VerifierCache) -> bool:
     raise ValueError(req.kind)
 
 
+def _decode(req: ProofRequest, device):
+    if req.obj is not None:
+        return req.obj
+    if req.kind == "keyswitch":
+        return sigma.KeySwitchProof.from_bytes(req.data, device)
+    if req.kind == "obfuscation":
+        return sigma.ObfuscationProof.from_bytes(req.data, device)
+    raise ValueError(req.kind)
+
+
+def verify_requests(reqs: list, sq, vn_id: str, vn_index: int, n_vns: int, device, cache: VerifierCache) -> list:
+    """VerifyProof for a VN's whole inbox.  Signatures and sampling per request;
+    the content of the short per-CN proofs (key switch, obfuscation) is verified
+    in one batched launch per kind; range proofs are already one batch each."""
+    codes = [None] * len(reqs)
+    todo: dict = {}
+    for i, req in enumerate(reqs):
+        if not verify_signature(req, sq.IDtoPublic.get(req.sender_id)):
+            codes[i] = PROOF_FALSE_SIGN
+        elif not should_verify(sq, req, vn_index, n_vns):
+            codes[i] = PROOF_RECEIVED
+        else:
+            todo.setdefault(req.kind, []).append(i)
+    for kind, idxs in todo.items():
+        with timers.timed(f"{vn_id}_{TIMER[kind]}"):
+            if kind in ("keyswitch", "obfuscation") and len(idxs) > 1:
+                objs, valid = [], []
+                for i in idxs:
+                    try:
+                        o = _decode(reqs[i], device)
+                        if kind == "keyswitch" and (o.X != sq.IDtoPublic.get(reqs[i].sender_id) or o.Q != sq.ClientPubKey):
+                            codes[i] = PROOF_FALSE
+                            continue
+                        objs.append(o)
+                        valid.append(i)
+                    except Exception as e:
+                        log.warning(f"{vn_id}: {kind} proof from {reqs[i].sender_id} rejected: {e}")
+                        codes[i] = PROOF_FALSE
+                if kind == "keyswitch":
+                    res = sigma.key_switch_batch_verification(objs, sq.KeySwitchingProofThreshold)
+                else:
+                    res = sigma.obfuscation_batch_verification(objs, sq.ObfuscationProofThreshold)
+                for i, r in zip(valid, res):
+                    codes[i] = PROOF_TRUE if r else PROOF_FALSE
+            else:
+                for i in idxs:
+                    try:
+                        ok = verify_content(reqs[i], sq, device, cache)
+                    except Exception as e:
+                        log.warning(f"{vn_id}: {kind} proof from {reqs[i].sender_id} rejected: {e}")
+                        ok = False
+                    codes[i] = PROOF_TRUE if ok else PROOF_FALSE
+    return codes
+
+
 def verify_proof(req: ProofRequest, sq, vn_id: str, vn_index: int, n_vns: int, device, cache: VerifierCache) -> int:
     """<Kind>ProofRequest.VerifyProof -> bitmap code."""
     with timers.timed(f"{vn_id}_{TIMER[req.kind]}"):

@@ -38,16 +38,30 @@ def _aff_bytes(jac: torch.Tensor) -> bytes:
 
 
 def fs_challenge(context: str, *parts) -> int:
+    """SHA-256 Fiat–Shamir challenge over the context and the affine encodings
+    of every point: all point tensors are normalised in ONE batched launch
+    (a transcript is 4-7 vectors of thousands of points)."""
     h = hashlib.sha256()
     h.update(context.encode())
+    jacs, layout = [], []
     for p in parts:
         if isinstance(p, torch.Tensor):
-            h.update(_aff_bytes(p))
+            jacs.append(p.contiguous().view(-1, 24))
+            layout.append(("pts", jacs[-1].shape[0]))
         elif isinstance(p, CipherVector):
-            h.update(_aff_bytes(p.K))
-            h.update(_aff_bytes(p.C))
+            for t in (p.K, p.C):
+                jacs.append(t.contiguous().view(-1, 24))
+                layout.append(("pts", jacs[-1].shape[0]))
         else:
-            h.update(p if isinstance(p, (bytes, bytearray)) else str(p).encode())
+            layout.append(("raw", p if isinstance(p, (bytes, bytearray)) else str(p).encode()))
+    allb = _aff_bytes(torch.cat(jacs)) if jacs else b""
+    o = 0
+    for kind, v in layout:
+        if kind == "pts":
+            h.update(allb[o: o + 64 * v])
+            o += 64 * v
+        else:
+            h.update(v)
     return int.from_bytes(h.digest(), "big") % O.R
 
 
@@ -195,6 +209,47 @@ def key_switch_share(x: int, K: torch.Tensor, Q_point, v: torch.Tensor | None = 
     return share, v
 
 
+def key_switch_shares_batch(secrets: list, publics: list, K: torch.Tensor, Q_point, with_proofs: bool):
+    """Key-switching shares (and proofs) of several co-located CNs over the same
+    K vector in a handful of launches sized (#CNs x n) instead of per CN."""
+    from ..crypto.elgamal import pk_table
+
+    dev = K.device
+    n, c = K.shape[0], len(secrets)
+    tabB = bn.base_table(dev)
+    tabQ = pk_table(Q_point, dev).tabP
+    Kt = K.repeat(c, 1).contiguous()
+    x_rep = torch.cat([_sc([x], dev).expand(n, 8) for x in secrets]).contiguous()
+    v = bn.random_scalars(c * n, dev)
+    scal = [x_rep]
+    if with_proofs:
+        bs = [O.random_scalar() for _ in secrets]
+        scal.append(torch.cat([_sc([b], dev).expand(n, 8) for b in bs]).contiguous())
+    prods = nt.g1_mul(torch.cat([Kt] * len(scal)).contiguous(), torch.cat(scal).contiguous())
+    xK = prods[: c * n].contiguous()
+    vB = nt.g1_fb_mul(tabB, v)
+    vQ = nt.g1_fb_mul(tabQ, v)
+    shares_all = CipherVector(vB, nt.g1_add(vQ, xK, subtract=True))
+    out = []
+    if with_proofs:
+        a = bn.random_scalars(c * n, dev)
+        T1 = nt.g1_fb_mul(tabB, a)
+        T2 = nt.g1_add(nt.g1_fb_mul(tabQ, a), prods[c * n:].contiguous(), subtract=True)
+    for j in range(c):
+        sl = slice(j * n, (j + 1) * n)
+        share = shares_all[sl]
+        pr = None
+        if with_proofs:
+            T3 = O.g1_to_bytes(O.g1_mul(bs[j], O.G1_GEN))
+            t1, t2 = T1[sl].contiguous(), T2[sl].contiguous()
+            ch = fs_challenge("proofTest/keyswitch", O.g1_to_bytes(publics[j]), O.g1_to_bytes(Q_point), K, share,
+                              t1, t2, T3)
+            za = nt.fr_arith(nt.FR_ADD, a[sl].contiguous(), nt.fr_arith(nt.FR_MUL, v[sl].contiguous(), _sc([ch], dev)))
+            pr = KeySwitchProof(publics[j], Q_point, K, share, t1, t2, T3, ch, za, (bs[j] + ch * secrets[j]) % O.R)
+        out.append((share, pr))
+    return out
+
+
 def key_switch_list_proof_creation(x: int, X, Q_point, K: torch.Tensor, share: CipherVector,
                                    v: torch.Tensor) -> KeySwitchProof:
     from ..crypto.elgamal import pk_table
@@ -212,6 +267,83 @@ def key_switch_list_proof_creation(x: int, X, Q_point, K: torch.Tensor, share: C
     za = nt.fr_arith(nt.FR_ADD, a, nt.fr_arith(nt.FR_MUL, v, _sc([c], dev)))
     zb = (b + c * x) % O.R
     return KeySwitchProof(X, Q_point, K, share, T1, T2, T3, c, za, zb)
+
+
+def key_switch_batch_verification(proofs: list, threshold: float = 1.0) -> list:
+    """Verify several CNs' key-switch proofs (same querier key) with ONE
+    variable-base launch for all of them (the vectors are short, so one launch
+    per proof would be latency-bound)."""
+    from ..crypto.elgamal import pk_table
+
+    if not proofs:
+        return []
+    ok = []
+    live = []
+    for pr in proofs:
+        n = pr.K.shape[0]
+        k = _first(n, threshold)
+        c = fs_challenge("proofTest/keyswitch", O.g1_to_bytes(pr.X), O.g1_to_bytes(pr.Q), pr.K, pr.share, pr.T1,
+                         pr.T2, pr.T3)
+        good = c == pr.c and O.g1_mul(pr.zb, O.G1_GEN) == O.g1_add(O.g1_from_bytes(pr.T3), O.g1_mul(c, pr.X))
+        ok.append(good)
+        if good and k > 0:
+            live.append((len(ok) - 1, pr, k))
+    if not live:
+        return ok
+    dev = live[0][1].K.device
+    tabB = bn.base_table(dev)
+    tabQ = pk_table(live[0][1].Q, dev).tabP
+    za = torch.cat([pr.za[:k] for _, pr, k in live]).contiguous()
+    c_rep = torch.cat([_sc([pr.c], dev).expand(k, 8) for _, pr, k in live])
+    zb_rep = torch.cat([_sc([pr.zb], dev).expand(k, 8) for _, pr, k in live])
+    shK = torch.cat([pr.share.K[:k] for _, pr, k in live])
+    shC = torch.cat([pr.share.C[:k] for _, pr, k in live])
+    Ks = torch.cat([pr.K[:k] for _, pr, k in live])
+    T1 = torch.cat([pr.T1[:k] for _, pr, k in live]).contiguous()
+    T2 = torch.cat([pr.T2[:k] for _, pr, k in live]).contiguous()
+    m = shK.shape[0]
+    prods = nt.g1_mul(torch.cat([shK, Ks, shC]).contiguous(), torch.cat([c_rep, zb_rep, c_rep]).contiguous())
+    fb = nt.g1_fb_mul(tabB, za)               # za B
+    fq = nt.g1_fb_mul(tabQ, za)               # za Q
+    ok1 = nt.g1_eq(fb, nt.g1_add(T1, prods[:m].contiguous()))
+    ok2 = nt.g1_eq(nt.g1_add(fq, prods[m:2 * m].contiguous(), subtract=True), nt.g1_add(T2, prods[2 * m:].contiguous()))
+    good = (ok1 & ok2).cpu()
+    o = 0
+    for idx, pr, k in live:
+        ok[idx] = bool(good[o: o + k].all())
+        o += k
+    return ok
+
+
+def obfuscation_batch_verification(proofs: list, threshold: float = 1.0) -> list:
+    """Several CNs' obfuscation proofs, one variable-base launch for all."""
+    ok, live = [], []
+    for pr in proofs:
+        k = _first(len(pr.C), threshold)
+        good = fs_challenge("proofTest/obfuscation", pr.C, pr.Co, pr.T) == pr.c
+        ok.append(good)
+        if good and k > 0:
+            live.append((len(ok) - 1, pr, k))
+    if not live:
+        return ok
+    dev = live[0][1].C.device
+    z = torch.cat([pr.z[:k] for _, pr, k in live])
+    c = torch.cat([_sc([pr.c], dev).expand(k, 8) for _, pr, k in live])
+    CK = torch.cat([pr.C.K[:k] for _, pr, k in live])
+    CC = torch.cat([pr.C.C[:k] for _, pr, k in live])
+    OK_ = torch.cat([pr.Co.K[:k] for _, pr, k in live])
+    OC = torch.cat([pr.Co.C[:k] for _, pr, k in live])
+    TK = torch.cat([pr.T.K[:k] for _, pr, k in live]).contiguous()
+    TC = torch.cat([pr.T.C[:k] for _, pr, k in live]).contiguous()
+    m = CK.shape[0]
+    prods = nt.g1_mul(torch.cat([CK, CC, OK_, OC]).contiguous(), torch.cat([z, z, c, c]).contiguous())
+    p = [prods[i * m:(i + 1) * m].contiguous() for i in range(4)]
+    good = (nt.g1_eq(p[0], nt.g1_add(TK, p[2])) & nt.g1_eq(p[1], nt.g1_add(TC, p[3]))).cpu()
+    o = 0
+    for idx, pr, k in live:
+        ok[idx] = bool(good[o: o + k].all())
+        o += k
+    return ok
 
 
 def key_switch_list_proof_verification(pr: KeySwitchProof, threshold: float = 1.0) -> bool:

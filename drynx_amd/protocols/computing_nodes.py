@@ -124,14 +124,17 @@ def key_switching(ctx, sq, agg, n_groups: int, n_out: int, noise, proofs: list):
         agg = agg.add(noise_rows)
     agg = ec.broadcast_cv(ctx.comm, agg, n_rows, root)
     Q = sq.ClientPubKey
-    local_K, local_C = [], []
-    for cn in ctx.cluster.local(ctx.rank, "cn"):
-        with timers.timed(f"{cn.id}_KeySwitchingPhase"):
-            share, v = sigma.key_switch_share(cn.keypair.secret, agg.K, Q)
-            local_K.append(share)
-            if sq.Query.Proofs:
-                pr = sigma.key_switch_list_proof_creation(cn.keypair.secret, cn.public, Q, agg.K, share, v)
-                proofs.append(prq.new_proof_request("keyswitch", pr, sq.SurveyID, cn.id, "", cn.keypair.secret))
+    local_K = []
+    cns = [cn for cn in ctx.cluster.local(ctx.rank, "cn") if cn.id in {s.id for s in sq.RosterServers.list}]
+    if cns:
+        # all co-located CNs in one batch of launches (short vectors are latency-bound)
+        with timers.timed("KeySwitchingPhase"):
+            res = sigma.key_switch_shares_batch([c.keypair.secret for c in cns], [c.public for c in cns], agg.K, Q,
+                                                bool(sq.Query.Proofs))
+            for cn, (share, pr) in zip(cns, res):
+                local_K.append(share)
+                if pr is not None:
+                    proofs.append(prq.new_proof_request("keyswitch", pr, sq.SurveyID, cn.id, "", cn.keypair.secret))
     total = ec.sum_to_root(ctx.comm, local_K, n_rows, root)
     if ctx.rank != root:
         return None

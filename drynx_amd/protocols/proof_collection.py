@@ -90,8 +90,8 @@ def verify_and_store(ctx, sq, vn, vn_index: int, n_vns: int, requests: list) -> 
     store = ctx.store(vn.id)
     bitmap = {}
     counts = {k: 0 for k in prq.VN_ORDER}
-    for req in requests:
-        code = prq.verify_proof(req, sq, vn.id, vn_index, n_vns, ctx.device, ctx.verifier_cache)
+    codes = prq.verify_requests(requests, sq, vn.id, vn_index, n_vns, ctx.device, ctx.verifier_cache)
+    for req, code in zip(requests, codes):
         key = req.key(vn.id)
         bitmap[key] = code
         counts[req.kind] += 1

@@ -82,3 +82,23 @@ def test_shuffle_proof():
 def test_noise_generation():
     v = ags.generate_noise_values_scale(100, 0.0, 2.0, 1.0, 1.0, 10)
     assert len(v) == 100 and max(abs(x) for x in v) <= 10 and v.count(0) > v.count(5)
+
+
+def test_batched_keyswitch_and_obfuscation_verification():
+    xs = [O.random_scalar() for _ in range(3)]
+    X = [O.g1_mul(x, O.G1_GEN) for x in xs]
+    P = eg.aggregate_keys(X)
+    cv, _ = eg.encrypt_ints(eg.pk_table(P), [4, -9, 16])
+    q = eg.KeyPair.generate()
+    res = sigma.key_switch_shares_batch(xs, X, cv.K, q.public, True)
+    prs = [pr for _, pr in res]
+    assert sigma.key_switch_batch_verification(prs) == [True, True, True]
+    tot = eg.CipherVector.sum([s for s, _ in res])
+    out = eg.CipherVector(tot.K, __import__("drynx_amd").native.g1_add(cv.C, tot.C))
+    assert eg.decrypt_ints(q.secret, out) == [4, -9, 16]
+    prs[1].za[0, 0] ^= 1  # break one element of one proof
+    assert sigma.key_switch_batch_verification(prs) == [True, False, True]
+    s = [bn.random_scalars(3) for _ in range(2)]
+    obf = [sigma.obfuscation_list_proof_creation(cv, cv.mul_scalars(si), si) for si in s]
+    obf.append(sigma.obfuscation_list_proof_creation(cv, cv.mul_scalars(s[0]), s[1]))
+    assert sigma.obfuscation_batch_verification(obf) == [True, True, False]
