@@ -65,3 +65,54 @@ int dx_rp_verify_items(int on_gpu, void *stream, const uint32_t *ZB_jac, const u
 }
 
 }  // extern "C"
+
+// GPU-only fused variant: every 64-lane workgroup computes 64 items and folds
+// both products (Miller values, a^rho) with an LDS tree, writing one Fp12 pair
+// per workgroup — the [n_items] intermediate never reaches HBM.
+namespace {
+constexpr int kVW = 64;
+__global__ void __launch_bounds__(kVW) rp_verify_fold_kernel(const uint32_t *ZB_jac, const uint32_t *Y_jac,
+                                                              const uint32_t *rho, const uint32_t *V_aff,
+                                                              const uint32_t *a, uint32_t *f_blk, uint32_t *g_blk,
+                                                              int64_t n_items, int S, int L) {
+  __shared__ Fp12 sf[kVW];
+  __shared__ Fp12 sg[kVW];
+  const int lane = threadIdx.x;
+  const int64_t it = (int64_t)blockIdx.x * kVW + lane;
+  Fp12 f = Fp12::one(), g = Fp12::one();
+  if (it < n_items) {
+    int64_t j = it % L;
+    int64_t pi = it / L;
+    int64_t p = pi / S;
+    G1J T = jadd(at<G1J>(ZB_jac, p * L + j), jneg(at<G1J>(Y_jac, pi)));
+    G1A P = to_affine(scalar_mul(T, rho + 8 * it));
+    f = miller_loop(P, at<G2A>(V_aff, it));
+    g = gt_pow(at<Fp12>(a, it), rho + 8 * it);
+  }
+  sf[lane] = f;
+  sg[lane] = g;
+  __syncthreads();
+  for (int s = kVW / 2; s > 0; s >>= 1) {
+    if (lane < s) {
+      sf[lane] = mul(sf[lane], sf[lane + s]);
+    } else if (lane < 2 * s) {
+      sg[lane - s] = mul(sg[lane - s], sg[lane]);
+    }
+    __syncthreads();
+  }
+  if (lane == 0) {
+    at<Fp12>(f_blk, blockIdx.x) = sf[0];
+    at<Fp12>(g_blk, blockIdx.x) = sg[0];
+  }
+}
+}  // namespace
+
+extern "C" int dx_rp_verify_fold(void *stream, const uint32_t *ZB_jac, const uint32_t *Y_jac, const uint32_t *rho,
+                                 const uint32_t *V_aff, const uint32_t *a, uint32_t *f_blk, uint32_t *g_blk,
+                                 int64_t n_items, int S, int L) {
+  if (n_items <= 0) return 0;
+  int64_t blocks = (n_items + kVW - 1) / kVW;
+  hipLaunchKernelGGL(rp_verify_fold_kernel, dim3((unsigned)blocks), dim3(kVW), 0, (hipStream_t)stream, ZB_jac, Y_jac,
+                     rho, V_aff, a, f_blk, g_blk, n_items, S, L);
+  return check_hip(hipGetLastError(), "rp_verify_fold");
+}

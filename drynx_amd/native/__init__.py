@@ -80,6 +80,7 @@ _SIGS = {
     "dx_version": [],
     "dx_lr_moments": [_P, _P, _P, _L, _I, _P, _I],
     "dx_g1_mul_fast": [_P, _P, _P, _P, _L, _I, _I],
+    "dx_rp_verify_fold": [_P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _I],
     "dx_rp_prove_a": [_I, _P, _P, _P, _P, _P, _P, _L, _I, _I],
     "dx_rp_prove_a_tab": [_I, _P, _P, _P, _P, _P, _P, _P, _L, _I, _I],
     "dx_rp_verify_items": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _I],
@@ -473,3 +474,22 @@ def rp_verify_items(ZB_jac, Y_jac, rho, V_aff, a, S: int, L: int):
     _call("dx_rp_verify_items", g, s, _ptr(ZB_jac), _ptr(Y_jac), _ptr(rho), _ptr(V_aff), _ptr(a), _ptr(f), _ptr(gg),
           n, S, L)
     return f, gg
+
+
+def rp_verify_products(ZB_jac, Y_jac, rho, V_aff, a, S: int, L: int):
+    """(prod_it ML_it, prod_it a_it^rho_it) as two [1, 96] tensors.  GPU: the
+    fused kernel folds each 64-item workgroup in LDS, then a short product tree
+    over the workgroup partials; host: per-item values + product tree."""
+    g, s = _ctx(ZB_jac, Y_jac, rho, V_aff, a)
+    if not g:
+        f, gg = rp_verify_items(ZB_jac, Y_jac, rho, V_aff, a, S, L)
+        return gt_prod(f.view(-1, 1, 96), chunk=4).view(1, 96), gt_prod(gg.view(-1, 1, 96), chunk=4).view(1, 96)
+    n = _rows(V_aff, 32)
+    nb = (n + 63) // 64
+    fb = torch.empty((nb, 96), dtype=torch.int32, device=V_aff.device)
+    gb = torch.empty((nb, 96), dtype=torch.int32, device=V_aff.device)
+    rc = _load().dx_rp_verify_fold(s, _ptr(ZB_jac), _ptr(Y_jac), _ptr(rho), _ptr(V_aff), _ptr(a), _ptr(fb), _ptr(gb),
+                                   n, S, L)
+    if rc:
+        raise RuntimeError(f"dx_rp_verify_fold failed rc={rc}")
+    return gt_prod(fb.view(-1, 1, 96), chunk=4).view(1, 96), gt_prod(gb.view(-1, 1, 96), chunk=4).view(1, 96)

@@ -438,10 +438,8 @@ def verify_range_proof_list(rpl: RangeProofList, sigmat: SigMaterial, P_point, t
     Ysel = sigmat.y_jac.to(device).index_select(0, y_idx).contiguous()
     Y = nt.g1_mul(Ysel, _rep(r.challenge, S))                         # [n*S]
     rho = _rand64(n * S * l, device)
-    f, g = nt.rp_verify_items(ZB, Y, rho, r.V, r.A, S, l)            # [n*S*l, 96] each
-    F = nt.gt_prod(f.view(-1, 1, 96))
-    G = nt.gt_prod(g.view(-1, 1, 96))
-    lhs_gt = nt.gt_mul(nt.final_exp(F.view(1, 96)), G.view(1, 96))
+    F, G = nt.rp_verify_products(ZB, Y, rho, r.V, r.A, S, l)         # Miller product, prod a^rho
+    lhs_gt = nt.gt_mul(nt.final_exp(F), G)
     e = _fr_sum_rows(nt.fr_arith(nt.FR_MUL, rho, r.zv), 1)           # sum rho Zv
     _, gt_tab = gt_generator_table(device)
     rhs_gt = nt.gt_fb_pow(gt_tab, e)
