@@ -271,6 +271,27 @@ def base2_table(device="cpu") -> torch.Tensor:
         return _tables[k]
 
 
+def g1_mul_point(k: int, P=None):
+    """k * P for one point on the native host path (P = None -> the base B,
+    fixed-base comb).  ~50 us instead of ~10 ms for the Python oracle; used
+    by Schnorr envelopes, proof transcripts and key generation."""
+    ks = scalars_tensor([k], "cpu")
+    if P is None or P == O.G1_GEN:
+        return g1_points_from_jac(nt.g1_fb_mul(base_table("cpu"), ks))[0]
+    if P is None:
+        return None
+    return g1_points_from_jac(nt.g1_mul(g1_jac_tensor([P], "cpu"), ks))[0]
+
+
+def g1_add_points(P, Q):
+    """P + Q for oracle-style affine points via the native host path."""
+    if P is None:
+        return Q
+    if Q is None:
+        return P
+    return g1_points_from_jac(nt.g1_add(g1_jac_tensor([P]), g1_jac_tensor([Q])))[0]
+
+
 def point_table(point_jac: torch.Tensor) -> torch.Tensor:
     """Comb table for an arbitrary G1 point (collective key P, querier key Q)."""
     return nt.g1_fb_table(nt.g1_to_affine(point_jac.reshape(1, 24).contiguous()))

@@ -33,11 +33,11 @@ class KeyPair:
     @staticmethod
     def generate() -> "KeyPair":
         x = O.random_scalar()
-        return KeyPair(x, O.g1_mul(x, O.G1_GEN))
+        return KeyPair(x, bn.g1_mul_point(x))
 
     @staticmethod
     def from_secret(x: int) -> "KeyPair":
-        return KeyPair(x % O.R, O.g1_mul(x, O.G1_GEN))
+        return KeyPair(x % O.R, bn.g1_mul_point(x % O.R))
 
     def public_jac(self, device="cpu") -> torch.Tensor:
         return bn.g1_jac_tensor([self.public], device)

@@ -48,7 +48,7 @@ G2_LEN, G1_LEN, GT_LEN, SC_LEN = 128, 64, 384, 32
 def init_range_proof_signature(u: int, secret: int | None = None, device="cpu") -> PublishSignatureBytes:
     """A CN's input-validation key for one output column: y = x*B, A_k = (x+k)^-1 * B2."""
     x = O.random_scalar() if secret is None else secret % O.R
-    y = O.g1_mul(x, O.G1_GEN)
+    y = bn.g1_mul_point(x)
     inv = [pow((x + k) % O.R, -1, O.R) for k in range(u)]
     A = nt.g2_fb_mul(bn.base2_table(device), bn.scalars_tensor(inv, device))
     return PublishSignatureBytes(O.g1_to_bytes(y), bn.g2_aff_to_bytes(A).tobytes())

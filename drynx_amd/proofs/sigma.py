@@ -76,8 +76,8 @@ def _first(n: int, threshold: float) -> int:
 # ----------------------------------------------------------------------------- Schnorr
 def schnorr_sign(secret: int, msg: bytes) -> bytes:
     k = O.random_scalar()
-    R = O.g1_mul(k, O.G1_GEN)
-    X = O.g1_mul(secret, O.G1_GEN)
+    R = bn.g1_mul_point(k)
+    X = bn.g1_mul_point(secret)
     e = int.from_bytes(hashlib.sha256(O.g1_to_bytes(R) + O.g1_to_bytes(X) + msg).digest(), "big") % O.R
     s = (k + e * secret) % O.R
     return O.g1_to_bytes(R) + O.scalar_to_bytes(s)
@@ -92,8 +92,8 @@ def schnorr_verify(public, msg: bytes, sig: bytes) -> bool:
         return False
     s = int.from_bytes(sig[64:], "big")
     e = int.from_bytes(hashlib.sha256(sig[:64] + O.g1_to_bytes(public) + msg).digest(), "big") % O.R
-    lhs = O.g1_mul(s, O.G1_GEN)
-    return lhs == O.g1_add(R, O.g1_mul(e, public))
+    lhs = bn.g1_mul_point(s)
+    return lhs == O.g1_add(R, bn.g1_mul_point(e, public))
 
 
 # ----------------------------------------------------------------------------- obfuscation (DLEQ)
@@ -240,7 +240,7 @@ def key_switch_shares_batch(secrets: list, publics: list, K: torch.Tensor, Q_poi
         share = shares_all[sl]
         pr = None
         if with_proofs:
-            T3 = O.g1_to_bytes(O.g1_mul(bs[j], O.G1_GEN))
+            T3 = O.g1_to_bytes(bn.g1_mul_point(bs[j]))
             t1, t2 = T1[sl].contiguous(), T2[sl].contiguous()
             ch = fs_challenge("proofTest/keyswitch", O.g1_to_bytes(publics[j]), O.g1_to_bytes(Q_point), K, share,
                               t1, t2, T3)
@@ -262,7 +262,7 @@ def key_switch_list_proof_creation(x: int, X, Q_point, K: torch.Tensor, share: C
     tabQ = pk_table(Q_point, dev).tabP
     T1 = nt.g1_fb_mul(tabB, a)
     T2 = nt.g1_add(nt.g1_fb_mul(tabQ, a), nt.g1_mul(K.contiguous(), _sc([b], dev)), subtract=True)
-    T3 = O.g1_to_bytes(O.g1_mul(b, O.G1_GEN))
+    T3 = O.g1_to_bytes(bn.g1_mul_point(b))
     c = fs_challenge("proofTest/keyswitch", O.g1_to_bytes(X), O.g1_to_bytes(Q_point), K, share, T1, T2, T3)
     za = nt.fr_arith(nt.FR_ADD, a, nt.fr_arith(nt.FR_MUL, v, _sc([c], dev)))
     zb = (b + c * x) % O.R
@@ -284,7 +284,7 @@ def key_switch_batch_verification(proofs: list, threshold: float = 1.0) -> list:
         k = _first(n, threshold)
         c = fs_challenge("proofTest/keyswitch", O.g1_to_bytes(pr.X), O.g1_to_bytes(pr.Q), pr.K, pr.share, pr.T1,
                          pr.T2, pr.T3)
-        good = c == pr.c and O.g1_mul(pr.zb, O.G1_GEN) == O.g1_add(O.g1_from_bytes(pr.T3), O.g1_mul(c, pr.X))
+        good = c == pr.c and bn.g1_mul_point(pr.zb) == O.g1_add(O.g1_from_bytes(pr.T3), bn.g1_mul_point(c, pr.X))
         ok.append(good)
         if good and k > 0:
             live.append((len(ok) - 1, pr, k))
@@ -359,7 +359,7 @@ def key_switch_list_proof_verification(pr: KeySwitchProof, threshold: float = 1.
         return False
     # zb B == T3 + c X
     T3 = O.g1_from_bytes(pr.T3)
-    if O.g1_mul(pr.zb, O.G1_GEN) != O.g1_add(T3, O.g1_mul(c, pr.X)):
+    if bn.g1_mul_point(pr.zb) != O.g1_add(T3, bn.g1_mul_point(c, pr.X)):
         return False
     dev = pr.K.device
     tabB = bn.base_table(dev)

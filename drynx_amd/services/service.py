@@ -94,6 +94,11 @@ class DrynxNode:
         t_exec = timers.start_timer("JustExecution")
         noise = cnp.dro_phase(self, sq, proofs)
         cn_sums, cn_inputs, dp_results = dcp.data_collection(self, sq)
+        # range proofs start right after encoding (the reference fires them
+        # asynchronously, data_collection_protocol.go:278-348): proving is queued
+        # on the GPU now, envelope marshalling + signing runs on a worker thread
+        # while the CN phases below proceed
+        range_future = self._range_proofs_async(sq, dp_results) if q.Proofs else None
         if dp_results:
             n_out = len(next(iter(dp_results.values()))["cv"]) // n_groups
         n_out = max(self.comm.all_gather_object(n_out if dp_results else 0)) or n_out
@@ -108,9 +113,8 @@ class DrynxNode:
             result = CipherVector.cat([result[g * n_out: g * n_out + per] for g in range(n_groups)])
             n_out = per
         timers.end_timer(t_exec)
-        # range proofs of the local DPs (generated off the query's critical path in the reference)
-        if q.Proofs:
-            self._range_proofs(sq, dp_results, proofs)
+        if range_future is not None:
+            proofs.extend(range_future.result())
         block = None
         if q.Proofs and q.RosterVNs is not None and len(q.RosterVNs.list):
             block = pcp.proof_collection(self, sq, proofs)
@@ -118,11 +122,14 @@ class DrynxNode:
         return SurveyResult(sq.SurveyID, result, n_groups, n_out, block, clear)
 
     def _range_proofs(self, sq, dp_results: dict, proofs: list):
-        q = sq.Query
+        """Synchronous variant (kept for callers/tests that patch it)."""
+        proofs.extend(self._sign_range(sq, self._prove_range(sq, dp_results)))
+
+    def _prove_range(self, sq, dp_results: dict) -> list:
         P = sq.RosterServers.aggregate()
+        out = []
         for dp_id, res in dp_results.items():
-            dp = self.cluster.by_id(dp_id)
-            with timers.timed(f"{dp_id}_AllProofs"):
+            with timers.timed(f"{dp_id}_AllProofs", sync=False):
                 lists = []
                 if any(b is not None for b in res["proofs"]):
                     sigmat = self.verifier_cache.sigmat(sq, self.device)
@@ -132,7 +139,30 @@ class DrynxNode:
                 else:  # no range proofs (ranges 0): ship the commitments only (dcp.go:283-288)
                     lists.append(rp.RangeProofList(0, 0, 0, [0] * len(res["cv"]), list(range(len(res["cv"]))),
                                                    res["cv"]))
-                proofs.append(prq.new_proof_request("range", lists, sq.SurveyID, dp_id, "", dp.keypair.secret))
+            out.append((dp_id, lists))
+        return out
+
+    def _sign_range(self, sq, proved: list) -> list:
+        reqs = []
+        for dp_id, lists in proved:
+            dp = self.cluster.by_id(dp_id)
+            reqs.append(prq.new_proof_request("range", lists, sq.SurveyID, dp_id, "", dp.keypair.secret))
+        return reqs
+
+    def _range_proofs_async(self, sq, dp_results: dict):
+        import concurrent.futures as cf
+
+        if not hasattr(self, "_pool"):
+            self._pool = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="drynx-proofs")
+        if type(self)._range_proofs is not DrynxNode._range_proofs or "_range_proofs" in self.__dict__:
+            # a patched (e.g. fault-injecting) prover: run it synchronously
+            lst: list = []
+            self._range_proofs(sq, dp_results, lst)
+            fut = cf.Future()
+            fut.set_result(lst)
+            return fut
+        proved = self._prove_range(sq, dp_results)  # GPU work is queued on this thread's stream
+        return self._pool.submit(self._sign_range, sq, proved)
 
     # ------------------------------------------------------------------ VN getters (api_skipchain.go)
     def get_genesis(self, vn_id: str):
