@@ -128,6 +128,7 @@ def main():
     for _ in range(args.steps):
         res, weights = one_step()
         blocks.append(res.block)
+    node.flush_stores()  # proof persistence overlaps the next step; the tail is timed too
     comm.barrier()
     if device.type == "cuda":
         torch.cuda.synchronize()

@@ -46,20 +46,24 @@ class Store:
             self._db.execute("COMMIT")
 
     def get(self, bucket: str, key: str):
+        self.flush()  # read-your-writes over queued updates
         with self._lock:
             r = self._db.execute("SELECT value FROM kv WHERE bucket=? AND key=?", (bucket, key)).fetchone()
         return None if r is None else bytes(r[0])
 
     def bucket(self, bucket: str) -> dict:
+        self.flush()  # read-your-writes over queued updates
         with self._lock:
             rows = self._db.execute("SELECT key, value FROM kv WHERE bucket=? ORDER BY key", (bucket,)).fetchall()
         return {k: bytes(v) for k, v in rows}
 
     def buckets(self) -> list:
+        self.flush()  # read-your-writes over queued updates
         with self._lock:
             return [r[0] for r in self._db.execute("SELECT DISTINCT bucket FROM kv ORDER BY bucket").fetchall()]
 
     def cursor_prefix(self, bucket_prefix: str) -> dict:
+        self.flush()  # read-your-writes over queued updates
         with self._lock:
             rows = self._db.execute("SELECT bucket, key, value FROM kv WHERE bucket LIKE ? ORDER BY bucket, key",
                                     (bucket_prefix + "%",)).fetchall()

@@ -101,7 +101,7 @@ def verify_and_store(ctx, sq, vn, vn_index: int, n_vns: int, requests: list) -> 
     for k in prq.VN_ORDER:
         if counts[k] != exp[k]:
             log.warning(f"{vn.id}: received {counts[k]} {k} proofs, expected {exp[k]}")
-    store.update(vn.id, f"{sq.SurveyID}/map", json.dumps(bitmap, sort_keys=True).encode())
+    store.update_async(vn.id, f"{sq.SurveyID}/map", json.dumps(bitmap, sort_keys=True).encode())
     ctx.local_bitmaps[(sq.SurveyID, vn.id)] = bitmap
     return bitmap
 
@@ -144,14 +144,15 @@ def proof_collection(ctx, sq, local_requests: list):
         block.ForwardSignatures.update(d)
     for vn in vns:
         if vn.rank == ctx.rank:
+            # proof blobs keep persisting on the store's writer thread (GetProofs /
+            # CloseDB flush); the block only depends on the bitmap
             st = ctx.store(vn.id)
-            st.flush()
             raw = block.to_bytes()
-            st.update("skipchain", block.Hash, raw)
-            st.update("skipchain", "latest", raw)
+            st.update_async("skipchain", block.Hash, raw)
+            st.update_async("skipchain", "latest", raw)
             if block.Index == 0:
-                st.update("genesis", "genesis", raw)
-            st.update("mapping", sq.SurveyID, block.Hash.encode())
+                st.update_async("genesis", "genesis", raw)
+            st.update_async("mapping", sq.SurveyID, block.Hash.encode())
     ctx.last_block = block
     timers.end_timer(t)
     return block

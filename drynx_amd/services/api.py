@@ -65,12 +65,19 @@ class DrynxClient:
     def send_survey_query(self, sq: SurveyQuery):
         """SendSurveyQuery: run the survey, decode every group.  Returns
         (group keys, list of decoded float vectors, SurveyResult)."""
-        res = self.entry.run_survey(sq)
-        groups, values = [], []
-        with timers.timed("Decode"):
-            for g, cv in enumerate(res.groups()):
-                groups.append(str(g))
-                values.append(self.decode(cv.to(self.device), sq.Query.Operation))
+        op = sq.Query.Operation
+
+        def decode_all(partial):
+            groups, values = [], []
+            with timers.timed("Decode"):
+                for g, cv in enumerate(partial.groups()):
+                    groups.append(str(g))
+                    values.append(self.decode(cv.to(self.device), op))
+            return groups, values
+
+        # decoding overlaps the VNs' proof verification (own thread + stream)
+        res = self.entry.run_survey(sq, on_result=decode_all)
+        groups, values = res.client_out
         return groups, values, res
 
     def decode(self, cv: eg.CipherVector, op: Operation):

@@ -292,7 +292,7 @@ class RemoteNode:
         self.roles = roles
         self.roster = roster
 
-    def run_survey(self, sq):
+    def run_survey(self, sq, on_result=None):
         from .service import SurveyResult
 
         out = request(self.address, {"cmd": "survey", "sq": sq.to_dict(), "roles": self.roles,
@@ -301,7 +301,10 @@ class RemoteNode:
             raise RuntimeError(out.get("error"))
         cv = CipherVector.from_bytes(bytes.fromhex(out["cv"]))
         blk = SkipBlock.from_bytes(out["block"].encode()) if out.get("block") else None
-        return SurveyResult(out["survey_id"], cv, out["n_groups"], out["n_out"], blk)
+        res = SurveyResult(out["survey_id"], cv, out["n_groups"], out["n_out"], blk)
+        if on_result is not None:
+            res.client_out = on_result(res)
+        return res
 
     def _vn(self, cmd, vn, **kw):
         out = request(self.address, dict({"cmd": cmd, "vn": vn}, **kw))

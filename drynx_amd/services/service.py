@@ -48,6 +48,7 @@ class SurveyResult:
     n_out: int
     block: SkipBlock | None = None
     clear_dp: dict = field(default_factory=dict)
+    client_out: object = None
 
     def groups(self):
         return [self.result[g * self.n_out:(g + 1) * self.n_out] for g in range(self.n_groups)]
@@ -80,8 +81,15 @@ class DrynxNode:
         return s
 
     # ------------------------------------------------------------------ main entry
-    def run_survey(self, sq: SurveyQuery | None) -> SurveyResult:
-        """Collective: every rank calls it; rank 0 passes the SurveyQuery."""
+    def run_survey(self, sq: SurveyQuery | None, on_result=None) -> SurveyResult:
+        """Collective: every rank calls it; rank 0 passes the SurveyQuery.
+
+        ``on_result(SurveyResult)`` (querier side) is handed the key-switched
+        result as soon as the CNs produce it and runs on a worker thread with
+        its own device stream, overlapping the VNs' proof collection -- as in
+        the reference, where the querier decodes while the VNs verify
+        (service.go:805-868 vs proof_collection_protocol.go); its return value
+        lands in ``SurveyResult.client_out``."""
         d = self.comm.broadcast_object(sq.to_dict() if sq is not None else None, src=0)
         sq = SurveyQuery.from_dict(d)
         self.surveys[sq.SurveyID] = sq
@@ -113,13 +121,39 @@ class DrynxNode:
             result = CipherVector.cat([result[g * n_out: g * n_out + per] for g in range(n_groups)])
             n_out = per
         timers.end_timer(t_exec)
+        client_future = None
+        if on_result is not None and result is not None:
+            client_future = self._submit_client(on_result, SurveyResult(sq.SurveyID, result, n_groups, n_out))
         if range_future is not None:
             proofs.extend(range_future.result())
         block = None
         if q.Proofs and q.RosterVNs is not None and len(q.RosterVNs.list):
             block = pcp.proof_collection(self, sq, proofs)
         clear = {k: v["clear"] for k, v in dp_results.items()}
-        return SurveyResult(sq.SurveyID, result, n_groups, n_out, block, clear)
+        out = SurveyResult(sq.SurveyID, result, n_groups, n_out, block, clear)
+        if client_future is not None:
+            out.client_out = client_future.result()
+        return out
+
+    def _submit_client(self, fn, partial: SurveyResult):
+        import concurrent.futures as cf
+
+        if not hasattr(self, "_client_pool"):
+            self._client_pool = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="drynx-querier")
+        if self.device.type != "cuda":
+            return self._client_pool.submit(fn, partial)
+        if not hasattr(self, "_client_stream"):
+            self._client_stream = torch.cuda.Stream(self.device)
+        side = self._client_stream
+        side.wait_stream(torch.cuda.current_stream(self.device))  # result tensors are ready on `side`
+
+        def run():
+            with torch.cuda.stream(side):
+                r = fn(partial)
+            side.synchronize()
+            return r
+
+        return self._client_pool.submit(run)
 
     def _range_proofs(self, sq, dp_results: dict, proofs: list):
         """Synchronous variant (kept for callers/tests that patch it)."""
@@ -194,6 +228,11 @@ class DrynxNode:
 
         raw = self.store(vn_id).get(vn_id, f"{survey_id}/map")
         return json.loads(raw) if raw else {}
+
+    def flush_stores(self):
+        """Wait until every queued ledger write is durable."""
+        for s in self._stores.values():
+            s.flush()
 
     def close_db(self, vn_id: str, remove: bool = False):
         s = self._stores.pop(vn_id, None)

@@ -21,8 +21,10 @@ _records: dict = defaultdict(list)
 
 
 def _sync():
+    # the calling thread's stream only: phases running on other threads/streams
+    # (querier decode, proof signing) keep overlapping
     if torch.cuda.is_available() and torch.cuda.is_initialized():
-        torch.cuda.synchronize()
+        torch.cuda.current_stream().synchronize()
 
 
 class Timer:
