@@ -22,6 +22,7 @@ from typing import Any
 import numpy as np
 import torch
 
+from ..query import ivsigs_digest
 from ..utils import timers
 from ..utils.log import get_logger
 from . import aggregation_shuffle as ags
@@ -157,13 +158,7 @@ class VerifierCache:
         """Keyed by a digest of the signature set, so repeated surveys over the
         same CN input-validation keys reuse the device tables."""
         sigs = sq.Query.IVSigs.InputValidationSigs
-        h = hashlib.sha256()
-        for row in sigs:
-            for s in row:
-                h.update(s.Public)
-                h.update(s.Signature[:128])
-                h.update(len(s.Signature).to_bytes(4, "little"))
-        key = (h.hexdigest(), len(sigs), len(sigs[0]) if sigs else 0, str(device))
+        key = (ivsigs_digest(sigs), len(sigs), len(sigs[0]) if sigs else 0, str(device))
         if key not in self._sig:
             if len(self._sig) > 8:
                 self._sig.clear()

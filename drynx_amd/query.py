@@ -12,6 +12,7 @@ Everything serialises to plain JSON-able dicts for the control plane.
 from __future__ import annotations
 
 import copy
+import hashlib
 import uuid
 from dataclasses import asdict, dataclass, field, fields, is_dataclass
 from typing import Optional
@@ -181,6 +182,30 @@ class SurveyQuery:
     @staticmethod
     def from_dict(d: dict) -> "SurveyQuery":
         return _survey_from_dict(d)
+
+
+_digest_memo: dict = {}
+
+
+def ivsigs_digest(sigs) -> str:
+    """sha256 over a signature set (memoised per list object: the same CN
+    input-validation keys serve many surveys)."""
+    if not sigs:
+        return ""
+    hit = _digest_memo.get(id(sigs))
+    if hit is not None and hit[0] is sigs:
+        return hit[1]
+    h = hashlib.sha256()
+    for row in sigs:
+        h.update(len(row).to_bytes(4, "little"))
+        for s in row:
+            h.update(s.Public)
+            h.update(s.Signature)
+    d = h.hexdigest()
+    if len(_digest_memo) > 16:
+        _digest_memo.clear()
+    _digest_memo[id(sigs)] = (sigs, d)
+    return d
 
 
 def _to_jsonable(obj):

@@ -17,6 +17,7 @@ Timer names follow the reference.
 """
 from __future__ import annotations
 
+import copy
 import os
 from dataclasses import dataclass, field
 
@@ -33,7 +34,7 @@ from ..proofs import requests as prq
 from ..protocols import computing_nodes as cnp
 from ..protocols import data_collection as dcp
 from ..protocols import proof_collection as pcp
-from ..query import SurveyQuery, add_diff_p, check_parameters
+from ..query import PublishSignatureBytes, SurveyQuery, add_diff_p, check_parameters, ivsigs_digest
 from ..utils import timers
 from ..utils.log import get_logger
 
@@ -90,8 +91,7 @@ class DrynxNode:
         the reference, where the querier decodes while the VNs verify
         (service.go:805-868 vs proof_collection_protocol.go); its return value
         lands in ``SurveyResult.client_out``."""
-        d = self.comm.broadcast_object(sq.to_dict() if sq is not None else None, src=0)
-        sq = SurveyQuery.from_dict(d)
+        sq = self._broadcast_query(sq)
         self.surveys[sq.SurveyID] = sq
         if self.rank == 0 and not check_parameters(sq, add_diff_p(sq.Query.DiffP)):
             log.warning("query parameters failed CheckParameters; continuing as the reference does")
@@ -154,6 +154,42 @@ class DrynxNode:
             return r
 
         return self._client_pool.submit(run)
+
+    def _broadcast_query(self, sq: SurveyQuery | None) -> SurveyQuery:
+        """Query to every rank (the reference broadcasts it down the CN tree,
+        service.go:263-330).  The CN input-validation signatures (MBs for wide
+        queries) travel only to ranks that do not hold that set yet (digest
+        keyed), as raw bytes."""
+        if self.comm.world == 1:
+            return sq
+        if not hasattr(self, "_ivsigs"):
+            self._ivsigs = {}
+        msg = None
+        if sq is not None:
+            sigs = sq.Query.IVSigs.InputValidationSigs
+            dg = ivsigs_digest(sigs)
+            if sigs:
+                self._ivsigs[dg] = sigs
+            lite = copy.copy(sq)
+            lite.Query = copy.copy(sq.Query)
+            lite.Query.IVSigs = copy.copy(sq.Query.IVSigs)
+            lite.Query.IVSigs.InputValidationSigs = None
+            msg = (lite.to_dict(), dg)
+        d, dg = self.comm.broadcast_object(msg, src=0)
+        missing = any(self.comm.all_gather_object(bool(dg) and dg not in self._ivsigs))
+        if missing:
+            raw = None
+            if self.rank == 0:
+                raw = [[(x.Public, x.Signature) for x in row] for row in self._ivsigs[dg]]
+            raw = self.comm.broadcast_object(raw, src=0)
+            if dg not in self._ivsigs:
+                if len(self._ivsigs) > 8:
+                    self._ivsigs.clear()
+                self._ivsigs[dg] = [[PublishSignatureBytes(p, g) for p, g in row] for row in raw]
+        out = SurveyQuery.from_dict(d)
+        if dg:
+            out.Query.IVSigs.InputValidationSigs = self._ivsigs[dg]
+        return out
 
     def _range_proofs(self, sq, dp_results: dict, proofs: list):
         """Synchronous variant (kept for callers/tests that patch it)."""
