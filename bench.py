@@ -10,7 +10,7 @@ One step = one complete survey through the framework:
   DP (one per rank/GPU): 1e6 synthetic SPECTF-shaped records (44 features,
   random-init data, generated once on the device = the DP's database) ->
   approximation-coefficient encoding (fp64 MFMA) -> 2070 ElGamal ciphertexts
-  -> 2070 range proofs (u=16, l=8, signed offset 2^31) with S = 3 CNs ->
+  -> 2070 range proofs (u=16, l=16 as in the reference's service tests, signed offset 2^62) with S = 3 CNs ->
   collective aggregation -> key switching (+ aggregation / key-switch proofs)
   -> querier decryption (BSGS) + gradient descent -> proof collection at the
   VNs (one per rank, every proof verified by exactly one VN: batched
@@ -61,8 +61,8 @@ def parse():
     ap.add_argument("--records", type=int, default=1_000_000, help="records per DP (one DP per GPU)")
     ap.add_argument("--features", type=int, default=44, help="SPECTF-shaped: 44 features -> 2070 outputs")
     ap.add_argument("--cns", type=int, default=3)
-    ap.add_argument("--u", type=int, default=16)
-    ap.add_argument("--l", type=int, default=8)
+    ap.add_argument("--u", "--base", dest="u", type=int, default=16)
+    ap.add_argument("--l", "--digits", dest="l", type=int, default=16)
     ap.add_argument("--precision", type=float, default=100.0)
     ap.add_argument("--max-iter", type=int, default=450)
     ap.add_argument("--device", default=None)
@@ -98,7 +98,8 @@ def main():
                                       StandardDeviations=sds, Lambda=1.0, Step=0.012, MaxIterations=args.max_iter,
                                       InitialWeights=[0.1] * (d + 1), K=2,
                                       PrecisionApproxCoefficients=args.precision)
-    offset = (args.u ** args.l) // 2
+    # signed coefficients: prove m + offset in [0, u^l) (offset fits the int64 wire field)
+    offset = min((args.u ** args.l) // 2, 1 << 62)
     client = DrynxClient(node, device=device) if rank == 0 else None
     template = None
     if rank == 0:  # CN input-validation keys are set up once, before the queries (as in the reference simulation)

@@ -1,17 +1,24 @@
-// K13: logistic-regression approximation-coefficient GEMM on fp64 MFMA.
+// K13: logistic-regression approximation-coefficient encoder on fp64 MFMA.
 //
-//   out[a][b] = sum_i w[i] * X[i][a] * X[i][b],   X: [N][D] row-major fp64, D <= 48
+// One pass over the DP's raw records computes BOTH coefficient levels:
 //
-// Reference: lib/encoding/logistic_regression.go:61-111 computes the level-2
-// coefficients record by record through cartesian products (O(N (d+1)^2)
-// scalar float ops in Go).  Here it is one tall-skinny GEMM over the records:
-// K = N is the reduction dimension of v_mfma_f64_16x16x4f64.  For one K-step of
-// 4 records, lane l holds X[k][16t + (l&15)] (k = l>>4) for the three 16-column
-// tiles t; the same registers are the B operand and, scaled by w[k], the A
-// operand, so the 3x3 output tiles need 3 loads + 9 MFMAs per step.  Waves
-// stride over records (grid-stride), the 4 waves of a block reduce through LDS
-// and each block writes one 48x48 partial; a tiny second pass (torch.sum on the
-// [blocks,48,48] slab) finishes deterministically.
+//   xa_i      = [1, (X_i - mean) / sd]                (standardise + augment, in registers)
+//   out[a][b] = sum_i w_i * xa_i[a] * xa_i[b]          (level 2, w_i = wa*y_i + wb or w[i])
+//   out[D][b] = sum_i g_i * xa_i[b],  g_i = 2 y_i - 1  (level 1, in the spare row D)
+//
+// Reference: lib/encoding/logistic_regression.go:61-111 computes the level-1
+// and level-2 coefficients record by record through cartesian products
+// (O(N (d+1)^2) scalar float ops in Go, after a separate standardisation pass,
+// :367-403).  Here it is one tall-skinny GEMM over the records: K = N is the
+// reduction dimension of v_mfma_f64_16x16x4f64.  For one K-step of 4 records,
+// lane l holds xa[k][16t + (l&15)] (k = l>>4) for the three 16-column tiles t;
+// the same registers are the B operand and, scaled by w[k], the A operand, so
+// the 3x3 output tiles need 3 loads + 9 MFMAs per step.  The level-1 vector
+// rides in the A operand's spare column D (A = g_i there, B = 0), so it costs
+// no extra pass over HBM (it used to be a separate rocBLAS gemv that ran on a
+// single workgroup).  Waves stride over records (grid-stride), the 4 waves of
+// a block reduce through LDS and each block writes one 48x48 partial; a tiny
+// second pass (torch.sum on the [blocks,48,48] slab) finishes deterministically.
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <cstdio>
@@ -24,32 +31,62 @@ constexpr int kTiles = 3;  // D <= 48
 constexpr int kD = kTile * kTiles;
 constexpr int kWaves = 4;
 
-__global__ void __launch_bounds__(256) lr_moments_kernel(const double *__restrict__ X, const double *__restrict__ w,
-                                                          int64_t N, int D, double *__restrict__ partial) {
+struct LrArgs {
+  const double *X;     // [N][dx], row stride ldx
+  int64_t ldx;
+  int64_t N;
+  int dx;              // raw feature columns
+  int aug;             // 1: prepend the constant-1 column
+  const double *mean;  // [dx] or null (no standardisation)
+  const double *sd;    // [dx] or null
+  const double *w;     // [N] per-record level-2 weight, or null -> wa*y + wb
+  const double *y;     // [N] labels (double) or null
+  double wa, wb;
+  int level1;          // 1: g = 2y - 1 accumulated in row D
+};
+
+__global__ void __launch_bounds__(256) lr_encode_kernel(LrArgs p, double *__restrict__ partial) {
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int col = lane & 15;
   const int kk = lane >> 4;  // 0..3 record within the K-step
+  const int D = p.dx + p.aug;
   dx_f64x4 acc[kTiles][kTiles];
 #pragma unroll
   for (int a = 0; a < kTiles; a++)
 #pragma unroll
     for (int b = 0; b < kTiles; b++) acc[a][b] = (dx_f64x4){0.0, 0.0, 0.0, 0.0};
 
+  // per-lane standardisation constants of the three columns this lane owns
+  double mu[kTiles], sdv[kTiles];
+  int src[kTiles];
+#pragma unroll
+  for (int t = 0; t < kTiles; t++) {
+    const int c = t * kTile + col;
+    src[t] = c - p.aug;  // raw column, -1 for the augmentation column
+    const bool raw = (c < D) && src[t] >= 0;
+    mu[t] = (raw && p.mean) ? p.mean[src[t]] : 0.0;
+    sdv[t] = (raw && p.sd) ? p.sd[src[t]] : 1.0;
+  }
+
   const int64_t gw = (int64_t)blockIdx.x * kWaves + wave;
   const int64_t nw = (int64_t)gridDim.x * kWaves;
-  const int64_t steps = (N + 3) / 4;
+  const int64_t steps = (p.N + 3) / 4;
   for (int64_t s = gw; s < steps; s += nw) {
     const int64_t row = s * 4 + kk;
     double v[kTiles];
-    double wi = 0.0;
-    if (row < N) {
-      wi = w[row];
-      const double *xr = X + row * (int64_t)D;
+    double wi = 0.0, gi = 0.0;
+    if (row < p.N) {
+      const double yi = p.y ? p.y[row] : 0.0;
+      wi = p.w ? p.w[row] : p.wa * yi + p.wb;
+      gi = 2.0 * yi - 1.0;
+      const double *xr = p.X + row * p.ldx;
 #pragma unroll
       for (int t = 0; t < kTiles; t++) {
-        int c = t * kTile + col;
-        v[t] = c < D ? xr[c] : 0.0;
+        const int c = t * kTile + col;
+        if (c >= D) v[t] = 0.0;
+        else if (src[t] < 0) v[t] = 1.0;
+        else v[t] = (xr[src[t]] - mu[t]) / sdv[t];
       }
     } else {
 #pragma unroll
@@ -57,7 +94,8 @@ __global__ void __launch_bounds__(256) lr_moments_kernel(const double *__restric
     }
 #pragma unroll
     for (int a = 0; a < kTiles; a++) {
-      const double av = v[a] * wi;
+      const int c = a * kTile + col;
+      const double av = (p.level1 && c == D) ? gi : v[a] * wi;
 #pragma unroll
       for (int b = 0; b < kTiles; b++) acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, v[b], acc[a][b], 0, 0, 0);
     }
@@ -78,16 +116,31 @@ __global__ void __launch_bounds__(256) lr_moments_kernel(const double *__restric
     out[e] = red[0][i][j] + red[1][i][j] + red[2][i][j] + red[3][i][j];
   }
 }
-}  // namespace
 
-extern "C" int dx_lr_moments(void *stream, const double *X, const double *w, int64_t N, int D, double *partial,
-                             int n_blocks) {
-  if (D > kD || D <= 0) return -2;
-  hipLaunchKernelGGL(lr_moments_kernel, dim3(n_blocks), dim3(256), 0, (hipStream_t)stream, X, w, N, D, partial);
+int launch(void *stream, const LrArgs &a, double *partial, int n_blocks) {
+  const int D = a.dx + a.aug;
+  if (a.dx <= 0 || D > kD || (a.level1 && D >= kD) || n_blocks <= 0) return -2;
+  if ((a.level1 || !a.w) && !a.y) return -2;
+  hipLaunchKernelGGL(lr_encode_kernel, dim3(n_blocks), dim3(256), 0, (hipStream_t)stream, a, partial);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
-    fprintf(stderr, "[drynx_amd native] lr_moments: %s\n", hipGetErrorString(e));
+    fprintf(stderr, "[drynx_amd native] lr_encode: %s\n", hipGetErrorString(e));
     return -1;
   }
   return 0;
+}
+}  // namespace
+
+// sum_i w_i X_i X_i^T over already-prepared rows (no standardisation, no level 1).
+extern "C" int dx_lr_moments(void *stream, const double *X, const double *w, int64_t N, int D, double *partial,
+                             int n_blocks) {
+  LrArgs a{X, D, N, D, 0, nullptr, nullptr, w, nullptr, 0.0, 0.0, 0};
+  return launch(stream, a, partial, n_blocks);
+}
+
+// Fused DP encoder: standardise + augment + level-1 (row D) + level-2 ((wa*y + wb) weights).
+extern "C" int dx_lr_encode(void *stream, const double *X, int64_t ldx, int64_t N, int dx, const double *mean,
+                            const double *sd, const double *y, double wa, double wb, double *partial, int n_blocks) {
+  LrArgs a{X, ldx, N, dx, 1, mean, sd, nullptr, y, wa, wb, 1};
+  return launch(stream, a, partial, n_blocks);
 }

@@ -106,6 +106,17 @@ def round_precision(v: torch.Tensor, precision: float) -> torch.Tensor:
 def encode_coefficients_int(X: torch.Tensor, y: torch.Tensor, params: LogisticRegressionParameters) -> torch.Tensor:
     """The packed int64 vector the DP encrypts (before encryption)."""
     X = X.to(torch.float64)
+    if X.is_cuda and params.K <= 2 and X.shape[1] + 1 < 48:
+        # one fused pass over the records: standardise + augment + level 1 + level 2 (dx_lr_encode)
+        if params.Means and params.StandardDeviations:
+            m = torch.as_tensor(params.Means, dtype=torch.float64)
+            s = torch.as_tensor(params.StandardDeviations, dtype=torch.float64)
+        else:
+            m, s = compute_means_sds(X)
+        # level-2 weight ypart = y - y*(-1)^2 - 1 = 0*y - 1
+        lvl1, lvl2 = nt.lr_encode(X.contiguous(), y, m, s, 0.0, -1.0)
+        levels = [lvl1] if params.K == 1 else [lvl1, lvl2.reshape(-1)]
+        return torch.cat([round_precision(lv, params.PrecisionApproxCoefficients) for lv in levels])
     if params.Means and params.StandardDeviations:
         Xs = standardise_with(X, params.Means, params.StandardDeviations)
     else:

@@ -79,6 +79,7 @@ _SIGS = {
     "dx_gt_prod_chunks": [_I, _P, _P, _P, _L, _L, _L],
     "dx_version": [],
     "dx_lr_moments": [_P, _P, _P, _L, _I, _P, _I],
+    "dx_lr_encode": [_P, _P, _L, _L, _I, _P, _P, _P, ctypes.c_double, ctypes.c_double, _P, _I],
     "dx_g1_mul_fast": [_P, _P, _P, _P, _L, _I, _I],
     "dx_rp_verify_fold": [_P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _I],
     "dx_rp_prove_a": [_I, _P, _P, _P, _P, _P, _P, _L, _I, _I],
@@ -446,6 +447,31 @@ def lr_moments(X: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     if rc != 0:
         raise RuntimeError(f"dx_lr_moments failed rc={rc}")
     return partial.sum(0)[:D, :D]
+
+
+def lr_encode(X: torch.Tensor, y: torch.Tensor, mean: torch.Tensor, sd: torch.Tensor, wa: float, wb: float):
+    """Fused DP encoder on the fp64-MFMA kernel (GPU tensors only): with
+    xa_i = [1, (X_i - mean)/sd], returns (sum_i (2y_i-1) xa_i  [D],
+    sum_i (wa*y_i + wb) xa_i xa_i^T  [D, D]), D = X.shape[1] + 1 <= 47."""
+    assert X.is_cuda and X.dtype == torch.float64 and X.dim() == 2 and X.stride(1) == 1
+    N, dx = X.shape
+    D = dx + 1
+    if D >= 48:
+        raise ValueError(f"lr_encode supports at most 46 features (got {dx})")
+    y = y.to(device=X.device, dtype=torch.float64).contiguous()
+    mean = mean.to(device=X.device, dtype=torch.float64).contiguous()
+    sd = sd.to(device=X.device, dtype=torch.float64).contiguous()
+    assert y.numel() == N and mean.numel() == dx and sd.numel() == dx
+    steps = (N + 3) // 4
+    n_blocks = int(max(1, min(1024, (steps + 15) // 16)))
+    partial = torch.empty((n_blocks, 48, 48), dtype=torch.float64, device=X.device)
+    _, s = _ctx(X)
+    rc = _load().dx_lr_encode(s, _ptr(X), X.stride(0), N, dx, _ptr(mean), _ptr(sd), _ptr(y), float(wa), float(wb),
+                              _ptr(partial), n_blocks)
+    if rc != 0:
+        raise RuntimeError(f"dx_lr_encode failed rc={rc}")
+    tot = partial.sum(0)
+    return tot[D, :D], tot[:D, :D]
 
 
 # ----------------------------------------------------------------------------- range proofs (K15/K16)

@@ -93,6 +93,23 @@ def test_lr_moments_mfma_matches_fp64(gpu_device):
         assert torch.allclose(got, ref, rtol=1e-10, atol=1e-9), (got - ref).abs().max()
 
 
+def test_lr_encode_fused_matches_torch(gpu_device):
+    """Fused standardise+augment+level1+level2 kernel vs the plain torch path."""
+    from drynx_amd.models import logistic_regression as lr
+
+    for N, d in [(5000, 44), (1001, 8), (77, 46)]:
+        X = torch.rand(N, d, dtype=torch.float64, device=gpu_device) * 4
+        y = torch.randint(0, 2, (N,), device=gpu_device)
+        m, s = lr.compute_means_sds(X)
+        Xa = lr.augment((X - m) / s)
+        yf = y.to(torch.float64)
+        ref1 = Xa.T @ (2 * yf - 1)
+        ref2 = -(Xa.T @ Xa)
+        g1, g2 = nt.lr_encode(X, y, m, s, 0.0, -1.0)
+        assert torch.allclose(g1, ref1, rtol=1e-10, atol=1e-8), (g1 - ref1).abs().max()
+        assert torch.allclose(g2, ref2, rtol=1e-10, atol=1e-8), (g2 - ref2).abs().max()
+
+
 def test_range_proofs_gpu(gpu_device):
     from drynx_amd.crypto import elgamal as eg
     from drynx_amd.ops.encoding import CreateProofBatch
