@@ -176,6 +176,7 @@ def main():
         if args.json_out:
             with open(args.json_out, "w") as f:
                 json.dump(line, f, indent=1)
+    timers.dump_trace(os.environ.get("DRYNX_TRACE") and f"{os.environ['DRYNX_TRACE']}.r{rank}.json")
     node.close(remove=True)
     if dist.is_initialized():
         dist.destroy_process_group()

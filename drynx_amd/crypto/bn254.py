@@ -67,14 +67,19 @@ _R_LIMBS = ints_to_limbs([R])[0]
 
 
 def random_scalars(n: int, device="cpu") -> torch.Tensor:
-    """n uniform scalars in [1, r) from the OS CSPRNG (rejection sampling)."""
+    """n uniform scalars in [1, r): ChaCha20 keyed from the OS CSPRNG, expanded
+    where the scalars are consumed (one GPU launch for a whole proof batch)."""
+    return nt.random_scalars(n, device)
+
+
+def random_scalars_host_rejection(n: int) -> np.ndarray:
+    """Reference sampler (os.urandom + rejection) kept for distribution tests."""
     out = np.empty((0, 8), dtype=np.uint32)
     need = n
     while need > 0:
         m = int(need * 1.4) + 8
         raw = np.frombuffer(os.urandom(32 * m), dtype="<u4").reshape(m, 8).copy()
         raw[:, 7] &= 0x3FFFFFFF  # < 2^254
-        # accept v < r and v != 0 : compare limb-wise from the top
         v = raw.astype(np.uint64)
         rl = _R_LIMBS.astype(np.uint64)
         less = np.zeros(m, dtype=bool)
@@ -83,10 +88,9 @@ def random_scalars(n: int, device="cpu") -> torch.Tensor:
             less |= eq & (v[:, k] < rl[k])
             eq &= v[:, k] == rl[k]
         nz = raw.any(axis=1)
-        good = raw[less & nz]
-        out = np.concatenate([out, good[:need]])
+        out = np.concatenate([out, raw[less & nz][:need]])
         need = n - out.shape[0]
-    return to_tensor(out, device)
+    return out
 
 
 # ----------------------------------------------------------------------------- points <-> tensors

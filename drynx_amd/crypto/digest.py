@@ -1,0 +1,49 @@
+"""Payload digests for signed proof envelopes.
+
+Reference: lib/proof/structs_proofs.go — every ``New*ProofRequest`` marshals
+its proof and Schnorr-signs the bytes (:117, :143, ...); ``VerifyProofSignature``
+re-checks them (:498-505).  A range-proof bundle of a wide query is tens of MB
+(per value ``256 + 32 l + 544 S l`` B), so the digest that is
+signed is a chunked SHA-256 whose slices hash in parallel where the bytes
+live (HBM on a GPU, dx_sha256_chunks):
+
+    digest(b) = SHA-256("DXTH1" || le64(len b) || le64(CHUNK) || H(s_0) || ... || H(s_k-1))
+
+with s_i the CHUNK-byte slices of b (the last may be short; an empty payload
+has one empty slice).  ``digest_bytes`` (hashlib) and ``digest_tensor`` (HIP
+kernel over a tensor's raw bytes) are bit-identical; tests pin that.
+"""
+from __future__ import annotations
+
+import hashlib
+import struct
+
+import numpy as np
+import torch
+
+from .. import native as nt
+
+CHUNK = 4096
+_TAG = b"DXTH1"
+
+
+def _finish(nbytes: int, slice_digests: bytes) -> bytes:
+    h = hashlib.sha256()
+    h.update(_TAG + struct.pack("<QQ", nbytes, CHUNK))
+    h.update(slice_digests)
+    return h.digest()
+
+
+def digest_bytes(b: bytes) -> bytes:
+    mv = memoryview(b)
+    n = len(mv)
+    parts = [hashlib.sha256(mv[o: o + CHUNK]).digest() for o in range(0, n, CHUNK)] or [hashlib.sha256(b"").digest()]
+    return _finish(n, b"".join(parts))
+
+
+def digest_tensor(t: torch.Tensor) -> bytes:
+    """Digest of the raw (little-endian) bytes of a contiguous tensor."""
+    t = t.contiguous()
+    words = nt.sha256_chunks(t, CHUNK)
+    be = words.cpu().numpy().view(np.uint32).astype(">u4").tobytes()
+    return _finish(t.numel() * t.element_size(), be)

@@ -7,21 +7,35 @@ Reference: each VN opens bbolt at ``"db:"+ServerIdentity.ID``
   <VN address>     key surveyID/map                        -> bitmap
   genesis          key genesis                             -> genesis block
   mapping          key surveyID                            -> block hash
-Here: SQLite (WAL) with one (bucket, key) -> blob table; writes can be queued
-to a background writer thread so proof persistence never sits on the
-verification critical path (``flush`` joins them).
+Here: SQLite (WAL) with one (bucket, key) -> value table; values above
+``BLOB_MIN`` bytes (range-proof bundles: tens of MB per DP) go to an
+append-only segment file next to the database and the table keeps a
+(offset, length) reference, so a wide query's proofs land with one sequential
+write instead of B-tree page churn.  Writes can be queued to a background
+writer thread so proof persistence never sits on the verification critical
+path (``flush`` joins them); a queued value may be a device tensor, copied to
+the host by the writer.
 """
 from __future__ import annotations
 
 import os
 import queue
 import sqlite3
+import struct
 import threading
+
+from ..utils import timers
+
+
+BLOB_MIN = 1 << 16
+_REF = b"\x00DXBLOB1"
 
 
 class Store:
     def __init__(self, path: str):
         self.path = path
+        self.blob_path = path + ".blobs"
+        self._blob_f = None
         d = os.path.dirname(os.path.abspath(path))
         os.makedirs(d, exist_ok=True)
         self._lock = threading.RLock()
@@ -33,29 +47,62 @@ class Store:
         self._writer = None
         self.closed = False
 
+    # ------------------------------------------------------------- values / blob segment
+    @staticmethod
+    def _as_bytes(value):
+        if hasattr(value, "cpu") and hasattr(value, "numpy"):  # a (device) tensor
+            return value.detach().cpu().contiguous().numpy().tobytes()
+        return bytes(value)
+
+    def _encode(self, value) -> bytes:
+        """Caller holds the lock."""
+        b = self._as_bytes(value)
+        if len(b) < BLOB_MIN:
+            return b
+        if self._blob_f is None:
+            self._blob_f = open(self.blob_path, "ab")
+        off = self._blob_f.seek(0, os.SEEK_END)
+        self._blob_f.write(b)
+        return _REF + struct.pack("<QQ", off, len(b))
+
+    def _decode(self, v) -> bytes:
+        v = bytes(v)
+        if len(v) == len(_REF) + 16 and v.startswith(_REF):
+            off, n = struct.unpack("<QQ", v[len(_REF):])
+            if self._blob_f is not None:
+                self._blob_f.flush()
+            with open(self.blob_path, "rb") as f:
+                f.seek(off)
+                return f.read(n)
+        return v
+
     # ------------------------------------------------------------- sync API
     def update(self, bucket: str, key: str, value: bytes):
         """UpdateDB(db, bucket, key, value)."""
         with self._lock:
-            self._db.execute("INSERT OR REPLACE INTO kv(bucket, key, value) VALUES (?,?,?)", (bucket, key, value))
+            self._db.execute("INSERT OR REPLACE INTO kv(bucket, key, value) VALUES (?,?,?)",
+                             (bucket, key, self._encode(value)))
 
     def update_many(self, rows):
         with self._lock:
+            enc = [(b, k, self._encode(v)) for b, k, v in rows]
+            if self._blob_f is not None:
+                self._blob_f.flush()
             self._db.execute("BEGIN")
-            self._db.executemany("INSERT OR REPLACE INTO kv(bucket, key, value) VALUES (?,?,?)", rows)
+            self._db.executemany("INSERT OR REPLACE INTO kv(bucket, key, value) VALUES (?,?,?)", enc)
             self._db.execute("COMMIT")
 
     def get(self, bucket: str, key: str):
         self.flush()  # read-your-writes over queued updates
         with self._lock:
             r = self._db.execute("SELECT value FROM kv WHERE bucket=? AND key=?", (bucket, key)).fetchone()
-        return None if r is None else bytes(r[0])
+            return None if r is None else self._decode(r[0])
 
     def bucket(self, bucket: str) -> dict:
         self.flush()  # read-your-writes over queued updates
         with self._lock:
             rows = self._db.execute("SELECT key, value FROM kv WHERE bucket=? ORDER BY key", (bucket,)).fetchall()
-        return {k: bytes(v) for k, v in rows}
+            return {k: self._decode(v) for k, v in rows}
 
     def buckets(self) -> list:
         self.flush()  # read-your-writes over queued updates
@@ -67,7 +114,7 @@ class Store:
         with self._lock:
             rows = self._db.execute("SELECT bucket, key, value FROM kv WHERE bucket LIKE ? ORDER BY bucket, key",
                                     (bucket_prefix + "%",)).fetchall()
-        return {(b, k): bytes(v) for b, k, v in rows}
+            return {(b, k): self._decode(v) for b, k, v in rows}
 
     # ------------------------------------------------------------- async writer
     def update_async(self, bucket: str, key: str, value: bytes):
@@ -93,7 +140,8 @@ class Store:
                     self._q.task_done()
                     break
                 batch.append(nxt)
-            self.update_many(batch)
+            with timers.span("store.write"):
+                self.update_many(batch)
             for _ in batch:
                 self._q.task_done()
 
@@ -110,9 +158,12 @@ class Store:
             self._writer = None
         with self._lock:
             self._db.close()
+            if self._blob_f is not None:
+                self._blob_f.close()
+                self._blob_f = None
         self.closed = True
         if remove:
-            for suf in ("", "-wal", "-shm"):
+            for suf in ("", "-wal", "-shm", ".blobs"):
                 try:
                     os.remove(self.path + suf)
                 except FileNotFoundError:

@@ -79,6 +79,8 @@ _SIGS = {
     "dx_gt_prod_chunks": [_I, _P, _P, _P, _L, _L, _L],
     "dx_version": [],
     "dx_lr_moments": [_P, _P, _P, _L, _I, _P, _I],
+    "dx_random_scalars": [_I, _P, _P, ctypes.c_uint32, _P, _L],
+    "dx_sha256_chunks": [_I, _P, _P, _L, _L, _P],
     "dx_lr_encode": [_P, _P, _L, _L, _I, _P, _P, _P, ctypes.c_double, ctypes.c_double, _P, _I],
     "dx_g1_mul_fast": [_P, _P, _P, _P, _L, _I, _I],
     "dx_rp_verify_fold": [_P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _I],
@@ -434,6 +436,33 @@ def gt_prod(x: torch.Tensor, chunk: int = 16) -> torch.Tensor:
 
 
 # ----------------------------------------------------------------------------- logistic-regression GEMM (K13)
+def random_scalars(n: int, device) -> torch.Tensor:
+    """n uniform nonzero Fr scalars [n, 8] (plain limbs): ChaCha20 keyed with
+    256 fresh bits of os.urandom per call, one block per scalar (dx_hash.hip)."""
+    import numpy as _np
+
+    device = torch.device(device)
+    out = torch.empty((max(0, n), 8), dtype=torch.int32, device=device)
+    if n <= 0:
+        return out
+    key = _np.frombuffer(os.urandom(32), dtype="<u4").copy()
+    g, s = _ctx(out)
+    _call("dx_random_scalars", g, s, key.ctypes.data_as(ctypes.c_void_p), 0, _ptr(out), n)
+    return out
+
+
+def sha256_chunks(data: torch.Tensor, chunk: int) -> torch.Tensor:
+    """[k, 8] big-endian SHA-256 words of every `chunk`-byte slice of the raw
+    bytes of a contiguous tensor (k = ceil(nbytes / chunk), >= 1)."""
+    data = data.contiguous()
+    nbytes = data.numel() * data.element_size()
+    k = max(1, (nbytes + chunk - 1) // chunk)
+    out = torch.empty((k, 8), dtype=torch.int32, device=data.device)
+    g, s = _ctx(data)
+    _call("dx_sha256_chunks", g, s, _ptr(data), nbytes, chunk, _ptr(out))
+    return out
+
+
 def lr_moments(X: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """sum_i w_i X_i X_i^T on the fp64-MFMA kernel (GPU tensors only)."""
     assert X.is_cuda and X.dtype == torch.float64 and X.dim() == 2 and X.shape[1] <= 48
@@ -518,4 +547,24 @@ def rp_verify_products(ZB_jac, Y_jac, rho, V_aff, a, S: int, L: int):
                                    n, S, L)
     if rc:
         raise RuntimeError(f"dx_rp_verify_fold failed rc={rc}")
-    return gt_prod(fb.view(-1, 1, 96), chunk=4).view(1, 96), gt_prod(gb.view(-1, 1, 96), chunk=4).view(1, 96)
+    return _finish_prod_on_host(fb), _finish_prod_on_host(gb)
+
+
+def _finish_prod_on_host(parts: torch.Tensor) -> torch.Tensor:
+    """Product of [n, 96] GT partials: wide GPU levels while n > 64, then the
+    short serial tail on the host (a lone GPU lane runs an Fp12 chain ~10x
+    slower than one host core).  Returns a [1, 96] HOST tensor."""
+    cur = parts.view(-1, 1, 96)
+    while cur.shape[0] > 64:
+        ch = min(32, max(2, (cur.shape[0] + 63) // 64))
+        cur = _gt_prod_level(cur, ch)
+    return gt_prod(cur.cpu(), chunk=4).view(1, 96)
+
+
+def _gt_prod_level(x: torch.Tensor, ch: int) -> torch.Tensor:
+    n_items, n_groups = x.shape[0], x.shape[1]
+    n_chunks = (n_items + ch - 1) // ch
+    out = torch.empty((n_chunks, n_groups, 96), dtype=torch.int32, device=x.device)
+    g, s = _ctx(x)
+    _call("dx_gt_prod_chunks", g, s, _ptr(x.contiguous()), _ptr(out), n_items, n_groups, ch)
+    return out

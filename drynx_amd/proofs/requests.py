@@ -16,12 +16,12 @@ from __future__ import annotations
 
 import hashlib
 import random
-from dataclasses import dataclass, field
 from typing import Any
 
 import numpy as np
 import torch
 
+from ..crypto import digest as payload_digest
 from ..query import ivsigs_digest
 from ..utils import timers
 from ..utils.log import get_logger
@@ -39,16 +39,41 @@ TIMER = {"range": "VerifyRange", "aggregation": "VerifyAggregation", "obfuscatio
          "shuffle": "VerifyShuffle", "keyswitch": "VerifyKeySwitch"}
 
 
-@dataclass
 class ProofRequest:
-    kind: str
-    survey_id: str
-    sender_id: str
-    differ_info: str
-    data: bytes
-    signature: bytes
-    obj: Any = field(default=None, repr=False, compare=False)  # decoded proof (in-process fast path)
-    data_digest: bytes = b""  # set for header-only copies (sharded verification: payload not shipped)
+    """One signed proof envelope.  The payload is either bytes or, for
+    range-proof bundles, the raw limb tensor itself (in HBM on a GPU): its
+    digest is computed on the device and its bytes are only materialised when
+    something needs them (ledger persistence, control-plane transport)."""
+
+    __slots__ = ("kind", "survey_id", "sender_id", "differ_info", "_data", "signature", "obj", "data_digest",
+                 "tensor")
+
+    def __init__(self, kind: str, survey_id: str, sender_id: str, differ_info: str, data: bytes | None,
+                 signature: bytes, obj: Any = None, data_digest: bytes = b"", tensor: torch.Tensor | None = None):
+        self.kind, self.survey_id, self.sender_id, self.differ_info = kind, survey_id, sender_id, differ_info
+        self._data = data
+        self.signature = signature
+        self.obj = obj  # decoded proof (in-process fast path)
+        self.data_digest = data_digest  # set for header-only copies (sharded verification)
+        self.tensor = tensor
+
+    @property
+    def data(self) -> bytes:
+        if self._data is None:
+            self._data = b"" if self.tensor is None else self.tensor.cpu().numpy().tobytes()
+        return self._data
+
+    @data.setter
+    def data(self, v: bytes):
+        self._data, self.tensor, self.data_digest = v, None, b""
+
+    def set_tensor(self, t: torch.Tensor):
+        """The payload is (now) this raw tensor; digest recomputed from it."""
+        self._data, self.tensor, self.data_digest = None, t, b""
+
+    def payload(self):
+        """Bytes or the device tensor, whichever is at hand (for the ledger)."""
+        return self.tensor if (self._data is None and self.tensor is not None) else self.data
 
     def base_key(self) -> str:
         return f"{self.survey_id}/{self.kind}/{self.sender_id}/{self.differ_info}"
@@ -59,12 +84,15 @@ class ProofRequest:
     def digest(self) -> bytes:
         if self.data_digest:
             return self.data_digest
-        self.data_digest = hashlib.sha256(self.data).digest()
+        if self._data is None and self.tensor is not None:
+            self.data_digest = payload_digest.digest_tensor(self.tensor)
+        else:
+            self.data_digest = payload_digest.digest_bytes(self.data)
         return self.data_digest
 
     @property
     def header_only(self) -> bool:
-        return not self.data and bool(self.data_digest)
+        return not self._data and self.tensor is None and bool(self.data_digest)
 
     def header(self) -> "ProofRequest":
         return ProofRequest(self.kind, self.survey_id, self.sender_id, self.differ_info, b"", self.signature,
@@ -120,10 +148,19 @@ def range_bundle_export_kyber(rpls) -> bytes:
 
 
 def new_proof_request(kind: str, proof, survey_id: str, sender_id: str, differ_info: str, secret: int) -> ProofRequest:
-    """New{Range,Aggregation,Obfuscation,Shuffle,KeySwitch}ProofRequest: marshal + Schnorr-sign."""
-    data = range_bundle_to_bytes(proof) if kind == "range" else proof.to_bytes()
-    sig = sigma.schnorr_sign(secret, hashlib.sha256(data).digest())
-    return ProofRequest(kind, survey_id, sender_id, differ_info, data, sig, obj=proof)
+    """New{Range,Aggregation,Obfuscation,Shuffle,KeySwitch}ProofRequest: marshal + Schnorr-sign.
+    Range bundles stay a device tensor; their digest is hashed on the device."""
+    with timers.span(f"sign.marshal.{kind}"):
+        if kind == "range":
+            req = ProofRequest(kind, survey_id, sender_id, differ_info, None, b"", obj=proof,
+                               tensor=range_bundle_pack(proof))
+        else:
+            req = ProofRequest(kind, survey_id, sender_id, differ_info, proof.to_bytes(), b"", obj=proof)
+    with timers.span(f"sign.digest.{kind}"):
+        dg = req.digest()
+    with timers.span(f"sign.schnorr.{kind}"):
+        req.signature = sigma.schnorr_sign(secret, dg)
+    return req
 
 
 def verify_signature(req: ProofRequest, public) -> bool:
@@ -180,7 +217,12 @@ def _ranges_ok(sq, rpl) -> bool:
 def verify_content(req: ProofRequest, sq, device, cache: VerifierCache) -> bool:
     P = sq.RosterServers.aggregate()
     if req.kind == "range":
-        rpls = req.obj if req.obj is not None else range_bundle_from_bytes(req.data, device)
+        if req.obj is not None:
+            rpls = req.obj
+        elif req.tensor is not None and req._data is None:
+            rpls = range_bundle_unpack(req.tensor.to(device))
+        else:
+            rpls = range_bundle_from_bytes(req.data, device)
         sigs = sq.Query.IVSigs.InputValidationSigs
         for r in rpls:
             if not r.has_rp:
@@ -224,7 +266,9 @@ def verify_requests(reqs: list, sq, vn_id: str, vn_index: int, n_vns: int, devic
     codes = [None] * len(reqs)
     todo: dict = {}
     for i, req in enumerate(reqs):
-        if not verify_signature(req, sq.IDtoPublic.get(req.sender_id)):
+        with timers.span(f"verify.signature.{req.kind}"):
+            sig_ok = verify_signature(req, sq.IDtoPublic.get(req.sender_id))
+        if not sig_ok:
             codes[i] = PROOF_FALSE_SIGN
         elif not should_verify(sq, req, vn_index, n_vns):
             codes[i] = PROOF_RECEIVED

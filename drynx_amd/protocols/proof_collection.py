@@ -80,8 +80,7 @@ def fan_out(ctx, sq, local_requests: list) -> list:
                 t = got_t[src][off: off + n]
                 off += n
                 req.obj = prq.range_bundle_unpack(t)
-                req.data = t.cpu().numpy().tobytes()  # signed bytes: the VN checks the digest itself
-                req.data_digest = b""
+                req.set_tensor(t)  # signed bytes: the VN re-hashes them on its device
             out.append(req)
     return out
 
@@ -96,7 +95,7 @@ def verify_and_store(ctx, sq, vn, vn_index: int, n_vns: int, requests: list) -> 
         bitmap[key] = code
         counts[req.kind] += 1
         if req.kind != "shuffle":  # storeProof skips shuffle proofs (proof_collection_protocol.go:318-331)
-            store.update_async(f"{sq.SurveyID}/{req.kind}", key, req.data)
+            store.update_async(f"{sq.SurveyID}/{req.kind}", key, req.payload())
     exp = expected_counts(sq)
     for k in prq.VN_ORDER:
         if counts[k] != exp[k]:

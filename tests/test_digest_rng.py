@@ -1,0 +1,58 @@
+"""Chunked payload digest (host hashlib vs native kernel) and the ChaCha20
+scalar CSPRNG.  GPU variants compare the device kernels with the host path."""
+import hashlib
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from drynx_amd import native as nt
+from drynx_amd.crypto import bn254 as bn
+from drynx_amd.crypto import digest as D
+from drynx_amd.crypto import oracle as O
+
+
+def _t(b: bytes, device="cpu"):
+    return torch.from_numpy(np.frombuffer(b, dtype="<i4").copy()).to(device)
+
+
+@pytest.mark.parametrize("n", [0, 4, 60, 64, 124, 4092, 4096, 4100, 3 * 4096 + 44, 65536])
+def test_digest_tensor_matches_bytes(n):
+    b = os.urandom(n)
+    assert D.digest_bytes(b) == D.digest_tensor(_t(b))
+
+
+def test_slice_digest_is_plain_sha256():
+    b = os.urandom(2 * D.CHUNK + 100)
+    w = nt.sha256_chunks(_t(b), D.CHUNK).numpy().view(np.uint32).astype(">u4")
+    for i in range(3):
+        assert w[i].tobytes() == hashlib.sha256(b[i * D.CHUNK:(i + 1) * D.CHUNK]).digest()
+
+
+def test_digest_sensitive_to_every_byte():
+    b = bytearray(os.urandom(3 * D.CHUNK))
+    d0 = D.digest_bytes(bytes(b))
+    for pos in (0, D.CHUNK - 1, D.CHUNK, len(b) - 1):
+        c = bytearray(b)
+        c[pos] ^= 1
+        assert D.digest_tensor(_t(bytes(c))) != d0
+
+
+def test_random_scalars_range_and_freshness():
+    a = bn.scalars_from_tensor(bn.random_scalars(20000))
+    b = bn.scalars_from_tensor(bn.random_scalars(20000))
+    assert all(0 < x < O.R for x in a)
+    assert len(set(a) | set(b)) == 40000  # fresh key per call
+    # top-bit frequency of a uniform value in [0, r): P(x >= 2^253) = 1 - 2^253/r
+    p = 1 - (1 << 253) / O.R
+    f = sum(x >> 253 for x in a) / len(a)
+    assert abs(f - p) < 0.02
+
+
+@pytest.mark.gpu
+def test_gpu_digest_and_rng(gpu_device):
+    b = os.urandom(5 * D.CHUNK + 12)
+    assert D.digest_tensor(_t(b, gpu_device)) == D.digest_bytes(b)
+    s = bn.scalars_from_tensor(bn.random_scalars(50000, gpu_device))
+    assert all(0 < x < O.R for x in s) and len(set(s)) == 50000
