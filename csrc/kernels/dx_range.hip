@@ -33,18 +33,36 @@ int dx_rp_prove_a(int on_gpu, void *stream, const uint32_t *negsB_aff, const uin
 // Table-driven prover (no pairing per item): a[it] = g_phi^{e[it]} * gT^{t[p*L+j]}
 // with g_phi = e(B, A_phi) comb-tabled per distinct signature point
 // (gphi_tables[tab_idx[it]]) and e = -s_j v_ij computed on the device.
+// gT^{t_pj} is shared by the S servers of a digit: computed once per (p, j)
+// (first pass, into a_out rows it = (p*S)*L + j) and reused by the others.
 int dx_rp_prove_a_tab(int on_gpu, void *stream, const uint32_t *gphi_tables, const int32_t *tab_idx,
                       const uint32_t *e_sc, const uint32_t *t_sc, const uint32_t *gt_table, uint32_t *a_out,
                       int64_t n_items, int S, int L) {
-  auto op = [=] __host__ __device__(int64_t it) {
-    int64_t j = it % L;
-    int64_t p = it / ((int64_t)S * L);
-    const Fp12 *T = reinterpret_cast<const Fp12 *>(gphi_tables) + (int64_t)tab_idx[it] * 8192;
-    Fp12 f = gt_fixed_pow(T, e_sc + 8 * it);
-    Fp12 g = gt_fixed_pow(reinterpret_cast<const Fp12 *>(gt_table), t_sc + 8 * (p * L + j));
-    at<Fp12>(a_out, it) = mul(f, g);
+  const int64_t n_pj = n_items / S;
+  auto p1 = [=] __host__ __device__(int64_t pj) {
+    const int64_t p = pj / L, j = pj % L;
+    at<Fp12>(a_out, p * S * L + j) = gt_fixed_pow(reinterpret_cast<const Fp12 *>(gt_table), t_sc + 8 * pj);
   };
-  return run(on_gpu, stream, n_items, op, true, "rp_prove_a_tab");
+  int rc = run(on_gpu, stream, n_pj, p1, true, "rp_prove_gt_t");
+  if (rc) return rc;
+  // servers i = S-1 .. 0 read the shared row before server 0 overwrites it: run
+  // the i > 0 items first, then i == 0
+  for (int pass = 0; pass < 2; pass++) {
+    const int64_t per = pass == 0 ? (int64_t)(S - 1) * L : (int64_t)L;  // items per value in this pass
+    if (per == 0) continue;
+    const int64_t n = n_pj / L * per;
+    auto p2 = [=] __host__ __device__(int64_t k) {
+      const int64_t p = k / per, r = k % per;
+      const int64_t i = pass == 0 ? 1 + r / L : 0, j = r % L;
+      const int64_t it = (p * S + i) * L + j;
+      const Fp12 *T = reinterpret_cast<const Fp12 *>(gphi_tables) + (int64_t)tab_idx[it] * 8192;
+      Fp12 f = gt_fixed_pow(T, e_sc + 8 * it);
+      at<Fp12>(a_out, it) = mul(f, at<Fp12>(a_out, p * S * L + j));
+    };
+    rc = run(on_gpu, stream, n, p2, true, "rp_prove_a_tab");
+    if (rc) return rc;
+  }
+  return 0;
 }
 
 // f[it] = ML(rho (ZB[p*L+j] - Y[p*S+i]), V[it]),  g[it] = a[it]^rho
@@ -66,20 +84,21 @@ int dx_rp_verify_items(int on_gpu, void *stream, const uint32_t *ZB_jac, const u
 
 }  // extern "C"
 
-// GPU-only fused variant: every 64-lane workgroup computes 64 items and folds
-// both products (Miller values, a^rho) with an LDS tree, writing one Fp12 pair
-// per workgroup — the [n_items] intermediate never reaches HBM.
+// GPU-only fused Miller fold: every 64-lane workgroup computes the Miller
+// values of 64 items and folds them with an LDS tree, writing one Fp12 per
+// workgroup -- the [n_items] intermediate never reaches HBM.  The a^rho side
+// of the batch equation is a separate bucket multi-exponentiation
+// (dx_gt_slice_prod below + rp_verify_products in native/__init__.py), so this
+// kernel carries only the Miller-loop state.
 namespace {
 constexpr int kVW = 64;
 __global__ void __launch_bounds__(kVW) rp_verify_fold_kernel(const uint32_t *ZB_jac, const uint32_t *Y_jac,
                                                               const uint32_t *rho, const uint32_t *V_aff,
-                                                              const uint32_t *a, uint32_t *f_blk, uint32_t *g_blk,
-                                                              int64_t n_items, int S, int L) {
+                                                              uint32_t *f_blk, int64_t n_items, int S, int L) {
   __shared__ Fp12 sf[kVW];
-  __shared__ Fp12 sg[kVW];
   const int lane = threadIdx.x;
   const int64_t it = (int64_t)blockIdx.x * kVW + lane;
-  Fp12 f = Fp12::one(), g = Fp12::one();
+  Fp12 f = Fp12::one();
   if (it < n_items) {
     int64_t j = it % L;
     int64_t pi = it / L;
@@ -87,32 +106,36 @@ __global__ void __launch_bounds__(kVW) rp_verify_fold_kernel(const uint32_t *ZB_
     G1J T = jadd(at<G1J>(ZB_jac, p * L + j), jneg(at<G1J>(Y_jac, pi)));
     G1A P = to_affine(scalar_mul(T, rho + 8 * it));
     f = miller_loop(P, at<G2A>(V_aff, it));
-    g = gt_pow(at<Fp12>(a, it), rho + 8 * it);
   }
   sf[lane] = f;
-  sg[lane] = g;
   __syncthreads();
   for (int s = kVW / 2; s > 0; s >>= 1) {
-    if (lane < s) {
-      sf[lane] = mul(sf[lane], sf[lane + s]);
-    } else if (lane < 2 * s) {
-      sg[lane - s] = mul(sg[lane - s], sg[lane]);
-    }
+    if (lane < s) sf[lane] = mul(sf[lane], sf[lane + s]);
     __syncthreads();
   }
-  if (lane == 0) {
-    at<Fp12>(f_blk, blockIdx.x) = sf[0];
-    at<Fp12>(g_blk, blockIdx.x) = sg[0];
-  }
+  if (lane == 0) at<Fp12>(f_blk, blockIdx.x) = sf[0];
 }
 }  // namespace
 
 extern "C" int dx_rp_verify_fold(void *stream, const uint32_t *ZB_jac, const uint32_t *Y_jac, const uint32_t *rho,
-                                 const uint32_t *V_aff, const uint32_t *a, uint32_t *f_blk, uint32_t *g_blk,
-                                 int64_t n_items, int S, int L) {
+                                 const uint32_t *V_aff, uint32_t *f_blk, int64_t n_items, int S, int L) {
   if (n_items <= 0) return 0;
   int64_t blocks = (n_items + kVW - 1) / kVW;
   hipLaunchKernelGGL(rp_verify_fold_kernel, dim3((unsigned)blocks), dim3(kVW), 0, (hipStream_t)stream, ZB_jac, Y_jac,
-                     rho, V_aff, a, f_blk, g_blk, n_items, S, L);
+                     rho, V_aff, f_blk, n_items, S, L);
   return check_hip(hipGetLastError(), "rp_verify_fold");
+}
+
+// Segmented GT products (bucket accumulation of a multi-exponentiation):
+//   out[s] = prod_{k < len[s]} src[idx ? idx[start[s] + k] : start[s] + k]
+extern "C" int dx_gt_slice_prod(int on_gpu, void *stream, const uint32_t *src, const int64_t *idx,
+                                const int64_t *start, const int32_t *len, uint32_t *out, int64_t n_slices) {
+  auto op = [=] __host__ __device__(int64_t s) {
+    const int64_t b = start[s];
+    const int n = len[s];
+    Fp12 acc = Fp12::one();
+    for (int k = 0; k < n; k++) acc = mul(acc, at<Fp12>(src, idx ? idx[b + k] : b + k));
+    at<Fp12>(out, s) = acc;
+  };
+  return run(on_gpu, stream, n_slices, op, true, "gt_slice_prod");
 }

@@ -5,8 +5,12 @@
 #include <hip/hip_runtime.h>
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
+#include <functional>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -29,35 +33,87 @@ __global__ void __launch_bounds__(64) for_each_kernel64(int64_t n, Op op) {
 inline int host_threads() {
   static int nt = [] {
     const char *e = getenv("DX_NUM_THREADS");
+    if (!e) e = getenv("OMP_NUM_THREADS");  // the box's CPU share (16 on a 1-GPU box)
     int v = e ? atoi(e) : (int)std::thread::hardware_concurrency();
     if (v <= 0) v = 1;
-    return std::min(v, 64);
+    return std::min(v, 32);
   }();
   return nt;
 }
 
+// Persistent host worker pool (the host path of every batched op, and the
+// short serial tails -- GT product trees, final exponentiations -- that the
+// device hands back).  One job at a time; a caller that finds the pool busy
+// (another Python thread's op) runs its job inline instead of waiting.
+class HostPool {
+ public:
+  static HostPool &get() {
+    static HostPool *p = new HostPool(host_threads() - 1);  // never destroyed: workers outlive static teardown
+    return *p;
+  }
+  template <class Op>
+  void for_each(int64_t n, const Op &op) {
+    const int64_t chunk = std::max<int64_t>(1, n / ((int64_t)(workers_.size() + 1) * 8));
+    std::unique_lock<std::mutex> busy(job_mu_, std::try_to_lock);
+    if (!busy.owns_lock() || workers_.empty() || n < 4) {
+      for (int64_t i = 0; i < n; i++) op(i);
+      return;
+    }
+    std::atomic<int64_t> next{0};
+    auto body = [&] {
+      for (;;) {
+        int64_t s = next.fetch_add(chunk);
+        if (s >= n) break;
+        int64_t e = std::min(n, s + chunk);
+        for (int64_t i = s; i < e; i++) op(i);
+      }
+    };
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      job_ = body;
+      pending_ = (int)workers_.size();
+      gen_++;
+    }
+    cv_.notify_all();
+    body();
+    std::unique_lock<std::mutex> g(mu_);
+    done_cv_.wait(g, [&] { return pending_ == 0; });
+    job_ = nullptr;
+  }
+
+ private:
+  explicit HostPool(int n) {
+    for (int t = 0; t < n; t++) workers_.emplace_back([this] { loop(); });
+    for (auto &w : workers_) w.detach();
+  }
+  void loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      std::function<void()> job;
+      {
+        std::unique_lock<std::mutex> g(mu_);
+        cv_.wait(g, [&] { return gen_ != seen; });
+        seen = gen_;
+        job = job_;
+      }
+      if (job) job();
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        if (--pending_ == 0) done_cv_.notify_all();
+      }
+    }
+  }
+  std::vector<std::thread> workers_;
+  std::mutex job_mu_, mu_;
+  std::condition_variable cv_, done_cv_;
+  std::function<void()> job_;
+  uint64_t gen_ = 0;
+  int pending_ = 0;
+};
+
 template <class Op>
 void host_for_each(int64_t n, const Op &op) {
-  int nt = host_threads();
-  if (n < 2 || nt == 1) {
-    for (int64_t i = 0; i < n; i++) op(i);
-    return;
-  }
-  std::atomic<int64_t> next{0};
-  const int64_t chunk = std::max<int64_t>(1, n / (nt * 8));
-  auto worker = [&] {
-    for (;;) {
-      int64_t s = next.fetch_add(chunk);
-      if (s >= n) break;
-      int64_t e = std::min(n, s + chunk);
-      for (int64_t i = s; i < e; i++) op(i);
-    }
-  };
-  std::vector<std::thread> th;
-  int use = (int)std::min<int64_t>(nt, (n + chunk - 1) / chunk);
-  for (int t = 1; t < use; t++) th.emplace_back(worker);
-  worker();
-  for (auto &t : th) t.join();
+  HostPool::get().for_each(n, op);
 }
 
 inline int check_hip(hipError_t e, const char *what) {

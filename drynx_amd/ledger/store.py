@@ -48,22 +48,20 @@ class Store:
         self.closed = False
 
     # ------------------------------------------------------------- values / blob segment
-    @staticmethod
-    def _as_bytes(value):
-        if hasattr(value, "cpu") and hasattr(value, "numpy"):  # a (device) tensor
-            return value.detach().cpu().contiguous().numpy().tobytes()
-        return bytes(value)
-
     def _encode(self, value) -> bytes:
-        """Caller holds the lock."""
-        b = self._as_bytes(value)
-        if len(b) < BLOB_MIN:
-            return b
+        """Caller holds the lock.  Large values are written straight from the
+        host buffer (no bytes() copy under the GIL)."""
+        if hasattr(value, "cpu") and hasattr(value, "numpy"):
+            buf = memoryview(value.detach().cpu().contiguous().numpy()).cast("B")
+        else:
+            buf = memoryview(value).cast("B") if not isinstance(value, bytes) else memoryview(value)
+        if buf.nbytes < BLOB_MIN:
+            return buf.tobytes()
         if self._blob_f is None:
             self._blob_f = open(self.blob_path, "ab")
         off = self._blob_f.seek(0, os.SEEK_END)
-        self._blob_f.write(b)
-        return _REF + struct.pack("<QQ", off, len(b))
+        self._blob_f.write(buf)
+        return _REF + struct.pack("<QQ", off, buf.nbytes)
 
     def _decode(self, v) -> bytes:
         v = bytes(v)

@@ -83,7 +83,8 @@ _SIGS = {
     "dx_sha256_chunks": [_I, _P, _P, _L, _L, _P],
     "dx_lr_encode": [_P, _P, _L, _L, _I, _P, _P, _P, ctypes.c_double, ctypes.c_double, _P, _I],
     "dx_g1_mul_fast": [_P, _P, _P, _P, _L, _I, _I],
-    "dx_rp_verify_fold": [_P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _I],
+    "dx_rp_verify_fold": [_P, _P, _P, _P, _P, _P, _L, _I, _I],
+    "dx_gt_slice_prod": [_I, _P, _P, _P, _P, _P, _P, _L],
     "dx_rp_prove_a": [_I, _P, _P, _P, _P, _P, _P, _L, _I, _I],
     "dx_rp_prove_a_tab": [_I, _P, _P, _P, _P, _P, _P, _P, _L, _I, _I],
     "dx_rp_verify_items": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _I],
@@ -532,32 +533,135 @@ def rp_verify_items(ZB_jac, Y_jac, rho, V_aff, a, S: int, L: int):
 
 
 def rp_verify_products(ZB_jac, Y_jac, rho, V_aff, a, S: int, L: int):
-    """(prod_it ML_it, prod_it a_it^rho_it) as two [1, 96] tensors.  GPU: the
-    fused kernel folds each 64-item workgroup in LDS, then a short product tree
-    over the workgroup partials; host: per-item values + product tree."""
+    """(prod_it ML_it, prod_it a_it^rho_it) as two [1, 96] HOST tensors.
+    GPU: the Miller values fold per 64-item workgroup in LDS (dx_rp_verify_fold)
+    and the a^rho product is a bucket multi-exponentiation (gt_multi_exp64);
+    host: per-item values + product tree."""
     g, s = _ctx(ZB_jac, Y_jac, rho, V_aff, a)
     if not g:
         f, gg = rp_verify_items(ZB_jac, Y_jac, rho, V_aff, a, S, L)
         return gt_prod(f.view(-1, 1, 96), chunk=4).view(1, 96), gt_prod(gg.view(-1, 1, 96), chunk=4).view(1, 96)
     n = _rows(V_aff, 32)
+    plan = _multi_exp64_plan(rho)  # index work first: its one host sync does not wait for the Miller fold
     nb = (n + 63) // 64
     fb = torch.empty((nb, 96), dtype=torch.int32, device=V_aff.device)
-    gb = torch.empty((nb, 96), dtype=torch.int32, device=V_aff.device)
-    rc = _load().dx_rp_verify_fold(s, _ptr(ZB_jac), _ptr(Y_jac), _ptr(rho), _ptr(V_aff), _ptr(a), _ptr(fb), _ptr(gb),
-                                   n, S, L)
+    rc = _load().dx_rp_verify_fold(s, _ptr(ZB_jac), _ptr(Y_jac), _ptr(rho), _ptr(V_aff), _ptr(fb), n, S, L)
     if rc:
         raise RuntimeError(f"dx_rp_verify_fold failed rc={rc}")
-    return _finish_prod_on_host(fb), _finish_prod_on_host(gb)
+    G = _multi_exp64_run(a, plan)
+    return _finish_prod_on_host(fb), G
+
+
+def gt_slice_prod(src: torch.Tensor, idx, start: torch.Tensor, length: torch.Tensor) -> torch.Tensor:
+    """out[s] = prod_k src[idx[start[s] + k]] (or src[start[s] + k]), k < length[s]."""
+    n = start.numel()
+    out = torch.empty((n, 96), dtype=torch.int32, device=src.device)
+    g, s = _ctx(src, idx, start, length)
+    _call("dx_gt_slice_prod", g, s, _ptr(src), _ptr(idx), _ptr(start), _ptr(length), _ptr(out), n)
+    return out
+
+
+_ME_C = 8          # window bits
+_ME_W = 64 // _ME_C
+_ME_SLICE = 8      # entries per thread in each segmented-product pass
+
+
+def _segment_passes(counts):
+    """Slice plans that reduce contiguous per-bucket runs of `counts` entries
+    to one product per bucket, <= _ME_SLICE factors per thread per pass (a
+    lone GPU lane runs an Fp12 chain latency-bound, so chains stay short and
+    each pass is wide).  Returns [(start, len), ...] numpy arrays per pass."""
+    import numpy as _np
+
+    passes = []
+    c = _np.asarray(counts, dtype=_np.int64)
+    while c.size and c.max() > 1:
+        n_sl = (c + _ME_SLICE - 1) // _ME_SLICE
+        first = _np.cumsum(c) - c
+        b = _np.repeat(_np.arange(c.size), n_sl)
+        k = _np.arange(b.size) - (_np.cumsum(n_sl) - n_sl)[b]
+        start = first[b] + k * _ME_SLICE
+        ln = _np.minimum(c[b] - k * _ME_SLICE, _ME_SLICE)
+        passes.append((start, ln))
+        c = n_sl
+    return passes
+
+
+def _multi_exp64_plan(rho: torch.Tensor):
+    """Bucket plan of prod_i a_i^{rho_i} for 64-bit exponents (limbs 0, 1 of
+    rho): window w, digit d -> bucket w*256+d; entries sorted by bucket, then
+    segmented-product passes down to one value per non-empty bucket."""
+    dev = rho.device
+    n = rho.shape[0]
+    digits = rho[:, :2].contiguous().view(torch.uint8).view(n, 8).to(torch.int64)   # little-endian bytes
+    keys = (torch.arange(_ME_W, device=dev).view(1, -1) * 256 + digits).reshape(-1)
+    item = torch.arange(n, device=dev).view(-1, 1).expand(n, _ME_W).reshape(-1)
+    keep = digits.reshape(-1) != 0
+    keys, item = keys[keep], item[keep]
+    keys, order = torch.sort(keys)
+    item = item[order].contiguous()
+    counts = torch.bincount(keys, minlength=_ME_W * 256).cpu().numpy()  # the one host sync
+    bk = counts.nonzero()[0]
+    passes = [(torch.from_numpy(st).to(dev), torch.from_numpy(ln.astype("int32")).to(dev))
+              for st, ln in _segment_passes(counts[bk])]
+    return {"item": item, "passes": passes, "bk": bk, "single": not passes}
+
+
+def _multi_exp64_run(a: torch.Tensor, plan) -> torch.Tensor:
+    """Finish prod a_i^{rho_i}: segmented passes -> bucket values B_{w,d} ->
+    B^d (GPU), then per-window products and the 8-window Horner combination
+    on the host (short serial Fp12 chains: one host core beats one GPU lane)."""
+    dev = a.device
+    bk = plan["bk"]
+    if bk.size == 0:
+        return gt_one("cpu").clone()
+    cur = a.index_select(0, plan["item"]).contiguous() if plan["single"] else None
+    for k, (st, ln) in enumerate(plan["passes"]):
+        cur = gt_slice_prod(a if k == 0 else cur, plan["item"] if k == 0 else None, st, ln)
+    sc = torch.zeros((bk.size, 8), dtype=torch.int32)
+    sc[:, 0] = torch.from_numpy((bk % 256).astype("int32"))
+    bkp = gt_pow(cur, sc.to(dev))
+    win = gt_one(dev).repeat(256 * _ME_W, 1)
+    win[torch.from_numpy((bk % 256) * _ME_W + bk // 256).to(dev)] = bkp
+    win = _gt_prod_level(win.view(256, _ME_W, 96), 8) if dev.type == "cuda" else win.view(256, _ME_W, 96)
+    S_w = gt_prod(win.cpu(), chunk=4)                                  # [W, 96] on the host
+    acc = S_w[_ME_W - 1: _ME_W].contiguous()
+    for w in range(_ME_W - 2, -1, -1):
+        acc = gt_pow(acc, _pow2_scalar(_ME_C))
+        acc = gt_mul(acc, S_w[w: w + 1].contiguous())
+    return acc
+
+
+_gt_one_cache: dict = {}
+
+
+def gt_one(device) -> torch.Tensor:
+    """Fp12 one (Montgomery limbs: c0.c0.c0 = R mod p)."""
+    key = str(device)
+    if key not in _gt_one_cache:
+        import numpy as _np
+
+        from ..crypto import bn254 as _bn
+
+        t = _np.zeros((1, 96), dtype=_np.uint32)
+        t[0, :8] = _bn.ints_to_limbs([_bn.mont(1)])[0]
+        _gt_one_cache[key] = _bn.to_tensor(t, device)
+    return _gt_one_cache[key]
+
+
+def _pow2_scalar(c: int) -> torch.Tensor:
+    t = torch.zeros((1, 8), dtype=torch.int32)
+    t[0, c // 32] = 1 << (c % 32)
+    return t
 
 
 def _finish_prod_on_host(parts: torch.Tensor) -> torch.Tensor:
-    """Product of [n, 96] GT partials: wide GPU levels while n > 64, then the
-    short serial tail on the host (a lone GPU lane runs an Fp12 chain ~10x
-    slower than one host core).  Returns a [1, 96] HOST tensor."""
+    """Product of [n, 96] GT partials: 8-way GPU levels while n > 256, then the
+    rest on the host pool (a lone GPU lane runs an Fp12 chain latency-bound,
+    ~30x slower than one host core).  Returns a [1, 96] HOST tensor."""
     cur = parts.view(-1, 1, 96)
-    while cur.shape[0] > 64:
-        ch = min(32, max(2, (cur.shape[0] + 63) // 64))
-        cur = _gt_prod_level(cur, ch)
+    while cur.shape[0] > 256:
+        cur = _gt_prod_level(cur, 8)
     return gt_prod(cur.cpu(), chunk=4).view(1, 96)
 
 

@@ -107,3 +107,20 @@ def test_wire_codecs_match_oracle():
 def test_random_scalars_in_range():
     s = bn.scalars_from_tensor(bn.random_scalars(500))
     assert all(0 < v < O.R for v in s) and len(set(s)) == 500
+
+
+def test_gt_bucket_multi_exp64_matches_direct():
+    """prod a_i^{rho_i} (64-bit rho) through the bucket plan == per-item powers."""
+    import os
+
+    import numpy as np
+
+    x = nt.pairing(bn.g1_generator_aff("cpu"), bn.g2_generator_aff("cpu"))
+    n = 200
+    a = nt.gt_pow(x, bn.random_scalars(n))
+    rho = torch.zeros((n, 8), dtype=torch.int32)
+    rho[:, :2] = torch.from_numpy(np.frombuffer(os.urandom(8 * n), dtype="<i4").reshape(n, 2).copy())
+    rho[:7, :2] = 0  # all-zero digits: items contribute nothing
+    got = nt._multi_exp64_run(a, nt._multi_exp64_plan(rho))
+    ref = nt.gt_prod(nt.gt_pow(a, rho).view(-1, 1, 96), chunk=4).view(1, 96)
+    assert torch.equal(got, ref)
