@@ -188,7 +188,9 @@ def init_distributed(backend: str | None = None):
     if world <= 1:
         return
     if backend is None:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        # DRYNX_DIST_BACKEND=gloo rehearses the multi-rank GPU path with several
+        # ranks sharing one GPU (RCCL needs one GPU per rank)
+        backend = os.environ.get("DRYNX_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
     if backend == "nccl":
         local = int(os.environ.get("LOCAL_RANK", "0"))
         torch.cuda.set_device(local)

@@ -173,8 +173,31 @@ def assigned_vns(sq, req: ProofRequest, n_vns: int):
     shard = int(getattr(sq, "VerificationSharding", 0) or 0)
     if shard <= 0 or n_vns <= 0:
         return None
+    if req.kind == "range":
+        # the heavy lists are balanced: DP number k -> VNs k+1 .. k+shard
+        # (round robin over the survey's DP order, offset by one so a VN placed
+        # with its DP on the same rank/GPU never checks that DP's proofs)
+        order = _dp_order(sq)
+        if req.sender_id in order:
+            k = order[req.sender_id]
+            return {(k + 1 + j) % n_vns for j in range(min(shard, n_vns))}
     h = int.from_bytes(hashlib.sha256(req.base_key().encode()).digest()[:8], "little")
     return {(h + k) % n_vns for k in range(min(shard, n_vns))}
+
+
+def _dp_order(sq) -> dict:
+    """DP id -> position in the survey's (broadcast, hence rank-consistent) DP roster."""
+    cache = getattr(sq, "_dp_order_cache", None)
+    if cache is None:
+        ids = []
+        for dps in (sq.ServerToDP or {}).values():
+            ids += [si.id for si in (dps or [])]
+        cache = {d: i for i, d in enumerate(ids)}
+        try:
+            sq._dp_order_cache = cache
+        except AttributeError:
+            pass
+    return cache
 
 
 def should_verify(sq, req: ProofRequest, vn_index: int, n_vns: int) -> bool:

@@ -57,7 +57,7 @@ def fan_out(ctx, sq, local_requests: list) -> list:
                 per_rank[d].append(r.header().to_wire())
             elif r.kind == "range" and r.obj is not None and d != ctx.rank:
                 if idx not in packed:
-                    packed[idx] = prq.range_bundle_pack(r.obj).to(ctx.device)
+                    packed[idx] = (r.tensor if r.tensor is not None else prq.range_bundle_pack(r.obj)).to(ctx.device)
                 w = r.header().to_wire()
                 w["digest"], w["tensor"] = b"", packed[idx].numel()
                 per_rank[d].append(w)
