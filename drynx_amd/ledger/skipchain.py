@@ -9,10 +9,12 @@ data)`` :498-505) or appends (:507-525).  Every VN's custom verifier
 VN's own DB.
 
 Here a block is hash-linked (SHA-256 over index, back link, roster and data)
-and carries a forward-link signature from every VN of the roster (Schnorr over
-the block hash) — each VN signs only after its bitmap verifier accepted the
-block.  (Cothority's BLS collective signature is replaced by the list of
-per-VN Schnorr signatures; documented simplification.)
+and carries a BLS collective signature of the VN roster over the block hash
+(BDN aggregation, crypto/bls.py, like cothority's BLS CoSi): each VN adds its
+partial signature only after its bitmap verifier accepted the block; the
+aggregate and the participation mask are stored in ``CoSig`` and checked with
+one pairing product.  Roster entries without a BLS key fall back to per-VN
+Schnorr signatures.
 """
 from __future__ import annotations
 
@@ -21,6 +23,9 @@ import json
 import time
 from dataclasses import dataclass, field
 
+import math
+
+from ..crypto import bls
 from ..crypto import oracle as O
 from ..proofs.sigma import schnorr_sign, schnorr_verify
 
@@ -53,8 +58,9 @@ class SkipBlock:
     BackLink: str                # hex hash of previous block ("" for genesis)
     VerifierIDs: list
     Hash: str = ""
-    ForwardSignatures: dict = field(default_factory=dict)  # vn id -> signature hex
+    ForwardSignatures: dict = field(default_factory=dict)  # vn id -> partial signature hex
     GenesisID: str = ""
+    CoSig: str = ""              # "<aggregate G1 hex>/<mask>" (BLS collective signature)
 
     def compute_hash(self) -> str:
         h = hashlib.sha256()
@@ -79,18 +85,45 @@ class SkipBlock:
     def data_block(self) -> DataBlock:
         return DataBlock.from_bytes(self.Data)
 
-    def verify_signatures(self, publics: dict) -> bool:
+    def bls_keys(self):
+        if not self.Roster or not all(vn.get("bls") for vn in self.Roster):
+            return None
+        return [O.g2_from_bytes(bytes.fromhex(vn["bls"])) for vn in self.Roster]
+
+    def verify_signatures(self, publics: dict | None = None, threshold: float = 1.0) -> bool:
+        """Hash check + the roster's collective signature (at least
+        ceil(threshold * n) signers; default: every VN of the roster)."""
         if self.compute_hash() != self.Hash:
             return False
+        keys = self.bls_keys()
+        if keys is not None:
+            if not self.CoSig:
+                return False
+            agg_hex, mask_hex = self.CoSig.split("/")
+            mask = bls.mask_from_hex(mask_hex)
+            if len(mask) != len(keys) or sum(mask) < math.ceil(threshold * len(keys)):
+                return False
+            try:
+                sig = O.g1_from_bytes(bytes.fromhex(agg_hex))
+            except ValueError:
+                return False
+            return bls.verify_multi(keys, mask, bytes.fromhex(self.Hash), sig)
         for vn in self.Roster:
             sig = self.ForwardSignatures.get(vn["id"])
-            if sig is None or not schnorr_verify(publics[vn["id"]], bytes.fromhex(self.Hash), bytes.fromhex(sig)):
+            if sig is None or publics is None or \
+                    not schnorr_verify(publics[vn["id"]], bytes.fromhex(self.Hash), bytes.fromhex(sig)):
                 return False
         return True
 
 
 def roster_json(identities) -> list:
-    return [{"id": si.id, "public": O.g1_to_bytes(si.public).hex()} for si in identities]
+    out = []
+    for si in identities:
+        e = {"id": si.id, "public": O.g1_to_bytes(si.public).hex()}
+        if getattr(si, "bls", None) is not None:
+            e["bls"] = O.g2_to_bytes(si.bls).hex()
+        out.append(e)
+    return out
 
 
 def new_data_block(survey_id: str, bitmap: dict, vn_identities, sample: float = 0.4) -> DataBlock:
@@ -116,4 +149,25 @@ def verify_bitmap(sb: SkipBlock, local_bitmap: dict, vn_address: str) -> bool:
 
 
 def sign_block(sb: SkipBlock, vn_id: str, secret: int):
-    sb.ForwardSignatures[vn_id] = schnorr_sign(secret, bytes.fromhex(sb.Hash)).hex()
+    """A VN's forward-link contribution: BLS partial signature of the block
+    hash (Schnorr when the roster carries no BLS keys)."""
+    if sb.bls_keys() is not None:
+        sb.ForwardSignatures[vn_id] = O.g1_to_bytes(bls.sign(secret, bytes.fromhex(sb.Hash))).hex()
+    else:
+        sb.ForwardSignatures[vn_id] = schnorr_sign(secret, bytes.fromhex(sb.Hash)).hex()
+
+
+def finalize_cosig(sb: SkipBlock):
+    """Aggregate the partial signatures present into CoSig (BDN coefficients
+    over the whole roster; the mask records who signed)."""
+    keys = sb.bls_keys()
+    if keys is None:
+        return
+    partials, mask = {}, []
+    for i, vn in enumerate(sb.Roster):
+        s = sb.ForwardSignatures.get(vn["id"])
+        mask.append(s is not None)
+        if s is not None:
+            partials[i] = O.g1_from_bytes(bytes.fromhex(s))
+    agg = bls.aggregate(keys, partials)
+    sb.CoSig = (O.g1_to_bytes(agg).hex() if agg is not None else "") + "/" + bls.mask_to_hex(mask)

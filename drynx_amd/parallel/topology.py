@@ -12,6 +12,7 @@ from __future__ import annotations
 
 from dataclasses import dataclass, field
 
+from ..crypto import bls
 from ..crypto import oracle as O
 from ..crypto.elgamal import KeyPair
 from ..query import Roster, ServerIdentity
@@ -24,9 +25,10 @@ class Party:
     rank: int
     public: tuple = None
     keypair: KeyPair = None  # only set on the hosting rank
+    bls_public: tuple = None  # VNs: G2 key of the skipchain collective signature
 
     def identity(self) -> ServerIdentity:
-        return ServerIdentity(self.id, self.public, f"rank{self.rank}/{self.id}", self.rank)
+        return ServerIdentity(self.id, self.public, f"rank{self.rank}/{self.id}", self.rank, self.bls_public)
 
 
 @dataclass
@@ -91,6 +93,9 @@ def build_cluster(n_cns: int, n_dps: int, n_vns: int, world: int = 1, rank: int 
             p.keypair = KeyPair.from_secret(1000 + i) if deterministic_keys else KeyPair.generate()
             p.public = p.keypair.public
             local_pub[p.id] = O.g1_to_bytes(p.public)
+            if p.role == "vn":
+                p.bls_public = bls.public_key(p.keypair.secret)
+                local_pub[p.id + "#bls"] = O.g2_to_bytes(p.bls_public)
     if comm is not None and comm.world > 1:
         allpub = {}
         for d in comm.all_gather_object(local_pub):
@@ -100,4 +105,6 @@ def build_cluster(n_cns: int, n_dps: int, n_vns: int, world: int = 1, rank: int 
     for p in cl.parties:
         if p.public is None:
             p.public = O.g1_from_bytes(allpub[p.id])
+        if p.bls_public is None and p.id + "#bls" in allpub:
+            p.bls_public = O.g2_from_bytes(allpub[p.id + "#bls"])
     return cl

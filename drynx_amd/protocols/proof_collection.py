@@ -141,6 +141,7 @@ def proof_collection(ctx, sq, local_requests: list):
                 log.warning(f"{vn.id} refused block for survey {sq.SurveyID}")
     for d in ctx.comm.all_gather_object(sigs):
         block.ForwardSignatures.update(d)
+    skc.finalize_cosig(block)  # BLS collective signature of the VN roster
     for vn in vns:
         if vn.rank == ctx.rank:
             # proof blobs keep persisting on the store's writer thread (GetProofs /

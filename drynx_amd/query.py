@@ -34,15 +34,20 @@ class ServerIdentity:
     public: Optional[tuple] = None  # G1 affine (oracle) point
     address: str = ""
     rank: int = 0
+    bls: Optional[tuple] = None     # G2 BLS key (verifying nodes: skipchain collective signature)
 
     def to_dict(self):
-        return {"id": self.id, "public": O.g1_to_bytes(self.public).hex() if self.public else None,
-                "address": self.address, "rank": self.rank}
+        d = {"id": self.id, "public": O.g1_to_bytes(self.public).hex() if self.public else None,
+             "address": self.address, "rank": self.rank}
+        if self.bls is not None:
+            d["bls"] = O.g2_to_bytes(self.bls).hex()
+        return d
 
     @staticmethod
     def from_dict(d):
         pub = O.g1_from_bytes(bytes.fromhex(d["public"])) if d.get("public") else None
-        return ServerIdentity(d["id"], pub, d.get("address", ""), d.get("rank", 0))
+        b = O.g2_from_bytes(bytes.fromhex(d["bls"])) if d.get("bls") else None
+        return ServerIdentity(d["id"], pub, d.get("address", ""), d.get("rank", 0), b)
 
     def __hash__(self):
         return hash(self.id)
