@@ -1,0 +1,26 @@
+# Build / test entry points (reference: Makefile + .travis.yml — build the
+# cmd/ binaries, run the test suite).
+PY ?= python
+
+.PHONY: build test test-gpu bench smoke simul clean
+
+build:            ## compile every HIP translation unit for gfx950 into drynx_amd/native/libdrynx_native.so
+	$(PY) -m drynx_amd.native.build
+
+test: build       ## CPU suite (host path of the same kernels, gloo multi-rank)
+	$(PY) -m pytest tests -m "not gpu" -q -n 4
+
+test-gpu: build   ## on an MI355X
+	$(PY) -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
+
+bench: build      ## headline benchmark, 1 GPU (N GPUs: torch.distributed.run ... bench.py --gpus N)
+	$(PY) bench.py --steps 3 --warmup 1
+
+smoke: build
+	$(PY) -c "import __graft_entry__ as g; g.smoke()"
+
+simul: build      ## onet-style runfile simulation with named-timer CSV
+	$(PY) -m drynx_amd.simul.simul drynx_amd/simul/runfiles/drynx.toml --csv timers.csv
+
+clean:
+	rm -rf build drynx_amd/native/libdrynx_native.so drynx_amd/native/libdrynx_native.so.stamp

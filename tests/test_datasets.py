@@ -44,3 +44,17 @@ def test_pima_training_converges():
     m, s = lr.compute_means_sds(X)
     Xt, yt = lr.load_csv_dataset(os.path.join(REF, "data/Pima_dataset_testing.txt"))
     assert lr.metrics(lr.predict(Xt, w, m, s), yt)["accuracy"] > 0.7
+
+
+def test_clean_data_pcs_and_gas(tmp_path):
+    from drynx_amd.models import datasets as ds
+
+    X, y, dropped = ds.clean_rows("PCS", ["7,1,2,3,4,5,6,7,8,9,0,11,12", "8,a,2,3,4,5,6,7,8,9,0,11,12"])
+    # index col 0 dropped -> label is the old column 1; cols 10, 11 dropped
+    assert y == [1] and X == [[2.0, 3.0, 4.0, 5.0, 6.0, 7.0, 8.0, 9.0, 12.0]] and dropped == 1
+    X, y, _ = ds.clean_rows("GAS_SENSOR_MULTI", ["3,1:0.5,2:1.5"], float)
+    assert y == [3.0] and X == [[0.5, 1.5]]
+    p = tmp_path / "m.txt"
+    p.write_text("1,0,255\n")
+    ds.clean_file("MNIST", str(p))
+    assert p.read_text().strip().split(",")[0] == "1" and abs(float(p.read_text().split(",")[2]) - 1.0) < 1e-12
