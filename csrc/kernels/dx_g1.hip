@@ -138,6 +138,20 @@ int dx_g1_sum_chunks(int on_gpu, void *stream, const uint32_t *in, uint32_t *out
   return run(on_gpu, stream, n_chunks * n_groups, op, true, "g1_sum_chunks");
 }
 
+// Segmented Jacobian sums (bucket accumulation of a multi-scalar multiplication):
+//   out[s] = sum_{k < len[s]} src[idx ? idx[start[s] + k] : start[s] + k]
+int dx_g1_slice_sum(int on_gpu, void *stream, const uint32_t *src, const int64_t *idx, const int64_t *start,
+                    const int32_t *len, uint32_t *out, int64_t n_slices) {
+  auto op = [=] __host__ __device__(int64_t s) {
+    const int64_t b = start[s];
+    const int n = len[s];
+    G1J acc = G1J::inf();
+    for (int k = 0; k < n; k++) acc = jadd(acc, at<G1J>(src, idx ? idx[b + k] : b + k));
+    at<G1J>(out, s) = acc;
+  };
+  return run(on_gpu, stream, n_slices, op, true, "g1_slice_sum");
+}
+
 // ---------------------------------------------------------------- ElGamal
 // K = r*B, C = m*B + r*P  (unlynx EncryptIntGetR with caller-provided r)
 int dx_elgamal_encrypt(int on_gpu, void *stream, const uint32_t *tabB, const uint32_t *tabP, const int64_t *m,

@@ -18,6 +18,8 @@ from __future__ import annotations
 import ctypes
 import os
 
+import numpy as np
+
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -85,6 +87,7 @@ _SIGS = {
     "dx_g1_mul_fast": [_P, _P, _P, _P, _L, _I, _I],
     "dx_rp_verify_fold": [_P, _P, _P, _P, _P, _P, _L, _I, _I],
     "dx_gt_slice_prod": [_I, _P, _P, _P, _P, _P, _P, _L],
+    "dx_g1_slice_sum": [_I, _P, _P, _P, _P, _P, _P, _L],
     "dx_rp_prove_a": [_I, _P, _P, _P, _P, _P, _P, _L, _I, _I],
     "dx_rp_prove_a_tab": [_I, _P, _P, _P, _P, _P, _P, _P, _L, _I, _I],
     "dx_rp_verify_items": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _I],
@@ -588,19 +591,24 @@ def _segment_passes(counts):
 
 
 def _multi_exp64_plan(rho: torch.Tensor):
-    """Bucket plan of prod_i a_i^{rho_i} for 64-bit exponents (limbs 0, 1 of
-    rho): window w, digit d -> bucket w*256+d; entries sorted by bucket, then
-    segmented-product passes down to one value per non-empty bucket."""
-    dev = rho.device
-    n = rho.shape[0]
-    digits = rho[:, :2].contiguous().view(torch.uint8).view(n, 8).to(torch.int64)   # little-endian bytes
-    keys = (torch.arange(_ME_W, device=dev).view(1, -1) * 256 + digits).reshape(-1)
-    item = torch.arange(n, device=dev).view(-1, 1).expand(n, _ME_W).reshape(-1)
+    """Bucket plan of prod_i a_i^{rho_i} for 64-bit exponents (limbs 0, 1 of rho)."""
+    return _bucket_plan(rho, _ME_W)
+
+
+def _bucket_plan(k: torch.Tensor, W: int):
+    """Bucket plan of a multi-scalar product over the low W bytes of the
+    scalars k [n, 8]: window w, digit d -> bucket w*256+d; entries sorted by
+    bucket, then segmented passes down to one value per non-empty bucket."""
+    dev = k.device
+    n = k.shape[0]
+    digits = k.contiguous().view(torch.uint8).view(n, 32)[:, :W].to(torch.int64)   # little-endian bytes
+    keys = (torch.arange(W, device=dev).view(1, -1) * 256 + digits).reshape(-1)
+    item = torch.arange(n, device=dev).view(-1, 1).expand(n, W).reshape(-1)
     keep = digits.reshape(-1) != 0
     keys, item = keys[keep], item[keep]
     keys, order = torch.sort(keys)
     item = item[order].contiguous()
-    counts = torch.bincount(keys, minlength=_ME_W * 256).cpu().numpy()  # the one host sync
+    counts = torch.bincount(keys, minlength=W * 256).cpu().numpy()  # the one host sync
     bk = counts.nonzero()[0]
     passes = [(torch.from_numpy(st).to(dev), torch.from_numpy(ln.astype("int32")).to(dev))
               for st, ln in _segment_passes(counts[bk])]
@@ -630,6 +638,53 @@ def _multi_exp64_run(a: torch.Tensor, plan) -> torch.Tensor:
         acc = gt_pow(acc, _pow2_scalar(_ME_C))
         acc = gt_mul(acc, S_w[w: w + 1].contiguous())
     return acc
+
+
+def g1_slice_sum(src: torch.Tensor, idx, start: torch.Tensor, length: torch.Tensor) -> torch.Tensor:
+    """out[s] = sum_k src[idx[start[s] + k]] (or src[start[s] + k]), k < length[s] (Jacobian)."""
+    n = start.numel()
+    out = torch.empty((n, 24), dtype=torch.int32, device=src.device)
+    g, s = _ctx(src, idx, start, length)
+    _call("dx_g1_slice_sum", g, s, _ptr(src), _ptr(idx), _ptr(start), _ptr(length), _ptr(out), n)
+    return out
+
+
+def g1_msm(P_jac: torch.Tensor, k: torch.Tensor, bits: int = 256) -> torch.Tensor:
+    """sum_i k_i P_i (Pippenger bucket method, 8-bit windows) -> [1, 24] HOST
+    Jacobian point.  Buckets accumulate in wide segmented passes on the device
+    (no per-point 256-step doubling chain: the cost is ~bits/8 additions per
+    point), bucket weights d*B_{w,d} are one short variable-base launch, and
+    the 32-window Horner combination runs on the host pool."""
+    from ..crypto.bn254 import g1_infinity_jac
+
+    assert P_jac.shape[0] == k.shape[0]
+    dev = P_jac.device
+    W = (bits + 7) // 8
+    if P_jac.shape[0] == 0:
+        return g1_infinity_jac(1, "cpu")
+    plan = _bucket_plan(k, W)
+    bk = plan["bk"]
+    if bk.size == 0:
+        return g1_infinity_jac(1, "cpu")
+    P_jac = P_jac.contiguous()
+    cur = P_jac.index_select(0, plan["item"]).contiguous() if plan["single"] else None
+    for i, (st, ln) in enumerate(plan["passes"]):
+        cur = g1_slice_sum(P_jac if i == 0 else cur, plan["item"] if i == 0 else None, st, ln)
+    sc = torch.zeros((bk.size, 8), dtype=torch.int32)
+    sc[:, 0] = torch.from_numpy((bk % 256).astype("int32"))
+    weighted = g1_mul(cur, sc.to(dev))                                   # d * B_{w,d}
+    # per-window sums: buckets are sorted by key = w*256 + d, so windows are contiguous runs
+    w_of = bk // 256
+    wins, counts = np.unique(w_of, return_counts=True)
+    cur = weighted
+    for st, ln in _segment_passes(counts):
+        cur = g1_slice_sum(cur, None, torch.from_numpy(st).to(dev), torch.from_numpy(ln.astype("int32")).to(dev))
+    S_w = cur.cpu()                                                      # [len(wins), 24]
+    sh = torch.zeros((len(wins), 8), dtype=torch.int32)
+    for j, w in enumerate(wins.tolist()):
+        sh[j, (8 * w) // 32] = 1 << ((8 * w) % 32)
+    T = g1_mul(S_w.contiguous(), sh)                                     # 2^{8w} S_w on the host pool
+    return g1_sum(T.view(-1, 1, 24)).view(1, 24)
 
 
 _gt_one_cache: dict = {}

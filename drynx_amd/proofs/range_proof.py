@@ -459,10 +459,16 @@ def verify_range_proof_list(rpl: RangeProofList, sigmat: SigMaterial, P_point, t
         Cp = nt.g1_add(Cp, nt.g1_fb_mul_i64(tabB, torch.tensor(r.offset, dtype=torch.int64, device=device)))
     uj = _powers(u, l, device).repeat(n, 1)
     z = _fr_sum_rows(nt.fr_arith(nt.FR_MUL, r.zphi, uj), n)
-    lhs = nt.g1_add(nt.g1_add(nt.g1_mul(Cp.contiguous(), r.challenge), nt.g1_fb_mul(tabP, r.zr)),
-                    nt.g1_fb_mul(tabB, z))
+    # all n D-equations as one random linear combination (weights w_p, 64 bit):
+    #   sum w c C' + (sum w Zr) P + (sum w z) B - sum w D == O   -- one Pippenger MSM
     with timers.span("rp.verify.dcheck"):
-        if not bool(nt.g1_eq(lhs, r.D).all()):
+        w = _rand64(n, device)
+        negD = nt.g1_add(bn.g1_infinity_jac(n, device), r.D.contiguous(), subtract=True)
+        pts = torch.cat([Cp.contiguous(), negD, bn.g1_jac_tensor([P_point, O.G1_GEN], device)])
+        sc = torch.cat([nt.fr_arith(nt.FR_MUL, w, r.challenge), w,
+                        _fr_sum_rows(nt.fr_arith(nt.FR_MUL, w, r.zr), 1),
+                        _fr_sum_rows(nt.fr_arith(nt.FR_MUL, w, z), 1)])
+        if bool(nt.g1_msm(pts.contiguous(), sc.contiguous())[0, 16:24].any()):
             return False
     # --- pairing equations, randomly combined
     ZB = nt.g1_fb_mul(tabB, r.zphi)                                  # [n*l]

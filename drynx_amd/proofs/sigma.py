@@ -41,28 +41,62 @@ def fs_challenge(context: str, *parts) -> int:
     """SHA-256 Fiat–Shamir challenge over the context and the affine encodings
     of every point: all point tensors are normalised in ONE batched launch
     (a transcript is 4-7 vectors of thousands of points)."""
-    h = hashlib.sha256()
-    h.update(context.encode())
-    jacs, layout = [], []
-    for p in parts:
-        if isinstance(p, torch.Tensor):
-            jacs.append(p.contiguous().view(-1, 24))
-            layout.append(("pts", jacs[-1].shape[0]))
-        elif isinstance(p, CipherVector):
-            for t in (p.K, p.C):
-                jacs.append(t.contiguous().view(-1, 24))
+    return fs_challenges([(context, parts)])[0]
+
+
+def fs_challenges(specs) -> list:
+    """Challenges of several transcripts [(context, parts), ...] with ONE
+    to_affine launch for all their points (short vectors are latency-bound)."""
+    jacs, layouts = [], []
+    for context, parts in specs:
+        layout = [("raw", context.encode())]
+        for p in parts:
+            if isinstance(p, torch.Tensor):
+                jacs.append(p.contiguous().view(-1, 24))
                 layout.append(("pts", jacs[-1].shape[0]))
-        else:
-            layout.append(("raw", p if isinstance(p, (bytes, bytearray)) else str(p).encode()))
+            elif isinstance(p, CipherVector):
+                for t in (p.K, p.C):
+                    jacs.append(t.contiguous().view(-1, 24))
+                    layout.append(("pts", jacs[-1].shape[0]))
+            else:
+                layout.append(("raw", p if isinstance(p, (bytes, bytearray)) else str(p).encode()))
+        layouts.append(layout)
     allb = _aff_bytes(torch.cat(jacs)) if jacs else b""
-    o = 0
-    for kind, v in layout:
-        if kind == "pts":
-            h.update(allb[o: o + 64 * v])
-            o += 64 * v
-        else:
-            h.update(v)
-    return int.from_bytes(h.digest(), "big") % O.R
+    out, o = [], 0
+    for layout in layouts:
+        h = hashlib.sha256()
+        for kind, v in layout:
+            if kind == "pts":
+                h.update(allb[o: o + 64 * v])
+                o += 64 * v
+            else:
+                h.update(v)
+        out.append(int.from_bytes(h.digest(), "big") % O.R)
+    return out
+
+
+def _rand64(n: int, device) -> torch.Tensor:
+    """Random nonzero 64-bit batch weights (device CSPRNG), unknown to provers."""
+    r = bn.random_scalars(n, device)
+    r[:, 2:] = 0
+    r[:, 0] |= 1
+    return r
+
+
+def _msm_is_zero(points: list, scalars: list) -> bool:
+    """sum_i k_i P_i == O over the concatenated lists (one Pippenger MSM)."""
+    res = nt.g1_msm(torch.cat(points).contiguous(), torch.cat(scalars).contiguous())
+    return not bool(res[0, 16:24].any())
+
+
+def _fr_sum(x: torch.Tensor) -> torch.Tensor:
+    """[m, 8] -> [1, 8] Fr sum (pairwise tree on the device)."""
+    cur = x
+    while cur.shape[0] > 1:
+        if cur.shape[0] % 2:
+            cur = torch.cat([cur, torch.zeros((1, 8), dtype=torch.int32, device=cur.device)])
+        cur = nt.fr_arith(nt.FR_ADD, cur[0::2].contiguous(), cur[1::2].contiguous())
+    return cur
 
 
 def _sc(vals, device):
@@ -270,80 +304,88 @@ def key_switch_list_proof_creation(x: int, X, Q_point, K: torch.Tensor, share: C
 
 
 def key_switch_batch_verification(proofs: list, threshold: float = 1.0) -> list:
-    """Verify several CNs' key-switch proofs (same querier key) with ONE
-    variable-base launch for all of them (the vectors are short, so one launch
-    per proof would be latency-bound)."""
-    from ..crypto.elgamal import pk_table
-
+    """Verify several CNs' key-switch proofs (same querier key) as ONE random
+    linear combination: with fresh 64-bit weights rho_i, sig_i per element,
+      (sum rho za) B + (sum sig za) Q - sum rho T1 - sum c rho (vB)
+        - sum zb sig K - sum sig T2 - sum c sig (vQ - xK) == O
+    is one Pippenger MSM (no per-element 256-step chains; soundness error
+    2^-64).  If the combined check fails, each proof is re-checked alone so the
+    bitmap blames exactly the bad ones."""
     if not proofs:
         return []
-    ok = []
-    live = []
-    for pr in proofs:
-        n = pr.K.shape[0]
-        k = _first(n, threshold)
-        c = fs_challenge("proofTest/keyswitch", O.g1_to_bytes(pr.X), O.g1_to_bytes(pr.Q), pr.K, pr.share, pr.T1,
-                         pr.T2, pr.T3)
+    cs = fs_challenges([("proofTest/keyswitch", (O.g1_to_bytes(pr.X), O.g1_to_bytes(pr.Q), pr.K, pr.share, pr.T1,
+                                                 pr.T2, pr.T3)) for pr in proofs])
+    ok, live = [], []
+    for pr, c in zip(proofs, cs):
+        k = _first(pr.K.shape[0], threshold)
         good = c == pr.c and bn.g1_mul_point(pr.zb) == O.g1_add(O.g1_from_bytes(pr.T3), bn.g1_mul_point(c, pr.X))
         ok.append(good)
         if good and k > 0:
             live.append((len(ok) - 1, pr, k))
     if not live:
         return ok
-    dev = live[0][1].K.device
-    tabB = bn.base_table(dev)
-    tabQ = pk_table(live[0][1].Q, dev).tabP
-    za = torch.cat([pr.za[:k] for _, pr, k in live]).contiguous()
-    c_rep = torch.cat([_sc([pr.c], dev).expand(k, 8) for _, pr, k in live])
-    zb_rep = torch.cat([_sc([pr.zb], dev).expand(k, 8) for _, pr, k in live])
-    shK = torch.cat([pr.share.K[:k] for _, pr, k in live])
-    shC = torch.cat([pr.share.C[:k] for _, pr, k in live])
-    Ks = torch.cat([pr.K[:k] for _, pr, k in live])
-    T1 = torch.cat([pr.T1[:k] for _, pr, k in live]).contiguous()
-    T2 = torch.cat([pr.T2[:k] for _, pr, k in live]).contiguous()
-    m = shK.shape[0]
-    prods = nt.g1_mul(torch.cat([shK, Ks, shC]).contiguous(), torch.cat([c_rep, zb_rep, c_rep]).contiguous())
-    fb = nt.g1_fb_mul(tabB, za)               # za B
-    fq = nt.g1_fb_mul(tabQ, za)               # za Q
-    ok1 = nt.g1_eq(fb, nt.g1_add(T1, prods[:m].contiguous()))
-    ok2 = nt.g1_eq(nt.g1_add(fq, prods[m:2 * m].contiguous(), subtract=True), nt.g1_add(T2, prods[2 * m:].contiguous()))
-    good = (ok1 & ok2).cpu()
-    o = 0
+    if _ks_combined(live):
+        return ok
     for idx, pr, k in live:
-        ok[idx] = bool(good[o: o + k].all())
-        o += k
+        ok[idx] = _ks_combined([(idx, pr, k)])
     return ok
 
 
+def _ks_combined(live) -> bool:
+    dev = live[0][1].K.device
+    pts, scs = [], []
+    sB, sQ = [], []
+    for _, pr, k in live:
+        rho, sig = _rand64(k, dev), _rand64(k, dev)
+        za = pr.za[:k].contiguous()
+        c, zb = _sc([pr.c], dev), _sc([pr.zb], dev)
+        neg = lambda t: nt.fr_arith(nt.FR_NEG, t)  # noqa: E731
+        pts += [pr.T1[:k], pr.share.K[:k], pr.K[:k], pr.T2[:k], pr.share.C[:k]]
+        scs += [neg(rho), neg(nt.fr_arith(nt.FR_MUL, rho, c)), neg(nt.fr_arith(nt.FR_MUL, sig, zb)), neg(sig),
+                neg(nt.fr_arith(nt.FR_MUL, sig, c))]
+        sB.append(_fr_sum(nt.fr_arith(nt.FR_MUL, rho, za)))
+        sQ.append(_fr_sum(nt.fr_arith(nt.FR_MUL, sig, za)))
+    Q = live[0][1].Q
+    pts += [bn.g1_jac_tensor([O.G1_GEN], dev), bn.g1_jac_tensor([Q], dev)]
+    scs += [_fr_sum(torch.cat(sB)), _fr_sum(torch.cat(sQ))]
+    return _msm_is_zero([p.contiguous() for p in pts], scs)
+
+
 def obfuscation_batch_verification(proofs: list, threshold: float = 1.0) -> list:
-    """Several CNs' obfuscation proofs, one variable-base launch for all."""
+    """Several CNs' obfuscation proofs as one random linear combination:
+      sum rho (z K - T1 - c Ko) + sum sig (z C - T2 - c Co) == O
+    (one MSM; per-proof re-check only if the combination fails)."""
+    if not proofs:
+        return []
+    cs = fs_challenges([("proofTest/obfuscation", (pr.C, pr.Co, pr.T)) for pr in proofs])
     ok, live = [], []
-    for pr in proofs:
+    for pr, c in zip(proofs, cs):
         k = _first(len(pr.C), threshold)
-        good = fs_challenge("proofTest/obfuscation", pr.C, pr.Co, pr.T) == pr.c
+        good = c == pr.c
         ok.append(good)
         if good and k > 0:
             live.append((len(ok) - 1, pr, k))
     if not live:
         return ok
-    dev = live[0][1].C.device
-    z = torch.cat([pr.z[:k] for _, pr, k in live])
-    c = torch.cat([_sc([pr.c], dev).expand(k, 8) for _, pr, k in live])
-    CK = torch.cat([pr.C.K[:k] for _, pr, k in live])
-    CC = torch.cat([pr.C.C[:k] for _, pr, k in live])
-    OK_ = torch.cat([pr.Co.K[:k] for _, pr, k in live])
-    OC = torch.cat([pr.Co.C[:k] for _, pr, k in live])
-    TK = torch.cat([pr.T.K[:k] for _, pr, k in live]).contiguous()
-    TC = torch.cat([pr.T.C[:k] for _, pr, k in live]).contiguous()
-    m = CK.shape[0]
-    prods = nt.g1_mul(torch.cat([CK, CC, OK_, OC]).contiguous(), torch.cat([z, z, c, c]).contiguous())
-    p = [prods[i * m:(i + 1) * m].contiguous() for i in range(4)]
-    good = (nt.g1_eq(p[0], nt.g1_add(TK, p[2])) & nt.g1_eq(p[1], nt.g1_add(TC, p[3]))).cpu()
-    o = 0
+    if _obf_combined(live):
+        return ok
     for idx, pr, k in live:
-        ok[idx] = bool(good[o: o + k].all())
-        o += k
+        ok[idx] = _obf_combined([(idx, pr, k)])
     return ok
+
+
+def _obf_combined(live) -> bool:
+    dev = live[0][1].C.device
+    pts, scs = [], []
+    for _, pr, k in live:
+        rho, sig = _rand64(k, dev), _rand64(k, dev)
+        z = pr.z[:k].contiguous()
+        c = _sc([pr.c], dev)
+        neg = lambda t: nt.fr_arith(nt.FR_NEG, t)  # noqa: E731
+        pts += [pr.C.K[:k], pr.T.K[:k], pr.Co.K[:k], pr.C.C[:k], pr.T.C[:k], pr.Co.C[:k]]
+        scs += [nt.fr_arith(nt.FR_MUL, rho, z), neg(rho), neg(nt.fr_arith(nt.FR_MUL, rho, c)),
+                nt.fr_arith(nt.FR_MUL, sig, z), neg(sig), neg(nt.fr_arith(nt.FR_MUL, sig, c))]
+    return _msm_is_zero([p.contiguous() for p in pts], scs)
 
 
 def key_switch_list_proof_verification(pr: KeySwitchProof, threshold: float = 1.0) -> bool:

@@ -102,3 +102,29 @@ def test_batched_keyswitch_and_obfuscation_verification():
     obf = [sigma.obfuscation_list_proof_creation(cv, cv.mul_scalars(si), si) for si in s]
     obf.append(sigma.obfuscation_list_proof_creation(cv, cv.mul_scalars(s[0]), s[1]))
     assert sigma.obfuscation_batch_verification(obf) == [True, True, False]
+
+
+def test_batch_verification_blames_only_the_bad_proof():
+    """Random-linear-combination (MSM) batch checks: one tampered proof among
+    good ones is pinned individually."""
+    kps = [eg.KeyPair.generate() for _ in range(3)]
+    q = eg.KeyPair.generate()
+    P = eg.aggregate_keys([k.public for k in kps])
+    pk = eg.pk_table(P)
+    cv, _ = eg.encrypt_ints(pk, [1, 2, 3, 4])
+    ks = []
+    for kp in kps:
+        share, v = sigma.key_switch_share(kp.secret, cv.K, q.public)
+        ks.append(sigma.key_switch_list_proof_creation(kp.secret, kp.public, q.public, cv.K, share, v))
+    assert sigma.key_switch_batch_verification(ks) == [True, True, True]
+    ks[1].za = ks[1].za.clone()
+    ks[1].za[2, 0] ^= 1
+    assert sigma.key_switch_batch_verification(ks) == [True, False, True]
+    obs = []
+    for _ in range(3):
+        s = bn.random_scalars(4)
+        obs.append(sigma.obfuscation_list_proof_creation(cv, cv.mul_scalars(s), s))
+    assert sigma.obfuscation_batch_verification(obs) == [True, True, True]
+    obs[2].z = obs[2].z.clone()
+    obs[2].z[0, 0] ^= 1
+    assert sigma.obfuscation_batch_verification(obs) == [True, True, False]
