@@ -120,6 +120,66 @@ DX_HD FieldT<PR> fdbl(const FieldT<PR> &a) {
   return fadd(a, a);
 }
 
+#ifdef __HIP_DEVICE_COMPILE__
+// acc(64) + hi(32) += x * y: one v_mad_u64_u32 whose carry-out (SGPR pair)
+// feeds one v_addc_co_u32 -- two instructions per 32x32 partial product
+// (the compiler's lowering of the same C++ needs ~5: a 64-bit add for the
+// carry word plus register-pair moves).
+__device__ __forceinline__ void dx_mac(uint64_t &acc, uint32_t &hi, uint32_t x, uint32_t y) {
+  uint64_t cy, unused;
+  asm("v_mad_u64_u32 %0, %2, %4, %5, %0\n\t"
+      "v_addc_co_u32_e64 %1, %3, %1, 0, %2"
+      : "+v"(acc), "+v"(hi), "=&s"(cy), "=&s"(unused)
+      : "v"(x), "v"(y));
+}
+
+// Montgomery multiplication on gfx950: finely integrated product scanning
+// (column-wise Comba, Montgomery digits m_i folded into the same columns) with
+// one 96-bit column accumulator: ~360 VALU instructions per product instead of
+// ~900 for the compiler-lowered CIOS loop (measured: +20% Miller loops/s,
+// +30% G1 scalar multiplications/s).  A second, interleaved accumulator per
+// column was measured slower: these kernels are issue-bound, not
+// latency-bound.  a, b < MOD -> result < MOD.
+template <class PR>
+__device__ __forceinline__ FieldT<PR> fmul(const FieldT<PR> &a, const FieldT<PR> &b) {
+  uint32_t m[8], u[8];
+  uint64_t acc = 0;
+  uint32_t hi = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+#pragma unroll
+    for (int j = 0; j < i; j++) {
+      dx_mac(acc, hi, a.v[j], b.v[i - j]);
+      dx_mac(acc, hi, m[j], PR::MOD[i - j]);
+    }
+    dx_mac(acc, hi, a.v[i], b.v[0]);
+    m[i] = (uint32_t)acc * PR::INV;
+    dx_mac(acc, hi, m[i], PR::MOD[0]);
+    acc = (acc >> 32) | ((uint64_t)hi << 32);
+    hi = 0;
+  }
+#pragma unroll
+  for (int i = 8; i < 16; i++) {
+#pragma unroll
+    for (int j = i - 7; j < 8; j++) {
+      dx_mac(acc, hi, a.v[j], b.v[i - j]);
+      dx_mac(acc, hi, m[j], PR::MOD[i - j]);
+    }
+    u[i - 8] = (uint32_t)acc;
+    acc = (acc >> 32) | ((uint64_t)hi << 32);
+    hi = 0;
+  }
+  // result = u + 2^256 * acc < 2 MOD: one conditional subtraction
+  uint32_t s[8], br = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) s[i] = subb32(u[i], PR::MOD[i], br);
+  const bool keep = ((uint32_t)acc == 0) && br;  // u < MOD and no overflow word
+  FieldT<PR> r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = keep ? u[i] : s[i];
+  return r;
+}
+#else
 // Montgomery multiplication, no-carry CIOS. a*b*2^-256 mod MOD.
 template <class PR>
 DX_MUL FieldT<PR> fmul(const FieldT<PR> &a, const FieldT<PR> &b) {
@@ -151,6 +211,7 @@ DX_MUL FieldT<PR> fmul(const FieldT<PR> &a, const FieldT<PR> &b) {
   for (int i = 0; i < 8; i++) r.v[i] = t[i];
   return r;
 }
+#endif
 
 template <class PR>
 DX_HD FieldT<PR> fsqr(const FieldT<PR> &a) {

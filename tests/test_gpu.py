@@ -143,3 +143,18 @@ def test_survey_end_to_end_gpu(gpu_device, tmp_path):
     assert abs(vals[0][0] - (tot[2] / tot[1] - m * m)) < 1e-9
     assert set(res.block.data_block().Proofs.values()) == {1}
     node.close(remove=True)
+
+
+def test_field_mul_edge_cases_gpu(gpu_device):
+    """Device Montgomery product (product-scanning asm path) vs the host CIOS
+    path on edge operands (0, 1, r-1, 2^k, values near 2^254)."""
+    edge = [0, 1, 2, O.R - 1, O.R - 2, (1 << 253) % O.R, (1 << 128) + 1, 0xFFFFFFFF, (O.R - 1) // 2]
+    vals = edge + [RNG.randrange(O.R) for _ in range(400)]
+    a = bn.scalars_tensor([x for x in vals for _ in vals[:9]])
+    b = bn.scalars_tensor([y for _ in vals for y in vals[:9]])
+    for op in (nt.FR_MUL, nt.FR_INV):
+        c, g = _both(lambda x, y: nt.fr_arith(op, x, y if op == nt.FR_MUL else None), a, b)
+        assert torch.equal(c, g)
+    got = bn.scalars_from_tensor(_both(lambda x, y: nt.fr_arith(nt.FR_MUL, x, y), a, b)[1])
+    ai, bi = bn.scalars_from_tensor(a), bn.scalars_from_tensor(b)
+    assert got == [(x * y) % O.R for x, y in zip(ai, bi)]
