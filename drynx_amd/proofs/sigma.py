@@ -200,8 +200,11 @@ class KeySwitchProof:
 
     def to_bytes(self) -> bytes:
         n = self.K.shape[0]
-        return b"".join([n.to_bytes(8, "little"), O.g1_to_bytes(self.X), O.g1_to_bytes(self.Q), _aff_bytes(self.K),
-                         self.share.to_bytes(), _aff_bytes(self.T1), _aff_bytes(self.T2), self.T3,
+        cached = getattr(self, "_aff", None)  # affine encodings kept from the prover's transcript
+        Kb, shb, t1b, t2b = cached if cached is not None else (
+            _aff_bytes(self.K), self.share.to_bytes(), _aff_bytes(self.T1), _aff_bytes(self.T2))
+        return b"".join([n.to_bytes(8, "little"), O.g1_to_bytes(self.X), O.g1_to_bytes(self.Q), Kb, shb, t1b, t2b,
+                         self.T3,
                          O.scalar_to_bytes(self.c), bn.scalars_to_bytes(self.za).tobytes(),
                          O.scalar_to_bytes(self.zb)])
 
@@ -269,17 +272,34 @@ def key_switch_shares_batch(secrets: list, publics: list, K: torch.Tensor, Q_poi
         a = bn.random_scalars(c * n, dev)
         T1 = nt.g1_fb_mul(tabB, a)
         T2 = nt.g1_add(nt.g1_fb_mul(tabQ, a), prods[c * n:].contiguous(), subtract=True)
+    if not with_proofs:
+        return [(shares_all[j * n:(j + 1) * n], None) for j in range(c)]
+    # every CN's transcript in ONE normalisation launch; the affine encodings are
+    # kept on the proofs so marshalling them later needs no further launch
+    T3s = [O.g1_to_bytes(bn.g1_mul_point(b)) for b in bs]
+    aff = _aff_bytes(torch.cat([K, shares_all.K, shares_all.C, T1, T2]))
+    seg = 64 * n
+    Kb = aff[:seg]
+
+    def part(block, j):
+        o = seg * (1 + block * c + j)
+        return aff[o: o + seg]
+
+    Qb = O.g1_to_bytes(Q_point)
     for j in range(c):
         sl = slice(j * n, (j + 1) * n)
         share = shares_all[sl]
-        pr = None
-        if with_proofs:
-            T3 = O.g1_to_bytes(bn.g1_mul_point(bs[j]))
-            t1, t2 = T1[sl].contiguous(), T2[sl].contiguous()
-            ch = fs_challenge("proofTest/keyswitch", O.g1_to_bytes(publics[j]), O.g1_to_bytes(Q_point), K, share,
-                              t1, t2, T3)
-            za = nt.fr_arith(nt.FR_ADD, a[sl].contiguous(), nt.fr_arith(nt.FR_MUL, v[sl].contiguous(), _sc([ch], dev)))
-            pr = KeySwitchProof(publics[j], Q_point, K, share, t1, t2, T3, ch, za, (bs[j] + ch * secrets[j]) % O.R)
+        t1, t2 = T1[sl].contiguous(), T2[sl].contiguous()
+        sKb, sCb, t1b, t2b = part(0, j), part(1, j), part(2, j), part(3, j)
+        h = hashlib.sha256()
+        for piece in (b"proofTest/keyswitch", O.g1_to_bytes(publics[j]), Qb, Kb, sKb, sCb, t1b, t2b, T3s[j]):
+            h.update(piece)
+        ch = int.from_bytes(h.digest(), "big") % O.R
+        za = nt.fr_arith(nt.FR_ADD, a[sl].contiguous(), nt.fr_arith(nt.FR_MUL, v[sl].contiguous(), _sc([ch], dev)))
+        pr = KeySwitchProof(publics[j], Q_point, K, share, t1, t2, T3s[j], ch, za, (bs[j] + ch * secrets[j]) % O.R)
+        shb = np.concatenate([np.frombuffer(sKb, np.uint8).reshape(n, 64),
+                              np.frombuffer(sCb, np.uint8).reshape(n, 64)], axis=1).tobytes()
+        pr._aff = (Kb, shb, t1b, t2b)
         out.append((share, pr))
     return out
 
