@@ -297,6 +297,13 @@ def verify_requests(reqs: list, sq, vn_id: str, vn_index: int, n_vns: int, devic
             codes[i] = PROOF_RECEIVED
         else:
             todo.setdefault(req.kind, []).append(i)
+    range_future = None
+    if "range" in todo and len(todo) > 1 and torch.device(device).type == "cuda":
+        # the range lists (the heavy pairing work) verify on a worker thread with
+        # their own HIP stream while this thread checks the short per-CN proofs
+        idxs = todo.pop("range")
+        range_future = _side_pool().submit(_verify_range_side, reqs, idxs, sq, vn_id, device, cache,
+                                           torch.cuda.current_stream(torch.device(device)))
     for kind, idxs in todo.items():
         with timers.timed(f"{vn_id}_{TIMER[kind]}"):
             if kind in ("keyswitch", "obfuscation") and len(idxs) > 1:
@@ -326,7 +333,42 @@ def verify_requests(reqs: list, sq, vn_id: str, vn_index: int, n_vns: int, devic
                         log.warning(f"{vn_id}: {kind} proof from {reqs[i].sender_id} rejected: {e}")
                         ok = False
                     codes[i] = PROOF_TRUE if ok else PROOF_FALSE
+    if range_future is not None:
+        for i, code in range_future.result():
+            codes[i] = code
     return codes
+
+
+_pool = None
+_streams: dict = {}
+
+
+def _side_pool():
+    global _pool
+    if _pool is None:
+        import concurrent.futures as cf
+
+        _pool = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="drynx-vn-range")
+    return _pool
+
+
+def _verify_range_side(reqs, idxs, sq, vn_id, device, cache, main) -> list:
+    dev = torch.device(device)
+    side = _streams.get(str(dev))
+    if side is None:
+        side = _streams[str(dev)] = torch.cuda.Stream(dev)
+    side.wait_stream(main)  # payloads / decoded lists are ready
+    out = []
+    with torch.cuda.stream(side), timers.timed(f"{vn_id}_{TIMER['range']}"):
+        for i in idxs:
+            try:
+                ok = verify_content(reqs[i], sq, device, cache)
+            except Exception as e:
+                log.warning(f"{vn_id}: range proof from {reqs[i].sender_id} rejected: {e}")
+                ok = False
+            out.append((i, PROOF_TRUE if ok else PROOF_FALSE))
+    side.synchronize()
+    return out
 
 
 def verify_proof(req: ProofRequest, sq, vn_id: str, vn_index: int, n_vns: int, device, cache: VerifierCache) -> int:

@@ -126,6 +126,8 @@ class DrynxNode:
             client_future = self._submit_client(on_result, SurveyResult(sq.SurveyID, result, n_groups, n_out))
         if range_future is not None:
             proofs.extend(range_future.result())
+            if hasattr(self, "_prove_stream"):
+                torch.cuda.current_stream(self.device).wait_stream(self._prove_stream)
         block = None
         if q.Proofs and q.RosterVNs is not None and len(q.RosterVNs.list):
             block = pcp.proof_collection(self, sq, proofs)
@@ -231,8 +233,26 @@ class DrynxNode:
             fut = cf.Future()
             fut.set_result(lst)
             return fut
-        proved = self._prove_range(sq, dp_results)  # GPU work is queued on this thread's stream
-        return self._pool.submit(self._sign_range, sq, proved)
+        if self.device.type != "cuda":
+            proved = self._prove_range(sq, dp_results)
+            return self._pool.submit(self._sign_range, sq, proved)
+        # proving runs on its own HIP stream so the CN phases (aggregation, key
+        # switching: short latency-bound launches) overlap it on the GPU instead
+        # of queueing behind ~20 ms of range-proof kernels
+        if not hasattr(self, "_prove_stream"):
+            self._prove_stream = torch.cuda.Stream(self.device)
+        side, main = self._prove_stream, torch.cuda.current_stream(self.device)
+        side.wait_stream(main)  # the DP ciphertexts / randomness are ready
+        with torch.cuda.stream(side):
+            proved = self._prove_range(sq, dp_results)
+
+        def sign():
+            with torch.cuda.stream(side):
+                reqs = self._sign_range(sq, proved)  # packing + digest kernels follow the proofs on `side`
+            side.synchronize()
+            return reqs
+
+        return self._pool.submit(sign)
 
     # ------------------------------------------------------------------ VN getters (api_skipchain.go)
     def get_genesis(self, vn_id: str):
