@@ -168,3 +168,50 @@ extern "C" int dx_sha256_chunks(int on_gpu, void *stream, const uint8_t *data, i
   };
   return run(on_gpu, stream, n, op, false, "sha256_chunks");
 }
+
+// Independent G1 generators h_i (unknown discrete logs) for commitment
+// schemes -- the permutation commitments of the shuffle proof.  For index i:
+// ctr = 0, 1, ...: x = SHA-256(seed || le64(i) || le32(ctr)) (big endian) mod p;
+// accept when x^3 + 3 is a square, y = (x^3+3)^((p+1)/4) with even canonical y.
+// BN254 G1 has cofactor 1, so every curve point is a generator.  Mirrored by
+// drynx_amd/proofs/shuffle.py:_hash_to_g1_index (host oracle).
+extern "C" int dx_hash_to_g1(int on_gpu, void *stream, const uint32_t *seed_host, const uint32_t *sqrt_exp_host,
+                             int64_t start, uint32_t *out_aff, int64_t n) {
+  struct Args {
+    uint32_t seed[8], e[8];
+  } A;
+  for (int i = 0; i < 8; i++) {
+    A.seed[i] = seed_host[i];
+    A.e[i] = sqrt_exp_host[i];
+  }
+  auto op = [=] __host__ __device__(int64_t k) {
+    const uint64_t idx = (uint64_t)(start + k);
+    G1A res = G1A::inf();
+    for (uint32_t ctr = 0; ctr < 128; ctr++) {
+      // one 44-byte message in one padded block
+      uint32_t w[16];
+      for (int i = 0; i < 8; i++) w[i] = A.seed[i];  // seed bytes as big-endian message words
+      w[8] = bswap32((uint32_t)idx);
+      w[9] = bswap32((uint32_t)(idx >> 32));
+      w[10] = bswap32(ctr);
+      w[11] = 0x80000000u;
+      for (int i = 12; i < 15; i++) w[i] = 0;
+      w[15] = 44 * 8;
+      Sha256 st;
+      st.init();
+      st.compress(w);
+      uint32_t le[8];
+      for (int i = 0; i < 8; i++) le[i] = st.h[7 - i];  // big-endian digest -> little-endian limbs
+      Fp x = to_mont(reduce_256<FpParams>(le));
+      Fp rhs = fadd(fmul(fsqr(x), x), Fp::from_limbs(Curve::B1));
+      Fp y = fpow(rhs, A.e);
+      if (fsqr(y) == rhs) {
+        if (from_mont(y).v[0] & 1u) y = fneg(y);
+        res = {x, y};
+        break;
+      }
+    }
+    at<G1A>(out_aff, k) = res;
+  };
+  return run(on_gpu, stream, n, op, true, "hash_to_g1");
+}

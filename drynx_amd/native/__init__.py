@@ -83,6 +83,7 @@ _SIGS = {
     "dx_lr_moments": [_P, _P, _P, _L, _I, _P, _I],
     "dx_random_scalars": [_I, _P, _P, ctypes.c_uint32, _P, _L],
     "dx_sha256_chunks": [_I, _P, _P, _L, _L, _P],
+    "dx_hash_to_g1": [_I, _P, _P, _P, _L, _P, _L],
     "dx_lr_encode": [_P, _P, _L, _L, _I, _P, _P, _P, ctypes.c_double, ctypes.c_double, _P, _I],
     "dx_g1_mul_fast": [_P, _P, _P, _P, _L, _I, _I],
     "dx_rp_verify_fold": [_P, _P, _P, _P, _P, _P, _L, _I, _I],
@@ -452,6 +453,36 @@ def random_scalars(n: int, device) -> torch.Tensor:
     key = _np.frombuffer(os.urandom(32), dtype="<u4").copy()
     g, s = _ctx(out)
     _call("dx_random_scalars", g, s, key.ctypes.data_as(ctypes.c_void_p), 0, _ptr(out), n)
+    return out
+
+
+def hash_to_g1(seed: bytes, start: int, n: int, device) -> torch.Tensor:
+    """[n, 16] affine G1 points h_start .. h_{start+n-1} derived from a 32-byte
+    seed by try-and-increment (dx_hash.hip; unknown discrete logarithms)."""
+    from ..crypto import oracle as _O
+
+    device = torch.device(device)
+    out = torch.empty((max(0, n), 16), dtype=torch.int32, device=device)
+    if n <= 0:
+        return out
+    sd = np.frombuffer(seed, dtype=">u4").astype("<u4").copy()  # seed words as big-endian message words
+    e = np.frombuffer(((_O.P + 1) // 4).to_bytes(32, "little"), dtype="<u4").copy()
+    g, s = _ctx(out)
+    _call("dx_hash_to_g1", g, s, sd.ctypes.data_as(ctypes.c_void_p), e.ctypes.data_as(ctypes.c_void_p), start,
+          _ptr(out), n)
+    return out
+
+
+def prg_scalars(key: bytes, n: int, device) -> torch.Tensor:
+    """n Fr scalars from ChaCha20 keyed by a 32-byte ``key`` (deterministic:
+    Fiat-Shamir challenge vectors expanded on the device)."""
+    device = torch.device(device)
+    out = torch.empty((max(0, n), 8), dtype=torch.int32, device=device)
+    if n <= 0:
+        return out
+    k = np.frombuffer(key[:32], dtype="<u4").copy()
+    g, s = _ctx(out)
+    _call("dx_random_scalars", g, s, k.ctypes.data_as(ctypes.c_void_p), 0, _ptr(out), n)
     return out
 
 

@@ -27,7 +27,7 @@ from ..utils import timers
 from ..utils.log import get_logger
 from . import aggregation_shuffle as ags
 from . import range_proof as rp
-from . import sigma
+from . import shuffle, sigma
 
 log = get_logger("proofs")
 
@@ -262,8 +262,8 @@ def verify_content(req: ProofRequest, sq, device, cache: VerifierCache) -> bool:
         pr = req.obj if req.obj is not None else sigma.ObfuscationProof.from_bytes(req.data, device)
         return sigma.obfuscation_list_proof_verification(pr, sq.ObfuscationProofThreshold)
     if req.kind == "shuffle":
-        pr = req.obj if req.obj is not None else ags.ShuffleProof.from_bytes(req.data, device)
-        return ags.shuffle_proof_verification(pr, P)
+        pr = req.obj if req.obj is not None else shuffle.ShuffleProof.from_bytes(req.data, device)
+        return shuffle.verify(pr, P)
     if req.kind == "keyswitch":
         pr = req.obj if req.obj is not None else sigma.KeySwitchProof.from_bytes(req.data, device)
         if pr.X != sq.IDtoPublic.get(req.sender_id) or pr.Q != sq.ClientPubKey:

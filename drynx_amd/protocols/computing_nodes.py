@@ -25,6 +25,7 @@ from ..crypto import bn254 as bn
 from ..crypto import elgamal as eg
 from ..parallel import ec_collectives as ec
 from ..proofs import aggregation_shuffle as ags
+from ..proofs import shuffle
 from ..proofs import requests as prq
 from ..proofs import sigma
 from ..query import add_diff_p
@@ -96,7 +97,7 @@ def dro_phase(ctx, sq, proofs: list):
             if ctx.rank == cn.rank:
                 Y, perm, rho = ags.shuffle_sequence(cur, P)
                 if sq.Query.Proofs:
-                    pr = ags.shuffle_proof_creation(cur, Y, perm, rho, P, k=ctx.shuffle_proof_k)
+                    pr = shuffle.prove(cur, Y, perm, rho, P)
                     proofs.append(prq.new_proof_request("shuffle", pr, sq.SurveyID, cn.id, "", cn.keypair.secret))
                 cur = Y
         root = cns[0].rank

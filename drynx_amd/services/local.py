@@ -25,11 +25,10 @@ RANGE_PRESETS = {  # simul/drynx_simul.go:133-281 `Ranges` codes -> (u, l)
 
 
 def local_cluster(n_cns=3, n_dps=5, n_vns=3, comm: Comm | None = None, device=None, workdir=None,
-                  deterministic_keys=False, dp_data=None, shuffle_proof_k=40):
+                  deterministic_keys=False, dp_data=None):
     comm = comm or LocalComm(device or ("cuda" if torch.cuda.is_available() else "cpu"))
     cl = build_cluster(n_cns, n_dps, n_vns, comm.world, comm.rank, comm, deterministic_keys)
-    node = DrynxNode(cl, comm, workdir or tempfile.mkdtemp(prefix="drynx_db_"), device or comm.device, dp_data,
-                     shuffle_proof_k)
+    node = DrynxNode(cl, comm, workdir or tempfile.mkdtemp(prefix="drynx_db_"), device or comm.device, dp_data)
     return cl, node
 
 

@@ -59,7 +59,7 @@ class DrynxNode:
     """Per-rank runtime hosting the logical parties placed on this rank."""
 
     def __init__(self, cluster: Cluster, comm: Comm | None = None, workdir: str = "./drynx_db", device=None,
-                 dp_data: dict | None = None, shuffle_proof_k: int = 40):
+                 dp_data: dict | None = None):
         self.comm = comm or LocalComm(device or ("cuda" if torch.cuda.is_available() else "cpu"))
         self.rank = self.comm.rank
         self.device = torch.device(device) if device is not None else self.comm.device
@@ -67,7 +67,6 @@ class DrynxNode:
         self.key_index = KeyIndex([p.id for p in cluster.parties])
         self.workdir = workdir
         self.dp_data = dp_data or {}
-        self.shuffle_proof_k = shuffle_proof_k
         self._stores: dict = {}
         self.verifier_cache = prq.VerifierCache()
         self.local_bitmaps: dict = {}

@@ -16,11 +16,12 @@ from ..crypto import elgamal as eg
 from ..ops.encoding import CreateProofBatch
 from ..proofs import aggregation_shuffle as ags
 from ..proofs import range_proof as rp
+from ..proofs import shuffle
 from ..proofs import sigma
 
 
 def create_random_good_test_data(P_point, querier_public, sigs, nbr_proofs: int, entity: eg.KeyPair | None = None,
-                                 device="cpu", u: int = 16, l: int = 16, shuffle_k: int = 8) -> dict:
+                                 device="cpu", u: int = 16, l: int = 16) -> dict:
     """kind -> [proof objects]; ``sigs`` = InputValidationSigs[cn][col] with >= 2 columns;
     ``entity`` = the key-switching CN's keypair (random if None, as the reference)."""
     device = torch.device(device)
@@ -40,7 +41,7 @@ def create_random_good_test_data(P_point, querier_public, sigs, nbr_proofs: int,
         x2, _ = eg.encrypt_ints(pk, [2, 4, 8, 6])
         X = eg.CipherVector.cat([x1, x2])
         Y, perm, rho = ags.shuffle_sequence(X, P_point)
-        out["shuffle"].append(ags.shuffle_proof_creation(X, Y, perm, rho, P_point, k=shuffle_k))
+        out["shuffle"].append(shuffle.prove(X, Y, perm, rho, P_point))
 
         c, _ = eg.encrypt_ints(pk, [1, 2])
         share, v = sigma.key_switch_share(entity.secret, c.K, querier_public)

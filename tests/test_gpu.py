@@ -158,3 +158,21 @@ def test_field_mul_edge_cases_gpu(gpu_device):
     got = bn.scalars_from_tensor(_both(lambda x, y: nt.fr_arith(nt.FR_MUL, x, y), a, b)[1])
     ai, bi = bn.scalars_from_tensor(a), bn.scalars_from_tensor(b)
     assert got == [(x * y) % O.R for x, y in zip(ai, bi)]
+
+
+def test_shuffle_proof_gpu(gpu_device):
+    """DRO shuffle proof on the device (N = 2000): prove, verify, reject a tampered output."""
+    from drynx_amd.crypto import elgamal as eg
+    from drynx_amd.proofs import aggregation_shuffle as ags
+    from drynx_amd.proofs import shuffle as sh
+
+    kp = eg.KeyPair.generate()
+    pk = eg.pk_table(kp.public, gpu_device)
+    X, _ = eg.encrypt_ints(pk, [RNG.randrange(-50, 50) for _ in range(2000)])
+    Y, perm, rho = ags.shuffle_sequence(X, kp.public)
+    pr = sh.prove(X, Y, perm, rho, kp.public)
+    assert sh.verify(pr, kp.public)
+    cpu = sh.ShuffleProof.from_bytes(pr.to_bytes(), "cpu")
+    assert sh.verify(cpu, kp.public)
+    Y.C[5] = Y.C[6]
+    assert not sh.verify(sh.prove(X, Y, perm, rho, kp.public), kp.public)

@@ -87,7 +87,6 @@ def test_proofs_skipchain_and_getters(env):
 
 def test_obfuscation_and_diffp_with_proofs(env):
     cl, node, client = env
-    node.shuffle_proof_k = 6
     sq = make_survey(client, cl, "union", query_min=0, query_max=4, rows=4, proofs=1, ranges=[2, 1],
                      obfuscation=True)
     _, vals, res = client.send_survey_query(sq)

@@ -68,15 +68,49 @@ def test_aggregation_proof():
 
 
 def test_shuffle_proof():
-    kp, pk, X = _cv([1, 2, 3, 4, 5])
+    from drynx_amd.proofs import shuffle as sh
+
+    kp, pk, X = _cv([1, 2, 3, 4, 5, 0, 7, 7])
     Y, perm, rho = ags.shuffle_sequence(X, kp.public)
-    assert sorted(eg.decrypt_ints(kp.secret, Y)) == [1, 2, 3, 4, 5]
-    pr = ags.shuffle_proof_creation(X, Y, perm, rho, kp.public, k=12)
-    assert ags.shuffle_proof_verification(pr, kp.public)
-    assert ags.shuffle_proof_verification(ags.ShuffleProof.from_bytes(pr.to_bytes()), kp.public)
-    Z, _ = eg.encrypt_ints(pk, [1, 2, 3, 4, 6])  # not a shuffle of X
-    pr2 = ags.shuffle_proof_creation(X, Z, perm, rho, kp.public, k=12)
-    assert not ags.shuffle_proof_verification(pr2, kp.public)
+    pr = sh.prove(X, Y, perm, rho, kp.public)
+    assert sh.verify(pr, kp.public)
+    assert sh.verify(sh.ShuffleProof.from_bytes(pr.to_bytes()), kp.public)
+    assert sorted(eg.decrypt_ints(kp.secret, Y)) == sorted(eg.decrypt_ints(kp.secret, X))
+    Z, _ = eg.encrypt_ints(pk, [1, 2, 3, 4, 6, 0, 7, 7])  # not a shuffle of X
+    assert not sh.verify(sh.prove(X, Z, perm, rho, kp.public), kp.public)
+    wrong = perm.clone()
+    wrong[[0, 1]] = wrong[[1, 0]]  # claimed permutation does not match Y
+    assert not sh.verify(sh.prove(X, Y, wrong, rho, kp.public), kp.public)
+    for field in ("kE", "kB"):
+        bad = sh.ShuffleProof.from_bytes(pr.to_bytes())
+        t = getattr(bad, field).clone()
+        t[2, 0] ^= 1
+        setattr(bad, field, t)
+        assert not sh.verify(bad, kp.public)
+    bad = sh.ShuffleProof.from_bytes(pr.to_bytes())
+    bad.kA ^= 1
+    assert not sh.verify(bad, kp.public)
+
+
+def test_shuffle_generators_match_host_hash():
+    import hashlib
+
+    from drynx_amd import native as nt
+    from drynx_amd.proofs import shuffle as sh
+
+    def h2g(i):
+        for ctr in range(128):
+            d = hashlib.sha256(sh.SEED + i.to_bytes(8, "little") + ctr.to_bytes(4, "little")).digest()
+            x = int.from_bytes(d, "big") % O.P
+            rhs = (x * x * x + 3) % O.P
+            y = pow(rhs, (O.P + 1) // 4, O.P)
+            if y * y % O.P == rhs:
+                return (x, O.P - y if y & 1 else y)
+
+    got = bn.g1_points_from_jac(sh.generators(9, "cpu"))
+    assert got == [h2g(i) for i in range(10)]
+    assert len(set(got)) == 10 and all(O.g1_on_curve(p) for p in got)
+    assert nt.hash_to_g1(sh.SEED, 3, 2, "cpu").shape == (2, 16)
 
 
 def test_noise_generation():
