@@ -14,6 +14,7 @@ Usage: python -m drynx_amd.simul.simul drynx_amd/simul/runfiles/drynx.toml [--cs
 from __future__ import annotations
 
 import argparse
+import ast
 import csv
 import os
 import shlex
@@ -41,9 +42,10 @@ def parse_runfile(text: str):
         if header is None and "=" in line and "," not in line.split("=")[0]:
             k, v = line.split("=", 1)
             v = v.strip()
+            lit = {"true": "True", "false": "False"}.get(v, v)
             try:
-                glob[k.strip()] = eval(v, {"__builtins__": {}}, {"true": True, "false": False})  # literals only
-            except Exception:
+                glob[k.strip()] = ast.literal_eval(lit)
+            except (ValueError, SyntaxError):
                 glob[k.strip()] = v.strip('"')
             continue
         parts = [p.strip() for p in next(csv.reader([line], skipinitialspace=True))]
