@@ -123,6 +123,18 @@ def encode_model_evaluation(data, pk, with_proofs=False, ranges=None):
     return _encrypt_with_proofs(pk, vals, with_proofs, ranges)
 
 
+def int_pair_moments(X: torch.Tensor, pairs: torch.Tensor, chunk: int = 1 << 16) -> torch.Tensor:
+    """Exact int64 sum_i X[i, a] * X[i, b] for the column pairs (a, b) = pairs[:, p]
+    (K14): elementwise products reduced over record chunks, so it runs on the
+    GPU too (no int64 GEMM there) and never leaves exact integer arithmetic."""
+    out = torch.zeros(pairs.shape[1], dtype=torch.int64, device=X.device)
+    a, b = pairs[0].to(X.device), pairs[1].to(X.device)
+    for s in range(0, X.shape[0], chunk):
+        blk = X[s: s + chunk]
+        out += (blk.index_select(1, a) * blk.index_select(1, b)).sum(0)
+    return out
+
+
 def encode_lin_reg(data, pk, with_proofs=False, ranges=None):
     """linear_regression_dims.go:23-106 — data = [x_0..x_{d-1}, y] columns.
 
@@ -131,10 +143,10 @@ def encode_lin_reg(data, pk, with_proofs=False, ranges=None):
     X = torch.stack(cols[:-1], dim=1)  # [N, d]
     y = cols[-1]
     N, d = X.shape
-    XtX = X.T @ X  # exact int64 matmul
+    iu = torch.triu_indices(d, d, device=X.device)
+    XtX_u = int_pair_moments(X, iu)  # exact int64 sum_i x_ij x_ik, j <= k
     vals = [N] + X.sum(0).cpu().tolist()
-    iu = torch.triu_indices(d, d)
-    vals += XtX[iu[0], iu[1]].cpu().tolist()
+    vals += XtX_u.cpu().tolist()
     vals += [local_sum(y)] + (X * y[:, None]).sum(0).cpu().tolist()
     return _encrypt_with_proofs(pk, vals, with_proofs, ranges)
 

@@ -176,3 +176,45 @@ def test_shuffle_proof_gpu(gpu_device):
     assert sh.verify(cpu, kp.public)
     Y.C[5] = Y.C[6]
     assert not sh.verify(sh.prove(X, Y, perm, rho, kp.public), kp.public)
+
+
+@pytest.mark.parametrize("op", ["sum", "mean", "variance", "cosim", "frequencyCount", "lin_reg", "MLeval",
+                                "min", "max", "bool_OR", "bool_AND", "union", "inter", "logistic regression"])
+def test_every_operation_on_gpu(gpu_device, tmp_path, op):
+    """Every operation end to end with every party on the GPU (encoders, HIP
+    aggregation/key switching/decryption), checked against the clear sum of the
+    DPs' answers."""
+    from drynx_amd.ops import encoding as enc
+    from drynx_amd.query import LogisticRegressionParameters
+    from drynx_amd.services.api import DrynxClient
+    from drynx_amd.services.local import local_cluster, make_survey
+
+    cl, node = local_cluster(2, 3, 1, device=gpu_device, workdir=str(tmp_path))
+    client = DrynxClient(node, device=gpu_device)
+    lp = None
+    if op == "logistic regression":
+        lp = LogisticRegressionParameters(NbrRecords=30, NbrFeatures=3, Means=[0.0] * 3, StandardDeviations=[1.0] * 3,
+                                          Lambda=1.0, Step=0.1, MaxIterations=5, InitialWeights=[0.1] * 4, K=2,
+                                          PrecisionApproxCoefficients=1e2)
+    bool_ops = ("min", "max", "bool_OR", "bool_AND", "union", "inter")
+    rows = [[2, 3, 5], [4, 5, 6], [3, 4, 5]]
+    if op in bool_ops:
+        node.dp_data = {dp.id: [torch.tensor(rows[i], dtype=torch.int64, device=gpu_device)]
+                        for i, dp in enumerate(cl.dps)}
+    sq = make_survey(client, cl, op, query_min=0, query_max=6, rows=10 if op not in bool_ops else 3, d=2,
+                     lr_params=lp)
+    _, vals, res = client.send_survey_query(sq)
+    if op in bool_ops:
+        sets = [set(r) for r in rows]
+        exp = {"min": [2.0], "max": [6.0], "bool_OR": [1.0], "bool_AND": [0.0],
+               "union": [float(any(i in s for s in sets)) for i in range(7)],
+               "inter": [float(all(i in s for s in sets)) for i in range(7)]}[op]
+        assert vals[0] == exp
+    elif op == "logistic regression":
+        assert len(vals[0]) == 4
+    else:
+        n = sq.Query.Operation.NbrOutput
+        tot = [sum(v[0][i] for v in res.clear_dp.values()) for i in range(n)]
+        exp = enc.decode_values(op, tot, sq.Query.Operation)
+        assert vals[0] == pytest.approx(exp, rel=1e-9, abs=1e-9)
+    node.close(remove=True)
