@@ -44,6 +44,18 @@ class CreateProofBatch:
         return len(self.values)
 
 
+def cat_proof_batches(batches: list) -> "CreateProofBatch":
+    """One CreateProofBatch out of several (several DPs' responses)."""
+    if len(batches) == 1:
+        return batches[0]
+    offs = []
+    for b in batches:
+        offs += list(b.offset) if b.offset else [0] * len(b)
+    return CreateProofBatch([v for b in batches for v in b.values], torch.cat([b.r for b in batches]).contiguous(),
+                            eg.CipherVector.cat([b.cv for b in batches]), [x for b in batches for x in b.u],
+                            [x for b in batches for x in b.l], [x for b in batches for x in b.sig_col], offs)
+
+
 @dataclass
 class EncodeResult:
     cv: eg.CipherVector

@@ -489,6 +489,26 @@ def verify_range_proof_list(rpl: RangeProofList, sigmat: SigMaterial, P_point, t
     return bool(nt.gt_eq(lhs_gt, rhs_gt).all())
 
 
+def rpl_cat(lists: list) -> RangeProofList:
+    """Concatenate proof lists sharing (u, l, S) into one batch (columnar)."""
+    r0 = lists[0]
+    if len(lists) == 1:
+        return r0
+    assert all((r.u, r.l, r.S) == (r0.u, r0.l, r0.S) for r in lists)
+    cat = lambda f: None if getattr(r0, f) is None else torch.cat([getattr(r, f) for r in lists])  # noqa: E731
+    return RangeProofList(r0.u, r0.l, r0.S, [o for r in lists for o in r.offset], [c for r in lists for c in r.cols],
+                          CipherVector.cat([r.commit for r in lists]), cat("challenge"), cat("zr"), cat("D"),
+                          cat("zphi"), cat("zv"), cat("V"), cat("A"))
+
+
+def rpl_range(r: RangeProofList, a: int, b: int) -> RangeProofList:
+    """Proofs a..b-1 of a list (views)."""
+    l, S = r.l, r.S
+    sl = lambda t, w: None if t is None else t[a * w: b * w]  # noqa: E731
+    return RangeProofList(r.u, l, S, r.offset[a:b], r.cols[a:b], r.commit[a:b], sl(r.challenge, 1), sl(r.zr, 1),
+                          sl(r.D, 1), sl(r.zphi, l), sl(r.zv, S * l), sl(r.V, S * l), sl(r.A, S * l))
+
+
 def _slice(r: RangeProofList, k: int) -> RangeProofList:
     l, S = r.l, r.S
     return RangeProofList(r.u, l, S, r.offset[:k], r.cols[:k], r.commit[:k], r.challenge[:k], r.zr[:k], r.D[:k],

@@ -15,6 +15,7 @@ coverage.
 from __future__ import annotations
 
 import hashlib
+import math
 import random
 from typing import Any
 
@@ -272,6 +273,64 @@ def verify_content(req: ProofRequest, sq, device, cache: VerifierCache) -> bool:
     raise ValueError(req.kind)
 
 
+def _range_lists(req: ProofRequest, device) -> list:
+    if req.obj is not None:
+        return req.obj
+    if req.tensor is not None and req._data is None:
+        return range_bundle_unpack(req.tensor.to(device))
+    return range_bundle_from_bytes(req.data, device)
+
+
+def verify_range_many(reqs: list, idxs: list, sq, device, cache: VerifierCache) -> dict:
+    """Range-proof requests of one VN as ONE batched verification: the sampled
+    prefix of every list (reference RangeProofThreshold semantics) of every
+    request, grouped by (u, l), folded into a single pairing batch.  If a
+    batch fails, each request is re-checked alone so the bitmap blames
+    exactly the bad ones.  -> {request index: bool}"""
+    P = sq.RosterServers.aggregate()
+    sigs = sq.Query.IVSigs.InputValidationSigs
+    out, parts = {}, {}
+    for i in idxs:
+        try:
+            lists = []
+            for r in _range_lists(reqs[i], device):
+                if not r.has_rp:
+                    continue
+                if sigs is None or not _ranges_ok(sq, r):
+                    raise ValueError("ranges / signatures do not match the query")
+                k = int(math.ceil(sq.RangeProofThreshold * len(r)))
+                if k:
+                    lists.append(r if k == len(r) else rp.rpl_range(r, 0, k))
+            parts[i] = lists
+            out[i] = True
+        except Exception as e:
+            log.warning(f"range proof from {reqs[i].sender_id} rejected: {e}")
+            out[i] = False
+    live = [i for i in idxs if out[i] and parts[i]]
+    if not live:
+        return out
+    sigmat = cache.sigmat(sq, device)
+    groups: dict = {}
+    for i in live:
+        for r in parts[i]:
+            groups.setdefault((r.u, r.l, r.S), []).append(r)
+    try:
+        ok = all(rp.verify_range_proof_list(rp.rpl_cat(g), sigmat, P, 1.0, device) for g in groups.values())
+    except Exception as e:
+        log.warning(f"batched range verification failed: {e}")
+        ok = False
+    if ok or len(live) == 1:
+        for i in live:
+            out[i] = ok
+        return out
+    for i in live:  # attribute the failure
+        try:
+            out[i] = all(rp.verify_range_proof_list(r, sigmat, P, 1.0, device) for r in parts[i])
+        except Exception:
+            out[i] = False
+    return out
+
+
 def _decode(req: ProofRequest, device):
     if req.obj is not None:
         return req.obj
@@ -306,7 +365,10 @@ def verify_requests(reqs: list, sq, vn_id: str, vn_index: int, n_vns: int, devic
                                            torch.cuda.current_stream(torch.device(device)))
     for kind, idxs in todo.items():
         with timers.timed(f"{vn_id}_{TIMER[kind]}"):
-            if kind in ("keyswitch", "obfuscation") and len(idxs) > 1:
+            if kind == "range":
+                for i, ok in verify_range_many(reqs, idxs, sq, device, cache).items():
+                    codes[i] = PROOF_TRUE if ok else PROOF_FALSE
+            elif kind in ("keyswitch", "obfuscation") and len(idxs) > 1:
                 objs, valid = [], []
                 for i in idxs:
                     try:
@@ -360,12 +422,7 @@ def _verify_range_side(reqs, idxs, sq, vn_id, device, cache, main) -> list:
     side.wait_stream(main)  # payloads / decoded lists are ready
     out = []
     with torch.cuda.stream(side), timers.timed(f"{vn_id}_{TIMER['range']}"):
-        for i in idxs:
-            try:
-                ok = verify_content(reqs[i], sq, device, cache)
-            except Exception as e:
-                log.warning(f"{vn_id}: range proof from {reqs[i].sender_id} rejected: {e}")
-                ok = False
+        for i, ok in verify_range_many(reqs, idxs, sq, device, cache).items():
             out.append((i, PROOF_TRUE if ok else PROOF_FALSE))
     side.synchronize()
     return out

@@ -19,12 +19,14 @@ from __future__ import annotations
 
 import copy
 import os
+import time
 from dataclasses import dataclass, field
 
 import torch
 
 from ..crypto.elgamal import CipherVector
 from ..ledger.skipchain import SkipBlock
+from ..ops.encoding import cat_proof_batches as dcp_batch_cat
 from ..ledger.store import Store
 from ..parallel.comm import Comm, LocalComm
 from ..parallel.ec_collectives import KeyIndex
@@ -197,21 +199,40 @@ class DrynxNode:
         proofs.extend(self._sign_range(sq, self._prove_range(sq, dp_results)))
 
     def _prove_range(self, sq, dp_results: dict) -> list:
+        """Range proofs of every DP hosted here as ONE prover batch per (u, l)
+        (ten DPs with one output each would otherwise be ten latency-bound
+        launch sequences), split back per DP afterwards."""
         P = sq.RosterServers.aggregate()
-        out = []
+        out = {dp_id: [] for dp_id in dp_results}
+        owners, batches = [], []
         for dp_id, res in dp_results.items():
-            with timers.timed(f"{dp_id}_AllProofs", sync=False):
-                lists = []
-                if any(b is not None for b in res["proofs"]):
-                    sigmat = self.verifier_cache.sigmat(sq, self.device)
-                    for b in res["proofs"]:
-                        if b is not None and len(b):
-                            lists += rp.create_range_proofs(b, sigmat, P, self.device)
-                else:  # no range proofs (ranges 0): ship the commitments only (dcp.go:283-288)
-                    lists.append(rp.RangeProofList(0, 0, 0, [0] * len(res["cv"]), list(range(len(res["cv"]))),
-                                                   res["cv"]))
-            out.append((dp_id, lists))
-        return out
+            bs = [b for b in res["proofs"] if b is not None and len(b)]
+            if bs:
+                for b in bs:
+                    owners.append((dp_id, b))
+                    batches.append(b)
+            elif not any(b is not None for b in res["proofs"]):
+                # no range proofs (ranges 0): ship the commitments only (dcp.go:283-288)
+                out[dp_id].append(rp.RangeProofList(0, 0, 0, [0] * len(res["cv"]), list(range(len(res["cv"]))),
+                                                    res["cv"]))
+        if batches:
+            t0 = time.perf_counter()
+            sigmat = self.verifier_cache.sigmat(sq, self.device)
+            big = dcp_batch_cat(batches)
+            lists = rp.create_range_proofs(big, sigmat, P, self.device)  # one list per (u, l), items in order
+            # every DP's items of a given (u, l) are contiguous inside that list
+            cursor = {}
+            for dp_id, b in owners:
+                for key in dict.fromkeys(zip(b.u, b.l)):
+                    cnt = sum(1 for uu, ll in zip(b.u, b.l) if (uu, ll) == key)
+                    gi = next(g for g, r in enumerate(lists) if (r.u, r.l) == key)
+                    a = cursor.get(gi, 0)
+                    out[dp_id].append(rp.rpl_range(lists[gi], a, a + cnt))
+                    cursor[gi] = a + cnt
+            dt = time.perf_counter() - t0
+            for dp_id in {o[0] for o in owners}:
+                timers.record(f"{dp_id}_AllProofs", dt)
+        return list(out.items())
 
     def _sign_range(self, sq, proved: list) -> list:
         reqs = []

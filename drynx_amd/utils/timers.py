@@ -116,6 +116,12 @@ def timed(name: str, sync: bool = True):
                 pass
 
 
+def record(name: str, seconds: float):
+    """Add an externally measured interval under ``name``."""
+    with _lock:
+        _records[name].append(seconds)
+
+
 def records() -> dict:
     with _lock:
         return {k: list(v) for k, v in _records.items()}

@@ -197,7 +197,7 @@ def test_every_operation_on_gpu(gpu_device, tmp_path, op):
                                           Lambda=1.0, Step=0.1, MaxIterations=5, InitialWeights=[0.1] * 4, K=2,
                                           PrecisionApproxCoefficients=1e2)
     bool_ops = ("min", "max", "bool_OR", "bool_AND", "union", "inter")
-    rows = [[2, 3, 5], [4, 5, 6], [3, 4, 5]]
+    rows = [[2, 3, 5], [1, 5, 6], [3, 4, 5]]  # bool ops read the DP's first value == 1
     if op in bool_ops:
         node.dp_data = {dp.id: [torch.tensor(rows[i], dtype=torch.int64, device=gpu_device)]
                         for i, dp in enumerate(cl.dps)}
@@ -206,7 +206,7 @@ def test_every_operation_on_gpu(gpu_device, tmp_path, op):
     _, vals, res = client.send_survey_query(sq)
     if op in bool_ops:
         sets = [set(r) for r in rows]
-        exp = {"min": [2.0], "max": [6.0], "bool_OR": [1.0], "bool_AND": [0.0],
+        exp = {"min": [1.0], "max": [6.0], "bool_OR": [1.0], "bool_AND": [0.0],
                "union": [float(any(i in s for s in sets)) for i in range(7)],
                "inter": [float(all(i in s for s in sets)) for i in range(7)]}[op]
         assert vals[0] == exp
