@@ -23,7 +23,9 @@ import numpy as np
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libdrynx_native.so")
+# DRYNX_NATIVE_LIB selects another build of the library (e.g. the host-sanitizer
+# build, build/libdrynx_native_asan.so); default: the in-tree gfx950 build
+LIB_PATH = os.environ.get("DRYNX_NATIVE_LIB") or os.path.join(_HERE, "libdrynx_native.so")
 
 _lib = None
 

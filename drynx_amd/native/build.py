@@ -46,14 +46,22 @@ def _digest(paths):
     return h.hexdigest()
 
 
-def _compile(src, hdr_digest):
-    os.makedirs(OBJDIR, exist_ok=True)
-    key = _digest([src]) + hdr_digest
-    obj = os.path.join(OBJDIR, os.path.basename(src) + ".o")
+# host-side sanitizers for the CPU path of every op: -fsanitize
+# goes to the host compilation only (-Xarch_host), never into gfx950 code
+SAN_FLAGS = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined",
+             "-Xarch_host", "-fno-omit-frame-pointer", "-Xarch_host", "-fno-sanitize-recover=undefined"]
+SAN_LIB = os.path.join(ROOT, "build", "libdrynx_native_asan.so")
+
+
+def _compile(src, hdr_digest, sanitize=False):
+    objdir = OBJDIR + ("_asan" if sanitize else "")
+    os.makedirs(objdir, exist_ok=True)
+    key = _digest([src]) + hdr_digest + ("san" if sanitize else "")
+    obj = os.path.join(objdir, os.path.basename(src) + ".o")
     stamp = obj + ".stamp"
     if os.path.exists(obj) and os.path.exists(stamp) and open(stamp).read() == key:
         return obj
-    cmd = [HIPCC, *FLAGS, "-I", CSRC, "-c", src, "-o", obj]
+    cmd = [HIPCC, *FLAGS, *(SAN_FLAGS if sanitize else []), "-I", CSRC, "-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=1800)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr[-4000:]}")
@@ -83,5 +91,29 @@ def build(force: bool = False, verbose: bool = True) -> str:
     return LIB
 
 
+def build_sanitized(verbose: bool = True) -> str:
+    """build/libdrynx_native_asan.so: the same library with ASan + UBSan on the
+    host path.  Run the CPU suite against it with
+      LD_PRELOAD=$(hipcc -print-file-name=libclang_rt.asan-x86_64.so) \
+      ASAN_OPTIONS=detect_leaks=0 DRYNX_NATIVE_LIB=build/libdrynx_native_asan.so pytest -m "not gpu"
+    (``make sanitize``)."""
+    gen = os.path.join(ROOT, "tools", "gen_constants.py")
+    subprocess.run([sys.executable, gen], check=True)
+    srcs = _sources()
+    hdr_digest = _digest(_headers())
+    workers = min(len(srcs), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4)), 16)
+    with cf.ThreadPoolExecutor(max_workers=workers) as ex:
+        objs = list(ex.map(lambda s: _compile(s, hdr_digest, True), srcs))
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-shared-libasan", "-fsanitize=address,undefined",
+           "-o", SAN_LIB, *objs, "-lpthread"]
+    subprocess.run(cmd, check=True, timeout=600)
+    if verbose:
+        print(f"[drynx_amd] built {SAN_LIB}")
+    return SAN_LIB
+
+
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
+    if "--sanitize" in sys.argv:
+        build_sanitized()
+    else:
+        build(force="--force" in sys.argv)
