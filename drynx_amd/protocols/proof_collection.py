@@ -127,6 +127,10 @@ def proof_collection(ctx, sq, local_requests: list):
         for vn in vns:
             merged.update(allbm.get(vn.id, {}))
         data = skc.new_data_block(sq.SurveyID, merged, [v.identity() for v in vns])
+        if ctx.last_block is None:
+            # resume an existing chain from the root VN's ledger (restart of a
+            # node over a persisted workdir) instead of starting a new genesis
+            ctx.last_block = ctx.get_latest_block(root.id)
         block = skc.make_block(ctx.last_block, data, [v.identity() for v in vns])
     block_bytes = ctx.comm.broadcast_object(block.to_bytes() if block is not None else None, src=root.rank)
     block = skc.SkipBlock.from_bytes(block_bytes)

@@ -148,3 +148,22 @@ def test_close_db(env, tmp_path):
     assert os.path.exists(path)
     client.send_close_db("vn0", remove=True)
     assert not os.path.exists(path)
+
+
+def test_chain_resumes_after_restart(tmp_path):
+    """Checkpoint/resume: a node restarted over the same workdir appends to the
+    persisted skipchain (back link to the last block) instead of a new genesis."""
+    cl, node = local_cluster(2, 2, 1, device="cpu", workdir=str(tmp_path), deterministic_keys=True)
+    client = DrynxClient(node)
+    sq = make_survey(client, cl, "sum", query_min=0, query_max=3, rows=4, proofs=1, ranges=[16, 2])
+    _, _, res1 = client.send_survey_query(sq)
+    node.close()
+    cl2, node2 = local_cluster(2, 2, 1, device="cpu", workdir=str(tmp_path), deterministic_keys=True)
+    client2 = DrynxClient(node2)
+    sq2 = make_survey(client2, cl2, "sum", query_min=0, query_max=3, rows=4, proofs=1, ranges=[16, 2])
+    _, _, res2 = client2.send_survey_query(sq2)
+    assert res2.block.Index == res1.block.Index + 1
+    assert res2.block.BackLink == res1.block.Hash
+    assert res2.block.GenesisID == res1.block.GenesisID
+    assert node2.get_genesis("vn0").Hash == res1.block.GenesisID
+    node2.close(remove=True)
