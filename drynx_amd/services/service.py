@@ -38,6 +38,7 @@ from ..protocols import data_collection as dcp
 from ..protocols import proof_collection as pcp
 from ..query import PublishSignatureBytes, SurveyQuery, add_diff_p, check_parameters, ivsigs_digest
 from ..utils import timers
+from ..utils.faults import FaultPlan
 from ..utils.log import get_logger
 
 log = get_logger("service")
@@ -74,6 +75,7 @@ class DrynxNode:
         self.local_bitmaps: dict = {}
         self.last_block: SkipBlock | None = None
         self.surveys: dict = {}
+        self.fault_plan = FaultPlan.from_env()  # misbehaving parties (tests / simulations)
 
     # ------------------------------------------------------------------ VN storage
     def store(self, vn_id: str) -> Store:
@@ -129,6 +131,8 @@ class DrynxNode:
             proofs.extend(range_future.result())
             if hasattr(self, "_prove_stream"):
                 torch.cuda.current_stream(self.device).wait_stream(self._prove_stream)
+        if self.fault_plan:
+            self.fault_plan.apply(proofs, lambda pid: self.cluster.by_id(pid).keypair.secret)
         block = None
         if q.Proofs and q.RosterVNs is not None and len(q.RosterVNs.list):
             block = pcp.proof_collection(self, sq, proofs)

@@ -167,3 +167,24 @@ def test_chain_resumes_after_restart(tmp_path):
     assert res2.block.GenesisID == res1.block.GenesisID
     assert node2.get_genesis("vn0").Hash == res1.block.GenesisID
     node2.close(remove=True)
+
+
+def test_fault_plan_marks_malicious_parties(tmp_path):
+    """FaultPlan: a DP with a corrupted range proof -> 0, a CN with a
+    forged key-switch envelope -> 4, an honest CN's aggregation proof -> 1."""
+    from drynx_amd.utils.faults import FaultPlan
+
+    cl, node = local_cluster(3, 3, 2, device="cpu", workdir=str(tmp_path))
+    client = DrynxClient(node)
+    node.fault_plan = FaultPlan({("dp1", "range"): "corrupt_proof", ("cn2", "keyswitch"): "bad_signature",
+                                 ("cn0", "aggregation"): "corrupt_proof"})
+    sq = make_survey(client, cl, "sum", query_min=0, query_max=3, rows=4, proofs=1, ranges=[16, 2])
+    _, _, res = client.send_survey_query(sq)
+    codes = res.block.data_block().Proofs
+    by = lambda frag: {v for k, v in codes.items() if frag in k}  # noqa: E731
+    assert by("/range/dp1/") == {prq.PROOF_FALSE}
+    assert by("/range/dp0/") == by("/range/dp2/") == {prq.PROOF_TRUE}
+    assert by("/keyswitch/cn2/") == {prq.PROOF_FALSE_SIGN}
+    assert by("/keyswitch/cn0/") == {prq.PROOF_TRUE}
+    assert by("/aggregation/cn0/") == {prq.PROOF_FALSE}
+    node.close(remove=True)
