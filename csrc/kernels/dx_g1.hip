@@ -71,6 +71,16 @@ int dx_g1_fb_mul(int on_gpu, void *stream, const uint32_t *table, const uint32_t
   return run(on_gpu, stream, n, op, true, "g1_fb_mul");
 }
 
+// k_i * base_{tab_idx[i]}: fixed-base multiplication over several comb tables.
+int dx_g1_fb_mul_idx(int on_gpu, void *stream, const uint32_t *tables, const int32_t *tab_idx,
+                     const uint32_t *scalars, uint32_t *out, int64_t n) {
+  auto op = [=] __host__ __device__(int64_t i) {
+    const G1A *T = reinterpret_cast<const G1A *>(tables) + (int64_t)tab_idx[i] * 8192;
+    at<G1J>(out, i) = fixed_base_mul(T, scalars + 8 * i);
+  };
+  return run(on_gpu, stream, n, op, true, "g1_fb_mul_idx");
+}
+
 // m * base for signed 64-bit m (unlynx IntToPoint).
 int dx_g1_fb_mul_i64(int on_gpu, void *stream, const uint32_t *table, const int64_t *m, uint32_t *out, int64_t n) {
   auto op = [=] __host__ __device__(int64_t i) {

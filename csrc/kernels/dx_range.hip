@@ -95,7 +95,12 @@ constexpr int kVW = 64;
 __global__ void __launch_bounds__(kVW) rp_verify_fold_kernel(const uint32_t *ZB_jac, const uint32_t *Y_jac,
                                                               const uint32_t *rho, const uint32_t *V_aff,
                                                               uint32_t *f_blk, int64_t n_items, int S, int L) {
-  __shared__ Fp12 sf[kVW];
+  // 32 Fp12 of LDS (12 KiB): the upper half of the live lanes hands its value
+  // down each level.  With 24 KiB (one slot per lane) the LDS capped a CU at 6
+  // of these workgroups, so a 99392-item batch (1553 workgroups) left 17 for a
+  // second, nearly empty round; at 12 KiB the register file (2 waves per SIMD,
+  // 8 per CU) is the cap and the whole batch is resident at once.
+  __shared__ Fp12 sf[kVW / 2];
   const int lane = threadIdx.x;
   const int64_t it = (int64_t)blockIdx.x * kVW + lane;
   Fp12 f = Fp12::one();
@@ -107,13 +112,13 @@ __global__ void __launch_bounds__(kVW) rp_verify_fold_kernel(const uint32_t *ZB_
     G1A P = to_affine(scalar_mul(T, rho + 8 * it));
     f = miller_loop(P, at<G2A>(V_aff, it));
   }
-  sf[lane] = f;
-  __syncthreads();
   for (int s = kVW / 2; s > 0; s >>= 1) {
-    if (lane < s) sf[lane] = mul(sf[lane], sf[lane + s]);
+    if (lane >= s && lane < 2 * s) sf[lane - s] = f;
+    __syncthreads();
+    if (lane < s) f = mul(f, sf[lane]);
     __syncthreads();
   }
-  if (lane == 0) at<Fp12>(f_blk, blockIdx.x) = sf[0];
+  if (lane == 0) at<Fp12>(f_blk, blockIdx.x) = f;
 }
 }  // namespace
 

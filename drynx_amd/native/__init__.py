@@ -58,6 +58,7 @@ _SIGS = {
     "dx_g1_fb_table": [_I, _P, _P, _P, _P, _L],
     "dx_g1_fb_mul": [_I, _P, _P, _P, _P, _L],
     "dx_g1_fb_mul_i64": [_I, _P, _P, _P, _P, _L],
+    "dx_g1_fb_mul_idx": [_I, _P, _P, _P, _P, _P, _L],
     "dx_g1_mul": [_I, _P, _P, _P, _P, _L, _I, _I],
     "dx_g1_add": [_I, _P, _P, _P, _P, _L, _I, _I],
     "dx_g1_to_affine": [_I, _P, _P, _P, _L],
@@ -195,6 +196,16 @@ def g1_fb_mul(table: torch.Tensor, scalars: torch.Tensor) -> torch.Tensor:
     out = torch.empty((n, 24), dtype=torch.int32, device=scalars.device)
     g, s = _ctx(table, scalars)
     _call("dx_g1_fb_mul", g, s, _ptr(table), _ptr(scalars), _ptr(out), n)
+    return out
+
+
+def g1_fb_mul_idx(tables: torch.Tensor, tab_idx: torch.Tensor, scalars: torch.Tensor) -> torch.Tensor:
+    """k_i * base_{tab_idx[i]} over stacked comb tables [n_bases*8192, 16]."""
+    n = _rows(scalars, 8)
+    assert tab_idx.dtype == torch.int32 and tab_idx.numel() == n
+    out = torch.empty((n, 24), dtype=torch.int32, device=scalars.device)
+    g, s = _ctx(tables, tab_idx, scalars)
+    _call("dx_g1_fb_mul_idx", g, s, _ptr(tables), _ptr(tab_idx), _ptr(scalars), _ptr(out), n)
     return out
 
 
@@ -577,15 +588,22 @@ def rp_verify_products(ZB_jac, Y_jac, rho, V_aff, a, S: int, L: int):
     if not g:
         f, gg = rp_verify_items(ZB_jac, Y_jac, rho, V_aff, a, S, L)
         return gt_prod(f.view(-1, 1, 96), chunk=4).view(1, 96), gt_prod(gg.view(-1, 1, 96), chunk=4).view(1, 96)
-    n = _rows(V_aff, 32)
     plan = _multi_exp64_plan(rho)  # index work first: its one host sync does not wait for the Miller fold
-    nb = (n + 63) // 64
-    fb = torch.empty((nb, 96), dtype=torch.int32, device=V_aff.device)
+    fb = rp_verify_fold(ZB_jac, Y_jac, rho, V_aff, S, L)
+    G = _multi_exp64_run(a, plan)
+    return _finish_prod_on_host(fb), G
+
+
+def rp_verify_fold(ZB_jac, Y_jac, rho, V_aff, S: int, L: int) -> torch.Tensor:
+    """Launch the fused Miller fold (GPU, asynchronous): [ceil(n/64), 96]
+    per-workgroup Miller products on the current stream."""
+    n = _rows(V_aff, 32)
+    _, s = _ctx(ZB_jac, Y_jac, rho, V_aff)
+    fb = torch.empty(((n + 63) // 64, 96), dtype=torch.int32, device=V_aff.device)
     rc = _load().dx_rp_verify_fold(s, _ptr(ZB_jac), _ptr(Y_jac), _ptr(rho), _ptr(V_aff), _ptr(fb), n, S, L)
     if rc:
         raise RuntimeError(f"dx_rp_verify_fold failed rc={rc}")
-    G = _multi_exp64_run(a, plan)
-    return _finish_prod_on_host(fb), G
+    return fb
 
 
 def gt_slice_prod(src: torch.Tensor, idx, start: torch.Tensor, length: torch.Tensor) -> torch.Tensor:
@@ -645,7 +663,12 @@ def _bucket_plan(k: torch.Tensor, W: int):
     bk = counts.nonzero()[0]
     passes = [(torch.from_numpy(st).to(dev), torch.from_numpy(ln.astype("int32")).to(dev))
               for st, ln in _segment_passes(counts[bk])]
-    return {"item": item, "passes": passes, "bk": bk, "single": not passes}
+    # bucket digits and scatter slots, staged now so the run needs no host->device copy
+    sc = torch.zeros((bk.size, 8), dtype=torch.int32)
+    sc[:, 0] = torch.from_numpy((bk % 256).astype("int32"))
+    slot = torch.from_numpy((bk % 256) * W + bk // 256)
+    return {"item": item, "passes": passes, "bk": bk, "single": not passes,
+            "digit_sc": sc.to(dev), "slot": slot.to(dev)}
 
 
 def _multi_exp64_run(a: torch.Tensor, plan) -> torch.Tensor:
@@ -659,11 +682,9 @@ def _multi_exp64_run(a: torch.Tensor, plan) -> torch.Tensor:
     cur = a.index_select(0, plan["item"]).contiguous() if plan["single"] else None
     for k, (st, ln) in enumerate(plan["passes"]):
         cur = gt_slice_prod(a if k == 0 else cur, plan["item"] if k == 0 else None, st, ln)
-    sc = torch.zeros((bk.size, 8), dtype=torch.int32)
-    sc[:, 0] = torch.from_numpy((bk % 256).astype("int32"))
-    bkp = gt_pow(cur, sc.to(dev))
+    bkp = gt_pow(cur, plan["digit_sc"])
     win = gt_one(dev).repeat(256 * _ME_W, 1)
-    win[torch.from_numpy((bk % 256) * _ME_W + bk // 256).to(dev)] = bkp
+    win[plan["slot"]] = bkp
     win = _gt_prod_level(win.view(256, _ME_W, 96), 8) if dev.type == "cuda" else win.view(256, _ME_W, 96)
     S_w = gt_prod(win.cpu(), chunk=4)                                  # [W, 96] on the host
     acc = S_w[_ME_W - 1: _ME_W].contiguous()

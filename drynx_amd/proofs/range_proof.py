@@ -101,6 +101,25 @@ class SigMaterial:
             canon.append(first.setdefault(k, i))
         self.canon = torch.tensor(canon, dtype=torch.long)  # A index -> first index with the same point
         self._ptab = {}
+        # distinct CN keys y_{i,col} (one per CN when the signature sets reuse
+        # a key, as InitRangeProofSignatureDeterministic does): comb tables let
+        # the verifier's c*y_i be fixed-base multiplications
+        ykeys = [O.g1_to_bytes(y) for y in ys]
+        yfirst: dict = {}
+        self.y_slot = [yfirst.setdefault(k, len(yfirst)) for k in ykeys]
+        self.y_distinct = [ys[ykeys.index(k)] for k in yfirst]
+        self._ytab = {}
+
+    def y_tables(self, device):
+        """(comb tables [n_distinct*8192, 16], slot per y index) or None when
+        there are too many distinct keys (0.5 MiB of HBM per table, <= 256)."""
+        if not self.y_distinct or len(self.y_distinct) > 256:
+            return None
+        key = str(torch.device(device))
+        if key not in self._ytab:
+            aff = bn.g1_aff_tensor(self.y_distinct, device)
+            self._ytab[key] = (nt.g1_fb_table(aff), torch.tensor(self.y_slot, dtype=torch.int32, device=device))
+        return self._ytab[key]
 
     def prover_tables(self, a_idx: torch.Tensor, device):
         """Comb tables (G2 for V = v*A, GT for e(B, A)) of the distinct signature
@@ -474,10 +493,28 @@ def verify_range_proof_list(rpl: RangeProofList, sigmat: SigMaterial, P_point, t
     ZB = nt.g1_fb_mul(tabB, r.zphi)                                  # [n*l]
     cols_t = torch.tensor(r.cols, dtype=torch.long, device=device)
     y_idx = (torch.arange(S, device=device).view(1, S) * sigmat.n_cols + cols_t.view(n, 1)).reshape(-1)
-    Ysel = sigmat.y_jac.to(device).index_select(0, y_idx).contiguous()
-    Y = nt.g1_mul(Ysel, _rep(r.challenge, S))                         # [n*S]
+    ytabs = sigmat.y_tables(device)
+    if ytabs is not None:                                             # c * y_i as fixed-base mults
+        Y = nt.g1_fb_mul_idx(ytabs[0], ytabs[1].index_select(0, y_idx).contiguous(), _rep(r.challenge, S))
+    else:
+        Ysel = sigmat.y_jac.to(device).index_select(0, y_idx).contiguous()
+        Y = nt.g1_mul(Ysel, _rep(r.challenge, S))                     # [n*S]
     rho = _rand64(n * S * l, device)
-    F, G = nt.rp_verify_products(ZB, Y, rho, r.V, r.A, S, l)         # Miller product, prod a^rho
+    if device.type == "cuda":
+        # GT multi-exponentiation of prod a^rho on an auxiliary stream: its bucket
+        # plan (one host sync) overlaps the fold's inputs, and its kernels are
+        # queued behind the Miller fold so they fill the CUs of the fold's last,
+        # partial round of waves
+        cur, aux = torch.cuda.current_stream(device), _aux_stream(device)
+        aux.wait_stream(cur)
+        with torch.cuda.stream(aux):
+            plan = nt._multi_exp64_plan(rho)
+        fb = nt.rp_verify_fold(ZB, Y, rho, r.V, S, l)                 # Miller values, LDS-folded
+        with torch.cuda.stream(aux):
+            G = nt._multi_exp64_run(r.A, plan)                         # prod a^rho (host tensor)
+        F = nt._finish_prod_on_host(fb)
+    else:
+        F, G = nt.rp_verify_products(ZB, Y, rho, r.V, r.A, S, l)     # Miller product, prod a^rho
     e = _fr_sum_rows(nt.fr_arith(nt.FR_MUL, rho, r.zv), 1)           # sum rho Zv
     # the closing single-element work (one final exponentiation, one GT power)
     # is a serial Fp12 chain: it runs on the host, where one core beats one GPU lane
@@ -487,6 +524,16 @@ def verify_range_proof_list(rpl: RangeProofList, sigmat: SigMaterial, P_point, t
     _, gt_tab = gt_generator_table("cpu")
     rhs_gt = nt.gt_fb_pow(gt_tab, e)
     return bool(nt.gt_eq(lhs_gt, rhs_gt).all())
+
+
+_aux: dict = {}
+
+
+def _aux_stream(device):
+    key = str(device)
+    if key not in _aux:
+        _aux[key] = torch.cuda.Stream(device)
+    return _aux[key]
 
 
 def rpl_cat(lists: list) -> RangeProofList:
