@@ -646,20 +646,24 @@ def _multi_exp64_plan(rho: torch.Tensor):
     return _bucket_plan(rho, _ME_W)
 
 
-def _bucket_plan(k: torch.Tensor, W: int):
+def _bucket_plan(k: torch.Tensor, W: int, group: torch.Tensor | None = None, n_groups: int = 1):
     """Bucket plan of a multi-scalar product over the low W bytes of the
-    scalars k [n, 8]: window w, digit d -> bucket w*256+d; entries sorted by
-    bucket, then segmented passes down to one value per non-empty bucket."""
+    scalars k [n, 8]: window w, digit d -> bucket w*256+d (plus g*W*256 for
+    entries of group g when `group` is given); entries sorted by bucket, then
+    segmented passes down to one value per non-empty bucket."""
     dev = k.device
     n = k.shape[0]
     digits = k.contiguous().view(torch.uint8).view(n, 32)[:, :W].to(torch.int64)   # little-endian bytes
-    keys = (torch.arange(W, device=dev).view(1, -1) * 256 + digits).reshape(-1)
+    keys = torch.arange(W, device=dev).view(1, -1) * 256 + digits
+    if group is not None:
+        keys = keys + group.to(device=dev, dtype=torch.int64).view(-1, 1) * (W * 256)
+    keys = keys.reshape(-1)
     item = torch.arange(n, device=dev).view(-1, 1).expand(n, W).reshape(-1)
     keep = digits.reshape(-1) != 0
     keys, item = keys[keep], item[keep]
     keys, order = torch.sort(keys)
     item = item[order].contiguous()
-    counts = torch.bincount(keys, minlength=W * 256).cpu().numpy()  # the one host sync
+    counts = torch.bincount(keys, minlength=W * 256 * n_groups).cpu().numpy()  # the one host sync
     bk = counts.nonzero()[0]
     passes = [(torch.from_numpy(st).to(dev), torch.from_numpy(ln.astype("int32")).to(dev))
               for st, ln in _segment_passes(counts[bk])]
@@ -709,36 +713,69 @@ def g1_msm(P_jac: torch.Tensor, k: torch.Tensor, bits: int = 256) -> torch.Tenso
     (no per-point 256-step doubling chain: the cost is ~bits/8 additions per
     point), bucket weights d*B_{w,d} are one short variable-base launch, and
     the 32-window Horner combination runs on the host pool."""
-    from ..crypto.bn254 import g1_infinity_jac
+    return g1_msm_grouped(P_jac, k, None, 1, bits)
 
+
+def g1_msm_grouped(P_jac: torch.Tensor, k: torch.Tensor, group: torch.Tensor | None, n_groups: int,
+                   bits: int = 256) -> torch.Tensor:
+    """G independent MSMs in one bucket pass: out[g] = sum_{i: group_i = g}
+    k_i P_i -> [n_groups, 24] HOST Jacobian points.  Only non-zero 8-bit
+    digits enter a bucket, so a 64-bit weight costs 8 bucket additions, not
+    32: batch verifiers keep the short random weights in their own group and
+    apply the shared full-size factor (a challenge) to the group's sum on the
+    host, instead of multiplying it into every per-element scalar."""
+    return g1_msm_finish(g1_msm_launch(P_jac, k, group, n_groups, bits))
+
+
+def g1_msm_launch(P_jac: torch.Tensor, k: torch.Tensor, group: torch.Tensor | None, n_groups: int,
+                  bits: int = 256) -> dict:
+    """First half of g1_msm_grouped: the bucket plan (one host sync on k) and
+    every device pass, queued on the current stream.  g1_msm_finish waits for
+    them and runs the Horner steps on the host."""
     assert P_jac.shape[0] == k.shape[0]
+    assert group is None or group.numel() == k.shape[0]
     dev = P_jac.device
     W = (bits + 7) // 8
+    h = {"n_groups": n_groups, "W": W, "S_w": None}
     if P_jac.shape[0] == 0:
-        return g1_infinity_jac(1, "cpu")
-    plan = _bucket_plan(k, W)
+        return h
+    plan = _bucket_plan(k, W, group, n_groups)
     bk = plan["bk"]
     if bk.size == 0:
-        return g1_infinity_jac(1, "cpu")
+        return h
     P_jac = P_jac.contiguous()
     cur = P_jac.index_select(0, plan["item"]).contiguous() if plan["single"] else None
     for i, (st, ln) in enumerate(plan["passes"]):
         cur = g1_slice_sum(P_jac if i == 0 else cur, plan["item"] if i == 0 else None, st, ln)
     sc = torch.zeros((bk.size, 8), dtype=torch.int32)
     sc[:, 0] = torch.from_numpy((bk % 256).astype("int32"))
-    weighted = g1_mul(cur, sc.to(dev))                                   # d * B_{w,d}
-    # per-window sums: buckets are sorted by key = w*256 + d, so windows are contiguous runs
-    w_of = bk // 256
-    wins, counts = np.unique(w_of, return_counts=True)
+    weighted = g1_mul(cur, sc.to(dev))                                   # d * B_{g,w,d}
+    # per-(group, window) sums: buckets are sorted by key = (g*W + w)*256 + d,
+    # so each (group, window) is a contiguous run
+    gws, counts = np.unique(bk // 256, return_counts=True)
     cur = weighted
     for st, ln in _segment_passes(counts):
         cur = g1_slice_sum(cur, None, torch.from_numpy(st).to(dev), torch.from_numpy(ln.astype("int32")).to(dev))
-    S_w = cur.cpu()                                                      # [len(wins), 24]
-    sh = torch.zeros((len(wins), 8), dtype=torch.int32)
-    for j, w in enumerate(wins.tolist()):
+    h["S_w"], h["gws"] = cur, gws
+    return h
+
+
+def g1_msm_finish(h: dict) -> torch.Tensor:
+    from ..crypto.bn254 import g1_infinity_jac
+
+    out = g1_infinity_jac(h["n_groups"], "cpu")
+    if h["S_w"] is None:
+        return out
+    W, gws = h["W"], h["gws"]
+    S_w = h["S_w"].cpu()                                                 # [len(gws), 24]
+    sh = torch.zeros((len(gws), 8), dtype=torch.int32)
+    for j, w in enumerate((gws % W).tolist()):
         sh[j, (8 * w) // 32] = 1 << ((8 * w) % 32)
-    T = g1_mul(S_w.contiguous(), sh)                                     # 2^{8w} S_w on the host pool
-    return g1_sum(T.view(-1, 1, 24)).view(1, 24)
+    T = g1_mul(S_w.contiguous(), sh)                                     # 2^{8w} S_{g,w} on the host pool
+    g_of = gws // W
+    for g in np.unique(g_of).tolist():
+        out[g] = g1_sum(T[torch.from_numpy(np.nonzero(g_of == g)[0])].view(-1, 1, 24)).view(24)
+    return out
 
 
 _gt_one_cache: dict = {}

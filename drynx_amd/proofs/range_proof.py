@@ -479,16 +479,26 @@ def verify_range_proof_list(rpl: RangeProofList, sigmat: SigMaterial, P_point, t
     uj = _powers(u, l, device).repeat(n, 1)
     z = _fr_sum_rows(nt.fr_arith(nt.FR_MUL, r.zphi, uj), n)
     # all n D-equations as one random linear combination (weights w_p, 64 bit):
-    #   sum w c C' + (sum w Zr) P + (sum w z) B - sum w D == O   -- one Pippenger MSM
-    with timers.span("rp.verify.dcheck"):
-        w = _rand64(n, device)
-        negD = nt.g1_add(bn.g1_infinity_jac(n, device), r.D.contiguous(), subtract=True)
-        pts = torch.cat([Cp.contiguous(), negD, bn.g1_jac_tensor([P_point, O.G1_GEN], device)])
-        sc = torch.cat([nt.fr_arith(nt.FR_MUL, w, r.challenge), w,
-                        _fr_sum_rows(nt.fr_arith(nt.FR_MUL, w, r.zr), 1),
-                        _fr_sum_rows(nt.fr_arith(nt.FR_MUL, w, z), 1)])
-        if bool(nt.g1_msm(pts.contiguous(), sc.contiguous())[0, 16:24].any()):
-            return False
+    #   sum (w c) C' + (sum w Zr) P + (sum w z) B == sum w D
+    # -- one grouped Pippenger MSM (the D side keeps its 64-bit weights).  On
+    # the GPU it runs on its own stream AFTER the Miller fold is queued, so its
+    # host-side bucket plans and Horner steps overlap the fold.
+    w = _rand64(n, device)
+    dpts = torch.cat([Cp.contiguous(), r.D.contiguous()])
+    dsc = torch.cat([nt.fr_arith(nt.FR_MUL, w, r.challenge), w])
+    dgrp = torch.cat([torch.zeros(n, dtype=torch.int32, device=device), torch.ones(n, dtype=torch.int32, device=device)])
+    dfull = torch.cat([_fr_sum_rows(nt.fr_arith(nt.FR_MUL, w, r.zr), 1), _fr_sum_rows(nt.fr_arith(nt.FR_MUL, w, z), 1)])
+
+    def dcheck_launch():
+        with timers.span("rp.verify.dcheck"):
+            return nt.g1_msm_launch(dpts, dsc, dgrp, 2, bits=256)
+
+    def dcheck_finish(h) -> bool:
+        G = nt.g1_msm_finish(h)
+        PB = nt.g1_mul(bn.g1_jac_tensor([P_point, O.G1_GEN], "cpu"), dfull.cpu())
+        lhs = nt.g1_sum(torch.stack([G[0:1], PB[0:1], PB[1:2]]))
+        return bool(nt.g1_eq(lhs, G[1:2])[0])
+
     # --- pairing equations, randomly combined
     ZB = nt.g1_fb_mul(tabB, r.zphi)                                  # [n*l]
     cols_t = torch.tensor(r.cols, dtype=torch.long, device=device)
@@ -501,10 +511,14 @@ def verify_range_proof_list(rpl: RangeProofList, sigmat: SigMaterial, P_point, t
         Y = nt.g1_mul(Ysel, _rep(r.challenge, S))                     # [n*S]
     rho = _rand64(n * S * l, device)
     if device.type == "cuda":
-        # GT multi-exponentiation of prod a^rho on an auxiliary stream: its bucket
-        # plan (one host sync) overlaps the fold's inputs, and its kernels are
-        # queued behind the Miller fold so they fill the CUs of the fold's last,
-        # partial round of waves
+        # the D-equation MSM runs to completion before the Miller fold is
+        # queued: a kernel sharing the SIMDs with the fold's waves is starved
+        # (a 128-workgroup bucket pass took 18 ms beside it, <1 ms alone), and
+        # its host steps are short (64-bit weights on the D side).  The GT
+        # multi-exponentiation's bucket plan (one host sync) is built before
+        # the fold too; its passes queue behind it on a side stream
+        if not dcheck_finish(dcheck_launch()):
+            return False
         cur, aux = torch.cuda.current_stream(device), _aux_stream(device)
         aux.wait_stream(cur)
         with torch.cuda.stream(aux):
@@ -514,6 +528,8 @@ def verify_range_proof_list(rpl: RangeProofList, sigmat: SigMaterial, P_point, t
             G = nt._multi_exp64_run(r.A, plan)                         # prod a^rho (host tensor)
         F = nt._finish_prod_on_host(fb)
     else:
+        if not dcheck_finish(dcheck_launch()):
+            return False
         F, G = nt.rp_verify_products(ZB, Y, rho, r.V, r.A, S, l)     # Miller product, prod a^rho
     e = _fr_sum_rows(nt.fr_arith(nt.FR_MUL, rho, r.zv), 1)           # sum rho Zv
     # the closing single-element work (one final exponentiation, one GT power)

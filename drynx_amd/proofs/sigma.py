@@ -352,23 +352,36 @@ def key_switch_batch_verification(proofs: list, threshold: float = 1.0) -> list:
 
 
 def _ks_combined(live) -> bool:
+    """Grouped MSM: every per-element weight stays 64 bit (8 bucket additions
+    per point instead of 32); the per-proof challenges c, zb multiply the five
+    group sums of each proof on the host."""
     dev = live[0][1].K.device
-    pts, scs = [], []
+    pts, scs, grp = [], [], []
     sB, sQ = [], []
-    for _, pr, k in live:
+    for j, (_, pr, k) in enumerate(live):
         rho, sig = _rand64(k, dev), _rand64(k, dev)
         za = pr.za[:k].contiguous()
-        c, zb = _sc([pr.c], dev), _sc([pr.zb], dev)
-        neg = lambda t: nt.fr_arith(nt.FR_NEG, t)  # noqa: E731
-        pts += [pr.T1[:k], pr.share.K[:k], pr.K[:k], pr.T2[:k], pr.share.C[:k]]
-        scs += [neg(rho), neg(nt.fr_arith(nt.FR_MUL, rho, c)), neg(nt.fr_arith(nt.FR_MUL, sig, zb)), neg(sig),
-                neg(nt.fr_arith(nt.FR_MUL, sig, c))]
+        # group 5j+0: rho T1, +1: rho vB, +2: sig K (x zb), +3: sig T2, +4: sig (vQ - xK) (x c)
+        for gi, (pt, w) in enumerate(((pr.T1, rho), (pr.share.K, rho), (pr.K, sig), (pr.T2, sig),
+                                      (pr.share.C, sig))):
+            pts.append(pt[:k])
+            scs.append(w)
+            grp.append(torch.full((k,), 5 * j + gi, dtype=torch.int32, device=dev))
         sB.append(_fr_sum(nt.fr_arith(nt.FR_MUL, rho, za)))
         sQ.append(_fr_sum(nt.fr_arith(nt.FR_MUL, sig, za)))
+    G = nt.g1_msm_grouped(torch.cat(pts).contiguous(), torch.cat(scs).contiguous(), torch.cat(grp),
+                          5 * len(live), bits=64)
     Q = live[0][1].Q
-    pts += [bn.g1_jac_tensor([O.G1_GEN], dev), bn.g1_jac_tensor([Q], dev)]
-    scs += [_fr_sum(torch.cat(sB)), _fr_sum(torch.cat(sQ))]
-    return _msm_is_zero([p.contiguous() for p in pts], scs)
+    full = torch.cat([_fr_sum(torch.cat(sB)), _fr_sum(torch.cat(sQ))]).cpu()
+    # lhs = (sum rho za) B + (sum sig za) Q; rhs = sum_j G0 + c G1 + zb G2 + G3 + c G4
+    lhs = nt.g1_add(*nt.g1_mul(bn.g1_jac_tensor([O.G1_GEN, Q], "cpu"), full).split(1))
+    facs, fpts = [], []
+    for j, (_, pr, _) in enumerate(live):
+        g = G[5 * j: 5 * j + 5]
+        facs += [1, pr.c, pr.zb, 1, pr.c]
+        fpts.append(g)
+    rhs = nt.g1_sum(nt.g1_mul(torch.cat(fpts).contiguous(), _sc(facs, "cpu")).view(-1, 1, 24))
+    return bool(nt.g1_eq(lhs, rhs)[0])
 
 
 def obfuscation_batch_verification(proofs: list, threshold: float = 1.0) -> list:
@@ -395,17 +408,31 @@ def obfuscation_batch_verification(proofs: list, threshold: float = 1.0) -> list
 
 
 def _obf_combined(live) -> bool:
+    """Grouped MSM: rho z K + sig z C (full-size weights), rho T1 + sig T2
+    and rho Ko + sig Co (64-bit weights, the latter times c on the host)."""
     dev = live[0][1].C.device
-    pts, scs = [], []
-    for _, pr, k in live:
+    pts, scs, grp = [], [], []
+    for j, (_, pr, k) in enumerate(live):
         rho, sig = _rand64(k, dev), _rand64(k, dev)
         z = pr.z[:k].contiguous()
-        c = _sc([pr.c], dev)
-        neg = lambda t: nt.fr_arith(nt.FR_NEG, t)  # noqa: E731
-        pts += [pr.C.K[:k], pr.T.K[:k], pr.Co.K[:k], pr.C.C[:k], pr.T.C[:k], pr.Co.C[:k]]
-        scs += [nt.fr_arith(nt.FR_MUL, rho, z), neg(rho), neg(nt.fr_arith(nt.FR_MUL, rho, c)),
-                nt.fr_arith(nt.FR_MUL, sig, z), neg(sig), neg(nt.fr_arith(nt.FR_MUL, sig, c))]
-    return _msm_is_zero([p.contiguous() for p in pts], scs)
+        terms = ((pr.C.K, nt.fr_arith(nt.FR_MUL, rho, z), 0), (pr.C.C, nt.fr_arith(nt.FR_MUL, sig, z), 0),
+                 (pr.T.K, rho, 1), (pr.T.C, sig, 1), (pr.Co.K, rho, 2), (pr.Co.C, sig, 2))
+        for pt, w, gi in terms:
+            pts.append(pt[:k])
+            scs.append(w)
+            grp.append(torch.full((k,), 3 * j + gi, dtype=torch.int32, device=dev))
+    pts, scs, grp = torch.cat(pts).contiguous(), torch.cat(scs).contiguous(), torch.cat(grp)
+    full = grp % 3 == 0
+    Gf = nt.g1_msm_grouped(pts[full].contiguous(), scs[full].contiguous(), grp[full] // 3, len(live))
+    Gs = nt.g1_msm_grouped(pts[~full].contiguous(), scs[~full].contiguous(), grp[~full] - grp[~full] // 3 - 1,
+                           2 * len(live), bits=64)
+    # sum_j A_j == sum_j B_j + c_j C_j
+    lhs = nt.g1_sum(Gf.view(-1, 1, 24))
+    facs = []
+    for _, pr, _ in live:
+        facs += [1, pr.c]
+    rhs = nt.g1_sum(nt.g1_mul(Gs.contiguous(), _sc(facs, "cpu")).view(-1, 1, 24))
+    return bool(nt.g1_eq(lhs, rhs)[0])
 
 
 def key_switch_list_proof_verification(pr: KeySwitchProof, threshold: float = 1.0) -> bool:

@@ -124,3 +124,22 @@ def test_gt_bucket_multi_exp64_matches_direct():
     got = nt._multi_exp64_run(a, nt._multi_exp64_plan(rho))
     ref = nt.gt_prod(nt.gt_pow(a, rho).view(-1, 1, 96), chunk=4).view(1, 96)
     assert torch.equal(got, ref)
+
+
+@pytest.mark.parametrize("bits", [64, 256])
+def test_g1_msm_grouped_matches_oracle(bits):
+    """Grouped Pippenger MSM (one bucket pass, G independent sums) vs oracle."""
+    n, G = 40, 3
+    ks = [RNG.randrange(1 << bits) % O.R for _ in range(n)]
+    ks[3] = 0
+    es = [RNG.randrange(1, O.R) for _ in range(n)]
+    grp = [RNG.randrange(G) for _ in range(n)]
+    grp[:G] = list(range(G))
+    pts = [O.g1_mul(e, O.G1_GEN) for e in es]
+    out = bn.g1_points_from_jac(nt.g1_msm_grouped(bn.g1_jac_tensor(pts), bn.scalars_tensor(ks),
+                                                  torch.tensor(grp, dtype=torch.int32), G + 1, bits=bits))
+    for g in range(G + 1):
+        exp = O.g1_mul(sum(k * e for k, e, gg in zip(ks, es, grp) if gg == g) % O.R, O.G1_GEN)
+        assert out[g] == exp
+    one = bn.g1_points_from_jac(nt.g1_msm(bn.g1_jac_tensor(pts), bn.scalars_tensor(ks)))
+    assert one[0] == O.g1_mul(sum(k * e for k, e in zip(ks, es)) % O.R, O.G1_GEN)
