@@ -28,6 +28,7 @@ import math
 from ..crypto import bls
 from ..crypto import oracle as O
 from ..proofs.sigma import schnorr_sign, schnorr_verify
+from ..wire.messages import data_block_from_wire, data_block_to_wire
 
 VERIFY_BITMAP = "VerifyBitmap"
 VERIFY_BASE = "VerifyBase"
@@ -43,11 +44,13 @@ class DataBlock:
     Proofs: dict                 # bitmap key -> code
 
     def to_bytes(self) -> bytes:
-        return json.dumps(self.__dict__, sort_keys=True).encode()
+        """network.Marshal(&DataBlock): onet envelope + dedis/protobuf body (wire/)."""
+        return data_block_to_wire(self.Roster, self.SurveyID, self.Sample, self.Time, self.ServerNumber,
+                                  self.Proofs)
 
     @staticmethod
     def from_bytes(b: bytes) -> "DataBlock":
-        return DataBlock(**json.loads(b.decode()))
+        return DataBlock(**data_block_from_wire(b))
 
 
 @dataclass

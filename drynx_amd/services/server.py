@@ -29,8 +29,8 @@ from ..crypto import oracle as O
 from ..crypto.elgamal import CipherVector, KeyPair
 from ..ledger.skipchain import SkipBlock
 from ..parallel.topology import Cluster, Party
-from ..query import SurveyQuery
 from ..utils.log import get_logger
+from ..wire.messages import survey_query_from_wire, survey_query_to_wire
 
 log = get_logger("server")
 
@@ -247,7 +247,8 @@ class NodeServer:
         cmd = msg.get("cmd")
         if cmd == "survey":
             node = self._ensure_node(msg["roles"])
-            sq = SurveyQuery.from_dict(msg["sq"]) if self.rank == 0 else None
+            # the survey travels as the reference's network.Marshal(&SurveyQuery)
+            sq = survey_query_from_wire(bytes.fromhex(msg["sq"])) if self.rank == 0 else None
             res = node.run_survey(sq)
             if self.rank == 0:
                 return {"survey_id": res.survey_id, "n_groups": res.n_groups, "n_out": res.n_out,
@@ -295,7 +296,7 @@ class RemoteNode:
     def run_survey(self, sq, on_result=None):
         from .service import SurveyResult
 
-        out = request(self.address, {"cmd": "survey", "sq": sq.to_dict(), "roles": self.roles,
+        out = request(self.address, {"cmd": "survey", "sq": survey_query_to_wire(sq).hex(), "roles": self.roles,
                                      "roster": self.roster})
         if not out.get("ok"):
             raise RuntimeError(out.get("error"))

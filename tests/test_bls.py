@@ -60,5 +60,6 @@ def test_skipchain_block_cosig():
     assert b3.verify_signatures(threshold=2 / 3)
     # tampered data breaks the hash
     b4 = skc.SkipBlock.from_bytes(b.to_bytes())
-    b4.Data = b4.Data.replace(b'"s1"', b'"s2"')
+    assert b"\x12\x02s1" in b4.Data                      # DataBlock.SurveyID (protobuf field 2)
+    b4.Data = b4.Data.replace(b"\x12\x02s1", b"\x12\x02s2")
     assert not b4.verify_signatures()
