@@ -27,15 +27,23 @@
 
 namespace dx {
 
+// Limb add/subtract with carry.  The clang builtins lower to one
+// v_add_co/v_addc_co (v_sub_co/v_subb_co) per limb with the carry kept in
+// VCC/an SGPR pair; the equivalent 64-bit C++ arithmetic was lowered to ~5
+// VALU instructions per limb on gfx950 (materialised 0/1 carries, 64-bit
+// adds, s_nop), which made the modular additions cost as much as the
+// Montgomery products around them.
 DX_HD uint32_t addc32(uint32_t a, uint32_t b, uint32_t &carry) {
-  uint64_t s = (uint64_t)a + b + carry;
-  carry = (uint32_t)(s >> 32);
-  return (uint32_t)s;
+  unsigned co;
+  const uint32_t r = __builtin_addc(a, b, carry, &co);
+  carry = co;
+  return r;
 }
 DX_HD uint32_t subb32(uint32_t a, uint32_t b, uint32_t &borrow) {
-  uint64_t d = (uint64_t)a - b - borrow;
-  borrow = (uint32_t)(d >> 63);
-  return (uint32_t)d;
+  unsigned bo;
+  const uint32_t r = __builtin_subc(a, b, borrow, &bo);
+  borrow = bo;
+  return r;
 }
 
 template <class PR>
@@ -174,6 +182,71 @@ __device__ __forceinline__ FieldT<PR> fmul(const FieldT<PR> &a, const FieldT<PR>
 #pragma unroll
   for (int i = 0; i < 8; i++) s[i] = subb32(u[i], PR::MOD[i], br);
   const bool keep = ((uint32_t)acc == 0) && br;  // u < MOD and no overflow word
+  FieldT<PR> r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = keep ? u[i] : s[i];
+  return r;
+}
+
+// Lazy reduction (device): the 512-bit product and the Montgomery reduction
+// as separate steps, so an Fp2 product reduces each output coefficient once
+// (2 reductions per 3 products instead of 3) and its additions run on the
+// unreduced halves without conditional subtractions.
+// acc(64) + hi(32) += x: one v_mad_u64_u32 with the inline constant 1.
+__device__ __forceinline__ void dx_add32(uint64_t &acc, uint32_t &hi, uint32_t x) {
+  uint64_t cy, unused;
+  asm("v_mad_u64_u32 %0, %2, %4, 1, %0\n\t"
+      "v_addc_co_u32_e64 %1, %3, %1, 0, %2"
+      : "+v"(acc), "+v"(hi), "=&s"(cy), "=&s"(unused)
+      : "v"(x));
+}
+
+// t[16] = a * b for a, b < 2^255 (product scanning, no reduction).
+__device__ __forceinline__ void fmul_wide(const uint32_t *a, const uint32_t *b, uint32_t *t) {
+  uint64_t acc = 0;
+  uint32_t hi = 0;
+#pragma unroll
+  for (int i = 0; i < 15; i++) {
+#pragma unroll
+    for (int j = (i > 7 ? i - 7 : 0); j <= (i < 7 ? i : 7); j++) dx_mac(acc, hi, a[j], b[i - j]);
+    t[i] = (uint32_t)acc;
+    acc = (acc >> 32) | ((uint64_t)hi << 32);
+    hi = 0;
+  }
+  t[15] = (uint32_t)acc;
+}
+
+// Montgomery reduction t * 2^-256 mod MOD of a 512-bit t < MOD * 2^256
+// (product scanning over the m_i * MOD columns) -> result < MOD.
+template <class PR>
+__device__ __forceinline__ FieldT<PR> fred_wide(const uint32_t *t) {
+  uint32_t m[8], u[8];
+  uint64_t acc = 0;
+  uint32_t hi = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+#pragma unroll
+    for (int j = 0; j < i; j++) dx_mac(acc, hi, m[j], PR::MOD[i - j]);
+    dx_add32(acc, hi, t[i]);
+    m[i] = (uint32_t)acc * PR::INV;
+    dx_mac(acc, hi, m[i], PR::MOD[0]);
+    acc = (acc >> 32) | ((uint64_t)hi << 32);
+    hi = 0;
+  }
+#pragma unroll
+  for (int i = 8; i < 16; i++) {
+#pragma unroll
+    for (int j = i - 7; j < 8; j++) dx_mac(acc, hi, m[j], PR::MOD[i - j]);
+    dx_add32(acc, hi, t[i]);
+    u[i - 8] = (uint32_t)acc;
+    acc = (acc >> 32) | ((uint64_t)hi << 32);
+    hi = 0;
+  }
+  // (t + m MOD) / 2^256 < 2 MOD: one conditional subtraction
+  uint32_t s[8], br = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) s[i] = subb32(u[i], PR::MOD[i], br);
+  const bool keep = ((uint32_t)acc == 0) && br;
   FieldT<PR> r;
 #pragma unroll
   for (int i = 0; i < 8; i++) r.v[i] = keep ? u[i] : s[i];

@@ -22,10 +22,41 @@ DX_HD Fp2 neg(const Fp2 &a) { return {fneg(a.c0), fneg(a.c1)}; }
 DX_HD Fp2 dbl(const Fp2 &a) { return {fdbl(a.c0), fdbl(a.c1)}; }
 DX_HD Fp2 conj(const Fp2 &a) { return {a.c0, fneg(a.c1)}; }
 DX_HD Fp2 mul(const Fp2 &a, const Fp2 &b) {
+#ifdef __HIP_DEVICE_COMPILE__
+  // Karatsuba with lazy reduction: three 512-bit products, two reductions.
+  //   c1 = (a0+a1)(b0+b1) - a0 b0 - a1 b1 = a0 b1 + a1 b0 < 2p^2
+  //   c0 = a0 b0 - a1 b1 (+ p 2^256 if negative: the reduction maps it to +p)
+  // Every reduction input is < p 2^256 (p < 2^254), as fred_wide requires.
+  uint32_t sa[8], sb[8], T0[16], T1[16], T2[16];
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) sa[i] = addc32(a.c0.v[i], a.c1.v[i], c);
+  c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) sb[i] = addc32(b.c0.v[i], b.c1.v[i], c);
+  fmul_wide(a.c0.v, b.c0.v, T0);
+  fmul_wide(a.c1.v, b.c1.v, T1);
+  fmul_wide(sa, sb, T2);
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 16; i++) T2[i] = subb32(T2[i], T0[i], br);
+  br = 0;
+#pragma unroll
+  for (int i = 0; i < 16; i++) T2[i] = subb32(T2[i], T1[i], br);
+  br = 0;
+#pragma unroll
+  for (int i = 0; i < 16; i++) T0[i] = subb32(T0[i], T1[i], br);
+  const uint32_t mask = 0u - br;
+  c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) T0[8 + i] = addc32(T0[8 + i], FpParams::MOD[i] & mask, c);
+  return {fred_wide<FpParams>(T0), fred_wide<FpParams>(T2)};
+#else
   Fp t0 = fmul(a.c0, b.c0);
   Fp t1 = fmul(a.c1, b.c1);
   Fp t2 = fmul(fadd(a.c0, a.c1), fadd(b.c0, b.c1));
   return {fsub(t0, t1), fsub(fsub(t2, t0), t1)};
+#endif
 }
 DX_HD Fp2 sqr(const Fp2 &a) {
   Fp t = fmul(a.c0, a.c1);
