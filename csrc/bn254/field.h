@@ -141,6 +141,97 @@ __device__ __forceinline__ void dx_mac(uint64_t &acc, uint32_t &hi, uint32_t x, 
       : "v"(x), "v"(y));
 }
 
+// Two to four MACs in ONE asm statement.  The hazard recognizer pads the
+// boundary between two inline-asm statements with an s_nop (it cannot see
+// that the next block only reads VGPRs), which cost one issue slot per MAC
+// when every MAC was its own statement; inside a statement the mad -> addc
+// carry hand-off needs no wait state (validated bit-exact against the oracle).
+#define DX_MAC_STEP(X, Y) "v_mad_u64_u32 %0, %2, %" #X ", %" #Y ", %0\n\tv_addc_co_u32_e64 %1, %3, %1, 0, %2\n\t"
+// YC = "v": both factors in VGPRs; YC = "s": the second factor is a uniform
+// constant (a modulus limb) read from an SGPR, so it occupies no VGPR.
+#define DX_MAC_FNS(SUF, YC)                                                                                      \
+  __device__ __forceinline__ void dx_mac1##SUF(uint64_t &acc, uint32_t &hi, uint32_t x0, uint32_t y0) {          \
+    uint64_t cy, unused;                                                                                         \
+    asm(DX_MAC_STEP(4, 5) : "+v"(acc), "+v"(hi), "=&s"(cy), "=&s"(unused) : "v"(x0), YC(y0));                   \
+  }                                                                                                              \
+  __device__ __forceinline__ void dx_mac2##SUF(uint64_t &acc, uint32_t &hi, uint32_t x0, uint32_t y0, uint32_t x1, \
+                                               uint32_t y1) {                                                    \
+    uint64_t cy, unused;                                                                                         \
+    asm(DX_MAC_STEP(4, 5) DX_MAC_STEP(6, 7)                                                                      \
+        : "+v"(acc), "+v"(hi), "=&s"(cy), "=&s"(unused) : "v"(x0), YC(y0), "v"(x1), YC(y1));                    \
+  }                                                                                                              \
+  __device__ __forceinline__ void dx_mac3##SUF(uint64_t &acc, uint32_t &hi, uint32_t x0, uint32_t y0, uint32_t x1, \
+                                               uint32_t y1, uint32_t x2, uint32_t y2) {                          \
+    uint64_t cy, unused;                                                                                         \
+    asm(DX_MAC_STEP(4, 5) DX_MAC_STEP(6, 7) DX_MAC_STEP(8, 9)                                                    \
+        : "+v"(acc), "+v"(hi), "=&s"(cy), "=&s"(unused)                                                          \
+        : "v"(x0), YC(y0), "v"(x1), YC(y1), "v"(x2), YC(y2));                                                    \
+  }                                                                                                              \
+  __device__ __forceinline__ void dx_mac4##SUF(uint64_t &acc, uint32_t &hi, uint32_t x0, uint32_t y0, uint32_t x1, \
+                                               uint32_t y1, uint32_t x2, uint32_t y2, uint32_t x3, uint32_t y3) { \
+    uint64_t cy, unused;                                                                                         \
+    asm(DX_MAC_STEP(4, 5) DX_MAC_STEP(6, 7) DX_MAC_STEP(8, 9) DX_MAC_STEP(10, 11)                                \
+        : "+v"(acc), "+v"(hi), "=&s"(cy), "=&s"(unused)                                                          \
+        : "v"(x0), YC(y0), "v"(x1), YC(y1), "v"(x2), YC(y2), "v"(x3), YC(y3));                                   \
+  }
+#define DX_YV(y) "v"(y)
+#define DX_YS(y) "s"(y)
+DX_MAC_FNS(_vv, DX_YV)
+DX_MAC_FNS(_vs, DX_YS)
+
+// Column accumulator that batches queued MACs into 4-MAC asm statements, one
+// queue for products of two variables and one for products by a modulus limb.
+// Loops around it are fully unrolled, so the counts are compile-time
+// constants at every call and the switches fold away.
+struct MacQ {
+  uint64_t acc = 0;
+  uint32_t hi = 0;
+  uint32_t xv[4], yv[4], xs[4], ys[4];
+  int nv = 0, ns = 0;
+  __device__ __forceinline__ void push(uint32_t a, uint32_t b) {
+    xv[nv] = a;
+    yv[nv] = b;
+    if (++nv == 4) flush_v();
+  }
+  __device__ __forceinline__ void push_mod(uint32_t a, uint32_t modlimb) {
+    xs[ns] = a;
+    ys[ns] = modlimb;
+    if (++ns == 4) flush_s();
+  }
+  __device__ __forceinline__ void flush_v() {
+    switch (nv) {
+      case 1: dx_mac1_vv(acc, hi, xv[0], yv[0]); break;
+      case 2: dx_mac2_vv(acc, hi, xv[0], yv[0], xv[1], yv[1]); break;
+      case 3: dx_mac3_vv(acc, hi, xv[0], yv[0], xv[1], yv[1], xv[2], yv[2]); break;
+      case 4: dx_mac4_vv(acc, hi, xv[0], yv[0], xv[1], yv[1], xv[2], yv[2], xv[3], yv[3]); break;
+      default: break;
+    }
+    nv = 0;
+  }
+  __device__ __forceinline__ void flush_s() {
+    switch (ns) {
+      case 1: dx_mac1_vs(acc, hi, xs[0], ys[0]); break;
+      case 2: dx_mac2_vs(acc, hi, xs[0], ys[0], xs[1], ys[1]); break;
+      case 3: dx_mac3_vs(acc, hi, xs[0], ys[0], xs[1], ys[1], xs[2], ys[2]); break;
+      case 4: dx_mac4_vs(acc, hi, xs[0], ys[0], xs[1], ys[1], xs[2], ys[2], xs[3], ys[3]); break;
+      default: break;
+    }
+    ns = 0;
+  }
+  __device__ __forceinline__ void flush() {
+    flush_v();
+    flush_s();
+  }
+  // flush, emit the low word of the column, shift the 96-bit accumulator
+  __device__ __forceinline__ uint32_t next_column() {
+    flush();
+    const uint32_t lo = (uint32_t)acc;
+    acc = (acc >> 32) | ((uint64_t)hi << 32);
+    hi = 0;
+    return lo;
+  }
+};
+
 // Montgomery multiplication on gfx950: finely integrated product scanning
 // (column-wise Comba, Montgomery digits m_i folded into the same columns) with
 // one 96-bit column accumulator: ~360 VALU instructions per product instead of
@@ -151,37 +242,34 @@ __device__ __forceinline__ void dx_mac(uint64_t &acc, uint32_t &hi, uint32_t x, 
 template <class PR>
 __device__ __forceinline__ FieldT<PR> fmul(const FieldT<PR> &a, const FieldT<PR> &b) {
   uint32_t m[8], u[8];
-  uint64_t acc = 0;
-  uint32_t hi = 0;
+  MacQ q;
 #pragma unroll
   for (int i = 0; i < 8; i++) {
 #pragma unroll
     for (int j = 0; j < i; j++) {
-      dx_mac(acc, hi, a.v[j], b.v[i - j]);
-      dx_mac(acc, hi, m[j], PR::MOD[i - j]);
+      q.push(a.v[j], b.v[i - j]);
+      q.push_mod(m[j], PR::MOD[i - j]);
     }
-    dx_mac(acc, hi, a.v[i], b.v[0]);
-    m[i] = (uint32_t)acc * PR::INV;
-    dx_mac(acc, hi, m[i], PR::MOD[0]);
-    acc = (acc >> 32) | ((uint64_t)hi << 32);
-    hi = 0;
+    q.push(a.v[i], b.v[0]);
+    q.flush();
+    m[i] = (uint32_t)q.acc * PR::INV;
+    q.push_mod(m[i], PR::MOD[0]);
+    (void)q.next_column();
   }
 #pragma unroll
   for (int i = 8; i < 16; i++) {
 #pragma unroll
     for (int j = i - 7; j < 8; j++) {
-      dx_mac(acc, hi, a.v[j], b.v[i - j]);
-      dx_mac(acc, hi, m[j], PR::MOD[i - j]);
+      q.push(a.v[j], b.v[i - j]);
+      q.push_mod(m[j], PR::MOD[i - j]);
     }
-    u[i - 8] = (uint32_t)acc;
-    acc = (acc >> 32) | ((uint64_t)hi << 32);
-    hi = 0;
+    u[i - 8] = q.next_column();
   }
   // result = u + 2^256 * acc < 2 MOD: one conditional subtraction
   uint32_t s[8], br = 0;
 #pragma unroll
   for (int i = 0; i < 8; i++) s[i] = subb32(u[i], PR::MOD[i], br);
-  const bool keep = ((uint32_t)acc == 0) && br;  // u < MOD and no overflow word
+  const bool keep = ((uint32_t)q.acc == 0) && br;  // u < MOD and no overflow word
   FieldT<PR> r;
 #pragma unroll
   for (int i = 0; i < 8; i++) r.v[i] = keep ? u[i] : s[i];
@@ -203,17 +291,14 @@ __device__ __forceinline__ void dx_add32(uint64_t &acc, uint32_t &hi, uint32_t x
 
 // t[16] = a * b for a, b < 2^255 (product scanning, no reduction).
 __device__ __forceinline__ void fmul_wide(const uint32_t *a, const uint32_t *b, uint32_t *t) {
-  uint64_t acc = 0;
-  uint32_t hi = 0;
+  MacQ q;
 #pragma unroll
   for (int i = 0; i < 15; i++) {
 #pragma unroll
-    for (int j = (i > 7 ? i - 7 : 0); j <= (i < 7 ? i : 7); j++) dx_mac(acc, hi, a[j], b[i - j]);
-    t[i] = (uint32_t)acc;
-    acc = (acc >> 32) | ((uint64_t)hi << 32);
-    hi = 0;
+    for (int j = (i > 7 ? i - 7 : 0); j <= (i < 7 ? i : 7); j++) q.push(a[j], b[i - j]);
+    t[i] = q.next_column();
   }
-  t[15] = (uint32_t)acc;
+  t[15] = (uint32_t)q.acc;
 }
 
 // Montgomery reduction t * 2^-256 mod MOD of a 512-bit t < MOD * 2^256
@@ -221,32 +306,30 @@ __device__ __forceinline__ void fmul_wide(const uint32_t *a, const uint32_t *b, 
 template <class PR>
 __device__ __forceinline__ FieldT<PR> fred_wide(const uint32_t *t) {
   uint32_t m[8], u[8];
-  uint64_t acc = 0;
-  uint32_t hi = 0;
+  MacQ q;
 #pragma unroll
   for (int i = 0; i < 8; i++) {
 #pragma unroll
-    for (int j = 0; j < i; j++) dx_mac(acc, hi, m[j], PR::MOD[i - j]);
-    dx_add32(acc, hi, t[i]);
-    m[i] = (uint32_t)acc * PR::INV;
-    dx_mac(acc, hi, m[i], PR::MOD[0]);
-    acc = (acc >> 32) | ((uint64_t)hi << 32);
-    hi = 0;
+    for (int j = 0; j < i; j++) q.push_mod(m[j], PR::MOD[i - j]);
+    q.flush();
+    dx_add32(q.acc, q.hi, t[i]);
+    m[i] = (uint32_t)q.acc * PR::INV;
+    q.push_mod(m[i], PR::MOD[0]);
+    (void)q.next_column();
   }
 #pragma unroll
   for (int i = 8; i < 16; i++) {
 #pragma unroll
-    for (int j = i - 7; j < 8; j++) dx_mac(acc, hi, m[j], PR::MOD[i - j]);
-    dx_add32(acc, hi, t[i]);
-    u[i - 8] = (uint32_t)acc;
-    acc = (acc >> 32) | ((uint64_t)hi << 32);
-    hi = 0;
+    for (int j = i - 7; j < 8; j++) q.push_mod(m[j], PR::MOD[i - j]);
+    q.flush();
+    dx_add32(q.acc, q.hi, t[i]);
+    u[i - 8] = q.next_column();
   }
   // (t + m MOD) / 2^256 < 2 MOD: one conditional subtraction
   uint32_t s[8], br = 0;
 #pragma unroll
   for (int i = 0; i < 8; i++) s[i] = subb32(u[i], PR::MOD[i], br);
-  const bool keep = ((uint32_t)acc == 0) && br;
+  const bool keep = ((uint32_t)q.acc == 0) && br;
   FieldT<PR> r;
 #pragma unroll
   for (int i = 0; i < 8; i++) r.v[i] = keep ? u[i] : s[i];
