@@ -36,6 +36,32 @@ int dx_fr_arith(int on_gpu, void *stream, int opc, const uint32_t *a, const uint
   return run(on_gpu, stream, n, op, false, "fr_arith");
 }
 
+// Chunked Fr dot products / sums of canonical scalars, per group of m rows:
+//   out[g * n_chunks + c] = sum_{k in chunk c} a[g*m + k] * B(g, k)
+// with B = 1 (b == null), b[g*m + k] (b_periodic == 0) or b[k] (b_periodic == 1).
+// A batch verifier's weighted sums (sum rho_i Zv_i over 10^5 items) take
+// ceil(log_chunk m) launches instead of a log2(m)-deep pairwise tree.
+int dx_fr_dot_chunks(int on_gpu, void *stream, const uint32_t *a, const uint32_t *b, int b_periodic, uint32_t *out,
+                     int64_t groups, int64_t m, int64_t chunk) {
+  const int64_t n_chunks = (m + chunk - 1) / chunk;
+  auto op = [=] __host__ __device__(int64_t t) {
+    const int64_t g = t / n_chunks, c = t % n_chunks;
+    const int64_t s = c * chunk, e = s + chunk < m ? s + chunk : m;
+    const Fr r2 = Fr::from_limbs(FrParams::R2);
+    Fr acc = Fr::zero();
+    for (int64_t k = s; k < e; k++) {
+      Fr x = reduce_256<FrParams>(a + 8 * (g * m + k));
+      if (b) {
+        const Fr y = reduce_256<FrParams>(b + 8 * (b_periodic ? k : g * m + k));
+        x = fmul(fmul(x, y), r2);  // x y R^-1 R^2 R^-1 = x y (canonical)
+      }
+      acc = fadd(acc, x);
+    }
+    at<Fr>(out, t) = acc;
+  };
+  return run(on_gpu, stream, groups * n_chunks, op, false, "fr_dot_chunks");
+}
+
 // ---------------------------------------------------------------- G1
 // Comb tables for n_bases points: table[b][w*256+d] = d * 2^(8w) * base_b (affine).
 // Two phases: (1) one thread per base walks the 256 doublings 2^k * base into

@@ -55,6 +55,8 @@ _SIGS = {
     "dx_fp_to_mont": [_I, _P, _P, _P, _L],
     "dx_fp_from_mont": [_I, _P, _P, _P, _L],
     "dx_fr_arith": [_I, _P, _I, _P, _P, _P, _L, _I],
+    "dx_fr_dot_chunks": [_I, _P, _P, _P, _I, _P, _L, _L, _L],
+    "dx_rp_challenges": [_I, _P, _P, _P, _P, _P, _P, _L],
     "dx_g1_fb_table": [_I, _P, _P, _P, _P, _L],
     "dx_g1_fb_mul": [_I, _P, _P, _P, _P, _L],
     "dx_g1_fb_mul_i64": [_I, _P, _P, _P, _P, _L],
@@ -177,6 +179,26 @@ def fr_arith(op: int, a: torch.Tensor, b: torch.Tensor | None = None) -> torch.T
     g, s = _ctx(a, bb)
     _call("dx_fr_arith", g, s, op, _ptr(a), _ptr(bb), _ptr(out), n, bcast)
     return out
+
+
+def fr_dot_rows(a: torch.Tensor, b: torch.Tensor | None, groups: int, b_periodic: bool = False,
+                chunk: int = 32) -> torch.Tensor:
+    """Per-group Fr sums of a[g*m + k] * b(g, k) -> [groups, 8] (canonical).
+    b: None (plain sums), [groups*m, 8] (per row) or [m, 8] (b_periodic)."""
+    n = _rows(a, 8)
+    m = n // groups
+    assert m * groups == n and m > 0
+    if b is not None:
+        assert _rows(b, 8) == (m if b_periodic else n)
+    cur, bb = a.contiguous(), None if b is None else b.contiguous()
+    while True:
+        n_chunks = (m + chunk - 1) // chunk
+        out = torch.empty((groups * n_chunks, 8), dtype=torch.int32, device=a.device)
+        g, s = _ctx(cur, bb)
+        _call("dx_fr_dot_chunks", g, s, _ptr(cur), _ptr(bb), int(b_periodic), _ptr(out), groups, m, chunk)
+        cur, bb, m = out, None, n_chunks
+        if m == 1:
+            return cur
 
 
 # ----------------------------------------------------------------------------- G1
@@ -566,6 +588,19 @@ def rp_prove_a_tab(gphi_tables, tab_idx, e_sc, t_sc, gt_table, S: int, L: int) -
     g, s = _ctx(gphi_tables, tab_idx, e_sc, t_sc, gt_table)
     _call("dx_rp_prove_a_tab", g, s, _ptr(gphi_tables), _ptr(tab_idx), _ptr(e_sc), _ptr(t_sc), _ptr(gt_table),
           _ptr(out), n, S, L)
+    return out
+
+
+def rp_challenges(C_aff: torch.Tensor, b_words: torch.Tensor, y_words: torch.Tensor,
+                  cols: torch.Tensor) -> torch.Tensor:
+    """Range-proof challenges SHA3-512(B || C_p || Y_col) mod r -> [n, 8]
+    canonical scalars (dx_keccak.hip).  b_words [16] and y_words [n_cols, 16]
+    are the 64-byte point encodings viewed as little-endian int32 words."""
+    n = _rows(C_aff, 16)
+    assert cols.dtype == torch.int32 and cols.numel() == n and b_words.numel() == 16
+    out = torch.empty((n, 8), dtype=torch.int32, device=C_aff.device)
+    g, s = _ctx(C_aff, b_words, y_words, cols)
+    _call("dx_rp_challenges", g, s, _ptr(C_aff), _ptr(b_words), _ptr(y_words), _ptr(cols), _ptr(out), n)
     return out
 
 

@@ -110,6 +110,16 @@ class SigMaterial:
         self.y_distinct = [ys[ykeys.index(k)] for k in yfirst]
         self._ytab = {}
 
+    def challenge_words(self, device):
+        """(B encoding [16], per-column sum_i y_i encodings [n_cols, 16]) as
+        little-endian int32 words for the device challenge hash."""
+        key = ("cw", str(torch.device(device)))
+        if key not in self._ytab:
+            b = np.frombuffer(O.g1_to_bytes(O.G1_GEN), dtype="<i4").copy()
+            y = np.frombuffer(b"".join(self.Ysum_bytes), dtype="<i4").reshape(-1, 16).copy()
+            self._ytab[key] = (torch.from_numpy(b).to(device), torch.from_numpy(y).to(device))
+        return self._ytab[key]
+
     def y_tables(self, device):
         """(comb tables [n_distinct*8192, 16], slot per y index) or None when
         there are too many distinct keys (0.5 MiB of HBM per table, <= 256)."""
@@ -325,20 +335,6 @@ def _rep(t: torch.Tensor, k: int) -> torch.Tensor:
     return t.repeat_interleave(k, dim=0).contiguous()
 
 
-def _fr_sum_rows(x: torch.Tensor, groups: int) -> torch.Tensor:
-    """x: [groups*m, 8] -> per-group Fr sum [groups, 8] (pairwise tree on device)."""
-    m = x.shape[0] // groups
-    cur = x.view(groups, m, 8)
-    while cur.shape[1] > 1:
-        if cur.shape[1] % 2:
-            pad = torch.zeros((groups, 1, 8), dtype=torch.int32, device=x.device)
-            cur = torch.cat([cur, pad], dim=1)
-        a = cur[:, 0::2].contiguous().view(-1, 8)
-        b = cur[:, 1::2].contiguous().view(-1, 8)
-        cur = nt.fr_arith(nt.FR_ADD, a, b).view(groups, -1, 8)
-    return cur[:, 0].contiguous()
-
-
 def _small_scalars(vals, device) -> torch.Tensor:
     a = np.zeros((len(vals), 8), dtype=np.uint32)
     v = np.asarray(vals, dtype=np.int64)
@@ -394,9 +390,8 @@ def _prove_group(u, l, vals, offs, cols, r, cv, sigmat, P_point, device) -> Rang
         phi = _digits(vals, offs, u, l)
     # Fiat–Shamir challenge per value
     with timers.span("rp.prove.challenge"):
-        C_bytes = bn.g1_aff_to_bytes(nt.g1_to_affine(cv.C))
-        c_int = _challenge_hash(C_bytes, [sigmat.Ysum_bytes[c] for c in cols])
-        c = bn.scalars_tensor(c_int, device)
+        bw, yw = sigmat.challenge_words(device)
+        c = nt.rp_challenges(nt.g1_to_affine(cv.C), bw, yw, torch.tensor(cols, dtype=torch.int32, device=device))
     # randomness
     with timers.span("rp.prove.random"):
         s = bn.random_scalars(n * l, device)
@@ -404,10 +399,8 @@ def _prove_group(u, l, vals, offs, cols, r, cv, sigmat, P_point, device) -> Rang
         m = bn.random_scalars(n * l, device)
         v = bn.random_scalars(n * S * l, device)
     # D = (sum_j u^j s_j) B + (sum_j m_j) P
-    with timers.span("rp.prove.uj"):
-        uj = _powers(u, l, device).repeat(n, 1)
-    us = _fr_sum_rows(nt.fr_arith(nt.FR_MUL, s, uj), n)
-    msum = _fr_sum_rows(m, n)
+    us = nt.fr_dot_rows(s, _powers(u, l, device), n, b_periodic=True)
+    msum = nt.fr_dot_rows(m, None, n)
     D = nt.g1_add(nt.g1_fb_mul(tabB, us), nt.g1_fb_mul(tabP, msum))
     # Zphi_j = s_j - c phi_j ; Zr = sum m - c r ; Zv_ij = t_j - c v_ij
     phi_sc = _small_scalars(phi.reshape(-1), device)
@@ -445,12 +438,12 @@ def _prove_group(u, l, vals, offs, cols, r, cv, sigmat, P_point, device) -> Rang
 
 # ----------------------------------------------------------------------------- verify
 def _rand64(n, device) -> torch.Tensor:
-    """Random 64-bit batch weights from the OS CSPRNG (unknown to the prover)."""
-    a = np.zeros((n, 8), dtype=np.uint32)
-    raw = np.frombuffer(os.urandom(8 * n), dtype="<u4").reshape(n, 2)
-    a[:, :2] = raw
-    a[:, 0] |= 1  # never zero
-    return bn.to_tensor(a, device)
+    """Random nonzero 64-bit batch weights from the ChaCha20 CSPRNG (device
+    or host path), unknown to the prover."""
+    r = bn.random_scalars(n, device)
+    r[:, 2:] = 0
+    r[:, 0] |= 1
+    return r
 
 
 def verify_range_proof_list(rpl: RangeProofList, sigmat: SigMaterial, P_point, threshold: float = 1.0,
@@ -476,18 +469,15 @@ def verify_range_proof_list(rpl: RangeProofList, sigmat: SigMaterial, P_point, t
     Cp = r.commit.C
     if any(r.offset):
         Cp = nt.g1_add(Cp, nt.g1_fb_mul_i64(tabB, torch.tensor(r.offset, dtype=torch.int64, device=device)))
-    uj = _powers(u, l, device).repeat(n, 1)
-    z = _fr_sum_rows(nt.fr_arith(nt.FR_MUL, r.zphi, uj), n)
+    z = nt.fr_dot_rows(r.zphi, _powers(u, l, device), n, b_periodic=True)   # sum_j Zphi_j u^j
     # all n D-equations as one random linear combination (weights w_p, 64 bit):
     #   sum (w c) C' + (sum w Zr) P + (sum w z) B == sum w D
-    # -- one grouped Pippenger MSM (the D side keeps its 64-bit weights).  On
-    # the GPU it runs on its own stream AFTER the Miller fold is queued, so its
-    # host-side bucket plans and Horner steps overlap the fold.
+    # -- one grouped Pippenger MSM (the D side keeps its 64-bit weights)
     w = _rand64(n, device)
     dpts = torch.cat([Cp.contiguous(), r.D.contiguous()])
     dsc = torch.cat([nt.fr_arith(nt.FR_MUL, w, r.challenge), w])
     dgrp = torch.cat([torch.zeros(n, dtype=torch.int32, device=device), torch.ones(n, dtype=torch.int32, device=device)])
-    dfull = torch.cat([_fr_sum_rows(nt.fr_arith(nt.FR_MUL, w, r.zr), 1), _fr_sum_rows(nt.fr_arith(nt.FR_MUL, w, z), 1)])
+    dfull = torch.cat([nt.fr_dot_rows(w, r.zr, 1), nt.fr_dot_rows(w, z, 1)])
 
     def dcheck_launch():
         with timers.span("rp.verify.dcheck"):
@@ -531,7 +521,7 @@ def verify_range_proof_list(rpl: RangeProofList, sigmat: SigMaterial, P_point, t
         if not dcheck_finish(dcheck_launch()):
             return False
         F, G = nt.rp_verify_products(ZB, Y, rho, r.V, r.A, S, l)     # Miller product, prod a^rho
-    e = _fr_sum_rows(nt.fr_arith(nt.FR_MUL, rho, r.zv), 1)           # sum rho Zv
+    e = nt.fr_dot_rows(rho, r.zv, 1)                                 # sum rho Zv
     # the closing single-element work (one final exponentiation, one GT power)
     # is a serial Fp12 chain: it runs on the host, where one core beats one GPU lane
     with timers.span("rp.verify.fold_wait"):

@@ -293,7 +293,9 @@ def verify_range_many(reqs: list, idxs: list, sq, device, cache: VerifierCache) 
     for i in idxs:
         try:
             lists = []
-            for r in _range_lists(reqs[i], device):
+            with timers.span("rp.verify.unpack"):
+                unpacked = _range_lists(reqs[i], device)
+            for r in unpacked:
                 if not r.has_rp:
                     continue
                 if sigs is None or not _ranges_ok(sq, r):
@@ -315,7 +317,9 @@ def verify_range_many(reqs: list, idxs: list, sq, device, cache: VerifierCache) 
         for r in parts[i]:
             groups.setdefault((r.u, r.l, r.S), []).append(r)
     try:
-        ok = all(rp.verify_range_proof_list(rp.rpl_cat(g), sigmat, P, 1.0, device) for g in groups.values())
+        with timers.span("rp.verify.cat"):
+            cats = [rp.rpl_cat(g) for g in groups.values()]
+        ok = all(rp.verify_range_proof_list(c, sigmat, P, 1.0, device) for c in cats)
     except Exception as e:
         log.warning(f"batched range verification failed: {e}")
         ok = False

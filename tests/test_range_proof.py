@@ -73,3 +73,24 @@ def test_deterministic_signature():
     a = rp.init_range_proof_signature_deterministic(3)
     b = rp.init_range_proof_signature_deterministic(3)
     assert a == b and len(a.Signature) == 3 * 128
+
+
+def test_device_challenge_hash_matches_sha3_512():
+    """dx_rp_challenges (Keccak on the device/host path) == hashlib SHA3-512 mod r."""
+    import numpy as np
+    import torch
+
+    from drynx_amd import native as nt
+    from drynx_amd.crypto import bn254 as bn
+    from drynx_amd.crypto import oracle as O
+    from drynx_amd.proofs import range_proof as rp
+
+    pts = [O.g1_mul(k, O.G1_GEN) for k in (1, 2, 3, 12345, O.R - 1)] + [None]
+    aff = bn.g1_aff_tensor(pts, "cpu")
+    ys = [O.g1_to_bytes(O.g1_mul(k, O.G1_GEN)) for k in (7, 11)]
+    cols = [0, 1, 1, 0, 1, 0]
+    bw = torch.from_numpy(np.frombuffer(O.g1_to_bytes(O.G1_GEN), dtype="<i4").copy())
+    yw = torch.from_numpy(np.frombuffer(b"".join(ys), dtype="<i4").reshape(-1, 16).copy())
+    got = bn.scalars_from_tensor(nt.rp_challenges(aff, bw, yw, torch.tensor(cols, dtype=torch.int32)))
+    exp = rp._challenge_hash(bn.g1_aff_to_bytes(aff), [ys[c] for c in cols])
+    assert got == exp
