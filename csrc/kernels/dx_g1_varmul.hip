@@ -31,7 +31,7 @@ __device__ __forceinline__ G1J lds_load(uint32_t (*tab)[24][kWG], int e, int lan
   return p;
 }
 
-__global__ void __launch_bounds__(kWG) g1_varmul_kernel(const uint32_t *__restrict__ pts, int pt_bcast,
+__global__ void __launch_bounds__(kWG) DX_OCC g1_varmul_kernel(const uint32_t *__restrict__ pts, int pt_bcast,
                                                          const uint32_t *__restrict__ sc, int k_bcast,
                                                          uint32_t *__restrict__ out, int64_t n) {
   __shared__ uint32_t tab[kEntries][24][kWG];

@@ -92,7 +92,7 @@ int dx_rp_verify_items(int on_gpu, void *stream, const uint32_t *ZB_jac, const u
 // kernel carries only the Miller-loop state.
 namespace {
 constexpr int kVW = 64;
-__global__ void __launch_bounds__(kVW) rp_verify_fold_kernel(const uint32_t *ZB_jac, const uint32_t *Y_jac,
+__global__ void __launch_bounds__(kVW) DX_OCC rp_verify_fold_kernel(const uint32_t *ZB_jac, const uint32_t *Y_jac,
                                                               const uint32_t *rho, const uint32_t *V_aff,
                                                               uint32_t *f_blk, int64_t n_items, int S, int L) {
   // 32 Fp12 of LDS (12 KiB): the upper half of the live lanes hands its value

@@ -16,8 +16,17 @@
 
 namespace dx {
 
+// Every kernel asks for at least 2 waves per SIMD.  The out-of-line tower and
+// curve functions are shared by all kernels of a translation unit, and the
+// AMDGPU attributor budgets their registers for the least demanding caller:
+// without a target on every kernel they may take 256 VGPRs plus up to ~200
+// AGPRs, i.e. 1 wave per SIMD, so a 1553-wave range fold ran as one full
+// round of 1024 waves and a half-empty second round.  At 2 waves per SIMD
+// (256 registers) the extra spills are a few call-frame slots.
+#define DX_OCC __attribute__((amdgpu_waves_per_eu(2)))
+
 template <class Op>
-__global__ void __launch_bounds__(256) for_each_kernel(int64_t n, Op op) {
+__global__ void __launch_bounds__(256) DX_OCC for_each_kernel(int64_t n, Op op) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) op(i);
 }
@@ -25,7 +34,7 @@ __global__ void __launch_bounds__(256) for_each_kernel(int64_t n, Op op) {
 // Heavy per-thread ops (pairings, scalar mults) use 64-thread blocks so many
 // workgroups exist even for modest batches (256 CUs want >>256 blocks).
 template <class Op>
-__global__ void __launch_bounds__(64) for_each_kernel64(int64_t n, Op op) {
+__global__ void __launch_bounds__(64) DX_OCC for_each_kernel64(int64_t n, Op op) {
   int64_t i = (int64_t)blockIdx.x * 64 + threadIdx.x;
   if (i < n) op(i);
 }

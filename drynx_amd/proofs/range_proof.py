@@ -484,6 +484,10 @@ def verify_range_proof_list(rpl: RangeProofList, sigmat: SigMaterial, P_point, t
             return nt.g1_msm_launch(dpts, dsc, dgrp, 2, bits=256)
 
     def dcheck_finish(h) -> bool:
+        with timers.span("rp.verify.dcheck_finish"):
+            return _dcheck_finish(h)
+
+    def _dcheck_finish(h) -> bool:
         G = nt.g1_msm_finish(h)
         PB = nt.g1_mul(bn.g1_jac_tensor([P_point, O.G1_GEN], "cpu"), dfull.cpu())
         lhs = nt.g1_sum(torch.stack([G[0:1], PB[0:1], PB[1:2]]))
@@ -501,21 +505,37 @@ def verify_range_proof_list(rpl: RangeProofList, sigmat: SigMaterial, P_point, t
         Y = nt.g1_mul(Ysel, _rep(r.challenge, S))                     # [n*S]
     rho = _rand64(n * S * l, device)
     if device.type == "cuda":
-        # the D-equation MSM runs to completion before the Miller fold is
-        # queued: a kernel sharing the SIMDs with the fold's waves is starved
-        # (a 128-workgroup bucket pass took 18 ms beside it, <1 ms alone), and
-        # its host steps are short (64-bit weights on the D side).  The GT
-        # multi-exponentiation's bucket plan (one host sync) is built before
-        # the fold too; its passes queue behind it on a side stream
-        if not dcheck_finish(dcheck_launch()):
-            return False
-        cur, aux = torch.cuda.current_stream(device), _aux_stream(device)
-        aux.wait_stream(cur)
-        with torch.cuda.stream(aux):
-            plan = nt._multi_exp64_plan(rho)
-        fb = nt.rp_verify_fold(ZB, Y, rho, r.V, S, l)                 # Miller values, LDS-folded
-        with torch.cuda.stream(aux):
-            G = nt._multi_exp64_run(r.A, plan)                         # prod a^rho (host tensor)
+        if os.environ.get("DRYNX_FOLD_FIRST", "1") == "1":
+            # the Miller fold (the long pole, ~20 ms for a 2070-value list)
+            # is queued as soon as its inputs are; the D-equation MSM and the
+            # GT multi-exponentiation run on a side stream beside it, so their
+            # host steps overlap the fold instead of delaying its launch
+            cur, aux = torch.cuda.current_stream(device), _aux_stream(device)
+            aux.wait_stream(cur)
+            fb = nt.rp_verify_fold(ZB, Y, rho, r.V, S, l)             # Miller values, LDS-folded
+            with torch.cuda.stream(aux):
+                if not dcheck_finish(dcheck_launch()):
+                    return False
+                with timers.span("rp.verify.gt_plan"):
+                    plan = nt._multi_exp64_plan(rho)
+                G = nt._multi_exp64_run(r.A, plan)                     # prod a^rho (host tensor)
+            cur.wait_stream(aux)
+        else:
+            # the D-equation MSM runs to completion before the Miller fold is
+            # queued: a kernel sharing the SIMDs with the fold's waves is starved
+            # (a 128-workgroup bucket pass took 18 ms beside it, <1 ms alone), and
+            # its host steps are short (64-bit weights on the D side).  The GT
+            # multi-exponentiation's bucket plan (one host sync) is built before
+            # the fold too; its passes queue behind it on a side stream
+            if not dcheck_finish(dcheck_launch()):
+                return False
+            cur, aux = torch.cuda.current_stream(device), _aux_stream(device)
+            aux.wait_stream(cur)
+            with torch.cuda.stream(aux), timers.span("rp.verify.gt_plan"):
+                plan = nt._multi_exp64_plan(rho)
+            fb = nt.rp_verify_fold(ZB, Y, rho, r.V, S, l)                 # Miller values, LDS-folded
+            with torch.cuda.stream(aux):
+                G = nt._multi_exp64_run(r.A, plan)                         # prod a^rho (host tensor)
         F = nt._finish_prod_on_host(fb)
     else:
         if not dcheck_finish(dcheck_launch()):

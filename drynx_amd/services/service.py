@@ -38,6 +38,7 @@ from ..protocols import data_collection as dcp
 from ..protocols import proof_collection as pcp
 from ..query import PublishSignatureBytes, SurveyQuery, add_diff_p, check_parameters, ivsigs_digest
 from ..utils import timers
+
 from ..utils.faults import FaultPlan
 from ..utils.log import get_logger
 
