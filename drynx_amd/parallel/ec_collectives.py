@@ -12,6 +12,9 @@ normalisation / big-endian conversion that the external wire format needs.
   it does a reduce-scatter by ownership (each rank sums 1/W of the rows) and
   gathers the shards to the root — on a full xGMI mesh that is 2 one-hop
   steps instead of a (W-1)-hop ring.
+* ``all_reduce_cv``: every rank ends with the sum: the same reduce-scatter
+  by ownership, then an all-gather of the reduced shards (C8/C9/C11 when
+  every CN needs the aggregate, e.g. to re-randomise it locally).
 * ``broadcast_cv``: root -> all ranks.
 """
 from __future__ import annotations
@@ -101,6 +104,26 @@ def sum_to_root(comm: Comm, local_cvs: list, n_rows: int, root: int = 0,
     if comm.rank != root:
         return None
     return CipherVector.cat([rows_to_cv(got2[s]) for s in range(W)])
+
+
+def all_reduce_cv(comm: Comm, local_cvs: list, n_rows: int) -> CipherVector:
+    """Homomorphic all-reduce: reduce-scatter by row ownership (rank d sums
+    rows [b_d, b_{d+1}) of every rank's vector with the K5 kernel), then an
+    all-gather of the W reduced shards.  Each rank sends and receives about
+    2 (W-1)/W of the vector over one hop of the xGMI mesh: no ring."""
+    local = CipherVector.sum(local_cvs) if local_cvs else CipherVector.zeros(n_rows, comm.device)
+    if comm.world == 1:
+        return local
+    W = comm.world
+    bounds = [(n_rows * i) // W for i in range(W + 1)]
+    rows = cv_to_rows(local)
+    got = comm.exchange({d: rows[bounds[d]: bounds[d + 1]] for d in range(W) if bounds[d + 1] > bounds[d]})
+    if bounds[comm.rank + 1] > bounds[comm.rank]:
+        mine = cv_to_rows(CipherVector.sum([rows_to_cv(got[s]) for s in sorted(got)]))
+        got2 = comm.exchange({d: mine for d in range(W)})
+    else:
+        got2 = comm.exchange({})
+    return CipherVector.cat([rows_to_cv(got2[s]) for s in range(W) if s in got2])
 
 
 def broadcast_cv(comm: Comm, cv: CipherVector | None, n_rows: int, root: int = 0) -> CipherVector:
