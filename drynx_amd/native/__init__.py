@@ -85,6 +85,7 @@ _SIGS = {
     "dx_gt_fb_pow": [_I, _P, _P, _P, _P, _P, _L],
     "dx_gt_prod_chunks": [_I, _P, _P, _P, _L, _L, _L],
     "dx_version": [],
+    "dx_stream_create_cu_mask": [_I, _P, _I, ctypes.POINTER(ctypes.c_void_p)],
     "dx_lr_moments": [_P, _P, _P, _L, _I, _P, _I],
     "dx_random_scalars": [_I, _P, _P, ctypes.c_uint32, _P, _L],
     "dx_sha256_chunks": [_I, _P, _P, _L, _L, _P],
@@ -109,6 +110,36 @@ def _declare(lib):
 
 def lib():
     return _load()
+
+
+_cu_streams: dict = {}
+
+
+def cu_masked_stream(device, reserve: int):
+    """A torch stream (ExternalStream over hipExtStreamCreateWithCUMask) that
+    leaves ``reserve`` CUs free, spread evenly over the CU ids (every XCD
+    keeps a few for other streams).  None when reserve <= 0.  Cached per
+    (device, reserve); the stream lives as long as the process."""
+    if reserve <= 0:
+        return None
+    dev = torch.device(device)
+    key = (dev.index or 0, reserve)
+    if key not in _cu_streams:
+        n_cu = torch.cuda.get_device_properties(dev).multi_processor_count
+        step = max(1, n_cu // reserve)
+        off = {(k * step + step - 1) % n_cu for k in range(reserve)}
+        words = (n_cu + 31) // 32
+        mask = [0] * words
+        for c in range(n_cu):
+            if c not in off:
+                mask[c // 32] |= 1 << (c % 32)
+        arr = (ctypes.c_uint32 * words)(*mask)
+        out = ctypes.c_void_p()
+        rc = _load().dx_stream_create_cu_mask(key[0], ctypes.cast(arr, ctypes.c_void_p), words, ctypes.byref(out))
+        if rc:
+            raise RuntimeError(f"dx_stream_create_cu_mask failed rc={rc}")
+        _cu_streams[key] = torch.cuda.ExternalStream(out.value, device=dev)
+    return _cu_streams[key]
 
 
 def loaded_path() -> str:

@@ -512,7 +512,17 @@ def verify_range_proof_list(rpl: RangeProofList, sigmat: SigMaterial, P_point, t
             # host steps overlap the fold instead of delaying its launch
             cur, aux = torch.cuda.current_stream(device), _aux_stream(device)
             aux.wait_stream(cur)
-            fb = nt.rp_verify_fold(ZB, Y, rho, r.V, S, l)             # Miller values, LDS-folded
+            # DRYNX_FOLD_RESERVE_CUS=k runs the fold on a CU-masked stream that
+            # leaves k CUs to the short launches beside it (D-check MSM, GT
+            # multi-exp, key-switch checks).  Measured slower on MI355X
+            # (k=16: 62 -> 78-80 ms per query, k=32: 66 ms), so off by default
+            fs = nt.cu_masked_stream(device, int(os.environ.get("DRYNX_FOLD_RESERVE_CUS", "0")))
+            if fs is not None:
+                fs.wait_stream(cur)
+                with torch.cuda.stream(fs):
+                    fb = nt.rp_verify_fold(ZB, Y, rho, r.V, S, l)
+            else:
+                fb = nt.rp_verify_fold(ZB, Y, rho, r.V, S, l)         # Miller values, LDS-folded
             with torch.cuda.stream(aux):
                 if not dcheck_finish(dcheck_launch()):
                     return False
@@ -520,6 +530,8 @@ def verify_range_proof_list(rpl: RangeProofList, sigmat: SigMaterial, P_point, t
                     plan = nt._multi_exp64_plan(rho)
                 G = nt._multi_exp64_run(r.A, plan)                     # prod a^rho (host tensor)
             cur.wait_stream(aux)
+            if fs is not None:
+                cur.wait_stream(fs)
         else:
             # the D-equation MSM runs to completion before the Miller fold is
             # queued: a kernel sharing the SIMDs with the fold's waves is starved
