@@ -110,7 +110,9 @@ def test_lr_encode_fused_matches_torch(gpu_device):
         assert torch.allclose(g2, ref2, rtol=1e-10, atol=1e-8), (g2 - ref2).abs().max()
 
 
-def test_range_proofs_gpu(gpu_device):
+@pytest.mark.parametrize("order", ["1", "0", "last"])
+def test_range_proofs_gpu(gpu_device, order, monkeypatch):
+    monkeypatch.setenv("DRYNX_FOLD_FIRST", order)
     from drynx_amd.crypto import elgamal as eg
     from drynx_amd.ops.encoding import CreateProofBatch
     from drynx_amd.proofs import range_proof as rp
