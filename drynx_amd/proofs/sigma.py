@@ -29,6 +29,7 @@ from .. import native as nt
 from ..crypto import bn254 as bn
 from ..crypto import oracle as O
 from ..crypto.elgamal import CipherVector
+from ..utils import timers
 
 
 def _aff_bytes(jac: torch.Tensor) -> bytes:
@@ -262,22 +263,26 @@ def key_switch_shares_batch(secrets: list, publics: list, K: torch.Tensor, Q_poi
     if with_proofs:
         bs = [O.random_scalar() for _ in secrets]
         scal.append(torch.cat([_sc([b], dev).expand(n, 8) for b in bs]).contiguous())
-    prods = nt.g1_mul(torch.cat([Kt] * len(scal)).contiguous(), torch.cat(scal).contiguous())
+    with timers.span("ks.varmul"):
+        prods = nt.g1_mul(torch.cat([Kt] * len(scal)).contiguous(), torch.cat(scal).contiguous())
     xK = prods[: c * n].contiguous()
-    vB = nt.g1_fb_mul(tabB, v)
-    vQ = nt.g1_fb_mul(tabQ, v)
-    shares_all = CipherVector(vB, nt.g1_add(vQ, xK, subtract=True))
+    with timers.span("ks.fixedbase"):
+        vB = nt.g1_fb_mul(tabB, v)
+        vQ = nt.g1_fb_mul(tabQ, v)
+        shares_all = CipherVector(vB, nt.g1_add(vQ, xK, subtract=True))
     out = []
     if with_proofs:
-        a = bn.random_scalars(c * n, dev)
-        T1 = nt.g1_fb_mul(tabB, a)
-        T2 = nt.g1_add(nt.g1_fb_mul(tabQ, a), prods[c * n:].contiguous(), subtract=True)
+        with timers.span("ks.commit"):
+            a = bn.random_scalars(c * n, dev)
+            T1 = nt.g1_fb_mul(tabB, a)
+            T2 = nt.g1_add(nt.g1_fb_mul(tabQ, a), prods[c * n:].contiguous(), subtract=True)
     if not with_proofs:
         return [(shares_all[j * n:(j + 1) * n], None) for j in range(c)]
     # every CN's transcript in ONE normalisation launch; the affine encodings are
     # kept on the proofs so marshalling them later needs no further launch
     T3s = [O.g1_to_bytes(bn.g1_mul_point(b)) for b in bs]
-    aff = _aff_bytes(torch.cat([K, shares_all.K, shares_all.C, T1, T2]))
+    with timers.span("ks.affine"):
+        aff = _aff_bytes(torch.cat([K, shares_all.K, shares_all.C, T1, T2]))
     seg = 64 * n
     Kb = aff[:seg]
 
@@ -291,9 +296,10 @@ def key_switch_shares_batch(secrets: list, publics: list, K: torch.Tensor, Q_poi
         share = shares_all[sl]
         t1, t2 = T1[sl].contiguous(), T2[sl].contiguous()
         sKb, sCb, t1b, t2b = part(0, j), part(1, j), part(2, j), part(3, j)
-        h = hashlib.sha256()
-        for piece in (b"proofTest/keyswitch", O.g1_to_bytes(publics[j]), Qb, Kb, sKb, sCb, t1b, t2b, T3s[j]):
-            h.update(piece)
+        with timers.span("ks.hash"):
+            h = hashlib.sha256()
+            for piece in (b"proofTest/keyswitch", O.g1_to_bytes(publics[j]), Qb, Kb, sKb, sCb, t1b, t2b, T3s[j]):
+                h.update(piece)
         ch = int.from_bytes(h.digest(), "big") % O.R
         za = nt.fr_arith(nt.FR_ADD, a[sl].contiguous(), nt.fr_arith(nt.FR_MUL, v[sl].contiguous(), _sc([ch], dev)))
         pr = KeySwitchProof(publics[j], Q_point, K, share, t1, t2, T3s[j], ch, za, (bs[j] + ch * secrets[j]) % O.R)
