@@ -7,7 +7,8 @@ sheets AllOps / DiffPri / LogReg, quoted in BASELINE.md), and draw both.
 
     python tools/plot_results.py [--profiles profiles] [--out profiles/plots] [--fmt pdf]
 
-Outputs: allops.<fmt> (per-operation query time, log scale), dro.<fmt>
+Outputs: allops.<fmt> (per-operation query time, log scale), scaling.<fmt>
+(ScaleServers / ScaleVNs sweeps), dro.<fmt>
 (shuffle prove/verify vs noise-list size), lr_timeline.<fmt> (phases of the
 headline verifiable LR query from the bench line's ``phase_s``), and
 summary.csv with the plotted numbers.
@@ -43,7 +44,8 @@ def load(profiles: str) -> dict:
     allops = [r for r in _jsonl(os.path.join(profiles, "r1_bench_allops_1gpu.log")) if "op" in r]
     dro = [r for r in _jsonl(os.path.join(profiles, "r1_bench_dro_shuffle_1gpu.log")) if "n" in r]
     bench = [r for r in _jsonl(os.path.join(profiles, "r1_bench_final_1gpu.log")) if "metric" in r]
-    return {"allops": allops, "dro": dro, "bench": bench[-1] if bench else None}
+    scaling = [r for r in _jsonl(os.path.join(profiles, "r1_bench_scaling_1gpu.log")) if "sweep" in r]
+    return {"allops": allops, "dro": dro, "bench": bench[-1] if bench else None, "scaling": scaling}
 
 
 def write_summary(data: dict, path: str):
@@ -58,6 +60,9 @@ def write_summary(data: dict, path: str):
             # the reference number is a whole query with that noise list, not the
             # shuffle alone: no speed-up is claimed for these rows
             w.writerow(["dro_shuffle_prove_plus_verify", r["n"], round(tot, 4), ref, ""])
+        for r in data.get("scaling", []):
+            w.writerow([r["sweep"], f"{r['cns']} CNs / {r['dps']} DPs / {r['vns']} VNs", r["seconds"],
+                        r["reference_s"] or "", r["speedup"] or ""])
         b = data["bench"]
         if b is not None:
             w.writerow(["lr_query", b["config"]["model"], b["e2e_latency_s"], REF_LR_SPECTF_S,
@@ -102,6 +107,24 @@ def plot(data: dict, out: str, fmt: str):
         ax.legend()
         fig.tight_layout()
         p = os.path.join(out, f"dro.{fmt}")
+        fig.savefig(p)
+        plt.close(fig)
+        made.append(p)
+    sc = data.get("scaling", [])
+    if sc:
+        fig, axes = plt.subplots(1, 2, figsize=(10, 4))
+        for ax, key, xname in ((axes[0], "ScaleServers", "cns"), (axes[1], "ScaleVNs", "vns")):
+            for sweep in dict.fromkeys(r["sweep"] for r in sc if r["sweep"].startswith(key)):
+                pts = [r for r in sc if r["sweep"] == sweep]
+                ax.plot([r[xname] for r in pts], [r["seconds"] for r in pts], "o-", label=f"drynx_amd: {sweep}")
+                ref = [r for r in pts if r["reference_s"]]
+                ax.plot([r[xname] for r in ref], [r["reference_s"] for r in ref], "x--", label=f"reference: {sweep}")
+            ax.set_yscale("log")
+            ax.set_xlabel("#" + xname.upper())
+            ax.set_ylabel("seconds per verifiable sum query")
+            ax.legend(fontsize=7)
+        fig.tight_layout()
+        p = os.path.join(out, f"scaling.{fmt}")
         fig.savefig(p)
         plt.close(fig)
         made.append(p)
