@@ -6,6 +6,8 @@ threshold.py):
   * ScaleServers rows 5-12: 6 -> 48 CNs, 10 DPs in total: 1.87 -> 5.25 s
   * ScaleVNs rows 5-26: 7 -> 42 VNs, threshold 1.0: 9.45 -> 25.04 s;
     threshold 0.3: 6.07 -> 15.8 s
+  * ScaleDPs rows 5-8 / 10-13: 600 -> 600k records with #DPs = #records:
+    9.7 / 62.9 / 489 / 3287 s; with 10 DPs: 2.2 / 3.4 / 3.8 / 4.4 s
   * Threshold rows 5-13, 26: (T, T_sub) = (1, 1) 8.75 s ... (0.2, 0.2) 4.35 s;
     (0, 0) 2.15 s
 Only the end points of each sweep are quoted in the survey, so
@@ -38,12 +40,12 @@ def _sync(dev):
         torch.cuda.synchronize()
 
 
-def _point(dev, n_cns, n_dps, n_vns, thresholds, reps):
+def _point(dev, n_cns, n_dps, n_vns, thresholds, reps, rows=10):
     cl, node = local_cluster(n_cns, n_dps, n_vns, device=dev, workdir=tempfile.mkdtemp(prefix="drynx_scale_"))
     client = DrynxClient(node, device=dev)
     times, codes = [], set()
     for i in range(reps + 1):
-        sq = make_survey(client, cl, "sum", query_min=0, query_max=100, rows=10, proofs=1, ranges=RANGES,
+        sq = make_survey(client, cl, "sum", query_min=0, query_max=100, rows=rows, proofs=1, ranges=RANGES,
                          thresholds=thresholds, sig_device=dev, deterministic_sigs=True)
         _sync(dev)
         t0 = time.perf_counter()
@@ -64,7 +66,7 @@ def main():
     if dev.type == "cuda":
         torch.cuda.set_device(dev)
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
-    sweeps = set(sys.argv[2].split(",")) if len(sys.argv) > 2 else {"servers", "vns", "threshold"}
+    sweeps = set(sys.argv[2].split(",")) if len(sys.argv) > 2 else {"servers", "vns", "threshold", "dps"}
     full = [1.0, 1.0, 1.0, 0.0, 1.0]  # [general, aggregation, range, obfuscation, keyswitch] (api.go:79-83)
     points = []
     if "servers" in sweeps:
@@ -79,8 +81,15 @@ def main():
         for (T, Ts), ref in (((1.0, 1.0), 8.75), ((0.6, 0.6), None), ((0.2, 0.2), 4.35), ((0.0, 0.0), 2.15)):
             points.append((f"Threshold (T, T_sub) = ({T}, {Ts})", dict(cns=3, dps=10, vns=3), [T, Ts, Ts, 0.0, Ts],
                            ref))
+    if "dps" in sweeps:
+        # ScaleDPs: 600 ... 600k records held by #DPs = #records (rows 5-8) or by 10 DPs (rows 10-13)
+        for total, ref in ((600, 2.2), (6000, 3.4), (60000, 3.8), (600000, 4.4)):
+            points.append((f"ScaleDPs 10 DPs, {total} records", dict(cns=3, dps=10, vns=3, rows=total // 10), full,
+                           ref))
+        for total, ref in ((600, 9.7), (6000, 62.9)):
+            points.append(("ScaleDPs #DPs = #records", dict(cns=3, dps=total, vns=3, rows=1), full, ref))
     for label, topo, thr, ref in points:
-        sec, codes = _point(dev, topo["cns"], topo["dps"], topo["vns"], thr, reps)
+        sec, codes = _point(dev, topo["cns"], topo["dps"], topo["vns"], thr, reps, topo.get("rows", 10))
         print(json.dumps({"sweep": label, **topo, "seconds": round(sec, 4), "reference_s": ref,
                           "speedup": round(ref / sec, 1) if ref else None, "proof_codes": codes}), flush=True)
 
