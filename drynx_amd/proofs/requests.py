@@ -365,15 +365,27 @@ def _decode(req: ProofRequest, device):
     raise ValueError(req.kind)
 
 
+_SIG_BATCH_MIN = 16  # inboxes at least this long check their envelope signatures in one batch
+
+
 def verify_requests(reqs: list, sq, vn_id: str, vn_index: int, n_vns: int, device, cache: VerifierCache) -> list:
     """VerifyProof for a VN's whole inbox.  Signatures and sampling per request;
     the content of the short per-CN proofs (key switch, obfuscation) is verified
     in one batched launch per kind; range proofs are already one batch each."""
     codes = [None] * len(reqs)
     todo: dict = {}
+    if len(reqs) >= _SIG_BATCH_MIN:
+        with timers.span("verify.signature.batch"):
+            sigs_ok = sigma.schnorr_verify_batch(
+                [(sq.IDtoPublic.get(r.sender_id), r.digest(), r.signature) for r in reqs], device)
+    else:
+        sigs_ok = None
     for i, req in enumerate(reqs):
-        with timers.span(f"verify.signature.{req.kind}"):
-            sig_ok = verify_signature(req, sq.IDtoPublic.get(req.sender_id))
+        if sigs_ok is not None:
+            sig_ok = sigs_ok[i]
+        else:
+            with timers.span(f"verify.signature.{req.kind}"):
+                sig_ok = verify_signature(req, sq.IDtoPublic.get(req.sender_id))
         if not sig_ok:
             codes[i] = PROOF_FALSE_SIGN
         elif not should_verify(sq, req, vn_index, n_vns):

@@ -131,6 +131,39 @@ def schnorr_verify(public, msg: bytes, sig: bytes) -> bool:
     return lhs == O.g1_add(R, bn.g1_mul_point(e, public))
 
 
+def schnorr_verify_batch(items: list, device="cpu") -> list:
+    """schnorr_verify over many (public, msg, sig) at once: s_i B by one
+    fixed-base launch, e_i X_i by one variable-base launch, one addition and
+    one equality launch.  A VN inbox holds one envelope per DP and per CN
+    proof; one host scalar multiplication per envelope made 6000-DP surveys
+    host-bound (structs_proofs.go:498-505 verifies each in its own goroutine)."""
+    out = [False] * len(items)
+    idx, R, X, s, e = [], [], [], [], []
+    for i, (public, msg, sig) in enumerate(items):
+        if len(sig) != 96 or public is None:
+            continue
+        try:
+            Ri = O.g1_from_bytes(sig[:64])
+        except ValueError:
+            continue
+        if Ri is None:
+            continue
+        idx.append(i)
+        R.append(Ri)
+        X.append(public)
+        s.append(int.from_bytes(sig[64:], "big") % O.R)
+        e.append(int.from_bytes(hashlib.sha256(sig[:64] + O.g1_to_bytes(public) + msg).digest(), "big") % O.R)
+    if not idx:
+        return out
+    dev = torch.device(device)
+    lhs = nt.g1_fb_mul(bn.base_table(dev), _sc(s, dev))
+    rhs = nt.g1_add(bn.g1_jac_tensor(R, dev), nt.g1_mul(bn.g1_jac_tensor(X, dev), _sc(e, dev)))
+    ok = nt.g1_eq(lhs, rhs).cpu().tolist()
+    for i, v in zip(idx, ok):
+        out[i] = bool(v)
+    return out
+
+
 # ----------------------------------------------------------------------------- obfuscation (DLEQ)
 @dataclass
 class ObfuscationProof:

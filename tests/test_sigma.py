@@ -162,3 +162,25 @@ def test_batch_verification_blames_only_the_bad_proof():
     obs[2].z = obs[2].z.clone()
     obs[2].z[0, 0] ^= 1
     assert sigma.obfuscation_batch_verification(obs) == [True, True, False]
+
+
+def test_schnorr_verify_batch_matches_single():
+    from drynx_amd.crypto import oracle as O
+    from drynx_amd.proofs import sigma
+
+    keys = [O.random_scalar() for _ in range(5)]
+    pubs = [O.g1_mul(k, O.G1_GEN) for k in keys]
+    items = []
+    for i, k in enumerate(keys):
+        msg = f"digest {i}".encode()
+        items.append((pubs[i], msg, sigma.schnorr_sign(k, msg)))
+    good_sig = items[0][2]
+    items.append((pubs[1], b"digest 0", good_sig))                      # wrong key
+    items.append((pubs[0], b"other", good_sig))                         # wrong message
+    items.append((pubs[0], b"digest 0", good_sig[:64] + (1).to_bytes(32, "big")))  # wrong s
+    items.append((None, b"digest 0", good_sig))                          # unknown sender
+    items.append((pubs[0], b"digest 0", good_sig[:90]))                  # truncated
+    items.append((pubs[0], b"digest 0", b"\x01" * 64 + good_sig[64:]))  # R off the curve
+    want = [sigma.schnorr_verify(p, m, s) for p, m, s in items]
+    assert want == [True] * 5 + [False] * 6
+    assert sigma.schnorr_verify_batch(items) == want
