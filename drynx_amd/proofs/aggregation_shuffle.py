@@ -33,6 +33,11 @@ class AggregationProof:
 
     def to_bytes(self) -> bytes:
         parts = [len(self.inputs).to_bytes(8, "little"), len(self.result).to_bytes(8, "little")]
+        if self.inputs and all(len(cv) == len(self.result) for cv in self.inputs):
+            # one normalisation + one device-to-host copy for every contributor
+            # (a CN with thousands of DPs would otherwise pay one sync per DP)
+            parts.append(CipherVector.cat(list(self.inputs) + [self.result]).to_bytes())
+            return b"".join(parts)
         for cv in self.inputs:
             parts.append(cv.to_bytes())
         parts.append(self.result.to_bytes())

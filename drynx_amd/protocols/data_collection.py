@@ -53,7 +53,7 @@ def generate_lr_data(params, device, gen: torch.Generator):
     return X, y
 
 
-def dp_encode(ctx, sq, dp) -> dict:
+def dp_encode(ctx, sq, dp, sync_timer: bool = True) -> dict:
     """Encode one DP's response for every group. Returns a dict with the
     stacked CipherVector (groups x NbrOutput), per-group proof batches, clear values."""
     q = sq.Query
@@ -84,7 +84,7 @@ def dp_encode(ctx, sq, dp) -> dict:
         op_eff = copy.copy(op)
         op_eff.NbrOutput = op.NbrOutput // cf
     cvs, proofs, clears = [], [], []
-    with timers.timed(f"{dp.id}_DPencoding"):
+    with timers.timed(f"{dp.id}_DPencoding", sync=sync_timer):
         for _ in groups:
             r = enc.encode(data, pk, op_eff, ranges=q.Ranges, with_proofs=with_proofs, lr_data=lr)
             cv = r.cv
@@ -107,10 +107,12 @@ def data_collection(ctx, sq) -> tuple:
         for si in dps or []:
             dp_to_cn[si.id] = cn_id
     dp_results, items = {}, []
-    for dp in cl.local(ctx.rank, "dp"):
-        if dp.id not in dp_to_cn:
-            continue
-        res = dp_encode(ctx, sq, dp)
+    local_dps = [dp for dp in cl.local(ctx.rank, "dp") if dp.id in dp_to_cn]
+    # the per-DP timer syncs the device only for a handful of DPs per rank: with
+    # thousands (ScaleDPs, one record each) the syncs serialise the encoders
+    sync_timer = len(local_dps) <= 16
+    for dp in local_dps:
+        res = dp_encode(ctx, sq, dp, sync_timer)
         dp_results[dp.id] = res
         cn = cl.by_id(dp_to_cn[dp.id])
         items.append((cn.rank, dp.id, res["cv"]))
