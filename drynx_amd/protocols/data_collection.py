@@ -36,8 +36,12 @@ def _seed(survey_id: str, dp_id: str) -> int:
 def generate_fake_data(op, nbr_rows: int, lo: int, hi: int, device, gen: torch.Generator):
     """createFakeDataForOperation: NbrInput columns of uniform ints in [lo, hi]."""
     n_in = max(1, op.NbrInput)
-    return [torch.randint(lo, hi + 1, (max(1, nbr_rows),), generator=gen, dtype=torch.int64).to(device)
-            for _ in range(n_in)]
+    t = torch.randint(lo, hi + 1, (n_in, max(1, nbr_rows)), generator=gen, dtype=torch.int64)
+    if torch.device(device).type == "cuda":
+        # one pinned, asynchronous upload: a pageable copy per column waits for
+        # the previous DP's kernels, which serialised thousands of small DPs
+        t = t.pin_memory().to(device, non_blocking=True)
+    return list(t.unbind(0))
 
 
 def generate_lr_data(params, device, gen: torch.Generator):
