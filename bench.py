@@ -1,27 +1,32 @@
 #!/usr/bin/env python3
-"""Headline benchmark: full verifiable logistic-regression query.
+"""Headline benchmark: full verifiable logistic-regression query on the
+reference's own LR-SPECTF configuration.
 
 BASELINE.json metric: "end-to-end query latency + range-proof verifications/sec,
-logreg on 1e6 records" — config 5: full verifiable query (logistic regression
-over 1e6 records, skipchain proof collection, batched range-proof
-verification).
+logreg on 1e6 records".  Configuration = the reference's LR SPECTF run
+(AllResults.xlsx LogRegr row 7, simul/runfiles/drynx.toml:13): 3 CNs, 3 VNs,
+10 DPs, logistic regression k=2 over 44 features (2070 encrypted outputs per
+DP), range proofs u = l = 16 on every output, every VN verifying every proof
+(threshold 1.0, no sharding), Boneh-Boyen input-validation keys drawn at random
+per CN and per column (InitRangeProofSignature, simul/drynx_simul.go:292-296).
+1e6 synthetic SPECTF-shaped records in total (1e5 per DP).
 
 One step = one complete survey through the framework:
-  DP (one per rank/GPU): 1e6 synthetic SPECTF-shaped records (44 features,
-  random-init data, generated once on the device = the DP's database) ->
-  approximation-coefficient encoding (fp64 MFMA) -> 2070 ElGamal ciphertexts
-  -> 2070 range proofs (u=16, l=16 as in the reference's service tests, signed offset 2^62) with S = 3 CNs ->
-  collective aggregation -> key switching (+ aggregation / key-switch proofs)
-  -> querier decryption (BSGS) + gradient descent -> proof collection at the
-  VNs (one per rank, every proof verified by exactly one VN: batched
-  pairing verification) -> DataBlock -> signed skipchain block.
+  10 DPs: fp64-MFMA encoding -> 20,700 ElGamal ciphertexts -> 20,700 range
+  proofs (signed offset 2^62) -> collective aggregation (+ proofs) -> key
+  switching (+ proofs) -> querier decryption (BSGS) + gradient descent ->
+  proof collection: 3 VNs x 20,700 range proofs (993,600 pairing equations
+  each) + aggregation / key-switch proofs -> DataBlock -> BLS-cosigned
+  skipchain block.
 
-value  = range proofs verified per second of end-to-end query time, summed
-         over the whole job (weak scaling: per-GPU work is fixed).
+value  = range-proof verifications per second of end-to-end query time
+         (20,700 proofs x 3 VNs per query), whole job.
 ms_per_step = end-to-end latency of one verifiable query (max over ranks).
-vs_baseline = value / 114.6, the reference's range-proof throughput derived
-         from its LR-SPECTF run (10 DPs x 2070 proofs, 180.59 s of proof
-         overhead; AllResults.xlsx LogRegr row 7).
+scaling = strong: the query is fixed; N GPUs share it (DPs round robin over the
+         ranks, CNs and VNs on distinct ranks, every VN's range checks pooled
+         over all ranks).
+vs_baseline = value / 315.6, the reference's verifications per second of
+         end-to-end time in that run (20,700 x 3 / 196.77 s).
 
 Run: python bench.py [--gpus N --steps K --warmup W]; for N>1 under
 torch.distributed.run (one rank per GPU, RCCL over xGMI).
@@ -49,8 +54,8 @@ from drynx_amd.services.api import DrynxClient  # noqa: E402
 from drynx_amd.services.local import local_cluster, make_survey  # noqa: E402
 from drynx_amd.utils import timers  # noqa: E402
 
-REFERENCE_RANGE_PROOFS_PER_S = 10 * 2070 / 180.59  # LR SPECTF, BASELINE.md
-REFERENCE_LR_SPECTF_S = 196.77
+REFERENCE_LR_SPECTF_S = 196.77  # AllResults.xlsx LogRegr row 7
+REFERENCE_VERIFICATIONS_PER_S = 10 * 2070 * 3 / REFERENCE_LR_SPECTF_S  # 10 DPs x 2070 proofs x 3 VNs
 
 
 def parse():
@@ -58,9 +63,13 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--records", type=int, default=1_000_000, help="records per DP (one DP per GPU)")
+    ap.add_argument("--records", type=int, default=1_000_000, help="records in total, split over the DPs")
     ap.add_argument("--features", type=int, default=44, help="SPECTF-shaped: 44 features -> 2070 outputs")
     ap.add_argument("--cns", type=int, default=3)
+    ap.add_argument("--dps", type=int, default=10)
+    ap.add_argument("--vns", type=int, default=3)
+    ap.add_argument("--deterministic-sigs", action="store_true",
+                    help="InitRangeProofSignatureDeterministic keys (the reference uses them only with CuttingFactor)")
     ap.add_argument("--u", "--base", dest="u", type=int, default=16)
     ap.add_argument("--l", "--digits", dest="l", type=int, default=16)
     ap.add_argument("--precision", type=float, default=100.0)
@@ -79,22 +88,25 @@ def main():
     if device.type == "cuda":
         torch.cuda.set_device(device)
     workdir = tempfile.mkdtemp(prefix=f"drynx_bench_r{rank}_")
-    n_dps, n_vns = world, world
-    cl, node = local_cluster(args.cns, n_dps, n_vns, comm=comm, device=device, workdir=workdir)
+    n_dps, n_vns = args.dps, args.vns
+    # CNs on ranks 0.., VNs right after them, DPs round robin over every rank
+    offsets = {"cn": 0, "vn": args.cns % world, "dp": 0}
+    cl, node = local_cluster(args.cns, n_dps, n_vns, comm=comm, device=device, workdir=workdir, offsets=offsets)
+    rec_per_dp = max(1, args.records // n_dps)
     d = args.features
     # the DP's database: generated once on its device (synthetic, random-init)
     g = torch.Generator(device=device).manual_seed(1234 + rank)
     dp_data = {}
     for dp in cl.local(rank, "dp"):
-        X = torch.randint(0, 4, (args.records, d), generator=g, device=device).to(torch.float64)
-        X += torch.rand((args.records, d), generator=g, device=device, dtype=torch.float64)
-        y = torch.randint(0, 2, (args.records,), generator=g, device=device)
+        X = torch.randint(0, 4, (rec_per_dp, d), generator=g, device=device).to(torch.float64)
+        X += torch.rand((rec_per_dp, d), generator=g, device=device, dtype=torch.float64)
+        y = torch.randint(0, 2, (rec_per_dp,), generator=g, device=device)
         dp_data[dp.id] = (X, y)
     node.dp_data = dp_data
     # global standardisation parameters (as the reference passes Means/SDs in the query)
     means = [2.0] * d
     sds = [1.15] * d
-    lp = LogisticRegressionParameters(NbrRecords=args.records * n_dps, NbrFeatures=d, Means=means,
+    lp = LogisticRegressionParameters(NbrRecords=rec_per_dp * n_dps, NbrFeatures=d, Means=means,
                                       StandardDeviations=sds, Lambda=1.0, Step=0.012, MaxIterations=args.max_iter,
                                       InitialWeights=[0.1] * (d + 1), K=2,
                                       PrecisionApproxCoefficients=args.precision)
@@ -104,8 +116,8 @@ def main():
     template = None
     if rank == 0:  # CN input-validation keys are set up once, before the queries (as in the reference simulation)
         template = make_survey(client, cl, "logistic regression", proofs=1, ranges=[args.u, args.l, offset],
-                               lr_params=lp, thresholds=[1.0, 1.0, 1.0, 0.0, 1.0], verification_sharding=1,
-                               sig_device=device, deterministic_sigs=True)
+                               lr_params=lp, thresholds=[1.0, 1.0, 1.0, 0.0, 1.0], verification_sharding=0,
+                               sig_device=device, deterministic_sigs=args.deterministic_sigs)
 
     def one_step():
         if rank == 0:
@@ -137,9 +149,10 @@ def main():
     elapsed = max(comm.all_gather_object(elapsed))
     n_out = (d + 1) + (d + 1) ** 2
     proofs_per_step = n_dps * n_out
+    verifs_per_step = proofs_per_step * n_vns  # threshold 1.0: every VN checks every proof
     ms = 1000.0 * elapsed / args.steps
-    value = proofs_per_step * args.steps / elapsed
-    ok = all(b is not None and all(v in (1, 2) for v in b.data_block().Proofs.values()) for b in blocks)
+    value = verifs_per_step * args.steps / elapsed
+    ok = all(b is not None and all(v == 1 for v in b.data_block().Proofs.values()) for b in blocks)
     allt = comm.all_gather_object(timers.summary())
     if rank == 0:
         phase = {}
@@ -155,17 +168,22 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms, 2),
             "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": round(value / REFERENCE_RANGE_PROOFS_PER_S, 3),
+            "scaling": "strong",
+            "vs_baseline": round(value / REFERENCE_VERIFICATIONS_PER_S, 3),
             "dtype": "bn254-exact/fp64",
-            "data": "synthetic (random SPECTF-shaped records, random keys)",
+            "data": "synthetic (random SPECTF-shaped records, random keys and input-validation signatures)",
             "config": {
                 "model": f"logistic regression k=2, d={d} ({n_out} encrypted outputs per DP), full verifiable query",
-                "global_batch": args.records * n_dps,
+                "global_batch": rec_per_dp * n_dps,
                 "seq_len": None,
-                "parallelism": f"{world} ranks: {n_dps} DPs, {args.cns} CNs, {n_vns} VNs (sharded verification)",
-                "records_per_dp": args.records,
-                "range_proof": {"u": args.u, "l": args.l, "servers": args.cns, "proofs_per_query": proofs_per_step},
+                "parallelism": f"{world} ranks: {n_dps} DPs, {args.cns} CNs, {n_vns} VNs, "
+                               f"VN range checks pooled over {world} rank(s)",
+                "dps": n_dps, "cns": args.cns, "vns": n_vns,
+                "records_per_dp": rec_per_dp,
+                "sigs": "deterministic" if args.deterministic_sigs else "random (per CN, per column)",
+                "verification": "every VN verifies every proof (threshold 1.0)",
+                "range_proof": {"u": args.u, "l": args.l, "servers": args.cns, "proofs_per_query": proofs_per_step,
+                                "verifications_per_query": verifs_per_step},
             },
             "e2e_latency_s": round(ms / 1000.0, 4),
             "latency_vs_reference_lr_spectf": round(REFERENCE_LR_SPECTF_S / (ms / 1000.0), 2),

@@ -103,4 +103,14 @@ DX_NI Fp12 gt_fixed_pow(const Fp12 *table, const uint32_t *k) {
   return r;
 }
 
+// 4-bit comb: table[w*15 + d - 1] = base^(d * 16^w), w < 64 (360 KiB per base).
+DX_NI Fp12 gt_fixed_pow4(const Fp12 *table, const uint32_t *k) {
+  Fp12 r = Fp12::one();
+  for (int w = 0; w < 64; w++) {
+    uint32_t d = (k[w >> 3] >> ((w & 7) * 4)) & 15u;
+    if (d) r = mul(r, table[w * 15 + d - 1]);
+  }
+  return r;
+}
+
 }  // namespace dx

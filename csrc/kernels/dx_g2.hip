@@ -40,6 +40,41 @@ int dx_g2_fb_mul(int on_gpu, void *stream, const uint32_t *tables, const int32_t
   return run(on_gpu, stream, n, op, true, "g2_fb_mul");
 }
 
+// 4-bit comb tables (fixed_base_mul4 layout): work[b*64 + w] = 16^w * base
+// (Jacobian), then table[b*960 + w*15 + d - 1] = d * 16^w * base (affine).
+int dx_g2_fb4_table(int on_gpu, void *stream, const uint32_t *bases_aff, uint32_t *work, uint32_t *table,
+                    int64_t n_bases) {
+  auto p1 = [=] __host__ __device__(int64_t b) {
+    G2J acc = G2J::from_aff(at<G2A>(bases_aff, b));
+    for (int w = 0; w < 64; w++) {
+      at<G2J>(work, b * 64 + w) = acc;
+      acc = jdbl(jdbl(jdbl(jdbl(acc))));
+    }
+  };
+  int rc = run(on_gpu, stream, n_bases, p1, true, "g2_fb4_table_pow16");
+  if (rc) return rc;
+  auto p2 = [=] __host__ __device__(int64_t t) {
+    const int64_t b = t / 960, i = t % 960;
+    const int w = (int)(i / 15), d = (int)(i % 15) + 1;
+    G2J q = at<G2J>(work, b * 64 + w), acc = G2J::inf();
+    for (int bit = 0; bit < 4; bit++) {
+      if ((d >> bit) & 1) acc = jadd(acc, q);
+      if (bit < 3 && (d >> (bit + 1))) q = jdbl(q);
+    }
+    at<G2A>(table, t) = to_affine(acc);
+  };
+  return run(on_gpu, stream, n_bases * 960, p2, true, "g2_fb4_table");
+}
+
+int dx_g2_fb4_mul(int on_gpu, void *stream, const uint32_t *tables, const int32_t *tab_idx, const uint32_t *scalars,
+                  uint32_t *out_aff, int64_t n) {
+  auto op = [=] __host__ __device__(int64_t i) {
+    const G2A *T = reinterpret_cast<const G2A *>(tables) + (int64_t)(tab_idx ? tab_idx[i] : 0) * 960;
+    at<G2A>(out_aff, i) = to_affine(fixed_base_mul4(T, scalars + 8 * i));
+  };
+  return run(on_gpu, stream, n, op, true, "g2_fb4_mul");
+}
+
 int dx_g2_mul(int on_gpu, void *stream, const uint32_t *pts_aff, const uint32_t *scalars, uint32_t *out_aff, int64_t n,
               int pt_bcast) {
   auto op = [=] __host__ __device__(int64_t i) {

@@ -73,6 +73,41 @@ int dx_gt_fb_pow(int on_gpu, void *stream, const uint32_t *tables, const int32_t
   return run(on_gpu, stream, n, op, true, "gt_fb_pow");
 }
 
+// 4-bit comb tables (gt_fixed_pow4 layout): work[b*64 + w] = base^(16^w), then
+// table[b*960 + w*15 + d - 1] = base^(d * 16^w).
+int dx_gt_fb4_table(int on_gpu, void *stream, const uint32_t *base, uint32_t *work, uint32_t *table,
+                    int64_t n_bases) {
+  auto p1 = [=] __host__ __device__(int64_t b) {
+    Fp12 acc = at<Fp12>(base, b);
+    for (int w = 0; w < 64; w++) {
+      at<Fp12>(work, b * 64 + w) = acc;
+      acc = cyclotomic_sqr(cyclotomic_sqr(cyclotomic_sqr(cyclotomic_sqr(acc))));
+    }
+  };
+  int rc = run(on_gpu, stream, n_bases, p1, true, "gt_fb4_table_pow16");
+  if (rc) return rc;
+  auto p2 = [=] __host__ __device__(int64_t t) {
+    const int64_t b = t / 960, i = t % 960;
+    const int w = (int)(i / 15), d = (int)(i % 15) + 1;
+    Fp12 q = at<Fp12>(work, b * 64 + w), acc = Fp12::one();
+    for (int bit = 0; bit < 4; bit++) {
+      if ((d >> bit) & 1) acc = mul(acc, q);
+      if (bit < 3 && (d >> (bit + 1))) q = cyclotomic_sqr(q);
+    }
+    at<Fp12>(table, t) = acc;
+  };
+  return run(on_gpu, stream, n_bases * 960, p2, true, "gt_fb4_table");
+}
+
+int dx_gt_fb4_pow(int on_gpu, void *stream, const uint32_t *tables, const int32_t *tab_idx, const uint32_t *scalars,
+                  uint32_t *out, int64_t n) {
+  auto op = [=] __host__ __device__(int64_t i) {
+    const Fp12 *T = reinterpret_cast<const Fp12 *>(tables) + (int64_t)(tab_idx ? tab_idx[i] : 0) * 960;
+    at<Fp12>(out, i) = gt_fixed_pow4(T, scalars + 8 * i);
+  };
+  return run(on_gpu, stream, n, op, true, "gt_fb4_pow");
+}
+
 // product over axis 0 chunks of in[n_items][n_groups] Fp12 (same scheme as g1_sum_chunks)
 int dx_gt_prod_chunks(int on_gpu, void *stream, const uint32_t *in, uint32_t *out, int64_t n_items, int64_t n_groups,
                       int64_t chunk) {

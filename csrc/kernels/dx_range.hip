@@ -35,9 +35,11 @@ int dx_rp_prove_a(int on_gpu, void *stream, const uint32_t *negsB_aff, const uin
 // (gphi_tables[tab_idx[it]]) and e = -s_j v_ij computed on the device.
 // gT^{t_pj} is shared by the S servers of a digit: computed once per (p, j)
 // (first pass, into a_out rows it = (p*S)*L + j) and reused by the others.
+// wbits = 8: gphi tables in the 8-bit comb layout (8192 entries per point);
+// wbits = 4: the 4-bit layout (960 entries per point, gt_fixed_pow4).
 int dx_rp_prove_a_tab(int on_gpu, void *stream, const uint32_t *gphi_tables, const int32_t *tab_idx,
                       const uint32_t *e_sc, const uint32_t *t_sc, const uint32_t *gt_table, uint32_t *a_out,
-                      int64_t n_items, int S, int L) {
+                      int64_t n_items, int S, int L, int wbits) {
   const int64_t n_pj = n_items / S;
   auto p1 = [=] __host__ __device__(int64_t pj) {
     const int64_t p = pj / L, j = pj % L;
@@ -55,8 +57,8 @@ int dx_rp_prove_a_tab(int on_gpu, void *stream, const uint32_t *gphi_tables, con
       const int64_t p = k / per, r = k % per;
       const int64_t i = pass == 0 ? 1 + r / L : 0, j = r % L;
       const int64_t it = (p * S + i) * L + j;
-      const Fp12 *T = reinterpret_cast<const Fp12 *>(gphi_tables) + (int64_t)tab_idx[it] * 8192;
-      Fp12 f = gt_fixed_pow(T, e_sc + 8 * it);
+      const Fp12 *T = reinterpret_cast<const Fp12 *>(gphi_tables) + (int64_t)tab_idx[it] * (wbits == 4 ? 960 : 8192);
+      Fp12 f = wbits == 4 ? gt_fixed_pow4(T, e_sc + 8 * it) : gt_fixed_pow(T, e_sc + 8 * it);
       at<Fp12>(a_out, it) = mul(f, at<Fp12>(a_out, p * S * L + j));
     };
     rc = run(on_gpu, stream, n, p2, true, "rp_prove_a_tab");

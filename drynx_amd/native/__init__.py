@@ -96,7 +96,11 @@ _SIGS = {
     "dx_gt_slice_prod": [_I, _P, _P, _P, _P, _P, _P, _L],
     "dx_g1_slice_sum": [_I, _P, _P, _P, _P, _P, _P, _L],
     "dx_rp_prove_a": [_I, _P, _P, _P, _P, _P, _P, _L, _I, _I],
-    "dx_rp_prove_a_tab": [_I, _P, _P, _P, _P, _P, _P, _P, _L, _I, _I],
+    "dx_rp_prove_a_tab": [_I, _P, _P, _P, _P, _P, _P, _P, _L, _I, _I, _I],
+    "dx_g2_fb4_table": [_I, _P, _P, _P, _P, _L],
+    "dx_g2_fb4_mul": [_I, _P, _P, _P, _P, _P, _L],
+    "dx_gt_fb4_table": [_I, _P, _P, _P, _P, _L],
+    "dx_gt_fb4_pow": [_I, _P, _P, _P, _P, _P, _L],
     "dx_rp_verify_items": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _I],
 }
 
@@ -404,6 +408,30 @@ def g2_fb_mul(tables: torch.Tensor, scalars: torch.Tensor, tab_idx: torch.Tensor
     return out
 
 
+FB4_ENTRIES = 960  # 64 windows x 15 non-zero digits
+
+
+def g2_fb4_table(base_aff: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """4-bit comb table(s) [n_bases*960, 32] (120 KiB per base).  ``out``: a
+    preallocated slice of a larger table tensor to fill in place."""
+    bases = base_aff.contiguous().view(-1, 32)
+    nb = bases.shape[0]
+    table = out if out is not None else torch.empty((nb * FB4_ENTRIES, 32), dtype=torch.int32, device=bases.device)
+    assert table.shape == (nb * FB4_ENTRIES, 32) and table.is_contiguous()
+    work = torch.empty((nb * 64, 48), dtype=torch.int32, device=bases.device)
+    g, s = _ctx(bases, table)
+    _call("dx_g2_fb4_table", g, s, _ptr(bases), _ptr(work), _ptr(table), nb)
+    return table
+
+
+def g2_fb4_mul(tables: torch.Tensor, scalars: torch.Tensor, tab_idx: torch.Tensor | None = None) -> torch.Tensor:
+    n = _rows(scalars, 8)
+    out = torch.empty((n, 32), dtype=torch.int32, device=scalars.device)
+    g, s = _ctx(tables, scalars, tab_idx)
+    _call("dx_g2_fb4_mul", g, s, _ptr(tables), _ptr(tab_idx), _ptr(scalars), _ptr(out), n)
+    return out
+
+
 def g2_mul(pts_aff: torch.Tensor, scalars: torch.Tensor) -> torch.Tensor:
     n = _rows(scalars, 8)
     np_ = _rows(pts_aff, 32)
@@ -488,6 +516,26 @@ def gt_fb_pow(tables: torch.Tensor, scalars: torch.Tensor, tab_idx: torch.Tensor
     out = torch.empty((n, 96), dtype=torch.int32, device=scalars.device)
     g, s = _ctx(tables, scalars, tab_idx)
     _call("dx_gt_fb_pow", g, s, _ptr(tables), _ptr(tab_idx), _ptr(scalars), _ptr(out), n)
+    return out
+
+
+def gt_fb4_table(bases: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """4-bit comb table(s) [n_bases*960, 96] (360 KiB per base)."""
+    bases = bases.contiguous()
+    nb = _rows(bases, 96)
+    table = out if out is not None else torch.empty((nb * FB4_ENTRIES, 96), dtype=torch.int32, device=bases.device)
+    assert table.shape == (nb * FB4_ENTRIES, 96) and table.is_contiguous()
+    work = torch.empty((nb * 64, 96), dtype=torch.int32, device=bases.device)
+    g, s = _ctx(bases, table)
+    _call("dx_gt_fb4_table", g, s, _ptr(bases), _ptr(work), _ptr(table), nb)
+    return table
+
+
+def gt_fb4_pow(tables: torch.Tensor, scalars: torch.Tensor, tab_idx: torch.Tensor | None = None) -> torch.Tensor:
+    n = _rows(scalars, 8)
+    out = torch.empty((n, 96), dtype=torch.int32, device=scalars.device)
+    g, s = _ctx(tables, scalars, tab_idx)
+    _call("dx_gt_fb4_pow", g, s, _ptr(tables), _ptr(tab_idx), _ptr(scalars), _ptr(out), n)
     return out
 
 
@@ -613,12 +661,14 @@ def rp_prove_a(negsB_aff, V_aff, t_sc, gt_table, S: int, L: int) -> torch.Tensor
     return out
 
 
-def rp_prove_a_tab(gphi_tables, tab_idx, e_sc, t_sc, gt_table, S: int, L: int) -> torch.Tensor:
+def rp_prove_a_tab(gphi_tables, tab_idx, e_sc, t_sc, gt_table, S: int, L: int, wbits: int = 8) -> torch.Tensor:
+    """wbits = 8: gphi_tables in the 8-bit comb layout; 4: the 4-bit layout (gt_fb4_table)."""
+    assert wbits in (4, 8)
     n = _rows(e_sc, 8)
     out = torch.empty((n, 96), dtype=torch.int32, device=e_sc.device)
     g, s = _ctx(gphi_tables, tab_idx, e_sc, t_sc, gt_table)
     _call("dx_rp_prove_a_tab", g, s, _ptr(gphi_tables), _ptr(tab_idx), _ptr(e_sc), _ptr(t_sc), _ptr(gt_table),
-          _ptr(out), n, S, L)
+          _ptr(out), n, S, L, wbits)
     return out
 
 

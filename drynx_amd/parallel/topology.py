@@ -80,13 +80,16 @@ class Cluster:
 
 
 def build_cluster(n_cns: int, n_dps: int, n_vns: int, world: int = 1, rank: int = 0, comm=None,
-                  deterministic_keys: bool = False) -> Cluster:
+                  deterministic_keys: bool = False, offsets: dict | None = None) -> Cluster:
     """Create parties, place them on ranks, generate each party's keys on its
-    hosting rank and share only the public keys (all_gather_object)."""
+    hosting rank and share only the public keys (all_gather_object).
+    ``offsets[role]`` shifts a role's round robin (e.g. VNs after the CNs, so
+    3 CNs and 3 VNs on an 8-GPU node occupy six different GPUs)."""
+    off = {"cn": 0, "dp": 0, "vn": 0, **(offsets or {})}
     cl = Cluster(world=world)
-    cl.cns = [Party(f"cn{i}", "cn", i % world) for i in range(n_cns)]
-    cl.dps = [Party(f"dp{i}", "dp", i % world) for i in range(n_dps)]
-    cl.vns = [Party(f"vn{i}", "vn", i % world) for i in range(n_vns)]
+    cl.cns = [Party(f"cn{i}", "cn", (off["cn"] + i) % world) for i in range(n_cns)]
+    cl.dps = [Party(f"dp{i}", "dp", (off["dp"] + i) % world) for i in range(n_dps)]
+    cl.vns = [Party(f"vn{i}", "vn", (off["vn"] + i) % world) for i in range(n_vns)]
     local_pub = {}
     for i, p in enumerate(cl.parties):
         if p.rank == rank:

@@ -55,6 +55,26 @@ def init_range_proof_signature(u: int, secret: int | None = None, device="cpu") 
     return PublishSignatureBytes(O.g1_to_bytes(y), bn.g2_aff_to_bytes(A).tobytes())
 
 
+def init_range_proof_signatures(us: list, device="cpu") -> list:
+    """Batched InitRangeProofSignature for many (CN, column) keys at once
+    (range_proof.go:270-288, simul/drynx_simul.go:292-296): one random secret
+    x per entry of ``us``; y = x*B and every A_k = (x+k)^-1 * B2 in two
+    fixed-base launches instead of one launch per key."""
+    n = len(us)
+    if n == 0:
+        return []
+    xs = [O.random_scalar() for _ in range(n)]
+    y = nt.g1_to_affine(nt.g1_fb_mul(bn.base_table(device), bn.scalars_tensor(xs, device)))
+    y_bytes = bn.g1_aff_to_bytes(y)
+    inv = [pow((x + k) % O.R, -1, O.R) for x, u in zip(xs, us) for k in range(int(u))]
+    A = bn.g2_aff_to_bytes(nt.g2_fb_mul(bn.base2_table(device), bn.scalars_tensor(inv, device)))
+    out, o = [], 0
+    for i, u in enumerate(us):
+        out.append(PublishSignatureBytes(y_bytes[i].tobytes(), A[o: o + int(u)].tobytes()))
+        o += int(u)
+    return out
+
+
 def init_range_proof_signature_deterministic(u: int, device="cpu") -> PublishSignatureBytes:
     """InitRangeProofSignatureDeterministic: x = 12 (range_proof.go:249)."""
     return init_range_proof_signature(u, 12, device)
@@ -131,21 +151,86 @@ class SigMaterial:
             self._ytab[key] = (nt.g1_fb_table(aff), torch.tensor(self.y_slot, dtype=torch.int32, device=device))
         return self._ytab[key]
 
+    def table_mode(self, device) -> int:
+        """Prover comb-table layout for this signature set on ``device``:
+        8 (8-bit combs, 4 MiB per distinct point: few distinct points, e.g.
+        InitRangeProofSignatureDeterministic), 4 (4-bit combs, 480 KiB per point:
+        the reference's random per-CN, per-column keys -- 99,360 points for a
+        SPECTF-shaped query with 3 CNs and u = 16, ~45 GiB of HBM) or 0 (no
+        tables: variable-base G2 + one pairing per item).  Budgets:
+        ``DRYNX_PROVER_TABLE_MB`` (8-bit, default 8 GiB on a GPU / 96 MiB on the
+        host) and ``DRYNX_PROVER_TABLE4_MB`` (4-bit, default 60% of the free HBM
+        / 64 MiB on the host)."""
+        dev = torch.device(device)
+        key = ("mode", str(dev))
+        if key in self._ptab:
+            return self._ptab[key]
+        n = self.n_distinct
+        forced = os.environ.get("DRYNX_PROVER_TABLE_BITS")
+        b8 = int(os.environ.get("DRYNX_PROVER_TABLE_MB", 8192 if dev.type == "cuda" else 96)) << 20
+        if "DRYNX_PROVER_TABLE4_MB" in os.environ:
+            b4 = int(os.environ["DRYNX_PROVER_TABLE4_MB"]) << 20
+        elif dev.type == "cuda":
+            b4 = int(0.6 * torch.cuda.mem_get_info(dev)[0])
+        else:
+            b4 = 64 << 20
+        if forced in ("0", "4", "8"):
+            mode = int(forced)
+        elif n * (4 << 20) <= b8:
+            mode = 8
+        elif n * nt.FB4_ENTRIES * (128 + 384) <= b4:
+            mode = 4
+        else:
+            mode = 0
+        self._ptab[key] = mode
+        return mode
+
+    @property
+    def n_distinct(self) -> int:
+        if not hasattr(self, "_n_distinct"):
+            self._n_distinct = int(torch.unique(self.canon).numel())
+        return self._n_distinct
+
+    def _prover_tables4(self, dev):
+        """4-bit comb tables of EVERY distinct signature point of the set, built
+        once (chunked) and kept in HBM for the set's lifetime; -> (g2, gt, slot
+        of each A index)."""
+        key = ("fb4", str(dev))
+        if key not in self._ptab:
+            uniq, slot = torch.unique(self.canon, return_inverse=True)
+            n = uniq.numel()
+            E = nt.FB4_ENTRIES
+            g2 = torch.empty((n * E, 32), dtype=torch.int32, device=dev)
+            gt = torch.empty((n * E, 96), dtype=torch.int32, device=dev)
+            A = self.A.to(dev)
+            step = 8192
+            with timers.span("rp.prove.tables4"):
+                for a in range(0, n, step):
+                    b = min(n, a + step)
+                    pts = A.index_select(0, uniq[a:b].to(dev)).contiguous()
+                    nt.g2_fb4_table(pts, out=g2[a * E: b * E])
+                    gphi = nt.pairing(bn.g1_generator_aff(dev).expand(b - a, 16).contiguous(), pts)
+                    nt.gt_fb4_table(gphi, out=gt[a * E: b * E])
+            self._ptab[key] = (g2, gt, slot.to(dev))
+        return self._ptab[key]
+
     def prover_tables(self, a_idx: torch.Tensor, device):
         """Comb tables (G2 for V = v*A, GT for e(B, A)) of the distinct signature
         points used by a proof batch, cached for the lifetime of the signature
-        set.  Returns (g2_tables, gt_tables, slot[a_idx-position]) or None when
-        the distinct points exceed the memory budget (1 MiB + 3 MiB each; budget
-        ``DRYNX_PROVER_TABLE_MB``, default 8 GiB on a GPU / 96 MiB on the host)."""
+        set.  Returns (g2_tables, gt_tables, slot[a_idx-position], wbits) or
+        None when no table layout fits the memory budget (``table_mode``)."""
         dev = torch.device(device)
+        mode = self.table_mode(dev)
+        if mode == 0:
+            return None
+        if mode == 4:
+            g2, gt, slot = self._prover_tables4(dev)
+            return g2, gt, slot.index_select(0, a_idx.to(dev)), 4
         canon = self.canon.to(a_idx.device).index_select(0, a_idx)
         uniq, inv = torch.unique(canon, return_inverse=True)
         key = str(dev)
         cache = self._ptab.setdefault(key, {"idx": [], "g2": None, "gt": None, "pos": {}})
         missing = [int(u) for u in uniq.tolist() if int(u) not in cache["pos"]]
-        budget = int(os.environ.get("DRYNX_PROVER_TABLE_MB", 8192 if dev.type == "cuda" else 96)) << 20
-        if (len(cache["pos"]) + len(missing)) * (4 << 20) > budget:
-            return None
         if missing:
             pts = self.A.to(dev).index_select(0, torch.tensor(missing, dtype=torch.long, device=dev)).contiguous()
             g2 = nt.g2_fb_table(pts)
@@ -157,7 +242,7 @@ class SigMaterial:
                 cache["pos"][m] = len(cache["idx"])
                 cache["idx"].append(m)
         slot_of_uniq = torch.tensor([cache["pos"][int(u)] for u in uniq.tolist()], dtype=torch.long, device=dev)
-        return cache["g2"], cache["gt"], slot_of_uniq.index_select(0, inv.to(dev))
+        return cache["g2"], cache["gt"], slot_of_uniq.index_select(0, inv.to(dev)), 8
 
 
 _gt_cache: dict = {}
@@ -420,12 +505,12 @@ def _prove_group(u, l, vals, offs, cols, r, cv, sigmat, P_point, device) -> Rang
     if tabs is not None:
         # table-driven prover: V = v * A_phi (G2 comb), a = e(B,A_phi)^{-s v} * gT^t (GT combs) —
         # no pairing and no final exponentiation per (value, server, digit)
-        g2_tabs, gphi_tabs, slot = tabs
+        g2_tabs, gphi_tabs, slot, wbits = tabs
         tidx = slot.index_select(0, inv).to(torch.int32).contiguous()
-        V = nt.g2_fb_mul(g2_tabs, v, tidx)
+        V = nt.g2_fb4_mul(g2_tabs, v, tidx) if wbits == 4 else nt.g2_fb_mul(g2_tabs, v, tidx)
         negs_rep = nt.fr_arith(nt.FR_NEG, s).view(n, 1, l, 8).expand(n, S, l, 8).reshape(-1, 8).contiguous()
         e = nt.fr_arith(nt.FR_MUL, negs_rep, v)
-        A = nt.rp_prove_a_tab(gphi_tabs, tidx, e, t, gt_tab, S, l)
+        A = nt.rp_prove_a_tab(gphi_tabs, tidx, e, t, gt_tab, S, l, wbits)
     else:
         A_sel = sigmat.A.to(device).index_select(0, a_index).contiguous()
         V = nt.g2_mul(A_sel, v)

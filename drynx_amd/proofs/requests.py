@@ -47,7 +47,7 @@ class ProofRequest:
     something needs them (ledger persistence, control-plane transport)."""
 
     __slots__ = ("kind", "survey_id", "sender_id", "differ_info", "_data", "signature", "obj", "data_digest",
-                 "tensor")
+                 "tensor", "decoded")
 
     def __init__(self, kind: str, survey_id: str, sender_id: str, differ_info: str, data: bytes | None,
                  signature: bytes, obj: Any = None, data_digest: bytes = b"", tensor: torch.Tensor | None = None):
@@ -57,6 +57,7 @@ class ProofRequest:
         self.obj = obj  # decoded proof (in-process fast path)
         self.data_digest = data_digest  # set for header-only copies (sharded verification)
         self.tensor = tensor
+        self.decoded = None  # the VN's own decode of the signed payload (cached across VNs of a rank)
 
     @property
     def data(self) -> bytes:
@@ -66,11 +67,11 @@ class ProofRequest:
 
     @data.setter
     def data(self, v: bytes):
-        self._data, self.tensor, self.data_digest = v, None, b""
+        self._data, self.tensor, self.data_digest, self.decoded = v, None, b"", None
 
     def set_tensor(self, t: torch.Tensor):
         """The payload is (now) this raw tensor; digest recomputed from it."""
-        self._data, self.tensor, self.data_digest = None, t, b""
+        self._data, self.tensor, self.data_digest, self.decoded = None, t, b"", None
 
     def payload(self):
         """Bytes or the device tensor, whichever is at hand (for the ledger)."""
@@ -261,12 +262,7 @@ def _ranges_ok(sq, rpl) -> bool:
 def verify_content(req: ProofRequest, sq, device, cache: VerifierCache) -> bool:
     P = sq.RosterServers.aggregate()
     if req.kind == "range":
-        if req.obj is not None:
-            rpls = req.obj
-        elif req.tensor is not None and req._data is None:
-            rpls = range_bundle_unpack(req.tensor.to(device))
-        else:
-            rpls = range_bundle_from_bytes(req.data, device)
+        rpls = _range_lists(req, device)
         sigs = sq.Query.IVSigs.InputValidationSigs
         for r in rpls:
             if not r.has_rp:
@@ -277,16 +273,16 @@ def verify_content(req: ProofRequest, sq, device, cache: VerifierCache) -> bool:
                 return False
         return True
     if req.kind == "aggregation":
-        pr = req.obj if req.obj is not None else ags.AggregationProof.from_bytes(req.data, device)
+        pr = _decode(req, device)
         return ags.aggregation_list_proof_verification(pr, sq.AggregationProofThreshold)
     if req.kind == "obfuscation":
-        pr = req.obj if req.obj is not None else sigma.ObfuscationProof.from_bytes(req.data, device)
+        pr = _decode(req, device)
         return sigma.obfuscation_list_proof_verification(pr, sq.ObfuscationProofThreshold)
     if req.kind == "shuffle":
-        pr = req.obj if req.obj is not None else shuffle.ShuffleProof.from_bytes(req.data, device)
+        pr = _decode(req, device)
         return shuffle.verify(pr, P)
     if req.kind == "keyswitch":
-        pr = req.obj if req.obj is not None else sigma.KeySwitchProof.from_bytes(req.data, device)
+        pr = _decode(req, device)
         if pr.X != sq.IDtoPublic.get(req.sender_id) or pr.Q != sq.ClientPubKey:
             return False
         return sigma.key_switch_list_proof_verification(pr, sq.KeySwitchingProofThreshold)
@@ -294,19 +290,28 @@ def verify_content(req: ProofRequest, sq, device, cache: VerifierCache) -> bool:
 
 
 def _range_lists(req: ProofRequest, device) -> list:
-    if req.obj is not None:
-        return req.obj
-    if req.tensor is not None and req._data is None:
-        return range_bundle_unpack(req.tensor.to(device))
-    return range_bundle_from_bytes(req.data, device)
+    """The VN's decode of the SIGNED payload (the raw limb tensor, or its bytes),
+    never the prover's in-memory object: what is verified is what the
+    signature covers (structs_proofs.go:158-182 unmarshals before verifying).
+    Decoding a packed tensor is views plus validity checks; the result is
+    cached on the request for the other VNs of this rank."""
+    if req.decoded is None:
+        if req.tensor is not None and req._data is None:
+            req.decoded = range_bundle_unpack(req.tensor.to(device))
+        else:
+            req.decoded = range_bundle_from_bytes(req.data, device)
+    return req.decoded
 
 
-def verify_range_many(reqs: list, idxs: list, sq, device, cache: VerifierCache) -> dict:
+def verify_range_many(reqs: list, idxs: list, sq, device, cache: VerifierCache, part=None) -> dict:
     """Range-proof requests of one VN as ONE batched verification: the sampled
     prefix of every list (reference RangeProofThreshold semantics) of every
     request, grouped by (u, l), folded into a single pairing batch.  If a
     batch fails, each request is re-checked alone so the bitmap blames
-    exactly the bad ones.  -> {request index: bool}"""
+    exactly the bad ones.  ``part = (k, W)`` checks only the k-th of W equal
+    slices of every sampled prefix (the pooled verification of a multi-GPU
+    node: W ranks each check one slice on the VN's behalf).
+    -> {request index: bool}"""
     P = sq.RosterServers.aggregate()
     sigs = sq.Query.IVSigs.InputValidationSigs
     out, parts = {}, {}
@@ -321,8 +326,11 @@ def verify_range_many(reqs: list, idxs: list, sq, device, cache: VerifierCache) 
                 if sigs is None or not _ranges_ok(sq, r):
                     raise ValueError("ranges / signatures do not match the query")
                 k = int(math.ceil(sq.RangeProofThreshold * len(r)))
-                if k:
-                    lists.append(r if k == len(r) else rp.rpl_range(r, 0, k))
+                lo, hi = 0, k
+                if part is not None:
+                    lo, hi = (k * part[0]) // part[1], (k * (part[0] + 1)) // part[1]
+                if hi > lo:
+                    lists.append(r if (lo, hi) == (0, len(r)) else rp.rpl_range(r, lo, hi))
             parts[i] = lists
             out[i] = True
         except Exception as e:
@@ -355,23 +363,30 @@ def verify_range_many(reqs: list, idxs: list, sq, device, cache: VerifierCache) 
     return out
 
 
+_DECODERS = {"keyswitch": lambda b, d: sigma.KeySwitchProof.from_bytes(b, d),
+             "obfuscation": lambda b, d: sigma.ObfuscationProof.from_bytes(b, d),
+             "aggregation": lambda b, d: ags.AggregationProof.from_bytes(b, d),
+             "shuffle": lambda b, d: shuffle.ShuffleProof.from_bytes(b, d)}
+
+
 def _decode(req: ProofRequest, device):
-    if req.obj is not None:
-        return req.obj
-    if req.kind == "keyswitch":
-        return sigma.KeySwitchProof.from_bytes(req.data, device)
-    if req.kind == "obfuscation":
-        return sigma.ObfuscationProof.from_bytes(req.data, device)
-    raise ValueError(req.kind)
+    """Unmarshal the signed bytes (cached per request across the VNs of a rank)."""
+    if req.decoded is None:
+        req.decoded = _DECODERS[req.kind](req.data, device)
+    return req.decoded
 
 
 _SIG_BATCH_MIN = 16  # inboxes at least this long check their envelope signatures in one batch
 
 
-def verify_requests(reqs: list, sq, vn_id: str, vn_index: int, n_vns: int, device, cache: VerifierCache) -> list:
+def verify_requests(reqs: list, sq, vn_id: str, vn_index: int, n_vns: int, device, cache: VerifierCache,
+                    range_pooled: dict | None = None) -> list:
     """VerifyProof for a VN's whole inbox.  Signatures and sampling per request;
     the content of the short per-CN proofs (key switch, obfuscation) is verified
-    in one batched launch per kind; range proofs are already one batch each."""
+    in one batched launch per kind; range proofs are already one batch each.
+    ``range_pooled``: {base_key: None (not sampled) | bool} -- this VN's range
+    results from the pooled verification (``pool_sampling`` decided the
+    sampling on this VN's rank beforehand)."""
     codes = [None] * len(reqs)
     todo: dict = {}
     if len(reqs) >= _SIG_BATCH_MIN:
@@ -388,6 +403,9 @@ def verify_requests(reqs: list, sq, vn_id: str, vn_index: int, n_vns: int, devic
                 sig_ok = verify_signature(req, sq.IDtoPublic.get(req.sender_id))
         if not sig_ok:
             codes[i] = PROOF_FALSE_SIGN
+        elif range_pooled is not None and req.kind == "range" and req.base_key() in range_pooled:
+            res = range_pooled[req.base_key()]
+            codes[i] = PROOF_RECEIVED if res is None else (PROOF_TRUE if res else PROOF_FALSE)
         elif not should_verify(sq, req, vn_index, n_vns):
             codes[i] = PROOF_RECEIVED
         else:
@@ -451,10 +469,12 @@ def verify_requests(reqs: list, sq, vn_id: str, vn_index: int, n_vns: int, devic
 
 
 class _EarlyReq:
-    __slots__ = ("obj", "sender_id")
+    """The prover's own lists, checked speculatively (opt-in DRYNX_EARLY_RANGE);
+    the result is only used for the request whose payload packs these lists."""
+    __slots__ = ("obj", "sender_id", "decoded")
 
     def __init__(self, obj, sender_id):
-        self.obj, self.sender_id = obj, sender_id
+        self.obj, self.sender_id, self.decoded = obj, sender_id, obj
 
 
 def start_early_range_verification(items: list, sq, device, cache: VerifierCache, ready_event=None):

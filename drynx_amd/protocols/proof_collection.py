@@ -17,6 +17,7 @@ block travel on the control plane.
 from __future__ import annotations
 
 import json
+import os
 
 import torch
 
@@ -36,10 +37,20 @@ def expected_counts(sq) -> dict:
     return dict(zip(prq.QUERY_ORDER, q))
 
 
-def fan_out(ctx, sq, local_requests: list) -> list:
-    """All requests, on every rank that hosts a VN (others get nothing)."""
+def use_pool(ctx) -> bool:
+    """Pooled range verification: on a multi-GPU node every rank checks a
+    1/world slice of every range-proof list on behalf of every VN (so three VNs
+    keep eight GPUs busy); the VN's own rank keeps the signature checks, the
+    sampling decision, the bitmap and the ledger.  ``DRYNX_VN_POOL=0`` leaves
+    each VN's range checks on its own rank."""
+    return ctx.comm.world > 1 and os.environ.get("DRYNX_VN_POOL", "1") != "0"
+
+
+def fan_out(ctx, sq, local_requests: list, all_ranks: bool = False) -> list:
+    """All requests, on every rank that hosts a VN (others get nothing), or on
+    every rank (``all_ranks``: pooled verification)."""
     vns = [ctx.cluster.by_id(si.id) for si in sq.Query.RosterVNs.list]
-    vn_ranks = sorted({v.rank for v in vns})
+    vn_ranks = list(range(ctx.comm.world)) if all_ranks else sorted({v.rank for v in vns})
     if ctx.comm.world == 1:
         return list(local_requests)
     # sharded verification: ship the payload only to ranks hosting an assigned
@@ -51,7 +62,7 @@ def fan_out(ctx, sq, local_requests: list) -> list:
     packed = {}
     for idx, r in enumerate(local_requests):
         assigned = prq.assigned_vns(sq, r, len(vns))
-        full_ranks = vn_ranks if assigned is None else {vns[i].rank for i in assigned}
+        full_ranks = vn_ranks if (assigned is None or all_ranks) else {vns[i].rank for i in assigned}
         for d in vn_ranks:
             if d not in full_ranks:
                 per_rank[d].append(r.header().to_wire())
@@ -79,17 +90,48 @@ def fan_out(ctx, sq, local_requests: list) -> list:
             if n:
                 t = got_t[src][off: off + n]
                 off += n
-                req.obj = prq.range_bundle_unpack(t)
-                req.set_tensor(t)  # signed bytes: the VN re-hashes them on its device
+                req.set_tensor(t)  # signed bytes: the VN re-hashes and decodes them on its device
             out.append(req)
     return out
 
 
-def verify_and_store(ctx, sq, vn, vn_index: int, n_vns: int, requests: list) -> dict:
+def pool_verify_ranges(ctx, sq, reqs: list, vns: list) -> dict:
+    """Pooled range verification (see ``use_pool``).  Sampling is decided by
+    each VN's own rank (reference ``rand.Float64() <= Threshold``, or the
+    sharding extension) and shared; rank k then checks slice k/W of the
+    sampled prefix of every list, one batch per VN with that VN's own random
+    weights; the slice verdicts are all-gathered and AND-ed.
+    -> {vn_id: {base_key: None (not sampled) | bool}} on every rank."""
+    W, k = ctx.comm.world, ctx.comm.rank
+    rng = [i for i, r in enumerate(reqs) if r.kind == "range" and not r.header_only]
+    local = {}
+    for vi, vn in enumerate(vns):
+        if vn.rank == ctx.rank:
+            local[vn.id] = {reqs[i].base_key(): prq.should_verify(sq, reqs[i], vi, len(vns)) for i in rng}
+    sampled = {}
+    for d in ctx.comm.all_gather_object(local):
+        sampled.update(d)
+    mine = {}
+    for vn in vns:
+        idxs = [i for i in rng if sampled[vn.id].get(reqs[i].base_key())]
+        res = {}
+        if idxs:
+            with timers.timed(f"{vn.id}_VerifyRange"):
+                res = prq.verify_range_many(reqs, idxs, sq, ctx.device, ctx.verifier_cache, part=(k, W))
+        mine[vn.id] = {reqs[i].base_key(): bool(ok) for i, ok in res.items()}
+    verdicts = ctx.comm.all_gather_object(mine)
+    out = {}
+    for vn in vns:
+        out[vn.id] = {key: (None if not smp else all(v[vn.id].get(key, False) for v in verdicts))
+                      for key, smp in sampled[vn.id].items()}
+    return out
+
+
+def verify_and_store(ctx, sq, vn, vn_index: int, n_vns: int, requests: list, range_pooled: dict | None = None) -> dict:
     store = ctx.store(vn.id)
     bitmap = {}
     counts = {k: 0 for k in prq.VN_ORDER}
-    codes = prq.verify_requests(requests, sq, vn.id, vn_index, n_vns, ctx.device, ctx.verifier_cache)
+    codes = prq.verify_requests(requests, sq, vn.id, vn_index, n_vns, ctx.device, ctx.verifier_cache, range_pooled)
     for req, code in zip(requests, codes):
         key = req.key(vn.id)
         bitmap[key] = code
@@ -108,13 +150,15 @@ def verify_and_store(ctx, sq, vn, vn_index: int, n_vns: int, requests: list) -> 
 def proof_collection(ctx, sq, local_requests: list):
     """Returns the new SkipBlock (on every rank)."""
     vns = [ctx.cluster.by_id(si.id) for si in sq.Query.RosterVNs.list]
+    pool = use_pool(ctx)
     with timers.timed("ProofFanOut"):
-        reqs = fan_out(ctx, sq, local_requests)
+        reqs = fan_out(ctx, sq, local_requests, all_ranks=pool)
     bitmaps = {}
     with timers.timed("ProofVerification"):
+        pooled = pool_verify_ranges(ctx, sq, reqs, vns) if pool else {}
         for idx, vn in enumerate(vns):
             if vn.rank == ctx.rank:
-                bitmaps[vn.id] = verify_and_store(ctx, sq, vn, idx, len(vns), reqs)
+                bitmaps[vn.id] = verify_and_store(ctx, sq, vn, idx, len(vns), reqs, pooled.get(vn.id))
     # bitmaps -> root VN (SharedBMChannel)
     allbm = {}
     for d in ctx.comm.all_gather_object(bitmaps):

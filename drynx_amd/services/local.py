@@ -25,27 +25,29 @@ RANGE_PRESETS = {  # simul/drynx_simul.go:133-281 `Ranges` codes -> (u, l)
 
 
 def local_cluster(n_cns=3, n_dps=5, n_vns=3, comm: Comm | None = None, device=None, workdir=None,
-                  deterministic_keys=False, dp_data=None):
+                  deterministic_keys=False, dp_data=None, offsets=None):
     comm = comm or LocalComm(device or ("cuda" if torch.cuda.is_available() else "cpu"))
-    cl = build_cluster(n_cns, n_dps, n_vns, comm.world, comm.rank, comm, deterministic_keys)
+    cl = build_cluster(n_cns, n_dps, n_vns, comm.world, comm.rank, comm, deterministic_keys, offsets)
     node = DrynxNode(cl, comm, workdir or tempfile.mkdtemp(prefix="drynx_db_"), device or comm.device, dp_data)
     return cl, node
 
 
 def make_signatures(cluster, ranges, device="cpu", deterministic=False):
     """InputValidationSigs[cn][col]: one BB key + u signatures per (CN, output)."""
+    if not deterministic:  # the reference default: fresh random keys per CN and per column
+        flat = rp.init_range_proof_signatures([int(r[0]) for _ in cluster.cns for r in ranges], device)
+        n = len(ranges)
+        return [flat[i * n:(i + 1) * n] for i in range(len(cluster.cns))]
     out = []
     det: dict = {}
     for _ in cluster.cns:
         row = []
         for r in ranges:
             u = int(r[0])
-            if deterministic:  # InitRangeProofSignatureDeterministic: identical keys (x = 12), computed once per u
-                if u not in det:
-                    det[u] = rp.init_range_proof_signature_deterministic(u, device)
-                row.append(det[u])
-            else:
-                row.append(rp.init_range_proof_signature(u, None, device))
+            # InitRangeProofSignatureDeterministic: identical keys (x = 12), computed once per u
+            if u not in det:
+                det[u] = rp.init_range_proof_signature_deterministic(u, device)
+            row.append(det[u])
         out.append(row)
     return out
 

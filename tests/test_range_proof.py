@@ -94,3 +94,19 @@ def test_device_challenge_hash_matches_sha3_512():
     got = bn.scalars_from_tensor(nt.rp_challenges(aff, bw, yw, torch.tensor(cols, dtype=torch.int32)))
     exp = rp._challenge_hash(bn.g1_aff_to_bytes(aff), [ys[c] for c in cols])
     assert got == exp
+
+
+@pytest.mark.parametrize("bits", ["8", "4", "0"])
+def test_prover_table_layouts_agree(setup, bits, monkeypatch):
+    """8-bit combs, 4-bit (HBM-sized, random per-CN per-column keys) and the
+    table-free prover all produce proofs the batched and the per-equation
+    reference verifiers accept."""
+    S, u, l, sigs, _, P, pk = setup
+    monkeypatch.setenv("DRYNX_PROVER_TABLE_BITS", bits)
+    sm = rp.SigMaterial(sigs)  # fresh: the layout is chosen once per signature set
+    assert sm.table_mode("cpu") == int(bits)
+    cv, r = eg.encrypt_ints(pk, [3, 40, 63])
+    b = CreateProofBatch([3, 40, 63], r, cv, [u] * 3, [l] * 3, [0, 1, 2], [0] * 3)
+    rpl = rp.create_range_proofs(b, sm, P)[0]
+    assert rp.verify_range_proof_list(rpl, sm, P)
+    assert all(rp.verify_range_proof_single_reference(rpl, p, sm, P) for p in range(3))
