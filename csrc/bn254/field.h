@@ -14,7 +14,12 @@
 #include "constants.h"
 
 #define DX_HD __host__ __device__ __forceinline__
+// DX_NI: out-of-line tower/curve functions (small code, shared by the kernels
+// of a translation unit).  A TU may predefine it as force-inline to get one
+// register-allocated body per kernel instead (dx_fold_inl.hip).
+#ifndef DX_NI
 #define DX_NI __host__ __device__ __noinline__ inline
+#endif
 // The Montgomery multiply is force-inlined into device code (register
 // allocation across a whole Fp2/Fp6 product) but kept out-of-line on the host,
 // where x86 instruction selection of thousands of unrolled 64-bit MACs would

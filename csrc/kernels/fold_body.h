@@ -1,0 +1,200 @@
+// Two-phase batched Miller fold of the range-proof verifier (K16 hot loop),
+// included by dx_fold.hip (tower functions out of line) and dx_fold_inl.hip
+// (everything force-inlined); FOLD_SFX names the variant's entry points.
+//
+// The verifier needs prod_it ML(P_it, V_it) over ~1e6 items per VN inbox
+// (lib/range/range_proof.go:522-553 computes 3 pairings per item instead).
+// One fused kernel per item holds the Fp12 accumulator (96 VGPRs), the twist
+// point (48), the G2 operand (32) and the tower temporaries at once, which
+// capped it at 256 VGPRs with call-frame spills.  Here:
+//   phase 1 (rp_lines): per item, the G2 side of the Miller loop only -- the
+//     88 sparse line values (l0, l1, l3) evaluated at P, streamed to HBM in a
+//     coalesced [step][12][item] uint4 image (192 B per step and item);
+//   phase 2 (rp_accum): per lane K items share ONE accumulator,
+//     f <- f^2 * prod_k l_k(P_k) (a multi-Miller loop: one Fp12 squaring per
+//     step for K items instead of K), then the LDS tree folds the workgroup.
+// The product over items is all the batch equation needs.
+#pragma once
+#include "common.h"
+
+#define FOLD_CAT2(a, b) a##b
+#define FOLD_CAT(a, b) FOLD_CAT2(a, b)
+#define FOLD_NAME(x) FOLD_CAT(x, FOLD_SFX)
+
+namespace FOLD_NAME(fold_ns_) {
+
+constexpr int kWG = 64;
+constexpr int count_add_steps() {
+  int c = 0;
+  for (int i = ATE_NAF_LEN - 2; i >= 0; i--) c += ATE_NAF[i] != 0 ? 1 : 0;
+  return c;
+}
+constexpr int kSteps = (ATE_NAF_LEN - 1) + count_add_steps() + 2;  // doublings + NAF additions + 2 Frobenius lines
+
+// line image: uint4 word q (0..11) of step s, item it at lines[(s*12 + q)*n + it]
+__device__ __forceinline__ void store_line(uint4 *lines, int64_t n, int s, int64_t it, const Fp2 &l0, const Fp2 &l1,
+                                           const Fp2 &l3) {
+  const Fp2 *src[3] = {&l0, &l1, &l3};
+#pragma unroll
+  for (int c = 0; c < 3; c++) {
+    const uint32_t *w = reinterpret_cast<const uint32_t *>(src[c]);
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+      lines[((int64_t)s * 12 + c * 4 + q) * n + it] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+  }
+}
+
+__device__ __forceinline__ void load_line(const uint4 *__restrict__ lines, int64_t n, int s, int64_t it, Fp2 &l0,
+                                          Fp2 &l1, Fp2 &l3) {
+  Fp2 *dst[3] = {&l0, &l1, &l3};
+#pragma unroll
+  for (int c = 0; c < 3; c++) {
+    uint32_t *w = reinterpret_cast<uint32_t *>(dst[c]);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const uint4 v = lines[((int64_t)s * 12 + c * 4 + q) * n + it];
+      w[4 * q] = v.x;
+      w[4 * q + 1] = v.y;
+      w[4 * q + 2] = v.z;
+      w[4 * q + 3] = v.w;
+    }
+  }
+}
+
+// Same formulas as pairing.h miller_dbl / miller_add (validated against the
+// oracle), reordered so each line value is stored as soon as it exists and
+// the twist-point update runs with the line temporaries already dead.
+__device__ __forceinline__ void line_dbl(Fp2 &X, Fp2 &Y, Fp2 &Z, const Fp &xP, const Fp &yP, uint4 *lines, int64_t n,
+                                         int s, int64_t it) {
+  const Fp2 b2 = Fp2::from_limbs(Curve::B2);
+  Fp2 X2 = sqr(X);
+  const Fp2 l1 = mul_fp(add(dbl(X2), X2), xP);
+  Fp2 Bq = sqr(Y);
+  Fp2 C = sqr(Z);
+  Fp2 H = sub(sub(sqr(add(Y, Z)), Bq), C);
+  const Fp2 l0 = neg(mul_fp(H, yP));
+  Fp2 E = mul(add(dbl(C), C), b2);
+  const Fp2 l3 = sub(E, Bq);
+  store_line(lines, n, s, it, l0, l1, l3);
+  Fp2 F = add(dbl(E), E);
+  Fp2 A = mul(X, Y);
+  X = dbl(mul(A, sub(Bq, F)));
+  Z = dbl(dbl(mul(Bq, H)));
+  Fp2 E2 = sqr(E);
+  Y = sub(sqr(add(Bq, F)), dbl(dbl(add(dbl(E2), E2))));
+}
+
+__device__ __forceinline__ void line_add(Fp2 &X, Fp2 &Y, Fp2 &Z, const Fp2 &x2, const Fp2 &y2, const Fp &xP,
+                                         const Fp &yP, uint4 *lines, int64_t n, int s, int64_t it) {
+  Fp2 th = sub(Y, mul(y2, Z));
+  Fp2 la = sub(X, mul(x2, Z));
+  store_line(lines, n, s, it, mul_fp(la, yP), neg(mul_fp(th, xP)), sub(mul(th, x2), mul(la, y2)));
+  Fp2 C = sqr(th), D = sqr(la);
+  Fp2 E = mul(D, la), F = mul(Z, C), G = mul(X, D);
+  Fp2 H = sub(add(E, F), dbl(G));
+  Y = sub(mul(th, sub(G, H)), mul(Y, E));
+  X = mul(la, H);
+  Z = mul(Z, E);
+}
+
+__global__ void __launch_bounds__(kWG) DX_OCC rp_lines_kernel(const uint32_t *__restrict__ P_aff,
+                                                              const uint32_t *__restrict__ V_aff,
+                                                              uint4 *__restrict__ lines, int64_t n) {
+  const int64_t it = (int64_t)blockIdx.x * kWG + threadIdx.x;
+  if (it >= n) return;
+  const G1A P = at<G1A>(P_aff, it);
+  const G2A Q = at<G2A>(V_aff, it);
+  if (P.is_inf() || Q.is_inf()) {  // ML = 1: identity lines
+    for (int s = 0; s < kSteps; s++) store_line(lines, n, s, it, Fp2::one(), Fp2::zero(), Fp2::zero());
+    return;
+  }
+  Fp2 X = Q.x, Y = Q.y, Z = Fp2::one();
+  int s = 0;
+  for (int i = ATE_NAF_LEN - 2; i >= 0; i--) {
+    line_dbl(X, Y, Z, P.x, P.y, lines, n, s++, it);
+    const int d = ATE_NAF[i];
+    if (d != 0) {
+      // re-read Q at each addition step instead of pinning 32 VGPRs for it
+      asm volatile("" ::: "memory");
+      const G2A q = at<G2A>(V_aff, it);
+      line_add(X, Y, Z, q.x, d > 0 ? q.y : neg(q.y), P.x, P.y, lines, n, s++, it);
+    }
+  }
+  asm volatile("" ::: "memory");
+  const G2A q = at<G2A>(V_aff, it);
+  line_add(X, Y, Z, mul(conj(q.x), Fp2::from_limbs(Frob::TWX1)), mul(conj(q.y), Fp2::from_limbs(Frob::TWY1)), P.x,
+           P.y, lines, n, s++, it);
+  line_add(X, Y, Z, mul(q.x, Fp2::from_limbs(Frob::TWX2)), neg(mul(q.y, Fp2::from_limbs(Frob::TWY2))), P.x, P.y,
+           lines, n, s++, it);
+}
+
+template <int K>
+__device__ __forceinline__ void accum_step(Fp12 &f, const uint4 *__restrict__ lines, int64_t n, int s, int64_t base) {
+#pragma unroll 1
+  for (int k = 0; k < K; k++) {
+    const int64_t it = base + (int64_t)k * kWG;
+    if (it < n) {
+      Fp2 l0, l1, l3;
+      load_line(lines, n, s, it, l0, l1, l3);
+      f = mul_line(f, l0, l1, l3);
+    }
+  }
+}
+
+// Lane `lane` of workgroup b owns items b*64*K + k*64 + lane (k < K): each
+// uint4 load of a step is one contiguous 1 KiB wave access.
+template <int K>
+__global__ void __launch_bounds__(kWG) DX_OCC rp_accum_kernel(const uint4 *__restrict__ lines, uint32_t *f_blk,
+                                                              int64_t n) {
+  __shared__ Fp12 sf[kWG / 2];
+  const int lane = threadIdx.x;
+  const int64_t base = (int64_t)blockIdx.x * kWG * K + lane;
+  Fp12 f = Fp12::one();
+  int s = 0;
+  for (int i = ATE_NAF_LEN - 2; i >= 0; i--) {
+    if (i != ATE_NAF_LEN - 2) f = sqr(f);
+    accum_step<K>(f, lines, n, s++, base);
+    if (ATE_NAF[i] != 0) accum_step<K>(f, lines, n, s++, base);
+  }
+  accum_step<K>(f, lines, n, s++, base);
+  accum_step<K>(f, lines, n, s++, base);
+  for (int h = kWG / 2; h > 0; h >>= 1) {
+    if (lane >= h && lane < 2 * h) sf[lane - h] = f;
+    __syncthreads();
+    if (lane < h) f = mul(f, sf[lane]);
+    __syncthreads();
+  }
+  if (lane == 0) at<Fp12>(f_blk, blockIdx.x) = f;
+}
+
+}  // namespace
+
+extern "C" {
+int FOLD_NAME(dx_fold_steps_)() { return FOLD_NAME(fold_ns_)::kSteps; }
+
+int FOLD_NAME(dx_rp_lines_)(void *stream, const uint32_t *P_aff, const uint32_t *V_aff, uint32_t *lines, int64_t n) {
+  using namespace FOLD_NAME(fold_ns_);
+  if (n <= 0) return 0;
+  const int64_t blocks = (n + kWG - 1) / kWG;
+  hipLaunchKernelGGL(rp_lines_kernel, dim3((unsigned)blocks), dim3(kWG), 0, (hipStream_t)stream, P_aff, V_aff,
+                     reinterpret_cast<uint4 *>(lines), n);
+  return check_hip(hipGetLastError(), "rp_lines");
+}
+
+// f_blk: ceil(n / (64 K)) Fp12 partial products.
+int FOLD_NAME(dx_rp_accum_)(void *stream, const uint32_t *lines, uint32_t *f_blk, int64_t n, int K) {
+  using namespace FOLD_NAME(fold_ns_);
+  if (n <= 0) return 0;
+  const int64_t blocks = (n + (int64_t)kWG * K - 1) / ((int64_t)kWG * K);
+  const uint4 *L = reinterpret_cast<const uint4 *>(lines);
+  hipStream_t st = (hipStream_t)stream;
+  switch (K) {
+    case 1: hipLaunchKernelGGL(rp_accum_kernel<1>, dim3((unsigned)blocks), dim3(kWG), 0, st, L, f_blk, n); break;
+    case 2: hipLaunchKernelGGL(rp_accum_kernel<2>, dim3((unsigned)blocks), dim3(kWG), 0, st, L, f_blk, n); break;
+    case 4: hipLaunchKernelGGL(rp_accum_kernel<4>, dim3((unsigned)blocks), dim3(kWG), 0, st, L, f_blk, n); break;
+    case 8: hipLaunchKernelGGL(rp_accum_kernel<8>, dim3((unsigned)blocks), dim3(kWG), 0, st, L, f_blk, n); break;
+    default: return -2;
+  }
+  return check_hip(hipGetLastError(), "rp_accum");
+}
+}  // extern "C"

@@ -101,6 +101,12 @@ _SIGS = {
     "dx_g2_fb4_mul": [_I, _P, _P, _P, _P, _P, _L],
     "dx_gt_fb4_table": [_I, _P, _P, _P, _P, _L],
     "dx_gt_fb4_pow": [_I, _P, _P, _P, _P, _P, _L],
+    "dx_fold_steps_ni": [],
+    "dx_rp_lines_ni": [_P, _P, _P, _P, _L],
+    "dx_rp_accum_ni": [_P, _P, _P, _L, _I],
+    "dx_fold_steps_inl": [],
+    "dx_rp_lines_inl": [_P, _P, _P, _P, _L],
+    "dx_rp_accum_inl": [_P, _P, _P, _L, _I],
     "dx_rp_verify_items": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _I],
 }
 
@@ -719,6 +725,37 @@ def rp_verify_fold(ZB_jac, Y_jac, rho, V_aff, S: int, L: int) -> torch.Tensor:
     rc = _load().dx_rp_verify_fold(s, _ptr(ZB_jac), _ptr(Y_jac), _ptr(rho), _ptr(V_aff), _ptr(fb), n, S, L)
     if rc:
         raise RuntimeError(f"dx_rp_verify_fold failed rc={rc}")
+    return fb
+
+
+FOLD_VARIANT = os.environ.get("DRYNX_FOLD_VARIANT", "ni")  # ni: tower out of line, inl: force-inlined
+
+
+def rp_fold_lines(P_aff: torch.Tensor, V_aff: torch.Tensor, variant: str | None = None) -> torch.Tensor:
+    """Phase 1 of the two-phase Miller fold (GPU): the sparse line values of
+    every item's Miller loop evaluated at its P -> flat int32 image
+    [steps * 12 * n * 4] (csrc/kernels/fold_body.h)."""
+    v = variant or FOLD_VARIANT
+    n = _rows(P_aff, 16)
+    assert _rows(V_aff, 32) == n and P_aff.is_cuda
+    steps = getattr(_load(), f"dx_fold_steps_{v}")()
+    lines = torch.empty((steps * 12 * n * 4,), dtype=torch.int32, device=P_aff.device)
+    _, s = _ctx(P_aff, V_aff)
+    rc = getattr(_load(), f"dx_rp_lines_{v}")(s, _ptr(P_aff), _ptr(V_aff), _ptr(lines), n)
+    if rc:
+        raise RuntimeError(f"dx_rp_lines_{v} failed rc={rc}")
+    return lines
+
+
+def rp_fold_accum(lines: torch.Tensor, n: int, K: int = 4, variant: str | None = None) -> torch.Tensor:
+    """Phase 2: per-workgroup products of the Miller values of 64*K items,
+    K items per lane sharing one accumulator -> [ceil(n / (64 K)), 96]."""
+    v = variant or FOLD_VARIANT
+    fb = torch.empty(((n + 64 * K - 1) // (64 * K), 96), dtype=torch.int32, device=lines.device)
+    _, s = _ctx(lines)
+    rc = getattr(_load(), f"dx_rp_accum_{v}")(s, _ptr(lines), _ptr(fb), n, K)
+    if rc:
+        raise RuntimeError(f"dx_rp_accum_{v} failed rc={rc}")
     return fb
 
 

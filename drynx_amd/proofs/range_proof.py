@@ -126,8 +126,13 @@ class SigMaterial:
         # the verifier's c*y_i be fixed-base multiplications
         ykeys = [O.g1_to_bytes(y) for y in ys]
         yfirst: dict = {}
-        self.y_slot = [yfirst.setdefault(k, len(yfirst)) for k in ykeys]
-        self.y_distinct = [ys[ykeys.index(k)] for k in yfirst]
+        first_idx: dict = {}
+        for i, k in enumerate(ykeys):
+            if k not in yfirst:
+                yfirst[k] = len(yfirst)
+                first_idx[k] = i
+        self.y_slot = [yfirst[k] for k in ykeys]
+        self.y_distinct = [ys[first_idx[k]] for k in yfirst]
         self._ytab = {}
 
     def challenge_words(self, device):
@@ -603,7 +608,7 @@ def verify_range_proof_list(rpl: RangeProofList, sigmat: SigMaterial, P_point, t
             with timers.span("rp.verify.gt_plan"):
                 plan = nt._multi_exp64_plan(rho)
             G = nt._multi_exp64_run(r.A, plan)
-            fb = nt.rp_verify_fold(ZB, Y, rho, r.V, S, l)
+            fb = _miller_fold(ZB, Y, rho, r.V, S, l)
         elif order == "1":
             # the Miller fold (the long pole, ~20 ms for a 2070-value list)
             # is queued as soon as its inputs are; the D-equation MSM and the
@@ -619,9 +624,9 @@ def verify_range_proof_list(rpl: RangeProofList, sigmat: SigMaterial, P_point, t
             if fs is not None:
                 fs.wait_stream(cur)
                 with torch.cuda.stream(fs):
-                    fb = nt.rp_verify_fold(ZB, Y, rho, r.V, S, l)
+                    fb = _miller_fold(ZB, Y, rho, r.V, S, l)
             else:
-                fb = nt.rp_verify_fold(ZB, Y, rho, r.V, S, l)         # Miller values, LDS-folded
+                fb = _miller_fold(ZB, Y, rho, r.V, S, l)         # Miller values, LDS-folded
             with torch.cuda.stream(aux):
                 if not dcheck_finish(dcheck_launch()):
                     return False
@@ -644,7 +649,7 @@ def verify_range_proof_list(rpl: RangeProofList, sigmat: SigMaterial, P_point, t
             aux.wait_stream(cur)
             with torch.cuda.stream(aux), timers.span("rp.verify.gt_plan"):
                 plan = nt._multi_exp64_plan(rho)
-            fb = nt.rp_verify_fold(ZB, Y, rho, r.V, S, l)                 # Miller values, LDS-folded
+            fb = _miller_fold(ZB, Y, rho, r.V, S, l)                 # Miller values, LDS-folded
             with torch.cuda.stream(aux):
                 G = nt._multi_exp64_run(r.A, plan)                         # prod a^rho (host tensor)
         F = nt._finish_prod_on_host(fb)
@@ -661,6 +666,29 @@ def verify_range_proof_list(rpl: RangeProofList, sigmat: SigMaterial, P_point, t
     _, gt_tab = gt_generator_table("cpu")
     rhs_gt = nt.gt_fb_pow(gt_tab, e)
     return bool(nt.gt_eq(lhs_gt, rhs_gt).all())
+
+
+def _miller_fold(ZB, Y, rho, V, S: int, L: int) -> torch.Tensor:
+    """GPU: per-workgroup partial products of ML(rho_it (ZB[p,j] - Y[p,i]), V_it)
+    over every item it = (p*S + i)*L + j.  Default: the two-phase fold
+    (csrc/kernels/fold_body.h) -- the G1 side as three wide launches (point
+    difference, 64-bit variable-base multiplication, affine conversion), then
+    the line image and the K-item multi-Miller accumulation.
+    ``DRYNX_FOLD=fused`` selects the previous one-kernel fold."""
+    if os.environ.get("DRYNX_FOLD", "2") == "fused":
+        return nt.rp_verify_fold(ZB, Y, rho, V, S, L)
+    n = V.shape[0]
+    if n == 0:
+        return nt.gt_one(V.device).clone()
+    npj = ZB.shape[0] // L
+    with timers.span("rp.verify.fold_points"):
+        zb = ZB.view(npj, 1, L, 24).expand(npj, S, L, 24).reshape(-1, 24)
+        yy = Y.view(npj, S, 1, 24).expand(npj, S, L, 24).reshape(-1, 24)
+        P = nt.g1_to_affine(nt.g1_mul(nt.g1_add(zb.contiguous(), yy.contiguous(), subtract=True), rho))
+    K = next((k for k in (8, 4, 2) if (n + 64 * k - 1) // (64 * k) >= 1024), 1)
+    with timers.span("rp.verify.fold_lines"):
+        lines = nt.rp_fold_lines(P, V)
+    return nt.rp_fold_accum(lines, n, K)
 
 
 _aux: dict = {}

@@ -245,3 +245,65 @@ def test_survey_early_range_and_cu_masked_fold_gpu(gpu_device, tmp_path, monkeyp
     assert set(res.block.data_block().Proofs.values()) == {1}
     assert not node.verifier_cache._early  # consumed
     node.close(remove=True)
+
+
+@pytest.mark.parametrize("variant", ["ni", "inl"])
+def test_two_phase_fold_matches_oracle(gpu_device, variant):
+    """Line image + K-item multi-Miller accumulation == product of the
+    oracle's pairings (after one final exponentiation), for every K."""
+    m = 67  # a ragged last workgroup for every K
+    ks = [RNG.randrange(1, O.R) for _ in range(m)]
+    kq = [RNG.randrange(1, O.R) for _ in range(m)]
+    P = nt.g1_to_affine(nt.g1_fb_mul(bn.base_table(gpu_device), bn.scalars_tensor(ks, gpu_device)))
+    V = nt.g2_fb_mul(bn.base2_table(gpu_device), bn.scalars_tensor(kq, gpu_device))
+    P[5] = 0  # a point at infinity contributes 1
+    # e(a B, b B2) = gT^(a b): the oracle's product of the pairings
+    gT = O.pairing(O.G1_GEN, O.G2_GEN)
+    expo = sum(a * b for i, (a, b) in enumerate(zip(ks, kq)) if i != 5) % O.R
+    want = gT ** expo
+    lines = nt.rp_fold_lines(P, V, variant)
+    for K in (1, 2, 4, 8):
+        fb = nt.rp_fold_accum(lines, m, K, variant)
+        got = nt.final_exp(nt._finish_prod_on_host(fb))
+        assert bn.gt_from_tensor(got)[0] == want, K
+
+
+def test_fb4_combs_match_oracle(gpu_device):
+    ks = [RNG.randrange(O.R) for _ in range(40)] + [0, 1, O.R - 1]
+    k = bn.scalars_tensor(ks, gpu_device)
+    Q = O.g2_mul(RNG.randrange(1, O.R), O.G2_GEN)
+    tab = nt.g2_fb4_table(bn.g2_aff_tensor([Q], gpu_device))
+    got = bn.g2_points_from_aff(nt.g2_fb4_mul(tab, k).cpu())
+    assert got == [O.g2_mul(x, Q) for x in ks]
+    e = nt.pairing(bn.g1_generator_aff(gpu_device), bn.g2_aff_tensor([Q], gpu_device))
+    gt_tab = nt.gt_fb4_table(e)
+    g = bn.gt_from_tensor(nt.gt_fb4_pow(gt_tab, k).cpu())
+    e0 = bn.gt_from_tensor(e.cpu())[0]
+    assert g[:3] == [e0 ** x for x in ks[:3]]
+    assert torch.equal(nt.gt_fb4_pow(gt_tab, k), nt.gt_pow(e.expand(len(ks), 96).contiguous(), k))
+
+
+@pytest.mark.parametrize("bits", ["8", "4", "0"])
+def test_range_prover_layouts_gpu(gpu_device, bits, monkeypatch):
+    """Every prover path on the GPU with random per-CN, per-column keys:
+    8-bit combs, the HBM-sized 4-bit combs, and the table-free path
+    (variable-base G2 + one pairing per item)."""
+    from drynx_amd.crypto import elgamal as eg
+    from drynx_amd.ops.encoding import CreateProofBatch
+    from drynx_amd.proofs import range_proof as rp
+
+    monkeypatch.setenv("DRYNX_PROVER_TABLE_BITS", bits)
+    S, u, l, ncol = 3, 16, 4, 5
+    sigs = [rp.init_range_proof_signatures([u] * ncol, gpu_device) for _ in range(S)]
+    sm = rp.SigMaterial(sigs, gpu_device)
+    assert sm.table_mode(gpu_device) == int(bits)
+    P = eg.aggregate_keys([eg.KeyPair.generate().public for _ in range(S)])
+    vals = [0, 1, 65535, 1234, 999]
+    cv, r = eg.encrypt_ints(eg.pk_table(P, gpu_device), vals)
+    rpl = rp.create_range_proofs(CreateProofBatch(vals, r, cv, [u] * 5, [l] * 5, list(range(5)), [0] * 5), sm, P,
+                                 gpu_device)[0]
+    assert rp.verify_range_proof_list(rpl, sm, P, 1.0, gpu_device)
+    cpu_sm = rp.SigMaterial(sigs, "cpu")
+    assert all(rp.verify_range_proof_single_reference(rpl.to("cpu"), p, cpu_sm, P) for p in (0, 3))
+    rpl.A[7, 5] ^= 1
+    assert not rp.verify_range_proof_list(rpl, sm, P, 1.0, gpu_device)
