@@ -65,13 +65,12 @@ def survey_run(a):
     ids = [n["Address"] for n in nodes]
     pubs = {n["Address"]: O.g1_from_bytes(bytes.fromhex(n["PublicKey"])) for n in nodes}
     cn, dps = ids[0], ids[1:]
-    roles = {"cn": [cn], "dp": dps, "vn": [cn]}
     roster = Roster([ServerIdentity(f"cn:{cn}", pubs[cn], cn, 0)])
     id_to_pub = {f"cn:{cn}": pubs[cn], f"vn:{cn}": pubs[cn]}
     id_to_pub.update({f"dp:{d}": pubs[d] for d in dps})
     s2dp = {f"cn:{cn}": [ServerIdentity(f"dp:{d}", pubs[d], d, i + 1) for i, d in enumerate(dps)]}
     op = choose_operation(cfg["Survey"]["Operation"], 0, 256, 5, 0)
-    client = DrynxClient(RemoteNode(entry, roles, [cn] + dps))
+    client = DrynxClient(RemoteNode(entry))  # the roster travels inside the SurveyQuery
     sq = client.generate_survey_query(roster, None, s2dp, id_to_pub, cfg["Survey"].get("Name"), op, None, None, 0,
                                       False, [0.0] * 5, QueryDiffP(), QueryDPDataGen([3, 2, 1], 10, 0, 256))
     groups, values, _ = client.send_survey_query(sq)

@@ -21,6 +21,10 @@ def main(argv=None):
     r = sub.add_parser("run", help="read the node config on stdin and serve")
     r.add_argument("--workdir", default=None)
     r.add_argument("--device", default=None)
+    r.add_argument("--group", default=None,
+                   help="group file: a TOML network config ([[Network.Nodes]] Address/PublicKey) listing the nodes "
+                        "this node may form a cluster with")
+    r.add_argument("--trust-any", action="store_true", help="accept a join from any root (local experiments)")
     a = ap.parse_args(argv)
     from ..services import server as srv
 
@@ -29,6 +33,11 @@ def main(argv=None):
         sys.stdout.write(toml_io.dumps({"Server": cfg}))
         return 0
     cfg = toml_io.loads(sys.stdin.read())["Server"]
+    if a.group:
+        with open(a.group) as f:
+            group = toml_io.loads(f.read())
+        cfg["Trusted"] = [n["PublicKey"] for n in group.get("Network", {}).get("Nodes", [])]
+    cfg["TrustAny"] = bool(a.trust_any)
     srv.NodeServer(cfg, a.workdir, a.device).serve_forever()
     return 0
 

@@ -126,6 +126,10 @@ def schnorr_verify(public, msg: bytes, sig: bytes) -> bool:
     except ValueError:
         return False
     s = int.from_bytes(sig[64:], "big")
+    # same acceptance rule as schnorr_verify_batch: R at infinity or a
+    # non-canonical s is rejected, whatever the size of the VN's inbox
+    if R is None or s >= O.R:
+        return False
     e = int.from_bytes(hashlib.sha256(sig[:64] + O.g1_to_bytes(public) + msg).digest(), "big") % O.R
     lhs = bn.g1_mul_point(s)
     return lhs == O.g1_add(R, bn.g1_mul_point(e, public))
@@ -146,12 +150,13 @@ def schnorr_verify_batch(items: list, device="cpu") -> list:
             Ri = O.g1_from_bytes(sig[:64])
         except ValueError:
             continue
-        if Ri is None:
+        si = int.from_bytes(sig[64:], "big")
+        if Ri is None or si >= O.R:
             continue
         idx.append(i)
         R.append(Ri)
         X.append(public)
-        s.append(int.from_bytes(sig[64:], "big") % O.R)
+        s.append(si)
         e.append(int.from_bytes(hashlib.sha256(sig[:64] + O.g1_to_bytes(public) + msg).digest(), "big") % O.R)
     if not idx:
         return out

@@ -203,4 +203,5 @@ def proof_collection(ctx, sq, local_requests: list):
             st.update_async("mapping", sq.SurveyID, block.Hash.encode())
     ctx.last_block = block
     timers.end_timer(t)
+    ctx.end_verification(sq.SurveyID, block)  # EndVerificationChannel <- block (service_skipchain.go:158)
     return block

@@ -90,8 +90,17 @@ class DrynxClient:
         return enc.decode(cv, self.keypair.secret, op, self.table)
 
     # ------------------------------------------------------------------ VN / skipchain calls
-    def send_end_verification(self, vn_id: str, survey_id: str):
-        return self.entry.get_block(vn_id, survey_id)
+    def send_survey_query_to_vns(self, sq: SurveyQuery):
+        """SendSurveyQueryToVNs (api_skipchain.go:16): announce the survey to the
+        VNs before running it (expected proof counts, ledger, chain)."""
+        return self.entry.register_vn_survey(sq)
+
+    def send_end_verification(self, vn_id: str, survey_id: str, timeout: float | None = 3600.0):
+        """SendEndVerification (api_skipchain.go:30): blocks until the VNs have
+        verified every proof of the survey and the root VN appended its block
+        (EndVerificationChannel, service_skipchain.go:158-166); returns it, or
+        None on timeout.  Callable before or while the survey runs."""
+        return self.entry.wait_end_verification(survey_id, timeout)
 
     def send_get_latest_block(self, vn_id: str):
         return self.entry.get_latest_block(vn_id)

@@ -77,6 +77,39 @@ class DrynxNode:
         self.last_block: SkipBlock | None = None
         self.surveys: dict = {}
         self.fault_plan = FaultPlan.from_env()  # misbehaving parties (tests / simulations)
+        # VN side of the API (service_skipchain.go:31-166): surveys announced to
+        # the VNs (SurveyQueryToVN) and the EndVerificationChannel per survey
+        self.vn_surveys: dict = {}
+        self._end_cv = __import__("threading").Condition()
+        self._end_blocks: dict = {}
+
+    # ------------------------------------------------------------------ VN API
+    def register_vn_survey(self, sq: SurveyQuery):
+        """HandleSurveyQueryToVN: the VNs learn the survey (expected proof
+        counts, DB, chain) before any proof arrives.  A survey that reaches the
+        VNs without this call is registered implicitly when it runs."""
+        from ..protocols.proof_collection import expected_counts
+
+        with self._end_cv:
+            self.vn_surveys[sq.SurveyID] = {"sq": sq, "expected": expected_counts(sq)}
+            if len(self.vn_surveys) > 256:
+                self.vn_surveys.pop(next(iter(self.vn_surveys)))
+
+    def end_verification(self, survey_id: str, block: SkipBlock):
+        """The root VN appended the survey's block: release the waiters."""
+        with self._end_cv:
+            self._end_blocks[survey_id] = block
+            if len(self._end_blocks) > 256:
+                self._end_blocks.pop(next(iter(self._end_blocks)))
+            self._end_cv.notify_all()
+
+    def wait_end_verification(self, survey_id: str, timeout: float | None = None) -> SkipBlock | None:
+        """SendEndVerification (api_skipchain.go:30, service_skipchain.go:166):
+        block until every VN finished the survey's proofs and the block is
+        appended; None on timeout."""
+        with self._end_cv:
+            self._end_cv.wait_for(lambda: survey_id in self._end_blocks, timeout)
+            return self._end_blocks.get(survey_id)
 
     # ------------------------------------------------------------------ VN storage
     def store(self, vn_id: str) -> Store:
@@ -97,6 +130,8 @@ class DrynxNode:
         lands in ``SurveyResult.client_out``."""
         sq = self._broadcast_query(sq)
         self.surveys[sq.SurveyID] = sq
+        if sq.Query.Proofs and sq.Query.RosterVNs is not None and sq.SurveyID not in self.vn_surveys:
+            self.register_vn_survey(sq)
         if self.rank == 0 and not check_parameters(sq, add_diff_p(sq.Query.DiffP)):
             log.warning("query parameters failed CheckParameters; continuing as the reference does")
         proofs: list = []

@@ -66,19 +66,36 @@ SURVEY_QUERY = (("SurveyID", "string"), ("RosterServers", ("msg", ROSTER)), ("Cl
                 ("VerificationSharding", "sint"))
 SURVEY_QUERY_TO_VN = (("SQ", ("msg", SURVEY_QUERY)),)
 SURVEY_QUERY_TO_DP = (("SQ", ("msg", SURVEY_QUERY)), ("Root", ("msg", SERVER_IDENTITY)))
-END_VERIFICATION_REQUEST = (("QueryInfoID", "string"),)
+# VN requests: the reference sends them to the VN's own server; here one entry
+# node hosts many logical VNs, so the VN id is an appended extension field
+END_VERIFICATION_REQUEST = (("QueryInfoID", "string"), ("VN", "string"), ("Timeout", "double"))
 CIPHERTEXT = (("K", "point"), ("C", "point"))
 CIPHERVECTOR = (("Slice", ("rep", ("msg", CIPHERTEXT))),)
-RESPONSE_DP = (("Data", ("map", "string", ("ptrslice", ("msg", CIPHERTEXT)))),)
+RESPONSE_DP = (("Data", ("map", "string", ("ptrslice", ("msg", CIPHERTEXT)))),
+               # drynx_amd extensions: survey id, the VN block of the survey (Reply.Latest encoding)
+               ("SurveyID", "string"), ("Block", "bytes"))
 RESPONSE_DP_BYTES = (("Data", ("map", "string", "bytes")), ("Len", "sint"))
 DATA_BLOCK = (("Roster", ("msg", ROSTER)), ("SurveyID", "string"), ("Sample", "double"), ("Time", "time"),
               ("ServerNumber", "sint"), ("Proofs", ("map", "string", "sint")))
 BITMAP = (("BitMap", ("map", "string", "sint")),)
-GET_PROOFS = (("ID", "string"),)
+GET_PROOFS = (("ID", "string"), ("VN", "string"))
 PROOFS_AS_MAP = (("Proofs", ("map", "string", "bytes")),)
-CLOSE_DB = (("Close", "sint"),)
-GET_GENESIS = ()
-GET_BLOCK = (("Roster", ("msg", ROSTER)), ("ID", "string"))
+CLOSE_DB = (("Close", "sint"), ("VN", "string"))
+GET_GENESIS = (("VN", "string"),)
+GET_BLOCK = (("Roster", ("msg", ROSTER)), ("ID", "string"), ("VN", "string"))
+GET_LATEST_BLOCK = (("Roster", ("msg", ROSTER)), ("Sb", "bytes"), ("VN", "string"))
+# Reply{Latest *skipchain.SkipBlock}: Latest carries this framework's block
+# encoding (drynx_amd/ledger/skipchain.py), not cothority's SkipBlock
+REPLY = (("Latest", "bytes"),)
+# control plane of the node servers (drynx_amd-specific)
+PING = ()
+PING_REPLY = (("Address", "string"), ("Public", "point"))
+JOIN = (("World", "sint"), ("Rank", "sint"), ("Master", "string"), ("Backend", "string"), ("Addrs", ("rep", "string")),
+        ("Publics", ("rep", "point")), ("Root", "string"), ("Nonce", "bytes"), ("Signature", "bytes"))
+JOIN_REPLY = (("Signature", "bytes"),)
+ACK = (("OK", "bool"),)
+ERROR = (("Message", "string"),)
+SHUTDOWN = ()
 
 MESSAGES = {
     "libdrynx.SurveyQuery": SURVEY_QUERY,
@@ -94,6 +111,15 @@ MESSAGES = {
     "libdrynx.CloseDB": CLOSE_DB,
     "libdrynx.GetGenesis": GET_GENESIS,
     "libdrynx.GetBlock": GET_BLOCK,
+    "libdrynx.GetLatestBlock": GET_LATEST_BLOCK,
+    "libdrynx.Reply": REPLY,
+    "drynx_amd.Ping": PING,
+    "drynx_amd.PingReply": PING_REPLY,
+    "drynx_amd.Join": JOIN,
+    "drynx_amd.JoinReply": JOIN_REPLY,
+    "drynx_amd.Ack": ACK,
+    "drynx_amd.Error": ERROR,
+    "drynx_amd.Shutdown": SHUTDOWN,
     "libdrynx.PublishSignatureBytes": PUBLISH_SIGNATURE_BYTES,
     "libdrynx.Query": QUERY,
     "libunlynx.CipherText": CIPHERTEXT,

@@ -30,11 +30,16 @@ def test_three_servers_mean_survey(tmp_path):
     addrs = [f"127.0.0.1:{_port()}" for _ in range(3)]
     procs, cfgs = [], []
     try:
-        for i, a in enumerate(addrs):
-            cfg = _run(["drynx_amd.cli.server", "gen", a])
-            cfgs.append(cfg)
+        cfgs = [_run(["drynx_amd.cli.server", "gen", a]) for a in addrs]
+        pubs = [[ln.split('"')[1] for ln in cfg.splitlines() if ln.startswith("Public")][0] for cfg in cfgs]
+        group = _run(["drynx_amd.cli.client", "network", "new"])
+        for a, pub in zip(addrs, pubs):
+            group = _run(["drynx_amd.cli.client", "network", "add-node", a, pub], group)
+        (tmp_path / "group.toml").write_text(group)  # each node's group file: the roster it may join
+        for i, cfg in enumerate(cfgs):
             p = subprocess.Popen(PY + ["drynx_amd.cli.server", "run", "--workdir", str(tmp_path / f"n{i}"),
-                                       "--device", "cpu"], stdin=subprocess.PIPE, stdout=subprocess.PIPE,
+                                       "--device", "cpu", "--group", str(tmp_path / "group.toml")],
+                                 stdin=subprocess.PIPE, stdout=subprocess.PIPE,
                                  stderr=subprocess.PIPE, text=True, cwd=ROOT,
                                  env=dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES=""))
             p.stdin.write(cfg)
@@ -50,8 +55,7 @@ def test_three_servers_mean_survey(tmp_path):
                 except OSError:
                     time.sleep(0.2)
         net = _run(["drynx_amd.cli.client", "network", "new"])
-        for a, cfg in zip(addrs, cfgs):
-            pub = [ln.split('"')[1] for ln in cfg.splitlines() if ln.startswith("Public")][0]
+        for a, pub in zip(addrs, pubs):
             net = _run(["drynx_amd.cli.client", "network", "add-node", a, pub], net)
         net = _run(["drynx_amd.cli.client", "network", "set-client", addrs[0]], net)
         assert net.count("127.0.0.1:") == 4  # client_network-new: 3 nodes + client
@@ -61,12 +65,9 @@ def test_three_servers_mean_survey(tmp_path):
         val = float(out.strip().split()[0])
         assert 0.0 <= val <= 256.0
     finally:
-        from drynx_amd.services.server import request
+        from drynx_amd.services.server import RemoteNode
 
-        try:
-            request(addrs[0], {"cmd": "shutdown"}, timeout=30)
-        except Exception:
-            pass
+        RemoteNode(addrs[0]).shutdown()
         for p in procs:
             try:
                 p.wait(timeout=30)

@@ -181,6 +181,14 @@ def test_schnorr_verify_batch_matches_single():
     items.append((None, b"digest 0", good_sig))                          # unknown sender
     items.append((pubs[0], b"digest 0", good_sig[:90]))                  # truncated
     items.append((pubs[0], b"digest 0", b"\x01" * 64 + good_sig[64:]))  # R off the curve
+    # R at infinity, which the key holder can produce (s B = e X): rejected by both paths
+    import hashlib
+
+    e = int.from_bytes(hashlib.sha256(bytes(64) + O.g1_to_bytes(pubs[0]) + b"inf").digest(), "big") % O.R
+    items.append((pubs[0], b"inf", bytes(64) + O.scalar_to_bytes(e * keys[0] % O.R)))
+    # a non-canonical s (s + r: the same group element)
+    s0 = int.from_bytes(good_sig[64:], "big")
+    items.append((pubs[0], b"digest 0", good_sig[:64] + (s0 + O.R).to_bytes(32, "big")))
     want = [sigma.schnorr_verify(p, m, s) for p, m, s in items]
-    assert want == [True] * 5 + [False] * 6
+    assert want == [True] * 5 + [False] * 8
     assert sigma.schnorr_verify_batch(items) == want
