@@ -159,6 +159,34 @@ int dx_g1_on_curve(int on_gpu, void *stream, const uint32_t *aff, uint8_t *out, 
   return run(on_gpu, stream, n, op, false, "g1_on_curve");
 }
 
+// Decoding checks of raw-limb payloads (RangeProofList.unpack): every 8-limb
+// row below its modulus (Fp for coordinates in Montgomery form, Fr for
+// scalars), and Jacobian G1 points on the curve (Y^2 = X^3 + b Z^6; Z = 0 is
+// the point at infinity).
+int dx_limbs_canonical(int on_gpu, void *stream, const uint32_t *x, int fr, uint8_t *out, int64_t n) {
+  auto op = [=] __host__ __device__(int64_t i) {
+    const uint32_t *v = x + 8 * i;
+    const uint32_t *m = fr ? FrParams::MOD : FpParams::MOD;
+    uint32_t br = 0;
+    for (int k = 0; k < 8; k++) (void)subb32(v[k], m[k], br);
+    out[i] = br ? 1 : 0;  // borrow: v < m
+  };
+  return run(on_gpu, stream, n, op, false, "limbs_canonical");
+}
+
+int dx_g1j_on_curve(int on_gpu, void *stream, const uint32_t *jac, uint8_t *out, int64_t n) {
+  auto op = [=] __host__ __device__(int64_t i) {
+    const G1J p = at<G1J>(jac, i);
+    if (p.is_inf()) {
+      out[i] = 1;
+      return;
+    }
+    const Fp z2 = fsqr(p.z), z6 = fmul(fsqr(z2), z2);
+    out[i] = fsqr(p.y) == fadd(fmul(fsqr(p.x), p.x), fmul(Fp::from_limbs(Curve::B1), z6)) ? 1 : 0;
+  };
+  return run(on_gpu, stream, n, op, false, "g1j_on_curve");
+}
+
 // Partial sums over axis 0 of in[n_items][n_groups] (Jacobian):
 // out[c][g] = sum_{i in chunk c} in[i][g], chunk = `chunk` items.
 int dx_g1_sum_chunks(int on_gpu, void *stream, const uint32_t *in, uint32_t *out, int64_t n_items, int64_t n_groups,

@@ -84,6 +84,28 @@ int dx_g2_mul(int on_gpu, void *stream, const uint32_t *pts_aff, const uint32_t 
   return run(on_gpu, stream, n, op, true, "g2_mul");
 }
 
+// G2 membership of a twist point (range-proof V_ij, strict mode): on the curve
+// and psi(Q) == [6u^2] Q (psi = untwist-Frobenius-twist, eigenvalue p = 6u^2
+// mod r on G2; the cofactor 2p - r has small factors, e.g. 10069, so points
+// outside G2 are rejected one by one, not in a random combination).
+int dx_g2_subgroup(int on_gpu, void *stream, const uint32_t *aff, uint8_t *out, int64_t n) {
+  auto op = [=] __host__ __device__(int64_t i) {
+    const G2A q = at<G2A>(aff, i);
+    if (!on_curve(q)) {
+      out[i] = 0;
+      return;
+    }
+    if (q.is_inf()) {
+      out[i] = 1;
+      return;
+    }
+    const G2J psi = {mul(conj(q.x), Fp2::from_limbs(Frob::TWX1)), mul(conj(q.y), Fp2::from_limbs(Frob::TWY1)),
+                     Fp2::one()};
+    out[i] = jeq(psi, scalar_mul(G2J::from_aff(q), SIX_U2)) ? 1 : 0;
+  };
+  return run(on_gpu, stream, n, op, true, "g2_subgroup");
+}
+
 int dx_g2_on_curve(int on_gpu, void *stream, const uint32_t *aff, uint8_t *out, int64_t n) {
   auto op = [=] __host__ __device__(int64_t i) { out[i] = on_curve(at<G2A>(aff, i)) ? 1 : 0; };
   return run(on_gpu, stream, n, op, false, "g2_on_curve");

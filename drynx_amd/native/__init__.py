@@ -101,6 +101,10 @@ _SIGS = {
     "dx_g2_fb4_mul": [_I, _P, _P, _P, _P, _P, _L],
     "dx_gt_fb4_table": [_I, _P, _P, _P, _P, _L],
     "dx_gt_fb4_pow": [_I, _P, _P, _P, _P, _P, _L],
+    "dx_gt_cyclotomic": [_I, _P, _P, _P, _L],
+    "dx_g2_subgroup": [_I, _P, _P, _P, _L],
+    "dx_limbs_canonical": [_I, _P, _P, _I, _P, _L],
+    "dx_g1j_on_curve": [_I, _P, _P, _P, _L],
     "dx_fold_steps_ni": [],
     "dx_rp_lines_ni": [_P, _P, _P, _P, _L],
     "dx_rp_accum_ni": [_P, _P, _P, _L, _I],
@@ -338,6 +342,41 @@ def g1_on_curve(aff: torch.Tensor) -> torch.Tensor:
     out = torch.empty((n,), dtype=torch.uint8, device=aff.device)
     g, s = _ctx(aff)
     _call("dx_g1_on_curve", g, s, _ptr(aff), _ptr(out), n)
+    return out
+
+
+def limbs_canonical(x: torch.Tensor, fr: bool = False) -> torch.Tensor:
+    """uint8 per 8-limb row: row < p (Fp, Montgomery coordinates) or < r (Fr)."""
+    n = _rows(x, 8)
+    out = torch.empty((n,), dtype=torch.uint8, device=x.device)
+    g, s = _ctx(x)
+    _call("dx_limbs_canonical", g, s, _ptr(x.contiguous()), int(fr), _ptr(out), n)
+    return out
+
+
+def g1j_on_curve(jac: torch.Tensor) -> torch.Tensor:
+    n = _rows(jac, 24)
+    out = torch.empty((n,), dtype=torch.uint8, device=jac.device)
+    g, s = _ctx(jac)
+    _call("dx_g1j_on_curve", g, s, _ptr(jac.contiguous()), _ptr(out), n)
+    return out
+
+
+def g2_subgroup(aff: torch.Tensor) -> torch.Tensor:
+    """uint8 per affine twist point: on the curve and in G2 (psi(Q) == [6u^2] Q)."""
+    n = _rows(aff, 32)
+    out = torch.empty((n,), dtype=torch.uint8, device=aff.device)
+    g, s = _ctx(aff)
+    _call("dx_g2_subgroup", g, s, _ptr(aff.contiguous()), _ptr(out), n)
+    return out
+
+
+def gt_cyclotomic(a: torch.Tensor) -> torch.Tensor:
+    """uint8 per Fp12: non-zero and in the cyclotomic subgroup (x^(p^4) x == x^(p^2))."""
+    n = _rows(a, 96)
+    out = torch.empty((n,), dtype=torch.uint8, device=a.device)
+    g, s = _ctx(a)
+    _call("dx_gt_cyclotomic", g, s, _ptr(a.contiguous()), _ptr(out), n)
     return out
 
 
@@ -825,7 +864,7 @@ def _bucket_plan(k: torch.Tensor, W: int, group: torch.Tensor | None = None, n_g
     sc[:, 0] = torch.from_numpy((bk % 256).astype("int32"))
     slot = torch.from_numpy((bk % 256) * W + bk // 256)
     return {"item": item, "passes": passes, "bk": bk, "single": not passes,
-            "digit_sc": sc.to(dev), "slot": slot.to(dev)}
+            "digit_sc": sc.to(dev), "slot": slot.to(dev), "W": W}
 
 
 def _multi_exp64_run(a: torch.Tensor, plan) -> torch.Tensor:
@@ -840,12 +879,13 @@ def _multi_exp64_run(a: torch.Tensor, plan) -> torch.Tensor:
     for k, (st, ln) in enumerate(plan["passes"]):
         cur = gt_slice_prod(a if k == 0 else cur, plan["item"] if k == 0 else None, st, ln)
     bkp = gt_pow(cur, plan["digit_sc"])
-    win = gt_one(dev).repeat(256 * _ME_W, 1)
+    W = plan.get("W", _ME_W)
+    win = gt_one(dev).repeat(256 * W, 1)
     win[plan["slot"]] = bkp
-    win = _gt_prod_level(win.view(256, _ME_W, 96), 8) if dev.type == "cuda" else win.view(256, _ME_W, 96)
+    win = _gt_prod_level(win.view(256, W, 96), 8) if dev.type == "cuda" else win.view(256, W, 96)
     S_w = gt_prod(win.cpu(), chunk=4)                                  # [W, 96] on the host
-    acc = S_w[_ME_W - 1: _ME_W].contiguous()
-    for w in range(_ME_W - 2, -1, -1):
+    acc = S_w[W - 1: W].contiguous()
+    for w in range(W - 2, -1, -1):
         acc = gt_pow(acc, _pow2_scalar(_ME_C))
         acc = gt_mul(acc, S_w[w: w + 1].contiguous())
     return acc

@@ -447,9 +447,10 @@ def _challenge_hash(C_aff_bytes: np.ndarray, ysum_bytes: list) -> list:
 
 
 # ----------------------------------------------------------------------------- prove
-def create_range_proofs(batch, sigmat: SigMaterial, P_point, device=None) -> list:
+def create_range_proofs(batch, sigmat: SigMaterial, P_point, device=None, mode: int = 0) -> list:
     """Batched CreatePredicateRangeProofForAllServ over a CreateProofBatch.
-    Returns a list of RangeProofList (one per distinct (u, l))."""
+    Returns a list of RangeProofList (one per distinct (u, l)).  ``mode`` 2
+    produces the v2 transcript (``SurveyQuery.RangeProofMode``)."""
     device = torch.device(device or batch.cv.device)
     groups: dict = {}
     for idx in range(len(batch)):
@@ -462,11 +463,44 @@ def create_range_proofs(batch, sigmat: SigMaterial, P_point, device=None) -> lis
         offs = [batch.offset[i] if batch.offset else 0 for i in idxs]
         cols = [batch.sig_col[i] for i in idxs]
         r = batch.r[sel].contiguous()
-        out.append(_prove_group(u, l, vals, offs, cols, r, cv.to(device), sigmat, P_point, device))
+        out.append(_prove_group(u, l, vals, offs, cols, r, cv.to(device), sigmat, P_point, device, mode))
     return out
 
 
-def _prove_group(u, l, vals, offs, cols, r, cv, sigmat, P_point, device) -> RangeProofList:
+def challenges(C_jac, cols, sigmat: SigMaterial, device, mode: int = 0, D=None, V=None, A=None, S: int = 1,
+               l: int = 1) -> torch.Tensor:
+    """Fiat-Shamir challenges [n, 8] of a proof list.
+    mode < 2: c = SHA3-512(B || C || sum_i y_i) mod r (range_proof.go:350-374),
+              on the device (Keccak kernel);
+    mode 2  : the v2 transcript, which also binds the commitments:
+              c = SHA3-512(B || C || sum_i y_i || D || H(V_p) || H(a_p)) mod r,
+              H = SHA-256 over the proof's raw V / a limbs (computed in HBM)."""
+    bw, yw = sigmat.challenge_words(device)
+    cols_t = torch.tensor(cols, dtype=torch.int32, device=device)
+    C_aff = nt.g1_to_affine(C_jac.contiguous())
+    if mode < 2:
+        return nt.rp_challenges(C_aff, bw, yw, cols_t)
+    n = C_jac.shape[0]
+    hV = nt.sha256_chunks(V.contiguous(), S * l * 128).cpu().numpy().view(np.uint32).astype(">u4").reshape(n, 8)
+    hA = nt.sha256_chunks(A.contiguous(), S * l * 384).cpu().numpy().view(np.uint32).astype(">u4").reshape(n, 8)
+    Cb = bn.g1_aff_to_bytes(C_aff)
+    Db = bn.g1_aff_to_bytes(nt.g1_to_affine(D.contiguous()))
+    Bb = O.g1_to_bytes(O.G1_GEN)
+    out = []
+    for p in range(n):
+        h = hashlib.sha3_512()
+        h.update(b"drynx_amd/range/v2")
+        h.update(Bb)
+        h.update(Cb[p].tobytes())
+        h.update(sigmat.Ysum_bytes[cols[p]])
+        h.update(Db[p].tobytes())
+        h.update(hV[p].tobytes())
+        h.update(hA[p].tobytes())
+        out.append(int.from_bytes(h.digest(), "big") % O.R)
+    return bn.scalars_tensor(out, device)
+
+
+def _prove_group(u, l, vals, offs, cols, r, cv, sigmat, P_point, device, mode=0) -> RangeProofList:
     n = len(vals)
     S = sigmat.S
     rpl = RangeProofList(u, l, S, offs, cols, cv)
@@ -478,27 +512,18 @@ def _prove_group(u, l, vals, offs, cols, r, cv, sigmat, P_point, device) -> Rang
     # digits of m + offset
     with timers.span("rp.prove.digits"):
         phi = _digits(vals, offs, u, l)
-    # Fiat–Shamir challenge per value
-    with timers.span("rp.prove.challenge"):
-        bw, yw = sigmat.challenge_words(device)
-        c = nt.rp_challenges(nt.g1_to_affine(cv.C), bw, yw, torch.tensor(cols, dtype=torch.int32, device=device))
     # randomness
     with timers.span("rp.prove.random"):
         s = bn.random_scalars(n * l, device)
         t = bn.random_scalars(n * l, device)
         m = bn.random_scalars(n * l, device)
         v = bn.random_scalars(n * S * l, device)
+    # commitments (independent of the challenge):
     # D = (sum_j u^j s_j) B + (sum_j m_j) P
     us = nt.fr_dot_rows(s, _powers(u, l, device), n, b_periodic=True)
     msum = nt.fr_dot_rows(m, None, n)
     D = nt.g1_add(nt.g1_fb_mul(tabB, us), nt.g1_fb_mul(tabP, msum))
-    # Zphi_j = s_j - c phi_j ; Zr = sum m - c r ; Zv_ij = t_j - c v_ij
-    phi_sc = _small_scalars(phi.reshape(-1), device)
-    zphi = nt.fr_arith(nt.FR_SUB, s, nt.fr_arith(nt.FR_MUL, _rep(c, l), phi_sc))
-    zr = nt.fr_arith(nt.FR_SUB, msum, nt.fr_arith(nt.FR_MUL, c, r))
-    t_rep = t.view(n, 1, l, 8).expand(n, S, l, 8).reshape(-1, 8).contiguous()
-    zv = nt.fr_arith(nt.FR_SUB, t_rep, nt.fr_arith(nt.FR_MUL, _rep(c, S * l), v))
-    # V_ij = v_ij * A_{i, col, phi_j}
+    # V_ij = v_ij * A_{i, col, phi_j};  a_ij = e(-s_j B, V_ij) e(t_j B, B2)
     cols_t = torch.tensor(cols, dtype=torch.long, device=device)
     i_idx = torch.arange(S, device=device)
     phi_t = torch.from_numpy(phi).to(device)
@@ -508,7 +533,7 @@ def _prove_group(u, l, vals, offs, cols, r, cv, sigmat, P_point, device) -> Rang
     uniq, inv = torch.unique(a_index, return_inverse=True)
     tabs = sigmat.prover_tables(uniq, device)
     if tabs is not None:
-        # table-driven prover: V = v * A_phi (G2 comb), a = e(B,A_phi)^{-s v} * gT^t (GT combs) —
+        # table-driven prover: V = v * A_phi (G2 comb), a = e(B,A_phi)^{-s v} * gT^t (GT combs) --
         # no pairing and no final exponentiation per (value, server, digit)
         g2_tabs, gphi_tabs, slot, wbits = tabs
         tidx = slot.index_select(0, inv).to(torch.int32).contiguous()
@@ -522,24 +547,67 @@ def _prove_group(u, l, vals, offs, cols, r, cv, sigmat, P_point, device) -> Rang
         # a_ij = FE(ML(-s_j B, V_ij)) * gT^{t_j}
         negsB = nt.g1_to_affine(nt.g1_fb_mul(tabB, nt.fr_arith(nt.FR_NEG, s)))
         A = nt.rp_prove_a(negsB, V, t, gt_tab, S, l)
+    # Fiat-Shamir challenge per value
+    with timers.span("rp.prove.challenge"):
+        c = challenges(cv.C, cols, sigmat, device, mode, D, V, A, S, l)
+    # responses: Zphi_j = s_j - c phi_j ; Zr = sum m - c r ; Zv_ij = t_j - c v_ij
+    phi_sc = _small_scalars(phi.reshape(-1), device)
+    zphi = nt.fr_arith(nt.FR_SUB, s, nt.fr_arith(nt.FR_MUL, _rep(c, l), phi_sc))
+    zr = nt.fr_arith(nt.FR_SUB, msum, nt.fr_arith(nt.FR_MUL, c, r))
+    t_rep = t.view(n, 1, l, 8).expand(n, S, l, 8).reshape(-1, 8).contiguous()
+    zv = nt.fr_arith(nt.FR_SUB, t_rep, nt.fr_arith(nt.FR_MUL, _rep(c, S * l), v))
     rpl.challenge, rpl.zr, rpl.D, rpl.zphi, rpl.zv, rpl.V, rpl.A = c, zr, D, zphi, zv, V, A
     return rpl
 
 
 # ----------------------------------------------------------------------------- verify
-def _rand64(n, device) -> torch.Tensor:
-    """Random nonzero 64-bit batch weights from the ChaCha20 CSPRNG (device
-    or host path), unknown to the prover."""
+def _rand64(n, device, bits: int = 64) -> torch.Tensor:
+    """Uniform ``bits``-bit batch weights from the ChaCha20 CSPRNG (device or
+    host path), unknown to the prover."""
     r = bn.random_scalars(n, device)
-    r[:, 2:] = 0
-    r[:, 0] |= 1
+    words = bits // 32
+    r[:, words:] = 0
+    if bits % 32:
+        r[:, words] &= (1 << (bits % 32)) - 1
     return r
 
 
+_SIX_U2 = None
+
+
+def _gt_in_subgroup(g: torch.Tensor) -> bool:
+    """Host test that a cyclotomic element is in GT (order r): g^p == g^(6u^2)
+    (p = 6u^2 mod r for BN curves; Scott's membership test)."""
+    global _SIX_U2
+    if _SIX_U2 is None:
+        _SIX_U2 = (bn.scalars_tensor([O.P], "cpu"), bn.scalars_tensor([6 * O.U * O.U], "cpu"))
+    g = g.cpu().contiguous()
+    return bool(nt.gt_eq(nt.gt_pow(g, _SIX_U2[0]), nt.gt_pow(g, _SIX_U2[1])).all())
+
+
+def validate_list(r: RangeProofList, mode: int = 0) -> bool:
+    """Decoding checks of a (raw-limb or kyber-layout) proof list before any
+    arithmetic on it: every coordinate below p and every scalar below r; the
+    commitment (K, C) and D on G1; V on the twist (in G2 when ``mode`` >= 1);
+    every a_ij non-zero and in the cyclotomic subgroup.  The prime-order part
+    of a_ij is enforced by the batch equation plus one independent random
+    combination tested in GT (``verify_range_proof_list``)."""
+    fp = lambda t: nt.limbs_canonical(t.reshape(-1, 8))  # noqa: E731
+    fr = lambda t: nt.limbs_canonical(t.reshape(-1, 8), fr=True)  # noqa: E731
+    flags = [fp(r.commit.K), fp(r.commit.C), nt.g1j_on_curve(r.commit.K), nt.g1j_on_curve(r.commit.C)]
+    if r.has_rp and len(r):
+        flags += [fp(r.D), nt.g1j_on_curve(r.D), fr(r.challenge), fr(r.zr), fr(r.zphi), fr(r.zv), fp(r.V), fp(r.A),
+                  nt.g2_subgroup(r.V) if mode >= 1 else nt.g2_on_curve(r.V), nt.gt_cyclotomic(r.A)]
+    return bool(torch.stack([f.bool().all() for f in flags]).all())
+
+
 def verify_range_proof_list(rpl: RangeProofList, sigmat: SigMaterial, P_point, threshold: float = 1.0,
-                            device=None) -> bool:
+                            device=None, mode: int = 0) -> bool:
     """RangeProofListVerification: verifies the first ceil(threshold * n)
-    proofs of the list (reference sampling semantics) as ONE batch."""
+    proofs of the list (reference sampling semantics) as ONE batch.
+    ``mode`` (``SurveyQuery.RangeProofMode``): 0 trusts the proof's challenge
+    like range_proof.go:504-565; >= 1 recomputes it (v1 / v2 transcript) and
+    requires every V_ij in G2."""
     if not rpl.has_rp:
         return True
     n_all = len(rpl)
@@ -553,6 +621,14 @@ def verify_range_proof_list(rpl: RangeProofList, sigmat: SigMaterial, P_point, t
     if r.zphi.shape[0] != n * l or r.zv.shape[0] != n * S * l or r.V.shape[0] != n * S * l \
             or r.A.shape[0] != n * S * l:
         return False
+    with timers.span("rp.verify.validate"):
+        if not validate_list(r, mode):
+            return False
+    if mode >= 1:
+        with timers.span("rp.verify.challenge"):
+            c = challenges(r.commit.C, r.cols, sigmat, device, mode, r.D, r.V, r.A, S, l)
+            if not torch.equal(c, r.challenge):
+                return False
     tabB = bn.base_table(device)
     tabP = pk_table(P_point, device).tabP
     # --- D == c*C' + Zr*P + (sum_j Zphi_j u^j) B, C' = C + offset*B
@@ -657,6 +733,15 @@ def verify_range_proof_list(rpl: RangeProofList, sigmat: SigMaterial, P_point, t
         if not dcheck_finish(dcheck_launch()):
             return False
         F, G = nt.rp_verify_products(ZB, Y, rho, r.V, r.A, S, l)     # Miller product, prod a^rho
+    # prime-order part of the a_ij: an independent 40-bit combination in GT
+    # (the smallest prime factor of the cyclotomic cofactor is ~2^38.8, so a
+    # non-GT component survives the batch equation AND this test with
+    # probability ~2^-77)
+    with timers.span("rp.verify.gt_membership"):
+        gam = _rand64(n * S * l, device, 40)
+        Gm = nt._multi_exp64_run(r.A, nt._bucket_plan(gam, 5))
+        if not _gt_in_subgroup(Gm):
+            return False
     e = nt.fr_dot_rows(rho, r.zv, 1)                                 # sum rho Zv
     # the closing single-element work (one final exponentiation, one GT power)
     # is a serial Fp12 chain: it runs on the host, where one core beats one GPU lane

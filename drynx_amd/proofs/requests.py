@@ -269,7 +269,8 @@ def verify_content(req: ProofRequest, sq, device, cache: VerifierCache) -> bool:
                 continue
             if sigs is None or not _ranges_ok(sq, r):
                 return False
-            if not rp.verify_range_proof_list(r, cache.sigmat(sq, device), P, sq.RangeProofThreshold, device):
+            if not rp.verify_range_proof_list(r, cache.sigmat(sq, device), P, sq.RangeProofThreshold, device,
+                                              sq.RangeProofMode):
                 return False
         return True
     if req.kind == "aggregation":
@@ -347,7 +348,7 @@ def verify_range_many(reqs: list, idxs: list, sq, device, cache: VerifierCache, 
     try:
         with timers.span("rp.verify.cat"):
             cats = [rp.rpl_cat(g) for g in groups.values()]
-        ok = all(rp.verify_range_proof_list(c, sigmat, P, 1.0, device) for c in cats)
+        ok = all(rp.verify_range_proof_list(c, sigmat, P, 1.0, device, sq.RangeProofMode) for c in cats)
     except Exception as e:
         log.warning(f"batched range verification failed: {e}")
         ok = False
@@ -357,7 +358,7 @@ def verify_range_many(reqs: list, idxs: list, sq, device, cache: VerifierCache, 
         return out
     for i in live:  # attribute the failure
         try:
-            out[i] = all(rp.verify_range_proof_list(r, sigmat, P, 1.0, device) for r in parts[i])
+            out[i] = all(rp.verify_range_proof_list(r, sigmat, P, 1.0, device, sq.RangeProofMode) for r in parts[i])
         except Exception:
             out[i] = False
     return out

@@ -173,6 +173,12 @@ class SurveyQuery:
     # (deterministic sharding of the verification work across GPUs); 0 -> the
     # reference's random sampling with probability Threshold.
     VerificationSharding: int = 0
+    # extension: range-proof verification mode.  0 = the reference
+    # (RangeProofVerification trusts the proof's challenge, range_proof.go:
+    # 504-565); 1 = strict: the VN recomputes c = SHA3-512(B||C||sum y) and
+    # checks every V_ij in G2; 2 = strict with the v2 transcript, whose
+    # challenge also binds D and every V_ij, a_ij (range_proof.go:350-374 omits them).
+    RangeProofMode: int = 0
 
     # -------------------------------------------------------------- helpers
     def all_dps(self):
@@ -272,6 +278,7 @@ def _survey_from_dict(d: dict) -> SurveyQuery:
         RangeProofThreshold=d.get("RangeProofThreshold", 0.0),
         KeySwitchingProofThreshold=d.get("KeySwitchingProofThreshold", 0.0),
         VerificationSharding=d.get("VerificationSharding", 0),
+        RangeProofMode=d.get("RangeProofMode", 0),
     )
 
 

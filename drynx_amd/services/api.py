@@ -40,7 +40,7 @@ class DrynxClient:
                               id_to_public: dict, survey_id: str | None, operation: Operation, ranges, ps,
                               proofs: int, obfuscation: bool, thresholds, diffp: QueryDiffP | None = None,
                               dpdatagen: QueryDPDataGen | None = None, cutting_factor: int = 0,
-                              verification_sharding: int = 0) -> SurveyQuery:
+                              verification_sharding: int = 0, range_proof_mode: int = 0) -> SurveyQuery:
         """GenerateSurveyQuery; thresholds = [general, aggregation, range, obfuscation, keyswitch] (api.go:79-83)."""
         sq = SurveyQuery(
             SurveyID=survey_id or new_survey_id(),
@@ -58,6 +58,7 @@ class DrynxClient:
             Threshold=thresholds[0], AggregationProofThreshold=thresholds[1], RangeProofThreshold=thresholds[2],
             ObfuscationProofThreshold=thresholds[3], KeySwitchingProofThreshold=thresholds[4],
             VerificationSharding=verification_sharding,
+            RangeProofMode=range_proof_mode,
         )
         return sq
 

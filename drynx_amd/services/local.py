@@ -55,7 +55,7 @@ def make_signatures(cluster, ranges, device="cpu", deterministic=False):
 def make_survey(client: DrynxClient, cluster, op_name: str, *, query_min=0, query_max=10, d=1, rows=10,
                 group_by=(1,), proofs=0, ranges=None, obfuscation=False, thresholds=None, diffp=None,
                 cutting_factor=0, lr_params=None, survey_id=None, sig_device="cpu", deterministic_sigs=False,
-                verification_sharding=0, with_vns=None):
+                verification_sharding=0, with_vns=None, range_proof_mode=0):
     op = choose_operation(op_name, query_min, query_max, d, cutting_factor)
     if op_name == "logistic regression":
         op.LRParameters = lr_params
@@ -75,7 +75,7 @@ def make_survey(client: DrynxClient, cluster, op_name: str, *, query_min=0, quer
     return client.generate_survey_query(
         cluster.roster_cns(), cluster.roster_vns() if with_vns else None, cluster.server_to_dp(), id_to_public,
         survey_id, op, ranges, ps, proofs, obfuscation, thresholds, diffp or QueryDiffP(), gen, cutting_factor,
-        verification_sharding)
+        verification_sharding, range_proof_mode)
 
 
 def clear_expected(op_name, clear_dp: dict):

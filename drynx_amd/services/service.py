@@ -259,7 +259,7 @@ class DrynxNode:
             t0 = time.perf_counter()
             sigmat = self.verifier_cache.sigmat(sq, self.device)
             big = dcp_batch_cat(batches)
-            lists = rp.create_range_proofs(big, sigmat, P, self.device)  # one list per (u, l), items in order
+            lists = rp.create_range_proofs(big, sigmat, P, self.device, sq.RangeProofMode)  # one list per (u, l)
             # every DP's items of a given (u, l) are contiguous inside that list
             cursor = {}
             for dp_id, b in owners:

@@ -92,6 +92,7 @@ def survey_query_to_msg(sq: SurveyQuery) -> dict:
         "RangeProofThreshold": sq.RangeProofThreshold,
         "KeySwitchingProofThreshold": sq.KeySwitchingProofThreshold,
         "VerificationSharding": sq.VerificationSharding,
+        "RangeProofMode": sq.RangeProofMode,
     }
 
 
@@ -129,6 +130,7 @@ def survey_query_from_msg(d: dict) -> SurveyQuery:
         RangeProofThreshold=d["RangeProofThreshold"],
         KeySwitchingProofThreshold=d["KeySwitchingProofThreshold"],
         VerificationSharding=d["VerificationSharding"],
+        RangeProofMode=d["RangeProofMode"],
     )
 
 

@@ -63,7 +63,7 @@ SURVEY_QUERY = (("SurveyID", "string"), ("RosterServers", ("msg", ROSTER)), ("Cl
                 ("AggregationProofThreshold", "double"), ("ObfuscationProofThreshold", "double"),
                 ("RangeProofThreshold", "double"), ("KeySwitchingProofThreshold", "double"),
                 # drynx_amd extension (after the reference fields): per-proof VN sharding
-                ("VerificationSharding", "sint"))
+                ("VerificationSharding", "sint"), ("RangeProofMode", "sint"))
 SURVEY_QUERY_TO_VN = (("SQ", ("msg", SURVEY_QUERY)),)
 SURVEY_QUERY_TO_DP = (("SQ", ("msg", SURVEY_QUERY)), ("Root", ("msg", SERVER_IDENTITY)))
 # VN requests: the reference sends them to the VN's own server; here one entry

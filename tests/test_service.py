@@ -188,3 +188,33 @@ def test_fault_plan_marks_malicious_parties(tmp_path):
     assert by("/keyswitch/cn0/") == {prq.PROOF_TRUE}
     assert by("/aggregation/cn0/") == {prq.PROOF_FALSE}
     node.close(remove=True)
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+def test_strict_range_modes_end_to_end(env, mode):
+    """SurveyQuery.RangeProofMode: the DPs prove (v2 transcript for mode 2),
+    every VN recomputes the challenge and checks V in G2 -> all codes 1."""
+    cl, node, client = env
+    sq = make_survey(client, cl, "sum", query_min=0, query_max=9, rows=6, proofs=1, ranges=[16, 2],
+                     range_proof_mode=mode)
+    _, vals, res = client.send_survey_query(sq)
+    assert vals[0][0] == sum(v[0][0] for v in res.clear_dp.values())
+    assert set(res.block.data_block().Proofs.values()) == {prq.PROOF_TRUE}
+
+
+def test_vn_api_registration_and_blocking_end_verification(env):
+    """SendSurveyQueryToVNs then a SendEndVerification issued BEFORE the survey
+    runs: it blocks until the root VN appended the survey's block."""
+    import threading
+
+    cl, node, client = env
+    sq = make_survey(client, cl, "sum", query_min=0, query_max=9, rows=6, proofs=1, ranges=[16, 2])
+    client.send_survey_query_to_vns(sq)
+    assert sq.SurveyID in node.vn_surveys
+    got = {}
+    t = threading.Thread(target=lambda: got.setdefault("b", client.send_end_verification("vn0", sq.SurveyID, 120)))
+    t.start()
+    _, _, res = client.send_survey_query(sq)
+    t.join(120)
+    assert got["b"] is not None and got["b"].Hash == res.block.Hash
+    assert client.send_end_verification("vn0", "no-such-survey", 0.05) is None
