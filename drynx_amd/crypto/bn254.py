@@ -39,7 +39,18 @@ def limbs_to_ints(arr) -> list[int]:
 
 
 def to_tensor(a: np.ndarray, device) -> torch.Tensor:
-    return torch.from_numpy(np.ascontiguousarray(a).view(np.int32)).to(device)
+    return h2d(torch.from_numpy(np.ascontiguousarray(a).view(np.int32)), device)
+
+
+def h2d(t: torch.Tensor, device) -> torch.Tensor:
+    """Host tensor -> ``device``.  To a GPU through pinned memory and an
+    asynchronous copy: a pageable copy blocks the host until every kernel
+    already queued on the stream has finished, which stalls the launch
+    sequences of the prover and verifier threads."""
+    dev = torch.device(device)
+    if dev.type != "cuda":
+        return t
+    return t.pin_memory().to(dev, non_blocking=True)
 
 
 def to_numpy(t: torch.Tensor) -> np.ndarray:

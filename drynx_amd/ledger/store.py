@@ -29,6 +29,80 @@ from ..utils import timers
 
 BLOB_MIN = 1 << 16
 _REF = b"\x00DXBLOB1"
+_REF2 = b"\x00DXBLOB2"  # + offset, length (u64) + path of a shared BlobSegment
+
+
+class BlobRef:
+    """A value living in a rank-level BlobSegment (written once, referenced by
+    the stores of every VN hosted on the rank)."""
+
+    def __init__(self, segment: "BlobSegment", future):
+        self.segment, self.future = segment, future
+
+    def result(self):
+        return self.future.result()
+
+
+class BlobSegment:
+    """Append-only file of large ledger values shared by the VNs of one rank:
+    the same proof payload is written once, however many co-hosted VNs store
+    it.  Values are produced by a callable on the segment's own worker thread
+    (and, on a GPU, its own HIP stream: device-to-host copies never queue on
+    the compute streams)."""
+
+    def __init__(self, path: str, device=None):
+        import concurrent.futures as cf
+
+        self.path = path
+        os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+        self._f = open(path, "ab")
+        self._ex = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="drynx-ledger")
+        self._done: dict = {}
+        self._lock = threading.Lock()
+        self._device = device
+        self._stream = None
+
+    def put(self, blob_id: str, produce) -> BlobRef:
+        with self._lock:
+            fut = self._done.get(blob_id)
+            if fut is None:
+                fut = self._done[blob_id] = self._ex.submit(self._write, produce)
+                if len(self._done) > 4096:
+                    self._done.pop(next(iter(self._done)))
+        return BlobRef(self, fut)
+
+    def _write(self, produce):
+        import torch
+
+        dev = torch.device(self._device) if self._device is not None else None
+        if dev is not None and dev.type == "cuda":
+            if self._stream is None:
+                self._stream = torch.cuda.Stream(dev)
+            with torch.cuda.stream(self._stream), timers.span("ledger.encode"):
+                data = produce()
+        else:
+            with timers.span("ledger.encode"):
+                data = produce()
+        with timers.span("ledger.write"):
+            off = self._f.seek(0, os.SEEK_END)
+            self._f.write(data)
+            self._f.flush()
+        return off, len(data)
+
+    def flush(self):
+        with self._lock:
+            futs = list(self._done.values())
+        for f in futs:
+            f.result()
+
+    def close(self, remove: bool = False):
+        self._ex.shutdown(wait=True)
+        self._f.close()
+        if remove:
+            try:
+                os.remove(self.path)
+            except FileNotFoundError:
+                pass
 
 
 class Store:
@@ -51,6 +125,9 @@ class Store:
     def _encode(self, value) -> bytes:
         """Caller holds the lock.  Large values are written straight from the
         host buffer (no bytes() copy under the GIL)."""
+        if isinstance(value, BlobRef):
+            off, n = value.result()
+            return _REF2 + struct.pack("<QQ", off, n) + value.segment.path.encode()
         if hasattr(value, "cpu") and hasattr(value, "numpy"):
             buf = memoryview(value.detach().cpu().contiguous().numpy()).cast("B")
         else:
@@ -65,6 +142,11 @@ class Store:
 
     def _decode(self, v) -> bytes:
         v = bytes(v)
+        if v.startswith(_REF2):
+            off, n = struct.unpack("<QQ", v[len(_REF2): len(_REF2) + 16])
+            with open(v[len(_REF2) + 16:].decode(), "rb") as f:
+                f.seek(off)
+                return f.read(n)
         if len(v) == len(_REF) + 16 and v.startswith(_REF):
             off, n = struct.unpack("<QQ", v[len(_REF):])
             if self._blob_f is not None:

@@ -476,7 +476,7 @@ def challenges(C_jac, cols, sigmat: SigMaterial, device, mode: int = 0, D=None, 
               c = SHA3-512(B || C || sum_i y_i || D || H(V_p) || H(a_p)) mod r,
               H = SHA-256 over the proof's raw V / a limbs (computed in HBM)."""
     bw, yw = sigmat.challenge_words(device)
-    cols_t = torch.tensor(cols, dtype=torch.int32, device=device)
+    cols_t = bn.h2d(torch.tensor(cols, dtype=torch.int32), device)
     C_aff = nt.g1_to_affine(C_jac.contiguous())
     if mode < 2:
         return nt.rp_challenges(C_aff, bw, yw, cols_t)
@@ -524,9 +524,9 @@ def _prove_group(u, l, vals, offs, cols, r, cv, sigmat, P_point, device, mode=0)
     msum = nt.fr_dot_rows(m, None, n)
     D = nt.g1_add(nt.g1_fb_mul(tabB, us), nt.g1_fb_mul(tabP, msum))
     # V_ij = v_ij * A_{i, col, phi_j};  a_ij = e(-s_j B, V_ij) e(t_j B, B2)
-    cols_t = torch.tensor(cols, dtype=torch.long, device=device)
+    cols_t = bn.h2d(torch.tensor(cols, dtype=torch.long), device)
     i_idx = torch.arange(S, device=device)
-    phi_t = torch.from_numpy(phi).to(device)
+    phi_t = bn.h2d(torch.from_numpy(phi), device)
     a_index = ((i_idx.view(1, S, 1) * sigmat.n_cols + cols_t.view(n, 1, 1)) * max(1, sigmat.umax)
                + phi_t.view(n, 1, l)).reshape(-1)
     _, gt_tab = gt_generator_table(device)
@@ -610,170 +610,136 @@ def verify_range_proof_list(rpl: RangeProofList, sigmat: SigMaterial, P_point, t
     requires every V_ij in G2."""
     if not rpl.has_rp:
         return True
-    n_all = len(rpl)
-    k = int(math.ceil(threshold * n_all))
+    k = int(math.ceil(threshold * len(rpl)))
     if k == 0:
         return True
-    device = torch.device(device or rpl.commit.device)
-    r = rpl if k == n_all else _slice(rpl, k)
+    r = rpl if k == len(rpl) else _slice(rpl, k)
+    return verify_range_proof_list_multi(r, sigmat, P_point, 1, device, mode)[0]
+
+
+def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_point, n_vn: int = 1, device=None,
+                                  mode: int = 0) -> list:
+    """``n_vn`` independent batch verifications of one proof list -- one per
+    verifying node hosted on this rank, each with its own random weights.
+
+    Per VN v the l*S pairing equations of all n proofs are combined with
+    uniform 64-bit weights rho_v, and the n D-equations with w_v:
+      FE(prod_it ML(rho_it (Zphi_j B - c y_i), V_it)) * prod_it a_it^rho_it
+          == gT^(sum rho Zv)                                  (one final exp)
+      sum w (c C') + (sum w Zr) P + (sum w z) B == sum w D       (one MSM)
+    plus GT membership of an independent 40-bit combination of the a_it.
+    What does not depend on the weights -- decoding checks, the strict-mode
+    challenge and G2 checks, Zphi*B, c*y_i and their differences -- is
+    computed once for the co-hosted VNs.  On a GPU the VNs' Miller folds are
+    queued back to back (no host round trip between them) while the
+    bucket-method MSM / multi-exponentiations run on a side stream; the
+    closing single-element work (final exponentiations, Horner steps) runs
+    on the host, where one core beats one GPU lane.  -> [bool] per VN."""
+    if not r.has_rp or len(r) == 0:
+        return [True] * n_vn
+    device = torch.device(device or r.commit.device)
     r = r.to(device)
-    n, l, S, u = k, r.l, r.S, r.u
+    n, l, S, u = len(r), r.l, r.S, r.u
     if r.zphi.shape[0] != n * l or r.zv.shape[0] != n * S * l or r.V.shape[0] != n * S * l \
-            or r.A.shape[0] != n * S * l:
-        return False
+            or r.A.shape[0] != n * S * l or r.challenge.shape[0] != n:
+        return [False] * n_vn
     with timers.span("rp.verify.validate"):
         if not validate_list(r, mode):
-            return False
+            return [False] * n_vn
     if mode >= 1:
         with timers.span("rp.verify.challenge"):
-            c = challenges(r.commit.C, r.cols, sigmat, device, mode, r.D, r.V, r.A, S, l)
-            if not torch.equal(c, r.challenge):
-                return False
+            if not torch.equal(challenges(r.commit.C, r.cols, sigmat, device, mode, r.D, r.V, r.A, S, l),
+                               r.challenge):
+                return [False] * n_vn
     tabB = bn.base_table(device)
-    tabP = pk_table(P_point, device).tabP
-    # --- D == c*C' + Zr*P + (sum_j Zphi_j u^j) B, C' = C + offset*B
-    Cp = r.commit.C
+    # --- shared, weight-free inputs
+    Cp = r.commit.C                                                    # C' = C + offset*B
     if any(r.offset):
-        Cp = nt.g1_add(Cp, nt.g1_fb_mul_i64(tabB, torch.tensor(r.offset, dtype=torch.int64, device=device)))
+        Cp = nt.g1_add(Cp, nt.g1_fb_mul_i64(tabB, bn.h2d(torch.tensor(r.offset, dtype=torch.int64), device)))
     z = nt.fr_dot_rows(r.zphi, _powers(u, l, device), n, b_periodic=True)   # sum_j Zphi_j u^j
-    # all n D-equations as one random linear combination (weights w_p, 64 bit):
-    #   sum (w c) C' + (sum w Zr) P + (sum w z) B == sum w D
-    # -- one grouped Pippenger MSM (the D side keeps its 64-bit weights)
-    w = _rand64(n, device)
-    dpts = torch.cat([Cp.contiguous(), r.D.contiguous()])
-    dsc = torch.cat([nt.fr_arith(nt.FR_MUL, w, r.challenge), w])
-    dgrp = torch.cat([torch.zeros(n, dtype=torch.int32, device=device), torch.ones(n, dtype=torch.int32, device=device)])
-    dfull = torch.cat([nt.fr_dot_rows(w, r.zr, 1), nt.fr_dot_rows(w, z, 1)])
-
-    def dcheck_launch():
-        with timers.span("rp.verify.dcheck"):
-            return nt.g1_msm_launch(dpts, dsc, dgrp, 2, bits=256)
-
-    def dcheck_finish(h) -> bool:
-        with timers.span("rp.verify.dcheck_finish"):
-            return _dcheck_finish(h)
-
-    def _dcheck_finish(h) -> bool:
-        G = nt.g1_msm_finish(h)
-        PB = nt.g1_mul(bn.g1_jac_tensor([P_point, O.G1_GEN], "cpu"), dfull.cpu())
-        lhs = nt.g1_sum(torch.stack([G[0:1], PB[0:1], PB[1:2]]))
-        return bool(nt.g1_eq(lhs, G[1:2])[0])
-
-    # --- pairing equations, randomly combined
-    ZB = nt.g1_fb_mul(tabB, r.zphi)                                  # [n*l]
-    cols_t = torch.tensor(r.cols, dtype=torch.long, device=device)
+    ZB = nt.g1_fb_mul(tabB, r.zphi)                                    # [n*l]
+    cols_t = bn.h2d(torch.tensor(r.cols, dtype=torch.long), device)
     y_idx = (torch.arange(S, device=device).view(1, S) * sigmat.n_cols + cols_t.view(n, 1)).reshape(-1)
     ytabs = sigmat.y_tables(device)
-    if ytabs is not None:                                             # c * y_i as fixed-base mults
+    if ytabs is not None:                                              # c * y_i as fixed-base mults
         Y = nt.g1_fb_mul_idx(ytabs[0], ytabs[1].index_select(0, y_idx).contiguous(), _rep(r.challenge, S))
     else:
-        Ysel = sigmat.y_jac.to(device).index_select(0, y_idx).contiguous()
-        Y = nt.g1_mul(Ysel, _rep(r.challenge, S))                     # [n*S]
-    rho = _rand64(n * S * l, device)
-    if device.type == "cuda":
-        order = os.environ.get("DRYNX_FOLD_FIRST", "1")
-        if order == "last":
-            # everything that does not need the Miller values (D-equation MSM,
-            # GT multi-exponentiation) runs to completion first, while the GPU
-            # still has room; the fold is queued last, so nothing is starved
-            # behind it and only the final exponentiation follows it.  Measured
-            # on one MI355X: 64.7 / 67.9 ms per LR query vs 59.2 / 67.3 ms for
-            # the default "1" (noisy box), so it stays opt-in
-            if not dcheck_finish(dcheck_launch()):
-                return False
-            with timers.span("rp.verify.gt_plan"):
-                plan = nt._multi_exp64_plan(rho)
-            G = nt._multi_exp64_run(r.A, plan)
-            fb = _miller_fold(ZB, Y, rho, r.V, S, l)
-        elif order == "1":
-            # the Miller fold (the long pole, ~20 ms for a 2070-value list)
-            # is queued as soon as its inputs are; the D-equation MSM and the
-            # GT multi-exponentiation run on a side stream beside it, so their
-            # host steps overlap the fold instead of delaying its launch
-            cur, aux = torch.cuda.current_stream(device), _aux_stream(device)
-            aux.wait_stream(cur)
-            # DRYNX_FOLD_RESERVE_CUS=k runs the fold on a CU-masked stream that
-            # leaves k CUs to the short launches beside it (D-check MSM, GT
-            # multi-exp, key-switch checks).  Measured slower on MI355X
-            # (k=16: 62 -> 78-80 ms per query, k=32: 66 ms), so off by default
-            fs = nt.cu_masked_stream(device, int(os.environ.get("DRYNX_FOLD_RESERVE_CUS", "0")))
-            if fs is not None:
-                fs.wait_stream(cur)
-                with torch.cuda.stream(fs):
-                    fb = _miller_fold(ZB, Y, rho, r.V, S, l)
-            else:
-                fb = _miller_fold(ZB, Y, rho, r.V, S, l)         # Miller values, LDS-folded
-            with torch.cuda.stream(aux):
-                if not dcheck_finish(dcheck_launch()):
-                    return False
-                with timers.span("rp.verify.gt_plan"):
-                    plan = nt._multi_exp64_plan(rho)
-                G = nt._multi_exp64_run(r.A, plan)                     # prod a^rho (host tensor)
-            cur.wait_stream(aux)
-            if fs is not None:
-                cur.wait_stream(fs)
-        else:
-            # the D-equation MSM runs to completion before the Miller fold is
-            # queued: a kernel sharing the SIMDs with the fold's waves is starved
-            # (a 128-workgroup bucket pass took 18 ms beside it, <1 ms alone), and
-            # its host steps are short (64-bit weights on the D side).  The GT
-            # multi-exponentiation's bucket plan (one host sync) is built before
-            # the fold too; its passes queue behind it on a side stream
-            if not dcheck_finish(dcheck_launch()):
-                return False
-            cur, aux = torch.cuda.current_stream(device), _aux_stream(device)
-            aux.wait_stream(cur)
-            with torch.cuda.stream(aux), timers.span("rp.verify.gt_plan"):
-                plan = nt._multi_exp64_plan(rho)
-            fb = _miller_fold(ZB, Y, rho, r.V, S, l)                 # Miller values, LDS-folded
-            with torch.cuda.stream(aux):
-                G = nt._multi_exp64_run(r.A, plan)                         # prod a^rho (host tensor)
-        F = nt._finish_prod_on_host(fb)
-    else:
-        if not dcheck_finish(dcheck_launch()):
-            return False
-        F, G = nt.rp_verify_products(ZB, Y, rho, r.V, r.A, S, l)     # Miller product, prod a^rho
-    # prime-order part of the a_ij: an independent 40-bit combination in GT
-    # (the smallest prime factor of the cyclotomic cofactor is ~2^38.8, so a
-    # non-GT component survives the batch equation AND this test with
-    # probability ~2^-77)
-    with timers.span("rp.verify.gt_membership"):
+        Y = nt.g1_mul(sigmat.y_jac.to(device).index_select(0, y_idx).contiguous(), _rep(r.challenge, S))  # [n*S]
+    dpts = torch.cat([Cp.contiguous(), r.D.contiguous()])
+    dgrp = torch.cat([torch.zeros(n, dtype=torch.int32, device=device), torch.ones(n, dtype=torch.int32, device=device)])
+    # --- per-VN weights and their bucket plans (host syncs, before any fold is queued)
+    vns = []
+    for _ in range(n_vn):
+        w = _rand64(n, device)
+        rho = _rand64(n * S * l, device)
         gam = _rand64(n * S * l, device, 40)
-        Gm = nt._multi_exp64_run(r.A, nt._bucket_plan(gam, 5))
-        if not _gt_in_subgroup(Gm):
-            return False
-    e = nt.fr_dot_rows(rho, r.zv, 1)                                 # sum rho Zv
-    # the closing single-element work (one final exponentiation, one GT power)
-    # is a serial Fp12 chain: it runs on the host, where one core beats one GPU lane
-    with timers.span("rp.verify.fold_wait"):
-        F, G, e = F.cpu(), G.cpu(), e.cpu()
-    lhs_gt = nt.gt_mul(nt.final_exp(F), G)
+        dsc = torch.cat([nt.fr_arith(nt.FR_MUL, w, r.challenge), w])
+        dfull = torch.cat([nt.fr_dot_rows(w, r.zr, 1), nt.fr_dot_rows(w, z, 1)])
+        with timers.span("rp.verify.plans"):
+            vns.append({"rho": rho, "dfull": dfull, "dcheck": nt.g1_msm_launch(dpts, dsc, dgrp, 2, bits=256),
+                        "plan": nt._multi_exp64_plan(rho), "gplan": nt._bucket_plan(gam, 5),
+                        "e": nt.fr_dot_rows(rho, r.zv, 1)})
+    if device.type == "cuda":
+        cur, aux = torch.cuda.current_stream(device), _aux_stream(device)
+        aux.wait_stream(cur)  # the a_ij and the plans are ready; the folds below are not awaited
+        with timers.span("rp.verify.fold_queue"):
+            T = _fold_points(ZB, Y, S, l)
+            for v in vns:                                              # Miller folds, back to back
+                v["fb"] = _miller_fold_T(T, v["rho"], r.V)
+        with torch.cuda.stream(aux), timers.span("rp.verify.multiexp"):
+            for v in vns:                                              # prod a^rho, prod a^gamma
+                v["G"] = nt._multi_exp64_run(r.A, v["plan"])
+                v["Gm"] = nt._multi_exp64_run(r.A, v["gplan"])
+        cur.wait_stream(aux)
+        with timers.span("rp.verify.fold_wait"):
+            for v in vns:
+                v["F"] = nt._finish_prod_on_host(v["fb"])
+    else:
+        T = _fold_points(ZB, Y, S, l)
+        for v in vns:
+            f = nt.miller_loop(nt.g1_to_affine(nt.g1_mul(T, v["rho"])), r.V)
+            v["F"] = nt.gt_prod(f.view(-1, 1, 96), chunk=4).view(1, 96)
+            v["G"] = nt._multi_exp64_run(r.A, v["plan"])
+            v["Gm"] = nt._multi_exp64_run(r.A, v["gplan"])
+    out = []
     _, gt_tab = gt_generator_table("cpu")
-    rhs_gt = nt.gt_fb_pow(gt_tab, e)
-    return bool(nt.gt_eq(lhs_gt, rhs_gt).all())
+    PB_base = bn.g1_jac_tensor([P_point, O.G1_GEN], "cpu")
+    for v in vns:
+        with timers.span("rp.verify.finish"):
+            G0 = nt.g1_msm_finish(v["dcheck"])
+            PB = nt.g1_mul(PB_base, v["dfull"].cpu())
+            d_ok = bool(nt.g1_eq(nt.g1_sum(torch.stack([G0[0:1], PB[0:1], PB[1:2]])), G0[1:2])[0])
+            # prime-order part of the a_ij: the independent 40-bit combination in
+            # GT (the smallest prime factor of the cyclotomic cofactor is ~2^38.8:
+            # a non-GT component survives the batch equation AND this test with
+            # probability ~2^-77)
+            m_ok = _gt_in_subgroup(v["Gm"])
+            lhs = nt.gt_mul(nt.final_exp(v["F"].cpu()), v["G"].cpu())
+            eq_ok = bool(nt.gt_eq(lhs, nt.gt_fb_pow(gt_tab, v["e"].cpu())).all())
+        out.append(d_ok and m_ok and eq_ok)
+    return out
 
 
-def _miller_fold(ZB, Y, rho, V, S: int, L: int) -> torch.Tensor:
-    """GPU: per-workgroup partial products of ML(rho_it (ZB[p,j] - Y[p,i]), V_it)
-    over every item it = (p*S + i)*L + j.  Default: the two-phase fold
-    (csrc/kernels/fold_body.h) -- the G1 side as three wide launches (point
-    difference, 64-bit variable-base multiplication, affine conversion), then
+def _fold_points(ZB, Y, S: int, L: int) -> torch.Tensor:
+    """T_it = ZB[p*L + j] - Y[p*S + i] for every item it = (p*S + i)*L + j (Jacobian)."""
+    npj = ZB.shape[0] // L
+    zb = ZB.view(npj, 1, L, 24).expand(npj, S, L, 24).reshape(-1, 24)
+    yy = Y.view(npj, S, 1, 24).expand(npj, S, L, 24).reshape(-1, 24)
+    return nt.g1_add(zb.contiguous(), yy.contiguous(), subtract=True)
+
+
+def _miller_fold_T(T, rho, V) -> torch.Tensor:
+    """GPU: per-workgroup partial products of ML(rho_it T_it, V_it).  Default:
+    the two-phase fold (csrc/kernels/fold_body.h) -- the G1 side as two wide
+    launches (64-bit variable-base multiplication, affine conversion), then
     the line image and the K-item multi-Miller accumulation.
     ``DRYNX_FOLD=fused`` selects the previous one-kernel fold."""
-    if os.environ.get("DRYNX_FOLD", "2") == "fused":
-        return nt.rp_verify_fold(ZB, Y, rho, V, S, L)
     n = V.shape[0]
-    if n == 0:
-        return nt.gt_one(V.device).clone()
-    npj = ZB.shape[0] // L
-    with timers.span("rp.verify.fold_points"):
-        zb = ZB.view(npj, 1, L, 24).expand(npj, S, L, 24).reshape(-1, 24)
-        yy = Y.view(npj, S, 1, 24).expand(npj, S, L, 24).reshape(-1, 24)
-        P = nt.g1_to_affine(nt.g1_mul(nt.g1_add(zb.contiguous(), yy.contiguous(), subtract=True), rho))
+    if os.environ.get("DRYNX_FOLD", "2") == "fused":
+        return nt.rp_verify_fold(T, bn.g1_infinity_jac(n, T.device), rho, V, 1, 1)
+    P = nt.g1_to_affine(nt.g1_mul(T, rho))
     K = next((k for k in (8, 4, 2) if (n + 64 * k - 1) // (64 * k) >= 1024), 1)
-    with timers.span("rp.verify.fold_lines"):
-        lines = nt.rp_fold_lines(P, V)
-    return nt.rp_fold_accum(lines, n, K)
+    return nt.rp_fold_accum(nt.rp_fold_lines(P, V), n, K)
 
 
 _aux: dict = {}

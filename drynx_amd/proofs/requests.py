@@ -305,17 +305,37 @@ def _range_lists(req: ProofRequest, device) -> list:
 
 
 def verify_range_many(reqs: list, idxs: list, sq, device, cache: VerifierCache, part=None) -> dict:
-    """Range-proof requests of one VN as ONE batched verification: the sampled
+    """Range-proof requests of one VN as ONE batched verification (see
+    ``verify_range_many_multi``).  -> {request index: bool}"""
+    return verify_range_many_multi(reqs, {"vn": idxs}, sq, device, cache, part)["vn"]
+
+
+def verify_range_many_multi(reqs: list, vn_idxs: dict, sq, device, cache: VerifierCache, part=None) -> dict:
+    """Range-proof requests of several VNs hosted on this rank: the sampled
     prefix of every list (reference RangeProofThreshold semantics) of every
-    request, grouped by (u, l), folded into a single pairing batch.  If a
-    batch fails, each request is re-checked alone so the bitmap blames
-    exactly the bad ones.  ``part = (k, W)`` checks only the k-th of W equal
-    slices of every sampled prefix (the pooled verification of a multi-GPU
-    node: W ranks each check one slice on the VN's behalf).
-    -> {request index: bool}"""
+    request, grouped by (u, l), folded into one pairing batch per VN with that
+    VN's own random weights; VNs that sample the same requests share the
+    decode and the weight-free work (``rp.verify_range_proof_list_multi``).
+    If a VN's batch fails, each request is re-checked alone for that VN so the
+    bitmap blames exactly the bad ones.  ``part = (k, W)`` checks only the
+    k-th of W equal slices of every sampled prefix (the pooled verification of
+    a multi-GPU node).  vn_idxs: {vn: [request index]} -> {vn: {index: bool}}"""
+    by_set: dict = {}
+    for vn, idxs in vn_idxs.items():
+        by_set.setdefault(tuple(sorted(idxs)), []).append(vn)
+    out = {}
+    for idxs, group in by_set.items():
+        res = _verify_range_group(reqs, list(idxs), sq, device, cache, part, len(group))
+        for vn, rv in zip(group, res):
+            out[vn] = rv
+    return out
+
+
+def _verify_range_group(reqs, idxs, sq, device, cache, part, n_vn) -> list:
     P = sq.RosterServers.aggregate()
     sigs = sq.Query.IVSigs.InputValidationSigs
-    out, parts = {}, {}
+    mode = int(getattr(sq, "RangeProofMode", 0) or 0)
+    base, parts = {}, {}
     for i in idxs:
         try:
             lists = []
@@ -333,35 +353,40 @@ def verify_range_many(reqs: list, idxs: list, sq, device, cache: VerifierCache, 
                 if hi > lo:
                     lists.append(r if (lo, hi) == (0, len(r)) else rp.rpl_range(r, lo, hi))
             parts[i] = lists
-            out[i] = True
+            base[i] = True
         except Exception as e:
             log.warning(f"range proof from {reqs[i].sender_id} rejected: {e}")
-            out[i] = False
-    live = [i for i in idxs if out[i] and parts[i]]
+            base[i] = False
+    outs = [dict(base) for _ in range(n_vn)]
+    live = [i for i in idxs if base[i] and parts[i]]
     if not live:
-        return out
+        return outs
     sigmat = cache.sigmat(sq, device)
     groups: dict = {}
     for i in live:
         for r in parts[i]:
             groups.setdefault((r.u, r.l, r.S), []).append(r)
+    oks = [True] * n_vn
     try:
         with timers.span("rp.verify.cat"):
             cats = [rp.rpl_cat(g) for g in groups.values()]
-        ok = all(rp.verify_range_proof_list(c, sigmat, P, 1.0, device, sq.RangeProofMode) for c in cats)
+        for c in cats:
+            for k, ok in enumerate(rp.verify_range_proof_list_multi(c, sigmat, P, n_vn, device, mode)):
+                oks[k] = oks[k] and ok
     except Exception as e:
         log.warning(f"batched range verification failed: {e}")
-        ok = False
-    if ok or len(live) == 1:
-        for i in live:
-            out[i] = ok
-        return out
-    for i in live:  # attribute the failure
-        try:
-            out[i] = all(rp.verify_range_proof_list(r, sigmat, P, 1.0, device, sq.RangeProofMode) for r in parts[i])
-        except Exception:
-            out[i] = False
-    return out
+        oks = [False] * n_vn
+    for k in range(n_vn):
+        if oks[k] or len(live) == 1:
+            for i in live:
+                outs[k][i] = oks[k]
+            continue
+        for i in live:  # attribute the failure (this VN's own re-check, request by request)
+            try:
+                outs[k][i] = all(rp.verify_range_proof_list(r, sigmat, P, 1.0, device, mode) for r in parts[i])
+            except Exception:
+                outs[k][i] = False
+    return outs
 
 
 _DECODERS = {"keyswitch": lambda b, d: sigma.KeySwitchProof.from_bytes(b, d),
@@ -390,6 +415,7 @@ def verify_requests(reqs: list, sq, vn_id: str, vn_index: int, n_vns: int, devic
     sampling on this VN's rank beforehand)."""
     codes = [None] * len(reqs)
     todo: dict = {}
+    pooled_idx: list = []
     if len(reqs) >= _SIG_BATCH_MIN:
         with timers.span("verify.signature.batch"):
             sigs_ok = sigma.schnorr_verify_batch(
@@ -404,9 +430,8 @@ def verify_requests(reqs: list, sq, vn_id: str, vn_index: int, n_vns: int, devic
                 sig_ok = verify_signature(req, sq.IDtoPublic.get(req.sender_id))
         if not sig_ok:
             codes[i] = PROOF_FALSE_SIGN
-        elif range_pooled is not None and req.kind == "range" and req.base_key() in range_pooled:
-            res = range_pooled[req.base_key()]
-            codes[i] = PROOF_RECEIVED if res is None else (PROOF_TRUE if res else PROOF_FALSE)
+        elif range_pooled is not None and req.kind == "range" and not req.header_only:
+            pooled_idx.append(i)  # resolved below: the pooled batch may still be running
         elif not should_verify(sq, req, vn_index, n_vns):
             codes[i] = PROOF_RECEIVED
         else:
@@ -466,6 +491,13 @@ def verify_requests(reqs: list, sq, vn_id: str, vn_index: int, n_vns: int, devic
         with timers.span("rp.verify.early_wait"):
             for i, (fut, j) in early.items():
                 codes[i] = PROOF_TRUE if fut.result()[j] else PROOF_FALSE
+    if pooled_idx:
+        with timers.span("rp.verify.pooled_wait"):
+            pooled = range_pooled.result() if hasattr(range_pooled, "result") else range_pooled
+            pooled = pooled.get(vn_id, {}) if vn_id in pooled else pooled
+        for i in pooled_idx:
+            res = pooled.get(reqs[i].base_key(), False)
+            codes[i] = PROOF_RECEIVED if res is None else (PROOF_TRUE if res else PROOF_FALSE)
     return codes
 
 

@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import json
 import os
+import time
 
 import torch
 
@@ -38,12 +39,13 @@ def expected_counts(sq) -> dict:
 
 
 def use_pool(ctx) -> bool:
-    """Pooled range verification: on a multi-GPU node every rank checks a
-    1/world slice of every range-proof list on behalf of every VN (so three VNs
-    keep eight GPUs busy); the VN's own rank keeps the signature checks, the
-    sampling decision, the bitmap and the ledger.  ``DRYNX_VN_POOL=0`` leaves
-    each VN's range checks on its own rank."""
-    return ctx.comm.world > 1 and os.environ.get("DRYNX_VN_POOL", "1") != "0"
+    """Pooled range verification: every rank checks a 1/world slice of every
+    range-proof list on behalf of every VN (so three VNs keep eight GPUs busy;
+    on one GPU the co-hosted VNs' batches share the decode and run back to
+    back); the VN's own rank keeps the signature checks, the sampling
+    decision, the bitmap and the ledger.  ``DRYNX_VN_POOL=0`` leaves each VN's
+    range checks to the VN's own rank, one VN at a time."""
+    return os.environ.get("DRYNX_VN_POOL", "1") != "0"
 
 
 def fan_out(ctx, sq, local_requests: list, all_ranks: bool = False) -> list:
@@ -111,14 +113,14 @@ def pool_verify_ranges(ctx, sq, reqs: list, vns: list) -> dict:
     sampled = {}
     for d in ctx.comm.all_gather_object(local):
         sampled.update(d)
+    vn_idxs = {vn.id: [i for i in rng if sampled[vn.id].get(reqs[i].base_key())] for vn in vns}
+    t0 = time.perf_counter()
+    res = prq.verify_range_many_multi(reqs, vn_idxs, sq, ctx.device, ctx.verifier_cache, part=(k, W))
+    dt = time.perf_counter() - t0
     mine = {}
     for vn in vns:
-        idxs = [i for i in rng if sampled[vn.id].get(reqs[i].base_key())]
-        res = {}
-        if idxs:
-            with timers.timed(f"{vn.id}_VerifyRange"):
-                res = prq.verify_range_many(reqs, idxs, sq, ctx.device, ctx.verifier_cache, part=(k, W))
-        mine[vn.id] = {reqs[i].base_key(): bool(ok) for i, ok in res.items()}
+        timers.record(f"{vn.id}_VerifyRange", dt)  # one shared pass for the co-hosted VNs
+        mine[vn.id] = {reqs[i].base_key(): bool(ok) for i, ok in res.get(vn.id, {}).items()}
     verdicts = ctx.comm.all_gather_object(mine)
     out = {}
     for vn in vns:
@@ -127,7 +129,32 @@ def pool_verify_ranges(ctx, sq, reqs: list, vns: list) -> dict:
     return out
 
 
-def verify_and_store(ctx, sq, vn, vn_index: int, n_vns: int, requests: list, range_pooled: dict | None = None) -> dict:
+def _pool_async(ctx, sq, reqs, vns):
+    """pool_verify_ranges on a worker thread with its own HIP stream: the
+    range batches (the GPU's long pole) run while this thread checks the
+    short per-CN proofs of each VN.  On a multi-rank node the worker also
+    owns the pool's collectives (the main thread issues none meanwhile)."""
+    import concurrent.futures as cf
+
+    if not hasattr(ctx, "_pool_exec"):
+        ctx._pool_exec = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="drynx-vn-pool")
+    if ctx.device.type != "cuda":
+        return ctx._pool_exec.submit(pool_verify_ranges, ctx, sq, reqs, vns)
+    if not hasattr(ctx, "_pool_stream"):
+        ctx._pool_stream = torch.cuda.Stream(ctx.device)
+    side, main = ctx._pool_stream, torch.cuda.current_stream(ctx.device)
+    side.wait_stream(main)
+
+    def run():
+        with torch.cuda.stream(side):
+            out = pool_verify_ranges(ctx, sq, reqs, vns)
+        side.synchronize()
+        return out
+
+    return ctx._pool_exec.submit(run)
+
+
+def verify_and_store(ctx, sq, vn, vn_index: int, n_vns: int, requests: list, range_pooled=None) -> dict:
     store = ctx.store(vn.id)
     bitmap = {}
     counts = {k: 0 for k in prq.VN_ORDER}
@@ -137,7 +164,7 @@ def verify_and_store(ctx, sq, vn, vn_index: int, n_vns: int, requests: list, ran
         bitmap[key] = code
         counts[req.kind] += 1
         if req.kind != "shuffle":  # storeProof skips shuffle proofs (proof_collection_protocol.go:318-331)
-            store.update_async(f"{sq.SurveyID}/{req.kind}", key, req.payload())
+            store.update_async(f"{sq.SurveyID}/{req.kind}", key, ctx.ledger_value(req))
     exp = expected_counts(sq)
     for k in prq.VN_ORDER:
         if counts[k] != exp[k]:
@@ -155,10 +182,12 @@ def proof_collection(ctx, sq, local_requests: list):
         reqs = fan_out(ctx, sq, local_requests, all_ranks=pool)
     bitmaps = {}
     with timers.timed("ProofVerification"):
-        pooled = pool_verify_ranges(ctx, sq, reqs, vns) if pool else {}
+        pooled = _pool_async(ctx, sq, reqs, vns) if pool else None
         for idx, vn in enumerate(vns):
             if vn.rank == ctx.rank:
-                bitmaps[vn.id] = verify_and_store(ctx, sq, vn, idx, len(vns), reqs, pooled.get(vn.id))
+                bitmaps[vn.id] = verify_and_store(ctx, sq, vn, idx, len(vns), reqs, pooled)
+        if pooled is not None:
+            pooled.result()
     # bitmaps -> root VN (SharedBMChannel)
     allbm = {}
     for d in ctx.comm.all_gather_object(bitmaps):

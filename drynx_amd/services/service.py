@@ -112,6 +112,29 @@ class DrynxNode:
             return self._end_blocks.get(survey_id)
 
     # ------------------------------------------------------------------ VN storage
+    def ledger_value(self, req):
+        """What a VN stores for a proof request (storeProof,
+        proof_collection_protocol.go:318-331).  Range proofs: the reference
+        layout network.Marshal(&RangeProofListBytes) (proofs/range_wire.py),
+        encoded once per rank on the ledger thread and shared by the stores
+        of the co-hosted VNs; other kinds: their marshalled payload."""
+        if req.kind != "range" or req.header_only:
+            return req.payload()
+        if not hasattr(self, "_blobs"):
+            from ..ledger.store import BlobSegment
+
+            self._blobs = BlobSegment(os.path.join(self.workdir, f"ledger_r{self.rank}.blobs"), self.device)
+
+        def produce():
+            from ..proofs import range_wire
+
+            try:
+                return range_wire.encode_bundle(prq._range_lists(req, self.device))
+            except Exception:  # undecodable payload: keep the bytes as received
+                return bytes(req.data)
+
+        return self._blobs.put(req.digest().hex(), produce)
+
     def store(self, vn_id: str) -> Store:
         s = self._stores.get(vn_id)
         if s is None or s.closed:
@@ -370,6 +393,8 @@ class DrynxNode:
         """Wait until every queued ledger write is durable."""
         for s in self._stores.values():
             s.flush()
+        if hasattr(self, "_blobs"):
+            self._blobs.flush()
 
     def close_db(self, vn_id: str, remove: bool = False):
         s = self._stores.pop(vn_id, None)
@@ -379,3 +404,6 @@ class DrynxNode:
     def close(self, remove: bool = False):
         for k in list(self._stores):
             self.close_db(k, remove)
+        if hasattr(self, "_blobs"):
+            self._blobs.close(remove)
+            del self._blobs

@@ -97,7 +97,14 @@ ACK = (("OK", "bool"),)
 ERROR = (("Message", "string"),)
 SHUTDOWN = ()
 
+# lib/range/range_proof.go:26-57 (RangeProofListBytes / RangeProofBytes / RangeProofDataBytes)
+RANGE_PROOF_DATA_BYTES = (("Challenge", "bytes"), ("Zr", "bytes"), ("D", "bytes"), ("Zv", ("rep", "bytes")),
+                          ("Zphi", "bytes"), ("V", ("rep", "bytes")), ("A", ("rep", "bytes")))
+RANGE_PROOF_BYTES = (("Commit", "bytes"), ("RP", ("msg", RANGE_PROOF_DATA_BYTES)))
+RANGE_PROOF_LIST_BYTES = (("Data", ("ptrslice", ("msg", RANGE_PROOF_BYTES))),)
+
 MESSAGES = {
+    "libdrynxrange.RangeProofListBytes": RANGE_PROOF_LIST_BYTES,
     "libdrynx.SurveyQuery": SURVEY_QUERY,
     "libdrynx.SurveyQueryToVN": SURVEY_QUERY_TO_VN,
     "libdrynx.SurveyQueryToDP": SURVEY_QUERY_TO_DP,

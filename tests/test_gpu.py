@@ -110,9 +110,9 @@ def test_lr_encode_fused_matches_torch(gpu_device):
         assert torch.allclose(g2, ref2, rtol=1e-10, atol=1e-8), (g2 - ref2).abs().max()
 
 
-@pytest.mark.parametrize("order", ["1", "0", "last"])
-def test_range_proofs_gpu(gpu_device, order, monkeypatch):
-    monkeypatch.setenv("DRYNX_FOLD_FIRST", order)
+@pytest.mark.parametrize("fold", ["2", "fused"])
+def test_range_proofs_gpu(gpu_device, fold, monkeypatch):
+    monkeypatch.setenv("DRYNX_FOLD", fold)
     from drynx_amd.crypto import elgamal as eg
     from drynx_amd.ops.encoding import CreateProofBatch
     from drynx_amd.proofs import range_proof as rp
@@ -222,15 +222,15 @@ def test_every_operation_on_gpu(gpu_device, tmp_path, op):
     node.close(remove=True)
 
 
-def test_survey_early_range_and_cu_masked_fold_gpu(gpu_device, tmp_path, monkeypatch):
-    """The opt-in schedules (VN range check started at proving time, Miller
-    fold on a CU-masked stream) give the same result and bitmap."""
+def test_survey_early_range_gpu(gpu_device, tmp_path, monkeypatch):
+    """The opt-in schedule (per-VN range checks, the VN's check started at
+    proving time) gives the same result and bitmap."""
     from drynx_amd.proofs import requests as prq
     from drynx_amd.services.api import DrynxClient
     from drynx_amd.services.local import local_cluster, make_survey
 
     monkeypatch.setenv("DRYNX_EARLY_RANGE", "1")
-    monkeypatch.setenv("DRYNX_FOLD_RESERVE_CUS", "32")
+    monkeypatch.setenv("DRYNX_VN_POOL", "0")
     started = []
     orig = prq.start_early_range_verification
     monkeypatch.setattr(prq, "start_early_range_verification",

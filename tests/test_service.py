@@ -218,3 +218,30 @@ def test_vn_api_registration_and_blocking_end_verification(env):
     t.join(120)
     assert got["b"] is not None and got["b"].Hash == res.block.Hash
     assert client.send_end_verification("vn0", "no-such-survey", 0.05) is None
+
+
+def test_get_proofs_reference_layout_roundtrip(env):
+    """GetProofs serves range proofs as network.Marshal(&RangeProofListBytes)
+    (range_proof.go:72-155, proof_collection_protocol.go:318-331): decode the
+    bytes with the query's ranges and verify them again."""
+    from drynx_amd.proofs import range_proof as rp
+    from drynx_amd.proofs import range_wire as rw
+
+    cl, node, client = env
+    sq = make_survey(client, cl, "mean", query_min=0, query_max=9, rows=6, proofs=1, ranges=[16, 3])
+    _, _, res = client.send_survey_query(sq)
+    proofs = client.send_get_proofs("vn1", sq.SurveyID)
+    rng = {k: v for k, v in proofs.items() if "/range/" in k}
+    assert len(rng) == 5
+    sm = node.verifier_cache.sigmat(sq, "cpu")
+    P = sq.RosterServers.aggregate()
+    for k, b in rng.items():
+        assert b[:16] == rw.onet.message_type_id(rw.LIST_TYPE)
+        lists = rw.decode_bundle(b, sq.Query.Ranges)
+        assert len(lists) == 1 and len(lists[0]) == 2  # mean: 2 outputs, one proof each
+        assert rp.verify_range_proof_list(lists[0], sm, P)
+    # a flipped byte inside one proof's A values breaks exactly that list
+    k0 = next(iter(rng))
+    bad = bytearray(rng[k0])
+    bad[-5] ^= 1
+    assert not rp.verify_range_proof_list(rw.decode_bundle(bytes(bad), sq.Query.Ranges)[0], sm, P)
