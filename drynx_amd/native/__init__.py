@@ -891,6 +891,44 @@ def _multi_exp64_run(a: torch.Tensor, plan) -> torch.Tensor:
     return acc
 
 
+def multi_exp_grouped(a: torch.Tensor, k: torch.Tensor, group: torch.Tensor, n_groups: int, W: int = _ME_W):
+    """Launch G independent multi-exponentiations prod_{i: group_i = g} a[i % n]^k_i
+    (n = rows of a, k [m, 8] with m a multiple of n, low W bytes of each
+    exponent) as ONE bucket plan (one host sync for all groups, e.g. the
+    batch weights of several verifying nodes).  Returns a handle for
+    ``multi_exp_grouped_finish``; device passes are queued on the current stream."""
+    n = a.shape[0]
+    plan = _bucket_plan(k, W, group, n_groups)
+    plan["item"] = (plan["item"] % n).contiguous()
+    bk = plan["bk"]
+    h = {"G": n_groups, "W": W, "win": None}
+    if bk.size == 0:
+        return h
+    cur = a.index_select(0, plan["item"]).contiguous() if plan["single"] else None
+    for i, (st, ln) in enumerate(plan["passes"]):
+        cur = gt_slice_prod(a if i == 0 else cur, plan["item"] if i == 0 else None, st, ln)
+    bkp = gt_pow(cur, plan["digit_sc"])
+    g, w, d = bk // (W * 256), (bk // 256) % W, bk % 256
+    slot = torch.from_numpy(d * (n_groups * W) + g * W + w).to(a.device)
+    win = gt_one(a.device).repeat(256 * n_groups * W, 1)
+    win[slot] = bkp
+    h["win"] = _gt_prod_level(win.view(256, n_groups * W, 96), 8) if a.is_cuda else win.view(256, n_groups * W, 96)
+    return h
+
+
+def multi_exp_grouped_finish(h) -> torch.Tensor:
+    """[G, 96] host results: per-window products and the Horner steps on the host."""
+    G, W = h["G"], h["W"]
+    if h["win"] is None:
+        return gt_one("cpu").repeat(G, 1)
+    S_w = gt_prod(h["win"].cpu(), chunk=4).view(G, W, 96)
+    acc = S_w[:, W - 1].contiguous()
+    sh = _pow2_scalar(_ME_C).expand(G, 8).contiguous()
+    for w in range(W - 2, -1, -1):
+        acc = gt_mul(gt_pow(acc, sh), S_w[:, w].contiguous())
+    return acc
+
+
 def g1_slice_sum(src: torch.Tensor, idx, start: torch.Tensor, length: torch.Tensor) -> torch.Tensor:
     """out[s] = sum_k src[idx[start[s] + k]] (or src[start[s] + k]), k < length[s] (Jacobian)."""
     n = start.numel()

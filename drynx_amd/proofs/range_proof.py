@@ -665,49 +665,56 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
         Y = nt.g1_fb_mul_idx(ytabs[0], ytabs[1].index_select(0, y_idx).contiguous(), _rep(r.challenge, S))
     else:
         Y = nt.g1_mul(sigmat.y_jac.to(device).index_select(0, y_idx).contiguous(), _rep(r.challenge, S))  # [n*S]
-    dpts = torch.cat([Cp.contiguous(), r.D.contiguous()])
-    dgrp = torch.cat([torch.zeros(n, dtype=torch.int32, device=device), torch.ones(n, dtype=torch.int32, device=device)])
-    # --- per-VN weights and their bucket plans (host syncs, before any fold is queued)
-    vns = []
-    for _ in range(n_vn):
-        w = _rand64(n, device)
-        rho = _rand64(n * S * l, device)
-        gam = _rand64(n * S * l, device, 40)
-        dsc = torch.cat([nt.fr_arith(nt.FR_MUL, w, r.challenge), w])
-        dfull = torch.cat([nt.fr_dot_rows(w, r.zr, 1), nt.fr_dot_rows(w, z, 1)])
-        with timers.span("rp.verify.plans"):
-            vns.append({"rho": rho, "dfull": dfull, "dcheck": nt.g1_msm_launch(dpts, dsc, dgrp, 2, bits=256),
-                        "plan": nt._multi_exp64_plan(rho), "gplan": nt._bucket_plan(gam, 5),
-                        "e": nt.fr_dot_rows(rho, r.zv, 1)})
+    # --- per-VN weights: every VN's bucket plans in ONE host sync each
+    G, m = n_vn, n * S * l
+    w_all = _rand64(G * n, device)                                    # D-equation weights
+    rho_all = _rand64(G * m, device)                                  # pairing-equation weights
+    gam_all = _rand64(G * m, device, 40)                              # GT-membership combination
+    vid = torch.arange(G, device=device)
+    with timers.span("rp.verify.plans"):
+        dpts = torch.cat([Cp.contiguous(), r.D.contiguous()]).repeat(G, 1)
+        wc = nt.fr_arith(nt.FR_MUL, w_all, r.challenge.repeat(G, 1))
+        dsc = torch.cat([torch.stack([wc.view(G, n, 8), w_all.view(G, n, 8)], 1).reshape(-1, 8)])
+        dgrp = (vid.view(G, 1, 1) * 2 + torch.arange(2, device=device).view(1, 2, 1)).expand(G, 2, n).reshape(-1)
+        dcheck = nt.g1_msm_launch(dpts, dsc.contiguous(), dgrp.to(torch.int32).contiguous(), 2 * G, bits=256)
+        mgrp = torch.cat([vid.repeat_interleave(m), G + vid.repeat_interleave(m)]).to(torch.int32)
+        aux = _aux_stream(device) if device.type == "cuda" else None
+        if aux is not None:
+            aux.wait_stream(torch.cuda.current_stream(device))
+        with (torch.cuda.stream(aux) if aux is not None else _nullctx()):
+            mexp = nt.multi_exp_grouped(r.A, torch.cat([rho_all, gam_all]), mgrp, 2 * G)   # queued on aux
+        e_all = nt.fr_dot_rows(rho_all, r.zv, G, b_periodic=True)                        # sum rho Zv per VN
+        dfull = torch.stack([nt.fr_dot_rows(w_all, r.zr, G, b_periodic=True),
+                             nt.fr_dot_rows(w_all, z, G, b_periodic=True)], 1)             # [G, 2, 8]
+    vns = [{"rho": rho_all[v * m:(v + 1) * m]} for v in range(G)]
+    T = _fold_points(ZB, Y, S, l)
     if device.type == "cuda":
-        cur, aux = torch.cuda.current_stream(device), _aux_stream(device)
-        aux.wait_stream(cur)  # the a_ij and the plans are ready; the folds below are not awaited
         with timers.span("rp.verify.fold_queue"):
-            T = _fold_points(ZB, Y, S, l)
             for v in vns:                                              # Miller folds, back to back
                 v["fb"] = _miller_fold_T(T, v["rho"], r.V)
-        with torch.cuda.stream(aux), timers.span("rp.verify.multiexp"):
-            for v in vns:                                              # prod a^rho, prod a^gamma
-                v["G"] = nt._multi_exp64_run(r.A, v["plan"])
-                v["Gm"] = nt._multi_exp64_run(r.A, v["gplan"])
-        cur.wait_stream(aux)
+        with timers.span("rp.verify.multiexp"):
+            aux.synchronize()
+            GG = nt.multi_exp_grouped_finish(mexp)                     # [2G, 96]: prod a^rho_v, prod a^gamma_v
         with timers.span("rp.verify.fold_wait"):
             for v in vns:
                 v["F"] = nt._finish_prod_on_host(v["fb"])
     else:
-        T = _fold_points(ZB, Y, S, l)
+        GG = nt.multi_exp_grouped_finish(mexp)
         for v in vns:
             f = nt.miller_loop(nt.g1_to_affine(nt.g1_mul(T, v["rho"])), r.V)
             v["F"] = nt.gt_prod(f.view(-1, 1, 96), chunk=4).view(1, 96)
-            v["G"] = nt._multi_exp64_run(r.A, v["plan"])
-            v["Gm"] = nt._multi_exp64_run(r.A, v["gplan"])
+    D_all = nt.g1_msm_finish(dcheck)                                   # [2G, 24]
+    e_all, dfull = e_all.cpu(), dfull.cpu()
+    for k, v in enumerate(vns):
+        v.update(G=GG[k: k + 1], Gm=GG[G + k: G + k + 1], dfull=dfull[k], e=e_all[k: k + 1],
+                 dcheck=D_all[2 * k: 2 * k + 2])
     out = []
     _, gt_tab = gt_generator_table("cpu")
     PB_base = bn.g1_jac_tensor([P_point, O.G1_GEN], "cpu")
     for v in vns:
         with timers.span("rp.verify.finish"):
-            G0 = nt.g1_msm_finish(v["dcheck"])
-            PB = nt.g1_mul(PB_base, v["dfull"].cpu())
+            G0 = v["dcheck"]
+            PB = nt.g1_mul(PB_base, v["dfull"])
             d_ok = bool(nt.g1_eq(nt.g1_sum(torch.stack([G0[0:1], PB[0:1], PB[1:2]])), G0[1:2])[0])
             # prime-order part of the a_ij: the independent 40-bit combination in
             # GT (the smallest prime factor of the cyclotomic cofactor is ~2^38.8:
@@ -718,6 +725,14 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
             eq_ok = bool(nt.gt_eq(lhs, nt.gt_fb_pow(gt_tab, v["e"].cpu())).all())
         out.append(d_ok and m_ok and eq_ok)
     return out
+
+
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
 
 
 def _fold_points(ZB, Y, S: int, L: int) -> torch.Tensor:

@@ -46,56 +46,73 @@ def _hdr(num: int, length: int) -> bytes:
     return _uvarint((num << 3) | 2) + _uvarint(length)
 
 
-def _block(h: bytes, n: int, *shape) -> np.ndarray:
-    return np.broadcast_to(np.frombuffer(h, dtype=np.uint8), (n, *shape, len(h)))
+def _block(h: bytes, n: int, *shape, device="cpu") -> torch.Tensor:
+    return torch.frombuffer(bytearray(h), dtype=torch.uint8).to(device).expand(n, *shape, len(h))
+
+
+def _be(t: torch.Tensor, mont: bool) -> torch.Tensor:
+    """8-limb rows -> canonical 32-byte big-endian rows (on the tensor's device):
+    out of Montgomery form for field elements, then the little-endian limb
+    string reversed."""
+    rows = t.reshape(-1, 8).contiguous()
+    if mont:
+        rows = nt.fp_from_mont(rows)
+    return rows.view(torch.uint8).view(-1, 32).flip(1)
 
 
 def list_fields(r: rp.RangeProofList) -> dict:
-    """Canonical kyber encodings of a list's fields as host uint8 arrays
-    (one device conversion + one copy per field)."""
+    """Canonical kyber encodings of a list's fields as uint8 tensors on the
+    list's device (G1 = x||y, G2 = x.c1||x.c0||y.c1||y.c0, GT = the 12 Fp
+    coefficients in reverse tower order, scalars 32 B big-endian)."""
     n, l, S = len(r), r.l, r.S
-    f = {"commit": np.frombuffer(r.commit.to_bytes(), dtype=np.uint8).reshape(n, 128)}
+    both = torch.stack([r.commit.K, r.commit.C], dim=1).reshape(-1, 24)
+    f = {"commit": _be(nt.g1_to_affine(both), True).reshape(n, 128)}
     if r.has_rp and n:
-        f["challenge"] = bn.scalars_to_bytes(r.challenge).reshape(n, 32)
-        f["zr"] = bn.scalars_to_bytes(r.zr).reshape(n, 32)
-        f["D"] = bn.g1_aff_to_bytes(nt.g1_to_affine(r.D.contiguous())).reshape(n, 64)
-        f["zv"] = bn.scalars_to_bytes(r.zv).reshape(n, S, 32 * l)
-        f["zphi"] = bn.scalars_to_bytes(r.zphi).reshape(n, 32 * l)
-        f["V"] = bn.g2_aff_to_bytes(r.V).reshape(n, S, 128 * l)
-        f["A"] = bn.gt_to_bytes(r.A).reshape(n, S, 384 * l)
+        f["challenge"] = _be(r.challenge, False).reshape(n, 32)
+        f["zr"] = _be(r.zr, False).reshape(n, 32)
+        f["D"] = _be(nt.g1_to_affine(r.D.contiguous()), True).reshape(n, 64)
+        f["zv"] = _be(r.zv, False).reshape(n, S, 32 * l)
+        f["zphi"] = _be(r.zphi, False).reshape(n, 32 * l)
+        f["V"] = _be(r.V, True).reshape(-1, 2, 32).flip(1).reshape(n, S, 128 * l)      # (imag, real) per Fp2
+        f["A"] = _be(r.A, True).reshape(-1, 12, 32).flip(1).reshape(n, S, 384 * l)     # reversed coefficients
     return f
 
 
-def _proof_messages(r: rp.RangeProofList, f: dict) -> np.ndarray:
+def _proof_messages(r: rp.RangeProofList, f: dict) -> torch.Tensor:
     """[n, k] uint8: every proof's RangeProofBytes message with its field-1
     header of the Data slice (all proofs of a list have the same length)."""
     n, l, S = len(r), r.l, r.S
-    commit = [_block(_hdr(1, 128), n), f["commit"]]
+    dev = f["commit"].device
+    B = lambda h, *shape: _block(h, n, *shape, device=dev)  # noqa: E731
+    commit = [B(_hdr(1, 128)), f["commit"]]
     if not (r.has_rp and n):
-        body = np.concatenate(commit + [_block(_hdr(2, 0), n)], axis=1)
+        body = torch.cat(commit + [B(_hdr(2, 0))], dim=1)
     else:
-        rp_parts = [_block(_hdr(1, 32), n), f["challenge"], _block(_hdr(2, 32), n), f["zr"],
-                    _block(_hdr(3, 64), n), f["D"],
-                    np.concatenate([_block(_hdr(4, 32 * l), n, S), f["zv"]], axis=2).reshape(n, -1),
-                    _block(_hdr(5, 32 * l), n), f["zphi"],
-                    np.concatenate([_block(_hdr(6, 128 * l), n, S), f["V"]], axis=2).reshape(n, -1),
-                    np.concatenate([_block(_hdr(7, 384 * l), n, S), f["A"]], axis=2).reshape(n, -1)]
+        rp_parts = [B(_hdr(1, 32)), f["challenge"], B(_hdr(2, 32)), f["zr"], B(_hdr(3, 64)), f["D"],
+                    torch.cat([B(_hdr(4, 32 * l), S), f["zv"]], dim=2).reshape(n, -1),
+                    B(_hdr(5, 32 * l)), f["zphi"],
+                    torch.cat([B(_hdr(6, 128 * l), S), f["V"]], dim=2).reshape(n, -1),
+                    torch.cat([B(_hdr(7, 384 * l), S), f["A"]], dim=2).reshape(n, -1)]
         rp_len = sum(p.shape[1] for p in rp_parts)
-        body = np.concatenate(commit + [_block(_hdr(2, rp_len), n)] + rp_parts, axis=1)
-    return np.concatenate([_block(_hdr(1, body.shape[1]), n), body], axis=1)
+        body = torch.cat(commit + [B(_hdr(2, rp_len))] + rp_parts, dim=1)
+    return torch.cat([B(_hdr(1, body.shape[1])), body], dim=1)
 
 
 def encode_bundle(rpls: list, fields: list | None = None) -> bytes:
     """network.Marshal(&RangeProofListBytes) of all proofs of a DP's bundle,
-    in output-column order."""
+    in output-column order.  Assembled on the proofs' device; one copy of the
+    finished bytes to the host."""
     fields = fields if fields is not None else [list_fields(r) for r in rpls]
     msgs = [_proof_messages(r, f) for r, f in zip(rpls, fields)]
     cols = [c for r in rpls for c in r.cols]
-    if len(msgs) == 1 and cols == sorted(cols):
-        inner = np.ascontiguousarray(msgs[0]).tobytes()
-    else:
+    if not msgs:
+        return onet.message_type_id(LIST_TYPE)
+    allm = msgs[0] if len(msgs) == 1 else None
+    if allm is None or cols != sorted(cols):
         rows = [m[i] for m in msgs for i in range(m.shape[0])]
-        inner = b"".join(rows[i].tobytes() for i in sorted(range(len(rows)), key=lambda i: cols[i]))
+        inner = b"".join(rows[i].cpu().numpy().tobytes() for i in sorted(range(len(rows)), key=lambda i: cols[i]))
+    else:
+        inner = allm.contiguous().cpu().numpy().tobytes()
     return onet.message_type_id(LIST_TYPE) + (_hdr(1, len(inner)) + inner if inner else b"")
 
 

@@ -85,3 +85,37 @@ def test_data_block_is_an_onet_message():
     back = DataBlock.from_bytes(b)
     assert back.Proofs == db.Proofs and back.Roster == db.Roster and back.SurveyID == "s1"
     assert abs(back.Time - db.Time) < 1e-6 and back.ServerNumber == 3 and back.Sample == db.Sample
+
+
+def test_range_proof_list_bytes_layout():
+    """The device-assembled RangeProofListBytes envelope equals the generic
+    dedis/protobuf encoding of the reference structs (range_proof.go:26-57,
+    72-155) built from the host codecs, and decodes back to a valid list."""
+    from drynx_amd import native as nt
+    from drynx_amd.crypto import bn254 as bn
+    from drynx_amd.crypto import elgamal as eg
+    from drynx_amd.ops.encoding import CreateProofBatch
+    from drynx_amd.proofs import range_proof as rp
+    from drynx_amd.proofs import range_wire as rw
+    from drynx_amd.wire import onet
+
+    S, u, l = 2, 4, 3
+    sigs = [rp.init_range_proof_signatures([u] * 3) for _ in range(S)]
+    P = eg.aggregate_keys([eg.KeyPair.generate().public for _ in range(S)])
+    sm = rp.SigMaterial(sigs)
+    cv, r = eg.encrypt_ints(eg.pk_table(P), [1, 5, 9])
+    rpl = rp.create_range_proofs(CreateProofBatch([1, 5, 9], r, cv, [u] * 3, [l] * 3, [0, 1, 2], [0] * 3), sm, P)[0]
+    b = rw.encode_bundle([rpl])
+    commit = [rpl.commit[p:p + 1].to_bytes() for p in range(3)]
+    D = bn.g1_aff_to_bytes(nt.g1_to_affine(rpl.D))
+    zv = bn.scalars_to_bytes(rpl.zv).reshape(3, S, l * 32)
+    V = bn.g2_aff_to_bytes(rpl.V).reshape(3, S, l * 128)
+    A = bn.gt_to_bytes(rpl.A).reshape(3, S, l * 384)
+    obj = {"Data": [{"Commit": commit[p], "RP": {
+        "Challenge": bn.scalars_to_bytes(rpl.challenge)[p].tobytes(), "Zr": bn.scalars_to_bytes(rpl.zr)[p].tobytes(),
+        "D": D[p].tobytes(), "Zv": [zv[p, i].tobytes() for i in range(S)],
+        "Zphi": bn.scalars_to_bytes(rpl.zphi).reshape(3, l * 32)[p].tobytes(),
+        "V": [V[p, i].tobytes() for i in range(S)], "A": [A[p, i].tobytes() for i in range(S)]}} for p in range(3)]}
+    assert b == onet.marshal(rw.LIST_TYPE, obj)
+    back = rw.decode_bundle(b, [[u, l]] * 3)
+    assert len(back) == 1 and rp.verify_range_proof_list(back[0], sm, P)
