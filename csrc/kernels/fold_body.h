@@ -16,6 +16,7 @@
 // The product over items is all the batch equation needs.
 #pragma once
 #include "common.h"
+#include "../bn254/g1_fast.h"
 
 #define FOLD_CAT2(a, b) a##b
 #define FOLD_CAT(a, b) FOLD_CAT2(a, b)
@@ -128,6 +129,61 @@ __global__ void __launch_bounds__(kWG) DX_OCC rp_lines_kernel(const uint32_t *__
            lines, n, s++, it);
 }
 
+// G1 side of the fold, one launch per VN: P_it = affine(rho_it (ZB[p*L+j] -
+// Y[p*S+i])) for it = (p*S + i)*L + j -- the gather, the point difference, a
+// 3-bit-window multiplication by the 64-bit batch weight (window table in
+// LDS, as g1_varmul_kernel) and the affine conversion, fused (no [n]
+// intermediates in HBM).
+constexpr int kPW = 3, kPE = (1 << kPW) - 1;
+__global__ void __launch_bounds__(kWG) DX_OCC rp_points_kernel(const uint32_t *__restrict__ ZB,
+                                                               const uint32_t *__restrict__ Yj,
+                                                               const uint32_t *__restrict__ rho,
+                                                               uint32_t *__restrict__ P_aff, int64_t n, int S, int L) {
+  __shared__ uint32_t tab[kPE][24][kWG];
+  const int lane = threadIdx.x;
+  const int64_t it = (int64_t)blockIdx.x * kWG + lane;
+  const int64_t ii = it < n ? it : n - 1;  // tail lanes recompute the last item (never stored)
+  const int64_t j = ii % L, pi = ii / L, p = pi / S;
+  G1J T = at<G1J>(ZB, p * L + j);
+  G1J y = at<G1J>(Yj, pi);
+  if (!y.is_inf()) {
+    y.y = fneg(y.y);
+    g1_add_i(T, y);
+  }
+  G1J acc = T;
+  for (int e = 0; e < kPE; e++) {
+    const uint32_t *w = reinterpret_cast<const uint32_t *>(&acc);
+#pragma unroll
+    for (int l = 0; l < 24; l++) tab[e][l][lane] = w[l];
+    if (e + 1 < kPE && !T.is_inf()) g1_add_i(acc, T);
+  }
+  const uint32_t *k = rho + 8 * ii;
+  auto digit = [&](int wdx) -> uint32_t {
+    const int bit = wdx * kPW;
+    uint32_t v = k[bit >> 5] >> (bit & 31);
+    if ((bit & 31) + kPW > 32 && (bit >> 5) + 1 < 8) v |= k[(bit >> 5) + 1] << (32 - (bit & 31));
+    return v & ((1u << kPW) - 1);
+  };
+  int top = (256 + kPW - 1) / kPW - 1;
+  while (top > 0 && digit(top) == 0) top--;
+  G1J r = G1J::inf();
+  if (!T.is_inf()) {
+    for (int wdx = top; wdx >= 0; wdx--) {
+#pragma unroll
+      for (int d = 0; d < kPW; d++) g1_dbl_i(r);
+      const uint32_t dg = digit(wdx);
+      if (dg) {
+        G1J q;
+        uint32_t *w = reinterpret_cast<uint32_t *>(&q);
+#pragma unroll
+        for (int l = 0; l < 24; l++) w[l] = tab[dg - 1][l][lane];
+        g1_add_i(r, q);
+      }
+    }
+  }
+  if (it < n) at<G1A>(P_aff, it) = to_affine(r);
+}
+
 template <int K>
 __device__ __forceinline__ void accum_step(Fp12 &f, const uint4 *__restrict__ lines, int64_t n, int s, int64_t base) {
 #pragma unroll 1
@@ -179,6 +235,16 @@ int FOLD_NAME(dx_rp_lines_)(void *stream, const uint32_t *P_aff, const uint32_t 
   hipLaunchKernelGGL(rp_lines_kernel, dim3((unsigned)blocks), dim3(kWG), 0, (hipStream_t)stream, P_aff, V_aff,
                      reinterpret_cast<uint4 *>(lines), n);
   return check_hip(hipGetLastError(), "rp_lines");
+}
+
+int FOLD_NAME(dx_rp_points_)(void *stream, const uint32_t *ZB_jac, const uint32_t *Y_jac, const uint32_t *rho,
+                             uint32_t *P_aff, int64_t n, int S, int L) {
+  using namespace FOLD_NAME(fold_ns_);
+  if (n <= 0) return 0;
+  const int64_t blocks = (n + kWG - 1) / kWG;
+  hipLaunchKernelGGL(rp_points_kernel, dim3((unsigned)blocks), dim3(kWG), 0, (hipStream_t)stream, ZB_jac, Y_jac, rho,
+                     P_aff, n, S, L);
+  return check_hip(hipGetLastError(), "rp_points");
 }
 
 // f_blk: ceil(n / (64 K)) Fp12 partial products.

@@ -87,7 +87,7 @@ class BlobSegment:
             off = self._f.seek(0, os.SEEK_END)
             self._f.write(data)
             self._f.flush()
-        return off, len(data)
+        return off, memoryview(data).nbytes
 
     def flush(self):
         with self._lock:

@@ -105,6 +105,8 @@ _SIGS = {
     "dx_g2_subgroup": [_I, _P, _P, _P, _L],
     "dx_limbs_canonical": [_I, _P, _P, _I, _P, _L],
     "dx_g1j_on_curve": [_I, _P, _P, _P, _L],
+    "dx_rp_points_ni": [_P, _P, _P, _P, _P, _L, _I, _I],
+    "dx_rp_points_inl": [_P, _P, _P, _P, _P, _L, _I, _I],
     "dx_fold_steps_ni": [],
     "dx_rp_lines_ni": [_P, _P, _P, _P, _L],
     "dx_rp_accum_ni": [_P, _P, _P, _L, _I],
@@ -767,7 +769,25 @@ def rp_verify_fold(ZB_jac, Y_jac, rho, V_aff, S: int, L: int) -> torch.Tensor:
     return fb
 
 
-FOLD_VARIANT = os.environ.get("DRYNX_FOLD_VARIANT", "ni")  # ni: tower out of line, inl: force-inlined
+# inl: tower force-inlined into the fold kernels (12.4M Miller loops/s on one
+# MI355X vs 10.0M for ni, the out-of-line tower; tools/fold_bench.py)
+FOLD_VARIANT = os.environ.get("DRYNX_FOLD_VARIANT", "inl")
+
+
+def rp_fold_points(ZB_jac: torch.Tensor, Y_jac: torch.Tensor, rho: torch.Tensor, S: int, L: int,
+                   variant: str | None = None) -> torch.Tensor:
+    """GPU: P_it = affine(rho_it (ZB[p*L+j] - Y[p*S+i])), it = (p*S+i)*L + j,
+    one fused launch -> [n, 16] (n = rows of rho)."""
+    v = variant or FOLD_VARIANT
+    n = _rows(rho, 8)
+    assert _rows(ZB_jac, 24) * S == n and _rows(Y_jac, 24) * L == n and ZB_jac.is_cuda
+    P = torch.empty((n, 16), dtype=torch.int32, device=rho.device)
+    _, s = _ctx(ZB_jac, Y_jac, rho)
+    rc = getattr(_load(), f"dx_rp_points_{v}")(s, _ptr(ZB_jac.contiguous()), _ptr(Y_jac.contiguous()), _ptr(rho),
+                                                  _ptr(P), n, S, L)
+    if rc:
+        raise RuntimeError(f"dx_rp_points_{v} failed rc={rc}")
+    return P
 
 
 def rp_fold_lines(P_aff: torch.Tensor, V_aff: torch.Tensor, variant: str | None = None) -> torch.Tensor:

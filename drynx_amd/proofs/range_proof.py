@@ -687,11 +687,10 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
         dfull = torch.stack([nt.fr_dot_rows(w_all, r.zr, G, b_periodic=True),
                              nt.fr_dot_rows(w_all, z, G, b_periodic=True)], 1)             # [G, 2, 8]
     vns = [{"rho": rho_all[v * m:(v + 1) * m]} for v in range(G)]
-    T = _fold_points(ZB, Y, S, l)
     if device.type == "cuda":
         with timers.span("rp.verify.fold_queue"):
             for v in vns:                                              # Miller folds, back to back
-                v["fb"] = _miller_fold_T(T, v["rho"], r.V)
+                v["fb"] = _miller_fold(ZB, Y, v["rho"], r.V, S, l)
         with timers.span("rp.verify.multiexp"):
             aux.synchronize()
             GG = nt.multi_exp_grouped_finish(mexp)                     # [2G, 96]: prod a^rho_v, prod a^gamma_v
@@ -700,6 +699,7 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
                 v["F"] = nt._finish_prod_on_host(v["fb"])
     else:
         GG = nt.multi_exp_grouped_finish(mexp)
+        T = _fold_points(ZB, Y, S, l)
         for v in vns:
             f = nt.miller_loop(nt.g1_to_affine(nt.g1_mul(T, v["rho"])), r.V)
             v["F"] = nt.gt_prod(f.view(-1, 1, 96), chunk=4).view(1, 96)
@@ -743,16 +743,16 @@ def _fold_points(ZB, Y, S: int, L: int) -> torch.Tensor:
     return nt.g1_add(zb.contiguous(), yy.contiguous(), subtract=True)
 
 
-def _miller_fold_T(T, rho, V) -> torch.Tensor:
-    """GPU: per-workgroup partial products of ML(rho_it T_it, V_it).  Default:
-    the two-phase fold (csrc/kernels/fold_body.h) -- the G1 side as two wide
-    launches (64-bit variable-base multiplication, affine conversion), then
-    the line image and the K-item multi-Miller accumulation.
-    ``DRYNX_FOLD=fused`` selects the previous one-kernel fold."""
+def _miller_fold(ZB, Y, rho, V, S: int, L: int) -> torch.Tensor:
+    """GPU: per-workgroup partial products of ML(rho_it (ZB[p,j] - Y[p,i]), V_it).
+    Default: the two-phase fold (csrc/kernels/fold_body.h) -- one fused G1
+    launch (gather, difference, 64-bit multiplication, affine), the line
+    image, the K-item multi-Miller accumulation.  ``DRYNX_FOLD=fused``
+    selects the previous one-kernel fold."""
     n = V.shape[0]
     if os.environ.get("DRYNX_FOLD", "2") == "fused":
-        return nt.rp_verify_fold(T, bn.g1_infinity_jac(n, T.device), rho, V, 1, 1)
-    P = nt.g1_to_affine(nt.g1_mul(T, rho))
+        return nt.rp_verify_fold(ZB, Y, rho, V, S, L)
+    P = nt.rp_fold_points(ZB, Y, rho, S, L)
     K = next((k for k in (8, 4, 2) if (n + 64 * k - 1) // (64 * k) >= 1024), 1)
     return nt.rp_fold_accum(nt.rp_fold_lines(P, V), n, K)
 

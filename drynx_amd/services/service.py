@@ -114,25 +114,38 @@ class DrynxNode:
     # ------------------------------------------------------------------ VN storage
     def ledger_value(self, req):
         """What a VN stores for a proof request (storeProof,
-        proof_collection_protocol.go:318-331).  Range proofs: the reference
-        layout network.Marshal(&RangeProofListBytes) (proofs/range_wire.py),
-        encoded once per rank on the ledger thread and shared by the stores
-        of the co-hosted VNs; other kinds: their marshalled payload."""
-        if req.kind != "range" or req.header_only:
+        proof_collection_protocol.go:318-331): the signed payload.  A range
+        bundle's raw-limb tensor goes to the rank's shared blob segment once
+        (however many co-hosted VNs store it) through a pinned, asynchronous
+        device-to-host copy on the ledger's own stream; ``get_proofs`` serves
+        it in the reference RangeProofListBytes layout (proofs/range_wire.py)."""
+        if req.kind != "range" or req.header_only or req.tensor is None or req._data is not None:
             return req.payload()
+        if os.environ.get("DRYNX_LEDGER_RANGE", "on") == "off":  # A/B runs only
+            return b""
         if not hasattr(self, "_blobs"):
             from ..ledger.store import BlobSegment
 
             self._blobs = BlobSegment(os.path.join(self.workdir, f"ledger_r{self.rank}.blobs"), self.device)
+        t = req.tensor
+        if t.is_cuda:
+            if not hasattr(self, "_ledger_stream"):
+                self._ledger_stream = torch.cuda.Stream(self.device)
+            st = self._ledger_stream
+            st.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(st):
+                host = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+                host.copy_(t, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(st)
+            t.record_stream(st)
 
-        def produce():
-            from ..proofs import range_wire
-
-            try:
-                return range_wire.encode_bundle(prq._range_lists(req, self.device))
-            except Exception:  # undecodable payload: keep the bytes as received
-                return bytes(req.data)
-
+            def produce():
+                ev.synchronize()
+                return memoryview(host.numpy()).cast("B")
+        else:
+            def produce():
+                return memoryview(t.contiguous().numpy()).cast("B")
         return self._blobs.put(req.digest().hex(), produce)
 
     def store(self, vn_id: str) -> Store:
@@ -376,11 +389,22 @@ class DrynxNode:
         return SkipBlock.from_bytes(raw) if raw else None
 
     def get_proofs(self, vn_id: str, survey_id: str) -> dict:
+        """HandleGetProofs (service_skipchain.go:240-320): the VN's stored proofs;
+        range bundles in the reference layout network.Marshal(&RangeProofListBytes)."""
+        from ..proofs import range_wire
+
         st = self.store(vn_id)
         st.flush()
+        sq = self.surveys.get(survey_id)
         out = {}
         for kind in prq.VN_ORDER:
-            out.update(st.bucket(f"{survey_id}/{kind}"))
+            for k, v in st.bucket(f"{survey_id}/{kind}").items():
+                if kind == "range" and v:
+                    try:
+                        v = range_wire.encode_bundle(prq.range_bundle_from_bytes(v, "cpu"))
+                    except Exception:
+                        pass  # not a raw bundle (already reference bytes / malformed): as stored
+                out[k] = v
         return out
 
     def get_bitmap(self, vn_id: str, survey_id: str) -> dict:

@@ -307,3 +307,20 @@ def test_range_prover_layouts_gpu(gpu_device, bits, monkeypatch):
     assert all(rp.verify_range_proof_single_reference(rpl.to("cpu"), p, cpu_sm, P) for p in (0, 3))
     rpl.A[7, 5] ^= 1
     assert not rp.verify_range_proof_list(rpl, sm, P, 1.0, gpu_device)
+
+
+@pytest.mark.parametrize("variant", ["ni", "inl"])
+def test_fold_points_match_g1_ops(gpu_device, variant):
+    """Fused gather + difference + 64-bit multiplication + affine == the same
+    through the separate G1 launches (including Y = infinity rows)."""
+    S, L, npj = 3, 4, 5
+    ZB = nt.g1_fb_mul(bn.base_table(gpu_device), bn.random_scalars(npj * L, gpu_device))
+    Y = nt.g1_fb_mul(bn.base_table(gpu_device), bn.random_scalars(npj * S, gpu_device))
+    Y[2] = bn.g1_infinity_jac(1, gpu_device)[0]
+    rho = bn.random_scalars(npj * S * L, gpu_device)
+    rho[:, 2:] = 0
+    got = nt.rp_fold_points(ZB, Y, rho, S, L, variant)
+    zb = ZB.view(npj, 1, L, 24).expand(npj, S, L, 24).reshape(-1, 24).contiguous()
+    yy = Y.view(npj, S, 1, 24).expand(npj, S, L, 24).reshape(-1, 24).contiguous()
+    want = nt.g1_to_affine(nt.g1_mul(nt.g1_add(zb, yy, subtract=True), rho))
+    assert torch.equal(got, want)
