@@ -98,13 +98,18 @@ __device__ __forceinline__ void line_add(Fp2 &X, Fp2 &Y, Fp2 &Z, const Fp2 &x2, 
   Z = mul(Z, E);
 }
 
+// Items it < n; several verifiers' batches over the same V may share one
+// launch: item it pairs P[it] with V[it % period] (period = n for one batch;
+// rows of P past a batch's own length are the point at infinity).
 __global__ void __launch_bounds__(kWG) DX_OCC rp_lines_kernel(const uint32_t *__restrict__ P_aff,
                                                               const uint32_t *__restrict__ V_aff,
-                                                              uint4 *__restrict__ lines, int64_t n) {
+                                                              uint4 *__restrict__ lines, int64_t n,
+                                                              int64_t period, int64_t n_v) {
   const int64_t it = (int64_t)blockIdx.x * kWG + threadIdx.x;
   if (it >= n) return;
+  const int64_t q = it % period;
   const G1A P = at<G1A>(P_aff, it);
-  const G2A Q = at<G2A>(V_aff, it);
+  const G2A Q = at<G2A>(V_aff, q < n_v ? q : 0);
   if (P.is_inf() || Q.is_inf()) {  // ML = 1: identity lines
     for (int s = 0; s < kSteps; s++) store_line(lines, n, s, it, Fp2::one(), Fp2::zero(), Fp2::zero());
     return;
@@ -117,15 +122,15 @@ __global__ void __launch_bounds__(kWG) DX_OCC rp_lines_kernel(const uint32_t *__
     if (d != 0) {
       // re-read Q at each addition step instead of pinning 32 VGPRs for it
       asm volatile("" ::: "memory");
-      const G2A q = at<G2A>(V_aff, it);
-      line_add(X, Y, Z, q.x, d > 0 ? q.y : neg(q.y), P.x, P.y, lines, n, s++, it);
+      const G2A qq = at<G2A>(V_aff, q < n_v ? q : 0);
+      line_add(X, Y, Z, qq.x, d > 0 ? qq.y : neg(qq.y), P.x, P.y, lines, n, s++, it);
     }
   }
   asm volatile("" ::: "memory");
-  const G2A q = at<G2A>(V_aff, it);
-  line_add(X, Y, Z, mul(conj(q.x), Fp2::from_limbs(Frob::TWX1)), mul(conj(q.y), Fp2::from_limbs(Frob::TWY1)), P.x,
+  const G2A qq = at<G2A>(V_aff, q < n_v ? q : 0);
+  line_add(X, Y, Z, mul(conj(qq.x), Fp2::from_limbs(Frob::TWX1)), mul(conj(qq.y), Fp2::from_limbs(Frob::TWY1)), P.x,
            P.y, lines, n, s++, it);
-  line_add(X, Y, Z, mul(q.x, Fp2::from_limbs(Frob::TWX2)), neg(mul(q.y, Fp2::from_limbs(Frob::TWY2))), P.x, P.y,
+  line_add(X, Y, Z, mul(qq.x, Fp2::from_limbs(Frob::TWX2)), neg(mul(qq.y, Fp2::from_limbs(Frob::TWY2))), P.x, P.y,
            lines, n, s++, it);
 }
 
@@ -228,12 +233,13 @@ __global__ void __launch_bounds__(kWG) DX_OCC rp_accum_kernel(const uint4 *__res
 extern "C" {
 int FOLD_NAME(dx_fold_steps_)() { return FOLD_NAME(fold_ns_)::kSteps; }
 
-int FOLD_NAME(dx_rp_lines_)(void *stream, const uint32_t *P_aff, const uint32_t *V_aff, uint32_t *lines, int64_t n) {
+int FOLD_NAME(dx_rp_lines_)(void *stream, const uint32_t *P_aff, const uint32_t *V_aff, uint32_t *lines, int64_t n,
+                            int64_t period, int64_t n_v) {
   using namespace FOLD_NAME(fold_ns_);
-  if (n <= 0) return 0;
+  if (n <= 0 || period <= 0 || n_v <= 0 || n_v > period) return n <= 0 ? 0 : -2;
   const int64_t blocks = (n + kWG - 1) / kWG;
   hipLaunchKernelGGL(rp_lines_kernel, dim3((unsigned)blocks), dim3(kWG), 0, (hipStream_t)stream, P_aff, V_aff,
-                     reinterpret_cast<uint4 *>(lines), n);
+                     reinterpret_cast<uint4 *>(lines), n, period, n_v);
   return check_hip(hipGetLastError(), "rp_lines");
 }
 

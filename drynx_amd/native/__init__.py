@@ -108,10 +108,10 @@ _SIGS = {
     "dx_rp_points_ni": [_P, _P, _P, _P, _P, _L, _I, _I],
     "dx_rp_points_inl": [_P, _P, _P, _P, _P, _L, _I, _I],
     "dx_fold_steps_ni": [],
-    "dx_rp_lines_ni": [_P, _P, _P, _P, _L],
+    "dx_rp_lines_ni": [_P, _P, _P, _P, _L, _L, _L],
     "dx_rp_accum_ni": [_P, _P, _P, _L, _I],
     "dx_fold_steps_inl": [],
-    "dx_rp_lines_inl": [_P, _P, _P, _P, _L],
+    "dx_rp_lines_inl": [_P, _P, _P, _P, _L, _L, _L],
     "dx_rp_accum_inl": [_P, _P, _P, _L, _I],
     "dx_rp_verify_items": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _I],
 }
@@ -775,13 +775,14 @@ FOLD_VARIANT = os.environ.get("DRYNX_FOLD_VARIANT", "inl")
 
 
 def rp_fold_points(ZB_jac: torch.Tensor, Y_jac: torch.Tensor, rho: torch.Tensor, S: int, L: int,
-                   variant: str | None = None) -> torch.Tensor:
+                   variant: str | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
     """GPU: P_it = affine(rho_it (ZB[p*L+j] - Y[p*S+i])), it = (p*S+i)*L + j,
-    one fused launch -> [n, 16] (n = rows of rho)."""
+    one fused launch -> [n, 16] (n = rows of rho), or into ``out``."""
     v = variant or FOLD_VARIANT
     n = _rows(rho, 8)
     assert _rows(ZB_jac, 24) * S == n and _rows(Y_jac, 24) * L == n and ZB_jac.is_cuda
-    P = torch.empty((n, 16), dtype=torch.int32, device=rho.device)
+    P = out if out is not None else torch.empty((n, 16), dtype=torch.int32, device=rho.device)
+    assert P.shape == (n, 16) and P.is_contiguous()
     _, s = _ctx(ZB_jac, Y_jac, rho)
     rc = getattr(_load(), f"dx_rp_points_{v}")(s, _ptr(ZB_jac.contiguous()), _ptr(Y_jac.contiguous()), _ptr(rho),
                                                   _ptr(P), n, S, L)
@@ -790,17 +791,22 @@ def rp_fold_points(ZB_jac: torch.Tensor, Y_jac: torch.Tensor, rho: torch.Tensor,
     return P
 
 
-def rp_fold_lines(P_aff: torch.Tensor, V_aff: torch.Tensor, variant: str | None = None) -> torch.Tensor:
+def rp_fold_lines(P_aff: torch.Tensor, V_aff: torch.Tensor, variant: str | None = None,
+                  period: int | None = None) -> torch.Tensor:
     """Phase 1 of the two-phase Miller fold (GPU): the sparse line values of
     every item's Miller loop evaluated at its P -> flat int32 image
-    [steps * 12 * n * 4] (csrc/kernels/fold_body.h)."""
+    [steps * 12 * n * 4] (csrc/kernels/fold_body.h).  ``period``: item it
+    pairs P[it] with V[it % period] (several verifiers' batches, each padded
+    to ``period`` rows, in one launch)."""
     v = variant or FOLD_VARIANT
     n = _rows(P_aff, 16)
-    assert _rows(V_aff, 32) == n and P_aff.is_cuda
+    nv = _rows(V_aff, 32)
+    period = period or n
+    assert nv <= period and n % period == 0 and P_aff.is_cuda
     steps = getattr(_load(), f"dx_fold_steps_{v}")()
     lines = torch.empty((steps * 12 * n * 4,), dtype=torch.int32, device=P_aff.device)
     _, s = _ctx(P_aff, V_aff)
-    rc = getattr(_load(), f"dx_rp_lines_{v}")(s, _ptr(P_aff), _ptr(V_aff), _ptr(lines), n)
+    rc = getattr(_load(), f"dx_rp_lines_{v}")(s, _ptr(P_aff), _ptr(V_aff), _ptr(lines), n, period, nv)
     if rc:
         raise RuntimeError(f"dx_rp_lines_{v} failed rc={rc}")
     return lines
@@ -858,6 +864,30 @@ def _multi_exp64_plan(rho: torch.Tensor):
     return _bucket_plan(rho, _ME_W)
 
 
+def _segment_passes_dev(counts, dev):
+    """``_segment_passes`` with the per-slice (start, len) arrays built on the
+    device: only the per-bucket counts (at most a few thousand) live on the
+    host, the millions of slice descriptors of a wide multi-exponentiation
+    never cross PCIe and never run through numpy."""
+    import numpy as _np
+
+    passes = []
+    c = _np.asarray(counts, dtype=_np.int64)
+    while c.size and c.max() > 1:
+        n_sl = (c + _ME_SLICE - 1) // _ME_SLICE
+        total = int(n_sl.sum())
+        ct = torch.from_numpy(c).to(dev)
+        nt_ = torch.from_numpy(n_sl).to(dev)
+        first = torch.cumsum(ct, 0) - ct
+        b = torch.repeat_interleave(torch.arange(c.size, device=dev), nt_, output_size=total)
+        k = torch.arange(total, device=dev) - (torch.cumsum(nt_, 0) - nt_)[b]
+        start = first[b] + k * _ME_SLICE
+        ln = torch.minimum(ct[b] - k * _ME_SLICE, torch.full_like(k, _ME_SLICE)).to(torch.int32)
+        passes.append((start.contiguous(), ln.contiguous()))
+        c = n_sl
+    return passes
+
+
 def _bucket_plan(k: torch.Tensor, W: int, group: torch.Tensor | None = None, n_groups: int = 1):
     """Bucket plan of a multi-scalar product over the low W bytes of the
     scalars k [n, 8]: window w, digit d -> bucket w*256+d (plus g*W*256 for
@@ -877,8 +907,7 @@ def _bucket_plan(k: torch.Tensor, W: int, group: torch.Tensor | None = None, n_g
     item = item[order].contiguous()
     counts = torch.bincount(keys, minlength=W * 256 * n_groups).cpu().numpy()  # the one host sync
     bk = counts.nonzero()[0]
-    passes = [(torch.from_numpy(st).to(dev), torch.from_numpy(ln.astype("int32")).to(dev))
-              for st, ln in _segment_passes(counts[bk])]
+    passes = _segment_passes_dev(counts[bk], dev)
     # bucket digits and scatter slots, staged now so the run needs no host->device copy
     sc = torch.zeros((bk.size, 8), dtype=torch.int32)
     sc[:, 0] = torch.from_numpy((bk % 256).astype("int32"))

@@ -43,9 +43,11 @@ class Comm:
     def all_gather_object(self, obj) -> list:
         return [obj]
 
-    def exchange(self, outgoing: dict) -> dict:
+    def exchange(self, outgoing: dict, recv_sizes: dict | None = None) -> dict:
         """outgoing: dst_rank -> int32 tensor (any shape, on self.device).
-        Returns src_rank -> flat int32 tensor received (only non-empty ones)."""
+        Returns src_rank -> flat int32 tensor received (only non-empty ones).
+        ``recv_sizes`` (src -> numel), when the protocol already knows them,
+        saves the size round (and its host synchronisation)."""
         return {self.rank: outgoing[self.rank].reshape(-1)} if self.rank in outgoing else {}
 
     def send(self, t: torch.Tensor, dst: int):
@@ -117,17 +119,23 @@ class DistComm(Comm):
         dist.all_gather_object(out, obj, group=self._ctrl)
         return out
 
-    def exchange(self, outgoing: dict) -> dict:
+    def exchange(self, outgoing: dict, recv_sizes: dict | None = None) -> dict:
         W = self.world
         flat = {d: t.reshape(-1).to(torch.int32) for d, t in outgoing.items()}
         sizes = torch.zeros(W, dtype=torch.int64)
         for d, t in flat.items():
             sizes[d] = t.numel()
         if self.backend == "nccl":
-            send_sizes = sizes.to(self.device)
-            recv_sizes = torch.empty_like(send_sizes)
-            dist.all_to_all_single(recv_sizes, send_sizes)
-            recv_sizes = recv_sizes.cpu()
+            if recv_sizes is not None:
+                known = recv_sizes
+                recv_sizes = torch.zeros(W, dtype=torch.int64)
+                for s_, n_ in known.items():
+                    recv_sizes[s_] = int(n_)
+            else:
+                send_sizes = sizes.to(self.device)
+                rs = torch.empty_like(send_sizes)
+                dist.all_to_all_single(rs, send_sizes)
+                recv_sizes = rs.cpu()
             send = torch.cat([flat.get(d, torch.empty(0, dtype=torch.int32, device=self.device)) for d in range(W)])
             if send.numel() == 0:
                 send = torch.empty(0, dtype=torch.int32, device=self.device)

@@ -40,25 +40,25 @@ def rows_to_cv(rows: torch.Tensor) -> CipherVector:
 def route(comm: Comm, items: list, key_index) -> dict:
     """items: list of (dst_rank, key, CipherVector).  Returns {key: CipherVector}
     of the items addressed to this rank.  ``key_index``: key -> int and back
-    (a ``KeyIndex``) shared by all ranks."""
+    (a ``KeyIndex``) shared by all ranks.  Per destination the buffer is
+    [count, key_0, n_0, key_1, n_1, ..., rows_0, rows_1, ...]: the receiver
+    copies only the 1 + 2 count header words to the host."""
     per_dst: dict = {}
     for dst, key, cv in items:
-        hdr = torch.tensor([key_index.encode(key), len(cv)], dtype=torch.int32, device=comm.device)
-        per_dst.setdefault(dst, []).append(torch.cat([hdr, cv_to_rows(cv).to(comm.device).reshape(-1)]))
+        per_dst.setdefault(dst, []).append((key_index.encode(key), len(cv), cv_to_rows(cv).to(comm.device).reshape(-1)))
     outgoing = {}
     for dst, parts in per_dst.items():
-        cnt = torch.tensor([len(parts)], dtype=torch.int32, device=comm.device)
-        outgoing[dst] = torch.cat([cnt] + parts)
+        hdr = [len(parts)] + [v for k, n, _ in parts for v in (k, n)]
+        outgoing[dst] = torch.cat([torch.tensor(hdr, dtype=torch.int32).to(comm.device)] + [r for _, _, r in parts])
     got = comm.exchange(outgoing)
     out = {}
     for src in sorted(got):
         buf = got[src]
-        hdr_all = buf.cpu() if buf.is_cuda else buf
-        n_items = int(hdr_all[0])
-        off = 1
-        for _ in range(n_items):
-            k, n = int(hdr_all[off]), int(hdr_all[off + 1])
-            off += 2
+        n_items = int(buf[0])
+        hdr = buf[1: 1 + 2 * n_items].cpu().tolist()
+        off = 1 + 2 * n_items
+        for q in range(n_items):
+            k, n = hdr[2 * q], hdr[2 * q + 1]
             out[key_index.decode(k)] = rows_to_cv(buf[off: off + n * ROW])
             off += n * ROW
     return out

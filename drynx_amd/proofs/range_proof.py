@@ -689,8 +689,8 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
     vns = [{"rho": rho_all[v * m:(v + 1) * m]} for v in range(G)]
     if device.type == "cuda":
         with timers.span("rp.verify.fold_queue"):
-            for v in vns:                                              # Miller folds, back to back
-                v["fb"] = _miller_fold(ZB, Y, v["rho"], r.V, S, l)
+            for v, fb in zip(vns, _miller_fold_multi(ZB, Y, [v["rho"] for v in vns], r.V, S, l)):
+                v["fb"] = fb
         with timers.span("rp.verify.multiexp"):
             aux.synchronize()
             GG = nt.multi_exp_grouped_finish(mexp)                     # [2G, 96]: prod a^rho_v, prod a^gamma_v
@@ -743,18 +743,42 @@ def _fold_points(ZB, Y, S: int, L: int) -> torch.Tensor:
     return nt.g1_add(zb.contiguous(), yy.contiguous(), subtract=True)
 
 
-def _miller_fold(ZB, Y, rho, V, S: int, L: int) -> torch.Tensor:
-    """GPU: per-workgroup partial products of ML(rho_it (ZB[p,j] - Y[p,i]), V_it).
-    Default: the two-phase fold (csrc/kernels/fold_body.h) -- one fused G1
-    launch (gather, difference, 64-bit multiplication, affine), the line
-    image, the K-item multi-Miller accumulation.  ``DRYNX_FOLD=fused``
-    selects the previous one-kernel fold."""
-    n = V.shape[0]
+def fold_k(n_items: int, slots: int = 2048) -> int:
+    """Items per lane of the multi-Miller accumulation: a workgroup's time is
+    ~ (12 + 13 K) Fp2 products per loop step (one shared squaring, K sparse
+    line products) and up to ``slots`` workgroups (2 waves on each of the
+    1024 SIMDs) run per round -> minimise rounds x (12 + 13 K)."""
+    best, best_k = None, 1
+    for k in (1, 2, 4, 8):
+        wgs = -(-n_items // (64 * k))
+        cost = -(-wgs // slots) * (12 + 13 * k)
+        if best is None or cost < best:
+            best, best_k = cost, k
+    return best_k
+
+
+def _miller_fold_multi(ZB, Y, rhos: list, V, S: int, L: int) -> list:
+    """GPU: for each verifier's weights rho_v, per-workgroup partial products
+    of ML(rho_it (ZB[p,j] - Y[p,i]), V_it).  The two-phase fold
+    (csrc/kernels/fold_body.h) over ALL verifiers at once: one fused G1
+    launch per verifier (gather, difference, 64-bit multiplication, affine)
+    into a shared point image whose per-verifier blocks are padded to whole
+    workgroups, then ONE line-image launch and ONE K-item accumulation (a
+    verifier's slice of a multi-GPU node is too short to fill the chip on
+    its own).  ``DRYNX_FOLD=fused`` selects the previous one-kernel fold."""
+    m = V.shape[0]
+    G = len(rhos)
     if os.environ.get("DRYNX_FOLD", "2") == "fused":
-        return nt.rp_verify_fold(ZB, Y, rho, V, S, L)
-    P = nt.rp_fold_points(ZB, Y, rho, S, L)
-    K = next((k for k in (8, 4, 2) if (n + 64 * k - 1) // (64 * k) >= 1024), 1)
-    return nt.rp_fold_accum(nt.rp_fold_lines(P, V), n, K)
+        return [nt.rp_verify_fold(ZB, Y, rho, V, S, L) for rho in rhos]
+    K = fold_k(G * m)
+    per = 64 * K
+    pad = -(-m // per) * per
+    P = torch.zeros((G * pad, 16), dtype=torch.int32, device=V.device)
+    for v, rho in enumerate(rhos):
+        nt.rp_fold_points(ZB, Y, rho, S, L, out=P[v * pad: v * pad + m])
+    fb = nt.rp_fold_accum(nt.rp_fold_lines(P, V, period=pad), G * pad, K)
+    blk = pad // per
+    return [fb[v * blk:(v + 1) * blk] for v in range(G)]
 
 
 _aux: dict = {}

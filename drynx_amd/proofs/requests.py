@@ -406,13 +406,15 @@ _SIG_BATCH_MIN = 16  # inboxes at least this long check their envelope signature
 
 
 def verify_requests(reqs: list, sq, vn_id: str, vn_index: int, n_vns: int, device, cache: VerifierCache,
-                    range_pooled: dict | None = None) -> list:
+                    range_pooled=None, defer: bool = False):
     """VerifyProof for a VN's whole inbox.  Signatures and sampling per request;
     the content of the short per-CN proofs (key switch, obfuscation) is verified
     in one batched launch per kind; range proofs are already one batch each.
     ``range_pooled``: {base_key: None (not sampled) | bool} -- this VN's range
     results from the pooled verification (``pool_sampling`` decided the
-    sampling on this VN's rank beforehand)."""
+    sampling on this VN's rank beforehand; a dict or a Future of one).
+    ``defer``: return a callable that waits for the pooled range results and
+    returns the codes (everything else is already checked)."""
     codes = [None] * len(reqs)
     todo: dict = {}
     pooled_idx: list = []
@@ -491,14 +493,17 @@ def verify_requests(reqs: list, sq, vn_id: str, vn_index: int, n_vns: int, devic
         with timers.span("rp.verify.early_wait"):
             for i, (fut, j) in early.items():
                 codes[i] = PROOF_TRUE if fut.result()[j] else PROOF_FALSE
-    if pooled_idx:
-        with timers.span("rp.verify.pooled_wait"):
-            pooled = range_pooled.result() if hasattr(range_pooled, "result") else range_pooled
-            pooled = pooled.get(vn_id, {}) if vn_id in pooled else pooled
-        for i in pooled_idx:
-            res = pooled.get(reqs[i].base_key(), False)
-            codes[i] = PROOF_RECEIVED if res is None else (PROOF_TRUE if res else PROOF_FALSE)
-    return codes
+    def resolve():
+        if pooled_idx:
+            with timers.span("rp.verify.pooled_wait"):
+                pooled = range_pooled.result() if hasattr(range_pooled, "result") else range_pooled
+                pooled = pooled.get(vn_id, {}) if vn_id in pooled else pooled
+            for i in pooled_idx:
+                res = pooled.get(reqs[i].base_key(), False)
+                codes[i] = PROOF_RECEIVED if res is None else (PROOF_TRUE if res else PROOF_FALSE)
+        return codes
+
+    return resolve if defer else resolve()
 
 
 class _EarlyReq:

@@ -78,15 +78,18 @@ def fan_out(ctx, sq, local_requests: list, all_ranks: bool = False) -> list:
             else:
                 per_rank[d].append(r.to_wire())
     got = ctx.comm.exchange_bytes({d: obj_to_bytes(per_rank[d]) for d in vn_ranks})
+    wires = {src: bytes_to_obj(b) for src, b in got.items()}
     tens = {d: torch.cat(per_rank_t[d]) for d in vn_ranks if per_rank_t[d]}
-    got_t = ctx.comm.exchange(tens)
+    # the envelopes announced every tensor's size: no size round for the payloads
+    sizes = {src: sum(w.get("tensor") or 0 for w in ws) for src, ws in wires.items() if src != ctx.rank}
+    got_t = ctx.comm.exchange(tens, recv_sizes={s_: n_ for s_, n_ in sizes.items() if n_})
     out = []
     for src in sorted(got):
         if src == ctx.rank:
             out += list(local_requests)  # keep decoded objects for locally produced proofs
             continue
         off = 0
-        for w in bytes_to_obj(got[src]):
+        for w in wires[src]:
             req = prq.ProofRequest.from_wire(w)
             n = w.get("tensor")
             if n:
@@ -155,10 +158,25 @@ def _pool_async(ctx, sq, reqs, vns):
 
 
 def verify_and_store(ctx, sq, vn, vn_index: int, n_vns: int, requests: list, range_pooled=None) -> dict:
+    return store_verdicts(ctx, sq, vn, requests, check_requests(ctx, sq, vn, vn_index, n_vns, requests, range_pooled))
+
+
+def check_requests(ctx, sq, vn, vn_index: int, n_vns: int, requests: list, range_pooled=None):
+    """VerifyProof over one VN's inbox; with pooled range checks the range
+    codes are left pending (``codes`` holds a resolver) so the VN's short
+    per-CN checks run while the pooled batch is still on the GPU."""
+    return prq.verify_requests(requests, sq, vn.id, vn_index, n_vns, ctx.device, ctx.verifier_cache, range_pooled,
+                               defer=True)
+
+
+def store_verdicts(ctx, sq, vn, requests: list, pending) -> dict:
+    """storeProof for every request of the inbox: bitmap entry, ledger write
+    (surveyID/type bucket, shuffle proofs not stored), expected-count check
+    and the VN's bitmap (proof_collection_protocol.go:307-406)."""
+    codes = pending() if callable(pending) else pending
     store = ctx.store(vn.id)
     bitmap = {}
     counts = {k: 0 for k in prq.VN_ORDER}
-    codes = prq.verify_requests(requests, sq, vn.id, vn_index, n_vns, ctx.device, ctx.verifier_cache, range_pooled)
     for req, code in zip(requests, codes):
         key = req.key(vn.id)
         bitmap[key] = code
@@ -183,9 +201,11 @@ def proof_collection(ctx, sq, local_requests: list):
     bitmaps = {}
     with timers.timed("ProofVerification"):
         pooled = _pool_async(ctx, sq, reqs, vns) if pool else None
-        for idx, vn in enumerate(vns):
-            if vn.rank == ctx.rank:
-                bitmaps[vn.id] = verify_and_store(ctx, sq, vn, idx, len(vns), reqs, pooled)
+        pending = {vn.id: check_requests(ctx, sq, vn, idx, len(vns), reqs, pooled)
+                   for idx, vn in enumerate(vns) if vn.rank == ctx.rank}
+        for vn in vns:
+            if vn.id in pending:
+                bitmaps[vn.id] = store_verdicts(ctx, sq, vn, reqs, pending[vn.id])
         if pooled is not None:
             pooled.result()
     # bitmaps -> root VN (SharedBMChannel)

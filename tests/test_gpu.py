@@ -324,3 +324,23 @@ def test_fold_points_match_g1_ops(gpu_device, variant):
     yy = Y.view(npj, S, 1, 24).expand(npj, S, L, 24).reshape(-1, 24).contiguous()
     want = nt.g1_to_affine(nt.g1_mul(nt.g1_add(zb, yy, subtract=True), rho))
     assert torch.equal(got, want)
+
+
+def test_merged_multi_verifier_fold(gpu_device):
+    """Several verifiers' folds in one padded line image / accumulation ==
+    each verifier's fold on its own (after the final exponentiation)."""
+    from drynx_amd.proofs import range_proof as rp
+
+    S, L, npj = 3, 4, 7
+    ZB = nt.g1_fb_mul(bn.base_table(gpu_device), bn.random_scalars(npj * L, gpu_device))
+    Y = nt.g1_fb_mul(bn.base_table(gpu_device), bn.random_scalars(npj * S, gpu_device))
+    m = npj * S * L
+    V = nt.g2_fb_mul(bn.base2_table(gpu_device), bn.random_scalars(m, gpu_device))
+    rhos = [rp._rand64(m, gpu_device) for _ in range(3)]
+    merged = rp._miller_fold_multi(ZB, Y, rhos, V, S, L)
+    for rho, fb in zip(rhos, merged):
+        P = nt.rp_fold_points(ZB, Y, rho, S, L)
+        alone = nt.rp_fold_accum(nt.rp_fold_lines(P, V), m, 1)
+        a = nt.final_exp(nt._finish_prod_on_host(fb))
+        b = nt.final_exp(nt._finish_prod_on_host(alone))
+        assert bool(nt.gt_eq(a, b).all())
