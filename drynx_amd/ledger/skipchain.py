@@ -11,10 +11,18 @@ VN's own DB.
 Here a block is hash-linked (SHA-256 over index, back link, roster and data)
 and carries a BLS collective signature of the VN roster over the block hash
 (BDN aggregation, crypto/bls.py, like cothority's BLS CoSi): each VN adds its
-partial signature only after its bitmap verifier accepted the block; the
-aggregate and the participation mask are stored in ``CoSig`` and checked with
-one pairing product.  Roster entries without a BLS key fall back to per-VN
-Schnorr signatures.
+partial signature only after its verifiers accepted the block -- the bitmap
+check (verifyFuncBitmap) and the structural check ``verify_base`` (cothority
+skipchain.VerifyBase: index, back link, genesis id, hash); the aggregate and
+the participation mask are stored in ``CoSig`` and checked with one pairing
+product.  The chain is created like ``CreateGenesis(roster, 1, 1, ...)``
+(service_skipchain.go:500): base 1, height 1, so every block has one back
+link and one forward link.  The forward link of block k is signed by block
+k's roster over (hash_k, hash_k+1) when block k+1 is appended and is stored
+with block k (outside its hash, as in cothority); ``update_chain`` walks and
+verifies them from any known block to the latest (GetUpdateChain,
+service_skipchain.go:195-205, 498-525).  Roster entries without a BLS key
+fall back to per-VN Schnorr signatures.
 """
 from __future__ import annotations
 
@@ -64,6 +72,7 @@ class SkipBlock:
     ForwardSignatures: dict = field(default_factory=dict)  # vn id -> partial signature hex
     GenesisID: str = ""
     CoSig: str = ""              # "<aggregate G1 hex>/<mask>" (BLS collective signature)
+    ForwardLinks: list = field(default_factory=list)  # [{"To": hash, "CoSig": ..., "Sigs": {...}}]
 
     def compute_hash(self) -> str:
         h = hashlib.sha256()
@@ -98,25 +107,31 @@ class SkipBlock:
         ceil(threshold * n) signers; default: every VN of the roster)."""
         if self.compute_hash() != self.Hash:
             return False
-        keys = self.bls_keys()
-        if keys is not None:
-            if not self.CoSig:
-                return False
-            agg_hex, mask_hex = self.CoSig.split("/")
-            mask = bls.mask_from_hex(mask_hex)
-            if len(mask) != len(keys) or sum(mask) < math.ceil(threshold * len(keys)):
-                return False
-            try:
-                sig = O.g1_from_bytes(bytes.fromhex(agg_hex))
-            except ValueError:
-                return False
-            return bls.verify_multi(keys, mask, bytes.fromhex(self.Hash), sig)
-        for vn in self.Roster:
-            sig = self.ForwardSignatures.get(vn["id"])
-            if sig is None or publics is None or \
-                    not schnorr_verify(publics[vn["id"]], bytes.fromhex(self.Hash), bytes.fromhex(sig)):
-                return False
-        return True
+        return _verify_cosig(self, self.CoSig, self.ForwardSignatures, bytes.fromhex(self.Hash), publics, threshold)
+
+
+def _verify_cosig(sb: "SkipBlock", cosig: str, sigs: dict, msg: bytes, publics=None, threshold: float = 1.0) -> bool:
+    """A collective signature of ``sb``'s roster over ``msg``: the BLS
+    aggregate (at least ceil(threshold * n) signers in the mask), or one
+    Schnorr signature per roster member when the roster has no BLS keys."""
+    keys = sb.bls_keys()
+    if keys is not None:
+        if not cosig:
+            return False
+        agg_hex, mask_hex = cosig.split("/")
+        mask = bls.mask_from_hex(mask_hex)
+        if len(mask) != len(keys) or sum(mask) < math.ceil(threshold * len(keys)):
+            return False
+        try:
+            sig = O.g1_from_bytes(bytes.fromhex(agg_hex))
+        except ValueError:
+            return False
+        return bls.verify_multi(keys, mask, msg, sig)
+    for vn in sb.Roster:
+        sig = sigs.get(vn["id"])
+        if sig is None or publics is None or not schnorr_verify(publics[vn["id"]], msg, bytes.fromhex(sig)):
+            return False
+    return True
 
 
 def roster_json(identities) -> list:
@@ -174,3 +189,74 @@ def finalize_cosig(sb: SkipBlock):
             partials[i] = O.g1_from_bytes(bytes.fromhex(s))
     agg = bls.aggregate(keys, partials)
     sb.CoSig = (O.g1_to_bytes(agg).hex() if agg is not None else "") + "/" + bls.mask_to_hex(mask)
+
+
+# ----------------------------------------------------------------------------- structure and forward links
+def verify_base(prev: SkipBlock | None, sb: SkipBlock) -> bool:
+    """skipchain.VerifyBase: the block is well formed and extends ``prev``
+    (index, back link, genesis id, hash, verifier list); ``prev`` None: a
+    genesis block."""
+    if sb.compute_hash() != sb.Hash or not sb.Roster or VERIFY_BASE not in sb.VerifierIDs:
+        return False
+    if prev is None:
+        return sb.Index == 0 and sb.BackLink == "" and sb.GenesisID == sb.Hash
+    return (sb.Index == prev.Index + 1 and sb.BackLink == prev.Hash
+            and sb.GenesisID == (prev.GenesisID or prev.Hash))
+
+
+def forward_link_message(frm: str, to: str) -> bytes:
+    return hashlib.sha256(b"drynx_amd/skipchain/forward-link/v1" + bytes.fromhex(frm) + bytes.fromhex(to)).digest()
+
+
+def sign_forward_link(prev: SkipBlock, to_hash: str, secret: int) -> str:
+    """A member of ``prev``'s roster signs the link prev -> to (BLS partial,
+    Schnorr when the roster has no BLS keys)."""
+    msg = forward_link_message(prev.Hash, to_hash)
+    if prev.bls_keys() is not None:
+        return O.g1_to_bytes(bls.sign(secret, msg)).hex()
+    return schnorr_sign(secret, msg).hex()
+
+
+def add_forward_link(prev: SkipBlock, to_hash: str, partials: dict):
+    """Aggregate the roster's partial signatures into prev's forward link."""
+    link = {"To": to_hash, "CoSig": "", "Sigs": {}}
+    keys = prev.bls_keys()
+    if keys is None:
+        link["Sigs"] = dict(partials)
+    else:
+        mask, parts = [], {}
+        for i, vn in enumerate(prev.Roster):
+            p = partials.get(vn["id"])
+            mask.append(p is not None)
+            if p is not None:
+                parts[i] = O.g1_from_bytes(bytes.fromhex(p))
+        agg = bls.aggregate(keys, parts)
+        link["CoSig"] = (O.g1_to_bytes(agg).hex() if agg is not None else "") + "/" + bls.mask_to_hex(mask)
+    prev.ForwardLinks = [lk for lk in prev.ForwardLinks if lk["To"] != to_hash] + [link]
+
+
+def verify_forward_link(prev: SkipBlock, link: dict, publics: dict | None = None, threshold: float = 1.0) -> bool:
+    return _verify_cosig(prev, link.get("CoSig", ""), link.get("Sigs", {}), forward_link_message(prev.Hash, link["To"]),
+                         publics, threshold)
+
+
+def update_chain(get_block, start: SkipBlock, publics: dict | None = None) -> list:
+    """GetUpdateChain: from ``start`` follow the (verified) forward links to the
+    latest block; every hop checks the link's collective signature, the next
+    block's structure (verify_base) and its own collective signature.
+    ``get_block(hash)`` -> SkipBlock | None.  Raises ValueError on a bad hop."""
+    chain = [start]
+    seen = {start.Hash}
+    while chain[-1].ForwardLinks:
+        cur = chain[-1]
+        link = cur.ForwardLinks[-1]
+        if not verify_forward_link(cur, link, publics):
+            raise ValueError(f"bad forward link from block {cur.Index}")
+        nxt = get_block(link["To"])
+        if nxt is None or nxt.Hash in seen:
+            raise ValueError(f"forward link from block {cur.Index} leads nowhere")
+        if not verify_base(cur, nxt) or not nxt.verify_signatures(publics):
+            raise ValueError(f"block {nxt.Index} does not extend block {cur.Index}")
+        seen.add(nxt.Hash)
+        chain.append(nxt)
+    return chain

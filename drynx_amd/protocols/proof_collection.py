@@ -227,23 +227,34 @@ def proof_collection(ctx, sq, local_requests: list):
         block = skc.make_block(ctx.last_block, data, [v.identity() for v in vns])
     block_bytes = ctx.comm.broadcast_object(block.to_bytes() if block is not None else None, src=root.rank)
     block = skc.SkipBlock.from_bytes(block_bytes)
-    # every VN runs the bitmap verifier (verifyFuncBitmap) and signs the forward link
-    sigs = {}
+    # every VN runs its verifiers (verifyFuncBitmap, VerifyBase against its own
+    # latest block), then signs the block and the forward link from its latest
+    sigs, links = {}, {}
     for vn in vns:
         if vn.rank == ctx.rank:
-            if skc.verify_bitmap(block, ctx.local_bitmaps.get((sq.SurveyID, vn.id), {}), vn.id):
+            prev = ctx.vn_latest(vn.id)
+            if skc.verify_bitmap(block, ctx.local_bitmaps.get((sq.SurveyID, vn.id), {}), vn.id) \
+                    and skc.verify_base(prev, block):
                 skc.sign_block(block, vn.id, vn.keypair.secret)
                 sigs[vn.id] = block.ForwardSignatures[vn.id]
+                if prev is not None:
+                    links[vn.id] = skc.sign_forward_link(prev, block.Hash, vn.keypair.secret)
             else:
                 log.warning(f"{vn.id} refused block for survey {sq.SurveyID}")
-    for d in ctx.comm.all_gather_object(sigs):
+    for d, fl in ctx.comm.all_gather_object((sigs, links)):
         block.ForwardSignatures.update(d)
+        links.update(fl)
     skc.finalize_cosig(block)  # BLS collective signature of the VN roster
     for vn in vns:
         if vn.rank == ctx.rank:
             # proof blobs keep persisting on the store's writer thread (GetProofs /
             # CloseDB flush); the block only depends on the bitmap
             st = ctx.store(vn.id)
+            prev = ctx.vn_latest(vn.id)
+            if prev is not None and links:
+                skc.add_forward_link(prev, block.Hash, links)   # stored with the previous block
+                st.update_async("skipchain", prev.Hash, prev.to_bytes())
+            ctx.set_vn_latest(vn.id, block)
             raw = block.to_bytes()
             st.update_async("skipchain", block.Hash, raw)
             st.update_async("skipchain", "latest", raw)

@@ -103,8 +103,10 @@ class DrynxClient:
         None on timeout.  Callable before or while the survey runs."""
         return self.entry.wait_end_verification(survey_id, timeout)
 
-    def send_get_latest_block(self, vn_id: str):
-        return self.entry.get_latest_block(vn_id)
+    def send_get_latest_block(self, vn_id: str, sb=None):
+        """SendGetLatestBlock (api_skipchain.go:44): the VN's head, or -- given a
+        known block ``sb`` -- the end of the verified update chain from it."""
+        return self.entry.get_latest_block(vn_id, sb) if sb is not None else self.entry.get_latest_block(vn_id)
 
     def send_get_genesis(self, vn_id: str):
         return self.entry.get_genesis(vn_id)

@@ -386,7 +386,8 @@ class NodeServer:
             if name == "libdrynx.GetGenesis":
                 out = _reply_block(node.get_genesis(vn))
             elif name == "libdrynx.GetLatestBlock":
-                out = _reply_block(node.get_latest_block(vn))
+                sb = SkipBlock.from_bytes(d["Sb"]) if d["Sb"] else None
+                out = _reply_block(node.get_latest_block(vn, sb))
             elif name == "libdrynx.GetBlock":
                 out = _reply_block(node.get_block(vn, d["ID"]))
             elif name == "libdrynx.GetProofs":
@@ -464,8 +465,8 @@ class RemoteNode:
     def get_genesis(self, vn):
         return self._block("libdrynx.GetGenesis", {"VN": vn})
 
-    def get_latest_block(self, vn):
-        return self._block("libdrynx.GetLatestBlock", {"VN": vn})
+    def get_latest_block(self, vn, sb=None):
+        return self._block("libdrynx.GetLatestBlock", {"VN": vn, "Sb": sb.to_bytes() if sb is not None else b""})
 
     def get_block(self, vn, survey_id):
         return self._block("libdrynx.GetBlock", {"VN": vn, "ID": survey_id})

@@ -26,6 +26,7 @@ import torch
 
 from ..crypto.elgamal import CipherVector
 from ..ledger.skipchain import SkipBlock
+from ..ledger.skipchain import update_chain as skc_update_chain
 from ..ops.encoding import cat_proof_batches as dcp_batch_cat
 from ..ledger.store import Store
 from ..parallel.comm import Comm, LocalComm
@@ -376,9 +377,41 @@ class DrynxNode:
         raw = self.store(vn_id).get("genesis", "genesis")
         return SkipBlock.from_bytes(raw) if raw else None
 
-    def get_latest_block(self, vn_id: str):
+    def vn_latest(self, vn_id: str):
+        """The VN's own latest block (its chain head), cached in memory."""
+        if not hasattr(self, "_vn_latest"):
+            self._vn_latest = {}
+        if vn_id not in self._vn_latest:
+            raw = self.store(vn_id).get("skipchain", "latest")
+            self._vn_latest[vn_id] = SkipBlock.from_bytes(raw) if raw else None
+        return self._vn_latest[vn_id]
+
+    def set_vn_latest(self, vn_id: str, block: SkipBlock):
+        if not hasattr(self, "_vn_latest"):
+            self._vn_latest = {}
+        self._vn_latest[vn_id] = block
+
+    def get_latest_block(self, vn_id: str, from_block: SkipBlock | None = None):
+        """GetLatestBlock (service_skipchain.go:195-205): without ``from_block``
+        the VN's head; with it, the last block of the update chain walked and
+        verified from ``from_block`` through the forward links (GetUpdateChain)."""
+        if from_block is not None:
+            return self.get_update_chain(vn_id, from_block)[-1]
         raw = self.store(vn_id).get("skipchain", "latest")
         return SkipBlock.from_bytes(raw) if raw else None
+
+    def get_update_chain(self, vn_id: str, from_block: SkipBlock) -> list:
+        """GetUpdateChain from ``from_block`` (re-read from this VN's ledger, so
+        its forward links are the current ones) to the head."""
+        st = self.store(vn_id)
+
+        def get(h):
+            raw = st.get("skipchain", h)
+            return SkipBlock.from_bytes(raw) if raw else None
+
+        start = get(from_block.Hash) or from_block
+        publics = {p.id: p.public for p in self.cluster.vns}
+        return skc_update_chain(get, start, publics)
 
     def get_block(self, vn_id: str, survey_id: str):
         st = self.store(vn_id)

@@ -245,3 +245,38 @@ def test_get_proofs_reference_layout_roundtrip(env):
     bad = bytearray(rng[k0])
     bad[-5] ^= 1
     assert not rp.verify_range_proof_list(rw.decode_bundle(bytes(bad), sq.Query.Ranges)[0], sm, P)
+
+
+def test_skipchain_forward_links_and_update_chain(env):
+    """Genesis -> latest through verified forward links (GetUpdateChain /
+    GetLatestBlock from a known block); VerifyBase and forward-link checks
+    reject a block with a bad back link or a forged forward link."""
+    import dataclasses
+
+    from drynx_amd.ledger import skipchain as skc
+
+    cl, node, client = env
+    for _ in range(2):
+        sq = make_survey(client, cl, "sum", query_min=0, query_max=3, rows=4, proofs=1, ranges=[16, 2])
+        client.send_survey_query(sq)
+    head = client.send_get_latest_block("vn0")
+    genesis = client.send_get_genesis("vn0")
+    chain = node.get_update_chain("vn0", genesis)
+    assert chain[0].Hash == genesis.Hash and chain[-1].Hash == head.Hash
+    assert [b.Index for b in chain] == list(range(head.Index + 1))
+    assert all(skc.verify_base(a, b) for a, b in zip(chain, chain[1:]))
+    assert client.send_get_latest_block("vn2", genesis).Hash == head.Hash
+    # structural checks
+    bad = dataclasses.replace(head, BackLink="00" * 32)
+    bad.Hash = bad.compute_hash()
+    assert not skc.verify_base(chain[-2], bad)
+    assert not skc.verify_base(chain[-2], dataclasses.replace(head, Index=head.Index + 5))
+    # a forward link whose signature does not cover the target is rejected
+    prev = chain[-2]
+    forged = dict(prev.ForwardLinks[-1], To=genesis.Hash)
+    assert skc.verify_forward_link(prev, prev.ForwardLinks[-1])
+    assert not skc.verify_forward_link(prev, forged)
+    import pytest as _pt
+    tampered = dataclasses.replace(prev, ForwardLinks=[forged])
+    with _pt.raises(ValueError):
+        skc.update_chain(lambda h: {b.Hash: b for b in chain}.get(h), tampered)
