@@ -30,6 +30,18 @@ vs_baseline = value / 315.6, the reference's verifications per second of
 
 Run: python bench.py [--gpus N --steps K --warmup W]; for N>1 under
 torch.distributed.run (one rank per GPU, RCCL over xGMI).
+
+Other BASELINE.json configs (``--query``; same harness, one JSON line each;
+value = end-to-end latency in seconds of one verifiable query, lower is
+better, vs_baseline = value / the reference's AllOps total for that operation):
+  --query mean | variance   config 2: 1e5 synthetic records (10 DPs x 1e4,
+                            values in [0, 3]), range proofs (16, 5) (the
+                            simulation's Ranges code 18), 3 CNs, 3 VNs;
+                            reference AllOps rows 6-7: 2.57 s / 2.74 s
+  --query lin_reg           config 3: Pima-shaped linear regression, d = 8,
+                            8 DPs x 960 records, feature values in [0, 200),
+                            range proofs (16, 8); reference AllOps row 16
+                            (lin_reg, d = 9): 15.97 s
 """
 from __future__ import annotations
 
@@ -56,6 +68,12 @@ from drynx_amd.utils import timers  # noqa: E402
 
 REFERENCE_LR_SPECTF_S = 196.77  # AllResults.xlsx LogRegr row 7
 REFERENCE_VERIFICATIONS_PER_S = 10 * 2070 * 3 / REFERENCE_LR_SPECTF_S  # 10 DPs x 2070 proofs x 3 VNs
+# AllOps totals (AllResults.xlsx rows 6, 7, 16) and this bench's shape for them
+QUERY_CONFIGS = {
+    "mean": dict(ref_s=2.57, dps=10, records=100_000, d=1, lo=0, hi=3, ranges=(16, 5)),
+    "variance": dict(ref_s=2.74, dps=10, records=100_000, d=1, lo=0, hi=3, ranges=(16, 5)),
+    "lin_reg": dict(ref_s=15.97, dps=8, records=7_680, d=8, lo=0, hi=199, ranges=(16, 8)),
+}
 
 
 def parse():
@@ -76,11 +94,15 @@ def parse():
     ap.add_argument("--max-iter", type=int, default=450)
     ap.add_argument("--device", default=None)
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--query", default="lr", choices=["lr", *QUERY_CONFIGS],
+                    help="lr = the headline; mean/variance/lin_reg = BASELINE.json configs 2 and 3")
     return ap.parse_args()
 
 
 def main():
     args = parse()
+    if args.query != "lr":
+        return main_query(args)
     init_distributed()
     comm = make_comm(args.device)
     world, rank = comm.world, comm.rank
@@ -195,6 +217,84 @@ def main():
             with open(args.json_out, "w") as f:
                 json.dump(line, f, indent=1)
     timers.dump_trace(os.environ.get("DRYNX_TRACE") and f"{os.environ['DRYNX_TRACE']}.r{rank}.json")
+    node.close(remove=True)
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+def main_query(args):
+    """BASELINE.json configs 2 and 3: one verifiable integer query per step."""
+    cfg = QUERY_CONFIGS[args.query]
+    init_distributed()
+    comm = make_comm(args.device)
+    world, rank = comm.world, comm.rank
+    device = comm.device
+    if device.type == "cuda":
+        torch.cuda.set_device(device)
+    n_dps = cfg["dps"]
+    offsets = {"cn": 0, "vn": args.cns % world, "dp": 0}
+    cl, node = local_cluster(args.cns, n_dps, args.vns, comm=comm, device=device,
+                             workdir=tempfile.mkdtemp(prefix=f"drynx_bench_r{rank}_"), offsets=offsets)
+    rows = cfg["records"] // n_dps
+    d = cfg["d"]
+    n_in = d + 1 if args.query == "lin_reg" else 1
+    g = torch.Generator(device=device).manual_seed(99 + rank)
+    node.dp_data = {dp.id: list(torch.randint(cfg["lo"], cfg["hi"] + 1, (n_in, rows), generator=g, device=device))
+                    for dp in cl.local(rank, "dp")}
+    u, l = cfg["ranges"]
+    client = DrynxClient(node, device=device) if rank == 0 else None
+    template = None
+    if rank == 0:
+        template = make_survey(client, cl, args.query, query_min=cfg["lo"], query_max=cfg["hi"], d=d, rows=rows,
+                               proofs=1, ranges=[u, l], thresholds=[1.0, 1.0, 1.0, 0.0, 1.0], sig_device=device,
+                               deterministic_sigs=args.deterministic_sigs)
+
+    def one_step():
+        if rank == 0:
+            sq = copy.copy(template)
+            sq.SurveyID = new_survey_id()
+            _, vals, res = client.send_survey_query(sq)
+            return res
+        return node.run_survey(None)
+
+    for _ in range(args.warmup):
+        one_step()
+    timers.reset()
+    comm.barrier()
+    if device.type == "cuda":
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    blocks = [one_step().block for _ in range(args.steps)]
+    node.flush_stores()
+    comm.barrier()
+    if device.type == "cuda":
+        torch.cuda.synchronize()
+    elapsed = max(comm.all_gather_object(time.perf_counter() - t0))
+    ok = all(b is not None and all(v == 1 for v in b.data_block().Proofs.values()) for b in blocks)
+    sec = elapsed / args.steps
+    n_out = len(template.Query.Ranges) if rank == 0 else None
+    if rank == 0:
+        line = {
+            "metric": f"end-to-end verifiable {args.query} query latency",
+            "value": round(sec, 5),
+            "unit": "s per query (whole job)",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1000 * sec, 2),
+            "higher_is_better": False, "scaling": "strong",
+            "vs_baseline": round(sec / cfg["ref_s"], 5),
+            "speedup_vs_reference": round(cfg["ref_s"] / sec, 1),
+            "dtype": "bn254-exact/int64",
+            "data": "synthetic (uniform integer records, random keys and input-validation signatures)",
+            "config": {"model": f"{args.query}" + (f" d={d}" if args.query == "lin_reg" else ""),
+                       "global_batch": rows * n_dps, "seq_len": None,
+                       "parallelism": f"{world} ranks: {n_dps} DPs, {args.cns} CNs, {args.vns} VNs",
+                       "dps": n_dps, "records_per_dp": rows, "outputs_per_dp": n_out,
+                       "range_proof": {"u": u, "l": l}, "verification": "every VN verifies every proof"},
+            "all_proofs_valid": ok,
+        }
+        print(json.dumps(line), flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                json.dump(line, f, indent=1)
     node.close(remove=True)
     if dist.is_initialized():
         dist.destroy_process_group()

@@ -43,6 +43,16 @@ class BlobRef:
         return self.future.result()
 
 
+class _Item:
+    """Future of the i-th value of a ``put_many`` job."""
+
+    def __init__(self, job, i):
+        self.job, self.i = job, i
+
+    def result(self):
+        return self.job.result()[self.i]
+
+
 class BlobSegment:
     """Append-only file of large ledger values shared by the VNs of one rank:
     the same proof payload is written once, however many co-hosted VNs store
@@ -67,11 +77,33 @@ class BlobSegment:
             fut = self._done.get(blob_id)
             if fut is None:
                 fut = self._done[blob_id] = self._ex.submit(self._write, produce)
-                if len(self._done) > 4096:
+                while len(self._done) > 1 << 16:
                     self._done.pop(next(iter(self._done)))
         return BlobRef(self, fut)
 
-    def _write(self, produce):
+    def get(self, blob_id: str):
+        """The BlobRef of a value already put (None if unknown)."""
+        with self._lock:
+            fut = self._done.get(blob_id)
+        return None if fut is None else BlobRef(self, fut)
+
+    def put_many(self, blob_ids: list, produce_all) -> list:
+        """Put several values produced together: ``produce_all()`` returns one
+        buffer per id (e.g. slices of one device-to-host copy); they are written
+        back to back by one job."""
+        job = self._ex.submit(self._write, produce_all, True)
+        refs = []
+        with self._lock:
+            for i, bid in enumerate(blob_ids):
+                fut = self._done.get(bid)
+                if fut is None:
+                    fut = self._done[bid] = _Item(job, i)
+                refs.append(BlobRef(self, fut))
+            while len(self._done) > 1 << 16:
+                self._done.pop(next(iter(self._done)))
+        return refs
+
+    def _write(self, produce, many: bool = False):
         import torch
 
         dev = torch.device(self._device) if self._device is not None else None
@@ -85,6 +117,15 @@ class BlobSegment:
                 data = produce()
         with timers.span("ledger.write"):
             off = self._f.seek(0, os.SEEK_END)
+            if many:
+                out = []
+                for d in data:
+                    n = memoryview(d).nbytes
+                    self._f.write(d)
+                    out.append((off, n))
+                    off += n
+                self._f.flush()
+                return out
             self._f.write(data)
             self._f.flush()
         return off, memoryview(data).nbytes

@@ -114,6 +114,7 @@ _SIGS = {
     "dx_rp_lines_inl": [_P, _P, _P, _P, _L, _L, _L],
     "dx_rp_accum_inl": [_P, _P, _P, _L, _I],
     "dx_rp_verify_items": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _I],
+    "dx_int_moments": [_I, _P, _P, _L, _I, _P, _L, _P, _I, _P, _P],
 }
 
 
@@ -656,6 +657,56 @@ def sha256_chunks(data: torch.Tensor, chunk: int) -> torch.Tensor:
     out = torch.empty((k, 8), dtype=torch.int32, device=data.device)
     g, s = _ctx(data)
     _call("dx_sha256_chunks", g, s, _ptr(data), nbytes, chunk, _ptr(out))
+    return out
+
+
+INT_MOMENTS_MAX_COLS = 64
+
+
+def _upload(a: np.ndarray, device) -> torch.Tensor:
+    t = torch.from_numpy(np.ascontiguousarray(a))
+    if torch.device(device).type == "cuda":
+        return t.pin_memory().to(device, non_blocking=True)
+    return t
+
+
+def int_moments(Z: torch.Tensor, seg_rows, pairs) -> torch.Tensor:
+    """K14 (csrc/kernels/dx_moments.hip): exact int64 ``out[g, p] = sum over the
+    rows of segment g of Z[i, a_p] * Z[i, b_p]`` (mod 2^64), column index
+    ``C = Z.shape[1]`` standing for a constant 1.  ``seg_rows`` are the host-known
+    row counts of the consecutive segments (one per DP); ``pairs`` a [P, 2]
+    int sequence.  One launch for all segments."""
+    assert Z.dtype == torch.int64 and Z.dim() == 2 and Z.stride(1) == 1
+    C = Z.shape[1]
+    pr = np.asarray(pairs, dtype=np.int16).reshape(-1, 2)
+    if C > INT_MOMENTS_MAX_COLS or pr.size == 0 or pr.min() < 0 or pr.max() > C:
+        raise ValueError(f"int_moments: {C} columns, pairs out of range")
+    counts = np.asarray(seg_rows, dtype=np.int64)
+    G, P = len(counts), pr.shape[0]
+    if counts.sum() != Z.shape[0]:
+        raise ValueError(f"int_moments: segments cover {counts.sum()} rows, Z has {Z.shape[0]}")
+    out = torch.zeros((G, P), dtype=torch.int64, device=Z.device)
+    # tiles: row ranges of one segment, sized so a big DP spreads over ~2k
+    # workgroups and each tile still streams >= 64 rows
+    per_tile = -(-int(counts.sum()) // 2048)
+    chunk = max(64, (per_tile + 63) // 64 * 64)
+    per = np.maximum(1, -(-counts // chunk)) * (counts > 0)
+    seg = np.repeat(np.arange(G, dtype=np.int64), per)
+    starts = np.concatenate([[0], np.cumsum(counts)[:-1]]).astype(np.int64)
+    first = np.concatenate([[0], np.cumsum(per)[:-1]]).astype(np.int64)
+    k = np.arange(len(seg), dtype=np.int64) - np.repeat(first, per)
+    r0 = np.repeat(starts, per) + k * chunk
+    r1 = np.minimum(r0 + chunk, np.repeat(starts + counts, per))
+    n_tiles = len(seg)
+    if n_tiles == 0:
+        return out
+    Zc = Z.contiguous()
+    tiles = _upload(np.stack([seg, r0, r1], axis=1), Z.device)
+    pairs_t = _upload(pr, Z.device)
+    g, s = _ctx(Zc)
+    partial = None if g else torch.empty((n_tiles, P), dtype=torch.int64)
+    _call("dx_int_moments", g, s, _ptr(Zc), Zc.stride(0), C, _ptr(tiles), n_tiles, _ptr(pairs_t), P, _ptr(out),
+          _ptr(partial))
     return out
 
 

@@ -90,33 +90,32 @@ def _t(x, device):
 
 
 # ----------------------------------------------------------------------------- simple moments
-def local_sum(x: torch.Tensor) -> int:
-    return int(x.sum().item())
+def _moments(name: str, data, device, n_cols: int) -> list:
+    """One DP's outputs of a moment operation through the K14 kernel (one
+    launch, one copy of the few results to the host)."""
+    cols = [_t(c, device).reshape(-1).to(torch.int64) for c in data[:n_cols]]
+    Z = torch.stack(cols, dim=1)
+    return batch_values(name, Z, [Z.shape[0]])[0].cpu().tolist()
 
 
 def encode_sum(data, pk, with_proofs=False, ranges=None):
     """sum.go:17 — [sum x]."""
-    x = _t(data[0], pk.device)
-    return _encrypt_with_proofs(pk, [local_sum(x)], with_proofs, ranges)
+    return _encrypt_with_proofs(pk, _moments("sum", data, pk.device, 1), with_proofs, ranges)
 
 
 def encode_mean(data, pk, with_proofs=False, ranges=None):
     """mean.go:17 — [sum x, N]."""
-    x = _t(data[0], pk.device)
-    return _encrypt_with_proofs(pk, [local_sum(x), x.numel()], with_proofs, ranges)
+    return _encrypt_with_proofs(pk, _moments("mean", data, pk.device, 1), with_proofs, ranges)
 
 
 def encode_variance(data, pk, with_proofs=False, ranges=None):
     """variance.go:17 — [sum x, N, sum x^2]."""
-    x = _t(data[0], pk.device)
-    return _encrypt_with_proofs(pk, [local_sum(x), x.numel(), local_sum(x * x)], with_proofs, ranges)
+    return _encrypt_with_proofs(pk, _moments("variance", data, pk.device, 1), with_proofs, ranges)
 
 
 def encode_cosim(data, pk, with_proofs=False, ranges=None):
     """cosim.go:18 — [sum a, sum b, sum a^2, sum b^2, sum ab]."""
-    a, b = _t(data[0], pk.device), _t(data[1], pk.device)
-    vals = [local_sum(a), local_sum(b), local_sum(a * a), local_sum(b * b), local_sum(a * b)]
-    return _encrypt_with_proofs(pk, vals, with_proofs, ranges)
+    return _encrypt_with_proofs(pk, _moments("cosim", data, pk.device, 2), with_proofs, ranges)
 
 
 def encode_frequency_count(data, qmin, qmax, pk, with_proofs=False, ranges=None):
@@ -130,37 +129,105 @@ def encode_frequency_count(data, qmin, qmax, pk, with_proofs=False, ranges=None)
 
 def encode_model_evaluation(data, pk, with_proofs=False, ranges=None):
     """model_evaluation.go:17 — [N, sum y, sum y^2, sum (pred - y)^2]; data = [y, pred]."""
-    y, pred = _t(data[0], pk.device), _t(data[1], pk.device)
-    vals = [y.numel(), local_sum(y), local_sum(y * y), local_sum((pred - y) * (pred - y))]
-    return _encrypt_with_proofs(pk, vals, with_proofs, ranges)
-
-
-def int_pair_moments(X: torch.Tensor, pairs: torch.Tensor, chunk: int = 1 << 16) -> torch.Tensor:
-    """Exact int64 sum_i X[i, a] * X[i, b] for the column pairs (a, b) = pairs[:, p]
-    (K14): elementwise products reduced over record chunks, so it runs on the
-    GPU too (no int64 GEMM there) and never leaves exact integer arithmetic."""
-    out = torch.zeros(pairs.shape[1], dtype=torch.int64, device=X.device)
-    a, b = pairs[0].to(X.device), pairs[1].to(X.device)
-    for s in range(0, X.shape[0], chunk):
-        blk = X[s: s + chunk]
-        out += (blk.index_select(1, a) * blk.index_select(1, b)).sum(0)
-    return out
+    return _encrypt_with_proofs(pk, _moments("MLeval", data, pk.device, 2), with_proofs, ranges)
 
 
 def encode_lin_reg(data, pk, with_proofs=False, ranges=None):
     """linear_regression_dims.go:23-106 — data = [x_0..x_{d-1}, y] columns.
 
     Output order: [N, sum x_j (d), sum x_j x_k j<=k (row-major upper tri), sum y, sum x_j y (d)]."""
-    cols = [_t(c, pk.device) for c in data]
-    X = torch.stack(cols[:-1], dim=1)  # [N, d]
-    y = cols[-1]
-    N, d = X.shape
-    iu = torch.triu_indices(d, d, device=X.device)
-    XtX_u = int_pair_moments(X, iu)  # exact int64 sum_i x_ij x_ik, j <= k
-    vals = [N] + X.sum(0).cpu().tolist()
-    vals += XtX_u.cpu().tolist()
-    vals += [local_sum(y)] + (X * y[:, None]).sum(0).cpu().tolist()
-    return _encrypt_with_proofs(pk, vals, with_proofs, ranges)
+    return _encrypt_with_proofs(pk, _moments("lin_reg", data, pk.device, len(data)), with_proofs, ranges)
+
+
+# ----------------------------------------------------------------------------- many DPs at once
+# Operations whose per-DP outputs are sums of products of record columns: the
+# K14 kernel computes them for every DP of a rank in one launch.
+MOMENT_OPS = ("sum", "mean", "variance", "cosim", "lin_reg", "MLeval")
+# Operations encoded as 0/1 bit vectors (OR/AND encodings, OR_AND.go).
+BIT_OPS = ("bool_AND", "bool_OR", "min", "max", "union", "inter")
+BATCH_OPS = MOMENT_OPS + BIT_OPS + ("frequencyCount",)
+
+
+def moment_pairs(name: str, C: int) -> list:
+    """Column pairs (a, b) of the K14 reduction whose sums are the outputs of
+    ``name``, in the reference's output order; index C is the constant 1
+    (N = (C, C), sum x_a = (a, C))."""
+    if name == "sum":
+        return [(0, C)]
+    if name == "mean":
+        return [(0, C), (C, C)]
+    if name == "variance":
+        return [(0, C), (C, C), (0, 0)]
+    if name == "cosim":
+        return [(0, C), (1, C), (0, 0), (1, 1), (0, 1)]
+    if name == "MLeval":  # Z = [y, pred - y]
+        return [(C, C), (0, C), (0, 0), (1, 1)]
+    if name == "lin_reg":  # Z = [x_0 .. x_{d-1}, y]
+        d = C - 1
+        return ([(C, C)] + [(j, C) for j in range(d)] + [(j, k) for j in range(d) for k in range(j, d)]
+                + [(d, C)] + [(j, d) for j in range(d)])
+    raise ValueError(f"{name} is not a moment operation")
+
+
+def batch_values(name: str, Z: torch.Tensor, seg_rows, qmin: int = 0, qmax: int = 0) -> torch.Tensor:
+    """[n_dp, n_out] int64 outputs of every DP of a batch, on Z's device.
+
+    Z [rows, n_in] holds the DPs' records back to back (``seg_rows[g]`` rows for
+    DP g, columns = the operation's input columns).  Moments: one K14 launch;
+    frequency counts: one bincount over (DP, bin); bit encodings: the 0/1
+    value each DP encrypts (OR-encoded bit, or the inverted AND bit), as in
+    ``encode_bits`` with proofs."""
+    from .. import native as nt
+
+    G = len(seg_rows)
+    dev = Z.device
+    if name in MOMENT_OPS:
+        if name == "MLeval":
+            Z = torch.stack([Z[:, 0], Z[:, 1] - Z[:, 0]], dim=1)
+        elif name in ("sum", "mean", "variance"):
+            Z = Z[:, :1]
+        return nt.int_moments(Z.contiguous(), seg_rows, moment_pairs(name, Z.shape[1]))
+    counts = torch.as_tensor(list(seg_rows), dtype=torch.int64)
+    x = Z[:, 0]
+    if name in ("bool_AND", "bool_OR"):  # the DP's bit is its first record == 1 (encode_decode.go:82-118)
+        first = torch.zeros(G, dtype=torch.int64, device=dev)
+        if x.numel():
+            starts = (counts.cumsum(0) - counts).clamp(max=x.numel() - 1).to(dev)
+            first = ((x[starts] == 1) & (counts > 0).to(dev)).to(torch.int64)
+        return (first if name == "bool_OR" else 1 - first)[:, None]
+    seg = torch.repeat_interleave(torch.arange(G, device=dev), counts.to(dev), output_size=Z.shape[0])
+    n = qmax - qmin + 1
+    if name == "frequencyCount":
+        keep = (x >= qmin) & (x <= qmax)
+        flat = (seg * n + (x - qmin))[keep]
+        return torch.bincount(flat, minlength=G * n)[: G * n].reshape(G, n)
+    grid = torch.arange(qmin, qmax + 1, device=dev)
+    if name in ("min", "max"):
+        big = torch.iinfo(torch.int64)
+        init = torch.full((G,), big.max if name == "min" else big.min, dtype=torch.int64, device=dev)
+        ext = init.scatter_reduce(0, seg, x, "amin" if name == "min" else "amax", include_self=True)
+        if name == "min":  # OR of bit_i = [i >= localMin]
+            return (grid[None, :] >= ext[:, None]).to(torch.int64)
+        return (grid[None, :] < ext[:, None]).to(torch.int64)  # inverted AND of [i >= localMax]
+    if name in ("union", "inter"):
+        keep = (x >= qmin) & (x <= qmax)
+        hit = torch.zeros(G * n, dtype=torch.int64, device=dev)
+        hit[(seg * n + (x - qmin))[keep]] = 1
+        hit = hit.reshape(G, n)
+        return hit if name == "union" else 1 - hit
+    raise ValueError(f"{name} has no batched encoder")
+
+
+def encrypt_batch(pk: eg.PublicKeyTable, values: torch.Tensor, bits: bool):
+    """One encryption launch for a whole batch: ints (EncryptIntVectorGetRs),
+    or for bit encodings without proofs a fresh random non-zero scalar where the
+    bit absorbs and 0 elsewhere (EncryptScalar, OR_AND.go)."""
+    m = values.reshape(-1).contiguous()
+    if not bits:
+        return eg.encrypt_ints(pk, m)
+    rnd = bn.random_scalars(m.numel(), pk.device)
+    s = torch.where((m != 0)[:, None], rnd, torch.zeros_like(rnd))
+    return eg.encrypt_scalars(pk, s.contiguous())
 
 
 # ----------------------------------------------------------------------------- boolean encodings

@@ -30,6 +30,7 @@ from ..crypto.elgamal import CipherVector, pk_table
 class AggregationProof:
     inputs: list          # list of CipherVector (one per contributor)
     result: CipherVector  # claimed sum
+    stacked: object = None  # decoded proofs: (K, C) [contributors, n, 24] behind ``inputs``
 
     def to_bytes(self) -> bytes:
         parts = [len(self.inputs).to_bytes(8, "little"), len(self.result).to_bytes(8, "little")]
@@ -47,13 +48,15 @@ class AggregationProof:
     def from_bytes(b: bytes, device="cpu") -> "AggregationProof":
         k = int.from_bytes(b[:8], "little")
         n = int.from_bytes(b[8:16], "little")
-        o = 16
-        ins = []
-        for _ in range(k):
-            ins.append(CipherVector.from_bytes(b[o: o + 128 * n], device))
-            o += 128 * n
-        res = CipherVector.from_bytes(b[o: o + 128 * n], device)
-        return AggregationProof(ins, res)
+        if len(b) != 16 + 128 * n * (k + 1):
+            raise ValueError("aggregation proof length does not match its header")
+        # every contributor and the result in one decode (a CN with thousands of
+        # DPs would otherwise pay one decode launch sequence per DP)
+        allcv = CipherVector.from_bytes(b[16:], device)
+        K = allcv.K.view(k + 1, n, 24)
+        C = allcv.C.view(k + 1, n, 24)
+        ins = [CipherVector(K[i], C[i]) for i in range(k)]
+        return AggregationProof(ins, CipherVector(K[k], C[k]), (K[:k], C[:k]))
 
 
 def aggregation_list_proof_creation(inputs: list, result: CipherVector) -> AggregationProof:
@@ -65,7 +68,10 @@ def aggregation_list_proof_verification(pr: AggregationProof, threshold: float =
     k = int(math.ceil(threshold * n))
     if k == 0 or not pr.inputs:
         return True
-    s = CipherVector.sum([cv[:k] for cv in pr.inputs])
+    if pr.stacked is not None and k == n:
+        s = CipherVector(nt.g1_sum(pr.stacked[0]), nt.g1_sum(pr.stacked[1]))
+    else:
+        s = CipherVector.sum([cv[:k] for cv in pr.inputs])
     r = pr.result[:k]
     return bool(nt.g1_eq(s.K, r.K).all()) and bool(nt.g1_eq(s.C, r.C).all())
 

@@ -13,6 +13,8 @@ xGMI, and each CN sums its DPs with the K5 reduction kernel.
 from __future__ import annotations
 
 import itertools
+import os
+import time
 import zlib
 
 import torch
@@ -100,6 +102,82 @@ def dp_encode(ctx, sq, dp, sync_timer: bool = True) -> dict:
     return {"cv": eg.CipherVector.cat(cvs), "proofs": proofs, "clear": clears, "n_groups": len(groups)}
 
 
+def _with_proofs(q) -> bool:
+    return q.Proofs != 0 and q.Ranges is not None and q.IVSigs.InputValidationSigs is not None \
+        and not all(r[0] == 0 and r[1] == 0 for r in q.Ranges)
+
+
+def dp_encode_batch(ctx, sq, dps: list) -> dict:
+    """Encode every DP of ``dps`` as ONE batch: their records are stacked into
+    one matrix (one pinned upload), the outputs of all DPs come from one K14
+    launch (or one bincount / scatter for histograms and bit encodings), all
+    ciphertexts of all groups from one encryption launch, and the values reach
+    the host in one copy (the clear results and the provers' inputs).
+
+    Same per-DP data (seeds), outputs, group replication and CuttingFactor
+    replication as :func:`dp_encode`; returns ``{dp_id: result}`` in its format.
+    The reference encodes DP by DP (data_collection_protocol.go:178-373); with
+    thousands of one-record DPs (ScaleDPs) per-DP launch sequences and syncs
+    were the whole cost."""
+    q = sq.Query
+    op = q.Operation
+    device = torch.device(ctx.device)
+    pk = eg.pk_table(sq.RosterServers.aggregate(), device)
+    g = q.DPDataGen
+    n_in = max(1, op.NbrInput)
+    mats, rows = [], []
+    for dp in dps:
+        if ctx.dp_data and dp.id in ctx.dp_data:
+            cols = [enc._t(c, device).reshape(-1).to(torch.int64) for c in ctx.dp_data[dp.id]]
+            mats.append(torch.stack(cols, dim=1))
+        else:  # generate_fake_data's draw, kept on the host until the one upload below
+            gen = torch.Generator().manual_seed(_seed(sq.SurveyID, dp.id))
+            t = torch.randint(g.GenerateDataMin, g.GenerateDataMax + 1, (n_in, max(1, g.GenerateRows)), generator=gen,
+                              dtype=torch.int64)
+            mats.append(t.t())
+        rows.append(mats[-1].shape[0])
+    if all(m.device.type == "cpu" for m in mats):
+        Z = torch.cat(mats).contiguous()
+        if device.type == "cuda":
+            Z = Z.pin_memory().to(device, non_blocking=True)
+    else:
+        Z = torch.cat([m.to(device) for m in mats]).contiguous()
+    groups = all_possible_groups(g.GroupByValues)
+    ng, cf = len(groups), q.CuttingFactor
+    vals = enc.batch_values(op.NameOp, Z, rows, op.QueryMin, op.QueryMax)  # [n_dp, n_out]
+    n_dp, n_out = vals.shape
+    with_proofs = _with_proofs(q)
+    bits = op.NameOp in enc.BIT_OPS and not with_proofs
+    # one fresh encryption per (DP, group, output); CuttingFactor replicates a
+    # group's ciphertexts cf times (same randomness), as dp_encode does
+    cv, r = enc.encrypt_batch(pk, vals[:, None, :].expand(n_dp, ng, n_out), bits)
+    rep = max(1, cf or 1)
+    idx = (torch.arange(ng, device=device)[:, None, None] * n_out
+           + torch.arange(n_out, device=device)[None, None, :]).expand(ng, rep, n_out).reshape(-1)
+    per_dp = ng * n_out
+    K = cv.K.reshape(n_dp, per_dp, -1)[:, idx]
+    C = cv.C.reshape(n_dp, per_dp, -1)[:, idx]
+    host = vals.cpu().tolist()
+    us = ls = offs = None
+    if with_proofs:
+        us, ls, offs = enc._ranges_uvl(q.Ranges, n_out)
+    out = {}
+    for i, dp in enumerate(dps):
+        v = host[i]
+        proofs = []
+        if with_proofs:
+            base = i * per_dp
+            for j in range(ng):
+                lo = base + j * n_out
+                proofs.append(enc.CreateProofBatch(list(v), r[lo: lo + n_out], cv[lo: lo + n_out], us, ls,
+                                                   list(range(n_out)), offs))
+        else:
+            proofs = [None] * ng
+        out[dp.id] = {"cv": eg.CipherVector(K[i], C[i]), "proofs": proofs, "clear": [list(v) for _ in groups],
+                      "n_groups": ng}
+    return out
+
+
 def data_collection(ctx, sq) -> tuple:
     """Run every local DP, route responses to their CN's rank, sum per CN.
 
@@ -115,8 +193,17 @@ def data_collection(ctx, sq) -> tuple:
     # the per-DP timer syncs the device only for a handful of DPs per rank: with
     # thousands (ScaleDPs, one record each) the syncs serialise the encoders
     sync_timer = len(local_dps) <= 16
+    if local_dps and sq.Query.Operation.NameOp in enc.BATCH_OPS and os.environ.get("DRYNX_DP_BATCH", "1") != "0":
+        # every DP of this rank in one batch; each DP's encoding latency is the batch's
+        with timers.timed("DPencodingBatch", sync=sync_timer) as t:
+            batch = dp_encode_batch(ctx, sq, local_dps)
+        dt = time.perf_counter() - t.t0
+        for dp in local_dps:
+            timers.record(f"{dp.id}_DPencoding", dt)
+    else:
+        batch = {dp.id: dp_encode(ctx, sq, dp, sync_timer) for dp in local_dps}
     for dp in local_dps:
-        res = dp_encode(ctx, sq, dp, sync_timer)
+        res = batch[dp.id]
         dp_results[dp.id] = res
         cn = cl.by_id(dp_to_cn[dp.id])
         items.append((cn.rank, dp.id, res["cv"]))

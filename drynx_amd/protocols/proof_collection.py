@@ -177,12 +177,14 @@ def store_verdicts(ctx, sq, vn, requests: list, pending) -> dict:
     store = ctx.store(vn.id)
     bitmap = {}
     counts = {k: 0 for k in prq.VN_ORDER}
+    stored = [req for req in requests if req.kind != "shuffle"]  # storeProof skips shuffle proofs (:318-331)
+    values = dict(zip(map(id, stored), ctx.ledger_values(stored)))
     for req, code in zip(requests, codes):
         key = req.key(vn.id)
         bitmap[key] = code
         counts[req.kind] += 1
-        if req.kind != "shuffle":  # storeProof skips shuffle proofs (proof_collection_protocol.go:318-331)
-            store.update_async(f"{sq.SurveyID}/{req.kind}", key, ctx.ledger_value(req))
+        if req.kind != "shuffle":
+            store.update_async(f"{sq.SurveyID}/{req.kind}", key, values[id(req)])
     exp = expected_counts(sq)
     for k in prq.VN_ORDER:
         if counts[k] != exp[k]:

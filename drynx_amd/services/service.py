@@ -114,40 +114,72 @@ class DrynxNode:
 
     # ------------------------------------------------------------------ VN storage
     def ledger_value(self, req):
-        """What a VN stores for a proof request (storeProof,
-        proof_collection_protocol.go:318-331): the signed payload.  A range
-        bundle's raw-limb tensor goes to the rank's shared blob segment once
-        (however many co-hosted VNs store it) through a pinned, asynchronous
-        device-to-host copy on the ledger's own stream; ``get_proofs`` serves
-        it in the reference RangeProofListBytes layout (proofs/range_wire.py)."""
-        if req.kind != "range" or req.header_only or req.tensor is None or req._data is not None:
-            return req.payload()
-        if os.environ.get("DRYNX_LEDGER_RANGE", "on") == "off":  # A/B runs only
-            return b""
+        return self.ledger_values([req])[0]
+
+    def ledger_values(self, reqs: list) -> list:
+        """What a VN stores for each proof request (storeProof,
+        proof_collection_protocol.go:318-331): the signed payload.  Range
+        bundles' raw-limb tensors go to the rank's shared blob segment once
+        (however many co-hosted VNs store them): every new one of the call is
+        gathered into one device buffer and moved by ONE pinned, asynchronous
+        device-to-host copy on the ledger's own stream (thousands of one-proof
+        DPs would otherwise cost one copy + event each); ``get_proofs`` serves
+        them in the reference RangeProofListBytes layout (proofs/range_wire.py)."""
+        out: list = [None] * len(reqs)
+        fresh: dict = {}
+        skip = os.environ.get("DRYNX_LEDGER_RANGE", "on") == "off"  # A/B runs only
+        for i, req in enumerate(reqs):
+            if req.kind != "range" or req.header_only or req.tensor is None or req._data is not None:
+                out[i] = req.payload()
+            elif skip:
+                out[i] = b""
+            else:
+                fresh.setdefault(req.digest().hex(), []).append(i)
+        if not fresh:
+            return out
         if not hasattr(self, "_blobs"):
             from ..ledger.store import BlobSegment
 
             self._blobs = BlobSegment(os.path.join(self.workdir, f"ledger_r{self.rank}.blobs"), self.device)
-        t = req.tensor
-        if t.is_cuda:
-            if not hasattr(self, "_ledger_stream"):
-                self._ledger_stream = torch.cuda.Stream(self.device)
-            st = self._ledger_stream
-            st.wait_stream(torch.cuda.current_stream(self.device))
-            with torch.cuda.stream(st):
-                host = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
-                host.copy_(t, non_blocking=True)
-                ev = torch.cuda.Event()
-                ev.record(st)
-            t.record_stream(st)
+        refs = {k: self._blobs.get(k) for k in fresh}
+        new = [k for k, v in refs.items() if v is None]
+        if new:
+            tensors = [reqs[fresh[k][0]].tensor.contiguous().reshape(-1).view(torch.uint8) for k in new]
+            for k, ref in zip(new, self._blobs.put_many(new, self._host_bytes(tensors))):
+                refs[k] = ref
+        for k, idxs in fresh.items():
+            for i in idxs:
+                out[i] = refs[k]
+        return out
 
-            def produce():
-                ev.synchronize()
-                return memoryview(host.numpy()).cast("B")
-        else:
-            def produce():
-                return memoryview(t.contiguous().numpy()).cast("B")
-        return self._blobs.put(req.digest().hex(), produce)
+    def _host_bytes(self, tensors: list):
+        """A producer of the host bytes of ``tensors`` (run by the ledger
+        thread): on a GPU one concatenation on the compute stream, then one
+        pinned copy on the ledger stream, so the producer only waits for it."""
+        sizes = [t.numel() for t in tensors]
+        if not tensors[0].is_cuda:
+            return lambda: [memoryview(t.numpy()) for t in tensors]
+        flat = torch.cat(tensors) if len(tensors) > 1 else tensors[0]
+        if not hasattr(self, "_ledger_stream"):
+            self._ledger_stream = torch.cuda.Stream(self.device)
+        st = self._ledger_stream
+        st.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(st):
+            host = torch.empty(flat.shape, dtype=torch.uint8, pin_memory=True)
+            host.copy_(flat, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(st)
+        flat.record_stream(st)
+
+        def produce():
+            ev.synchronize()
+            mv = memoryview(host.numpy())
+            out, o = [], 0
+            for n in sizes:
+                out.append(mv[o: o + n])
+                o += n
+            return out
+        return produce
 
     def store(self, vn_id: str) -> Store:
         s = self._stores.get(vn_id)

@@ -344,3 +344,40 @@ def test_merged_multi_verifier_fold(gpu_device):
         a = nt.final_exp(nt._finish_prod_on_host(fb))
         b = nt.final_exp(nt._finish_prod_on_host(alone))
         assert bool(nt.gt_eq(a, b).all())
+
+
+def test_int_moments_gpu_matches_host(gpu_device):
+    """K14 on gfx950 vs the host path: one 1e5-record DP split over many
+    workgroups, thousands of one-record DPs, empty DPs, and the widest pair
+    list (64 columns + the constant -> 2145 pairs, L = 1, 9 units per thread)."""
+    g = torch.Generator().manual_seed(5)
+    for C, counts, lo, hi in ((1, [100_000, 3, 0, 77], -(1 << 20), 1 << 20),
+                              (9, [1] * 6000 + [0, 64, 65, 129], 0, 4),
+                              (64, [1000, 1, 333], -(1 << 40), 1 << 40)):
+        Z = torch.randint(lo, hi, (sum(counts), C), generator=g, dtype=torch.int64)
+        pairs = [(a, b) for a in range(C + 1) for b in range(a, C + 1)]
+        c, gg = _both(lambda z: nt.int_moments(z, counts, pairs), Z)
+        assert torch.equal(c, gg), C
+
+
+def test_batched_dp_encoding_gpu(gpu_device, tmp_path):
+    """All DPs of a rank encoded as one batch on the GPU == the per-DP encoder."""
+    from drynx_amd.crypto import elgamal as eg
+    from drynx_amd.protocols import data_collection as dcp
+    from drynx_amd.services.api import DrynxClient
+    from drynx_amd.services.local import local_cluster, make_survey
+
+    cl, node = local_cluster(3, 40, 1, device=gpu_device, workdir=str(tmp_path))
+    client = DrynxClient(node, device=gpu_device)
+    secret = sum(cn.keypair.secret for cn in cl.cns) % O.R
+    try:
+        for op in ("variance", "lin_reg", "frequencyCount", "min"):
+            sq = make_survey(client, cl, op, query_min=0, query_max=5, rows=50, d=3, proofs=1, ranges=[16, 16],
+                             sig_device=gpu_device, deterministic_sigs=True)
+            batch = dcp.dp_encode_batch(node, sq, list(cl.dps))
+            for dp in list(cl.dps)[:5]:
+                single = dcp.dp_encode(node, sq, dp)
+                assert batch[dp.id]["clear"] == single["clear"], op
+                assert eg.decrypt_ints(secret, batch[dp.id]["cv"]) == batch[dp.id]["clear"][0], op
+    finally:
+        node.close(remove=True)

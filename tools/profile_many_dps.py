@@ -38,13 +38,16 @@ def main():
     pr.disable()
     s = io.StringIO()
     s.write(f"{n} DPs: {t:.3f} s\n")
-    pstats.Stats(pr, stream=s).sort_stats("tottime").print_stats(30)
-    pstats.Stats(pr, stream=s).sort_stats("cumulative").print_stats(45)
+    pstats.Stats(pr, stream=s).sort_stats("tottime").print_stats(40)
+    pstats.Stats(pr, stream=s).sort_stats("cumulative").print_stats(100)
     txt = s.getvalue()
     if out:
         with open(out, "w") as f:
             f.write(txt)
     print(txt[:200])
+    from drynx_amd.utils import timers
+
+    timers.dump_trace()
     node.close(remove=True)
 
 
