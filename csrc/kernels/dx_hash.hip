@@ -169,6 +169,24 @@ extern "C" int dx_sha256_chunks(int on_gpu, void *stream, const uint8_t *data, i
   return run(on_gpu, stream, n, op, false, "sha256_chunks");
 }
 
+// The same slice digests for `rows` equally long payloads laid out every
+// `stride` bytes (one envelope per DP of a batch): out[(r*k + i)*8 ..] with
+// k = ceil(len / chunk) slices per row (1 for an empty payload).
+extern "C" int dx_sha256_rows(int on_gpu, void *stream, const uint8_t *data, int64_t rows, int64_t stride,
+                              int64_t len, int64_t chunk, uint32_t *out) {
+  if (chunk <= 0 || (chunk & 63) != 0 || rows < 0 || stride < len) return -2;
+  const int64_t k = len == 0 ? 1 : (len + chunk - 1) / chunk;
+  auto op = [=] __host__ __device__(int64_t t) {
+    const int64_t r = t / k, i = t - r * k;
+    const int64_t off = i * chunk;
+    const int64_t m = len - off < chunk ? len - off : chunk;
+    uint32_t d[8];
+    sha256_bytes(data + r * stride + off, m, d);
+    for (int q = 0; q < 8; q++) out[8 * t + q] = d[q];
+  };
+  return run(on_gpu, stream, rows * k, op, false, "sha256_rows");
+}
+
 // Independent G1 generators h_i (unknown discrete logs) for commitment
 // schemes -- the permutation commitments of the shuffle proof.  For index i:
 // ctr = 0, 1, ...: x = SHA-256(seed || le64(i) || le32(ctr)) (big endian) mod p;

@@ -61,6 +61,9 @@ class DataBlock:
         return DataBlock(**data_block_from_wire(b))
 
 
+_DATA_BLOCKS: dict = {}
+
+
 @dataclass
 class SkipBlock:
     Index: int
@@ -95,7 +98,17 @@ class SkipBlock:
         return SkipBlock(**d)
 
     def data_block(self) -> DataBlock:
-        return DataBlock.from_bytes(self.Data)
+        """The decoded DataBlock (treat as read-only: decodes are shared by
+        content hash, so the VNs of a rank checking the same block decode its
+        bitmap -- one entry per proof -- once)."""
+        key = hashlib.sha256(self.Data).digest()
+        db = _DATA_BLOCKS.get(key)
+        if db is None:
+            db = DataBlock.from_bytes(self.Data)
+            if len(_DATA_BLOCKS) >= 8:
+                _DATA_BLOCKS.pop(next(iter(_DATA_BLOCKS)))
+            _DATA_BLOCKS[key] = db
+        return db
 
     def bls_keys(self):
         if not self.Roster or not all(vn.get("bls") for vn in self.Roster):

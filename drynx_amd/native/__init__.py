@@ -115,6 +115,7 @@ _SIGS = {
     "dx_rp_accum_inl": [_P, _P, _P, _L, _I],
     "dx_rp_verify_items": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _I],
     "dx_int_moments": [_I, _P, _P, _L, _I, _P, _L, _P, _I, _P, _P],
+    "dx_sha256_rows": [_I, _P, _P, _L, _L, _L, _L, _P],
 }
 
 
@@ -707,6 +708,19 @@ def int_moments(Z: torch.Tensor, seg_rows, pairs) -> torch.Tensor:
     partial = None if g else torch.empty((n_tiles, P), dtype=torch.int64)
     _call("dx_int_moments", g, s, _ptr(Zc), Zc.stride(0), C, _ptr(tiles), n_tiles, _ptr(pairs_t), P, _ptr(out),
           _ptr(partial))
+    return out
+
+
+def sha256_rows(data: torch.Tensor, chunk: int) -> torch.Tensor:
+    """[rows, k, 8] big-endian SHA-256 words of every `chunk`-byte slice of
+    every row of a contiguous 2-D tensor (k = ceil(row bytes / chunk), >= 1)."""
+    assert data.dim() == 2 and data.is_contiguous()
+    rows = data.shape[0]
+    row_bytes = data.shape[1] * data.element_size()
+    k = max(1, (row_bytes + chunk - 1) // chunk)
+    out = torch.empty((rows, k, 8), dtype=torch.int32, device=data.device)
+    g, s = _ctx(data)
+    _call("dx_sha256_rows", g, s, _ptr(data), rows, row_bytes, row_bytes, chunk, _ptr(out))
     return out
 
 

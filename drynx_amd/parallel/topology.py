@@ -42,17 +42,27 @@ class Cluster:
     def parties(self):
         return self.cns + self.dps + self.vns
 
+    def _ids(self) -> dict:
+        """id -> (position, party), rebuilt when the party lists change size
+        (thousands of DPs made the linear scan quadratic)."""
+        n = (len(self.cns), len(self.dps), len(self.vns))
+        idx = self.__dict__.get("_id_index")
+        if idx is None or idx[0] != n:
+            idx = (n, {p.id: (i, p) for i, p in enumerate(self.parties)})
+            self.__dict__["_id_index"] = idx
+        return idx[1]
+
     def by_id(self, pid: str) -> Party:
-        for p in self.parties:
-            if p.id == pid:
-                return p
-        raise KeyError(pid)
+        e = self._ids().get(pid)
+        if e is None:
+            raise KeyError(pid)
+        return e[1]
 
     def index_of(self, pid: str) -> int:
-        for i, p in enumerate(self.parties):
-            if p.id == pid:
-                return i
-        raise KeyError(pid)
+        e = self._ids().get(pid)
+        if e is None:
+            raise KeyError(pid)
+        return e[0]
 
     def local(self, rank: int, role: str | None = None):
         return [p for p in self.parties if p.rank == rank and (role is None or p.role == role)]

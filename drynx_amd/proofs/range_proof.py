@@ -350,15 +350,27 @@ class RangeProofList:
         return torch.cat(parts)
 
     @staticmethod
-    def unpack(t: torch.Tensor) -> "RangeProofList":
-        meta = t[:5].cpu().tolist()
-        assert meta[0] == 0x52505231, "not a packed RangeProofList"
+    def unpack(t: torch.Tensor, meta=None, offs=None, cols=None) -> "RangeProofList":
+        """Views into a packed list; ``meta``/``offs``/``cols`` may be given when
+        the caller already fetched the header words (batched unpack)."""
+        if meta is None:
+            meta = t[:5].cpu().tolist()
+        if meta[0] != 0x52505231:
+            raise ValueError("not a packed RangeProofList")
         n, u, l, S = meta[1:]
+        if n < 0 or l < 0 or S < 0:
+            raise ValueError("malformed RangeProofList header")
         o = 5
-        offs = t[o: o + 2 * n].cpu().clone().view(torch.int64).tolist()
+        if offs is None:
+            offs = t[o: o + 2 * n].cpu().clone().view(torch.int64).tolist()
         o += 2 * n
-        cols = t[o: o + n].cpu().tolist()
+        if cols is None:
+            cols = t[o: o + n].cpu().tolist()
         o += n
+        has_rp = not (u == 0 and l == 0)
+        need = o + 48 * n + ((8 + 8 + 24) * n + 8 * n * l + (8 + 32 + 96) * n * S * l if has_rp and n else 0)
+        if need != t.numel():
+            raise ValueError(f"packed RangeProofList has {t.numel()} words, header implies {need}")
 
         def take(rows, width):
             nonlocal o

@@ -120,9 +120,118 @@ def range_bundle_pack(rpls) -> torch.Tensor:
     return torch.cat([hdr] + packed)
 
 
+def _rows_view(ts: list):
+    """[G, numel] view of G equally shaped contiguous tensors that sit back to
+    back in one storage (slices of one prover batch), else None."""
+    t0 = ts[0]
+    n = t0.numel()
+    if not all(t.is_contiguous() and t.numel() == n for t in ts):
+        return None
+    step = n * t0.element_size()
+    p0 = t0.data_ptr()
+    if any(t.data_ptr() != p0 + g * step for g, t in enumerate(ts)):
+        return None
+    if t0.storage_offset() + len(ts) * n > t0.untyped_storage().nbytes() // t0.element_size():
+        return None
+    return t0.new_empty(0).set_(t0.untyped_storage(), t0.storage_offset(), (len(ts), n), (n, 1))
+
+
+def _stack_rows(ts: list) -> torch.Tensor:
+    v = _rows_view(ts)
+    return v if v is not None else torch.stack([t.reshape(-1) for t in ts])
+
+
+def range_bundle_pack_many(bundles: list):
+    """``range_bundle_pack`` of many DPs' bundles.  When every bundle is one
+    list of the same shape (n, u, l, S) -- thousands of one-output DPs -- all
+    are packed by one concatenation into a [G, L] tensor whose rows are the
+    bundles (returned too, for one-launch digests); otherwise bundle by bundle.
+    -> (list of per-bundle tensors, [G, L] tensor or None)"""
+    if len(bundles) > 1 and all(len(b) == 1 for b in bundles):
+        rs = [b[0] for b in bundles]
+        r0 = rs[0]
+        shape = (len(r0), r0.u, r0.l, r0.S, r0.has_rp, r0.commit.device)
+        if len(r0) and all((len(r), r.u, r.l, r.S, r.has_rp, r.commit.device) == shape for r in rs):
+            G, n = len(rs), len(r0)
+            fields = [lambda r: r.commit.K, lambda r: r.commit.C]
+            if r0.has_rp:
+                fields += [lambda r, a=a: getattr(r, a) for a in ("challenge", "zr", "D", "zphi", "zv", "V", "A")]
+            per = [_stack_rows([f(r) for r in rs]) for f in fields]
+            size = 5 + 3 * n + sum(p.shape[1] for p in per)
+            head = np.empty((G, 2 + 5 + 3 * n), dtype=np.int32)
+            head[:, :7] = [1, size, 0x52505231, n, r0.u, r0.l, r0.S]
+            head[:, 7: 7 + 2 * n] = np.asarray([o for r in rs for o in r.offset], dtype=np.int64).view(np.int32)\
+                .reshape(G, 2 * n)
+            head[:, 7 + 2 * n:] = np.asarray([c for r in rs for c in r.cols], dtype=np.int32).reshape(G, n)
+            ht = torch.from_numpy(head)
+            dev = per[0].device
+            if dev.type == "cuda":
+                ht = ht.pin_memory().to(dev, non_blocking=True)
+            packed = torch.cat([ht] + per, dim=1)
+            return list(packed.unbind(0)), packed
+    return [range_bundle_pack(b) for b in bundles], None
+
+
+def new_range_requests(items: list, survey_id: str, secrets: list, device) -> list:
+    """NewRangeProofRequest for many DPs at once (``items`` = [(dp_id, lists)]):
+    one packing concatenation, one digest launch, one signing launch."""
+    with timers.span("sign.marshal.range"):
+        tensors, packed = range_bundle_pack_many([lists for _, lists in items])
+    with timers.span("sign.digest.range"):
+        if packed is not None:
+            dgs = payload_digest.digest_rows(packed)
+        else:
+            dgs = [payload_digest.digest_tensor(t) for t in tensors]
+    with timers.span("sign.schnorr.range"):
+        sigs = sigma.schnorr_sign_batch(secrets, dgs, device)
+    return [ProofRequest("range", survey_id, dp_id, "", None, sig, obj=lists, data_digest=dg, tensor=t)
+            for (dp_id, lists), t, dg, sig in zip(items, tensors, dgs, sigs)]
+
+
+_HEAD = 7 + 3 * 64  # header ints fetched per bundle by the batched unpack (lists of <= 64 proofs)
+
+
+def _unpack_one(t: torch.Tensor, head: list) -> list:
+    """One bundle of a single list whose header words (count, size, meta,
+    offsets, cols) are already on the host."""
+    k, size, magic, n, u, l, S = head[:7]
+    if k != 1 or magic != 0x52505231 or size != t.numel() - 2 or n < 0 or 7 + 3 * n > len(head):
+        raise ValueError("malformed range bundle header")
+    offs = np.asarray(head[7: 7 + 2 * n], dtype=np.int32).view(np.int64).tolist()
+    cols = head[7 + 2 * n: 7 + 3 * n]
+    return [rp.RangeProofList.unpack(t[2:], (magic, n, u, l, S), offs, cols)]
+
+
+def range_bundle_unpack_many(ts: list) -> list:
+    """``range_bundle_unpack`` of many bundles with one device-to-host copy of
+    their headers (instead of a handful of small synchronous copies each);
+    bundles with several lists or > 64 proofs take the single path.  An entry
+    is the list of RangeProofLists or the exception that rejects the bundle."""
+    out: list = [None] * len(ts)
+    short = [i for i, t in enumerate(ts) if t.numel() >= 7]
+    if short:
+        heads = torch.nn.utils.rnn.pad_sequence([ts[i][: _HEAD] for i in short], batch_first=True).cpu().tolist()
+    for j, i in enumerate(short):
+        h = heads[j]
+        try:
+            if h[0] == 1 and 0 <= h[3] <= 64:
+                out[i] = _unpack_one(ts[i], h[: min(len(h), ts[i].numel())])
+        except Exception as e:  # noqa: BLE001 -- a malformed bundle is a rejected proof
+            out[i] = e
+    for i, t in enumerate(ts):
+        if out[i] is None:
+            try:
+                out[i] = range_bundle_unpack(t)
+            except Exception as e:  # noqa: BLE001
+                out[i] = e
+    return out
+
+
 def range_bundle_unpack(t: torch.Tensor) -> list:
     k = int(t[0])
     sizes = t[1: 1 + k].cpu().tolist()
+    if k < 0 or any(s < 0 for s in sizes) or 1 + k + sum(sizes) != t.numel():
+        raise ValueError("malformed range bundle")
     o, out = 1 + k, []
     for s in sizes:
         out.append(rp.RangeProofList.unpack(t[o: o + s]))
@@ -290,6 +399,17 @@ def verify_content(req: ProofRequest, sq, device, cache: VerifierCache) -> bool:
     raise ValueError(req.kind)
 
 
+def _prefetch_range_lists(reqs: list, idxs: list, device):
+    """Decode the tensor payloads of many range requests at once (see
+    ``range_bundle_unpack_many``); a malformed one keeps its exception so
+    ``_range_lists`` raises it for that request alone."""
+    todo = [i for i in idxs if reqs[i].decoded is None and reqs[i].tensor is not None and reqs[i]._data is None]
+    if len(todo) < 2:
+        return
+    for i, r in zip(todo, range_bundle_unpack_many([reqs[i].tensor.to(device) for i in todo])):
+        reqs[i].decoded = r
+
+
 def _range_lists(req: ProofRequest, device) -> list:
     """The VN's decode of the SIGNED payload (the raw limb tensor, or its bytes),
     never the prover's in-memory object: what is verified is what the
@@ -301,6 +421,8 @@ def _range_lists(req: ProofRequest, device) -> list:
             req.decoded = range_bundle_unpack(req.tensor.to(device))
         else:
             req.decoded = range_bundle_from_bytes(req.data, device)
+    if isinstance(req.decoded, Exception):
+        raise req.decoded
     return req.decoded
 
 
@@ -336,6 +458,8 @@ def _verify_range_group(reqs, idxs, sq, device, cache, part, n_vn) -> list:
     sigs = sq.Query.IVSigs.InputValidationSigs
     mode = int(getattr(sq, "RangeProofMode", 0) or 0)
     base, parts = {}, {}
+    with timers.span("rp.verify.unpack_many"):
+        _prefetch_range_lists(reqs, idxs, device)
     for i in idxs:
         try:
             lists = []

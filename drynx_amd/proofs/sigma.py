@@ -118,6 +118,27 @@ def schnorr_sign(secret: int, msg: bytes) -> bytes:
     return O.g1_to_bytes(R) + O.scalar_to_bytes(s)
 
 
+def schnorr_sign_batch(secrets: list, msgs: list, device="cpu") -> list:
+    """``schnorr_sign`` of many (secret, message) pairs (the envelopes of every
+    DP of a rank): the nonce points R_i = k_i B and the public keys X_i = x_i B
+    come from one fixed-base launch, their encodings from one conversion; the
+    challenges and responses are host hashing and scalar arithmetic."""
+    n = len(secrets)
+    if n == 0:
+        return []
+    ks = [O.random_scalar() for _ in range(n)]
+    dev = torch.device(device)
+    pts = nt.g1_fb_mul(bn.base_table(dev), bn.scalars_tensor(ks + [int(x) for x in secrets], dev))
+    enc = bn.g1_aff_to_bytes(nt.g1_to_affine(pts))
+    out = []
+    for i in range(n):
+        Rb, Xb = enc[i].tobytes(), enc[n + i].tobytes()
+        x = int(secrets[i]) % O.R
+        e = int.from_bytes(hashlib.sha256(Rb + Xb + msgs[i]).digest(), "big") % O.R
+        out.append(Rb + O.scalar_to_bytes((ks[i] + e * x) % O.R))
+    return out
+
+
 def schnorr_verify(public, msg: bytes, sig: bytes) -> bool:
     if len(sig) != 96 or public is None:
         return False

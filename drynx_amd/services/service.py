@@ -344,11 +344,11 @@ class DrynxNode:
         return list(out.items())
 
     def _sign_range(self, sq, proved: list) -> list:
-        reqs = []
-        for dp_id, lists in proved:
-            dp = self.cluster.by_id(dp_id)
-            reqs.append(prq.new_proof_request("range", lists, sq.SurveyID, dp_id, "", dp.keypair.secret))
-        return reqs
+        """Every hosted DP's range request: one packing, digest and signing
+        pass for all of them (``prq.new_range_requests``)."""
+        items = list(proved)
+        secrets = [self.cluster.by_id(dp_id).keypair.secret for dp_id, _ in items]
+        return prq.new_range_requests(items, sq.SurveyID, secrets, self.device)
 
     def _early_range_verification(self, sq, proved: list, stream):
         """When every VN of the survey lives on this rank, start the VN's range

@@ -1,0 +1,88 @@
+"""Batched envelopes for many DPs (ScaleDPs: thousands of one-proof DPs per
+rank): packing, digests and Schnorr signatures of all bundles at once, and the
+VN's batched decode, against the one-bundle paths
+(lib/proof/structs_proofs.go:110-182 marshal + sign / unmarshal)."""
+import pytest
+import torch
+
+from drynx_amd.crypto import digest as dg
+from drynx_amd.crypto import elgamal as eg
+from drynx_amd.crypto import oracle as O
+from drynx_amd.ops.encoding import CreateProofBatch
+from drynx_amd.proofs import range_proof as rp
+from drynx_amd.proofs import requests as prq
+from drynx_amd.proofs import sigma
+
+
+@pytest.fixture(scope="module")
+def bundles():
+    S, u, l = 2, 4, 3
+    sigs = [rp.init_range_proof_signatures([u] * 2) for _ in range(S)]
+    kps = [eg.KeyPair.generate() for _ in range(S)]
+    P = eg.aggregate_keys([k.public for k in kps])
+    pk = eg.pk_table(P)
+    vals = [1, 5, 7, 2, 9, 3, 0, 4]
+    cv, r = eg.encrypt_ints(pk, vals)
+    n = len(vals)
+    big = rp.create_range_proofs(CreateProofBatch(vals, r, cv, [u] * n, [l] * n, [0, 1] * (n // 2), [0] * n),
+                                 rp.SigMaterial(sigs), P)[0]
+    # four DPs with two proofs each: consecutive slices of one prover batch
+    return [[rp.rpl_range(big, 2 * g, 2 * g + 2)] for g in range(4)], rp.SigMaterial(sigs), P
+
+
+def test_pack_many_matches_single(bundles):
+    bs, _, _ = bundles
+    ts, packed = prq.range_bundle_pack_many(bs)
+    assert packed is not None and packed.shape[0] == 4
+    for b, t in zip(bs, ts):
+        assert torch.equal(t, prq.range_bundle_pack(b))
+    # non-consecutive inputs take the stacking path, same bytes
+    ts2, packed2 = prq.range_bundle_pack_many([bs[2], bs[0]])
+    assert torch.equal(ts2[0], prq.range_bundle_pack(bs[2])) and torch.equal(ts2[1], prq.range_bundle_pack(bs[0]))
+    # mixed shapes: bundle by bundle
+    ts3, packed3 = prq.range_bundle_pack_many([bs[0], bs[1] + bs[2]])
+    assert packed3 is None and torch.equal(ts3[1], prq.range_bundle_pack(bs[1] + bs[2]))
+
+
+def test_digest_rows_matches_digest_tensor(bundles):
+    ts, packed = prq.range_bundle_pack_many(bundles[0])
+    assert dg.digest_rows(packed) == [dg.digest_tensor(t) for t in ts]
+    assert dg.digest_rows(packed) == [dg.digest_bytes(t.numpy().tobytes()) for t in ts]
+
+
+def test_schnorr_sign_batch_verifies():
+    secrets = [O.random_scalar() for _ in range(5)]
+    msgs = [bytes([i]) * (i + 1) for i in range(5)]
+    sigs = sigma.schnorr_sign_batch(secrets, msgs)
+    for x, m, s in zip(secrets, msgs, sigs):
+        X = O.g1_mul(x, O.G1_GEN)
+        assert sigma.schnorr_verify(X, m, s)
+        assert not sigma.schnorr_verify(X, m + b"!", s)
+
+
+def test_new_range_requests_and_unpack_many(bundles):
+    bs, sm, P = bundles
+    secrets = [O.random_scalar() for _ in bs]
+    reqs = prq.new_range_requests([(f"dp{i}", b) for i, b in enumerate(bs)], "s1", secrets, "cpu")
+    for req, x in zip(reqs, secrets):
+        assert prq.verify_signature(req, O.g1_mul(x, O.G1_GEN))
+        fresh = prq.ProofRequest("range", "s1", req.sender_id, "", None, b"", tensor=req.tensor)
+        assert fresh.digest() == req.digest()
+    dec = prq.range_bundle_unpack_many([r.tensor for r in reqs])
+    for d, b in zip(dec, bs):
+        assert len(d) == 1 and d[0].cols == b[0].cols and d[0].offset == b[0].offset
+        assert torch.equal(d[0].A, b[0].A) and torch.equal(d[0].commit.K, b[0].commit.K)
+        assert rp.verify_range_proof_list(d[0], sm, P)
+
+
+def test_unpack_many_rejects_malformed(bundles):
+    ts, _ = prq.range_bundle_pack_many(bundles[0])
+    bad_len = ts[0][:-5].clone()                   # truncated payload
+    bad_size = ts[1].clone()
+    bad_size[1] += 1                               # size word does not match
+    bad_n = ts[2].clone()
+    bad_n[3] = 3                                   # proof count does not match the fields
+    tiny = torch.tensor([1, 2, 3], dtype=torch.int32)
+    out = prq.range_bundle_unpack_many([bad_len, bad_size, bad_n, tiny, ts[3]])
+    assert all(isinstance(o, Exception) for o in out[:4])
+    assert isinstance(out[4], list)
