@@ -18,6 +18,12 @@
 #include "common.h"
 #include "../bn254/g1_fast.h"
 
+// Occupancy target of the line and accumulation kernels (a variant TU may ask
+// for 1 wave per SIMD: 512 registers, AGPRs as spill space instead of scratch).
+#ifndef FOLD_OCC
+#define FOLD_OCC DX_OCC
+#endif
+
 #define FOLD_CAT2(a, b) a##b
 #define FOLD_CAT(a, b) FOLD_CAT2(a, b)
 #define FOLD_NAME(x) FOLD_CAT(x, FOLD_SFX)
@@ -101,7 +107,7 @@ __device__ __forceinline__ void line_add(Fp2 &X, Fp2 &Y, Fp2 &Z, const Fp2 &x2, 
 // Items it < n; several verifiers' batches over the same V may share one
 // launch: item it pairs P[it] with V[it % period] (period = n for one batch;
 // rows of P past a batch's own length are the point at infinity).
-__global__ void __launch_bounds__(kWG) DX_OCC rp_lines_kernel(const uint32_t *__restrict__ P_aff,
+__global__ void __launch_bounds__(kWG) FOLD_OCC rp_lines_kernel(const uint32_t *__restrict__ P_aff,
                                                               const uint32_t *__restrict__ V_aff,
                                                               uint4 *__restrict__ lines, int64_t n,
                                                               int64_t period, int64_t n_v) {
@@ -132,6 +138,126 @@ __global__ void __launch_bounds__(kWG) DX_OCC rp_lines_kernel(const uint32_t *__
            P.y, lines, n, s++, it);
   line_add(X, Y, Z, mul(qq.x, Fp2::from_limbs(Frob::TWX2)), neg(mul(qq.y, Fp2::from_limbs(Frob::TWY2))), P.x, P.y,
            lines, n, s++, it);
+}
+
+// ---- shared-V variant: the line COEFFICIENTS depend on V only (the
+// evaluation at P is two Fp2-by-Fp products), so verifiers folding the same
+// proofs with their own weights share one coefficient image:
+//   l0 = c0 * yP, l1 = c1 * xP, l3 = c3
+// (dbl: c0 = -H, c1 = 3X^2, c3 = E - B; add: c0 = lambda, c1 = -theta,
+// c3 = theta x2 - lambda y2).  The accumulation evaluates at P as it goes.
+__device__ __forceinline__ void coef_dbl(Fp2 &X, Fp2 &Y, Fp2 &Z, uint4 *lines, int64_t n, int s, int64_t it) {
+  const Fp2 b2 = Fp2::from_limbs(Curve::B2);
+  Fp2 X2 = sqr(X);
+  const Fp2 c1 = add(dbl(X2), X2);
+  Fp2 Bq = sqr(Y);
+  Fp2 C = sqr(Z);
+  Fp2 H = sub(sub(sqr(add(Y, Z)), Bq), C);
+  Fp2 E = mul(add(dbl(C), C), b2);
+  store_line(lines, n, s, it, neg(H), c1, sub(E, Bq));
+  Fp2 F = add(dbl(E), E);
+  Fp2 A = mul(X, Y);
+  X = dbl(mul(A, sub(Bq, F)));
+  Z = dbl(dbl(mul(Bq, H)));
+  Fp2 E2 = sqr(E);
+  Y = sub(sqr(add(Bq, F)), dbl(dbl(add(dbl(E2), E2))));
+}
+
+__device__ __forceinline__ void coef_add(Fp2 &X, Fp2 &Y, Fp2 &Z, const Fp2 &x2, const Fp2 &y2, uint4 *lines,
+                                         int64_t n, int s, int64_t it) {
+  Fp2 th = sub(Y, mul(y2, Z));
+  Fp2 la = sub(X, mul(x2, Z));
+  store_line(lines, n, s, it, la, neg(th), sub(mul(th, x2), mul(la, y2)));
+  Fp2 C = sqr(th), D = sqr(la);
+  Fp2 E = mul(D, la), F = mul(Z, C), G = mul(X, D);
+  Fp2 H = sub(add(E, F), dbl(G));
+  Y = sub(mul(th, sub(G, H)), mul(Y, E));
+  X = mul(la, H);
+  Z = mul(Z, E);
+}
+
+// One item per V (m items); V at infinity gets zero coefficients (the
+// accumulation skips it: ML(P, O) = 1).
+__global__ void __launch_bounds__(kWG) FOLD_OCC rp_coeffs_kernel(const uint32_t *__restrict__ V_aff,
+                                                               uint4 *__restrict__ lines, int64_t m) {
+  const int64_t it = (int64_t)blockIdx.x * kWG + threadIdx.x;
+  if (it >= m) return;
+  const G2A Q = at<G2A>(V_aff, it);
+  if (Q.is_inf()) {
+    for (int s = 0; s < kSteps; s++) store_line(lines, m, s, it, Fp2::zero(), Fp2::zero(), Fp2::zero());
+    return;
+  }
+  Fp2 X = Q.x, Y = Q.y, Z = Fp2::one();
+  int s = 0;
+  for (int i = ATE_NAF_LEN - 2; i >= 0; i--) {
+    coef_dbl(X, Y, Z, lines, m, s++, it);
+    const int d = ATE_NAF[i];
+    if (d != 0) {
+      asm volatile("" ::: "memory");
+      const G2A qq = at<G2A>(V_aff, it);
+      coef_add(X, Y, Z, qq.x, d > 0 ? qq.y : neg(qq.y), lines, m, s++, it);
+    }
+  }
+  asm volatile("" ::: "memory");
+  const G2A qq = at<G2A>(V_aff, it);
+  coef_add(X, Y, Z, mul(conj(qq.x), Fp2::from_limbs(Frob::TWX1)), mul(conj(qq.y), Fp2::from_limbs(Frob::TWY1)),
+           lines, m, s++, it);
+  coef_add(X, Y, Z, mul(qq.x, Fp2::from_limbs(Frob::TWX2)), neg(mul(qq.y, Fp2::from_limbs(Frob::TWY2))), lines, m,
+           s++, it);
+}
+
+template <int K>
+__device__ __forceinline__ void accum_p_step(Fp12 &f, const uint4 *__restrict__ coef, const uint32_t *__restrict__ P_aff,
+                                             int64_t m, int s, int64_t qbase, int64_t pbase, uint32_t live) {
+#pragma unroll 1
+  for (int k = 0; k < K; k++) {
+    if ((live >> k) & 1u) {
+      Fp2 c0, c1, c3;
+      load_line(coef, m, s, qbase + (int64_t)k * kWG, c0, c1, c3);
+      const G1A P = at<G1A>(P_aff, pbase + (int64_t)k * kWG);
+      f = mul_line(f, mul_fp(c0, P.y), mul_fp(c1, P.x), c3);
+    }
+  }
+}
+
+// G verifiers' point images P[v * period + q] (q < m live) against ONE
+// coefficient image.  Block b runs verifier v on coefficient block qb with
+// the G blocks sharing qb dealt to one XCD back to back (blocks b and b + 8
+// share an XCD), so the second and third reads of a coefficient come from
+// that XCD's L2.  Requires period % (64 K 8) == 0.
+template <int K>
+__global__ void __launch_bounds__(kWG) FOLD_OCC rp_accum_p_kernel(const uint4 *__restrict__ coef,
+                                                                const uint32_t *__restrict__ P_aff,
+                                                                const uint32_t *__restrict__ V_aff, uint32_t *f_blk,
+                                                                int64_t m, int64_t period, int G) {
+  __shared__ Fp12 sf[kWG / 2];
+  const int lane = threadIdx.x;
+  const int64_t b = blockIdx.x, slot = b >> 3;
+  const int v = (int)(slot % G);
+  const int64_t qb = (slot / G) * 8 + (b & 7);
+  const int64_t qbase = qb * kWG * K + lane, pbase = (int64_t)v * period + qbase;
+  uint32_t live = 0;
+#pragma unroll 1
+  for (int k = 0; k < K; k++) {
+    const int64_t q = qbase + (int64_t)k * kWG;
+    if (q < m && !at<G1A>(P_aff, pbase + (int64_t)k * kWG).is_inf() && !at<G2A>(V_aff, q).is_inf()) live |= 1u << k;
+  }
+  Fp12 f = Fp12::one();
+  int s = 0;
+  for (int i = ATE_NAF_LEN - 2; i >= 0; i--) {
+    if (i != ATE_NAF_LEN - 2) f = sqr(f);
+    accum_p_step<K>(f, coef, P_aff, m, s++, qbase, pbase, live);
+    if (ATE_NAF[i] != 0) accum_p_step<K>(f, coef, P_aff, m, s++, qbase, pbase, live);
+  }
+  accum_p_step<K>(f, coef, P_aff, m, s++, qbase, pbase, live);
+  accum_p_step<K>(f, coef, P_aff, m, s++, qbase, pbase, live);
+  for (int h = kWG / 2; h > 0; h >>= 1) {
+    if (lane >= h && lane < 2 * h) sf[lane - h] = f;
+    __syncthreads();
+    if (lane < h) f = mul(f, sf[lane]);
+    __syncthreads();
+  }
+  if (lane == 0) at<Fp12>(f_blk, (int64_t)v * (period / ((int64_t)kWG * K)) + qb) = f;
 }
 
 // G1 side of the fold, one launch per VN: P_it = affine(rho_it (ZB[p*L+j] -
@@ -205,7 +331,7 @@ __device__ __forceinline__ void accum_step(Fp12 &f, const uint4 *__restrict__ li
 // Lane `lane` of workgroup b owns items b*64*K + k*64 + lane (k < K): each
 // uint4 load of a step is one contiguous 1 KiB wave access.
 template <int K>
-__global__ void __launch_bounds__(kWG) DX_OCC rp_accum_kernel(const uint4 *__restrict__ lines, uint32_t *f_blk,
+__global__ void __launch_bounds__(kWG) FOLD_OCC rp_accum_kernel(const uint4 *__restrict__ lines, uint32_t *f_blk,
                                                               int64_t n) {
   __shared__ Fp12 sf[kWG / 2];
   const int lane = threadIdx.x;
@@ -251,6 +377,34 @@ int FOLD_NAME(dx_rp_points_)(void *stream, const uint32_t *ZB_jac, const uint32_
   hipLaunchKernelGGL(rp_points_kernel, dim3((unsigned)blocks), dim3(kWG), 0, (hipStream_t)stream, ZB_jac, Y_jac, rho,
                      P_aff, n, S, L);
   return check_hip(hipGetLastError(), "rp_points");
+}
+
+int FOLD_NAME(dx_rp_coeffs_)(void *stream, const uint32_t *V_aff, uint32_t *coef, int64_t m) {
+  using namespace FOLD_NAME(fold_ns_);
+  if (m <= 0) return 0;
+  const int64_t blocks = (m + kWG - 1) / kWG;
+  hipLaunchKernelGGL(rp_coeffs_kernel, dim3((unsigned)blocks), dim3(kWG), 0, (hipStream_t)stream, V_aff,
+                     reinterpret_cast<uint4 *>(coef), m);
+  return check_hip(hipGetLastError(), "rp_coeffs");
+}
+
+// f_blk: G * period / (64 K) Fp12 partial products, verifier-major.
+int FOLD_NAME(dx_rp_accum_p_)(void *stream, const uint32_t *coef, const uint32_t *P_aff, const uint32_t *V_aff,
+                              uint32_t *f_blk, int64_t m, int64_t period, int G, int K) {
+  using namespace FOLD_NAME(fold_ns_);
+  if (m <= 0 || G <= 0) return 0;
+  if (period < m || period % ((int64_t)kWG * K * 8) != 0) return -2;
+  const int64_t blocks = (int64_t)G * (period / ((int64_t)kWG * K));
+  const uint4 *C = reinterpret_cast<const uint4 *>(coef);
+  hipStream_t st = (hipStream_t)stream;
+  switch (K) {
+    case 1: hipLaunchKernelGGL(rp_accum_p_kernel<1>, dim3((unsigned)blocks), dim3(kWG), 0, st, C, P_aff, V_aff, f_blk, m, period, G); break;
+    case 2: hipLaunchKernelGGL(rp_accum_p_kernel<2>, dim3((unsigned)blocks), dim3(kWG), 0, st, C, P_aff, V_aff, f_blk, m, period, G); break;
+    case 4: hipLaunchKernelGGL(rp_accum_p_kernel<4>, dim3((unsigned)blocks), dim3(kWG), 0, st, C, P_aff, V_aff, f_blk, m, period, G); break;
+    case 8: hipLaunchKernelGGL(rp_accum_p_kernel<8>, dim3((unsigned)blocks), dim3(kWG), 0, st, C, P_aff, V_aff, f_blk, m, period, G); break;
+    default: return -2;
+  }
+  return check_hip(hipGetLastError(), "rp_accum_p");
 }
 
 // f_blk: ceil(n / (64 K)) Fp12 partial products.

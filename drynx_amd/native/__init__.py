@@ -113,6 +113,10 @@ _SIGS = {
     "dx_fold_steps_inl": [],
     "dx_rp_lines_inl": [_P, _P, _P, _P, _L, _L, _L],
     "dx_rp_accum_inl": [_P, _P, _P, _L, _I],
+    "dx_rp_coeffs_ni": [_P, _P, _P, _L],
+    "dx_rp_accum_p_ni": [_P, _P, _P, _P, _P, _L, _L, _I, _I],
+    "dx_rp_coeffs_inl": [_P, _P, _P, _L],
+    "dx_rp_accum_p_inl": [_P, _P, _P, _P, _P, _L, _L, _I, _I],
     "dx_rp_verify_items": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _I],
     "dx_int_moments": [_I, _P, _P, _L, _I, _P, _L, _P, _I, _P, _P],
     "dx_sha256_rows": [_I, _P, _P, _L, _L, _L, _L, _P],
@@ -886,6 +890,43 @@ def rp_fold_accum(lines: torch.Tensor, n: int, K: int = 4, variant: str | None =
     rc = getattr(_load(), f"dx_rp_accum_{v}")(s, _ptr(lines), _ptr(fb), n, K)
     if rc:
         raise RuntimeError(f"dx_rp_accum_{v} failed rc={rc}")
+    return fb
+
+
+def rp_fold_coeffs(V_aff: torch.Tensor, variant: str | None = None) -> torch.Tensor:
+    """Shared-V phase 1: the line coefficients of every V's Miller loop (no P)
+    -> flat int32 image [steps * 12 * m * 4]; several verifiers folding the
+    same proofs share it (``rp_fold_accum_p`` evaluates at their P)."""
+    v = variant or FOLD_VARIANT
+    m = _rows(V_aff, 32)
+    assert V_aff.is_cuda and V_aff.is_contiguous()
+    steps = getattr(_load(), f"dx_fold_steps_{v}")()
+    coef = torch.empty((steps * 12 * m * 4,), dtype=torch.int32, device=V_aff.device)
+    _, s = _ctx(V_aff)
+    rc = getattr(_load(), f"dx_rp_coeffs_{v}")(s, _ptr(V_aff), _ptr(coef), m)
+    if rc:
+        raise RuntimeError(f"dx_rp_coeffs_{v} failed rc={rc}")
+    return coef
+
+
+FOLD_P_ALIGN = 8  # verifier blocks are padded to 64 K * 8 items (XCD-paired block mapping)
+
+
+def rp_fold_accum_p(coef: torch.Tensor, P_aff: torch.Tensor, V_aff: torch.Tensor, period: int, G: int, K: int = 4,
+                    variant: str | None = None) -> torch.Tensor:
+    """Shared-V phase 2: G verifiers' point images (P[v * period + q], q < m)
+    folded against one coefficient image -> [G * period / (64 K), 96]
+    partial products, verifier-major."""
+    v = variant or FOLD_VARIANT
+    m = _rows(V_aff, 32)
+    assert _rows(P_aff, 16) == G * period and period >= m and period % (64 * K * FOLD_P_ALIGN) == 0
+    steps = getattr(_load(), f"dx_fold_steps_{v}")()
+    assert coef.numel() == steps * 12 * m * 4
+    fb = torch.empty((G * period // (64 * K), 96), dtype=torch.int32, device=P_aff.device)
+    _, s = _ctx(coef, P_aff, V_aff)
+    rc = getattr(_load(), f"dx_rp_accum_p_{v}")(s, _ptr(coef), _ptr(P_aff), _ptr(V_aff), _ptr(fb), m, period, G, K)
+    if rc:
+        raise RuntimeError(f"dx_rp_accum_p_{v} failed rc={rc}")
     return fb
 
 

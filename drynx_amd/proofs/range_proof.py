@@ -777,12 +777,26 @@ def _miller_fold_multi(ZB, Y, rhos: list, V, S: int, L: int) -> list:
     into a shared point image whose per-verifier blocks are padded to whole
     workgroups, then ONE line-image launch and ONE K-item accumulation (a
     verifier's slice of a multi-GPU node is too short to fill the chip on
-    its own).  ``DRYNX_FOLD=fused`` selects the previous one-kernel fold."""
+    its own).  The line coefficients depend on V only, so they are computed
+    ONCE for all verifiers (``rp_fold_coeffs``) and each verifier's points
+    are evaluated inside the accumulation (``rp_fold_accum_p``).
+    ``DRYNX_FOLD=2`` selects the per-verifier line image, ``fused`` the
+    one-kernel fold (A/B)."""
     m = V.shape[0]
     G = len(rhos)
-    if os.environ.get("DRYNX_FOLD", "2") == "fused":
+    mode = os.environ.get("DRYNX_FOLD", "3")
+    if mode == "fused":
         return [nt.rp_verify_fold(ZB, Y, rho, V, S, L) for rho in rhos]
     K = fold_k(G * m)
+    if mode == "3":
+        per = 64 * K * nt.FOLD_P_ALIGN
+        pad = -(-m // per) * per
+        P = torch.zeros((G * pad, 16), dtype=torch.int32, device=V.device)
+        for v, rho in enumerate(rhos):
+            nt.rp_fold_points(ZB, Y, rho, S, L, out=P[v * pad: v * pad + m])
+        fb = nt.rp_fold_accum_p(nt.rp_fold_coeffs(V.contiguous()), P, V.contiguous(), pad, G, K)
+        blk = pad // (64 * K)
+        return [fb[v * blk:(v + 1) * blk] for v in range(G)]
     per = 64 * K
     pad = -(-m // per) * per
     P = torch.zeros((G * pad, 16), dtype=torch.int32, device=V.device)

@@ -110,7 +110,7 @@ def test_lr_encode_fused_matches_torch(gpu_device):
         assert torch.allclose(g2, ref2, rtol=1e-10, atol=1e-8), (g2 - ref2).abs().max()
 
 
-@pytest.mark.parametrize("fold", ["2", "fused"])
+@pytest.mark.parametrize("fold", ["3", "2", "fused"])
 def test_range_proofs_gpu(gpu_device, fold, monkeypatch):
     monkeypatch.setenv("DRYNX_FOLD", fold)
     from drynx_amd.crypto import elgamal as eg
@@ -326,11 +326,14 @@ def test_fold_points_match_g1_ops(gpu_device, variant):
     assert torch.equal(got, want)
 
 
-def test_merged_multi_verifier_fold(gpu_device):
-    """Several verifiers' folds in one padded line image / accumulation ==
-    each verifier's fold on its own (after the final exponentiation)."""
+@pytest.mark.parametrize("mode", ["2", "3"])
+def test_merged_multi_verifier_fold(gpu_device, mode, monkeypatch):
+    """Several verifiers' folds in one padded line image / accumulation (mode
+    2) or over one shared coefficient image (mode 3) == each verifier's fold
+    on its own (after the final exponentiation)."""
     from drynx_amd.proofs import range_proof as rp
 
+    monkeypatch.setenv("DRYNX_FOLD", mode)
     S, L, npj = 3, 4, 7
     ZB = nt.g1_fb_mul(bn.base_table(gpu_device), bn.random_scalars(npj * L, gpu_device))
     Y = nt.g1_fb_mul(bn.base_table(gpu_device), bn.random_scalars(npj * S, gpu_device))
@@ -381,3 +384,27 @@ def test_batched_dp_encoding_gpu(gpu_device, tmp_path):
                 assert eg.decrypt_ints(secret, batch[dp.id]["cv"]) == batch[dp.id]["clear"][0], op
     finally:
         node.close(remove=True)
+
+
+@pytest.mark.parametrize("K", [1, 8])
+def test_shared_v_fold_infinities(gpu_device, K):
+    """Shared-V coefficients + per-verifier evaluation: items whose P or V is
+    the point at infinity contribute 1, as in the per-item line image."""
+    m, G = 700, 2
+    period = -(-m // (64 * K * nt.FOLD_P_ALIGN)) * 64 * K * nt.FOLD_P_ALIGN
+    V = nt.g2_fb_mul(bn.base2_table(gpu_device), bn.random_scalars(m, gpu_device))
+    V[5] = 0
+    V[640] = 0
+    P = torch.zeros((G * period, 16), dtype=torch.int32, device=gpu_device)
+    for v in range(G):
+        Pv = nt.g1_to_affine(nt.g1_fb_mul(bn.base_table(gpu_device), bn.random_scalars(m, gpu_device)))
+        Pv[3 + v] = 0
+        P[v * period: v * period + m] = Pv
+    fb = nt.rp_fold_accum_p(nt.rp_fold_coeffs(V), P, V, period, G, K)
+    blk = period // (64 * K)
+    for v in range(G):
+        Pv = P[v * period: v * period + m].contiguous()
+        alone = nt.rp_fold_accum(nt.rp_fold_lines(Pv, V), m, 1)
+        a = nt.final_exp(nt._finish_prod_on_host(fb[v * blk:(v + 1) * blk]))
+        b = nt.final_exp(nt._finish_prod_on_host(alone))
+        assert bool(nt.gt_eq(a, b).all()), v

@@ -15,6 +15,9 @@ from drynx_amd import native as nt  # noqa: E402
 from drynx_amd.crypto import bn254 as bn  # noqa: E402
 
 
+VARIANTS = os.environ.get("FOLD_VARIANTS", "inl").split(",")
+
+
 def timed(fn, reps=3):
     fn()
     torch.cuda.synchronize()
@@ -38,7 +41,7 @@ def main():
     # reference value on a small prefix: FE(prod ML) via per-item Miller loops
     m = 4096
     ref = nt.final_exp(nt._finish_prod_on_host(nt.miller_loop(P[:m].contiguous(), V[:m].contiguous())))
-    for v in ("ni", "inl"):
+    for v in VARIANTS:
         for K in (1, 2, 4, 8):
             fb = nt.rp_fold_accum(nt.rp_fold_lines(P[:m].contiguous(), V[:m].contiguous(), v), m, K, v)
             got = nt.final_exp(nt._finish_prod_on_host(fb))
@@ -49,15 +52,31 @@ def main():
     Y = bn.g1_infinity_jac(n, dev)
     rho = torch.zeros((n, 8), dtype=torch.int32, device=dev)
     rho[:, 0] = 1
-    t, _ = timed(lambda: nt.rp_verify_fold(ZB, Y, rho, V, 1, 1))
-    print(json.dumps({"variant": "fused", "n": n, "ms": round(1e3 * t, 2), "ml_per_s": round(n / t)}), flush=True)
-    for v in ("ni", "inl"):
+    if os.environ.get("FOLD_FUSED", "0") == "1":
+        t, _ = timed(lambda: nt.rp_verify_fold(ZB, Y, rho, V, 1, 1))
+        print(json.dumps({"variant": "fused", "n": n, "ms": round(1e3 * t, 2), "ml_per_s": round(n / t)}), flush=True)
+    for v in VARIANTS:
         tl, lines = timed(lambda: nt.rp_fold_lines(P, V, v))
         for K in (1, 2, 4, 8):
             ta, _ = timed(lambda: nt.rp_fold_accum(lines, n, K, v))
             print(json.dumps({"variant": v, "K": K, "n": n, "lines_ms": round(1e3 * tl, 2), "accum_ms": round(1e3 * ta, 2),
                               "ml_per_s": round(n / (tl + ta))}), flush=True)
         del lines
+        torch.cuda.empty_cache()
+        # shared-V: one coefficient image, G verifiers' points evaluated in the accumulation
+        G = int(os.environ.get("FOLD_G", "3"))
+        tc, coef = timed(lambda: nt.rp_fold_coeffs(V, v))
+        for K in (4, 8):
+            per = 64 * K * nt.FOLD_P_ALIGN
+            pad = -(-n // per) * per
+            PG = torch.zeros((G * pad, 16), dtype=torch.int32, device=dev)
+            for g in range(G):
+                PG[g * pad: g * pad + n] = P
+            ta, _ = timed(lambda: nt.rp_fold_accum_p(coef, PG, V, pad, G, K, v))
+            print(json.dumps({"variant": v + "-sharedV", "G": G, "K": K, "n": n, "coeffs_ms": round(1e3 * tc, 2),
+                              "accum_ms": round(1e3 * ta, 2), "ml_per_s": round(G * n / (tc + ta))}), flush=True)
+            del PG
+        del coef
         torch.cuda.empty_cache()
 
 

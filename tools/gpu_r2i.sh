@@ -11,3 +11,6 @@ DRYNX_TRACE=gpurun_out/trace6000.json timeout -k 10 300 python -u tools/profile_
 rc=$?; head -1 gpurun_out/prof6000.txt; fatal $rc prof
 timeout -k 10 300 python -u tools/bench_scaling.py 3 dps > gpurun_out/scaling_dps.log 2>&1
 rc=$?; cut -c1-200 gpurun_out/scaling_dps.log; fatal $rc scaling
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_lr -o lr -- python3 bench.py --steps 2 --warmup 1 > gpurun_out/bench_prof.log 2>&1
+rc=$?; tail -1 gpurun_out/bench_prof.log | cut -c1-200; fatal $rc rocprof
