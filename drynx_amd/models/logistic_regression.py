@@ -90,6 +90,31 @@ def approx_coefficients(Xa: torch.Tensor, y: torch.Tensor, k: int) -> list:
     return out
 
 
+def distinct_approx_coefficients(x, y: int, k: int) -> list:
+    """ComputeDistinctApproxCoefficients (lib/encoding/logistic_regression.go:
+    322-363) for ONE (augmented) record: level j holds the products over the
+    multisets i_1 <= ... <= i_j of the record's entries, in lexicographic
+    order, times the level's sign -- (2y - 1) for level 1, then the previous
+    level's sign times ypart = y - y (-1)^(j+1) - 1.  The cartesian layout of
+    ``approx_coefficients`` is the same values with every ordering repeated."""
+    import itertools
+
+    xs = [float(v) for v in x]
+    sign = 2.0 * float(y) - 1.0
+    out = []
+    for j in range(1, k + 1):
+        if j > 1:
+            sign *= float(y) - float(y) * (-1.0) ** j - 1.0
+        lvl = []
+        for combo in itertools.combinations_with_replacement(range(len(xs)), j):
+            prod = 1.0
+            for i in combo:
+                prod *= xs[i]
+            lvl.append(prod * sign + 0.0)  # + 0.0: no negative zeros
+        out.append(lvl)
+    return out
+
+
 def lr_moment_gemm(Xa: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """sum_i w_i x_i x_i^T (K13).  On GPU: the native fp64-MFMA kernel."""
     if Xa.is_cuda:

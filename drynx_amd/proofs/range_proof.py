@@ -469,6 +469,11 @@ def create_range_proofs(batch, sigmat: SigMaterial, P_point, device=None, mode: 
         groups.setdefault((batch.u[idx], batch.l[idx]), []).append(idx)
     out = []
     for (u, l), idxs in groups.items():
+        bad = [batch.sig_col[i] for i in idxs
+               if batch.sig_col[i] >= sigmat.n_cols or sigmat.u[batch.sig_col[i]] < u]
+        if bad:
+            raise ValueError(f"query Ranges base u={u} exceeds the input-validation signatures of column(s) "
+                             f"{sorted(set(bad))[:8]} (the CNs signed fewer digits)")
         sel = torch.tensor(idxs, dtype=torch.long, device=batch.cv.device)
         cv = CipherVector(batch.cv.K[sel], batch.cv.C[sel])
         vals = [batch.values[i] for i in idxs]

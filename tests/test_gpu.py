@@ -213,7 +213,15 @@ def test_every_operation_on_gpu(gpu_device, tmp_path, op):
                "inter": [float(all(i in s for s in sets)) for i in range(7)]}[op]
         assert vals[0] == exp
     elif op == "logistic regression":
+        # the weights are the clear-text gradient descent on the clear aggregate
+        # of the DPs' coefficient vectors (nothing lost in encryption/decoding)
+        from drynx_amd.models.logistic_regression import decode_logistic_regression_values
+
+        n = len(next(iter(res.clear_dp.values()))[0])
+        tot = [sum(v[0][i] for v in res.clear_dp.values()) for i in range(n)]
+        exp = decode_logistic_regression_values(tot, lp)
         assert len(vals[0]) == 4
+        assert vals[0] == pytest.approx(list(exp), rel=1e-9, abs=1e-12)
     else:
         n = sq.Query.Operation.NbrOutput
         tot = [sum(v[0][i] for v in res.clear_dp.values()) for i in range(n)]
@@ -408,3 +416,25 @@ def test_shared_v_fold_infinities(gpu_device, K):
         a = nt.final_exp(nt._finish_prod_on_host(fb[v * blk:(v + 1) * blk]))
         b = nt.final_exp(nt._finish_prod_on_host(alone))
         assert bool(nt.gt_eq(a, b).all()), v
+
+
+def test_gpu_ops_match_oracle(gpu_device):
+    """GT exponentiation, G2 scalar multiplication and the G1 MSM on gfx950
+    against the pure-Python oracle (not the native host path)."""
+    ks = [RNG.randrange(O.R) for _ in range(6)] + [0, 1, O.R - 1]
+    kt = bn.scalars_tensor(ks, gpu_device)
+    e = O.pairing(O.G1_GEN, O.G2_GEN)
+    g = nt.gt_pow(bn.gt_tensor([e], gpu_device), kt).cpu()
+    assert bn.gt_from_tensor(g) == [e ** k for k in ks]
+    q = O.g2_mul(7, O.G2_GEN)
+    g2 = nt.g2_mul(bn.g2_aff_tensor([q], gpu_device), kt).cpu()
+    assert bn.g2_points_from_aff(g2) == [None if k % O.R == 0 else O.g2_mul(k, q) for k in ks]
+    g2 = nt.g2_fb_mul(bn.base2_table(gpu_device), kt).cpu()
+    assert bn.g2_points_from_aff(g2) == [None if k % O.R == 0 else O.g2_mul(k, O.G2_GEN) for k in ks]
+    pts = [O.g1_mul(RNG.randrange(1, O.R), O.G1_GEN) for _ in range(300)]
+    sc = [RNG.randrange(O.R) for _ in range(300)]
+    got = nt.g1_msm(bn.g1_jac_tensor(pts, gpu_device), bn.scalars_tensor(sc, gpu_device))
+    exp = None
+    for p, k in zip(pts, sc):
+        exp = O.g1_add(exp, O.g1_mul(k, p))
+    assert bn.g1_points_from_jac(got)[0] == exp

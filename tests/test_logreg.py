@@ -99,3 +99,45 @@ def test_predict_homomorphic_close_to_clear():
     kp = eg.KeyPair.generate()
     he = lr.predict_homomorphic(X, w, eg.pk_table(kp.public), kp.secret, precision=100.0)
     assert torch.allclose(he, lr.predict(X, w), atol=0.01)
+
+
+# literal vectors of lib/encoding/logistic_regression_test.go:20-72 (TestComputeApproxCoefficients)
+_X5 = [0, 1, 2, 3, 4]
+_L2 = [0, 0, 0, 0, 0, 1, 2, 3, 4, 4, 6, 8, 9, 12, 16]
+_L3 = [0] * 15 + [1, 2, 3, 4, 4, 6, 8, 9, 12, 16, 8, 12, 16, 18, 24, 32, 27, 36, 48, 64]
+
+
+@pytest.mark.parametrize("y,k,expected", [
+    (1, 1, [[0, 1, 2, 3, 4]]),
+    (0, 1, [[0, -1, -2, -3, -4]]),
+    (1, 2, [[0, 1, 2, 3, 4], [-v for v in _L2]]),
+    (0, 2, [[0, -1, -2, -3, -4], _L2]),
+    (1, 3, [[0, 1, 2, 3, 4], [-v for v in _L2], [-v for v in _L3]]),
+    (0, 3, [[0, -1, -2, -3, -4], _L2, [-v for v in _L3]]),
+])
+def test_distinct_approx_coefficients_reference_vectors(y, k, expected):
+    from drynx_amd.models.logistic_regression import distinct_approx_coefficients
+
+    assert distinct_approx_coefficients(_X5, y, k) == [[float(v) for v in lvl] for lvl in expected]
+
+
+@pytest.mark.parametrize("y", [0, 1])
+def test_cartesian_coefficients_expand_distinct(y):
+    """The encoder's cartesian layout (approx_coefficients = the reference's
+    ComputeAllApproxCoefficients, one record) holds the multiset product of
+    every ordering.  The two reference functions sign levels >= 2 differently
+    (ComputeAll: ypart_j; Distinct: the running product of the ypart factors,
+    logistic_regression.go:338-361 vs :382-399), so magnitudes are compared."""
+    import itertools
+
+    from drynx_amd.models.logistic_regression import approx_coefficients, distinct_approx_coefficients
+
+    x = [1.0, 0.5, -2.0, 3.0]
+    cart = approx_coefficients(torch.tensor([x], dtype=torch.float64), torch.tensor([y]), 3)
+    dist = distinct_approx_coefficients(x, y, 3)
+    n = len(x)
+    for j in (1, 2, 3):
+        lookup = dict(zip(itertools.combinations_with_replacement(range(n), j), dist[j - 1]))
+        flat = cart[j - 1].tolist()
+        for pos, idx in enumerate(itertools.product(range(n), repeat=j)):
+            assert abs(flat[pos]) == pytest.approx(abs(lookup[tuple(sorted(idx))]))

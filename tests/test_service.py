@@ -280,3 +280,39 @@ def test_skipchain_forward_links_and_update_chain(env):
     tampered = dataclasses.replace(prev, ForwardLinks=[forged])
     with _pt.raises(ValueError):
         skc.update_chain(lambda h: {b.Hash: b for b in chain}.get(h), tampered)
+
+
+def test_malformed_queries_give_bitmap_codes(env):
+    """Queries whose range proofs cannot verify end with a block of 0 codes,
+    not an exception: (a) Ranges too narrow for the DPs' values (u^l = 2:
+    every DP's sum is >= 2), (b) input-validation signatures for a smaller
+    base than the query's Ranges announce (u = 4 keys, Ranges u = 16) as seen
+    by the VNs; a DP asked to prove against such a query refuses up front."""
+    cl, node, client = env
+    sq = make_survey(client, cl, "sum", query_min=1, query_max=3, rows=4, proofs=1, ranges=[2, 1])
+    _, vals, res = client.send_survey_query(sq)
+    codes = res.block.data_block().Proofs
+    rng = {v for k, v in codes.items() if "/range/" in k}
+    assert rng == {prq.PROOF_FALSE}
+    assert {v for k, v in codes.items() if "/aggregation/" in k or "/keyswitch/" in k} == {prq.PROOF_TRUE}
+    assert vals[0][0] == float(sum(v[0][0] for v in res.clear_dp.values()))  # the query result itself is unaffected
+
+    orig = node._range_proofs
+
+    def then_widen(sq, dp_results, proofs):  # proofs made for u = 4; the VNs' query says u = 16
+        orig(sq, dp_results, proofs)
+        sq.Query.Ranges = [[16, 2]]
+
+    sq = make_survey(client, cl, "sum", query_min=0, query_max=3, rows=4, proofs=1, ranges=[4, 2])
+    node._range_proofs = then_widen
+    try:
+        _, _, res = client.send_survey_query(sq)
+    finally:
+        del node._range_proofs
+    codes = res.block.data_block().Proofs
+    assert {v for k, v in codes.items() if "/range/" in k} == {prq.PROOF_FALSE}
+
+    sq = make_survey(client, cl, "sum", query_min=0, query_max=3, rows=4, proofs=1, ranges=[4, 2])
+    sq.Query.Ranges = [[16, 2]]
+    with pytest.raises(ValueError, match="signatures"):
+        client.send_survey_query(sq)

@@ -1,6 +1,6 @@
 """Per-kernel statistics from a rocprofv3 SQLite (rocpd) database: total /
 count / mean time per kernel name, sorted by total; optional time window
-(the last N ms of the trace).  Usage: python tools/rocpd_stats.py db [top]"""
+(the last N ms of the trace).  Usage: python tools/rocpd_stats.py db [top] [last_ms]"""
 import collections
 import sqlite3
 import sys
@@ -9,11 +9,16 @@ import sys
 def main():
     db = sqlite3.connect(sys.argv[1])
     top = int(sys.argv[2]) if len(sys.argv) > 2 else 30
+    last_ms = float(sys.argv[3]) if len(sys.argv) > 3 else None
     names = {r[0]: (r[1], r[2], r[3], r[4]) for r in db.execute(
         "select id, display_name, arch_vgpr_count, accum_vgpr_count, private_segment_size from rocpd_info_kernel_symbol")}
     agg = collections.defaultdict(lambda: [0, 0.0])
     t_min, t_max = None, None
-    for kid, s, e in db.execute("select kernel_id, start, end from rocpd_kernel_dispatch"):
+    rows = db.execute("select kernel_id, start, end from rocpd_kernel_dispatch").fetchall()
+    if last_ms is not None and rows:
+        t_end = max(r[2] for r in rows)
+        rows = [r for r in rows if r[1] >= t_end - last_ms * 1e6]
+    for kid, s, e in rows:
         a = agg[kid]
         a[0] += 1
         a[1] += (e - s) / 1e6
