@@ -389,6 +389,9 @@ int FOLD_NAME(dx_rp_coeffs_)(void *stream, const uint32_t *V_aff, uint32_t *coef
 }
 
 // f_blk: G * period / (64 K) Fp12 partial products, verifier-major.
+// (Taking a lane's items two at a time -- two sparse lines multiplied
+// together first, 23 Fp2 products instead of 26 -- was measured 7% SLOWER:
+// more spills; profiles/r2/fold_bench_pair_ab.log.)
 int FOLD_NAME(dx_rp_accum_p_)(void *stream, const uint32_t *coef, const uint32_t *P_aff, const uint32_t *V_aff,
                               uint32_t *f_blk, int64_t m, int64_t period, int G, int K) {
   using namespace FOLD_NAME(fold_ns_);
@@ -397,7 +400,7 @@ int FOLD_NAME(dx_rp_accum_p_)(void *stream, const uint32_t *coef, const uint32_t
   const int64_t blocks = (int64_t)G * (period / ((int64_t)kWG * K));
   const uint4 *C = reinterpret_cast<const uint4 *>(coef);
   hipStream_t st = (hipStream_t)stream;
-  switch (K) {
+switch (K) {
     case 1: hipLaunchKernelGGL(rp_accum_p_kernel<1>, dim3((unsigned)blocks), dim3(kWG), 0, st, C, P_aff, V_aff, f_blk, m, period, G); break;
     case 2: hipLaunchKernelGGL(rp_accum_p_kernel<2>, dim3((unsigned)blocks), dim3(kWG), 0, st, C, P_aff, V_aff, f_blk, m, period, G); break;
     case 4: hipLaunchKernelGGL(rp_accum_p_kernel<4>, dim3((unsigned)blocks), dim3(kWG), 0, st, C, P_aff, V_aff, f_blk, m, period, G); break;

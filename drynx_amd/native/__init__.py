@@ -120,6 +120,8 @@ _SIGS = {
     "dx_rp_verify_items": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _I],
     "dx_int_moments": [_I, _P, _P, _L, _I, _P, _L, _P, _I, _P, _P],
     "dx_sha256_rows": [_I, _P, _P, _L, _L, _L, _L, _P],
+    "dx_rp_points_glv": [_P, _P, _P, _P, _P, _P, _L, _I, _I],
+    "dx_gt_frob8": [_I, _P, _P, _P, _L],
 }
 
 
@@ -891,6 +893,64 @@ def rp_fold_accum(lines: torch.Tensor, n: int, K: int = 4, variant: str | None =
     if rc:
         raise RuntimeError(f"dx_rp_accum_{v} failed rc={rc}")
     return fb
+
+
+# GLV batch weights (csrc/kernels/dx_glv.hip): rho = a + b * GLV_LAMBDA mod r with
+# a, b 32-bit; phi(x, y) = (GLV_BETA x, y) = [GLV_LAMBDA] on G1; x^GLV_LAMBDA =
+# x^(p^8) on GT.  Both constants are checked against the oracle in the tests.
+GLV_BETA = 0x59E26BCEA0D48BACD4F263F1ACDB5C4F5763473177FFFFFE
+GLV_LAMBDA = 0xB3C4D79D41A917585BFC41088D8DAAA78B17EA66B99C90DD
+_glv_consts: dict = {}
+
+
+def _glv_const(kind: str, device) -> torch.Tensor:
+    from ..crypto import bn254 as _bn
+
+    key = (kind, str(device))
+    if key not in _glv_consts:
+        if kind == "beta":
+            v = _bn.to_tensor(_bn.ints_to_limbs([_bn.mont(GLV_BETA)]), device)
+        else:
+            v = _bn.to_tensor(_bn.ints_to_limbs([GLV_LAMBDA]), device)
+        _glv_consts[key] = v.contiguous()
+    return _glv_consts[key]
+
+
+def glv_weights(n: int, device):
+    """n GLV batch weights: (ab [n, 2] int32 = the 32-bit halves (a, b),
+    rho [n, 8] = a + b * GLV_LAMBDA as canonical scalars)."""
+    from ..crypto import bn254 as _bn
+
+    raw = _bn.random_scalars(n, device)
+    ab = raw[:, :2].contiguous()
+    a = torch.zeros_like(raw)
+    b = torch.zeros_like(raw)
+    a[:, 0] = ab[:, 0]
+    b[:, 0] = ab[:, 1]
+    rho = fr_arith(FR_ADD, a, fr_arith(FR_MUL, b, _glv_const("lambda", device)))
+    return ab, rho
+
+
+def rp_fold_points_glv(ZB_jac: torch.Tensor, Y_jac: torch.Tensor, ab: torch.Tensor, S: int, L: int,
+                       out: torch.Tensor | None = None) -> torch.Tensor:
+    """G1 side of the fold with GLV weights: affine((a + b lambda)(ZB - Y)) per
+    item, one launch -> [n, 16] (GPU only)."""
+    n = _rows(ab, 2)
+    assert ab.dtype == torch.int32 and _rows(ZB_jac, 24) * S == n and _rows(Y_jac, 24) * L == n and ZB_jac.is_cuda
+    P = out if out is not None else torch.empty((n, 16), dtype=torch.int32, device=ab.device)
+    assert P.shape == (n, 16) and P.is_contiguous()
+    _, s = _ctx(ZB_jac, Y_jac, ab)
+    _call("dx_rp_points_glv", s, _ptr(ZB_jac.contiguous()), _ptr(Y_jac.contiguous()), _ptr(ab.contiguous()),
+          _ptr(_glv_const("beta", ab.device)), _ptr(P), n, S, L)
+    return P
+
+
+def gt_frob8(a: torch.Tensor) -> torch.Tensor:
+    """a^(p^8) per row (= a^GLV_LAMBDA on GT)."""
+    out = torch.empty_like(a)
+    g, s = _ctx(a)
+    _call("dx_gt_frob8", g, s, _ptr(a.contiguous()), _ptr(out), _rows(a, 96))
+    return out
 
 
 def rp_fold_coeffs(V_aff: torch.Tensor, variant: str | None = None) -> torch.Tensor:

@@ -685,32 +685,56 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
     # --- per-VN weights: every VN's bucket plans in ONE host sync each
     G, m = n_vn, n * S * l
     w_all = _rand64(G * n, device)                                    # D-equation weights
-    rho_all = _rand64(G * m, device)                                  # pairing-equation weights
+    # pairing-equation weights: rho = a + b lambda (GLV, a and b 32-bit: 2^64
+    # distinct residues, so the same 2^-64 soundness as uniform 64-bit weights;
+    # csrc/kernels/dx_glv.hip) or, with DRYNX_RHO=64, uniform 64-bit
+    glv = os.environ.get("DRYNX_RHO", "glv") == "glv"
+    if glv:
+        ab_all, rho_all = nt.glv_weights(G * m, device)
+    else:
+        ab_all, rho_all = None, _rand64(G * m, device)
     gam_all = _rand64(G * m, device, 40)                              # GT-membership combination
     vid = torch.arange(G, device=device)
-    with timers.span("rp.verify.plans"):
+    vns = [{"rho": rho_all[v * m:(v + 1) * m], "ab": None if ab_all is None else ab_all[v * m:(v + 1) * m]}
+           for v in range(G)]
+    aux = _aux_stream(device) if device.type == "cuda" else None
+    if aux is not None:
+        # the Miller folds (~all of the GPU time) are queued FIRST on this
+        # stream; the MSM / multi-exponentiation bucket plans (host syncs) then
+        # run on the aux stream, so their syncs wait only for aux work and the
+        # GPU never idles while the host plans
+        aux.wait_stream(torch.cuda.current_stream(device))
+        with timers.span("rp.verify.fold_queue"):
+            for v, fb in zip(vns, _miller_fold_multi(ZB, Y, [v["rho"] for v in vns], r.V, S, l,
+                                                       [v["ab"] for v in vns] if glv else None)):
+                v["fb"] = fb
+    with timers.span("rp.verify.plans"), (torch.cuda.stream(aux) if aux is not None else _nullctx()):
         dpts = torch.cat([Cp.contiguous(), r.D.contiguous()]).repeat(G, 1)
         wc = nt.fr_arith(nt.FR_MUL, w_all, r.challenge.repeat(G, 1))
         dsc = torch.cat([torch.stack([wc.view(G, n, 8), w_all.view(G, n, 8)], 1).reshape(-1, 8)])
         dgrp = (vid.view(G, 1, 1) * 2 + torch.arange(2, device=device).view(1, 2, 1)).expand(G, 2, n).reshape(-1)
         dcheck = nt.g1_msm_launch(dpts, dsc.contiguous(), dgrp.to(torch.int32).contiguous(), 2 * G, bits=256)
-        mgrp = torch.cat([vid.repeat_interleave(m), G + vid.repeat_interleave(m)]).to(torch.int32)
-        aux = _aux_stream(device) if device.type == "cuda" else None
-        if aux is not None:
-            aux.wait_stream(torch.cuda.current_stream(device))
-        with (torch.cuda.stream(aux) if aux is not None else _nullctx()):
-            mexp = nt.multi_exp_grouped(r.A, torch.cat([rho_all, gam_all]), mgrp, 2 * G)   # queued on aux
+        if glv:  # prod a^rho = prod a^a' * frob^8(a)^b': 32-bit exponents over (A, frob^8 A)
+            A2 = torch.cat([r.A, nt.gt_frob8(r.A)])
+            k = torch.zeros((2, G, 2 * m, 8), dtype=torch.int32, device=device)
+            abv = ab_all.view(G, m, 2)
+            k[0, :, :m, 0] = abv[:, :, 0]
+            k[0, :, m:, 0] = abv[:, :, 1]
+            k[1, :, :m] = gam_all.view(G, m, 8)
+            mgrp = torch.cat([vid.repeat_interleave(2 * m), G + vid.repeat_interleave(2 * m)]).to(torch.int32)
+            mexp = nt.multi_exp_grouped(A2, k.view(-1, 8), mgrp, 2 * G, W=5)
+        else:
+            mgrp = torch.cat([vid.repeat_interleave(m), G + vid.repeat_interleave(m)]).to(torch.int32)
+            mexp = nt.multi_exp_grouped(r.A, torch.cat([rho_all, gam_all]), mgrp, 2 * G)
         e_all = nt.fr_dot_rows(rho_all, r.zv, G, b_periodic=True)                        # sum rho Zv per VN
         dfull = torch.stack([nt.fr_dot_rows(w_all, r.zr, G, b_periodic=True),
                              nt.fr_dot_rows(w_all, z, G, b_periodic=True)], 1)             # [G, 2, 8]
-    vns = [{"rho": rho_all[v * m:(v + 1) * m]} for v in range(G)]
     if device.type == "cuda":
-        with timers.span("rp.verify.fold_queue"):
-            for v, fb in zip(vns, _miller_fold_multi(ZB, Y, [v["rho"] for v in vns], r.V, S, l)):
-                v["fb"] = fb
         with timers.span("rp.verify.multiexp"):
-            aux.synchronize()
+            aux.synchronize()                                          # aux results are read on this stream/host
             GG = nt.multi_exp_grouped_finish(mexp)                     # [2G, 96]: prod a^rho_v, prod a^gamma_v
+            D_all = nt.g1_msm_finish(dcheck)                           # [2G, 24]
+            e_all, dfull = e_all.cpu(), dfull.cpu()
         with timers.span("rp.verify.fold_wait"):
             for v in vns:
                 v["F"] = nt._finish_prod_on_host(v["fb"])
@@ -720,8 +744,9 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
         for v in vns:
             f = nt.miller_loop(nt.g1_to_affine(nt.g1_mul(T, v["rho"])), r.V)
             v["F"] = nt.gt_prod(f.view(-1, 1, 96), chunk=4).view(1, 96)
-    D_all = nt.g1_msm_finish(dcheck)                                   # [2G, 24]
-    e_all, dfull = e_all.cpu(), dfull.cpu()
+    if device.type != "cuda":
+        D_all = nt.g1_msm_finish(dcheck)                               # [2G, 24]
+        e_all, dfull = e_all.cpu(), dfull.cpu()
     for k, v in enumerate(vns):
         v.update(G=GG[k: k + 1], Gm=GG[G + k: G + k + 1], dfull=dfull[k], e=e_all[k: k + 1],
                  dcheck=D_all[2 * k: 2 * k + 2])
@@ -774,7 +799,7 @@ def fold_k(n_items: int, slots: int = 2048) -> int:
     return best_k
 
 
-def _miller_fold_multi(ZB, Y, rhos: list, V, S: int, L: int) -> list:
+def _miller_fold_multi(ZB, Y, rhos: list, V, S: int, L: int, abs_: list | None = None) -> list:
     """GPU: for each verifier's weights rho_v, per-workgroup partial products
     of ML(rho_it (ZB[p,j] - Y[p,i]), V_it).  The two-phase fold
     (csrc/kernels/fold_body.h) over ALL verifiers at once: one fused G1
@@ -782,7 +807,8 @@ def _miller_fold_multi(ZB, Y, rhos: list, V, S: int, L: int) -> list:
     into a shared point image whose per-verifier blocks are padded to whole
     workgroups, then ONE line-image launch and ONE K-item accumulation (a
     verifier's slice of a multi-GPU node is too short to fill the chip on
-    its own).  The line coefficients depend on V only, so they are computed
+    its own).  ``abs_``: the verifiers' GLV weight halves (a, b), used by the
+    point kernel instead of the full rho.  The line coefficients depend on V only, so they are computed
     ONCE for all verifiers (``rp_fold_coeffs``) and each verifier's points
     are evaluated inside the accumulation (``rp_fold_accum_p``).
     ``DRYNX_FOLD=2`` selects the per-verifier line image, ``fused`` the
@@ -798,7 +824,10 @@ def _miller_fold_multi(ZB, Y, rhos: list, V, S: int, L: int) -> list:
         pad = -(-m // per) * per
         P = torch.zeros((G * pad, 16), dtype=torch.int32, device=V.device)
         for v, rho in enumerate(rhos):
-            nt.rp_fold_points(ZB, Y, rho, S, L, out=P[v * pad: v * pad + m])
+            if abs_ is not None:  # GLV weights: 32-bit joint ladder
+                nt.rp_fold_points_glv(ZB, Y, abs_[v], S, L, out=P[v * pad: v * pad + m])
+            else:
+                nt.rp_fold_points(ZB, Y, rho, S, L, out=P[v * pad: v * pad + m])
         fb = nt.rp_fold_accum_p(nt.rp_fold_coeffs(V.contiguous()), P, V.contiguous(), pad, G, K)
         blk = pad // (64 * K)
         return [fb[v * blk:(v + 1) * blk] for v in range(G)]

@@ -196,7 +196,25 @@ class DrynxNode:
         its own device stream, overlapping the VNs' proof collection -- as in
         the reference, where the querier decodes while the VNs verify
         (service.go:805-868 vs proof_collection_protocol.go); its return value
-        lands in ``SurveyResult.client_out``."""
+        lands in ``SurveyResult.client_out``.
+
+        On a GPU the survey's own (latency-bound: CN phases, short proof
+        checks) launches run on a HIGH-priority stream, so the dispatcher hands
+        them the next free CU slots instead of queueing them behind the
+        long-running workgroups of the range prover / verifier, which keep
+        normal-priority streams (DRYNX_HP_STREAM=0 turns this off)."""
+        if self.device.type != "cuda" or os.environ.get("DRYNX_HP_STREAM", "1") == "0":
+            return self._run_survey(sq, on_result)
+        if not hasattr(self, "_hp_stream"):
+            self._hp_stream = torch.cuda.Stream(self.device, priority=-1)
+        hp, outer = self._hp_stream, torch.cuda.current_stream(self.device)
+        hp.wait_stream(outer)
+        with torch.cuda.stream(hp):
+            out = self._run_survey(sq, on_result)
+        outer.wait_stream(hp)
+        return out
+
+    def _run_survey(self, sq: SurveyQuery | None, on_result=None) -> SurveyResult:
         sq = self._broadcast_query(sq)
         self.surveys[sq.SurveyID] = sq
         if sq.Query.Proofs and sq.Query.RosterVNs is not None and sq.SurveyID not in self.vn_surveys:

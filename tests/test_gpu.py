@@ -110,9 +110,11 @@ def test_lr_encode_fused_matches_torch(gpu_device):
         assert torch.allclose(g2, ref2, rtol=1e-10, atol=1e-8), (g2 - ref2).abs().max()
 
 
-@pytest.mark.parametrize("fold", ["3", "2", "fused"])
+@pytest.mark.parametrize("fold", ["3", "2", "fused", "3-rho64"])
 def test_range_proofs_gpu(gpu_device, fold, monkeypatch):
-    monkeypatch.setenv("DRYNX_FOLD", fold)
+    if fold.endswith("-rho64"):
+        monkeypatch.setenv("DRYNX_RHO", "64")
+    monkeypatch.setenv("DRYNX_FOLD", fold.split("-")[0])
     from drynx_amd.crypto import elgamal as eg
     from drynx_amd.ops.encoding import CreateProofBatch
     from drynx_amd.proofs import range_proof as rp
@@ -438,3 +440,20 @@ def test_gpu_ops_match_oracle(gpu_device):
     for p, k in zip(pts, sc):
         exp = O.g1_add(exp, O.g1_mul(k, p))
     assert bn.g1_points_from_jac(got)[0] == exp
+
+
+def test_glv_points_match_host(gpu_device):
+    """GLV point kernel == affine((a + b lambda)(ZB - Y)) computed with the
+    host path's full-scalar multiplication, incl. T at infinity."""
+    from drynx_amd.proofs import range_proof as rp
+
+    S, L, npj = 2, 3, 9
+    ZB = nt.g1_fb_mul(bn.base_table(gpu_device), bn.random_scalars(npj * L, gpu_device))
+    Y = nt.g1_fb_mul(bn.base_table(gpu_device), bn.random_scalars(npj * S, gpu_device))
+    Y[1] = ZB[0]  # T = ZB - Y = infinity for every item of (p=0, i=1, j=0)
+    m = npj * S * L
+    ab, rho = nt.glv_weights(m, gpu_device)
+    got = nt.rp_fold_points_glv(ZB, Y, ab, S, L).cpu()
+    T = rp._fold_points(ZB.cpu(), Y.cpu(), S, L)
+    exp = nt.g1_to_affine(nt.g1_mul(T, rho.cpu()))
+    assert torch.equal(got, exp)

@@ -143,3 +143,22 @@ def test_g1_msm_grouped_matches_oracle(bits):
         assert out[g] == exp
     one = bn.g1_points_from_jac(nt.g1_msm(bn.g1_jac_tensor(pts), bn.scalars_tensor(ks)))
     assert one[0] == O.g1_mul(sum(k * e for k, e in zip(ks, es)) % O.R, O.G1_GEN)
+
+
+def test_glv_weight_constants_match_oracle():
+    """GLV batch weights (csrc/kernels/dx_glv.hip): phi(x, y) = (beta x, y) is
+    [lambda] on G1 and x^lambda = x^(p^8) on GT; rho = a + b lambda."""
+    from drynx_amd import native as nt
+    from drynx_amd.crypto import bn254 as bn
+    from drynx_amd.crypto import oracle as O
+
+    x = O.g1_mul(987654321, O.G1_GEN)
+    assert O.g1_mul(nt.GLV_LAMBDA, x) == (nt.GLV_BETA * x[0] % O.P, x[1])
+    assert pow(O.P, 8, O.R) == nt.GLV_LAMBDA
+    e = O.pairing(O.G1_GEN, O.G2_GEN) ** 12345
+    got = bn.gt_from_tensor(nt.gt_frob8(bn.gt_tensor([e])))[0]
+    assert got == e ** nt.GLV_LAMBDA
+    ab, rho = nt.glv_weights(64, "cpu")
+    for (a, b), r in zip(ab.tolist(), bn.scalars_from_tensor(rho)):
+        a, b = a & 0xFFFFFFFF, b & 0xFFFFFFFF
+        assert r == a + b * nt.GLV_LAMBDA  # < r: no reduction, all 2^64 (a, b) distinct
