@@ -122,6 +122,12 @@ _SIGS = {
     "dx_sha256_rows": [_I, _P, _P, _L, _L, _L, _L, _P],
     "dx_rp_points_glv": [_P, _P, _P, _P, _P, _P, _L, _I, _I],
     "dx_gt_frob8": [_I, _P, _P, _P, _L],
+    "dx_gls6_entries": [],
+    "dx_g2_gls6_table": [_I, _P, _P, _P, _P, _L],
+    "dx_g2_gls6_mul": [_I, _P, _P, _P, _P, _P, _L],
+    "dx_gt_gls6_table": [_I, _P, _P, _P, _P, _L],
+    "dx_gt_gls6_pow": [_I, _P, _P, _P, _P, _P, _L],
+    "dx_rp_prove_a_gls6": [_I, _P, _P, _P, _P, _P, _P, _P, _L, _I, _I],
 }
 
 
@@ -487,6 +493,50 @@ def g2_fb4_mul(tables: torch.Tensor, scalars: torch.Tensor, tab_idx: torch.Tenso
     return out
 
 
+GLS6_ENTRIES = 1386  # 22 six-bit windows x 63 non-zero digits (csrc/kernels/dx_gls.hip)
+
+
+def g2_gls6_table(base_aff: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """GLS-2 6-bit fixed-base table(s) [n_bases*1386, 32] (177 KiB per base)."""
+    bases = base_aff.contiguous().view(-1, 32)
+    nb = bases.shape[0]
+    table = out if out is not None else torch.empty((nb * GLS6_ENTRIES, 32), dtype=torch.int32, device=bases.device)
+    assert table.shape == (nb * GLS6_ENTRIES, 32) and table.is_contiguous()
+    work = torch.empty((nb * 22, 48), dtype=torch.int32, device=bases.device)
+    g, s = _ctx(bases, table)
+    _call("dx_g2_gls6_table", g, s, _ptr(bases), _ptr(work), _ptr(table), nb)
+    return table
+
+
+def g2_gls6_mul(tables: torch.Tensor, scalars: torch.Tensor, tab_idx: torch.Tensor | None = None) -> torch.Tensor:
+    """k * A (affine) with k = k0 + k1 lambda2, psi(k1 A) + k0 A from one table."""
+    n = _rows(scalars, 8)
+    out = torch.empty((n, 32), dtype=torch.int32, device=scalars.device)
+    g, s = _ctx(tables, scalars, tab_idx)
+    _call("dx_g2_gls6_mul", g, s, _ptr(tables), _ptr(tab_idx), _ptr(scalars), _ptr(out), n)
+    return out
+
+
+def gt_gls6_table(bases: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """GLS-2 6-bit fixed-base table(s) [n_bases*1386, 96] of GT elements (532 KiB per base)."""
+    bases = bases.contiguous()
+    nb = _rows(bases, 96)
+    table = out if out is not None else torch.empty((nb * GLS6_ENTRIES, 96), dtype=torch.int32, device=bases.device)
+    assert table.shape == (nb * GLS6_ENTRIES, 96) and table.is_contiguous()
+    work = torch.empty((nb * 22, 96), dtype=torch.int32, device=bases.device)
+    g, s = _ctx(bases, table)
+    _call("dx_gt_gls6_table", g, s, _ptr(bases), _ptr(work), _ptr(table), nb)
+    return table
+
+
+def gt_gls6_pow(tables: torch.Tensor, scalars: torch.Tensor, tab_idx: torch.Tensor | None = None) -> torch.Tensor:
+    n = _rows(scalars, 8)
+    out = torch.empty((n, 96), dtype=torch.int32, device=scalars.device)
+    g, s = _ctx(tables, scalars, tab_idx)
+    _call("dx_gt_gls6_pow", g, s, _ptr(tables), _ptr(tab_idx), _ptr(scalars), _ptr(out), n)
+    return out
+
+
 def g2_mul(pts_aff: torch.Tensor, scalars: torch.Tensor) -> torch.Tensor:
     n = _rows(scalars, 8)
     np_ = _rows(pts_aff, 32)
@@ -780,11 +830,16 @@ def rp_prove_a(negsB_aff, V_aff, t_sc, gt_table, S: int, L: int) -> torch.Tensor
 
 
 def rp_prove_a_tab(gphi_tables, tab_idx, e_sc, t_sc, gt_table, S: int, L: int, wbits: int = 8) -> torch.Tensor:
-    """wbits = 8: gphi_tables in the 8-bit comb layout; 4: the 4-bit layout (gt_fb4_table)."""
-    assert wbits in (4, 8)
+    """wbits = 8: gphi_tables in the 8-bit comb layout; 4: the 4-bit layout
+    (gt_fb4_table); 6: the GLS-2 6-bit layout (gt_gls6_table)."""
+    assert wbits in (4, 6, 8)
     n = _rows(e_sc, 8)
     out = torch.empty((n, 96), dtype=torch.int32, device=e_sc.device)
     g, s = _ctx(gphi_tables, tab_idx, e_sc, t_sc, gt_table)
+    if wbits == 6:
+        _call("dx_rp_prove_a_gls6", g, s, _ptr(gphi_tables), _ptr(tab_idx), _ptr(e_sc), _ptr(t_sc), _ptr(gt_table),
+              _ptr(out), n, S, L)
+        return out
     _call("dx_rp_prove_a_tab", g, s, _ptr(gphi_tables), _ptr(tab_idx), _ptr(e_sc), _ptr(t_sc), _ptr(gt_table),
           _ptr(out), n, S, L, wbits)
     return out

@@ -162,3 +162,23 @@ def test_glv_weight_constants_match_oracle():
     for (a, b), r in zip(ab.tolist(), bn.scalars_from_tensor(rho)):
         a, b = a & 0xFFFFFFFF, b & 0xFFFFFFFF
         assert r == a + b * nt.GLV_LAMBDA  # < r: no reduction, all 2^64 (a, b) distinct
+
+
+def test_gls6_tables_match_oracle():
+    """GLS-2 6-bit tables (prover mode 6): k A = k0 A + psi(k1 A) and
+    E^k = E^k0 frob(E^k1) with k = k0 + k1 * 6u^2 -- against the oracle."""
+    import random
+
+    from drynx_amd import native as nt
+    from drynx_amd.crypto import bn254 as bn
+    from drynx_amd.crypto import oracle as O
+
+    rng = random.Random(3)
+    A = O.g2_mul(rng.randrange(1, O.R), O.G2_GEN)
+    E = O.pairing(O.g1_mul(5, O.G1_GEN), A)
+    ks = [rng.randrange(O.R) for _ in range(5)] + [0, 1, O.R - 1, 6 * O.U * O.U, 6 * O.U * O.U - 1]
+    kt = bn.scalars_tensor(ks)
+    g2 = nt.g2_gls6_mul(nt.g2_gls6_table(bn.g2_aff_tensor([A])), kt)
+    assert bn.g2_points_from_aff(g2) == [None if k % O.R == 0 else O.g2_mul(k, A) for k in ks]
+    gt = nt.gt_gls6_pow(nt.gt_gls6_table(bn.gt_tensor([E])), kt)
+    assert bn.gt_from_tensor(gt) == [E ** k for k in ks]
