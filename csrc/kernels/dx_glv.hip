@@ -33,7 +33,7 @@ __global__ void __launch_bounds__(kWG) DX_OCC rp_points_glv_kernel(const uint32_
                                                                  const uint32_t *__restrict__ ab,
                                                                  const uint32_t *__restrict__ beta_m,
                                                                  uint32_t *__restrict__ P_aff, int64_t n, int S,
-                                                                 int L) {
+                                                                 int L, int uv) {
   const int64_t it = (int64_t)blockIdx.x * kWG + threadIdx.x;
   if (it >= n) return;
   const int64_t j = it % L, pi = it / L, p = pi / S;
@@ -73,18 +73,37 @@ __global__ void __launch_bounds__(kWG) DX_OCC rp_points_glv_kernel(const uint32_
       g1_madd_i(r, q);
     }
   }
-  at<G1A>(P_aff, it) = to_affine(r);
+  if (!uv) {
+    at<G1A>(P_aff, it) = to_affine(r);
+  } else if (r.is_inf()) {
+    at<G1A>(P_aff, it) = G1A{Fp::zero(), Fp::zero()};
+  } else {  // (x/y, 1/y) = (X Z / Y, Z^3 / Y): the normalised-line fold's point form
+    const Fp iy = finv(r.y);
+    at<G1A>(P_aff, it) = G1A{fmul(fmul(r.x, r.z), iy), fmul(fmul(fsqr(r.z), r.z), iy)};
+  }
 }
 }  // namespace
 
 extern "C" {
+// uv = 1: the points as (x/y, 1/y) (fold mode 4) instead of affine (x, y)
 int dx_rp_points_glv(void *stream, const uint32_t *ZB_jac, const uint32_t *Y_jac, const uint32_t *ab,
-                     const uint32_t *beta_m, uint32_t *P_aff, int64_t n, int S, int L) {
+                     const uint32_t *beta_m, uint32_t *P_aff, int64_t n, int S, int L, int uv) {
   if (n <= 0) return 0;
   const int64_t blocks = (n + kWG - 1) / kWG;
   hipLaunchKernelGGL(rp_points_glv_kernel, dim3((unsigned)blocks), dim3(kWG), 0, (hipStream_t)stream, ZB_jac, Y_jac,
-                     ab, beta_m, P_aff, n, S, L);
+                     ab, beta_m, P_aff, n, S, L, uv);
   return check_hip(hipGetLastError(), "rp_points_glv");
+}
+
+// affine (x, y) -> (x/y, 1/y) in place (infinity stays zeros)
+int dx_g1_aff_to_uv(int on_gpu, void *stream, uint32_t *aff, int64_t n) {
+  auto op = [=] __host__ __device__(int64_t i) {
+    G1A a = at<G1A>(aff, i);
+    if (a.is_inf()) return;
+    const Fp iy = finv(a.y);
+    at<G1A>(aff, i) = G1A{fmul(a.x, iy), iy};
+  };
+  return run(on_gpu, stream, n, op, true, "g1_aff_to_uv");
 }
 
 // out[i] = a[i]^(p^8) (four Frobenius-squared maps; x^(p^8) = x^lambda on GT)

@@ -260,6 +260,205 @@ __global__ void __launch_bounds__(kWG) FOLD_OCC rp_accum_p_kernel(const uint4 *_
   if (lane == 0) at<Fp12>(f_blk, (int64_t)v * (period / ((int64_t)kWG * K)) + qb) = f;
 }
 
+// ---- normalised shared-V variant (fold mode 4).  The final exponentiation
+// kills every factor from Fp6 (p^6 - 1 divides (p^12 - 1) / r), so a line
+// l0 + l1 w + l3 w^3 = (c0 yP) (1 + (c1/c0)(xP/yP) w + (c3/c0)(1/yP) w^3)
+// may be replaced by 1 + (a u) w + (b v) w^3 with a = c1/c0, b = c3/c0 per V
+// (normalised once, shared by every verifier: one Fp2 inversion per item via
+// Montgomery's trick over its 88 steps) and u = xP/yP, v = 1/yP per point (the
+// point kernel's one inversion).  The product by such a line costs 10 Fp2
+// products instead of 13, and the image is 128 B per step instead of 192.
+__device__ __forceinline__ void store_ab(uint4 *img, int64_t n, int s, int64_t it, const Fp2 &a, const Fp2 &b) {
+  const Fp2 *src[2] = {&a, &b};
+#pragma unroll
+  for (int c = 0; c < 2; c++) {
+    const uint32_t *w = reinterpret_cast<const uint32_t *>(src[c]);
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+      img[((int64_t)s * 8 + c * 4 + q) * n + it] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+  }
+}
+
+__device__ __forceinline__ void load_ab(const uint4 *__restrict__ img, int64_t n, int s, int64_t it, Fp2 &a, Fp2 &b) {
+  Fp2 *dst[2] = {&a, &b};
+#pragma unroll
+  for (int c = 0; c < 2; c++) {
+    uint32_t *w = reinterpret_cast<uint32_t *>(dst[c]);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const uint4 v = img[((int64_t)s * 8 + c * 4 + q) * n + it];
+      w[4 * q] = v.x;
+      w[4 * q + 1] = v.y;
+      w[4 * q + 2] = v.z;
+      w[4 * q + 3] = v.w;
+    }
+  }
+}
+
+// one Fp2 per step and item: scratch [step][4][n] uint4
+__device__ __forceinline__ void store_fp2(uint4 *buf, int64_t n, int s, int64_t it, const Fp2 &x) {
+  const uint32_t *w = reinterpret_cast<const uint32_t *>(&x);
+#pragma unroll
+  for (int q = 0; q < 4; q++) buf[((int64_t)s * 4 + q) * n + it] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+}
+
+__device__ __forceinline__ Fp2 load_fp2(const uint4 *buf, int64_t n, int s, int64_t it) {
+  Fp2 x;
+  uint32_t *w = reinterpret_cast<uint32_t *>(&x);
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const uint4 v = buf[((int64_t)s * 4 + q) * n + it];
+    w[4 * q] = v.x;
+    w[4 * q + 1] = v.y;
+    w[4 * q + 2] = v.z;
+    w[4 * q + 3] = v.w;
+  }
+  return x;
+}
+
+// forward half of a step: raw (c1, c3) to the image, c0 and the prefix product
+// before it to scratch
+__device__ __forceinline__ void ncoef_put(uint4 *img, uint4 *c0s, uint4 *pre, int64_t m, int s, int64_t it,
+                                          const Fp2 &c0, const Fp2 &c1, const Fp2 &c3, Fp2 &prod) {
+  store_ab(img, m, s, it, c1, c3);
+  store_fp2(c0s, m, s, it, c0);
+  store_fp2(pre, m, s, it, prod);
+  prod = mul(prod, c0);
+}
+
+__global__ void __launch_bounds__(kWG) FOLD_OCC rp_ncoeffs_kernel(const uint32_t *__restrict__ V_aff,
+                                                                uint4 *__restrict__ img, uint4 *__restrict__ c0s,
+                                                                uint4 *__restrict__ pre, int64_t m) {
+  const int64_t it = (int64_t)blockIdx.x * kWG + threadIdx.x;
+  if (it >= m) return;
+  const G2A Q = at<G2A>(V_aff, it);
+  if (Q.is_inf()) {
+    for (int s = 0; s < kSteps; s++) store_ab(img, m, s, it, Fp2::zero(), Fp2::zero());
+    return;
+  }
+  const Fp2 b2 = Fp2::from_limbs(Curve::B2);
+  Fp2 X = Q.x, Y = Q.y, Z = Fp2::one(), prod = Fp2::one();
+  int s = 0;
+  auto dbl_step = [&]() {
+    Fp2 X2 = sqr(X);
+    const Fp2 c1 = add(dbl(X2), X2);
+    Fp2 Bq = sqr(Y);
+    Fp2 C = sqr(Z);
+    Fp2 H = sub(sub(sqr(add(Y, Z)), Bq), C);
+    Fp2 E = mul(add(dbl(C), C), b2);
+    ncoef_put(img, c0s, pre, m, s++, it, neg(H), c1, sub(E, Bq), prod);
+    Fp2 F = add(dbl(E), E);
+    Fp2 A = mul(X, Y);
+    X = dbl(mul(A, sub(Bq, F)));
+    Z = dbl(dbl(mul(Bq, H)));
+    Fp2 E2 = sqr(E);
+    Y = sub(sqr(add(Bq, F)), dbl(dbl(add(dbl(E2), E2))));
+  };
+  auto add_step = [&](const Fp2 &x2, const Fp2 &y2) {
+    Fp2 th = sub(Y, mul(y2, Z));
+    Fp2 la = sub(X, mul(x2, Z));
+    ncoef_put(img, c0s, pre, m, s++, it, la, neg(th), sub(mul(th, x2), mul(la, y2)), prod);
+    Fp2 C = sqr(th), D = sqr(la);
+    Fp2 E = mul(D, la), F = mul(Z, C), G = mul(X, D);
+    Fp2 H = sub(add(E, F), dbl(G));
+    Y = sub(mul(th, sub(G, H)), mul(Y, E));
+    X = mul(la, H);
+    Z = mul(Z, E);
+  };
+  for (int i = ATE_NAF_LEN - 2; i >= 0; i--) {
+    dbl_step();
+    const int d = ATE_NAF[i];
+    if (d != 0) {
+      asm volatile("" ::: "memory");
+      const G2A qq = at<G2A>(V_aff, it);
+      add_step(qq.x, d > 0 ? qq.y : neg(qq.y));
+    }
+  }
+  asm volatile("" ::: "memory");
+  {
+    const G2A qq = at<G2A>(V_aff, it);
+    add_step(mul(conj(qq.x), Fp2::from_limbs(Frob::TWX1)), mul(conj(qq.y), Fp2::from_limbs(Frob::TWY1)));
+  }
+  asm volatile("" ::: "memory");
+  {
+    const G2A qq = at<G2A>(V_aff, it);
+    add_step(mul(qq.x, Fp2::from_limbs(Frob::TWX2)), neg(mul(qq.y, Fp2::from_limbs(Frob::TWY2))));
+  }
+  // backward: (c1, c3) / c0 with one inversion (Montgomery's trick)
+  Fp2 inv = ::dx::inv(prod);
+  for (int t = kSteps - 1; t >= 0; t--) {
+    const Fp2 inv_t = mul(inv, load_fp2(pre, m, t, it));
+    inv = mul(inv, load_fp2(c0s, m, t, it));
+    Fp2 a, b;
+    load_ab(img, m, t, it, a, b);
+    store_ab(img, m, t, it, mul(a, inv_t), mul(b, inv_t));
+  }
+}
+
+// f * (1 + l1 w + l3 w^3): 10 Fp2 products
+__device__ __forceinline__ Fp12 mul_line1(const Fp12 &f, const Fp2 &l1, const Fp2 &l3) {
+  const Fp6 &g = f.c1;
+  const Fp2 u0 = mul(g.c0, l1), u1 = mul(g.c1, l3);
+  const Fp6 t1 = {add(u0, mul_xi(mul(g.c2, l3))), sub(sub(mul(add(g.c0, g.c1), add(l1, l3)), u0), u1),
+                  add(mul(g.c2, l1), u1)};
+  const Fp6 sm = add(f.c0, f.c1);
+  const Fp2 m0 = add(Fp2::one(), l1);
+  const Fp2 v0 = mul(sm.c0, m0), v1 = mul(sm.c1, l3);
+  const Fp6 t2 = {add(v0, mul_xi(mul(sm.c2, l3))), sub(sub(mul(add(sm.c0, sm.c1), add(m0, l3)), v0), v1),
+                  add(mul(sm.c2, m0), v1)};
+  return {add(f.c0, mul_v(t1)), sub(sub(t2, f.c0), t1)};
+}
+
+template <int K>
+__device__ __forceinline__ void accum_n_step(Fp12 &f, const uint4 *__restrict__ img, const uint32_t *__restrict__ UV,
+                                             int64_t m, int s, int64_t qbase, int64_t pbase, uint32_t live) {
+#pragma unroll 1
+  for (int k = 0; k < K; k++) {
+    if ((live >> k) & 1u) {
+      Fp2 a, b;
+      load_ab(img, m, s, qbase + (int64_t)k * kWG, a, b);
+      const G1A uv = at<G1A>(UV, pbase + (int64_t)k * kWG);  // (u, v) = (x/y, 1/y)
+      f = mul_line1(f, mul_fp(a, uv.x), mul_fp(b, uv.y));
+    }
+  }
+}
+
+// as rp_accum_p_kernel, over the normalised image and (u, v) point images
+template <int K>
+__global__ void __launch_bounds__(kWG) FOLD_OCC rp_accum_n_kernel(const uint4 *__restrict__ img,
+                                                                const uint32_t *__restrict__ UV,
+                                                                const uint32_t *__restrict__ V_aff, uint32_t *f_blk,
+                                                                int64_t m, int64_t period, int G) {
+  __shared__ Fp12 sf[kWG / 2];
+  const int lane = threadIdx.x;
+  const int64_t b = blockIdx.x, slot = b >> 3;
+  const int v = (int)(slot % G);
+  const int64_t qb = (slot / G) * 8 + (b & 7);
+  const int64_t qbase = qb * kWG * K + lane, pbase = (int64_t)v * period + qbase;
+  uint32_t live = 0;
+#pragma unroll 1
+  for (int k = 0; k < K; k++) {
+    const int64_t q = qbase + (int64_t)k * kWG;
+    if (q < m && !at<G1A>(UV, pbase + (int64_t)k * kWG).is_inf() && !at<G2A>(V_aff, q).is_inf()) live |= 1u << k;
+  }
+  Fp12 f = Fp12::one();
+  int s = 0;
+  for (int i = ATE_NAF_LEN - 2; i >= 0; i--) {
+    if (i != ATE_NAF_LEN - 2) f = sqr(f);
+    accum_n_step<K>(f, img, UV, m, s++, qbase, pbase, live);
+    if (ATE_NAF[i] != 0) accum_n_step<K>(f, img, UV, m, s++, qbase, pbase, live);
+  }
+  accum_n_step<K>(f, img, UV, m, s++, qbase, pbase, live);
+  accum_n_step<K>(f, img, UV, m, s++, qbase, pbase, live);
+  for (int h = kWG / 2; h > 0; h >>= 1) {
+    if (lane >= h && lane < 2 * h) sf[lane - h] = f;
+    __syncthreads();
+    if (lane < h) f = mul(f, sf[lane]);
+    __syncthreads();
+  }
+  if (lane == 0) at<Fp12>(f_blk, (int64_t)v * (period / ((int64_t)kWG * K)) + qb) = f;
+}
+
 // G1 side of the fold, one launch per VN: P_it = affine(rho_it (ZB[p*L+j] -
 // Y[p*S+i])) for it = (p*S + i)*L + j -- the gather, the point difference, a
 // 3-bit-window multiplication by the 64-bit batch weight (window table in
@@ -408,6 +607,35 @@ switch (K) {
     default: return -2;
   }
   return check_hip(hipGetLastError(), "rp_accum_p");
+}
+
+// normalised image [steps * 8 * m] uint4 (+ scratch 2 x [steps * 4 * m] uint4)
+int FOLD_NAME(dx_rp_ncoeffs_)(void *stream, const uint32_t *V_aff, uint32_t *img, uint32_t *scratch, int64_t m) {
+  using namespace FOLD_NAME(fold_ns_);
+  if (m <= 0) return 0;
+  const int64_t blocks = (m + kWG - 1) / kWG;
+  uint4 *sc = reinterpret_cast<uint4 *>(scratch);
+  hipLaunchKernelGGL(rp_ncoeffs_kernel, dim3((unsigned)blocks), dim3(kWG), 0, (hipStream_t)stream, V_aff,
+                     reinterpret_cast<uint4 *>(img), sc, sc + (int64_t)kSteps * 4 * m, m);
+  return check_hip(hipGetLastError(), "rp_ncoeffs");
+}
+
+int FOLD_NAME(dx_rp_accum_n_)(void *stream, const uint32_t *img, const uint32_t *UV, const uint32_t *V_aff,
+                              uint32_t *f_blk, int64_t m, int64_t period, int G, int K) {
+  using namespace FOLD_NAME(fold_ns_);
+  if (m <= 0 || G <= 0) return 0;
+  if (period < m || period % ((int64_t)kWG * K * 8) != 0) return -2;
+  const int64_t blocks = (int64_t)G * (period / ((int64_t)kWG * K));
+  const uint4 *C = reinterpret_cast<const uint4 *>(img);
+  hipStream_t st = (hipStream_t)stream;
+  switch (K) {
+    case 1: hipLaunchKernelGGL(rp_accum_n_kernel<1>, dim3((unsigned)blocks), dim3(kWG), 0, st, C, UV, V_aff, f_blk, m, period, G); break;
+    case 2: hipLaunchKernelGGL(rp_accum_n_kernel<2>, dim3((unsigned)blocks), dim3(kWG), 0, st, C, UV, V_aff, f_blk, m, period, G); break;
+    case 4: hipLaunchKernelGGL(rp_accum_n_kernel<4>, dim3((unsigned)blocks), dim3(kWG), 0, st, C, UV, V_aff, f_blk, m, period, G); break;
+    case 8: hipLaunchKernelGGL(rp_accum_n_kernel<8>, dim3((unsigned)blocks), dim3(kWG), 0, st, C, UV, V_aff, f_blk, m, period, G); break;
+    default: return -2;
+  }
+  return check_hip(hipGetLastError(), "rp_accum_n");
 }
 
 // f_blk: ceil(n / (64 K)) Fp12 partial products.

@@ -120,7 +120,12 @@ _SIGS = {
     "dx_rp_verify_items": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _I],
     "dx_int_moments": [_I, _P, _P, _L, _I, _P, _L, _P, _I, _P, _P],
     "dx_sha256_rows": [_I, _P, _P, _L, _L, _L, _L, _P],
-    "dx_rp_points_glv": [_P, _P, _P, _P, _P, _P, _L, _I, _I],
+    "dx_rp_points_glv": [_P, _P, _P, _P, _P, _P, _L, _I, _I, _I],
+    "dx_g1_aff_to_uv": [_I, _P, _P, _L],
+    "dx_rp_ncoeffs_ni": [_P, _P, _P, _P, _L],
+    "dx_rp_accum_n_ni": [_P, _P, _P, _P, _P, _L, _L, _I, _I],
+    "dx_rp_ncoeffs_inl": [_P, _P, _P, _P, _L],
+    "dx_rp_accum_n_inl": [_P, _P, _P, _P, _P, _L, _L, _I, _I],
     "dx_gt_frob8": [_I, _P, _P, _P, _L],
     "dx_gls6_entries": [],
     "dx_g2_gls6_table": [_I, _P, _P, _P, _P, _L],
@@ -987,17 +992,58 @@ def glv_weights(n: int, device):
 
 
 def rp_fold_points_glv(ZB_jac: torch.Tensor, Y_jac: torch.Tensor, ab: torch.Tensor, S: int, L: int,
-                       out: torch.Tensor | None = None) -> torch.Tensor:
+                       out: torch.Tensor | None = None, uv: bool = False) -> torch.Tensor:
     """G1 side of the fold with GLV weights: affine((a + b lambda)(ZB - Y)) per
-    item, one launch -> [n, 16] (GPU only)."""
+    item (or, ``uv``, its (x/y, 1/y) form for the normalised fold), one launch
+    -> [n, 16] (GPU only)."""
     n = _rows(ab, 2)
     assert ab.dtype == torch.int32 and _rows(ZB_jac, 24) * S == n and _rows(Y_jac, 24) * L == n and ZB_jac.is_cuda
     P = out if out is not None else torch.empty((n, 16), dtype=torch.int32, device=ab.device)
     assert P.shape == (n, 16) and P.is_contiguous()
     _, s = _ctx(ZB_jac, Y_jac, ab)
     _call("dx_rp_points_glv", s, _ptr(ZB_jac.contiguous()), _ptr(Y_jac.contiguous()), _ptr(ab.contiguous()),
-          _ptr(_glv_const("beta", ab.device)), _ptr(P), n, S, L)
+          _ptr(_glv_const("beta", ab.device)), _ptr(P), n, S, L, int(uv))
     return P
+
+
+def g1_aff_to_uv_(aff: torch.Tensor) -> torch.Tensor:
+    """In place: affine (x, y) rows -> (x/y, 1/y) (infinity stays zeros)."""
+    g, s = _ctx(aff)
+    _call("dx_g1_aff_to_uv", g, s, _ptr(aff), _rows(aff, 16))
+    return aff
+
+
+def rp_fold_ncoeffs(V_aff: torch.Tensor, variant: str | None = None) -> torch.Tensor:
+    """Normalised shared-V line image: per V and step (c1/c0, c3/c0) ->
+    flat int32 [steps * 8 * m * 4] (fold mode 4, csrc/kernels/fold_body.h)."""
+    v = variant or FOLD_VARIANT
+    m = _rows(V_aff, 32)
+    assert V_aff.is_cuda and V_aff.is_contiguous()
+    steps = getattr(_load(), f"dx_fold_steps_{v}")()
+    img = torch.empty((steps * 8 * m * 4,), dtype=torch.int32, device=V_aff.device)
+    scratch = torch.empty((2 * steps * 4 * m * 4,), dtype=torch.int32, device=V_aff.device)
+    _, s = _ctx(V_aff)
+    rc = getattr(_load(), f"dx_rp_ncoeffs_{v}")(s, _ptr(V_aff), _ptr(img), _ptr(scratch), m)
+    if rc:
+        raise RuntimeError(f"dx_rp_ncoeffs_{v} failed rc={rc}")
+    return img
+
+
+def rp_fold_accum_n(img: torch.Tensor, UV: torch.Tensor, V_aff: torch.Tensor, period: int, G: int, K: int = 4,
+                    variant: str | None = None) -> torch.Tensor:
+    """Normalised shared-V accumulation: G verifiers' (u, v) point images
+    against one normalised line image -> [G * period / (64 K), 96]."""
+    v = variant or FOLD_VARIANT
+    m = _rows(V_aff, 32)
+    assert _rows(UV, 16) == G * period and period >= m and period % (64 * K * FOLD_P_ALIGN) == 0
+    steps = getattr(_load(), f"dx_fold_steps_{v}")()
+    assert img.numel() == steps * 8 * m * 4
+    fb = torch.empty((G * period // (64 * K), 96), dtype=torch.int32, device=UV.device)
+    _, s = _ctx(img, UV, V_aff)
+    rc = getattr(_load(), f"dx_rp_accum_n_{v}")(s, _ptr(img), _ptr(UV), _ptr(V_aff), _ptr(fb), m, period, G, K)
+    if rc:
+        raise RuntimeError(f"dx_rp_accum_n_{v} failed rc={rc}")
+    return fb
 
 
 def gt_frob8(a: torch.Tensor) -> torch.Tensor:

@@ -816,13 +816,27 @@ def _miller_fold_multi(ZB, Y, rhos: list, V, S: int, L: int, abs_: list | None =
     ONCE for all verifiers (``rp_fold_coeffs``) and each verifier's points
     are evaluated inside the accumulation (``rp_fold_accum_p``).
     ``DRYNX_FOLD=2`` selects the per-verifier line image, ``fused`` the
-    one-kernel fold (A/B)."""
+    one-kernel fold (A/B); the default ``4`` normalises every line to
+    1 + (a u) w + (b v) w^3 (10 Fp2 products per line instead of 13)."""
     m = V.shape[0]
     G = len(rhos)
-    mode = os.environ.get("DRYNX_FOLD", "3")
+    mode = os.environ.get("DRYNX_FOLD", "4")
     if mode == "fused":
         return [nt.rp_verify_fold(ZB, Y, rho, V, S, L) for rho in rhos]
     K = fold_k(G * m)
+    if mode == "4":  # normalised lines: (c1/c0, c3/c0) per V, (x/y, 1/y) per point
+        per = 64 * K * nt.FOLD_P_ALIGN
+        pad = -(-m // per) * per
+        UV = torch.zeros((G * pad, 16), dtype=torch.int32, device=V.device)
+        for v, rho in enumerate(rhos):
+            blk = UV[v * pad: v * pad + m]
+            if abs_ is not None:
+                nt.rp_fold_points_glv(ZB, Y, abs_[v], S, L, out=blk, uv=True)
+            else:
+                nt.g1_aff_to_uv_(nt.rp_fold_points(ZB, Y, rho, S, L, out=blk))
+        fb = nt.rp_fold_accum_n(nt.rp_fold_ncoeffs(V.contiguous()), UV, V.contiguous(), pad, G, K)
+        blk = pad // (64 * K)
+        return [fb[v * blk:(v + 1) * blk] for v in range(G)]
     if mode == "3":
         per = 64 * K * nt.FOLD_P_ALIGN
         pad = -(-m // per) * per

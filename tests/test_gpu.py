@@ -110,7 +110,7 @@ def test_lr_encode_fused_matches_torch(gpu_device):
         assert torch.allclose(g2, ref2, rtol=1e-10, atol=1e-8), (g2 - ref2).abs().max()
 
 
-@pytest.mark.parametrize("fold", ["3", "2", "fused", "3-rho64"])
+@pytest.mark.parametrize("fold", ["4", "3", "2", "fused", "4-rho64"])
 def test_range_proofs_gpu(gpu_device, fold, monkeypatch):
     if fold.endswith("-rho64"):
         monkeypatch.setenv("DRYNX_RHO", "64")
@@ -336,7 +336,7 @@ def test_fold_points_match_g1_ops(gpu_device, variant):
     assert torch.equal(got, want)
 
 
-@pytest.mark.parametrize("mode", ["2", "3"])
+@pytest.mark.parametrize("mode", ["2", "3", "4"])
 def test_merged_multi_verifier_fold(gpu_device, mode, monkeypatch):
     """Several verifiers' folds in one padded line image / accumulation (mode
     2) or over one shared coefficient image (mode 3) == each verifier's fold
@@ -457,3 +457,26 @@ def test_glv_points_match_host(gpu_device):
     T = rp._fold_points(ZB.cpu(), Y.cpu(), S, L)
     exp = nt.g1_to_affine(nt.g1_mul(T, rho.cpu()))
     assert torch.equal(got, exp)
+
+
+@pytest.mark.parametrize("K", [1, 8])
+def test_normalised_fold_matches_shared_v(gpu_device, K):
+    """Fold mode 4 (lines normalised to 1 + (a u) w + (b v) w^3) == mode 3
+    after the final exponentiation, with points / V at infinity."""
+    m, G = 700, 2
+    period = -(-m // (64 * K * nt.FOLD_P_ALIGN)) * 64 * K * nt.FOLD_P_ALIGN
+    V = nt.g2_fb_mul(bn.base2_table(gpu_device), bn.random_scalars(m, gpu_device))
+    V[7] = 0
+    P = torch.zeros((G * period, 16), dtype=torch.int32, device=gpu_device)
+    for v in range(G):
+        Pv = nt.g1_to_affine(nt.g1_fb_mul(bn.base_table(gpu_device), bn.random_scalars(m, gpu_device)))
+        Pv[11 + v] = 0
+        P[v * period: v * period + m] = Pv
+    ref = nt.rp_fold_accum_p(nt.rp_fold_coeffs(V), P, V, period, G, K)
+    UV = nt.g1_aff_to_uv_(P.clone())
+    got = nt.rp_fold_accum_n(nt.rp_fold_ncoeffs(V), UV, V, period, G, K)
+    blk = period // (64 * K)
+    for v in range(G):
+        a = nt.final_exp(nt._finish_prod_on_host(got[v * blk:(v + 1) * blk]))
+        b = nt.final_exp(nt._finish_prod_on_host(ref[v * blk:(v + 1) * blk]))
+        assert bool(nt.gt_eq(a, b).all()), v

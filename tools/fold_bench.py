@@ -78,6 +78,21 @@ def main():
             del PG
         del coef
         torch.cuda.empty_cache()
+        # normalised lines (fold mode 4): (c1/c0, c3/c0) per V, (x/y, 1/y) per point
+        tn, img = timed(lambda: nt.rp_fold_ncoeffs(V, v))
+        for K in (4, 8):
+            per = 64 * K * nt.FOLD_P_ALIGN
+            pad = -(-n // per) * per
+            UV = torch.zeros((G * pad, 16), dtype=torch.int32, device=dev)
+            uv1 = nt.g1_aff_to_uv_(P.clone())
+            for g in range(G):
+                UV[g * pad: g * pad + n] = uv1
+            ta, _ = timed(lambda: nt.rp_fold_accum_n(img, UV, V, pad, G, K, v))
+            print(json.dumps({"variant": v + "-normalised", "G": G, "K": K, "n": n, "coeffs_ms": round(1e3 * tn, 2),
+                              "accum_ms": round(1e3 * ta, 2), "ml_per_s": round(G * n / (tn + ta))}), flush=True)
+            del UV
+        del img
+        torch.cuda.empty_cache()
 
 
 if __name__ == "__main__":
