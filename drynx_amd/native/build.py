@@ -38,10 +38,12 @@ def _headers():
 
 
 def _digest(paths):
+    """Content digest of sources/headers, keyed by repo-relative paths (the
+    tree is copied to other locations, e.g. a GPU box, and must not rebuild)."""
     h = hashlib.sha256()
     for p in paths:
         with open(p, "rb") as f:
-            h.update(p.encode() + f.read())
+            h.update(os.path.relpath(p, ROOT).encode() + f.read())
     h.update(" ".join(FLAGS).encode())
     return h.hexdigest()
 
