@@ -133,6 +133,12 @@ _SIGS = {
     "dx_gt_gls6_table": [_I, _P, _P, _P, _P, _L],
     "dx_gt_gls6_pow": [_I, _P, _P, _P, _P, _P, _L],
     "dx_rp_prove_a_gls6": [_I, _P, _P, _P, _P, _P, _P, _P, _L, _I, _I],
+    "dx_g2_joint_table": [_I, _P, _P, _P, _L],
+    "dx_rp_u_joint": [_I, _P, _P, _P, _P, _L, _I, _I, _L],
+    "dx_g2_slice_sum": [_I, _P, _P, _P, _P, _P, _P, _L, _I, _L],
+    "dx_g2_mul_small": [_I, _P, _P, _P, _P, _L],
+    "dx_g2_horner": [_I, _P, _P, _P, _I, _I, _I, _L, _L],
+    "dx_rp_msm_uv": [_I, _P, _P, _P, _L, _I, _L],
 }
 
 
@@ -1131,25 +1137,27 @@ def _multi_exp64_plan(rho: torch.Tensor):
     return _bucket_plan(rho, _ME_W)
 
 
-def _segment_passes_dev(counts, dev):
+def _segment_passes_dev(counts, dev, first_slice: int | None = None):
     """``_segment_passes`` with the per-slice (start, len) arrays built on the
     device: only the per-bucket counts (at most a few thousand) live on the
     host, the millions of slice descriptors of a wide multi-exponentiation
-    never cross PCIe and never run through numpy."""
+    never cross PCIe and never run through numpy.  ``first_slice``: entries
+    per thread in the first pass (later passes use _ME_SLICE)."""
     import numpy as _np
 
     passes = []
     c = _np.asarray(counts, dtype=_np.int64)
     while c.size and c.max() > 1:
-        n_sl = (c + _ME_SLICE - 1) // _ME_SLICE
+        sl = first_slice if (first_slice and not passes) else _ME_SLICE
+        n_sl = (c + sl - 1) // sl
         total = int(n_sl.sum())
         ct = torch.from_numpy(c).to(dev)
         nt_ = torch.from_numpy(n_sl).to(dev)
         first = torch.cumsum(ct, 0) - ct
         b = torch.repeat_interleave(torch.arange(c.size, device=dev), nt_, output_size=total)
         k = torch.arange(total, device=dev) - (torch.cumsum(nt_, 0) - nt_)[b]
-        start = first[b] + k * _ME_SLICE
-        ln = torch.minimum(ct[b] - k * _ME_SLICE, torch.full_like(k, _ME_SLICE)).to(torch.int32)
+        start = first[b] + k * sl
+        ln = torch.minimum(ct[b] - k * sl, torch.full_like(k, sl)).to(torch.int32)
         passes.append((start.contiguous(), ln.contiguous()))
         c = n_sl
     return passes
@@ -1329,6 +1337,134 @@ def g1_msm_finish(h: dict) -> torch.Tensor:
     for w in range(top - 1, -1, -1):
         out = g1_add(g1_mul(out, sh8), rows[:, w].contiguous())
     return out
+
+
+# ----------------------------------------------------------------------------- G2 MSM (verifier mode "msm")
+# csrc/kernels/dx_rpmsm.hip: range-proof batch verification by bilinearity
+G2_JOINT_ENTRIES = 15
+
+
+def g2_joint_table(V_aff: torch.Tensor) -> torch.Tensor:
+    """Per V: the 15 affine points da V + db [lambda] V ((da, db) in [0, 3]^2,
+    not both 0) -> [m * 15, 32]; the U-combination kernel's window table."""
+    m = _rows(V_aff, 32)
+    out = torch.empty((m * G2_JOINT_ENTRIES, 32), dtype=torch.int32, device=V_aff.device)
+    g, s = _ctx(V_aff)
+    _call("dx_g2_joint_table", g, s, _ptr(V_aff.contiguous()), _ptr(out), m)
+    return out
+
+
+def rp_u_joint(table: torch.Tensor, ab: torch.Tensor, n_groups: int, G: int, L: int, out: torch.Tensor,
+               pad: int) -> torch.Tensor:
+    """out[v*pad + q] = affine(sum_j (a + b lambda)_{v, q*L+j} V_{q*L+j}) for every
+    verifier v < G and group q < n_groups (ab [G * n_groups * L, 2] int32)."""
+    assert _rows(table, 32) == n_groups * L * G2_JOINT_ENTRIES and _rows(ab, 2) == G * n_groups * L
+    assert _rows(out, 32) >= (G - 1) * pad + n_groups and pad >= n_groups and out.is_contiguous()
+    g, s = _ctx(table, ab, out)
+    _call("dx_rp_u_joint", g, s, _ptr(table), _ptr(ab.contiguous()), _ptr(out), n_groups, G, L, pad)
+    return out
+
+
+def g2_slice_sum(src: torch.Tensor, idx, start: torch.Tensor, length: torch.Tensor, src_aff: bool,
+                 idx_mod: int = 0) -> torch.Tensor:
+    """out[s] = sum_k src[idx[start[s] + k] % idx_mod] (or src[start[s] + k]),
+    k < length[s], from affine (mixed additions) or Jacobian G2 rows -> Jacobian [n, 48]."""
+    n = start.numel()
+    assert src.shape[-1] == (32 if src_aff else 48)
+    out = torch.empty((n, 48), dtype=torch.int32, device=src.device)
+    g, s = _ctx(src, idx, start, length)
+    _call("dx_g2_slice_sum", g, s, _ptr(src), _ptr(idx), _ptr(start), _ptr(length), _ptr(out), n, int(src_aff),
+          int(idx_mod))
+    return out
+
+
+def g2_mul_small(jac: torch.Tensor, d: torch.Tensor) -> torch.Tensor:
+    """d[i] * jac[i] (Jacobian G2, 0 <= d < 2^31)."""
+    n = _rows(jac, 48)
+    assert d.dtype == torch.int32 and d.numel() == n
+    out = torch.empty_like(jac)
+    g, s = _ctx(jac, d)
+    _call("dx_g2_mul_small", g, s, _ptr(jac.contiguous()), _ptr(d.contiguous()), _ptr(out), n)
+    return out
+
+
+def _window_digits(k: torch.Tensor, c: int, W: int) -> torch.Tensor:
+    """[n, 8] canonical scalars -> [n, W] int64 c-bit window digits (LSB first)."""
+    kk = k.to(torch.int64) & 0xFFFFFFFF
+    mask = (1 << c) - 1
+    cols = []
+    for w in range(W):
+        li, sh = divmod(w * c, 32)
+        if li >= 8:
+            cols.append(torch.zeros_like(kk[:, 0]))
+            continue
+        d = kk[:, li] >> sh
+        if sh + c > 32 and li + 1 < 8:
+            d = d | (kk[:, li + 1] << (32 - sh))
+        cols.append(d & mask)
+    return torch.stack(cols, 1)
+
+
+def g2_msm_launch(P_aff: torch.Tensor, k: torch.Tensor, group: torch.Tensor | None, n_groups: int,
+                  c: int = 13, bits: int = 254, first_slice: int = 32) -> dict:
+    """Bucket plan (ONE host sync, on the bincount) of G independent G2 MSMs
+    out[g] = sum_{t: group_t = g} k_t P[t % m] (m = rows of P_aff, k [n, 8]
+    with n a multiple of m): c-bit windows, keys (g, w, d) sorted on the
+    device.  ``g2_msm_run`` queues the device passes."""
+    dev = P_aff.device
+    n, m = k.shape[0], _rows(P_aff, 32)
+    assert n % m == 0 and (group is None or group.numel() == n)
+    W = -(-bits // c)
+    dig = _window_digits(k, c, W)                                       # [n, W]
+    keys = torch.arange(W, device=dev).view(1, -1) * (1 << c) + dig
+    if group is not None:
+        keys = keys + group.to(device=dev, dtype=torch.int64).view(-1, 1) * (W << c)
+    keep = dig.reshape(-1) != 0
+    item = torch.arange(n, device=dev).view(-1, 1).expand(n, W).reshape(-1)[keep]
+    keys = keys.reshape(-1)[keep]
+    keys, order = torch.sort(keys)
+    item = item[order].contiguous()
+    counts = torch.bincount(keys, minlength=(W << c) * n_groups).cpu().numpy()  # the one host sync
+    bk = counts.nonzero()[0]
+    h = {"G": n_groups, "W": W, "c": c, "m": m, "bk": bk, "item": item}
+    if bk.size:
+        passes = _segment_passes_dev(counts[bk], dev, first_slice)
+        if not passes:  # every bucket holds one entry
+            passes = [(torch.arange(bk.size, device=dev), torch.ones(bk.size, dtype=torch.int32, device=dev))]
+        h["passes"] = passes
+        h["d"] = torch.from_numpy((bk & ((1 << c) - 1)).astype("int32")).to(dev)
+        gws, gcounts = np.unique(bk >> c, return_counts=True)
+        h["gws"] = torch.from_numpy(gws.astype(np.int64)).to(dev)
+        h["gpasses"] = _segment_passes_dev(gcounts, dev)
+    return h
+
+
+def g2_msm_run(P_aff: torch.Tensor, h: dict, out_aff: torch.Tensor, stride: int, offset: int) -> torch.Tensor:
+    """Device passes of a ``g2_msm_launch`` plan, queued on the current stream:
+    bucket sums, weights d B_d, per-(group, window) sums, and one Horner lane
+    per group writing affine(out[g]) to out_aff[g * stride + offset]."""
+    G, W, c = h["G"], h["W"], h["c"]
+    S = torch.zeros((G * W, 48), dtype=torch.int32, device=P_aff.device)   # Jacobian infinity = Z 0
+    if h["bk"].size:
+        cur = None
+        for i, (st, ln) in enumerate(h["passes"]):
+            cur = g2_slice_sum(P_aff if i == 0 else cur, h["item"] if i == 0 else None, st, ln, i == 0,
+                               h["m"] if i == 0 else 0)
+        cur = g2_mul_small(cur, h["d"])
+        for st, ln in h["gpasses"]:
+            cur = g2_slice_sum(cur, None, st, ln, False)
+        S[h["gws"]] = cur
+    g, s = _ctx(S, out_aff)
+    _call("dx_g2_horner", g, s, _ptr(S), _ptr(out_aff), G, W, c, stride, offset)
+    return out_aff
+
+
+def rp_msm_uv(Y_jac: torch.Tensor, UV: torch.Tensor, n_groups: int, G: int, pad: int) -> torch.Tensor:
+    """UV[v*pad + q] = (x/y, 1/y) of -Y_q (q < n_groups) and of B (q = n_groups)."""
+    assert _rows(Y_jac, 24) == n_groups and _rows(UV, 16) >= (G - 1) * pad + n_groups + 1 and pad > n_groups
+    g, s = _ctx(Y_jac, UV)
+    _call("dx_rp_msm_uv", g, s, _ptr(Y_jac.contiguous()), _ptr(UV), n_groups, G, pad)
+    return UV
 
 
 _gt_one_cache: dict = {}

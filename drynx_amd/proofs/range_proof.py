@@ -701,16 +701,24 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
     vid = torch.arange(G, device=device)
     vns = [{"rho": rho_all[v * m:(v + 1) * m], "ab": None if ab_all is None else ab_all[v * m:(v + 1) * m]}
            for v in range(G)]
+    # pairing side: "msm" regroups the product by bilinearity (one G2 MSM and
+    # n*S L-point combinations per VN, n*S + 1 Miller loops); "fold" runs one
+    # Miller loop per item (the two-phase shared-V fold)
+    use_msm = glv and os.environ.get("DRYNX_RPV", "msm") == "msm"
     aux = _aux_stream(device) if device.type == "cuda" else None
     if aux is not None:
-        # the Miller folds (~all of the GPU time) are queued FIRST on this
+        # the pairing work (~all of the GPU time) is queued FIRST on this
         # stream; the MSM / multi-exponentiation bucket plans (host syncs) then
         # run on the aux stream, so their syncs wait only for aux work and the
         # GPU never idles while the host plans
         aux.wait_stream(torch.cuda.current_stream(device))
         with timers.span("rp.verify.fold_queue"):
-            for v, fb in zip(vns, _miller_fold_multi(ZB, Y, [v["rho"] for v in vns], r.V, S, l,
-                                                       [v["ab"] for v in vns] if glv else None)):
+            if use_msm:
+                fbs = _msm_fold_multi(Y, r.zphi, r.V, ab_all, rho_all, G, n, S, l)
+            else:
+                fbs = _miller_fold_multi(ZB, Y, [v["rho"] for v in vns], r.V, S, l,
+                                         [v["ab"] for v in vns] if glv else None)
+            for v, fb in zip(vns, fbs):
                 v["fb"] = fb
     with timers.span("rp.verify.plans"), (torch.cuda.stream(aux) if aux is not None else _nullctx()):
         dpts = torch.cat([Cp.contiguous(), r.D.contiguous()]).repeat(G, 1)
@@ -744,10 +752,14 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
                 v["F"] = nt._finish_prod_on_host(v["fb"])
     else:
         GG = nt.multi_exp_grouped_finish(mexp)
-        T = _fold_points(ZB, Y, S, l)
-        for v in vns:
-            f = nt.miller_loop(nt.g1_to_affine(nt.g1_mul(T, v["rho"])), r.V)
-            v["F"] = nt.gt_prod(f.view(-1, 1, 96), chunk=4).view(1, 96)
+        if use_msm:
+            for v, fb in zip(vns, _msm_fold_multi(Y, r.zphi, r.V, ab_all, rho_all, G, n, S, l)):
+                v["F"] = nt.gt_prod(fb.view(-1, 1, 96), chunk=4).view(1, 96)
+        else:
+            T = _fold_points(ZB, Y, S, l)
+            for v in vns:
+                f = nt.miller_loop(nt.g1_to_affine(nt.g1_mul(T, v["rho"])), r.V)
+                v["F"] = nt.gt_prod(f.view(-1, 1, 96), chunk=4).view(1, 96)
     if device.type != "cuda":
         D_all = nt.g1_msm_finish(dcheck)                               # [2G, 24]
         e_all, dfull = e_all.cpu(), dfull.cpu()
@@ -779,6 +791,49 @@ class _nullctx:
 
     def __exit__(self, *a):
         return False
+
+
+def _msm_fold_multi(Y, zphi, V, ab_all, rho_all, G: int, n: int, S: int, L: int) -> list:
+    """Pairing side of G verifiers' batches regrouped by bilinearity
+    (csrc/kernels/dx_rpmsm.hip):
+        prod_it ML(rho_it (Zphi_pj B - Y_pi), V_it)
+          ~ ML(B, R_v) * prod_q ML(-Y_q, U_vq)         (equal after the final exp)
+    with R_v = sum_it (rho_it Zphi_pj) V_it (one Pippenger G2 MSM per VN, all
+    VNs in one bucket plan) and U_vq = sum_j rho_(q,j) V_(q,j) (q = p*S + i; a
+    joint 2-bit-window ladder over the 15-entry per-V table shared by the
+    VNs).  GPU: the U's and R's land in one list (VN-major, blocks padded to
+    whole accumulation workgroups) that the normalised fold kernels pair
+    with uv(-Y_q) / uv(B); returns each VN's per-workgroup partial products.
+    Host: per-item Miller loops over the same n*S + 1 pairs per VN."""
+    dev = V.device
+    m, nq = n * S * L, n * S
+    # R scalars rho_it * Zphi_(p, j) and the bucket plan (the one host sync)
+    it = torch.arange(m, device=dev)
+    zi = (it // (S * L)) * L + it % L
+    s_r = nt.fr_arith(nt.FR_MUL, rho_all, zphi.index_select(0, zi).repeat(G, 1).contiguous())
+    grp = torch.arange(G, device=dev, dtype=torch.int32).repeat_interleave(m)
+    with timers.span("rp.verify.msm_plan"):
+        hR = nt.g2_msm_launch(V, s_r, grp, G)
+    table = nt.g2_joint_table(V)
+    if dev.type == "cuda":
+        K = fold_k(G * (nq + 1))
+        pad = -(-(nq + 1) // (64 * K)) * (64 * K)
+        period = -(-(G * pad) // (64 * K * nt.FOLD_P_ALIGN)) * (64 * K * nt.FOLD_P_ALIGN)
+        Uall = torch.zeros((G * pad, 32), dtype=torch.int32, device=dev)
+        nt.rp_u_joint(table, ab_all, nq, G, L, Uall, pad)
+        nt.g2_msm_run(V, hR, Uall, pad, nq)
+        UV = torch.zeros((period, 16), dtype=torch.int32, device=dev)
+        nt.rp_msm_uv(Y, UV, nq, G, pad)
+        fb = nt.rp_fold_accum_n(nt.rp_fold_ncoeffs(Uall), UV, Uall, period, 1, K)
+        blk = pad // (64 * K)
+        return [fb[v * blk:(v + 1) * blk] for v in range(G)]
+    pad = nq + 1
+    Uall = torch.zeros((G * pad, 32), dtype=torch.int32, device=dev)
+    nt.rp_u_joint(table, ab_all, nq, G, L, Uall, pad)
+    nt.g2_msm_run(V, hR, Uall, pad, nq)
+    negY = nt.g1_to_affine(nt.g1_add(bn.g1_infinity_jac(nq, dev), Y.contiguous(), subtract=True))
+    P1 = torch.cat([negY, nt.g1_to_affine(bn.g1_jac_tensor([O.G1_GEN], dev))])
+    return [nt.miller_loop(P1, Uall[v * pad:(v + 1) * pad].contiguous()) for v in range(G)]
 
 
 def _fold_points(ZB, Y, S: int, L: int) -> torch.Tensor:

@@ -1,0 +1,150 @@
+"""Range-proof verification by bilinearity (verifier mode "msm",
+csrc/kernels/dx_rpmsm.hip): the G2 joint table, the L-point combinations
+U, the Pippenger G2 MSM and the regrouped pairing product, each against the
+pure-Python oracle (host path here, the gfx950 kernels under -m gpu), and the
+"msm" verifier against the per-item "fold" verifier on the same proofs."""
+import random
+
+import pytest
+import torch
+
+from drynx_amd import native as nt
+from drynx_amd.crypto import bn254 as bn
+from drynx_amd.crypto import elgamal as eg
+from drynx_amd.crypto import oracle as O
+from drynx_amd.ops.encoding import CreateProofBatch
+from drynx_amd.proofs import range_proof as rp
+
+DEVICES = ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)]
+
+
+def _dev(name):
+    if name == "cuda" and not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device(name)
+
+
+def _g2_points(k, seed):
+    rnd = random.Random(seed)
+    return [O.g2_mul(rnd.randrange(1, O.R), O.G2_GEN) for _ in range(k)]
+
+
+def _lam_mul(a: int, b: int, Q):
+    return O.g2_mul((a + b * nt.GLV_LAMBDA) % O.R, Q)
+
+
+@pytest.mark.parametrize("device", DEVICES)
+def test_joint_table_entries(device):
+    dev = _dev(device)
+    pts = _g2_points(3, 1) + [None]                       # None = infinity row
+    V = bn.g2_aff_tensor(pts, dev)
+    T = bn.g2_points_from_aff(nt.g2_joint_table(V).cpu())
+    for i, Q in enumerate(pts):
+        for e in range(15):
+            da, db = (e + 1) % 4, (e + 1) // 4
+            want = None if Q is None else _lam_mul(da, db, Q)
+            assert T[i * 15 + e] == want, (i, da, db)
+
+
+@pytest.mark.parametrize("device", DEVICES)
+def test_u_joint_combinations(device):
+    dev = _dev(device)
+    G, nq, L = 2, 3, 4
+    pts = _g2_points(nq * L, 2)
+    pts[5] = None                                         # an infinity V inside a group
+    V = bn.g2_aff_tensor(pts, dev)
+    rnd = random.Random(3)
+    ab = [[rnd.getrandbits(32), rnd.getrandbits(32)] for _ in range(G * nq * L)]
+    ab[0] = [0, 0]
+    ab_t = torch.tensor(ab, dtype=torch.int64).to(torch.int32).to(dev)
+    pad = nq + 2
+    out = torch.zeros((G * pad, 32), dtype=torch.int32, device=dev)
+    nt.rp_u_joint(nt.g2_joint_table(V), ab_t, nq, G, L, out, pad)
+    got = bn.g2_points_from_aff(out.cpu())
+    for v in range(G):
+        for q in range(nq):
+            acc = None
+            for j in range(L):
+                Q = pts[q * L + j]
+                if Q is not None:
+                    a, b = ab[(v * nq + q) * L + j]
+                    acc = O.g2_add(acc, _lam_mul(a, b, Q))
+            assert got[v * pad + q] == acc, (v, q)
+        assert got[v * pad + nq] is None                  # untouched rows stay infinity
+
+
+@pytest.mark.parametrize("device", DEVICES)
+@pytest.mark.parametrize("c", [13, 4])
+def test_g2_msm_grouped(device, c):
+    dev = _dev(device)
+    m, G = 11, 3
+    pts = _g2_points(m, 4)
+    V = bn.g2_aff_tensor(pts, dev)
+    rnd = random.Random(5)
+    ks = [rnd.randrange(O.R) for _ in range(G * m)]
+    ks[2] = 0
+    ks[7] = O.R - 1
+    k = bn.scalars_tensor(ks, dev)
+    grp = torch.arange(G, dtype=torch.int32, device=dev).repeat_interleave(m)
+    h = nt.g2_msm_launch(V, k, grp, G, c=c)
+    stride, off = 4, 1
+    out = torch.zeros((G * stride, 32), dtype=torch.int32, device=dev)
+    nt.g2_msm_run(V, h, out, stride, off)
+    got = bn.g2_points_from_aff(out.cpu())
+    for g in range(G):
+        want = None
+        for t in range(m):
+            want = O.g2_add(want, O.g2_mul(ks[g * m + t], pts[t]))
+        assert got[g * stride + off] == want, g
+
+
+@pytest.fixture(scope="module")
+def proofs():
+    S, u, l = 2, 4, 3
+    sigs = [[rp.init_range_proof_signature(u) for _ in range(3)] for _ in range(S)]
+    kps = [eg.KeyPair.generate() for _ in range(S)]
+    P = eg.aggregate_keys([k.public for k in kps])
+    sm = rp.SigMaterial(sigs)
+    vals = [0, 17, 63, 5]
+    cv, r = eg.encrypt_ints(eg.pk_table(P), vals)
+    n = len(vals)
+    b = CreateProofBatch(vals, r, cv, [u] * n, [l] * n, [0, 1, 2, 0], [0] * n)
+    return rp.create_range_proofs(b, sm, P)[0], sm, P
+
+
+@pytest.mark.parametrize("device", DEVICES)
+def test_msm_pairing_product_matches_per_item_fold(device, proofs):
+    """FE(ML(B, R) prod ML(-Y_q, U_q)) == FE(prod_it ML(rho (Zphi B - Y), V_it))
+    for the same weights: the regrouping is an identity, not a new check."""
+    dev = _dev(device)
+    rpl, sm, _ = proofs
+    r = rpl.to(dev)
+    n, l, S = len(r), r.l, r.S
+    m, G = n * S * l, 2
+    ZB = nt.g1_fb_mul(bn.base_table(dev), r.zphi)
+    y_idx = (torch.arange(S, device=dev).view(1, S) * sm.n_cols
+             + torch.tensor(r.cols, device=dev).view(n, 1)).reshape(-1)
+    Y = nt.g1_mul(sm.y_jac.to(dev).index_select(0, y_idx).contiguous(), rp._rep(r.challenge, S))
+    ab, rho = nt.glv_weights(G * m, dev)
+    fbs = rp._msm_fold_multi(Y, r.zphi, r.V, ab, rho, G, n, S, l)
+    T = rp._fold_points(ZB.cpu(), Y.cpu(), S, l)
+    for v in range(G):
+        F_msm = nt._finish_prod_on_host(fbs[v]) if dev.type == "cuda" else \
+            nt.gt_prod(fbs[v].view(-1, 1, 96), chunk=4).view(1, 96)
+        f = nt.miller_loop(nt.g1_to_affine(nt.g1_mul(T, rho[v * m:(v + 1) * m].cpu().contiguous())), r.V.cpu())
+        F_fold = nt.gt_prod(f.view(-1, 1, 96), chunk=4).view(1, 96)
+        assert bool(nt.gt_eq(nt.final_exp(F_msm.cpu()), nt.final_exp(F_fold)).all()), v
+
+
+@pytest.mark.parametrize("device", DEVICES)
+@pytest.mark.parametrize("mode", ["msm", "fold"])
+def test_both_verifier_modes_accept_and_reject(device, mode, proofs, monkeypatch):
+    dev = _dev(device)
+    monkeypatch.setenv("DRYNX_RPV", mode)
+    rpl, sm, P = proofs
+    assert rp.verify_range_proof_list_multi(rpl.to(dev), sm, P, 3, dev) == [True] * 3
+    bad = rpl.to(dev)
+    V = bad.V.clone()
+    V[4] = V[5]                                           # a valid G2 point, wrong item
+    bad.V = V
+    assert rp.verify_range_proof_list_multi(bad, sm, P, 2, dev) == [False] * 2
