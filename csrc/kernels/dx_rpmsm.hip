@@ -102,7 +102,7 @@ DX_HD void u_joint_one(const uint32_t *T_aff, const uint32_t *ab, uint32_t *U_af
   at<G2A>(U_aff, v * pad + q) = to_affine(acc);
 }
 
-DX_HD void slice_sum_one(const uint32_t *src, const int64_t *idx, const int64_t *start, const int32_t *len,
+DX_HD void slice_sum_one(const uint32_t *src, const int32_t *idx, const int64_t *start, const int32_t *len,
                          uint32_t *out, int src_aff, int64_t idx_mod, int64_t s) {
   const int64_t b = start[s];
   const int n = len[s];
@@ -157,7 +157,29 @@ DX_HD void msm_uv_one(const uint32_t *Y_jac, uint32_t *UV, int64_t n_groups, int
   at<G1A>(UV, v * pad + q) = G1A{fmul(a.x, iy), iy};
 }
 
+// Bucket keys of a c-bit-window Pippenger plan: entry (t, w) of the n x W
+// grid gets key ((g_t W + w) << c) | d_tw and item t, or the sentinel key
+// 0x7fffffff (sorted past every bucket) when its digit d_tw is zero.
+DX_HD void msm_keys_one(const uint32_t *k, const int32_t *grp, int64_t n, int c, int W, int32_t *keys,
+                        int32_t *items, int64_t e) {
+  const int64_t t = e / W;
+  const int w = (int)(e % W);
+  const uint32_t *kt = k + 8 * t;
+  const int bit = w * c, li = bit >> 5, sh = bit & 31;
+  uint32_t d = li < 8 ? kt[li] >> sh : 0u;
+  if (sh + c > 32 && li + 1 < 8) d |= kt[li + 1] << (32 - sh);
+  d &= (1u << c) - 1u;
+  const int64_t g = grp ? grp[t] : 0;
+  keys[e] = d ? (int32_t)((((int64_t)g * W + w) << c) | d) : 0x7fffffff;
+  items[e] = (int32_t)t;
+}
+
 #define DX_TID() const int64_t i = (int64_t)blockIdx.x * kWG + threadIdx.x
+__global__ void __launch_bounds__(256) msm_keys_kernel(const uint32_t *k, const int32_t *grp, int64_t n, int c, int W,
+                                                       int32_t *keys, int32_t *items) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n * W) msm_keys_one(k, grp, n, c, W, keys, items, i);
+}
 __global__ void __launch_bounds__(kWG) DX_OCC joint_table_kernel(const uint32_t *V, uint32_t *T, int64_t m) {
   DX_TID();
   if (i < m) joint_table_one(V, T, i);
@@ -167,7 +189,7 @@ __global__ void __launch_bounds__(kWG) DX_OCC u_joint_kernel(const uint32_t *T, 
   DX_TID();
   if (i < n) u_joint_one(T, ab, U, n_groups, L, pad, i);
 }
-__global__ void __launch_bounds__(kWG) DX_OCC slice_sum_kernel(const uint32_t *src, const int64_t *idx,
+__global__ void __launch_bounds__(kWG) DX_OCC slice_sum_kernel(const uint32_t *src, const int32_t *idx,
                                                               const int64_t *start, const int32_t *len,
                                                               uint32_t *out, int src_aff, int64_t idx_mod,
                                                               int64_t n) {
@@ -196,6 +218,18 @@ inline dim3 grid_of(int64_t n) { return dim3((unsigned)((n + kWG - 1) / kWG)); }
 
 extern "C" {
 
+int dx_msm_keys(int on_gpu, void *stream, const uint32_t *k, const int32_t *grp, int64_t n, int c, int W,
+                int32_t *keys, int32_t *items) {
+  if (n <= 0) return 0;
+  if (!on_gpu) {
+    host_for_each(n * W, [=](int64_t e) { msm_keys_one(k, grp, n, c, W, keys, items, e); });
+    return 0;
+  }
+  hipLaunchKernelGGL(msm_keys_kernel, dim3((unsigned)((n * W + 255) / 256)), dim3(256), 0, (hipStream_t)stream, k,
+                     grp, n, c, W, keys, items);
+  return check_hip(hipGetLastError(), "msm_keys");
+}
+
 int dx_g2_joint_table(int on_gpu, void *stream, const uint32_t *V_aff, uint32_t *T_aff, int64_t m) {
   if (m <= 0) return 0;
   if (!on_gpu) {
@@ -223,7 +257,7 @@ int dx_rp_u_joint(int on_gpu, void *stream, const uint32_t *T_aff, const uint32_
 
 // out[s] = sum_{k < len[s]} src[e_k], e_k = idx[start[s] + k] (mod idx_mod when
 // > 0) or start[s] + k; src affine G2 (mixed additions) or Jacobian G2.
-int dx_g2_slice_sum(int on_gpu, void *stream, const uint32_t *src, const int64_t *idx, const int64_t *start,
+int dx_g2_slice_sum(int on_gpu, void *stream, const uint32_t *src, const int32_t *idx, const int64_t *start,
                     const int32_t *len, uint32_t *out, int64_t n_slices, int src_aff, int64_t idx_mod) {
   if (n_slices <= 0) return 0;
   if (!on_gpu) {

@@ -139,6 +139,7 @@ _SIGS = {
     "dx_g2_mul_small": [_I, _P, _P, _P, _P, _L],
     "dx_g2_horner": [_I, _P, _P, _P, _I, _I, _I, _L, _L],
     "dx_rp_msm_uv": [_I, _P, _P, _P, _L, _I, _L],
+    "dx_msm_keys": [_I, _P, _P, _P, _L, _I, _I, _P, _P],
 }
 
 
@@ -1170,17 +1171,18 @@ def _bucket_plan(k: torch.Tensor, W: int, group: torch.Tensor | None = None, n_g
     segmented passes down to one value per non-empty bucket."""
     dev = k.device
     n = k.shape[0]
-    digits = k.contiguous().view(torch.uint8).view(n, 32)[:, :W].to(torch.int64)   # little-endian bytes
-    keys = torch.arange(W, device=dev).view(1, -1) * 256 + digits
-    if group is not None:
-        keys = keys + group.to(device=dev, dtype=torch.int64).view(-1, 1) * (W * 256)
-    keys = keys.reshape(-1)
-    item = torch.arange(n, device=dev).view(-1, 1).expand(n, W).reshape(-1)
-    keep = digits.reshape(-1) != 0
-    keys, item = keys[keep], item[keep]
-    keys, order = torch.sort(keys)
-    item = item[order].contiguous()
-    counts = torch.bincount(keys, minlength=W * 256 * n_groups).cpu().numpy()  # the one host sync
+    nb = W * 256 * n_groups
+    assert n * W < 2 ** 31 and nb < 2 ** 31 - 1
+    keys = torch.empty(n * W, dtype=torch.int32, device=dev)
+    item = torch.empty(n * W, dtype=torch.int32, device=dev)
+    grp = None if group is None else group.to(device=dev, dtype=torch.int32).contiguous()
+    g, s = _ctx(k, keys)
+    _call("dx_msm_keys", g, s, _ptr(k.contiguous()), _ptr(grp), n, 8, W, _ptr(keys), _ptr(item))  # csrc/kernels/dx_rpmsm.hip
+    keys, order = torch.sort(keys)          # zero digits carry a sentinel key that sorts last
+    item = item.index_select(0, order).to(torch.int64)
+    offs = torch.searchsorted(keys, torch.arange(nb + 1, device=dev, dtype=torch.int32))
+    counts = (offs[1:] - offs[:-1]).cpu().numpy()                    # the one host sync
+    item = item[: int(counts.sum())]                                    # drop the zero-digit sentinels
     bk = counts.nonzero()[0]
     passes = _segment_passes_dev(counts[bk], dev)
     # bucket digits and scatter slots, staged now so the run needs no host->device copy
@@ -1370,7 +1372,8 @@ def g2_slice_sum(src: torch.Tensor, idx, start: torch.Tensor, length: torch.Tens
     """out[s] = sum_k src[idx[start[s] + k] % idx_mod] (or src[start[s] + k]),
     k < length[s], from affine (mixed additions) or Jacobian G2 rows -> Jacobian [n, 48]."""
     n = start.numel()
-    assert src.shape[-1] == (32 if src_aff else 48)
+    assert src.shape[-1] == (32 if src_aff else 48) and (idx is None or idx.dtype == torch.int32)
+    assert start.dtype == torch.int64 and length.dtype == torch.int32
     out = torch.empty((n, 48), dtype=torch.int32, device=src.device)
     g, s = _ctx(src, idx, start, length)
     _call("dx_g2_slice_sum", g, s, _ptr(src), _ptr(idx), _ptr(start), _ptr(length), _ptr(out), n, int(src_aff),
@@ -1388,45 +1391,30 @@ def g2_mul_small(jac: torch.Tensor, d: torch.Tensor) -> torch.Tensor:
     return out
 
 
-def _window_digits(k: torch.Tensor, c: int, W: int) -> torch.Tensor:
-    """[n, 8] canonical scalars -> [n, W] int64 c-bit window digits (LSB first)."""
-    kk = k.to(torch.int64) & 0xFFFFFFFF
-    mask = (1 << c) - 1
-    cols = []
-    for w in range(W):
-        li, sh = divmod(w * c, 32)
-        if li >= 8:
-            cols.append(torch.zeros_like(kk[:, 0]))
-            continue
-        d = kk[:, li] >> sh
-        if sh + c > 32 and li + 1 < 8:
-            d = d | (kk[:, li + 1] << (32 - sh))
-        cols.append(d & mask)
-    return torch.stack(cols, 1)
-
-
 def g2_msm_launch(P_aff: torch.Tensor, k: torch.Tensor, group: torch.Tensor | None, n_groups: int,
                   c: int = 13, bits: int = 254, first_slice: int = 32) -> dict:
-    """Bucket plan (ONE host sync, on the bincount) of G independent G2 MSMs
-    out[g] = sum_{t: group_t = g} k_t P[t % m] (m = rows of P_aff, k [n, 8]
-    with n a multiple of m): c-bit windows, keys (g, w, d) sorted on the
-    device.  ``g2_msm_run`` queues the device passes."""
+    """Bucket plan of G independent G2 MSMs out[g] = sum_{t: group_t = g}
+    k_t P[t % m] (m = rows of P_aff, k [n, 8] with n a multiple of m):
+    c-bit windows; int32 keys (g, w, d) built by one kernel (zero digits get
+    a sentinel that sorts last), one radix sort, per-bucket counts by a
+    binary search of the bucket boundaries -- ONE host sync (the counts).
+    ``g2_msm_run`` queues the device passes."""
     dev = P_aff.device
     n, m = k.shape[0], _rows(P_aff, 32)
-    assert n % m == 0 and (group is None or group.numel() == n)
     W = -(-bits // c)
-    dig = _window_digits(k, c, W)                                       # [n, W]
-    keys = torch.arange(W, device=dev).view(1, -1) * (1 << c) + dig
-    if group is not None:
-        keys = keys + group.to(device=dev, dtype=torch.int64).view(-1, 1) * (W << c)
-    keep = dig.reshape(-1) != 0
-    item = torch.arange(n, device=dev).view(-1, 1).expand(n, W).reshape(-1)[keep]
-    keys = keys.reshape(-1)[keep]
+    nb = (W << c) * n_groups
+    assert n % m == 0 and n < 2 ** 31 and nb < 2 ** 31 - 1 and (group is None or group.numel() == n)
+    keys = torch.empty(n * W, dtype=torch.int32, device=dev)
+    items = torch.empty(n * W, dtype=torch.int32, device=dev)
+    grp = None if group is None else group.to(device=dev, dtype=torch.int32).contiguous()
+    g, s = _ctx(k, keys)
+    _call("dx_msm_keys", g, s, _ptr(k.contiguous()), _ptr(grp), n, c, W, _ptr(keys), _ptr(items))
     keys, order = torch.sort(keys)
-    item = item[order].contiguous()
-    counts = torch.bincount(keys, minlength=(W << c) * n_groups).cpu().numpy()  # the one host sync
+    items = items.index_select(0, order).contiguous()
+    offs = torch.searchsorted(keys, torch.arange(nb + 1, device=dev, dtype=torch.int32))
+    counts = (offs[1:] - offs[:-1]).cpu().numpy()                       # the one host sync
     bk = counts.nonzero()[0]
-    h = {"G": n_groups, "W": W, "c": c, "m": m, "bk": bk, "item": item}
+    h = {"G": n_groups, "W": W, "c": c, "m": m, "bk": bk, "item": items[: int(counts.sum())]}
     if bk.size:
         passes = _segment_passes_dev(counts[bk], dev, first_slice)
         if not passes:  # every bucket holds one entry
@@ -1439,11 +1427,11 @@ def g2_msm_launch(P_aff: torch.Tensor, k: torch.Tensor, group: torch.Tensor | No
     return h
 
 
-def g2_msm_run(P_aff: torch.Tensor, h: dict, out_aff: torch.Tensor, stride: int, offset: int) -> torch.Tensor:
+def g2_msm_run(P_aff: torch.Tensor, h: dict) -> torch.Tensor:
     """Device passes of a ``g2_msm_launch`` plan, queued on the current stream:
-    bucket sums, weights d B_d, per-(group, window) sums, and one Horner lane
-    per group writing affine(out[g]) to out_aff[g * stride + offset]."""
-    G, W, c = h["G"], h["W"], h["c"]
+    bucket sums, weights d B_d, per-(group, window) sums -> [G * W, 48]
+    Jacobian window sums (``g2_msm_finish`` combines them)."""
+    G, W = h["G"], h["W"]
     S = torch.zeros((G * W, 48), dtype=torch.int32, device=P_aff.device)   # Jacobian infinity = Z 0
     if h["bk"].size:
         cur = None
@@ -1454,8 +1442,19 @@ def g2_msm_run(P_aff: torch.Tensor, h: dict, out_aff: torch.Tensor, stride: int,
         for st, ln in h["gpasses"]:
             cur = g2_slice_sum(cur, None, st, ln, False)
         S[h["gws"]] = cur
+    return S
+
+
+def g2_msm_finish(S: torch.Tensor, h: dict, out_aff: torch.Tensor | None = None, stride: int = 1,
+                  offset: int = 0) -> torch.Tensor:
+    """Horner over the windows, one lane per group (W*c doublings), on the
+    tensor's device: out_aff[g * stride + offset] = affine(out[g]).  On the
+    host (CPU tensors) a core runs this serial chain ~5x faster than one GPU lane."""
+    G, W, c = h["G"], h["W"], h["c"]
+    if out_aff is None:
+        out_aff = torch.zeros((G, 32), dtype=torch.int32, device=S.device)
     g, s = _ctx(S, out_aff)
-    _call("dx_g2_horner", g, s, _ptr(S), _ptr(out_aff), G, W, c, stride, offset)
+    _call("dx_g2_horner", g, s, _ptr(S.contiguous()), _ptr(out_aff), G, W, c, stride, offset)
     return out_aff
 
 

@@ -697,7 +697,7 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
         ab_all, rho_all = nt.glv_weights(G * m, device)
     else:
         ab_all, rho_all = None, _rand64(G * m, device)
-    gam_all = _rand64(G * m, device, 40)                              # GT-membership combination
+    gam_all = _rand64(m, device, 40)                                  # GT-membership combination
     vid = torch.arange(G, device=device)
     vns = [{"rho": rho_all[v * m:(v + 1) * m], "ab": None if ab_all is None else ab_all[v * m:(v + 1) * m]}
            for v in range(G)]
@@ -712,49 +712,65 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
         # run on the aux stream, so their syncs wait only for aux work and the
         # GPU never idles while the host plans
         aux.wait_stream(torch.cuda.current_stream(device))
-        with timers.span("rp.verify.fold_queue"):
-            if use_msm:
-                fbs = _msm_fold_multi(Y, r.zphi, r.V, ab_all, rho_all, G, n, S, l)
-            else:
-                fbs = _miller_fold_multi(ZB, Y, [v["rho"] for v in vns], r.V, S, l,
-                                         [v["ab"] for v in vns] if glv else None)
-            for v, fb in zip(vns, fbs):
-                v["fb"] = fb
+        if use_msm:
+            # msm: the U side (no plan, no sync) fills this stream at once; the
+            # bucket plans (host syncs) and the R passes go to the high-priority
+            # aux stream, whose short plan kernels then overtake the U kernels
+            with timers.span("rp.verify.msm_queue"):
+                msq = _msm_queue(Y, r.V, ab_all, G, n, S, l)
+                for v, fb in zip(vns, msq["fb"]):
+                    v["fb"] = fb
+        else:
+            with timers.span("rp.verify.fold_queue"):
+                for v, fb in zip(vns, _miller_fold_multi(ZB, Y, [v["rho"] for v in vns], r.V, S, l,
+                                                           [v["ab"] for v in vns] if glv else None)):
+                    v["fb"] = fb
     with timers.span("rp.verify.plans"), (torch.cuda.stream(aux) if aux is not None else _nullctx()):
+        if use_msm and aux is not None:
+            hR = _msm_plan(r.zphi, r.V, rho_all, G, n, S, l)
         dpts = torch.cat([Cp.contiguous(), r.D.contiguous()]).repeat(G, 1)
         wc = nt.fr_arith(nt.FR_MUL, w_all, r.challenge.repeat(G, 1))
         dsc = torch.cat([torch.stack([wc.view(G, n, 8), w_all.view(G, n, 8)], 1).reshape(-1, 8)])
         dgrp = (vid.view(G, 1, 1) * 2 + torch.arange(2, device=device).view(1, 2, 1)).expand(G, 2, n).reshape(-1)
         dcheck = nt.g1_msm_launch(dpts, dsc.contiguous(), dgrp.to(torch.int32).contiguous(), 2 * G, bits=256)
+        # the GT-membership combination is a property of the proof data, not of
+        # a VN's weights: ONE random combination per rank serves every co-hosted VN
         if glv:  # prod a^rho = prod a^a' * frob^8(a)^b': 32-bit exponents over (A, frob^8 A)
             A2 = torch.cat([r.A, nt.gt_frob8(r.A)])
-            k = torch.zeros((2, G, 2 * m, 8), dtype=torch.int32, device=device)
+            k = torch.zeros((G + 1, 2 * m, 8), dtype=torch.int32, device=device)
             abv = ab_all.view(G, m, 2)
-            k[0, :, :m, 0] = abv[:, :, 0]
-            k[0, :, m:, 0] = abv[:, :, 1]
-            k[1, :, :m] = gam_all.view(G, m, 8)
-            mgrp = torch.cat([vid.repeat_interleave(2 * m), G + vid.repeat_interleave(2 * m)]).to(torch.int32)
-            mexp = nt.multi_exp_grouped(A2, k.view(-1, 8), mgrp, 2 * G, W=5)
+            k[:G, :m, 0] = abv[:, :, 0]
+            k[:G, m:, 0] = abv[:, :, 1]
+            k[G, :m] = gam_all
+            mgrp = torch.arange(G + 1, device=device, dtype=torch.int32).repeat_interleave(2 * m)
+            mexp = nt.multi_exp_grouped(A2, k.view(-1, 8), mgrp, G + 1, W=5)
         else:
-            mgrp = torch.cat([vid.repeat_interleave(m), G + vid.repeat_interleave(m)]).to(torch.int32)
-            mexp = nt.multi_exp_grouped(r.A, torch.cat([rho_all, gam_all]), mgrp, 2 * G)
+            mgrp = torch.arange(G + 1, device=device, dtype=torch.int32).repeat_interleave(m)
+            mexp = nt.multi_exp_grouped(r.A, torch.cat([rho_all, gam_all]), mgrp, G + 1)
+        if use_msm and aux is not None:
+            S_R = nt.g2_msm_run(r.V, hR)                               # R window sums, behind the plans
         e_all = nt.fr_dot_rows(rho_all, r.zv, G, b_periodic=True)                        # sum rho Zv per VN
         dfull = torch.stack([nt.fr_dot_rows(w_all, r.zr, G, b_periodic=True),
                              nt.fr_dot_rows(w_all, z, G, b_periodic=True)], 1)             # [G, 2, 8]
     if device.type == "cuda":
         with timers.span("rp.verify.multiexp"):
             aux.synchronize()                                          # aux results are read on this stream/host
-            GG = nt.multi_exp_grouped_finish(mexp)                     # [2G, 96]: prod a^rho_v, prod a^gamma_v
+            GG = nt.multi_exp_grouped_finish(mexp)                     # [G+1, 96]: prod a^rho_v, prod a^gamma
             D_all = nt.g1_msm_finish(dcheck)                           # [2G, 24]
             e_all, dfull = e_all.cpu(), dfull.cpu()
         with timers.span("rp.verify.fold_wait"):
             for v in vns:
                 v["F"] = nt._finish_prod_on_host(v["fb"])
+            if use_msm:
+                for v, f in zip(vns, _msm_r_miller(hR, S_R)):
+                    v["F"] = nt.gt_mul(v["F"], f.view(1, 96))
     else:
         GG = nt.multi_exp_grouped_finish(mexp)
         if use_msm:
-            for v, fb in zip(vns, _msm_fold_multi(Y, r.zphi, r.V, ab_all, rho_all, G, n, S, l)):
-                v["F"] = nt.gt_prod(fb.view(-1, 1, 96), chunk=4).view(1, 96)
+            hR = _msm_plan(r.zphi, r.V, rho_all, G, n, S, l)
+            msq = _msm_queue(Y, r.V, ab_all, G, n, S, l)
+            for v, fb, f in zip(vns, msq["fb"], _msm_r_miller(hR, nt.g2_msm_run(r.V, hR))):
+                v["F"] = nt.gt_mul(nt.gt_prod(fb.view(-1, 1, 96), chunk=4).view(1, 96), f.view(1, 96))
         else:
             T = _fold_points(ZB, Y, S, l)
             for v in vns:
@@ -764,9 +780,13 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
         D_all = nt.g1_msm_finish(dcheck)                               # [2G, 24]
         e_all, dfull = e_all.cpu(), dfull.cpu()
     for k, v in enumerate(vns):
-        v.update(G=GG[k: k + 1], Gm=GG[G + k: G + k + 1], dfull=dfull[k], e=e_all[k: k + 1],
-                 dcheck=D_all[2 * k: 2 * k + 2])
+        v.update(G=GG[k: k + 1], dfull=dfull[k], e=e_all[k: k + 1], dcheck=D_all[2 * k: 2 * k + 2])
     out = []
+    # prime-order part of the a_ij: the independent 40-bit combination in GT
+    # (the smallest prime factor of the cyclotomic cofactor is ~2^38.8: a
+    # non-GT component survives the batch equation AND this test with
+    # probability ~2^-77)
+    m_ok = _gt_in_subgroup(GG[G: G + 1])
     _, gt_tab = gt_generator_table("cpu")
     PB_base = bn.g1_jac_tensor([P_point, O.G1_GEN], "cpu")
     for v in vns:
@@ -774,11 +794,6 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
             G0 = v["dcheck"]
             PB = nt.g1_mul(PB_base, v["dfull"])
             d_ok = bool(nt.g1_eq(nt.g1_sum(torch.stack([G0[0:1], PB[0:1], PB[1:2]])), G0[1:2])[0])
-            # prime-order part of the a_ij: the independent 40-bit combination in
-            # GT (the smallest prime factor of the cyclotomic cofactor is ~2^38.8:
-            # a non-GT component survives the batch equation AND this test with
-            # probability ~2^-77)
-            m_ok = _gt_in_subgroup(v["Gm"])
             lhs = nt.gt_mul(nt.final_exp(v["F"].cpu()), v["G"].cpu())
             eq_ok = bool(nt.gt_eq(lhs, nt.gt_fb_pow(gt_tab, v["e"].cpu())).all())
         out.append(d_ok and m_ok and eq_ok)
@@ -793,47 +808,59 @@ class _nullctx:
         return False
 
 
-def _msm_fold_multi(Y, zphi, V, ab_all, rho_all, G: int, n: int, S: int, L: int) -> list:
-    """Pairing side of G verifiers' batches regrouped by bilinearity
-    (csrc/kernels/dx_rpmsm.hip):
-        prod_it ML(rho_it (Zphi_pj B - Y_pi), V_it)
-          ~ ML(B, R_v) * prod_q ML(-Y_q, U_vq)         (equal after the final exp)
-    with R_v = sum_it (rho_it Zphi_pj) V_it (one Pippenger G2 MSM per VN, all
-    VNs in one bucket plan) and U_vq = sum_j rho_(q,j) V_(q,j) (q = p*S + i; a
-    joint 2-bit-window ladder over the 15-entry per-V table shared by the
-    VNs).  GPU: the U's and R's land in one list (VN-major, blocks padded to
-    whole accumulation workgroups) that the normalised fold kernels pair
-    with uv(-Y_q) / uv(B); returns each VN's per-workgroup partial products.
-    Host: per-item Miller loops over the same n*S + 1 pairs per VN."""
+def _msm_plan(zphi, V, rho_all, G: int, n: int, S: int, L: int) -> dict:
+    """Verifier mode "msm", step 1 (one host sync): the R-MSM bucket plan of
+    every VN, R_v = sum_it (rho_it Zphi_(p, j)) V_it."""
     dev = V.device
-    m, nq = n * S * L, n * S
-    # R scalars rho_it * Zphi_(p, j) and the bucket plan (the one host sync)
+    m = n * S * L
     it = torch.arange(m, device=dev)
     zi = (it // (S * L)) * L + it % L
     s_r = nt.fr_arith(nt.FR_MUL, rho_all, zphi.index_select(0, zi).repeat(G, 1).contiguous())
     grp = torch.arange(G, device=dev, dtype=torch.int32).repeat_interleave(m)
-    with timers.span("rp.verify.msm_plan"):
-        hR = nt.g2_msm_launch(V, s_r, grp, G)
+    return nt.g2_msm_launch(V, s_r, grp, G)
+
+
+def _msm_queue(Y, V, ab_all, G: int, n: int, S: int, L: int) -> dict:
+    """Verifier mode "msm", the U side (no host sync; csrc/kernels/dx_rpmsm.hip):
+    the pairing side of G verifiers' batches regrouped by bilinearity,
+        prod_it ML(rho_it (Zphi_pj B - Y_pi), V_it)
+          ~ ML(B, R_v) * prod_q ML(-Y_q, U_vq)         (equal after the final exp)
+    with U_vq = sum_j rho_(q,j) V_(q,j) (q = p*S + i; a joint 2-bit-window
+    ladder over the 15-entry per-V table shared by the VNs) and R_v the
+    Pippenger G2 MSM of ``_msm_plan`` (queued separately: ``nt.g2_msm_run``,
+    finished by ``_msm_r_miller``).  GPU: the U's of all VNs form one list
+    (VN-major, blocks padded to whole accumulation workgroups) that the
+    normalised fold kernels pair with uv(-Y_q) -> each VN's per-workgroup
+    partial products ("fb"); host: per-item Miller loops over the same pairs."""
+    dev = V.device
+    nq = n * S
     table = nt.g2_joint_table(V)
+    out = {}
     if dev.type == "cuda":
         K = fold_k(G * (nq + 1))
         pad = -(-(nq + 1) // (64 * K)) * (64 * K)
         period = -(-(G * pad) // (64 * K * nt.FOLD_P_ALIGN)) * (64 * K * nt.FOLD_P_ALIGN)
         Uall = torch.zeros((G * pad, 32), dtype=torch.int32, device=dev)
         nt.rp_u_joint(table, ab_all, nq, G, L, Uall, pad)
-        nt.g2_msm_run(V, hR, Uall, pad, nq)
         UV = torch.zeros((period, 16), dtype=torch.int32, device=dev)
         nt.rp_msm_uv(Y, UV, nq, G, pad)
         fb = nt.rp_fold_accum_n(nt.rp_fold_ncoeffs(Uall), UV, Uall, period, 1, K)
         blk = pad // (64 * K)
-        return [fb[v * blk:(v + 1) * blk] for v in range(G)]
-    pad = nq + 1
-    Uall = torch.zeros((G * pad, 32), dtype=torch.int32, device=dev)
-    nt.rp_u_joint(table, ab_all, nq, G, L, Uall, pad)
-    nt.g2_msm_run(V, hR, Uall, pad, nq)
-    negY = nt.g1_to_affine(nt.g1_add(bn.g1_infinity_jac(nq, dev), Y.contiguous(), subtract=True))
-    P1 = torch.cat([negY, nt.g1_to_affine(bn.g1_jac_tensor([O.G1_GEN], dev))])
-    return [nt.miller_loop(P1, Uall[v * pad:(v + 1) * pad].contiguous()) for v in range(G)]
+        out["fb"] = [fb[v * blk:(v + 1) * blk] for v in range(G)]
+    else:
+        Uall = torch.zeros((G * nq, 32), dtype=torch.int32, device=dev)
+        nt.rp_u_joint(table, ab_all, nq, G, L, Uall, nq)
+        negY = nt.g1_to_affine(nt.g1_add(bn.g1_infinity_jac(nq, dev), Y.contiguous(), subtract=True))
+        out["fb"] = [nt.miller_loop(negY, Uall[v * nq:(v + 1) * nq].contiguous()) for v in range(G)]
+    return out
+
+
+def _msm_r_miller(hR, S_dev) -> torch.Tensor:
+    """Host tail of the R side: Horner over the window sums (one core per VN
+    beats one GPU lane at this serial chain) and ML(B, R_v) -> [G, 96] host."""
+    R = nt.g2_msm_finish(S_dev.cpu(), hR)
+    B = nt.g1_to_affine(bn.g1_jac_tensor([O.G1_GEN], "cpu")).repeat(R.shape[0], 1)
+    return nt.miller_loop(B, R)
 
 
 def _fold_points(ZB, Y, S: int, L: int) -> torch.Tensor:
@@ -920,7 +947,7 @@ _aux: dict = {}
 def _aux_stream(device):
     key = str(device)
     if key not in _aux:
-        _aux[key] = torch.cuda.Stream(device)
+        _aux[key] = torch.cuda.Stream(device, priority=-1)  # plans: short kernels overtake the pairing side
     return _aux[key]
 
 

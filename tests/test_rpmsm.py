@@ -89,7 +89,9 @@ def test_g2_msm_grouped(device, c):
     h = nt.g2_msm_launch(V, k, grp, G, c=c)
     stride, off = 4, 1
     out = torch.zeros((G * stride, 32), dtype=torch.int32, device=dev)
-    nt.g2_msm_run(V, h, out, stride, off)
+    nt.g2_msm_finish(nt.g2_msm_run(V, h), h, out, stride, off)     # device Horner lanes
+    assert bn.g2_points_from_aff(nt.g2_msm_finish(nt.g2_msm_run(V, h).cpu(), h).cpu()) == \
+        [bn.g2_points_from_aff(out.cpu())[g * stride + off] for g in range(G)]   # host Horner
     got = bn.g2_points_from_aff(out.cpu())
     for g in range(G):
         want = None
@@ -126,11 +128,15 @@ def test_msm_pairing_product_matches_per_item_fold(device, proofs):
              + torch.tensor(r.cols, device=dev).view(n, 1)).reshape(-1)
     Y = nt.g1_mul(sm.y_jac.to(dev).index_select(0, y_idx).contiguous(), rp._rep(r.challenge, S))
     ab, rho = nt.glv_weights(G * m, dev)
-    fbs = rp._msm_fold_multi(Y, r.zphi, r.V, ab, rho, G, n, S, l)
+    hR = rp._msm_plan(r.zphi, r.V, rho, G, n, S, l)
+    q = rp._msm_queue(Y, r.V, ab, G, n, S, l)
+    fR = rp._msm_r_miller(hR, nt.g2_msm_run(r.V, hR))
     T = rp._fold_points(ZB.cpu(), Y.cpu(), S, l)
     for v in range(G):
-        F_msm = nt._finish_prod_on_host(fbs[v]) if dev.type == "cuda" else \
-            nt.gt_prod(fbs[v].view(-1, 1, 96), chunk=4).view(1, 96)
+        fbv = q["fb"][v]
+        F_msm = nt._finish_prod_on_host(fbv) if dev.type == "cuda" else \
+            nt.gt_prod(fbv.view(-1, 1, 96), chunk=4).view(1, 96)
+        F_msm = nt.gt_mul(F_msm.cpu(), fR[v:v + 1])
         f = nt.miller_loop(nt.g1_to_affine(nt.g1_mul(T, rho[v * m:(v + 1) * m].cpu().contiguous())), r.V.cpu())
         F_fold = nt.gt_prod(f.view(-1, 1, 96), chunk=4).view(1, 96)
         assert bool(nt.gt_eq(nt.final_exp(F_msm.cpu()), nt.final_exp(F_fold)).all()), v
