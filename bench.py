@@ -160,10 +160,12 @@ def main():
         torch.cuda.synchronize()
     t0 = time.perf_counter()
     blocks = []
+    prof = _torch_profiler(rank)
     for _ in range(args.steps):
         res, weights = one_step()
         blocks.append(res.block)
     node.flush_stores()  # proof persistence overlaps the next step; the tail is timed too
+    _torch_profiler_dump(prof, rank)
     comm.barrier()
     if device.type == "cuda":
         torch.cuda.synchronize()
@@ -220,6 +222,33 @@ def main():
     node.close(remove=True)
     if dist.is_initialized():
         dist.destroy_process_group()
+
+
+def _torch_profiler(rank):
+    """DRYNX_TORCH_PROF=<file>: torch.profiler over the timed steps (which
+    torch ops launch the framework kernels' helper copies/fills); off by default."""
+    path = os.environ.get("DRYNX_TORCH_PROF")
+    if not path or rank != 0:
+        return None
+    from torch.profiler import ProfilerActivity, profile
+
+    p = profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True, with_stack=True)
+    p.__enter__()
+    return p
+
+
+def _torch_profiler_dump(p, rank):
+    if p is None:
+        return
+    torch.cuda.synchronize()
+    p.__exit__(None, None, None)
+    path = os.environ["DRYNX_TORCH_PROF"]
+    with open(path, "w") as f:
+        f.write(p.key_averages(group_by_input_shape=True).table(sort_by="cuda_time_total", row_limit=60,
+                                                                max_name_column_width=40, max_shapes_column_width=60))
+        f.write("\n\n")
+        f.write(p.key_averages(group_by_stack_n=6).table(sort_by="cuda_time_total", row_limit=40,
+                                                         max_name_column_width=40))
 
 
 def main_query(args):

@@ -140,6 +140,11 @@ _SIGS = {
     "dx_g2_horner": [_I, _P, _P, _P, _I, _I, _I, _L, _L],
     "dx_rp_msm_uv": [_I, _P, _P, _P, _L, _I, _L],
     "dx_msm_keys": [_I, _P, _P, _P, _L, _I, _I, _P, _P],
+    "dx_gls8_entries": [],
+    "dx_g2_gls8_table": [_I, _P, _P, _P, _P, _L],
+    "dx_gt_gls8_table": [_I, _P, _P, _P, _P, _L],
+    "dx_g2_gls8_mul": [_I, _P, _P, _P, _P, _P, _L],
+    "dx_rp_prove_a_gls8": [_I, _P, _P, _P, _P, _P, _P, _P, _L, _I, _I],
 }
 
 
@@ -549,6 +554,43 @@ def gt_gls6_pow(tables: torch.Tensor, scalars: torch.Tensor, tab_idx: torch.Tens
     return out
 
 
+GLS8_ENTRIES = 2176  # 17 signed byte windows x 128 digits (csrc/kernels/dx_gls8.hip)
+
+
+def g2_gls8_table(base_aff: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """GLS-2 signed 8-bit fixed-base table(s) [n_bases*2176, 32] (272 KiB per base)."""
+    bases = base_aff.contiguous().view(-1, 32)
+    nb = bases.shape[0]
+    table = out if out is not None else torch.empty((nb * GLS8_ENTRIES, 32), dtype=torch.int32, device=bases.device)
+    assert table.shape == (nb * GLS8_ENTRIES, 32) and table.is_contiguous()
+    work = torch.empty((nb * 17, 48), dtype=torch.int32, device=bases.device)
+    g, s = _ctx(bases, table)
+    _call("dx_g2_gls8_table", g, s, _ptr(bases), _ptr(work), _ptr(table), nb)
+    return table
+
+
+def gt_gls8_table(bases: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """GLS-2 signed 8-bit fixed-base table(s) [n_bases*2176, 96] of GT elements (816 KiB per base)."""
+    bases = bases.contiguous()
+    nb = _rows(bases, 96)
+    table = out if out is not None else torch.empty((nb * GLS8_ENTRIES, 96), dtype=torch.int32, device=bases.device)
+    assert table.shape == (nb * GLS8_ENTRIES, 96) and table.is_contiguous()
+    work = torch.empty((nb * 17, 96), dtype=torch.int32, device=bases.device)
+    g, s = _ctx(bases, table)
+    _call("dx_gt_gls8_table", g, s, _ptr(bases), _ptr(work), _ptr(table), nb)
+    return table
+
+
+def g2_gls8_mul(tables: torch.Tensor, scalars: torch.Tensor, tab_idx: torch.Tensor | None = None) -> torch.Tensor:
+    """k * A (affine) from the signed 8-bit GLS-2 table of A: 34 mixed additions."""
+    n = _rows(scalars, 8)
+    assert tab_idx is None or (tab_idx.dtype == torch.int32 and tab_idx.numel() == n)
+    out = torch.empty((n, 32), dtype=torch.int32, device=scalars.device)
+    g, s = _ctx(tables, scalars, tab_idx)
+    _call("dx_g2_gls8_mul", g, s, _ptr(tables), _ptr(tab_idx), _ptr(scalars), _ptr(out), n)
+    return out
+
+
 def g2_mul(pts_aff: torch.Tensor, scalars: torch.Tensor) -> torch.Tensor:
     n = _rows(scalars, 8)
     np_ = _rows(pts_aff, 32)
@@ -843,11 +885,17 @@ def rp_prove_a(negsB_aff, V_aff, t_sc, gt_table, S: int, L: int) -> torch.Tensor
 
 def rp_prove_a_tab(gphi_tables, tab_idx, e_sc, t_sc, gt_table, S: int, L: int, wbits: int = 8) -> torch.Tensor:
     """wbits = 8: gphi_tables in the 8-bit comb layout; 4: the 4-bit layout
-    (gt_fb4_table); 6: the GLS-2 6-bit layout (gt_gls6_table)."""
-    assert wbits in (4, 6, 8)
+    (gt_fb4_table); 6: the GLS-2 6-bit layout (gt_gls6_table); 7: the GLS-2
+    signed 8-bit layout (gt_gls8_table)."""
+    assert wbits in (4, 6, 7, 8)
     n = _rows(e_sc, 8)
     out = torch.empty((n, 96), dtype=torch.int32, device=e_sc.device)
     g, s = _ctx(gphi_tables, tab_idx, e_sc, t_sc, gt_table)
+    if wbits == 7:
+        assert tab_idx.dtype == torch.int32 and tab_idx.numel() == n and n % (S * L) == 0
+        _call("dx_rp_prove_a_gls8", g, s, _ptr(gphi_tables), _ptr(tab_idx), _ptr(e_sc), _ptr(t_sc), _ptr(gt_table),
+              _ptr(out), n, S, L)
+        return out
     if wbits == 6:
         _call("dx_rp_prove_a_gls6", g, s, _ptr(gphi_tables), _ptr(tab_idx), _ptr(e_sc), _ptr(t_sc), _ptr(gt_table),
               _ptr(out), n, S, L)

@@ -159,11 +159,12 @@ class SigMaterial:
     def table_mode(self, device) -> int:
         """Prover comb-table layout for this signature set on ``device``:
         8 (8-bit combs, 4 MiB per distinct point: few distinct points, e.g.
-        InitRangeProofSignatureDeterministic), 6 (GLS-2 tables with 6-bit
-        windows, 693 KiB per point, 44 additions per evaluation: the reference's
-        random per-CN, per-column keys -- 99,360 points for a SPECTF-shaped
-        query with 3 CNs and u = 16, ~66 GiB of HBM), 4 (4-bit combs, 480 KiB
-        per point, 64 additions) or 0 (no
+        InitRangeProofSignatureDeterministic), 7 (GLS-2 tables with signed
+        8-bit windows, 1.09 MiB per point, 34 additions per evaluation: the
+        reference's random per-CN, per-column keys -- 99,360 points for a
+        SPECTF-shaped query with 3 CNs and u = 16, ~111 GB of HBM), 6 (GLS-2
+        with unsigned 6-bit windows, 693 KiB per point, 44 additions), 4 (4-bit
+        combs, 480 KiB per point, 64 additions) or 0 (no
         tables: variable-base G2 + one pairing per item).  Budgets:
         ``DRYNX_PROVER_TABLE_MB`` (8-bit, default 8 GiB on a GPU / 96 MiB on the
         host) and ``DRYNX_PROVER_TABLE4_MB`` (4-bit, default 60% of the free HBM
@@ -181,10 +182,12 @@ class SigMaterial:
             b4 = int(0.6 * torch.cuda.mem_get_info(dev)[0])
         else:
             b4 = 64 << 20
-        if forced in ("0", "4", "6", "8"):
+        if forced in ("0", "4", "6", "7", "8"):
             mode = int(forced)
         elif n * (4 << 20) <= b8:
             mode = 8
+        elif n * nt.GLS8_ENTRIES * (128 + 384) <= b4:
+            mode = 7
         elif n * nt.GLS6_ENTRIES * (128 + 384) <= b4:
             mode = 6
         elif n * nt.FB4_ENTRIES * (128 + 384) <= b4:
@@ -200,15 +203,17 @@ class SigMaterial:
             self._n_distinct = int(torch.unique(self.canon).numel())
         return self._n_distinct
 
-    def _prover_tables4(self, dev, gls: bool = False):
-        """4-bit comb (or, ``gls``, GLS-2 6-bit) tables of EVERY distinct
-        signature point of the set, built once (chunked) and kept in HBM for the
-        set's lifetime; -> (g2, gt, slot of each A index)."""
-        key = ("gls6" if gls else "fb4", str(dev))
+    def _prover_tables4(self, dev, mode: int = 4):
+        """4-bit comb, GLS-2 6-bit (``mode`` 6) or GLS-2 signed 8-bit (7) tables
+        of EVERY distinct signature point of the set, built once (chunked) and
+        kept in HBM for the set's lifetime; -> (g2, gt, slot of each A index)."""
+        key = (mode, str(dev))
         if key not in self._ptab:
             uniq, slot = torch.unique(self.canon, return_inverse=True)
             n = uniq.numel()
-            E = nt.GLS6_ENTRIES if gls else nt.FB4_ENTRIES
+            E, g2_tab, gt_tab = {4: (nt.FB4_ENTRIES, nt.g2_fb4_table, nt.gt_fb4_table),
+                                 6: (nt.GLS6_ENTRIES, nt.g2_gls6_table, nt.gt_gls6_table),
+                                 7: (nt.GLS8_ENTRIES, nt.g2_gls8_table, nt.gt_gls8_table)}[mode]
             g2 = torch.empty((n * E, 32), dtype=torch.int32, device=dev)
             gt = torch.empty((n * E, 96), dtype=torch.int32, device=dev)
             A = self.A.to(dev)
@@ -217,9 +222,9 @@ class SigMaterial:
                 for a in range(0, n, step):
                     b = min(n, a + step)
                     pts = A.index_select(0, uniq[a:b].to(dev)).contiguous()
-                    (nt.g2_gls6_table if gls else nt.g2_fb4_table)(pts, out=g2[a * E: b * E])
+                    g2_tab(pts, out=g2[a * E: b * E])
                     gphi = nt.pairing(bn.g1_generator_aff(dev).expand(b - a, 16).contiguous(), pts)
-                    (nt.gt_gls6_table if gls else nt.gt_fb4_table)(gphi, out=gt[a * E: b * E])
+                    gt_tab(gphi, out=gt[a * E: b * E])
             self._ptab[key] = (g2, gt, slot.to(dev))
         return self._ptab[key]
 
@@ -232,8 +237,8 @@ class SigMaterial:
         mode = self.table_mode(dev)
         if mode == 0:
             return None
-        if mode in (4, 6):
-            g2, gt, slot = self._prover_tables4(dev, gls=mode == 6)
+        if mode in (4, 6, 7):
+            g2, gt, slot = self._prover_tables4(dev, mode)
             return g2, gt, slot.index_select(0, a_idx.to(dev)), mode
         canon = self.canon.to(a_idx.device).index_select(0, a_idx)
         uniq, inv = torch.unique(canon, return_inverse=True)
@@ -558,7 +563,7 @@ def _prove_group(u, l, vals, offs, cols, r, cv, sigmat, P_point, device, mode=0)
         # no pairing and no final exponentiation per (value, server, digit)
         g2_tabs, gphi_tabs, slot, wbits = tabs
         tidx = slot.index_select(0, inv).to(torch.int32).contiguous()
-        V = {4: nt.g2_fb4_mul, 6: nt.g2_gls6_mul, 8: nt.g2_fb_mul}[wbits](g2_tabs, v, tidx)
+        V = {4: nt.g2_fb4_mul, 6: nt.g2_gls6_mul, 7: nt.g2_gls8_mul, 8: nt.g2_fb_mul}[wbits](g2_tabs, v, tidx)
         negs_rep = nt.fr_arith(nt.FR_NEG, s).view(n, 1, l, 8).expand(n, S, l, 8).reshape(-1, 8).contiguous()
         e = nt.fr_arith(nt.FR_MUL, negs_rep, v)
         A = nt.rp_prove_a_tab(gphi_tabs, tidx, e, t, gt_tab, S, l, wbits)

@@ -293,7 +293,7 @@ def test_fb4_combs_match_oracle(gpu_device):
     assert torch.equal(nt.gt_fb4_pow(gt_tab, k), nt.gt_pow(e.expand(len(ks), 96).contiguous(), k))
 
 
-@pytest.mark.parametrize("bits", ["8", "6", "4", "0"])
+@pytest.mark.parametrize("bits", ["8", "7", "6", "4", "0"])
 def test_range_prover_layouts_gpu(gpu_device, bits, monkeypatch):
     """Every prover path on the GPU with random per-CN, per-column keys:
     8-bit combs, the HBM-sized 4-bit combs, and the table-free path

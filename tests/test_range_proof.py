@@ -96,7 +96,7 @@ def test_device_challenge_hash_matches_sha3_512():
     assert got == exp
 
 
-@pytest.mark.parametrize("bits", ["8", "6", "4", "0"])
+@pytest.mark.parametrize("bits", ["8", "7", "6", "4", "0"])
 def test_prover_table_layouts_agree(setup, bits, monkeypatch):
     """8-bit combs, 4-bit (HBM-sized, random per-CN per-column keys) and the
     table-free prover all produce proofs the batched and the per-equation

@@ -1,0 +1,34 @@
+#!/usr/bin/env python3
+"""Per-kernel GPU time of the LAST query in a rocprofv3 kernel trace (CSV):
+queries start at the first ElGamal encryption after a >100 ms gap (as
+gpu_busy.py).  With AMD_SERIALIZE_KERNEL=3 the durations are each kernel's
+cost alone on the chip (no overlap inflation).  Usage: kernel_cost.py trace.csv"""
+import csv
+import sys
+from collections import defaultdict
+
+
+def _name(n: str) -> str:
+    if n.startswith("(anonymous namespace)::"):
+        n = n[len("(anonymous namespace)::"):]
+    if "for_each_kernel" in n and "<" in n:
+        return n.split("<", 1)[1].split("::")[0]
+    return n.split("(")[0][:70]
+
+
+rows = list(csv.DictReader(open(sys.argv[1])))
+iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows)
+enc = [s for s, e, n in iv if "dx_elgamal_encrypt" in n]
+starts = [enc[0]] + [b for a, b in zip(enc, enc[1:]) if b - a > 100e6]
+t0 = starts[-1]
+agg = defaultdict(lambda: [0, 0.0])
+for s, e, n in iv:
+    if s >= t0:
+        a = agg[_name(n)]
+        a[0] += 1
+        a[1] += (e - s) / 1e6
+tot = sum(v[1] for v in agg.values())
+print(f"last query: {sum(v[0] for v in agg.values())} kernels, {tot:.1f} ms of kernel time (serialized)")
+print(f"{'ms':>8} {'n':>6}  kernel")
+for k, (c, ms) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
+    print(f"{ms:8.2f} {c:6d}  {k}")
