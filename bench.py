@@ -246,9 +246,22 @@ def _torch_profiler_dump(p, rank):
     with open(path, "w") as f:
         f.write(p.key_averages(group_by_input_shape=True).table(sort_by="cuda_time_total", row_limit=60,
                                                                 max_name_column_width=40, max_shapes_column_width=60))
-        f.write("\n\n")
-        f.write(p.key_averages(group_by_stack_n=6).table(sort_by="cuda_time_total", row_limit=40,
-                                                         max_name_column_width=40))
+        f.write("\n\n# GPU time of torch ops by (op, innermost framework frame)\n")
+        from collections import defaultdict
+
+        agg, cnt = defaultdict(float), defaultdict(int)
+        for e in p.events():
+            if not e.name.startswith("aten::") or e.cpu_parent is not None and e.cpu_parent.name.startswith("aten::"):
+                continue
+            t = getattr(e, "device_time_total", None) or getattr(e, "cuda_time_total", 0)
+            if t <= 0:
+                continue
+            frames = [fr for fr in (e.stack or []) if "drynx_amd" in fr or "bench.py" in fr]
+            key = (e.name, frames[0] if frames else "?")
+            agg[key] += t
+            cnt[key] += 1
+        for (name, fr), t in sorted(agg.items(), key=lambda kv: -kv[1])[:60]:
+            f.write(f"{t / 1e3:9.2f} ms {cnt[(name, fr)]:5d}  {name:28s} {fr}\n")
 
 
 def main_query(args):

@@ -160,7 +160,7 @@ DX_HD void msm_uv_one(const uint32_t *Y_jac, uint32_t *UV, int64_t n_groups, int
 // Bucket keys of a c-bit-window Pippenger plan: entry (t, w) of the n x W
 // grid gets key ((g_t W + w) << c) | d_tw and item t, or the sentinel key
 // 0x7fffffff (sorted past every bucket) when its digit d_tw is zero.
-DX_HD void msm_keys_one(const uint32_t *k, const int32_t *grp, int64_t n, int c, int W, int32_t *keys,
+DX_HD void msm_keys_one(const uint32_t *k, const int32_t *grp, int64_t gstride, int c, int W, int32_t *keys,
                         int32_t *items, int64_t e) {
   const int64_t t = e / W;
   const int w = (int)(e % W);
@@ -169,16 +169,16 @@ DX_HD void msm_keys_one(const uint32_t *k, const int32_t *grp, int64_t n, int c,
   uint32_t d = li < 8 ? kt[li] >> sh : 0u;
   if (sh + c > 32 && li + 1 < 8) d |= kt[li + 1] << (32 - sh);
   d &= (1u << c) - 1u;
-  const int64_t g = grp ? grp[t] : 0;
+  const int64_t g = grp ? grp[t] : (gstride > 0 ? t / gstride : 0);  // group of entry t: explicit or t / gstride
   keys[e] = d ? (int32_t)((((int64_t)g * W + w) << c) | d) : 0x7fffffff;
   items[e] = (int32_t)t;
 }
 
 #define DX_TID() const int64_t i = (int64_t)blockIdx.x * kWG + threadIdx.x
-__global__ void __launch_bounds__(256) msm_keys_kernel(const uint32_t *k, const int32_t *grp, int64_t n, int c, int W,
-                                                       int32_t *keys, int32_t *items) {
+__global__ void __launch_bounds__(256) msm_keys_kernel(const uint32_t *k, const int32_t *grp, int64_t gstride,
+                                                       int64_t n, int c, int W, int32_t *keys, int32_t *items) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i < n * W) msm_keys_one(k, grp, n, c, W, keys, items, i);
+  if (i < n * W) msm_keys_one(k, grp, gstride, c, W, keys, items, i);
 }
 __global__ void __launch_bounds__(kWG) DX_OCC joint_table_kernel(const uint32_t *V, uint32_t *T, int64_t m) {
   DX_TID();
@@ -218,15 +218,16 @@ inline dim3 grid_of(int64_t n) { return dim3((unsigned)((n + kWG - 1) / kWG)); }
 
 extern "C" {
 
-int dx_msm_keys(int on_gpu, void *stream, const uint32_t *k, const int32_t *grp, int64_t n, int c, int W,
-                int32_t *keys, int32_t *items) {
+// grp: group per scalar, or nullptr and gstride > 0 (group = t / gstride), or neither (one group)
+int dx_msm_keys(int on_gpu, void *stream, const uint32_t *k, const int32_t *grp, int64_t gstride, int64_t n, int c,
+                int W, int32_t *keys, int32_t *items) {
   if (n <= 0) return 0;
   if (!on_gpu) {
-    host_for_each(n * W, [=](int64_t e) { msm_keys_one(k, grp, n, c, W, keys, items, e); });
+    host_for_each(n * W, [=](int64_t e) { msm_keys_one(k, grp, gstride, c, W, keys, items, e); });
     return 0;
   }
   hipLaunchKernelGGL(msm_keys_kernel, dim3((unsigned)((n * W + 255) / 256)), dim3(256), 0, (hipStream_t)stream, k,
-                     grp, n, c, W, keys, items);
+                     grp, gstride, n, c, W, keys, items);
   return check_hip(hipGetLastError(), "msm_keys");
 }
 

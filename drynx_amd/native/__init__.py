@@ -139,7 +139,7 @@ _SIGS = {
     "dx_g2_mul_small": [_I, _P, _P, _P, _P, _L],
     "dx_g2_horner": [_I, _P, _P, _P, _I, _I, _I, _L, _L],
     "dx_rp_msm_uv": [_I, _P, _P, _P, _L, _I, _L],
-    "dx_msm_keys": [_I, _P, _P, _P, _L, _I, _I, _P, _P],
+    "dx_msm_keys": [_I, _P, _P, _P, _L, _L, _I, _I, _P, _P],
     "dx_gls8_entries": [],
     "dx_g2_gls8_table": [_I, _P, _P, _P, _P, _L],
     "dx_gt_gls8_table": [_I, _P, _P, _P, _P, _L],
@@ -1212,6 +1212,17 @@ def _segment_passes_dev(counts, dev, first_slice: int | None = None):
     return passes
 
 
+def _group_arg(group, n: int, dev):
+    """(explicit int32 group tensor or None, group stride): an int ``group``
+    means entry t belongs to group t // group (no per-entry tensor)."""
+    if group is None:
+        return None, 0
+    if isinstance(group, int):
+        return None, group
+    assert group.numel() == n
+    return group.to(device=dev, dtype=torch.int32).contiguous(), 0
+
+
 def _bucket_plan(k: torch.Tensor, W: int, group: torch.Tensor | None = None, n_groups: int = 1):
     """Bucket plan of a multi-scalar product over the low W bytes of the
     scalars k [n, 8]: window w, digit d -> bucket w*256+d (plus g*W*256 for
@@ -1223,9 +1234,9 @@ def _bucket_plan(k: torch.Tensor, W: int, group: torch.Tensor | None = None, n_g
     assert n * W < 2 ** 31 and nb < 2 ** 31 - 1
     keys = torch.empty(n * W, dtype=torch.int32, device=dev)
     item = torch.empty(n * W, dtype=torch.int32, device=dev)
-    grp = None if group is None else group.to(device=dev, dtype=torch.int32).contiguous()
+    grp, gstride = _group_arg(group, n, dev)
     g, s = _ctx(k, keys)
-    _call("dx_msm_keys", g, s, _ptr(k.contiguous()), _ptr(grp), n, 8, W, _ptr(keys), _ptr(item))  # csrc/kernels/dx_rpmsm.hip
+    _call("dx_msm_keys", g, s, _ptr(k.contiguous()), _ptr(grp), gstride, n, 8, W, _ptr(keys), _ptr(item))  # dx_rpmsm.hip
     keys, order = torch.sort(keys)          # zero digits carry a sentinel key that sorts last
     item = item.index_select(0, order).to(torch.int64)
     offs = torch.searchsorted(keys, torch.arange(nb + 1, device=dev, dtype=torch.int32))
@@ -1442,7 +1453,8 @@ def g2_mul_small(jac: torch.Tensor, d: torch.Tensor) -> torch.Tensor:
 def g2_msm_launch(P_aff: torch.Tensor, k: torch.Tensor, group: torch.Tensor | None, n_groups: int,
                   c: int = 13, bits: int = 254, first_slice: int = 32) -> dict:
     """Bucket plan of G independent G2 MSMs out[g] = sum_{t: group_t = g}
-    k_t P[t % m] (m = rows of P_aff, k [n, 8] with n a multiple of m):
+    k_t P[t % m] (m = rows of P_aff, k [n, 8] with n a multiple of m; group:
+    int32 tensor, or an int stride s meaning group_t = t // s):
     c-bit windows; int32 keys (g, w, d) built by one kernel (zero digits get
     a sentinel that sorts last), one radix sort, per-bucket counts by a
     binary search of the bucket boundaries -- ONE host sync (the counts).
@@ -1451,12 +1463,12 @@ def g2_msm_launch(P_aff: torch.Tensor, k: torch.Tensor, group: torch.Tensor | No
     n, m = k.shape[0], _rows(P_aff, 32)
     W = -(-bits // c)
     nb = (W << c) * n_groups
-    assert n % m == 0 and n < 2 ** 31 and nb < 2 ** 31 - 1 and (group is None or group.numel() == n)
+    assert n % m == 0 and n < 2 ** 31 and nb < 2 ** 31 - 1
     keys = torch.empty(n * W, dtype=torch.int32, device=dev)
     items = torch.empty(n * W, dtype=torch.int32, device=dev)
-    grp = None if group is None else group.to(device=dev, dtype=torch.int32).contiguous()
+    grp, gstride = _group_arg(group, n, dev)
     g, s = _ctx(k, keys)
-    _call("dx_msm_keys", g, s, _ptr(k.contiguous()), _ptr(grp), n, c, W, _ptr(keys), _ptr(items))
+    _call("dx_msm_keys", g, s, _ptr(k.contiguous()), _ptr(grp), gstride, n, c, W, _ptr(keys), _ptr(items))
     keys, order = torch.sort(keys)
     items = items.index_select(0, order).contiguous()
     offs = torch.searchsorted(keys, torch.arange(nb + 1, device=dev, dtype=torch.int32))

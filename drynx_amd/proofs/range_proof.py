@@ -747,11 +747,9 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
             k[:G, :m, 0] = abv[:, :, 0]
             k[:G, m:, 0] = abv[:, :, 1]
             k[G, :m] = gam_all
-            mgrp = torch.arange(G + 1, device=device, dtype=torch.int32).repeat_interleave(2 * m)
-            mexp = nt.multi_exp_grouped(A2, k.view(-1, 8), mgrp, G + 1, W=5)
+            mexp = nt.multi_exp_grouped(A2, k.view(-1, 8), 2 * m, G + 1, W=5)        # group = row // 2m
         else:
-            mgrp = torch.arange(G + 1, device=device, dtype=torch.int32).repeat_interleave(m)
-            mexp = nt.multi_exp_grouped(r.A, torch.cat([rho_all, gam_all]), mgrp, G + 1)
+            mexp = nt.multi_exp_grouped(r.A, torch.cat([rho_all, gam_all]), m, G + 1)
         if use_msm and aux is not None:
             S_R = nt.g2_msm_run(r.V, hR)                               # R window sums, behind the plans
         e_all = nt.fr_dot_rows(rho_all, r.zv, G, b_periodic=True)                        # sum rho Zv per VN
@@ -821,8 +819,7 @@ def _msm_plan(zphi, V, rho_all, G: int, n: int, S: int, L: int) -> dict:
     it = torch.arange(m, device=dev)
     zi = (it // (S * L)) * L + it % L
     s_r = nt.fr_arith(nt.FR_MUL, rho_all, zphi.index_select(0, zi).repeat(G, 1).contiguous())
-    grp = torch.arange(G, device=dev, dtype=torch.int32).repeat_interleave(m)
-    return nt.g2_msm_launch(V, s_r, grp, G)
+    return nt.g2_msm_launch(V, s_r, m, G)                              # group (VN) = row // m
 
 
 def _msm_queue(Y, V, ab_all, G: int, n: int, S: int, L: int) -> dict:

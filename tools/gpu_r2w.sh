@@ -4,6 +4,6 @@ set -o pipefail
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0 TMPDIR=/tmp
 fatal() { case $1 in 124|134|137|139) echo "fatal rc=$1 in $2"; exit $1;; esac; }
-AMD_SERIALIZE_KERNEL=3 DRYNX_TORCH_PROF=gpurun_out/torch_prof.txt timeout -k 10 600 python -u bench.py --steps 1 --warmup 1 > gpurun_out/bench_w.log 2>&1
+DRYNX_TORCH_PROF=gpurun_out/torch_prof.txt timeout -k 10 600 python -u bench.py --steps 1 --warmup 1 > gpurun_out/bench_w.log 2>&1
 rc=$?; tail -1 gpurun_out/bench_w.log | cut -c1-120; fatal $rc bench
-grep -v "^\s*$" gpurun_out/torch_prof.txt | cut -c1-40,120-175,200-330 | head -150 > gpurun_out/torch_prof_short.txt; head -60 gpurun_out/torch_prof_short.txt
+sed -n "/# GPU time of torch ops/,\$p" gpurun_out/torch_prof.txt | head -62
