@@ -149,10 +149,43 @@ DX_HD void g2_mul_one(const uint32_t *tables, const int32_t *tab_idx, const uint
   at<G2A>(out_aff, i) = to_affine(g2_gls8_eval(T, scalars + 8 * i));
 }
 
-// prover pass 1: a[p*S*L + j] = gT^(t[p*L + j]) (shared by the S servers)
-DX_HD void prove_t_one(const uint32_t *t_sc, const uint32_t *gt_table, uint32_t *a_out, int S, int L, int64_t pj) {
+// ---- gT with signed 16-bit windows: T16[w*32768 + d-1] = gT^(d 2^(16w)),
+// d = 1..32768, w < 17 (214 MB, one table per device): 17 products per
+// exponentiation instead of the 32 of the 8-bit comb
+constexpr int kB16 = 16, kH16 = 1 << 15, kW16 = 17;
+DX_HD void gt16_entry_one(const uint32_t *pow2, uint32_t *table, int64_t t) {
+  const int w = (int)(t / kH16), d = (int)(t % kH16) + 1;
+  const Fp12 q = at<Fp12>(pow2, w);
+  Fp12 acc = Fp12::one();
+  for (int bit = kB16 - 1; bit >= 0; bit--) {  // d <= 2^15
+    acc = cyclotomic_sqr(acc);
+    if ((d >> bit) & 1) acc = mul(acc, q);
+  }
+  at<Fp12>(table, t) = acc;
+}
+DX_HD Fp12 gt16_pow(const Fp12 *T, const uint32_t *k) {
+  Fp12 f = Fp12::one();
+  uint32_t carry = 0;
+  for (int w = 0; w < kW16; w++) {
+    const uint32_t raw = w < 16 ? (k[w >> 1] >> (16 * (w & 1))) & 0xFFFFu : 0u;
+    const uint32_t v = raw + carry;
+    carry = v > (uint32_t)kH16 ? 1u : 0u;
+    const int d = carry ? (int)v - 65536 : (int)v;
+    if (d) {
+      const Fp12 &e = T[w * kH16 + (d > 0 ? d : -d) - 1];
+      f = mul(f, d > 0 ? e : conj(e));
+    }
+  }
+  return f;
+}
+
+// prover pass 1: a[p*S*L + j] = gT^(t[p*L + j]) (shared by the S servers);
+// t16: gt_table is the signed 16-bit table instead of the 8-bit comb
+DX_HD void prove_t_one(const uint32_t *t_sc, const uint32_t *gt_table, uint32_t *a_out, int S, int L, int t16,
+                       int64_t pj) {
   const int64_t p = pj / L, j = pj % L;
-  at<Fp12>(a_out, p * S * L + j) = gt_fixed_pow(reinterpret_cast<const Fp12 *>(gt_table), t_sc + 8 * pj);
+  const Fp12 *T = reinterpret_cast<const Fp12 *>(gt_table);
+  at<Fp12>(a_out, p * S * L + j) = t16 ? gt16_pow(T, t_sc + 8 * pj) : gt_fixed_pow(T, t_sc + 8 * pj);
 }
 // prover pass 2 over the items of one server range [i_lo, i_hi): a[it] = E^(e[it]) * a[p*S*L + j]
 DX_HD void prove_e_one(const uint32_t *gphi_tables, const int32_t *tab_idx, const uint32_t *e_sc, uint32_t *a_out,
@@ -188,9 +221,13 @@ __global__ void __launch_bounds__(kWG) DX_OCC g2_mul_kernel(const uint32_t *tabl
   if (i < n) g2_mul_one(tables, tab_idx, sc, out, i);
 }
 __global__ void __launch_bounds__(kWG) DX_OCC prove_t_kernel(const uint32_t *t_sc, const uint32_t *gt_table,
-                                                            uint32_t *a_out, int S, int L, int64_t n) {
+                                                            uint32_t *a_out, int S, int L, int t16, int64_t n) {
   DX_TID();
-  if (i < n) prove_t_one(t_sc, gt_table, a_out, S, L, i);
+  if (i < n) prove_t_one(t_sc, gt_table, a_out, S, L, t16, i);
+}
+__global__ void __launch_bounds__(kWG) DX_OCC gt16_entry_kernel(const uint32_t *pow2, uint32_t *table, int64_t n) {
+  DX_TID();
+  if (i < n) gt16_entry_one(pow2, table, i);
 }
 __global__ void __launch_bounds__(kWG) DX_OCC prove_e_kernel(const uint32_t *gphi, const int32_t *tab_idx,
                                                             const uint32_t *e_sc, uint32_t *a_out, int S, int L,
@@ -205,6 +242,18 @@ inline dim3 grid_of(int64_t n) { return dim3((unsigned)((n + kWG - 1) / kWG)); }
 
 extern "C" {
 int dx_gls8_entries() { return kEnt; }
+int dx_gt16_entries() { return kW16 * kH16; }
+
+// pow2[w] = gT^(2^(16w)) for w < 17 (host-computed), table [17*32768, 96]
+int dx_gt16_table(int on_gpu, void *stream, const uint32_t *pow2, uint32_t *table) {
+  const int64_t n = (int64_t)kW16 * kH16;
+  if (!on_gpu) {
+    host_for_each(n, [=](int64_t t) { gt16_entry_one(pow2, table, t); });
+    return 0;
+  }
+  hipLaunchKernelGGL(gt16_entry_kernel, grid_of(n), dim3(kWG), 0, (hipStream_t)stream, pow2, table, n);
+  return check_hip(hipGetLastError(), "gt16_table");
+}
 
 // table[b*2176 + w*128 + d-1] = d 2^(8w) A_b (affine); work [nb*17] Jacobian
 int dx_g2_gls8_table(int on_gpu, void *stream, const uint32_t *bases_aff, uint32_t *work, uint32_t *table,
@@ -253,12 +302,12 @@ int dx_g2_gls8_mul(int on_gpu, void *stream, const uint32_t *tables, const int32
 // until its own launch overwrites it last).
 int dx_rp_prove_a_gls8(int on_gpu, void *stream, const uint32_t *gphi_tables, const int32_t *tab_idx,
                        const uint32_t *e_sc, const uint32_t *t_sc, const uint32_t *gt_table, uint32_t *a_out,
-                       int64_t n_items, int S, int L) {
+                       int64_t n_items, int S, int L, int t16) {
   if (n_items <= 0) return 0;
   const int64_t n_pj = n_items / S, n_p = n_pj / L;
   const int ranges[2][2] = {{1, S}, {0, 1}};
   if (!on_gpu) {
-    host_for_each(n_pj, [=](int64_t pj) { prove_t_one(t_sc, gt_table, a_out, S, L, pj); });
+    host_for_each(n_pj, [=](int64_t pj) { prove_t_one(t_sc, gt_table, a_out, S, L, t16, pj); });
     for (auto &rg : ranges) {
       const int lo = rg[0], hi = rg[1];
       if (hi <= lo) continue;
@@ -268,7 +317,7 @@ int dx_rp_prove_a_gls8(int on_gpu, void *stream, const uint32_t *gphi_tables, co
     return 0;
   }
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(prove_t_kernel, grid_of(n_pj), dim3(kWG), 0, s, t_sc, gt_table, a_out, S, L, n_pj);
+  hipLaunchKernelGGL(prove_t_kernel, grid_of(n_pj), dim3(kWG), 0, s, t_sc, gt_table, a_out, S, L, t16, n_pj);
   for (auto &rg : ranges) {
     const int lo = rg[0], hi = rg[1];
     if (hi <= lo) continue;

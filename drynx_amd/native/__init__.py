@@ -144,7 +144,9 @@ _SIGS = {
     "dx_g2_gls8_table": [_I, _P, _P, _P, _P, _L],
     "dx_gt_gls8_table": [_I, _P, _P, _P, _P, _L],
     "dx_g2_gls8_mul": [_I, _P, _P, _P, _P, _P, _L],
-    "dx_rp_prove_a_gls8": [_I, _P, _P, _P, _P, _P, _P, _P, _L, _I, _I],
+    "dx_rp_prove_a_gls8": [_I, _P, _P, _P, _P, _P, _P, _P, _L, _I, _I, _I],
+    "dx_gt16_entries": [],
+    "dx_gt16_table": [_I, _P, _P, _P],
 }
 
 
@@ -591,6 +593,32 @@ def g2_gls8_mul(tables: torch.Tensor, scalars: torch.Tensor, tab_idx: torch.Tens
     return out
 
 
+_gt16: dict = {}
+
+
+def gt16_table(device) -> torch.Tensor:
+    """gT with signed 16-bit windows: [17 * 32768, 96], gT^(d 2^(16w)) (214 MB,
+    built once per device; csrc/kernels/dx_gls8.hip)."""
+    key = str(torch.device(device))
+    if key not in _gt16:
+        from ..crypto import bn254 as _bn
+        from ..crypto import oracle as _O
+
+        g = _O.pairing(_O.G1_GEN, _O.G2_GEN)
+        pows = []
+        for _ in range(17):
+            pows.append(g)
+            for _ in range(16):
+                g = g * g
+        pow2 = _bn.gt_tensor(pows, device)
+        n = _load().dx_gt16_entries()
+        table = torch.empty((n, 96), dtype=torch.int32, device=pow2.device)
+        gg, s = _ctx(pow2, table)
+        _call("dx_gt16_table", gg, s, _ptr(pow2), _ptr(table))
+        _gt16[key] = table
+    return _gt16[key]
+
+
 def g2_mul(pts_aff: torch.Tensor, scalars: torch.Tensor) -> torch.Tensor:
     n = _rows(scalars, 8)
     np_ = _rows(pts_aff, 32)
@@ -893,8 +921,9 @@ def rp_prove_a_tab(gphi_tables, tab_idx, e_sc, t_sc, gt_table, S: int, L: int, w
     g, s = _ctx(gphi_tables, tab_idx, e_sc, t_sc, gt_table)
     if wbits == 7:
         assert tab_idx.dtype == torch.int32 and tab_idx.numel() == n and n % (S * L) == 0
-        _call("dx_rp_prove_a_gls8", g, s, _ptr(gphi_tables), _ptr(tab_idx), _ptr(e_sc), _ptr(t_sc), _ptr(gt_table),
-              _ptr(out), n, S, L)
+        t16 = gt16_table(e_sc.device) if e_sc.is_cuda else None                # gT^t in 17 products
+        _call("dx_rp_prove_a_gls8", g, s, _ptr(gphi_tables), _ptr(tab_idx), _ptr(e_sc), _ptr(t_sc),
+              _ptr(t16 if t16 is not None else gt_table), _ptr(out), n, S, L, int(t16 is not None))
         return out
     if wbits == 6:
         _call("dx_rp_prove_a_gls6", g, s, _ptr(gphi_tables), _ptr(tab_idx), _ptr(e_sc), _ptr(t_sc), _ptr(gt_table),
@@ -1223,20 +1252,20 @@ def _group_arg(group, n: int, dev):
     return group.to(device=dev, dtype=torch.int32).contiguous(), 0
 
 
-def _bucket_plan(k: torch.Tensor, W: int, group: torch.Tensor | None = None, n_groups: int = 1):
-    """Bucket plan of a multi-scalar product over the low W bytes of the
-    scalars k [n, 8]: window w, digit d -> bucket w*256+d (plus g*W*256 for
-    entries of group g when `group` is given); entries sorted by bucket, then
-    segmented passes down to one value per non-empty bucket."""
+def _bucket_plan(k: torch.Tensor, W: int, group: torch.Tensor | None = None, n_groups: int = 1, c: int = 8):
+    """Bucket plan of a multi-scalar product over the low W c-bit windows of
+    the scalars k [n, 8]: window w, digit d -> bucket (w << c) + d (plus
+    g * (W << c) for entries of group g when `group` is given); entries sorted
+    by bucket, then segmented passes down to one value per non-empty bucket."""
     dev = k.device
     n = k.shape[0]
-    nb = W * 256 * n_groups
+    nb = (W << c) * n_groups
     assert n * W < 2 ** 31 and nb < 2 ** 31 - 1
     keys = torch.empty(n * W, dtype=torch.int32, device=dev)
     item = torch.empty(n * W, dtype=torch.int32, device=dev)
     grp, gstride = _group_arg(group, n, dev)
     g, s = _ctx(k, keys)
-    _call("dx_msm_keys", g, s, _ptr(k.contiguous()), _ptr(grp), gstride, n, 8, W, _ptr(keys), _ptr(item))  # dx_rpmsm.hip
+    _call("dx_msm_keys", g, s, _ptr(k.contiguous()), _ptr(grp), gstride, n, c, W, _ptr(keys), _ptr(item))  # dx_rpmsm.hip
     keys, order = torch.sort(keys)          # zero digits carry a sentinel key that sorts last
     item = item.index_select(0, order).to(torch.int64)
     offs = torch.searchsorted(keys, torch.arange(nb + 1, device=dev, dtype=torch.int32))
@@ -1245,11 +1274,12 @@ def _bucket_plan(k: torch.Tensor, W: int, group: torch.Tensor | None = None, n_g
     bk = counts.nonzero()[0]
     passes = _segment_passes_dev(counts[bk], dev)
     # bucket digits and scatter slots, staged now so the run needs no host->device copy
+    mask = (1 << c) - 1
     sc = torch.zeros((bk.size, 8), dtype=torch.int32)
-    sc[:, 0] = torch.from_numpy((bk % 256).astype("int32"))
-    slot = torch.from_numpy((bk % 256) * W + bk // 256)
+    sc[:, 0] = torch.from_numpy((bk & mask).astype("int32"))
+    slot = torch.from_numpy((bk & mask) * W + (bk >> c))
     return {"item": item, "passes": passes, "bk": bk, "single": not passes,
-            "digit_sc": sc.to(dev), "slot": slot.to(dev), "W": W}
+            "digit_sc": sc.to(dev), "slot": slot.to(dev), "W": W, "c": c}
 
 
 def _multi_exp64_run(a: torch.Tensor, plan) -> torch.Tensor:
@@ -1264,40 +1294,49 @@ def _multi_exp64_run(a: torch.Tensor, plan) -> torch.Tensor:
     for k, (st, ln) in enumerate(plan["passes"]):
         cur = gt_slice_prod(a if k == 0 else cur, plan["item"] if k == 0 else None, st, ln)
     bkp = gt_pow(cur, plan["digit_sc"])
-    W = plan.get("W", _ME_W)
-    win = gt_one(dev).repeat(256 * W, 1)
+    W, c = plan.get("W", _ME_W), plan.get("c", _ME_C)
+    win = gt_one(dev).repeat((1 << c) * W, 1)
     win[plan["slot"]] = bkp
-    win = _gt_prod_level(win.view(256, W, 96), 8) if dev.type == "cuda" else win.view(256, W, 96)
+    win = win.view(1 << c, W, 96)
+    if dev.type == "cuda":
+        while win.shape[0] > 32:
+            win = _gt_prod_level(win, 8)
     S_w = gt_prod(win.cpu(), chunk=4)                                  # [W, 96] on the host
     acc = S_w[W - 1: W].contiguous()
     for w in range(W - 2, -1, -1):
-        acc = gt_pow(acc, _pow2_scalar(_ME_C))
+        acc = gt_pow(acc, _pow2_scalar(c))
         acc = gt_mul(acc, S_w[w: w + 1].contiguous())
     return acc
 
 
-def multi_exp_grouped(a: torch.Tensor, k: torch.Tensor, group: torch.Tensor, n_groups: int, W: int = _ME_W):
+def multi_exp_grouped(a: torch.Tensor, k: torch.Tensor, group, n_groups: int, W: int = _ME_W, c: int = 8):
     """Launch G independent multi-exponentiations prod_{i: group_i = g} a[i % n]^k_i
-    (n = rows of a, k [m, 8] with m a multiple of n, low W bytes of each
-    exponent) as ONE bucket plan (one host sync for all groups, e.g. the
-    batch weights of several verifying nodes).  Returns a handle for
-    ``multi_exp_grouped_finish``; device passes are queued on the current stream."""
+    (n = rows of a, k [m, 8] with m a multiple of n, low W c-bit windows of
+    each exponent; ``group`` an int32 tensor or an int stride) as ONE bucket
+    plan (one host sync for all groups, e.g. the batch weights of several
+    verifying nodes).  Returns a handle for ``multi_exp_grouped_finish``;
+    device passes are queued on the current stream."""
     n = a.shape[0]
-    plan = _bucket_plan(k, W, group, n_groups)
+    plan = _bucket_plan(k, W, group, n_groups, c)
     plan["item"] = (plan["item"] % n).contiguous()
     bk = plan["bk"]
-    h = {"G": n_groups, "W": W, "win": None}
+    h = {"G": n_groups, "W": W, "c": c, "win": None}
     if bk.size == 0:
         return h
     cur = a.index_select(0, plan["item"]).contiguous() if plan["single"] else None
     for i, (st, ln) in enumerate(plan["passes"]):
         cur = gt_slice_prod(a if i == 0 else cur, plan["item"] if i == 0 else None, st, ln)
     bkp = gt_pow(cur, plan["digit_sc"])
-    g, w, d = bk // (W * 256), (bk // 256) % W, bk % 256
+    D = 1 << c
+    g, w, d = bk // (W * D), (bk >> c) % W, bk & (D - 1)
     slot = torch.from_numpy(d * (n_groups * W) + g * W + w).to(a.device)
-    win = gt_one(a.device).repeat(256 * n_groups * W, 1)
+    win = gt_one(a.device).repeat(D * n_groups * W, 1)
     win[slot] = bkp
-    h["win"] = _gt_prod_level(win.view(256, n_groups * W, 96), 8) if a.is_cuda else win.view(256, n_groups * W, 96)
+    win = win.view(D, n_groups * W, 96)
+    if a.is_cuda:  # 8-way device levels down to <= 32 rows per (group, window): the host finishes
+        while win.shape[0] > 32:
+            win = _gt_prod_level(win, 8)
+    h["win"] = win
     return h
 
 
@@ -1308,7 +1347,7 @@ def multi_exp_grouped_finish(h) -> torch.Tensor:
         return gt_one("cpu").repeat(G, 1)
     S_w = gt_prod(h["win"].cpu(), chunk=4).view(G, W, 96)
     acc = S_w[:, W - 1].contiguous()
-    sh = _pow2_scalar(_ME_C).expand(G, 8).contiguous()
+    sh = _pow2_scalar(h.get("c", _ME_C)).expand(G, 8).contiguous()
     for w in range(W - 2, -1, -1):
         acc = gt_mul(gt_pow(acc, sh), S_w[:, w].contiguous())
     return acc

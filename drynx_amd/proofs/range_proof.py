@@ -747,7 +747,10 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
             k[:G, :m, 0] = abv[:, :, 0]
             k[:G, m:, 0] = abv[:, :, 1]
             k[G, :m] = gam_all
-            mexp = nt.multi_exp_grouped(A2, k.view(-1, 8), 2 * m, G + 1, W=5)        # group = row // 2m
+            # GPU: 11-bit windows (3 per 32-bit half, 4 for the 40-bit combination);
+            # host: bytes (fewer buckets for the host's serial bucket products)
+            wc = (4, 11) if device.type == "cuda" else (5, 8)
+            mexp = nt.multi_exp_grouped(A2, k.view(-1, 8), 2 * m, G + 1, W=wc[0], c=wc[1])  # group = row // 2m
         else:
             mexp = nt.multi_exp_grouped(r.A, torch.cat([rho_all, gam_all]), m, G + 1)
         if use_msm and aux is not None:
