@@ -2,13 +2,16 @@
 # cmd/ binaries, run the test suite).
 PY ?= python
 
-.PHONY: build test test-gpu sanitize bench smoke simul clean
+.PHONY: build test test-gpu lint sanitize bench smoke simul clean
 
 build:            ## compile every HIP translation unit for gfx950 into drynx_amd/native/libdrynx_native.so
 	$(PY) -m drynx_amd.native.build
 
 test: build       ## CPU suite (host path of the same kernels, gloo multi-rank)
 	$(PY) -m pytest tests -m "not gpu" -q -n 4
+
+lint:             ## stdlib source lint (syntax, unused imports, whitespace, line length, no CUDA spellings)
+	$(PY) tools/lint.py
 
 test-gpu: build   ## on an MI355X
 	$(PY) -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread

@@ -333,7 +333,8 @@ def g1_mul(pts_jac: torch.Tensor, scalars: torch.Tensor) -> torch.Tensor:
         if rc:
             raise RuntimeError(f"dx_g1_mul_fast failed rc={rc}")
         return out
-    _call("dx_g1_mul", g, s, _ptr(pts_jac), _ptr(scalars), _ptr(out), n, int(np_ == 1 and n > 1), int(nk == 1 and n > 1))
+    _call("dx_g1_mul", g, s, _ptr(pts_jac), _ptr(scalars), _ptr(out), n, int(np_ == 1 and n > 1),
+          int(nk == 1 and n > 1))
     return out
 
 
@@ -1265,7 +1266,8 @@ def _bucket_plan(k: torch.Tensor, W: int, group: torch.Tensor | None = None, n_g
     item = torch.empty(n * W, dtype=torch.int32, device=dev)
     grp, gstride = _group_arg(group, n, dev)
     g, s = _ctx(k, keys)
-    _call("dx_msm_keys", g, s, _ptr(k.contiguous()), _ptr(grp), gstride, n, c, W, _ptr(keys), _ptr(item))  # dx_rpmsm.hip
+    _call("dx_msm_keys", g, s, _ptr(k.contiguous()), _ptr(grp), gstride, n, c, W, _ptr(keys),  # dx_rpmsm.hip
+          _ptr(item))
     keys, order = torch.sort(keys)          # zero digits carry a sentinel key that sorts last
     item = item.index_select(0, order).to(torch.int64)
     offs = torch.searchsorted(keys, torch.arange(nb + 1, device=dev, dtype=torch.int32))

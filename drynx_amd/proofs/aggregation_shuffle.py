@@ -12,16 +12,14 @@ proofs/shuffle.py (commitment-consistent proof of a shuffle, one MSM to verify).
 """
 from __future__ import annotations
 
-import hashlib
 import math
-from dataclasses import dataclass, field
+from dataclasses import dataclass
 
 import numpy as np
 import torch
 
 from .. import native as nt
 from ..crypto import bn254 as bn
-from ..crypto import oracle as O
 from ..crypto.elgamal import CipherVector, pk_table
 
 

@@ -351,7 +351,8 @@ class RangeProofList:
         dev = self.commit.device
         n, l, S = len(self), self.l, self.S
         meta = torch.tensor([0x52505231, n, self.u, l, S], dtype=torch.int32)
-        offs = torch.tensor(self.offset, dtype=torch.int64).view(torch.int32) if n else torch.empty(0, dtype=torch.int32)
+        offs = (torch.tensor(self.offset, dtype=torch.int64).view(torch.int32) if n
+                else torch.empty(0, dtype=torch.int32))
         cols = torch.tensor(self.cols, dtype=torch.int32)
         parts = [meta.to(dev), offs.to(dev), cols.to(dev), self.commit.K.reshape(-1), self.commit.C.reshape(-1)]
         if self.has_rp and n:

@@ -588,7 +588,8 @@ def verify_requests(reqs: list, sq, vn_id: str, vn_index: int, n_vns: int, devic
                 for i in idxs:
                     try:
                         o = _decode(reqs[i], device)
-                        if kind == "keyswitch" and (o.X != sq.IDtoPublic.get(reqs[i].sender_id) or o.Q != sq.ClientPubKey):
+                        if kind == "keyswitch" and (o.X != sq.IDtoPublic.get(reqs[i].sender_id)
+                                                    or o.Q != sq.ClientPubKey):
                             codes[i] = PROOF_FALSE
                             continue
                         objs.append(o)

@@ -521,7 +521,8 @@ def key_switch_list_proof_verification(pr: KeySwitchProof, threshold: float = 1.
     cs = _sc([c], dev)
     za = pr.za[:k].contiguous()
     # za B == T1 + c (vB)
-    ok1 = nt.g1_eq(nt.g1_fb_mul(tabB, za), nt.g1_add(pr.T1[:k].contiguous(), nt.g1_mul(pr.share.K[:k].contiguous(), cs)))
+    ok1 = nt.g1_eq(nt.g1_fb_mul(tabB, za),
+                   nt.g1_add(pr.T1[:k].contiguous(), nt.g1_mul(pr.share.K[:k].contiguous(), cs)))
     # za Q - zb K == T2 + c (vQ - xK)
     lhs = nt.g1_add(nt.g1_fb_mul(tabQ, za), nt.g1_mul(pr.K[:k].contiguous(), _sc([pr.zb], dev)), subtract=True)
     rhs = nt.g1_add(pr.T2[:k].contiguous(), nt.g1_mul(pr.share.C[:k].contiguous(), cs))

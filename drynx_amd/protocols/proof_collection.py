@@ -144,7 +144,12 @@ def _pool_async(ctx, sq, reqs, vns):
     if ctx.device.type != "cuda":
         return ctx._pool_exec.submit(pool_verify_ranges, ctx, sq, reqs, vns)
     if not hasattr(ctx, "_pool_stream"):
-        ctx._pool_stream = torch.cuda.Stream(ctx.device)
+        # DRYNX_POOL_RESERVE_CUS=k: the pool's heavy kernels (long-running
+        # workgroups) leave k CUs to the short plan / per-CN-proof launches
+        from .. import native as nt
+
+        k = int(os.environ.get("DRYNX_POOL_RESERVE_CUS", "0"))
+        ctx._pool_stream = nt.cu_masked_stream(ctx.device, k) if k > 0 else torch.cuda.Stream(ctx.device)
     side, main = ctx._pool_stream, torch.cuda.current_stream(ctx.device)
     side.wait_stream(main)
 

@@ -14,7 +14,7 @@ from __future__ import annotations
 import copy
 import hashlib
 import uuid
-from dataclasses import asdict, dataclass, field, fields, is_dataclass
+from dataclasses import dataclass, field, fields, is_dataclass
 from typing import Optional
 
 from .crypto import oracle as O

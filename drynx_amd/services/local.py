@@ -15,7 +15,7 @@ from ..crypto import oracle as O
 from ..parallel.comm import Comm, LocalComm
 from ..parallel.topology import build_cluster
 from ..proofs import range_proof as rp
-from ..query import QueryDiffP, QueryDPDataGen, Roster, choose_operation, lr_nbr_outputs
+from ..query import QueryDiffP, QueryDPDataGen, choose_operation, lr_nbr_outputs
 from .api import DrynxClient
 from .service import DrynxNode
 

@@ -407,7 +407,11 @@ class DrynxNode:
         # switching: short latency-bound launches) overlap it on the GPU instead
         # of queueing behind ~20 ms of range-proof kernels
         if not hasattr(self, "_prove_stream"):
-            self._prove_stream = torch.cuda.Stream(self.device)
+            # DRYNX_PROVE_RESERVE_CUS=k: the prover leaves k CUs to the CN phases
+            k = int(os.environ.get("DRYNX_PROVE_RESERVE_CUS", "0"))
+            from .. import native as nt
+
+            self._prove_stream = nt.cu_masked_stream(self.device, k) if k > 0 else torch.cuda.Stream(self.device)
         side, main = self._prove_stream, torch.cuda.current_stream(self.device)
         side.wait_stream(main)  # the DP ciphertexts / randomness are ready
         with torch.cuda.stream(side):

@@ -16,12 +16,8 @@ from __future__ import annotations
 import argparse
 import ast
 import csv
-import os
-import shlex
 import sys
 import tempfile
-
-import torch
 
 from ..parallel.comm import init_distributed, make_comm
 from ..query import QueryDiffP, LogisticRegressionParameters
@@ -103,7 +99,8 @@ def run_row(glob: dict, row: dict, comm, device, workdir):
                                           StandardDeviations=[1.1] * n_feat)
     diffp = None
     if int(row.get("DiffPSize", 0)):
-        diffp = QueryDiffP(LapMean=float(row.get("DiffPEpsilon", 0)), LapScale=max(1e-3, float(row.get("DiffPDelta", 1))),
+        diffp = QueryDiffP(LapMean=float(row.get("DiffPEpsilon", 0)),
+                           LapScale=max(1e-3, float(row.get("DiffPDelta", 1))),
                            NoiseListSize=int(row["DiffPSize"]), Quanta=float(row.get("DiffPQuanta", 1)),
                            Scale=float(row.get("DiffPScale", 1)), Limit=float(row.get("DiffPLimit", 1)))
     results = []

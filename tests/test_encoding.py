@@ -112,7 +112,8 @@ def test_batched_encoder_matches_per_dp(env, op, proofs):
         assert b["clear"] == single["clear"] and b["n_groups"] == single["n_groups"] == 2
         assert len(b["cv"]) == len(single["cv"])
         if bits and not proofs:
-            assert eg.decrypt_check_zero(secret, b["cv"]).tolist() == eg.decrypt_check_zero(secret, single["cv"]).tolist()
+            assert (eg.decrypt_check_zero(secret, b["cv"]).tolist()
+                    == eg.decrypt_check_zero(secret, single["cv"]).tolist())
         else:
             assert eg.decrypt_ints(secret, b["cv"]) == [v for grp in b["clear"] for v in grp]
         if proofs:

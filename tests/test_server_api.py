@@ -74,7 +74,8 @@ def test_vn_api_over_tcp(tmp_path):
 
     addrs = [f"127.0.0.1:{_port()}" for _ in range(2)]
     kps = [KeyPair.generate() for _ in addrs]
-    group = "[Network]\n" + "".join(f'[[Network.Nodes]]\nAddress = "{a}"\nPublicKey = "{O.g1_to_bytes(k.public).hex()}"\n'
+    group = "[Network]\n" + "".join(f'[[Network.Nodes]]\nAddress = "{a}"\n'
+                                     f'PublicKey = "{O.g1_to_bytes(k.public).hex()}"\n'
                                      for a, k in zip(addrs, kps))
     (tmp_path / "group.toml").write_text(group)
     env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")

@@ -3,7 +3,6 @@ operation end to end, proofs + VNs + skipchain, getters, malicious parties."""
 import pytest
 import torch
 
-from drynx_amd.crypto import elgamal as eg
 from drynx_amd.ops import encoding as enc
 from drynx_amd.proofs import requests as prq
 from drynx_amd.query import QueryDiffP

@@ -1,6 +1,5 @@
 """Obfuscation (incl. the negative test of obfuscation_proof_test.go:30-31),
 key-switch, Schnorr, aggregation and shuffle proofs."""
-import torch
 
 from drynx_amd.crypto import bn254 as bn
 from drynx_amd.crypto import elgamal as eg

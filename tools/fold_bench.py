@@ -59,7 +59,8 @@ def main():
         tl, lines = timed(lambda: nt.rp_fold_lines(P, V, v))
         for K in (1, 2, 4, 8):
             ta, _ = timed(lambda: nt.rp_fold_accum(lines, n, K, v))
-            print(json.dumps({"variant": v, "K": K, "n": n, "lines_ms": round(1e3 * tl, 2), "accum_ms": round(1e3 * ta, 2),
+            print(json.dumps({"variant": v, "K": K, "n": n, "lines_ms": round(1e3 * tl, 2),
+                              "accum_ms": round(1e3 * ta, 2),
                               "ml_per_s": round(n / (tl + ta))}), flush=True)
         del lines
         torch.cuda.empty_cache()

@@ -5,7 +5,8 @@ import time
 
 import torch
 
-sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(
+    __import__("os").path.abspath(__file__))))
 from drynx_amd import native as nt  # noqa: E402
 from drynx_amd.crypto import bn254 as bn  # noqa: E402
 from drynx_amd.crypto import oracle as O  # noqa: E402

@@ -11,7 +11,8 @@ def main():
     top = int(sys.argv[2]) if len(sys.argv) > 2 else 30
     last_ms = float(sys.argv[3]) if len(sys.argv) > 3 else None
     names = {r[0]: (r[1], r[2], r[3], r[4]) for r in db.execute(
-        "select id, display_name, arch_vgpr_count, accum_vgpr_count, private_segment_size from rocpd_info_kernel_symbol")}
+        "select id, display_name, arch_vgpr_count, accum_vgpr_count, private_segment_size "
+        "from rocpd_info_kernel_symbol")}
     agg = collections.defaultdict(lambda: [0, 0.0])
     t_min, t_max = None, None
     rows = db.execute("select kernel_id, start, end from rocpd_kernel_dispatch").fetchall()
@@ -25,7 +26,8 @@ def main():
         t_min = s if t_min is None else min(t_min, s)
         t_max = e if t_max is None else max(t_max, e)
     tot = sum(v[1] for v in agg.values())
-    print(f"kernels: {sum(v[0] for v in agg.values())} dispatches, {tot:.1f} ms busy, span {(t_max - t_min) / 1e6:.1f} ms")
+    print(f"kernels: {sum(v[0] for v in agg.values())} dispatches, {tot:.1f} ms busy, "
+          f"span {(t_max - t_min) / 1e6:.1f} ms")
     print(f"{'ms':>9} {'n':>6} {'mean_us':>9} {'vgpr':>5} {'agpr':>5} {'scratch':>7}  kernel")
     for kid, (n, ms) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:top]:
         nm, vg, ag, sc = names.get(kid, ("?", 0, 0, 0))
