@@ -1311,7 +1311,13 @@ def _multi_exp64_run(a: torch.Tensor, plan) -> torch.Tensor:
     return acc
 
 
-def multi_exp_grouped(a: torch.Tensor, k: torch.Tensor, group, n_groups: int, W: int = _ME_W, c: int = 8):
+def multi_exp_plan(k: torch.Tensor, group, n_groups: int, W: int = _ME_W, c: int = 8) -> dict:
+    """The bucket plan of ``multi_exp_grouped`` alone (its one host sync)."""
+    return _bucket_plan(k, W, group, n_groups, c)
+
+
+def multi_exp_grouped(a: torch.Tensor, k: torch.Tensor, group, n_groups: int, W: int = _ME_W, c: int = 8,
+                      plan: dict | None = None):
     """Launch G independent multi-exponentiations prod_{i: group_i = g} a[i % n]^k_i
     (n = rows of a, k [m, 8] with m a multiple of n, low W c-bit windows of
     each exponent; ``group`` an int32 tensor or an int stride) as ONE bucket
@@ -1319,7 +1325,8 @@ def multi_exp_grouped(a: torch.Tensor, k: torch.Tensor, group, n_groups: int, W:
     verifying nodes).  Returns a handle for ``multi_exp_grouped_finish``;
     device passes are queued on the current stream."""
     n = a.shape[0]
-    plan = _bucket_plan(k, W, group, n_groups, c)
+    if plan is None:
+        plan = _bucket_plan(k, W, group, n_groups, c)
     plan["item"] = (plan["item"] % n).contiguous()
     bk = plan["bk"]
     h = {"G": n_groups, "W": W, "c": c, "win": None}
@@ -1384,19 +1391,27 @@ def g1_msm_grouped(P_jac: torch.Tensor, k: torch.Tensor, group: torch.Tensor | N
     return g1_msm_finish(g1_msm_launch(P_jac, k, group, n_groups, bits))
 
 
+def g1_msm_plan(k: torch.Tensor, group, n_groups: int, bits: int = 256) -> dict:
+    """The bucket plan of ``g1_msm_launch`` alone (its one host sync), so a
+    caller can take every plan's sync before queueing any heavy pass."""
+    return _bucket_plan(k, (bits + 7) // 8, group, n_groups) if k.shape[0] else None
+
+
 def g1_msm_launch(P_jac: torch.Tensor, k: torch.Tensor, group: torch.Tensor | None, n_groups: int,
-                  bits: int = 256) -> dict:
-    """First half of g1_msm_grouped: the bucket plan (one host sync on k) and
-    every device pass, queued on the current stream.  g1_msm_finish waits for
-    them and runs the Horner steps on the host."""
+                  bits: int = 256, plan: dict | None = None) -> dict:
+    """First half of g1_msm_grouped: the bucket plan (one host sync on k,
+    unless ``plan`` comes from ``g1_msm_plan``) and every device pass, queued
+    on the current stream.  g1_msm_finish waits for them and runs the Horner
+    steps on the host."""
     assert P_jac.shape[0] == k.shape[0]
-    assert group is None or group.numel() == k.shape[0]
+    assert group is None or isinstance(group, int) or group.numel() == k.shape[0]
     dev = P_jac.device
     W = (bits + 7) // 8
     h = {"n_groups": n_groups, "W": W, "S_w": None}
     if P_jac.shape[0] == 0:
         return h
-    plan = _bucket_plan(k, W, group, n_groups)
+    if plan is None:
+        plan = _bucket_plan(k, W, group, n_groups)
     bk = plan["bk"]
     if bk.size == 0:
         return h

@@ -732,13 +732,14 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
                                                            [v["ab"] for v in vns] if glv else None)):
                     v["fb"] = fb
     with timers.span("rp.verify.plans"), (torch.cuda.stream(aux) if aux is not None else _nullctx()):
+        # every bucket plan (one host sync each) first, then every pass: a sync
+        # never waits behind another plan's heavy passes
         if use_msm and aux is not None:
             hR = _msm_plan(r.zphi, r.V, rho_all, G, n, S, l)
         dpts = torch.cat([Cp.contiguous(), r.D.contiguous()]).repeat(G, 1)
         wc = nt.fr_arith(nt.FR_MUL, w_all, r.challenge.repeat(G, 1))
-        dsc = torch.cat([torch.stack([wc.view(G, n, 8), w_all.view(G, n, 8)], 1).reshape(-1, 8)])
-        dgrp = (vid.view(G, 1, 1) * 2 + torch.arange(2, device=device).view(1, 2, 1)).expand(G, 2, n).reshape(-1)
-        dcheck = nt.g1_msm_launch(dpts, dsc.contiguous(), dgrp.to(torch.int32).contiguous(), 2 * G, bits=256)
+        dsc = torch.stack([wc.view(G, n, 8), w_all.view(G, n, 8)], 1).reshape(-1, 8).contiguous()
+        dplan = nt.g1_msm_plan(dsc, n, 2 * G)                             # group = row // n
         # the GT-membership combination is a property of the proof data, not of
         # a VN's weights: ONE random combination per rank serves every co-hosted VN
         if glv:  # prod a^rho = prod a^a' * frob^8(a)^b': 32-bit exponents over (A, frob^8 A)
@@ -750,12 +751,15 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
             k[G, :m] = gam_all
             # GPU: 11-bit windows (3 per 32-bit half, 4 for the 40-bit combination);
             # host: bytes (fewer buckets for the host's serial bucket products)
-            wc = (4, 11) if device.type == "cuda" else (5, 8)
-            mexp = nt.multi_exp_grouped(A2, k.view(-1, 8), 2 * m, G + 1, W=wc[0], c=wc[1])  # group = row // 2m
+            wc_ = (4, 11) if device.type == "cuda" else (5, 8)
+            k = k.view(-1, 8)
+            mplan = nt.multi_exp_plan(k, 2 * m, G + 1, W=wc_[0], c=wc_[1])          # group = row // 2m
+            mexp = nt.multi_exp_grouped(A2, k, 2 * m, G + 1, W=wc_[0], c=wc_[1], plan=mplan)
         else:
             mexp = nt.multi_exp_grouped(r.A, torch.cat([rho_all, gam_all]), m, G + 1)
         if use_msm and aux is not None:
-            S_R = nt.g2_msm_run(r.V, hR)                               # R window sums, behind the plans
+            S_R = nt.g2_msm_run(r.V, hR)                               # R window sums
+        dcheck = nt.g1_msm_launch(dpts, dsc, n, 2 * G, bits=256, plan=dplan)
         e_all = nt.fr_dot_rows(rho_all, r.zv, G, b_periodic=True)                        # sum rho Zv per VN
         dfull = torch.stack([nt.fr_dot_rows(w_all, r.zr, G, b_periodic=True),
                              nt.fr_dot_rows(w_all, z, G, b_periodic=True)], 1)             # [G, 2, 8]

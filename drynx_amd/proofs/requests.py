@@ -47,11 +47,12 @@ class ProofRequest:
     something needs them (ledger persistence, control-plane transport)."""
 
     __slots__ = ("kind", "survey_id", "sender_id", "differ_info", "_data", "signature", "obj", "data_digest",
-                 "tensor", "decoded")
+                 "tensor", "decoded", "sig_ok")
 
     def __init__(self, kind: str, survey_id: str, sender_id: str, differ_info: str, data: bytes | None,
                  signature: bytes, obj: Any = None, data_digest: bytes = b"", tensor: torch.Tensor | None = None):
         self.kind, self.survey_id, self.sender_id, self.differ_info = kind, survey_id, sender_id, differ_info
+        self.sig_ok = None  # ((public, digest, signature), verdict): shared by the VNs of this rank
         self._data = data
         self.signature = signature
         self.obj = obj  # decoded proof (in-process fast path)
@@ -543,9 +544,15 @@ def verify_requests(reqs: list, sq, vn_id: str, vn_index: int, n_vns: int, devic
     todo: dict = {}
     pooled_idx: list = []
     if len(reqs) >= _SIG_BATCH_MIN:
-        with timers.span("verify.signature.batch"):
-            sigs_ok = sigma.schnorr_verify_batch(
-                [(sq.IDtoPublic.get(r.sender_id), r.digest(), r.signature) for r in reqs], device)
+        # each envelope's Schnorr check is a deterministic function of the signed
+        # bytes and the roster key: done once per rank, read by every co-hosted VN
+        keys = [(sq.IDtoPublic.get(r.sender_id), r.digest(), r.signature) for r in reqs]
+        fresh = [i for i, r in enumerate(reqs) if r.sig_ok is None or r.sig_ok[0] != keys[i]]
+        if fresh:
+            with timers.span("verify.signature.batch"):
+                for i, v in zip(fresh, sigma.schnorr_verify_batch([keys[i] for i in fresh], device)):
+                    reqs[i].sig_ok = (keys[i], v)
+        sigs_ok = [r.sig_ok[1] for r in reqs]
     else:
         sigs_ok = None
     for i, req in enumerate(reqs):

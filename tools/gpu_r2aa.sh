@@ -1,0 +1,10 @@
+#!/bin/bash
+# Kernel timeline of the current schedule: GPU busy vs wall per query, idle gaps.
+set -o pipefail
+mkdir -p gpurun_out
+export HSA_ENABLE_IPC_MODE_LEGACY=0 TMPDIR=/tmp
+fatal() { case $1 in 124|134|137|139) echo "fatal rc=$1 in $2"; exit $1;; esac; }
+rm -rf gpurun_out/prof
+timeout -k 10 600 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/prof -o bench -- python3 bench.py --steps 3 --warmup 1 > gpurun_out/prof_run.log 2>&1
+rc=$?; echo "prof rc=$rc"; fatal $rc prof
+python tools/gpu_busy.py gpurun_out/prof/bench_kernel_trace.csv timeline > gpurun_out/gpu_busy_aa.txt; grep "^step" gpurun_out/gpu_busy_aa.txt
