@@ -124,6 +124,9 @@ def dp_encode_batch(ctx, sq, dps: list) -> dict:
     device = torch.device(ctx.device)
     pk = eg.pk_table(sq.RosterServers.aggregate(), device)
     g = q.DPDataGen
+    groups = all_possible_groups(g.GroupByValues)
+    if op.NameOp == "logistic regression":
+        return _encode_batch_tail(ctx, sq, dps, _lr_values(ctx, sq, dps, device), groups, pk)
     n_in = max(1, op.NbrInput)
     mats, rows = [], []
     for dp in dps:
@@ -142,9 +145,39 @@ def dp_encode_batch(ctx, sq, dps: list) -> dict:
             Z = Z.pin_memory().to(device, non_blocking=True)
     else:
         Z = torch.cat([m.to(device) for m in mats]).contiguous()
-    groups = all_possible_groups(g.GroupByValues)
-    ng, cf = len(groups), q.CuttingFactor
     vals = enc.batch_values(op.NameOp, Z, rows, op.QueryMin, op.QueryMax)  # [n_dp, n_out]
+    return _encode_batch_tail(ctx, sq, dps, vals, groups, pk)
+
+
+def _lr_values(ctx, sq, dps: list, device) -> torch.Tensor:
+    """[n_dp, n_out] int64 coefficient vectors of every DP's logistic-regression
+    data (the fused fp64-MFMA encoder per DP, no host round trip in between)."""
+    from ..models.logistic_regression import encode_coefficients_int, n_coeffs
+
+    op = sq.Query.Operation
+    params = op.LRParameters
+    out = []
+    for dp in dps:
+        if ctx.dp_data and dp.id in ctx.dp_data:
+            X, y = ctx.dp_data[dp.id]
+        else:
+            X, y = generate_lr_data(params, device, torch.Generator().manual_seed(_seed(sq.SurveyID, dp.id)))
+        if X is None or len(X) == 0:
+            out.append(torch.zeros(n_coeffs(params.NbrFeatures, params.K), dtype=torch.int64, device=device))
+        else:
+            out.append(encode_coefficients_int(torch.as_tensor(X, device=device), torch.as_tensor(y, device=device),
+                                               params).to(device))
+    return torch.stack(out)
+
+
+def _encode_batch_tail(ctx, sq, dps: list, vals: torch.Tensor, groups, pk) -> dict:
+    """Shared tail of ``dp_encode_batch``: one encryption launch for every
+    (DP, group, output), CuttingFactor replication, one host copy, the proof
+    batches per DP."""
+    q = sq.Query
+    op = q.Operation
+    device = torch.device(ctx.device)
+    ng, cf = len(groups), q.CuttingFactor
     n_dp, n_out = vals.shape
     with_proofs = _with_proofs(q)
     bits = op.NameOp in enc.BIT_OPS and not with_proofs
@@ -193,7 +226,8 @@ def data_collection(ctx, sq) -> tuple:
     # the per-DP timer syncs the device only for a handful of DPs per rank: with
     # thousands (ScaleDPs, one record each) the syncs serialise the encoders
     sync_timer = len(local_dps) <= 16
-    if local_dps and sq.Query.Operation.NameOp in enc.BATCH_OPS and os.environ.get("DRYNX_DP_BATCH", "1") != "0":
+    batchable = sq.Query.Operation.NameOp in enc.BATCH_OPS + ("logistic regression",)
+    if local_dps and batchable and os.environ.get("DRYNX_DP_BATCH", "1") != "0":
         # every DP of this rank in one batch; each DP's encoding latency is the batch's
         with timers.timed("DPencodingBatch", sync=sync_timer) as t:
             batch = dp_encode_batch(ctx, sq, local_dps)

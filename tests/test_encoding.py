@@ -137,3 +137,29 @@ def test_batched_encoder_cutting_factor(env):
         assert len(b["cv"]) == 2  # the one output replicated CuttingFactor times (same ciphertext)
         assert torch.equal(b["cv"].K[0], b["cv"].K[1])
         assert eg.decrypt_ints(secret, b["cv"]) == b["clear"][0] * 2
+
+
+@pytest.mark.parametrize("proofs", [0, 1])
+def test_batched_lr_encoder_matches_per_dp(env, proofs):
+    """Logistic regression through the batched encoder (per-DP fused encoder,
+    one encryption launch for all DPs) == the per-DP path."""
+    from drynx_amd.query import LogisticRegressionParameters
+
+    cl, node, client = env
+    d = 3
+    lp = LogisticRegressionParameters(NbrRecords=24, NbrFeatures=d, Means=[0.5] * d, StandardDeviations=[1.1] * d,
+                                      Lambda=1.0, Step=0.1, MaxIterations=5, InitialWeights=[0.1] * (d + 1), K=2,
+                                      PrecisionApproxCoefficients=100.0)
+    sq = make_survey(client, cl, "logistic regression", proofs=proofs, ranges=[16, 8, 1 << 31] if proofs else None,
+                     lr_params=lp, deterministic_sigs=True)
+    dps = list(cl.dps)
+    batch = dcp.dp_encode_batch(node, sq, dps)
+    secret = sum(cn.keypair.secret for cn in cl.cns) % O.R
+    for dp in dps:
+        single = dcp.dp_encode(node, sq, dp)
+        b = batch[dp.id]
+        assert b["clear"] == single["clear"]
+        assert eg.decrypt_ints(secret, b["cv"]) == [v for grp in b["clear"] for v in grp]
+        if proofs:
+            for pb, ps in zip(b["proofs"], single["proofs"]):
+                assert pb.values == ps.values and pb.offset == ps.offset and pb.u == ps.u and pb.l == ps.l
