@@ -419,15 +419,21 @@ def to_base(n: int, b: int, l: int) -> list:
 def _digits(vals, offs, u: int, l: int) -> np.ndarray:
     """[n, l] base-u digits of m + offset (ToBase per value, vectorised when
     every m + offset fits an unsigned 64-bit word)."""
-    x = [int(v) + int(o) for v, o in zip(vals, offs)]
-    if x and 0 <= min(x) and max(x) < (1 << 64) and u >= 2:
-        a = np.asarray(x, dtype=np.uint64)
-        out = np.empty((len(x), l), dtype=np.int64)
+    try:  # int64 values and offsets: m + offset computed in uint64 without a Python loop
+        v = np.asarray(vals, dtype=np.int64).reshape(-1)
+        o = np.asarray(offs, dtype=np.int64).reshape(-1)
+        ok64 = u >= 2 and v.size > 0 and bool((o >= 0).all() and (v >= -o).all())
+    except OverflowError:
+        ok64 = False
+    if ok64:
+        a = v.astype(np.uint64) + o.astype(np.uint64)      # 0 <= m + offset < 2^64: exact
+        out = np.empty((a.size, l), dtype=np.int64)
         uu = np.uint64(u)
         for j in range(l):
             out[:, j] = (a % uu).astype(np.int64)
             a //= uu
         return out
+    x = [int(v) + int(o) for v, o in zip(vals, offs)]
     return np.array([to_base(v, u, l)[:l] for v in x], dtype=np.int64).reshape(len(x), l)
 
 
