@@ -876,7 +876,11 @@ def _msm_r_miller(hR, S_dev) -> torch.Tensor:
     beats one GPU lane at this serial chain) and ML(B, R_v) -> [G, 96] host."""
     R = nt.g2_msm_finish(S_dev.cpu(), hR)
     B = nt.g1_to_affine(bn.g1_jac_tensor([O.G1_GEN], "cpu")).repeat(R.shape[0], 1)
-    return nt.miller_loop(B, R)
+    f = nt.miller_loop(B, R)
+    inf = ~R.bool().any(dim=1)                                         # R = O: e(B, O) = 1
+    if bool(inf.any()):
+        f[inf] = nt.gt_one("cpu")
+    return f
 
 
 def _fold_points(ZB, Y, S: int, L: int) -> torch.Tensor:
