@@ -235,9 +235,32 @@ __global__ void __launch_bounds__(kWG) DX_OCC prove_e_kernel(const uint32_t *gph
   DX_TID();
   if (i < n) prove_e_one(gphi, tab_idx, e_sc, a_out, S, L, i_lo, i_hi, i);
 }
+// One-wave-per-SIMD variants of the two prover kernels (A/B, DRYNX_PROVE_WAVES=1):
+// the whole register file (VGPRs + AGPRs) instead of 256 registers and scratch spills
+#define DX_OCC1 __attribute__((amdgpu_waves_per_eu(1, 1)))
+__global__ void __launch_bounds__(kWG) DX_OCC1 prove_t_kernel_w1(const uint32_t *t_sc, const uint32_t *gt_table,
+                                                               uint32_t *a_out, int S, int L, int t16, int64_t n) {
+  DX_TID();
+  if (i < n) prove_t_one(t_sc, gt_table, a_out, S, L, t16, i);
+}
+__global__ void __launch_bounds__(kWG) DX_OCC1 prove_e_kernel_w1(const uint32_t *gphi, const int32_t *tab_idx,
+                                                               const uint32_t *e_sc, uint32_t *a_out, int S, int L,
+                                                               int i_lo, int i_hi, int64_t n) {
+  DX_TID();
+  if (i < n) prove_e_one(gphi, tab_idx, e_sc, a_out, S, L, i_lo, i_hi, i);
+}
+#undef DX_OCC1
 #undef DX_TID
 
 inline dim3 grid_of(int64_t n) { return dim3((unsigned)((n + kWG - 1) / kWG)); }
+
+inline bool prove_one_wave() {
+  static const bool w1 = [] {
+    const char *e = getenv("DRYNX_PROVE_WAVES");
+    return e && e[0] == '1';
+  }();
+  return w1;
+}
 }  // namespace
 
 extern "C" {
@@ -317,13 +340,21 @@ int dx_rp_prove_a_gls8(int on_gpu, void *stream, const uint32_t *gphi_tables, co
     return 0;
   }
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(prove_t_kernel, grid_of(n_pj), dim3(kWG), 0, s, t_sc, gt_table, a_out, S, L, t16, n_pj);
+  const bool w1 = prove_one_wave();
+  if (w1)
+    hipLaunchKernelGGL(prove_t_kernel_w1, grid_of(n_pj), dim3(kWG), 0, s, t_sc, gt_table, a_out, S, L, t16, n_pj);
+  else
+    hipLaunchKernelGGL(prove_t_kernel, grid_of(n_pj), dim3(kWG), 0, s, t_sc, gt_table, a_out, S, L, t16, n_pj);
   for (auto &rg : ranges) {
     const int lo = rg[0], hi = rg[1];
     if (hi <= lo) continue;
     const int64_t n = n_p * (hi - lo) * L;
-    hipLaunchKernelGGL(prove_e_kernel, grid_of(n), dim3(kWG), 0, s, gphi_tables, tab_idx, e_sc, a_out, S, L, lo, hi,
-                       n);
+    if (w1)
+      hipLaunchKernelGGL(prove_e_kernel_w1, grid_of(n), dim3(kWG), 0, s, gphi_tables, tab_idx, e_sc, a_out, S, L, lo,
+                         hi, n);
+    else
+      hipLaunchKernelGGL(prove_e_kernel, grid_of(n), dim3(kWG), 0, s, gphi_tables, tab_idx, e_sc, a_out, S, L, lo, hi,
+                         n);
   }
   return check_hip(hipGetLastError(), "rp_prove_a_gls8");
 }
