@@ -312,6 +312,39 @@ def _dp_order(sq) -> dict:
     return cache
 
 
+def prewarm_keyswitch(reqs: list, sq, vn_ids: list, device, cache: VerifierCache):
+    """Key-switch proofs of an inbox verified for SEVERAL co-hosted VNs at once
+    (``sigma.key_switch_batch_verification_multi``: one grouped MSM, each VN
+    with its own random weights) when every VN verifies every request
+    (Threshold 1, no sharding); ``verify_requests`` then reads its VN's
+    verdicts from ``cache.ks_pre``."""
+    if len(vn_ids) < 2 or sq.Threshold < 1.0 or getattr(sq, "VerificationSharding", 0):
+        return
+    ks = [i for i, r in enumerate(reqs) if r.kind == "keyswitch" and not r.header_only]
+    if len(ks) < 2:
+        return
+    objs, valid, verdict = [], [], {}
+    for i in ks:
+        try:
+            o = _decode(reqs[i], device)
+        except Exception as e:
+            log.warning(f"keyswitch proof from {reqs[i].sender_id} rejected: {e}")
+            verdict[i] = False
+            continue
+        if o.X != sq.IDtoPublic.get(reqs[i].sender_id) or o.Q != sq.ClientPubKey:
+            verdict[i] = False
+            continue
+        objs.append(o)
+        valid.append(i)
+    for vn_id, res in zip(vn_ids, sigma.key_switch_batch_verification_multi(objs, sq.KeySwitchingProofThreshold,
+                                                                             len(vn_ids))):
+        m = dict(verdict)
+        m.update(zip(valid, res))
+        cache.ks_pre[(sq.SurveyID, vn_id)] = m
+    while len(cache.ks_pre) > 64:
+        cache.ks_pre.pop(next(iter(cache.ks_pre)))
+
+
 def should_verify(sq, req: ProofRequest, vn_index: int, n_vns: int) -> bool:
     a = assigned_vns(sq, req, n_vns)
     if a is not None:
@@ -326,6 +359,7 @@ class VerifierCache:
     def __init__(self):
         self._sig = {}
         self._early: dict = {}  # SurveyID -> {id(lists): (lists, future, index)}
+        self.ks_pre: dict = {}  # (SurveyID, vn_id) -> {request index: bool} (prewarm_keyswitch)
 
     def put_early(self, survey_id: str, objs: list, fut):
         if len(self._early) > 8:
@@ -585,6 +619,11 @@ def verify_requests(reqs: list, sq, vn_id: str, vn_index: int, n_vns: int, devic
         idxs = todo.pop("range")
         range_future = _side_pool().submit(_verify_range_side, reqs, idxs, sq, vn_id, device, cache,
                                            torch.cuda.current_stream(torch.device(device)))
+    pre = cache.ks_pre.pop((sq.SurveyID, vn_id), None)
+    if pre is not None and "keyswitch" in todo and all(i in pre for i in todo["keyswitch"]):
+        with timers.timed(f"{vn_id}_{TIMER['keyswitch']}"):
+            for i in todo.pop("keyswitch"):
+                codes[i] = PROOF_TRUE if pre[i] else PROOF_FALSE
     for kind, idxs in todo.items():
         with timers.timed(f"{vn_id}_{TIMER[kind]}"):
             if kind == "range":

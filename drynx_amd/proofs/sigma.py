@@ -388,7 +388,7 @@ def key_switch_list_proof_creation(x: int, X, Q_point, K: torch.Tensor, share: C
     return KeySwitchProof(X, Q_point, K, share, T1, T2, T3, c, za, zb)
 
 
-def key_switch_batch_verification(proofs: list, threshold: float = 1.0) -> list:
+def key_switch_batch_verification(proofs: list, threshold: float = 1.0, combine: bool = True) -> list:
     """Verify several CNs' key-switch proofs (same querier key) as ONE random
     linear combination: with fresh 64-bit weights rho_i, sig_i per element,
       (sum rho za) B + (sum sig za) Q - sum rho T1 - sum c rho (vB)
@@ -415,47 +415,81 @@ def key_switch_batch_verification(proofs: list, threshold: float = 1.0) -> list:
         ok.append(pr._fs_ok)
         if pr._fs_ok and k > 0:
             live.append((len(ok) - 1, pr, k))
-    if not live:
+    if not live or not combine:
         return ok
     with timers.span("ks.verify.msm"):
-        if _ks_combined(live):
+        if _ks_combined(live)[0]:
             return ok
     for idx, pr, k in live:
-        ok[idx] = _ks_combined([(idx, pr, k)])
+        ok[idx] = _ks_combined([(idx, pr, k)])[0]
     return ok
 
 
-def _ks_combined(live) -> bool:
+def key_switch_batch_verification_multi(proofs: list, threshold: float, n_vn: int) -> list:
+    """``key_switch_batch_verification`` for ``n_vn`` verifying nodes hosted on
+    one rank: the weight-free part once, every VN's random combination in ONE
+    grouped MSM (one bucket plan and host sync instead of one per VN), each
+    VN's verdict from its own weights.  -> [per-VN list of bools]."""
+    if not proofs:
+        return [[] for _ in range(n_vn)]
+    ok = key_switch_batch_verification(proofs, threshold, combine=False)
+    live = [(i, pr, _first(pr.K.shape[0], threshold)) for i, pr in enumerate(proofs)]
+    live = [(i, pr, k) for i, pr, k in live if ok[i] and k > 0]
+    if not live:
+        return [list(ok) for _ in range(n_vn)]
+    with timers.span("ks.verify.msm_multi"):
+        verdicts = _ks_combined(live, n_vn)
+    out = []
+    for v in range(n_vn):
+        res = list(ok)
+        if not verdicts[v]:  # this VN's own per-proof re-check blames the bad ones
+            for idx, pr, k in live:
+                res[idx] = _ks_combined([(idx, pr, k)])[0]
+        out.append(res)
+    return out
+
+
+def _ks_combined(live, n_vn: int = 1):
     """Grouped MSM: every per-element weight stays 64 bit (8 bucket additions
     per point instead of 32); the per-proof challenges c, zb multiply the five
     group sums of each proof on the host."""
+    """Grouped MSM: every per-element weight stays 64 bit (8 bucket additions
+    per point instead of 32); the per-proof challenges c, zb multiply the five
+    group sums of each proof on the host.  ``n_vn`` independent combinations
+    (fresh weights each) share the one MSM launch -> [bool] per combination."""
     dev = live[0][1].K.device
+    nl = len(live)
     pts, scs, grp = [], [], []
     sB, sQ = [], []
-    for j, (_, pr, k) in enumerate(live):
-        rho, sig = _rand64(k, dev), _rand64(k, dev)
-        za = pr.za[:k].contiguous()
-        # group 5j+0: rho T1, +1: rho vB, +2: sig K (x zb), +3: sig T2, +4: sig (vQ - xK) (x c)
-        for gi, (pt, w) in enumerate(((pr.T1, rho), (pr.share.K, rho), (pr.K, sig), (pr.T2, sig),
-                                      (pr.share.C, sig))):
-            pts.append(pt[:k])
-            scs.append(w)
-            grp.append(torch.full((k,), 5 * j + gi, dtype=torch.int32, device=dev))
-        sB.append(_fr_sum(nt.fr_arith(nt.FR_MUL, rho, za)))
-        sQ.append(_fr_sum(nt.fr_arith(nt.FR_MUL, sig, za)))
+    for v in range(n_vn):
+        for j, (_, pr, k) in enumerate(live):
+            rho, sig = _rand64(k, dev), _rand64(k, dev)
+            za = pr.za[:k].contiguous()
+            # group 5j+0: rho T1, +1: rho vB, +2: sig K (x zb), +3: sig T2, +4: sig (vQ - xK) (x c)
+            for gi, (pt, w) in enumerate(((pr.T1, rho), (pr.share.K, rho), (pr.K, sig), (pr.T2, sig),
+                                          (pr.share.C, sig))):
+                pts.append(pt[:k])
+                scs.append(w)
+                grp.append(torch.full((k,), (v * nl + j) * 5 + gi, dtype=torch.int32, device=dev))
+            sB.append(_fr_sum(nt.fr_arith(nt.FR_MUL, rho, za)))
+            sQ.append(_fr_sum(nt.fr_arith(nt.FR_MUL, sig, za)))
     G = nt.g1_msm_grouped(torch.cat(pts).contiguous(), torch.cat(scs).contiguous(), torch.cat(grp),
-                          5 * len(live), bits=64)
+                          5 * nl * n_vn, bits=64)
     Q = live[0][1].Q
-    full = torch.cat([_fr_sum(torch.cat(sB)), _fr_sum(torch.cat(sQ))]).cpu()
-    # lhs = (sum rho za) B + (sum sig za) Q; rhs = sum_j G0 + c G1 + zb G2 + G3 + c G4
-    lhs = nt.g1_add(*nt.g1_mul(bn.g1_jac_tensor([O.G1_GEN, Q], "cpu"), full).split(1))
-    facs, fpts = [], []
-    for j, (_, pr, _) in enumerate(live):
-        g = G[5 * j: 5 * j + 5]
-        facs += [1, pr.c, pr.zb, 1, pr.c]
-        fpts.append(g)
-    rhs = nt.g1_sum(nt.g1_mul(torch.cat(fpts).contiguous(), _sc(facs, "cpu")).view(-1, 1, 24))
-    return bool(nt.g1_eq(lhs, rhs)[0])
+    out = []
+    for v in range(n_vn):
+        full = torch.cat([_fr_sum(torch.cat(sB[v * nl:(v + 1) * nl])),
+                          _fr_sum(torch.cat(sQ[v * nl:(v + 1) * nl]))]).cpu()
+        # lhs = (sum rho za) B + (sum sig za) Q; rhs = sum_j G0 + c G1 + zb G2 + G3 + c G4
+        lhs = nt.g1_add(*nt.g1_mul(bn.g1_jac_tensor([O.G1_GEN, Q], "cpu"), full).split(1))
+        facs, fpts = [], []
+        for j, (_, pr, _) in enumerate(live):
+            g = G[5 * (v * nl + j): 5 * (v * nl + j) + 5]
+            facs += [1, pr.c, pr.zb, 1, pr.c]
+            fpts.append(g)
+        rhs = nt.g1_sum(nt.g1_mul(torch.cat(fpts).contiguous(), _sc(facs, "cpu")).view(-1, 1, 24))
+        out.append(bool(nt.g1_eq(lhs, rhs)[0]))
+    return out
 
 
 def obfuscation_batch_verification(proofs: list, threshold: float = 1.0) -> list:

@@ -208,6 +208,10 @@ def proof_collection(ctx, sq, local_requests: list):
     bitmaps = {}
     with timers.timed("ProofVerification"):
         pooled = _pool_async(ctx, sq, reqs, vns) if pool else None
+        local_vns = [vn.id for vn in vns if vn.rank == ctx.rank]
+        if len(local_vns) > 1:  # co-hosted VNs: one grouped key-switch MSM for all of them
+            with timers.span("verify.keyswitch.multi"):
+                prq.prewarm_keyswitch(reqs, sq, local_vns, ctx.device, ctx.verifier_cache)
         pending = {vn.id: check_requests(ctx, sq, vn, idx, len(vns), reqs, pooled)
                    for idx, vn in enumerate(vns) if vn.rank == ctx.rank}
         for vn in vns:

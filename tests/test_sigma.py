@@ -191,3 +191,20 @@ def test_schnorr_verify_batch_matches_single():
     want = [sigma.schnorr_verify(p, m, s) for p, m, s in items]
     assert want == [True] * 5 + [False] * 8
     assert sigma.schnorr_verify_batch(items) == want
+
+
+def test_multi_vn_keyswitch_verification_matches_single():
+    """Co-hosted VNs' key-switch checks in one grouped MSM (each with its own
+    weights) give every VN the single-VN verdicts, including the blame."""
+    kps = [eg.KeyPair.generate() for _ in range(3)]
+    q = eg.KeyPair.generate()
+    cv, _ = eg.encrypt_ints(eg.pk_table(eg.aggregate_keys([k.public for k in kps])), [5, 6, 7])
+    ks = []
+    for kp in kps:
+        share, v = sigma.key_switch_share(kp.secret, cv.K, q.public)
+        ks.append(sigma.key_switch_list_proof_creation(kp.secret, kp.public, q.public, cv.K, share, v))
+    assert sigma.key_switch_batch_verification_multi(ks, 1.0, 3) == [[True] * 3] * 3
+    ks[2].za = ks[2].za.clone()
+    ks[2].za[1, 0] ^= 1
+    assert sigma.key_switch_batch_verification_multi(ks, 1.0, 2) == [[True, True, False]] * 2
+    assert sigma.key_switch_batch_verification_multi([], 1.0, 2) == [[], []]
