@@ -112,7 +112,9 @@ def main():
     workdir = tempfile.mkdtemp(prefix=f"drynx_bench_r{rank}_")
     n_dps, n_vns = args.dps, args.vns
     # CNs on ranks 0.., VNs right after them, DPs round robin over every rank
-    offsets = {"cn": 0, "vn": args.cns % world, "dp": 0}
+    # starting after the CN / VN ranks (the ranks that draw an extra DP are the
+    # ones without a CN or VN role: N=4 -> ranks 2, 3; N=8 -> ranks 6, 7)
+    offsets = {"cn": 0, "vn": args.cns % world, "dp": (args.cns + args.vns) % world}
     cl, node = local_cluster(args.cns, n_dps, n_vns, comm=comm, device=device, workdir=workdir, offsets=offsets)
     rec_per_dp = max(1, args.records // n_dps)
     d = args.features
@@ -274,7 +276,7 @@ def main_query(args):
     if device.type == "cuda":
         torch.cuda.set_device(device)
     n_dps = cfg["dps"]
-    offsets = {"cn": 0, "vn": args.cns % world, "dp": 0}
+    offsets = {"cn": 0, "vn": args.cns % world, "dp": (args.cns + args.vns) % world}
     cl, node = local_cluster(args.cns, n_dps, args.vns, comm=comm, device=device,
                              workdir=tempfile.mkdtemp(prefix=f"drynx_bench_r{rank}_"), offsets=offsets)
     rows = cfg["records"] // n_dps
