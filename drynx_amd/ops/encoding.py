@@ -39,6 +39,7 @@ class CreateProofBatch:
     l: list
     sig_col: list
     offset: list = field(default_factory=list)
+    values_t: Optional[torch.Tensor] = None   # the values as a device int64 tensor (prover digits on the device)
 
     def __len__(self):
         return len(self.values)
@@ -51,9 +52,10 @@ def cat_proof_batches(batches: list) -> "CreateProofBatch":
     offs = []
     for b in batches:
         offs += list(b.offset) if b.offset else [0] * len(b)
+    vt = torch.cat([b.values_t for b in batches]) if all(b.values_t is not None for b in batches) else None
     return CreateProofBatch([v for b in batches for v in b.values], torch.cat([b.r for b in batches]).contiguous(),
                             eg.CipherVector.cat([b.cv for b in batches]), [x for b in batches for x in b.u],
-                            [x for b in batches for x in b.l], [x for b in batches for x in b.sig_col], offs)
+                            [x for b in batches for x in b.l], [x for b in batches for x in b.sig_col], offs, vt)
 
 
 @dataclass

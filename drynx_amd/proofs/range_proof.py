@@ -480,6 +480,20 @@ def create_range_proofs(batch, sigmat: SigMaterial, P_point, device=None, mode: 
     Returns a list of RangeProofList (one per distinct (u, l)).  ``mode`` 2
     produces the v2 transcript (``SurveyQuery.RangeProofMode``)."""
     device = torch.device(device or batch.cv.device)
+    n = len(batch)
+    u_arr, l_arr = np.asarray(batch.u, dtype=np.int64), np.asarray(batch.l, dtype=np.int64)
+    if n and (u_arr == u_arr[0]).all() and (l_arr == l_arr[0]).all():
+        # one (u, l) for the whole batch (every query the simulation runs): no per-item Python loops
+        u, l = int(u_arr[0]), int(l_arr[0])
+        cols_a = np.asarray(batch.sig_col, dtype=np.int64)
+        su = np.asarray(sigmat.u + [0], dtype=np.int64)
+        bad_m = (cols_a >= sigmat.n_cols) | (cols_a < 0) | (su[np.clip(cols_a, 0, sigmat.n_cols)] < u)
+        if bad_m.any():
+            raise ValueError(f"query Ranges base u={u} exceeds the input-validation signatures of column(s) "
+                             f"{sorted(set(cols_a[bad_m].tolist()))[:8]} (the CNs signed fewer digits)")
+        offs = list(batch.offset) if batch.offset else [0] * n
+        return [_prove_group(u, l, batch.values, offs, list(batch.sig_col), batch.r.contiguous(),
+                             batch.cv.to(device), sigmat, P_point, device, mode, vals_t=batch.values_t)]
     groups: dict = {}
     for idx in range(len(batch)):
         groups.setdefault((batch.u[idx], batch.l[idx]), []).append(idx)
@@ -533,7 +547,22 @@ def challenges(C_jac, cols, sigmat: SigMaterial, device, mode: int = 0, D=None, 
     return bn.scalars_tensor(out, device)
 
 
-def _prove_group(u, l, vals, offs, cols, r, cv, sigmat, P_point, device, mode=0) -> RangeProofList:
+def _digits_dev(vals_t: torch.Tensor, offs: list, u: int, l: int, device, vals: list | None = None):
+    """Device [n, l] base-u digits of m + offset (low l digits, as ``_digits``)
+    when every power u^j (j < l) and every m + offset fit int64 (|m| < 2^62,
+    checked on the host copy ``vals``; 0 <= offset <= 2^62), else None."""
+    if u < 2 or u ** (l - 1) >= (1 << 62) or not offs or max(offs) > (1 << 62) or min(offs) < 0:
+        return None
+    if vals is not None and vals and (max(vals) >= (1 << 62) or min(vals) <= -(1 << 62)):
+        return None
+    x = vals_t.to(device=device, dtype=torch.int64)
+    o = offs[0]
+    x = x + (o if offs.count(o) == len(offs) else bn.h2d(torch.tensor(offs, dtype=torch.int64), device))
+    pw = bn.h2d(torch.tensor([u ** j for j in range(l)], dtype=torch.int64), device)
+    return torch.remainder(torch.div(x.view(-1, 1), pw.view(1, -1), rounding_mode="floor"), u)
+
+
+def _prove_group(u, l, vals, offs, cols, r, cv, sigmat, P_point, device, mode=0, vals_t=None) -> RangeProofList:
     n = len(vals)
     S = sigmat.S
     rpl = RangeProofList(u, l, S, offs, cols, cv)
@@ -544,7 +573,8 @@ def _prove_group(u, l, vals, offs, cols, r, cv, sigmat, P_point, device, mode=0)
     tabP = pk_table(P_point, device).tabP
     # digits of m + offset
     with timers.span("rp.prove.digits"):
-        phi = _digits(vals, offs, u, l)
+        phi_t = _digits_dev(vals_t, offs, u, l, device, vals) if vals_t is not None else None
+        phi = _digits(vals, offs, u, l) if phi_t is None else None
     # randomness
     with timers.span("rp.prove.random"):
         s = bn.random_scalars(n * l, device)
@@ -559,7 +589,8 @@ def _prove_group(u, l, vals, offs, cols, r, cv, sigmat, P_point, device, mode=0)
     # V_ij = v_ij * A_{i, col, phi_j};  a_ij = e(-s_j B, V_ij) e(t_j B, B2)
     cols_t = bn.h2d(torch.tensor(cols, dtype=torch.long), device)
     i_idx = torch.arange(S, device=device)
-    phi_t = bn.h2d(torch.from_numpy(phi), device)
+    if phi_t is None:
+        phi_t = bn.h2d(torch.from_numpy(phi), device)
     a_index = ((i_idx.view(1, S, 1) * sigmat.n_cols + cols_t.view(n, 1, 1)) * max(1, sigmat.umax)
                + phi_t.view(n, 1, l)).reshape(-1)
     _, gt_tab = gt_generator_table(device)
@@ -584,7 +615,11 @@ def _prove_group(u, l, vals, offs, cols, r, cv, sigmat, P_point, device, mode=0)
     with timers.span("rp.prove.challenge"):
         c = challenges(cv.C, cols, sigmat, device, mode, D, V, A, S, l)
     # responses: Zphi_j = s_j - c phi_j ; Zr = sum m - c r ; Zv_ij = t_j - c v_ij
-    phi_sc = _small_scalars(phi.reshape(-1), device)
+    if phi is None:
+        phi_sc = torch.zeros((n * l, 8), dtype=torch.int32, device=device)
+        phi_sc[:, 0] = phi_t.reshape(-1).to(torch.int32)              # 0 <= phi < u < 2^31
+    else:
+        phi_sc = _small_scalars(phi.reshape(-1), device)
     zphi = nt.fr_arith(nt.FR_SUB, s, nt.fr_arith(nt.FR_MUL, _rep(c, l), phi_sc))
     zr = nt.fr_arith(nt.FR_SUB, msum, nt.fr_arith(nt.FR_MUL, c, r))
     t_rep = t.view(n, 1, l, 8).expand(n, S, l, 8).reshape(-1, 8).contiguous()

@@ -203,7 +203,7 @@ def _encode_batch_tail(ctx, sq, dps: list, vals: torch.Tensor, groups, pk) -> di
             for j in range(ng):
                 lo = base + j * n_out
                 proofs.append(enc.CreateProofBatch(list(v), r[lo: lo + n_out], cv[lo: lo + n_out], us, ls,
-                                                   list(range(n_out)), offs))
+                                                   list(range(n_out)), offs, vals[i]))
         else:
             proofs = [None] * ng
         out[dp.id] = {"cv": eg.CipherVector(K[i], C[i]), "proofs": proofs, "clear": [list(v) for _ in groups],

@@ -110,3 +110,18 @@ def test_prover_table_layouts_agree(setup, bits, monkeypatch):
     rpl = rp.create_range_proofs(b, sm, P)[0]
     assert rp.verify_range_proof_list(rpl, sm, P)
     assert all(rp.verify_range_proof_single_reference(rpl, p, sm, P) for p in range(3))
+
+
+def test_device_digits_match_host_digits():
+    """The prover's device digit decomposition (int64, low l digits of
+    m + offset) equals the host one, and declines values outside its range."""
+    import random
+
+    import torch
+
+    for u, l in [(16, 16), (4, 3), (2, 5), (10, 6)]:
+        off = min(u ** l // 2, 1 << 62)
+        vals = [random.randint(-off, min(u ** l - off - 1, (1 << 62) - 1)) for _ in range(200)]
+        got = rp._digits_dev(torch.tensor(vals), [off] * 200, u, l, "cpu", vals)
+        assert (got.numpy() == rp._digits(vals, [off] * 200, u, l)).all()
+    assert rp._digits_dev(torch.tensor([1 << 62]), [0], 16, 16, "cpu", [1 << 62]) is None
