@@ -61,6 +61,16 @@ def sign(secret: int, msg: bytes) -> tuple:
     return bn.g1_mul_point(secret % O.R, hash_to_g1(msg))
 
 
+def sign_many(items: list) -> list:
+    """[(secret, msg)] -> signatures, all scalar multiplications in ONE native
+    batch (the VNs co-hosted on a rank sign a block and a forward link each)."""
+    if not items:
+        return []
+    pts = bn.g1_jac_tensor([hash_to_g1(m) for _, m in items], "cpu")
+    ks = bn.scalars_tensor([sk % O.R for sk, _ in items], "cpu")
+    return bn.g1_points_from_jac(nt.g1_mul(pts, ks))
+
+
 def bdn_coefficients(publics: list) -> list:
     """t_i = first 128 bits of SHA-256(tag || i || X2_0 || ... || X2_{n-1})."""
     h = hashlib.sha256(_COEF_TAG)

@@ -230,6 +230,37 @@ def sign_forward_link(prev: SkipBlock, to_hash: str, secret: int) -> str:
     return schnorr_sign(secret, msg).hex()
 
 
+def cosign_many(sb: SkipBlock, signers: list) -> tuple:
+    """Several VNs of one rank sign ``sb`` (and, when they hold a previous
+    block, the forward link prev -> sb) in one batch of BLS scalar
+    multiplications.  signers: [(vn_id, secret, prev | None)] ->
+    ({vn_id: block partial hex}, {vn_id: link partial hex})."""
+    if sb.bls_keys() is None:
+        sigs, links = {}, {}
+        for vn_id, sk, prev in signers:
+            sign_block(sb, vn_id, sk)
+            sigs[vn_id] = sb.ForwardSignatures[vn_id]
+            if prev is not None:
+                links[vn_id] = sign_forward_link(prev, sb.Hash, sk)
+        return sigs, links
+    items, where = [], []
+    for vn_id, sk, prev in signers:
+        items.append((sk, bytes.fromhex(sb.Hash)))
+        where.append(("b", vn_id))
+        if prev is not None:
+            items.append((sk, forward_link_message(prev.Hash, sb.Hash)))
+            where.append(("l", vn_id))
+    sigs, links = {}, {}
+    for (kind, vn_id), sig in zip(where, bls.sign_many(items)):
+        h = O.g1_to_bytes(sig).hex()
+        if kind == "b":
+            sb.ForwardSignatures[vn_id] = h
+            sigs[vn_id] = h
+        else:
+            links[vn_id] = h
+    return sigs, links
+
+
 def add_forward_link(prev: SkipBlock, to_hash: str, partials: dict):
     """Aggregate the roster's partial signatures into prev's forward link."""
     link = {"To": to_hash, "CoSig": "", "Sigs": {}}

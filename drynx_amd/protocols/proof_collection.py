@@ -240,18 +240,16 @@ def proof_collection(ctx, sq, local_requests: list):
     block = skc.SkipBlock.from_bytes(block_bytes)
     # every VN runs its verifiers (verifyFuncBitmap, VerifyBase against its own
     # latest block), then signs the block and the forward link from its latest
-    sigs, links = {}, {}
+    signers = []
     for vn in vns:
         if vn.rank == ctx.rank:
             prev = ctx.vn_latest(vn.id)
             if skc.verify_bitmap(block, ctx.local_bitmaps.get((sq.SurveyID, vn.id), {}), vn.id) \
                     and skc.verify_base(prev, block):
-                skc.sign_block(block, vn.id, vn.keypair.secret)
-                sigs[vn.id] = block.ForwardSignatures[vn.id]
-                if prev is not None:
-                    links[vn.id] = skc.sign_forward_link(prev, block.Hash, vn.keypair.secret)
+                signers.append((vn.id, vn.keypair.secret, prev))
             else:
                 log.warning(f"{vn.id} refused block for survey {sq.SurveyID}")
+    sigs, links = skc.cosign_many(block, signers)  # the co-hosted VNs' partials in one batch
     for d, fl in ctx.comm.all_gather_object((sigs, links)):
         block.ForwardSignatures.update(d)
         links.update(fl)
