@@ -293,8 +293,6 @@ def g1_mul_point(k: int, P=None):
     ks = scalars_tensor([k], "cpu")
     if P is None or P == O.G1_GEN:
         return g1_points_from_jac(nt.g1_fb_mul(base_table("cpu"), ks))[0]
-    if P is None:
-        return None
     return g1_points_from_jac(nt.g1_mul(g1_jac_tensor([P], "cpu"), ks))[0]
 
 

@@ -452,9 +452,6 @@ def key_switch_batch_verification_multi(proofs: list, threshold: float, n_vn: in
 def _ks_combined(live, n_vn: int = 1):
     """Grouped MSM: every per-element weight stays 64 bit (8 bucket additions
     per point instead of 32); the per-proof challenges c, zb multiply the five
-    group sums of each proof on the host."""
-    """Grouped MSM: every per-element weight stays 64 bit (8 bucket additions
-    per point instead of 32); the per-proof challenges c, zb multiply the five
     group sums of each proof on the host.  ``n_vn`` independent combinations
     (fresh weights each) share the one MSM launch -> [bool] per combination."""
     dev = live[0][1].K.device
