@@ -7,8 +7,9 @@ torch.distributed:
 
 * device tensors (ciphertext vectors, proof blobs) go over the ``nccl``
   backend, which on ROCm is RCCL over xGMI;
-* small control messages (the SurveyQuery, bitmaps, acks) use
-  ``broadcast_object_list`` / ``all_gather_object`` on a gloo group.
+* small control messages (the SurveyQuery, bitmaps, acks) are msgpack-coded
+  (``obj_to_bytes``: plain data only -- no pickle, nothing executable crosses a
+  rank boundary) and broadcast / all-gathered as byte tensors on a gloo group.
 
 Point-to-point patterns used by the protocols:
   - ``exchange``: personalised all-to-all (star gathers DP->CN, CN->root, proof
@@ -22,8 +23,8 @@ kernels (parallel/ec_collectives.py).
 from __future__ import annotations
 
 import os
-import pickle
 
+import msgpack
 import numpy as np
 import torch
 import torch.distributed as dist
@@ -110,14 +111,28 @@ class DistComm(Comm):
             dist.barrier()
 
     def broadcast_object(self, obj, src: int = 0):
-        lst = [obj]
-        dist.broadcast_object_list(lst, src=src, group=self._ctrl)
-        return lst[0]
+        if self.rank == src:
+            b = obj_to_bytes(obj)
+            n = torch.tensor([len(b)], dtype=torch.int64)
+        else:
+            n = torch.zeros(1, dtype=torch.int64)
+        dist.broadcast(n, src, group=self._ctrl)
+        buf = (torch.frombuffer(bytearray(b), dtype=torch.uint8) if self.rank == src
+               else torch.empty(int(n), dtype=torch.uint8))
+        dist.broadcast(buf, src, group=self._ctrl)
+        return obj if self.rank == src else bytes_to_obj(buf.numpy().tobytes())
 
     def all_gather_object(self, obj) -> list:
-        out = [None] * self.world
-        dist.all_gather_object(out, obj, group=self._ctrl)
-        return out
+        b = obj_to_bytes(obj)
+        sizes = [torch.zeros(1, dtype=torch.int64) for _ in range(self.world)]
+        dist.all_gather(sizes, torch.tensor([len(b)], dtype=torch.int64), group=self._ctrl)
+        m = max(int(x) for x in sizes)
+        mine = torch.zeros(m, dtype=torch.uint8)
+        mine[: len(b)] = torch.frombuffer(bytearray(b), dtype=torch.uint8)
+        bufs = [torch.empty(m, dtype=torch.uint8) for _ in range(self.world)]
+        dist.all_gather(bufs, mine, group=self._ctrl)
+        return [obj if r == self.rank else bytes_to_obj(bufs[r][: int(sizes[r])].numpy().tobytes())
+                for r in range(self.world)]
 
     def exchange(self, outgoing: dict, recv_sizes: dict | None = None) -> dict:
         W = self.world
@@ -207,10 +222,74 @@ def init_distributed(backend: str | None = None):
         dist.init_process_group("gloo")
 
 
+# ---------------------------------------------------------------- control codec
+# msgpack plus four extension types; anything else is refused when encoding.
+# Decoding builds only ints, floats, str, bytes, lists, dicts, tuples, sets,
+# numpy arrays and CPU tensors of whitelisted dtypes: a peer's message cannot
+# name code to run (the reference's onet messages are protobuf for the same
+# reason).
+_X_INT, _X_TUPLE, _X_SET, _X_TENSOR, _X_NDARRAY = 1, 2, 3, 4, 5
+_TORCH_DTYPES = {str(d).removeprefix("torch."): d for d in (
+    torch.uint8, torch.int8, torch.int16, torch.int32, torch.int64, torch.bool, torch.float16, torch.bfloat16,
+    torch.float32, torch.float64)}
+_NP_DTYPES = {np.dtype(t).str for t in (np.uint8, np.int8, np.int16, np.int32, np.int64, np.uint16, np.uint32,
+                                        np.uint64, np.bool_, np.float16, np.float32, np.float64)}
+
+
+def _pack_default(o):
+    if isinstance(o, bool):
+        return bool(o)
+    if isinstance(o, int):  # beyond 64 bits (BN254 scalars, coordinates)
+        return msgpack.ExtType(_X_INT, int(o).to_bytes(int(o).bit_length() // 8 + 1, "little", signed=True))
+    if isinstance(o, tuple):
+        return msgpack.ExtType(_X_TUPLE, obj_to_bytes(list(o)))
+    if isinstance(o, (set, frozenset)):
+        return msgpack.ExtType(_X_SET, obj_to_bytes(list(o)))
+    if isinstance(o, (bytearray, memoryview)):
+        return bytes(o)
+    if isinstance(o, np.generic):
+        return o.item()
+    for base in (dict, list, str, float, bytes):  # subclasses (OrderedDict, IntEnum-like str, ...)
+        if isinstance(o, base):
+            return base(o)
+    if isinstance(o, torch.Tensor):
+        t = o.detach().cpu().contiguous()
+        name = str(t.dtype).removeprefix("torch.")
+        if name not in _TORCH_DTYPES:
+            raise TypeError(f"control message: tensor dtype {t.dtype} not supported")
+        raw = t.reshape(-1).view(torch.uint8).numpy().tobytes() if t.numel() else b""
+        return msgpack.ExtType(_X_TENSOR, obj_to_bytes([name, list(t.shape), raw]))
+    if isinstance(o, np.ndarray):
+        a = np.ascontiguousarray(o)
+        if a.dtype.str not in _NP_DTYPES:
+            raise TypeError(f"control message: array dtype {a.dtype} not supported")
+        return msgpack.ExtType(_X_NDARRAY, obj_to_bytes([a.dtype.str, list(a.shape), a.tobytes()]))
+    raise TypeError(f"control message: {type(o).__name__} is not plain data")
+
+
+def _ext_hook(code, data):
+    if code == _X_INT:
+        return int.from_bytes(data, "little", signed=True)
+    if code == _X_TUPLE:
+        return tuple(bytes_to_obj(data))
+    if code == _X_SET:
+        return set(bytes_to_obj(data))
+    if code == _X_TENSOR:
+        name, shape, raw = bytes_to_obj(data)
+        dt = _TORCH_DTYPES[name]
+        flat = torch.frombuffer(bytearray(raw), dtype=torch.uint8) if raw else torch.zeros(0, dtype=torch.uint8)
+        return flat.view(dt).reshape(shape)
+    if code == _X_NDARRAY:
+        dts, shape, raw = bytes_to_obj(data)
+        if dts not in _NP_DTYPES:
+            raise ValueError(f"control message: array dtype {dts} not supported")
+        return np.frombuffer(raw, dtype=np.dtype(dts)).reshape(shape).copy()
+    raise ValueError(f"control message: unknown extension type {code}")
+
+
 def obj_to_bytes(obj) -> bytes:
-    return pickle.dumps(obj, protocol=pickle.HIGHEST_PROTOCOL)
+    return msgpack.packb(obj, default=_pack_default, strict_types=True, use_bin_type=True)
 
 
 def bytes_to_obj(b: bytes):
-    # only ever applied to payloads produced by this framework's own ranks
-    return pickle.loads(b)
+    return msgpack.unpackb(b, ext_hook=_ext_hook, raw=False, strict_map_key=False)
