@@ -94,6 +94,8 @@ def parse():
     ap.add_argument("--max-iter", type=int, default=450)
     ap.add_argument("--device", default=None)
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--range-mode", type=int, default=0,
+                    help="SurveyQuery.RangeProofMode: 0 reference semantics, 1 recomputed challenge + V in G2")
     ap.add_argument("--query", default="lr", choices=["lr", *QUERY_CONFIGS],
                     help="lr = the headline; mean/variance/lin_reg = BASELINE.json configs 2 and 3")
     return ap.parse_args()
@@ -141,7 +143,8 @@ def main():
     if rank == 0:  # CN input-validation keys are set up once, before the queries (as in the reference simulation)
         template = make_survey(client, cl, "logistic regression", proofs=1, ranges=[args.u, args.l, offset],
                                lr_params=lp, thresholds=[1.0, 1.0, 1.0, 0.0, 1.0], verification_sharding=0,
-                               sig_device=device, deterministic_sigs=args.deterministic_sigs)
+                               sig_device=device, deterministic_sigs=args.deterministic_sigs,
+                               range_proof_mode=args.range_mode)
 
     def one_step():
         if rank == 0:

@@ -187,6 +187,32 @@ extern "C" int dx_sha256_rows(int on_gpu, void *stream, const uint8_t *data, int
   return run(on_gpu, stream, rows * k, op, false, "sha256_rows");
 }
 
+// Slice digests of MANY payloads in one launch (a VN inbox: every proof
+// envelope of every CN / DP, and the transcripts inside them).  seg[3*q ..]
+// = (address, byte length, first output slice) of payload q, in ascending
+// first-slice order; every payload has ceil(len / chunk) slices (1 if empty).
+// One thread per slice finds its payload by binary search.
+extern "C" int dx_sha256_segments(int on_gpu, void *stream, const int64_t *seg, int64_t n_seg, int64_t total,
+                                  int64_t chunk, uint32_t *out) {
+  if (chunk <= 0 || (chunk & 63) != 0 || n_seg <= 0) return -2;
+  auto op = [=] __host__ __device__(int64_t t) {
+    int64_t lo = 0, hi = n_seg - 1;
+    while (lo < hi) {  // last segment whose first slice <= t
+      const int64_t mid = (lo + hi + 1) >> 1;
+      if (seg[3 * mid + 2] <= t) lo = mid;
+      else hi = mid - 1;
+    }
+    const uint8_t *base = (const uint8_t *)(uintptr_t)seg[3 * lo];
+    const int64_t len = seg[3 * lo + 1];
+    const int64_t off = (t - seg[3 * lo + 2]) * chunk;
+    const int64_t m = len - off < chunk ? len - off : chunk;
+    uint32_t d[8];
+    sha256_bytes(base + off, m > 0 ? m : 0, d);
+    for (int q = 0; q < 8; q++) out[8 * t + q] = d[q];
+  };
+  return run(on_gpu, stream, total, op, false, "sha256_segments");
+}
+
 // Independent G1 generators h_i (unknown discrete logs) for commitment
 // schemes -- the permutation commitments of the shuffle proof.  For index i:
 // ctr = 0, 1, ...: x = SHA-256(seed || le64(i) || le32(ctr)) (big endian) mod p;

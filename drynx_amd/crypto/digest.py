@@ -57,3 +57,23 @@ def digest_rows(t: torch.Tensor) -> list:
     be = words.cpu().numpy().view(np.uint32).astype(">u4")
     row_bytes = t.shape[1] * t.element_size()
     return [_finish(row_bytes, be[r].tobytes()) for r in range(t.shape[0])]
+
+
+def digest_many(tensors: list) -> list:
+    """``digest_tensor`` of many tensors of one device: one segmented launch
+    and ONE device-to-host copy for all of them (a VN inbox's envelopes)."""
+    if not tensors:
+        return []
+    dev = tensors[0].device
+    same = all(t.device == dev for t in tensors)
+    if not same:
+        return [digest_tensor(t) for t in tensors]
+    parts = nt.sha256_segments(tensors, CHUNK)
+    flat = torch.cat(parts) if len(parts) > 1 else parts[0]
+    be = flat.cpu().numpy().view(np.uint32).astype(">u4")
+    out, o = [], 0
+    for t, p in zip(tensors, parts):
+        k = p.shape[0]
+        out.append(_finish(t.numel() * t.element_size(), be[o: o + k].tobytes()))
+        o += k
+    return out

@@ -120,6 +120,7 @@ _SIGS = {
     "dx_rp_verify_items": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _I],
     "dx_int_moments": [_I, _P, _P, _L, _I, _P, _L, _P, _I, _P, _P],
     "dx_sha256_rows": [_I, _P, _P, _L, _L, _L, _L, _P],
+    "dx_sha256_segments": [_I, _P, _P, _L, _L, _L, _P],
     "dx_rp_points_glv": [_P, _P, _P, _P, _P, _P, _L, _I, _I, _I],
     "dx_g1_aff_to_uv": [_I, _P, _P, _L],
     "dx_rp_ncoeffs_ni": [_P, _P, _P, _P, _L],
@@ -798,6 +799,30 @@ def sha256_chunks(data: torch.Tensor, chunk: int) -> torch.Tensor:
     g, s = _ctx(data)
     _call("dx_sha256_chunks", g, s, _ptr(data), nbytes, chunk, _ptr(out))
     return out
+
+
+def sha256_segments(tensors: list, chunk: int) -> list:
+    """``sha256_chunks`` of many contiguous tensors (same device) in ONE
+    launch -> list of [k_i, 8] views of one output tensor."""
+    if not tensors:
+        return []
+    dev = tensors[0].device
+    ts = [t.contiguous() for t in tensors]
+    nbytes = [t.numel() * t.element_size() for t in ts]
+    ks = [max(1, (b + chunk - 1) // chunk) for b in nbytes]
+    first = np.concatenate([[0], np.cumsum(ks)[:-1]]).astype(np.int64)
+    desc = np.empty((len(ts), 3), dtype=np.int64)
+    desc[:, 0] = [t.data_ptr() for t in ts]
+    desc[:, 1] = nbytes
+    desc[:, 2] = first
+    total = int(sum(ks))
+    out = torch.empty((total, 8), dtype=torch.int32, device=dev)
+    d = _upload(desc, dev)
+    g, s = _ctx(out)
+    # (the descriptor and any contiguous copies are allocated on this stream:
+    # the caching allocator reuses them only behind this launch)
+    _call("dx_sha256_segments", g, s, _ptr(d), len(ts), total, chunk, _ptr(out))
+    return [out[a: a + k] for a, k in zip(first.tolist(), ks)]
 
 
 INT_MOMENTS_MAX_COLS = 64

@@ -13,9 +13,10 @@ torch.distributed:
 
 Point-to-point patterns used by the protocols:
   - ``exchange``: personalised all-to-all (star gathers DP->CN, CN->root, proof
-    fan-out to VNs).  On RCCL this is ONE ``all_to_all_single`` whose per-peer
-    splits go straight over the 7 xGMI links (no ring hops); gloo has no
-    all-to-all so it falls back to all_gather of padded buffers.
+    fan-out to VNs): ONE ``all_to_all_single`` whose per-peer splits go
+    straight over the 7 xGMI links on RCCL (no ring hops).  gloo runs the very
+    same call on host-staged buffers, so every CPU multi-process test
+    exercises the split / size logic of the RCCL path.
   - ``send/recv``: the DRO shuffle chain CN_i -> CN_{i+1}.
 RCCL cannot add BN254 points, so EC reductions are exchange + HIP reduce
 kernels (parallel/ec_collectives.py).
@@ -34,6 +35,8 @@ class Comm:
     rank: int = 0
     world: int = 1
     device: torch.device = torch.device("cpu")
+    bytes_sent: int = 0  # data-plane bytes to / from other ranks (traffic accounting)
+    bytes_recv: int = 0
 
     def barrier(self):
         pass
@@ -103,6 +106,9 @@ class DistComm(Comm):
         self.device = torch.device(device)
         # control plane: gloo group (CPU objects) even when the data plane is RCCL
         self._ctrl = dist.new_group(backend="gloo") if self.backend == "nccl" else None
+        # where the data plane's all_to_all_single buffers live: HBM for RCCL,
+        # host memory for gloo (whose all-to-all is CPU only)
+        self._stage = self.device if self.backend == "nccl" else torch.device("cpu")
 
     def barrier(self):
         if self.backend == "nccl":
@@ -135,61 +141,48 @@ class DistComm(Comm):
                 for r in range(self.world)]
 
     def exchange(self, outgoing: dict, recv_sizes: dict | None = None) -> dict:
+        """ONE ``all_to_all_single`` whatever the backend: on RCCL the per-peer
+        splits go straight over the xGMI links from HBM; on gloo (CPU tests,
+        one-GPU rehearsals) the same call runs on host-staged buffers.  Unknown
+        receive sizes cost one size round (a W-element all-to-all)."""
         W = self.world
+        stage = self._stage
         flat = {d: t.reshape(-1).to(torch.int32) for d, t in outgoing.items()}
-        sizes = torch.zeros(W, dtype=torch.int64)
+        send_sizes = [0] * W
         for d, t in flat.items():
-            sizes[d] = t.numel()
-        if self.backend == "nccl":
-            if recv_sizes is not None:
-                known = recv_sizes
-                recv_sizes = torch.zeros(W, dtype=torch.int64)
-                for s_, n_ in known.items():
-                    recv_sizes[s_] = int(n_)
-            else:
-                send_sizes = sizes.to(self.device)
-                rs = torch.empty_like(send_sizes)
-                dist.all_to_all_single(rs, send_sizes)
-                recv_sizes = rs.cpu()
-            send = torch.cat([flat.get(d, torch.empty(0, dtype=torch.int32, device=self.device)) for d in range(W)])
-            if send.numel() == 0:
-                send = torch.empty(0, dtype=torch.int32, device=self.device)
-            recv = torch.empty(int(recv_sizes.sum()), dtype=torch.int32, device=self.device)
-            dist.all_to_all_single(recv, send.to(self.device), output_split_sizes=recv_sizes.tolist(),
-                                   input_split_sizes=sizes.tolist())
-            out, off = {}, 0
-            for s in range(W):
-                n = int(recv_sizes[s])
-                if n:
-                    out[s] = recv[off: off + n]
-                off += n
-            return out
-        # gloo: all_gather a [W, maxlen] matrix of padded per-destination payloads
-        all_sizes = [torch.zeros(W, dtype=torch.int64) for _ in range(W)]
-        dist.all_gather(all_sizes, sizes)
-        mat = torch.stack(all_sizes)  # [src, dst]
-        maxlen = int(mat.max()) if mat.numel() else 0
-        if maxlen == 0:
-            return {}
-        buf = torch.zeros((W, maxlen), dtype=torch.int32)
-        for d, t in flat.items():
-            buf[d, : t.numel()] = t.cpu()
-        gathered = [torch.zeros((W, maxlen), dtype=torch.int32) for _ in range(W)]
-        dist.all_gather(gathered, buf)
-        out = {}
+            send_sizes[d] = t.numel()
+        if recv_sizes is None:
+            ss = torch.tensor(send_sizes, dtype=torch.int64, device=stage)
+            rs = torch.empty_like(ss)
+            dist.all_to_all_single(rs, ss)
+            recv = [int(v) for v in rs.tolist()]
+        else:
+            recv = [int(recv_sizes.get(s, 0)) for s in range(W)]
+        parts = [flat[d].to(stage) for d in range(W) if send_sizes[d]]
+        send = torch.cat(parts) if parts else torch.empty(0, dtype=torch.int32, device=stage)
+        buf = torch.empty(sum(recv), dtype=torch.int32, device=stage)
+        dist.all_to_all_single(buf, send, output_split_sizes=recv, input_split_sizes=send_sizes)
+        self.bytes_sent += 4 * (sum(send_sizes) - send_sizes[self.rank])
+        self.bytes_recv += 4 * (sum(recv) - recv[self.rank])
+        if buf.device != self.device:
+            buf = buf.to(self.device, non_blocking=True)
+        out, off = {}, 0
         for s in range(W):
-            n = int(mat[s, self.rank])
-            if n:
-                out[s] = gathered[s][self.rank, :n].to(self.device)
+            if recv[s]:
+                out[s] = buf[off: off + recv[s]]
+            off += recv[s]
         return out
 
     def send(self, t: torch.Tensor, dst: int):
-        dist.send(t.contiguous(), dst)
+        t = t.contiguous().to(self._stage)
+        self.bytes_sent += t.numel() * t.element_size()
+        dist.send(t, dst)
 
     def recv(self, numel: int, src: int) -> torch.Tensor:
-        t = torch.empty(numel, dtype=torch.int32, device=self.device)
+        t = torch.empty(numel, dtype=torch.int32, device=self._stage)
         dist.recv(t, src)
-        return t
+        self.bytes_recv += 4 * numel
+        return t.to(self.device)
 
 
 def make_comm(device=None) -> Comm:

@@ -52,16 +52,30 @@ def route(comm: Comm, items: list, key_index) -> dict:
         outgoing[dst] = torch.cat([torch.tensor(hdr, dtype=torch.int32).to(comm.device)] + [r for _, _, r in parts])
     got = comm.exchange(outgoing)
     out = {}
-    for src in sorted(got):
+    srcs = sorted(got)
+    if not srcs:
+        return out
+    # every source's header words in ONE device-to-host copy (up to _HDR_ITEMS
+    # items per source; a longer header is fetched on its own)
+    H = 1 + 2 * _HDR_ITEMS
+    heads = torch.nn.utils.rnn.pad_sequence([got[s][:H] for s in srcs], batch_first=True).cpu().tolist()
+    for src, head in zip(srcs, heads):
         buf = got[src]
-        n_items = int(buf[0])
-        hdr = buf[1: 1 + 2 * n_items].cpu().tolist()
+        n_items = int(head[0])
+        if n_items < 0 or 1 + 2 * n_items > buf.numel():
+            raise ValueError(f"route: malformed header from rank {src}")
+        hdr = head[1: 1 + 2 * n_items] if n_items <= _HDR_ITEMS else buf[1: 1 + 2 * n_items].cpu().tolist()
         off = 1 + 2 * n_items
         for q in range(n_items):
             k, n = hdr[2 * q], hdr[2 * q + 1]
+            if n < 0 or off + n * ROW > buf.numel():
+                raise ValueError(f"route: item {q} from rank {src} overruns its buffer")
             out[key_index.decode(k)] = rows_to_cv(buf[off: off + n * ROW])
             off += n * ROW
     return out
+
+
+_HDR_ITEMS = 64
 
 
 class KeyIndex:

@@ -56,3 +56,15 @@ def test_gpu_digest_and_rng(gpu_device):
     assert D.digest_tensor(_t(b, gpu_device)) == D.digest_bytes(b)
     s = bn.scalars_from_tensor(bn.random_scalars(50000, gpu_device))
     assert all(0 < x < O.R for x in s) and len(set(s)) == 50000
+
+
+def test_digest_many_matches_single():
+    import torch
+
+    from drynx_amd.crypto import digest as dg
+
+    ts = [torch.arange(n, dtype=torch.int32) * 7 + n for n in (0, 1, 1023, 1024, 1025, 5000, 3)]
+    ts.append(torch.arange(300, dtype=torch.uint8))
+    got = dg.digest_many(ts)
+    for t, d in zip(ts, got):
+        assert d == dg.digest_bytes(t.numpy().tobytes())
