@@ -1086,12 +1086,14 @@ def _glv_const(kind: str, device) -> torch.Tensor:
     return _glv_consts[key]
 
 
-def glv_weights(n: int, device):
+def glv_weights(n: int, device, raw: torch.Tensor | None = None):
     """n GLV batch weights: (ab [n, 2] int32 = the 32-bit halves (a, b),
-    rho [n, 8] = a + b * GLV_LAMBDA as canonical scalars)."""
+    rho [n, 8] = a + b * GLV_LAMBDA as canonical scalars); ``raw``: [n, 8]
+    uniform scalars to take the halves from (a verifier's own coins)."""
     from ..crypto import bn254 as _bn
 
-    raw = _bn.random_scalars(n, device)
+    if raw is None:
+        raw = _bn.random_scalars(n, device)
     ab = raw[:, :2].contiguous()
     a = torch.zeros_like(raw)
     b = torch.zeros_like(raw)

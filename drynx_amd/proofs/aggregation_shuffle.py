@@ -24,12 +24,17 @@ from ..crypto.elgamal import CipherVector, pk_table
 
 
 # ----------------------------------------------------------------------------- aggregation
+AGG_MAGIC = 0x41475031  # "AGP1"
+_AGG_HEAD = 3           # magic, contributors k, rows n
+
+
 @dataclass
 class AggregationProof:
     inputs: list          # list of CipherVector (one per contributor)
     result: CipherVector  # claimed sum
     stacked: object = None  # decoded proofs: (K, C) [contributors, n, 24] behind ``inputs``
 
+    # reference-style export (kyber affine encodings): ledger / GetProofs
     def to_bytes(self) -> bytes:
         parts = [len(self.inputs).to_bytes(8, "little"), len(self.result).to_bytes(8, "little")]
         if self.inputs and all(len(cv) == len(self.result) for cv in self.inputs):
@@ -56,22 +61,73 @@ class AggregationProof:
         ins = [CipherVector(K[i], C[i]) for i in range(k)]
         return AggregationProof(ins, CipherVector(K[k], C[k]), (K[:k], C[:k]))
 
+    # intra-cluster payload: raw Jacobian limbs of [K inputs..., K result] and
+    # [C inputs..., C result], assembled on the device with no host marshalling
+    def pack(self) -> torch.Tensor:
+        dev = self.result.device
+        k, n = len(self.inputs), len(self.result)
+        if any(len(cv) != n for cv in self.inputs):
+            raise ValueError("aggregation proof inputs differ in length from the result")
+        head = bn.h2d(torch.tensor([AGG_MAGIC, k, n], dtype=torch.int32), dev)
+        Ks = [cv.K.reshape(-1) for cv in self.inputs] + [self.result.K.reshape(-1)]
+        Cs = [cv.C.reshape(-1) for cv in self.inputs] + [self.result.C.reshape(-1)]
+        return torch.cat([head] + Ks + Cs)
+
+    @staticmethod
+    def unpack(t: torch.Tensor, head: list | None = None) -> "AggregationProof":
+        if head is None:
+            head = t[:_AGG_HEAD].cpu().tolist()
+        magic, k, n = head[:3]
+        if magic != AGG_MAGIC or k < 0 or n < 0 or t.numel() != _AGG_HEAD + 2 * (k + 1) * n * 24:
+            raise ValueError("malformed packed aggregation proof")
+        K = t[_AGG_HEAD: _AGG_HEAD + (k + 1) * n * 24].view(k + 1, n, 24)
+        C = t[_AGG_HEAD + (k + 1) * n * 24:].view(k + 1, n, 24)
+        ins = [CipherVector(K[i], C[i]) for i in range(k)]
+        return AggregationProof(ins, CipherVector(K[k], C[k]), (K[:k], C[:k]))
+
+
+def unpack_many(tensors: list) -> list:
+    """Unpack many packed aggregation proofs with ONE header copy (an entry is
+    the proof or the exception that rejects it)."""
+    if not tensors:
+        return []
+    heads = torch.nn.utils.rnn.pad_sequence([t[:_AGG_HEAD] for t in tensors], batch_first=True).cpu().tolist()
+    out = []
+    for t, h in zip(tensors, heads):
+        try:
+            out.append(AggregationProof.unpack(t, h))
+        except Exception as e:  # noqa: BLE001 -- a malformed payload is a rejected proof
+            out.append(e)
+    return out
+
 
 def aggregation_list_proof_creation(inputs: list, result: CipherVector) -> AggregationProof:
     return AggregationProof(list(inputs), result)
 
 
-def aggregation_list_proof_verification(pr: AggregationProof, threshold: float = 1.0) -> bool:
+def aggregation_check(pr: AggregationProof, threshold: float = 1.0) -> torch.Tensor:
+    """Device bool (no host sync): the inputs' canonical, on-curve limbs sum to
+    the claimed result on the first ceil(threshold * n) rows (K5 reduction +
+    projective comparison)."""
     n = len(pr.result)
     k = int(math.ceil(threshold * n))
+    dev = pr.result.device
     if k == 0 or not pr.inputs:
-        return True
-    if pr.stacked is not None and k == n:
-        s = CipherVector(nt.g1_sum(pr.stacked[0]), nt.g1_sum(pr.stacked[1]))
+        return torch.ones((), dtype=torch.bool, device=dev)
+    if pr.stacked is not None:
+        Ks, Cs = pr.stacked[0][:, :k], pr.stacked[1][:, :k]
     else:
-        s = CipherVector.sum([cv[:k] for cv in pr.inputs])
-    r = pr.result[:k]
-    return bool(nt.g1_eq(s.K, r.K).all()) and bool(nt.g1_eq(s.C, r.C).all())
+        Ks = torch.stack([cv.K[:k] for cv in pr.inputs])
+        Cs = torch.stack([cv.C[:k] for cv in pr.inputs])
+    pts = torch.cat([Ks.reshape(-1, 24), Cs.reshape(-1, 24), pr.result.K[:k], pr.result.C[:k]])
+    valid = nt.limbs_canonical(pts.reshape(-1, 8)).bool().all() & nt.g1j_on_curve(pts).bool().all()
+    sK, sC = nt.g1_sum(Ks.contiguous()), nt.g1_sum(Cs.contiguous())
+    eq = nt.g1_eq(torch.cat([sK, sC]), torch.cat([pr.result.K[:k], pr.result.C[:k]]).contiguous())
+    return valid & eq.bool().all()
+
+
+def aggregation_list_proof_verification(pr: AggregationProof, threshold: float = 1.0) -> bool:
+    return bool(aggregation_check(pr, threshold))
 
 
 # ----------------------------------------------------------------------------- shuffle

@@ -653,6 +653,18 @@ def _gt_in_subgroup(g: torch.Tensor) -> bool:
     return bool(nt.gt_eq(nt.gt_pow(g, _SIX_U2[0]), nt.gt_pow(g, _SIX_U2[1])).all())
 
 
+def _gt_in_subgroup_each(g: torch.Tensor) -> list:
+    """``_gt_in_subgroup`` of every row of [k, 96] -> [bool] (one batch)."""
+    global _SIX_U2
+    if _SIX_U2 is None:
+        _SIX_U2 = (bn.scalars_tensor([O.P], "cpu"), bn.scalars_tensor([6 * O.U * O.U], "cpu"))
+    g = g.cpu().contiguous()
+    k = g.shape[0]
+    a = nt.gt_pow(g, _SIX_U2[0].expand(k, 8).contiguous())
+    b = nt.gt_pow(g, _SIX_U2[1].expand(k, 8).contiguous())
+    return [bool(v) for v in nt.gt_eq(a, b).tolist()]
+
+
 def validate_list(r: RangeProofList, mode: int = 0) -> bool:
     """Decoding checks of a (raw-limb or kyber-layout) proof list before any
     arithmetic on it: every coordinate below p and every scalar below r; the
@@ -670,7 +682,7 @@ def validate_list(r: RangeProofList, mode: int = 0) -> bool:
 
 
 def verify_range_proof_list(rpl: RangeProofList, sigmat: SigMaterial, P_point, threshold: float = 1.0,
-                            device=None, mode: int = 0) -> bool:
+                            device=None, mode: int = 0, coins=None) -> bool:
     """RangeProofListVerification: verifies the first ceil(threshold * n)
     proofs of the list (reference sampling semantics) as ONE batch.
     ``mode`` (``SurveyQuery.RangeProofMode``): 0 trusts the proof's challenge
@@ -682,21 +694,24 @@ def verify_range_proof_list(rpl: RangeProofList, sigmat: SigMaterial, P_point, t
     if k == 0:
         return True
     r = rpl if k == len(rpl) else _slice(rpl, k)
-    return verify_range_proof_list_multi(r, sigmat, P_point, 1, device, mode)[0]
+    return verify_range_proof_list_multi(r, sigmat, P_point, 1, device, mode, coins=[coins])[0]
 
 
 def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_point, n_vn: int = 1, device=None,
-                                  mode: int = 0) -> list:
+                                  mode: int = 0, coins: list | None = None) -> list:
     """``n_vn`` independent batch verifications of one proof list -- one per
-    verifying node hosted on this rank, each with its own random weights.
+    verifying node hosted on this rank, each with its own random weights
+    drawn from its own ``coins[v]`` (crypto/coins.py; fresh CSPRNG output
+    when None).
 
     Per VN v the l*S pairing equations of all n proofs are combined with
     uniform 64-bit weights rho_v, and the n D-equations with w_v:
       FE(prod_it ML(rho_it (Zphi_j B - c y_i), V_it)) * prod_it a_it^rho_it
           == gT^(sum rho Zv)                                  (one final exp)
       sum w (c C') + (sum w Zr) P + (sum w z) B == sum w D       (one MSM)
-    plus GT membership of an independent 40-bit combination of the a_it.
-    What does not depend on the weights -- decoding checks, the strict-mode
+    plus GT membership of the a_it: each VN's own independent 40-bit
+    combination gamma_v.  What does not depend on the weights -- decoding
+    checks, the strict-mode
     challenge and G2 checks, Zphi*B, c*y_i and their differences -- is
     computed once for the co-hosted VNs.  On a GPU the VNs' Miller folds are
     queued back to back (no host round trip between them) while the
@@ -733,18 +748,27 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
         Y = nt.g1_fb_mul_idx(ytabs[0], ytabs[1].index_select(0, y_idx).contiguous(), _rep(r.challenge, S))
     else:
         Y = nt.g1_mul(sigmat.y_jac.to(device).index_select(0, y_idx).contiguous(), _rep(r.challenge, S))  # [n*S]
-    # --- per-VN weights: every VN's bucket plans in ONE host sync each
+    # --- per-VN weights (each from its own coins): every VN's bucket plans in ONE host sync each
     G, m = n_vn, n * S * l
-    w_all = _rand64(G * n, device)                                    # D-equation weights
+    cl = list(coins) if coins is not None else [None] * G
+    cl += [None] * (G - len(cl))
+
+    def _cat_draw(fn):
+        return torch.cat([fn(c) for c in cl]) if G > 1 else fn(cl[0])
+
+    w_all = _cat_draw(lambda c: c.bits(n, device, 64) if c is not None else _rand64(n, device))  # D-equation weights
     # pairing-equation weights: rho = a + b lambda (GLV, a and b 32-bit: 2^64
     # distinct residues, so the same 2^-64 soundness as uniform 64-bit weights;
     # csrc/kernels/dx_glv.hip) or, with DRYNX_RHO=64, uniform 64-bit
     glv = os.environ.get("DRYNX_RHO", "glv") == "glv"
     if glv:
-        ab_all, rho_all = nt.glv_weights(G * m, device)
+        pairs = [c.glv(m, device) if c is not None else nt.glv_weights(m, device) for c in cl]
+        ab_all = torch.cat([p_[0] for p_ in pairs]) if G > 1 else pairs[0][0]
+        rho_all = torch.cat([p_[1] for p_ in pairs]) if G > 1 else pairs[0][1]
     else:
-        ab_all, rho_all = None, _rand64(G * m, device)
-    gam_all = _rand64(m, device, 40)                                  # GT-membership combination
+        ab_all, rho_all = None, _cat_draw(lambda c: c.bits(m, device, 64) if c is not None else _rand64(m, device))
+    # GT-membership combinations: one independent 40-bit gamma set PER VN
+    gam_all = _cat_draw(lambda c: c.bits(m, device, 40) if c is not None else _rand64(m, device, 40))
     vid = torch.arange(G, device=device)
     vns = [{"rho": rho_all[v * m:(v + 1) * m], "ab": None if ab_all is None else ab_all[v * m:(v + 1) * m]}
            for v in range(G)]
@@ -781,23 +805,23 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
         wc = nt.fr_arith(nt.FR_MUL, w_all, r.challenge.repeat(G, 1))
         dsc = torch.stack([wc.view(G, n, 8), w_all.view(G, n, 8)], 1).reshape(-1, 8).contiguous()
         dplan = nt.g1_msm_plan(dsc, n, 2 * G)                             # group = row // n
-        # the GT-membership combination is a property of the proof data, not of
-        # a VN's weights: ONE random combination per rank serves every co-hosted VN
+        # groups 0..G-1: prod a^rho_v; groups G..2G-1: each VN's own GT-membership
+        # combination prod a^gamma_v
         if glv:  # prod a^rho = prod a^a' * frob^8(a)^b': 32-bit exponents over (A, frob^8 A)
             A2 = torch.cat([r.A, nt.gt_frob8(r.A)])
-            k = torch.zeros((G + 1, 2 * m, 8), dtype=torch.int32, device=device)
+            k = torch.zeros((2 * G, 2 * m, 8), dtype=torch.int32, device=device)
             abv = ab_all.view(G, m, 2)
             k[:G, :m, 0] = abv[:, :, 0]
             k[:G, m:, 0] = abv[:, :, 1]
-            k[G, :m] = gam_all
-            # GPU: 11-bit windows (3 per 32-bit half, 4 for the 40-bit combination);
+            k[G:, :m] = gam_all.view(G, m, 8)
+            # GPU: 11-bit windows (3 per 32-bit half, 4 for the 40-bit combinations);
             # host: bytes (fewer buckets for the host's serial bucket products)
             wc_ = (4, 11) if device.type == "cuda" else (5, 8)
             k = k.view(-1, 8)
-            mplan = nt.multi_exp_plan(k, 2 * m, G + 1, W=wc_[0], c=wc_[1])          # group = row // 2m
-            mexp = nt.multi_exp_grouped(A2, k, 2 * m, G + 1, W=wc_[0], c=wc_[1], plan=mplan)
+            mplan = nt.multi_exp_plan(k, 2 * m, 2 * G, W=wc_[0], c=wc_[1])          # group = row // 2m
+            mexp = nt.multi_exp_grouped(A2, k, 2 * m, 2 * G, W=wc_[0], c=wc_[1], plan=mplan)
         else:
-            mexp = nt.multi_exp_grouped(r.A, torch.cat([rho_all, gam_all]), m, G + 1)
+            mexp = nt.multi_exp_grouped(r.A, torch.cat([rho_all, gam_all]), m, 2 * G)
         if use_msm and aux is not None:
             S_R = nt.g2_msm_run(r.V, hR)                               # R window sums
         dcheck = nt.g1_msm_launch(dpts, dsc, n, 2 * G, bits=256, plan=dplan)
@@ -807,7 +831,7 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
     if device.type == "cuda":
         with timers.span("rp.verify.multiexp"):
             aux.synchronize()                                          # aux results are read on this stream/host
-            GG = nt.multi_exp_grouped_finish(mexp)                     # [G+1, 96]: prod a^rho_v, prod a^gamma
+            GG = nt.multi_exp_grouped_finish(mexp)                     # [2G, 96]: prod a^rho_v, prod a^gamma_v
             D_all = nt.g1_msm_finish(dcheck)                           # [2G, 24]
             e_all, dfull = e_all.cpu(), dfull.cpu()
         with timers.span("rp.verify.fold_wait"):
@@ -834,11 +858,11 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
     for k, v in enumerate(vns):
         v.update(G=GG[k: k + 1], dfull=dfull[k], e=e_all[k: k + 1], dcheck=D_all[2 * k: 2 * k + 2])
     out = []
-    # prime-order part of the a_ij: the independent 40-bit combination in GT
-    # (the smallest prime factor of the cyclotomic cofactor is ~2^38.8: a
-    # non-GT component survives the batch equation AND this test with
-    # probability ~2^-77)
-    m_ok = _gt_in_subgroup(GG[G: G + 1])
+    # prime-order part of the a_ij: each VN's own independent 40-bit
+    # combination in GT (the smallest prime factor of the cyclotomic cofactor
+    # is ~2^38.8: a non-GT component survives the batch equation AND this test
+    # with probability ~2^-77)
+    m_oks = _gt_in_subgroup_each(GG[G: 2 * G])
     _, gt_tab = gt_generator_table("cpu")
     PB_base = bn.g1_jac_tensor([P_point, O.G1_GEN], "cpu")
     for v in vns:
@@ -848,7 +872,7 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
             d_ok = bool(nt.g1_eq(nt.g1_sum(torch.stack([G0[0:1], PB[0:1], PB[1:2]])), G0[1:2])[0])
             lhs = nt.gt_mul(nt.final_exp(v["F"].cpu()), v["G"].cpu())
             eq_ok = bool(nt.gt_eq(lhs, nt.gt_fb_pow(gt_tab, v["e"].cpu())).all())
-        out.append(d_ok and m_ok and eq_ok)
+        out.append(d_ok and m_oks[len(out)] and eq_ok)
     return out
 
 

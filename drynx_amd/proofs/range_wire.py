@@ -98,6 +98,17 @@ def _proof_messages(r: rp.RangeProofList, f: dict) -> torch.Tensor:
     return torch.cat([B(_hdr(1, body.shape[1])), body], dim=1)
 
 
+def is_raw_bundle(b: bytes) -> bool:
+    """A raw-limb range bundle (``requests.range_bundle_pack``: [count, sizes...,
+    'RPR1' list...]) rather than reference-layout bytes."""
+    if len(b) < 12 or len(b) % 4:
+        return False
+    k = int.from_bytes(b[:4], "little")
+    if k < 1 or 4 * (2 + k) > len(b):
+        return False
+    return int.from_bytes(b[4 * (1 + k): 4 * (2 + k)], "little") == 0x52505231
+
+
 def encode_bundle(rpls: list, fields: list | None = None) -> bytes:
     """network.Marshal(&RangeProofListBytes) of all proofs of a DP's bundle,
     in output-column order.  Assembled on the proofs' device; one copy of the

@@ -47,12 +47,12 @@ class ProofRequest:
     something needs them (ledger persistence, control-plane transport)."""
 
     __slots__ = ("kind", "survey_id", "sender_id", "differ_info", "_data", "signature", "obj", "data_digest",
-                 "tensor", "decoded", "sig_ok")
+                 "tensor", "decoded", "slice_of")
 
     def __init__(self, kind: str, survey_id: str, sender_id: str, differ_info: str, data: bytes | None,
                  signature: bytes, obj: Any = None, data_digest: bytes = b"", tensor: torch.Tensor | None = None):
         self.kind, self.survey_id, self.sender_id, self.differ_info = kind, survey_id, sender_id, differ_info
-        self.sig_ok = None  # ((public, digest, signature), verdict): shared by the VNs of this rank
+        self.slice_of = None  # pooled helper copy: (lo, hi) bounds per list of the signed bundle (fan_out)
         self._data = data
         self.signature = signature
         self.obj = obj  # decoded proof (in-process fast path)
@@ -259,20 +259,47 @@ def range_bundle_export_kyber(rpls) -> bytes:
     return b"".join(out)
 
 
+PACKED_KINDS = ("aggregation", "keyswitch", "obfuscation")
+
+
 def new_proof_request(kind: str, proof, survey_id: str, sender_id: str, differ_info: str, secret: int) -> ProofRequest:
-    """New{Range,Aggregation,Obfuscation,Shuffle,KeySwitch}ProofRequest: marshal + Schnorr-sign.
-    Range bundles stay a device tensor; their digest is hashed on the device."""
-    with timers.span(f"sign.marshal.{kind}"):
-        if kind == "range":
-            req = ProofRequest(kind, survey_id, sender_id, differ_info, None, b"", obj=proof,
-                               tensor=range_bundle_pack(proof))
-        else:
-            req = ProofRequest(kind, survey_id, sender_id, differ_info, proof.to_bytes(), b"", obj=proof)
-    with timers.span(f"sign.digest.{kind}"):
-        dg = req.digest()
-    with timers.span(f"sign.schnorr.{kind}"):
-        req.signature = sigma.schnorr_sign(secret, dg)
-    return req
+    """New{Range,Aggregation,Obfuscation,Shuffle,KeySwitch}ProofRequest: marshal + Schnorr-sign."""
+    return new_proof_requests([(kind, proof, sender_id, differ_info, secret)], survey_id)[0]
+
+
+def new_proof_requests(items: list, survey_id: str) -> list:
+    """Many envelopes at once (``items`` = [(kind, proof, sender_id,
+    differ_info, secret)]).  Range bundles and the per-CN proofs
+    (aggregation, key switch, obfuscation) are raw limb tensors assembled
+    where the proof lives (no host marshalling); their digests are ONE
+    segmented device launch and one copy to the host; the Schnorr signatures
+    are one batch.  Shuffle proofs stay bytes (reference-style export)."""
+    if not items:
+        return []
+    reqs = []
+    with timers.span("sign.marshal"):
+        for kind, proof, sender_id, differ_info, _ in items:
+            if kind == "range":
+                reqs.append(ProofRequest(kind, survey_id, sender_id, differ_info, None, b"", obj=proof,
+                                         tensor=range_bundle_pack(proof)))
+            elif kind in PACKED_KINDS:
+                reqs.append(ProofRequest(kind, survey_id, sender_id, differ_info, None, b"", obj=proof,
+                                         tensor=proof.pack()))
+            else:
+                reqs.append(ProofRequest(kind, survey_id, sender_id, differ_info, proof.to_bytes(), b"", obj=proof))
+    with timers.span("sign.digest"):
+        tens = [i for i, r in enumerate(reqs) if r.tensor is not None]
+        devs = {reqs[i].tensor.device for i in tens}
+        if len(devs) == 1 and len(tens) > 1:
+            for i, d in zip(tens, payload_digest.digest_many([reqs[i].tensor for i in tens])):
+                reqs[i].data_digest = d
+        dgs = [r.digest() for r in reqs]
+    with timers.span("sign.schnorr"):
+        dev = next(iter(devs)) if devs else "cpu"
+        sigs = sigma.schnorr_sign_batch([it[4] for it in items], dgs, dev)
+    for r, sig in zip(reqs, sigs):
+        r.signature = sig
+    return reqs
 
 
 def verify_signature(req: ProofRequest, public) -> bool:
@@ -312,17 +339,19 @@ def _dp_order(sq) -> dict:
     return cache
 
 
-def prewarm_keyswitch(reqs: list, sq, vn_ids: list, device, cache: VerifierCache):
+def prewarm_keyswitch(reqs: list, sq, vn_ids: list, device, cache: "VerifierCache", coins: dict | None = None):
     """Key-switch proofs of an inbox verified for SEVERAL co-hosted VNs at once
-    (``sigma.key_switch_batch_verification_multi``: one grouped MSM, each VN
-    with its own random weights) when every VN verifies every request
-    (Threshold 1, no sharding); ``verify_requests`` then reads its VN's
-    verdicts from ``cache.ks_pre``."""
+    when every VN verifies every request (Threshold 1, no sharding): one
+    grouped MSM in which every VN's random combination uses that VN's own
+    coins, and every VN's own Fiat-Shamir / T3 checks
+    (``sigma.key_switch_batch_verification_multi``); ``verify_requests``
+    then reads its VN's verdicts from ``cache.ks_pre``."""
     if len(vn_ids) < 2 or sq.Threshold < 1.0 or getattr(sq, "VerificationSharding", 0):
         return
     ks = [i for i, r in enumerate(reqs) if r.kind == "keyswitch" and not r.header_only]
     if len(ks) < 2:
         return
+    _prefetch_packed(reqs, ks, device)
     objs, valid, verdict = [], [], {}
     for i in ks:
         try:
@@ -336,8 +365,9 @@ def prewarm_keyswitch(reqs: list, sq, vn_ids: list, device, cache: VerifierCache
             continue
         objs.append(o)
         valid.append(i)
-    for vn_id, res in zip(vn_ids, sigma.key_switch_batch_verification_multi(objs, sq.KeySwitchingProofThreshold,
-                                                                             len(vn_ids))):
+    coins = coins or {}
+    for vn_id, res in zip(vn_ids, sigma.key_switch_batch_verification_multi(
+            objs, sq.KeySwitchingProofThreshold, [coins.get(v) for v in vn_ids])):
         m = dict(verdict)
         m.update(zip(valid, res))
         cache.ks_pre[(sq.SurveyID, vn_id)] = m
@@ -345,11 +375,13 @@ def prewarm_keyswitch(reqs: list, sq, vn_ids: list, device, cache: VerifierCache
         cache.ks_pre.pop(next(iter(cache.ks_pre)))
 
 
-def should_verify(sq, req: ProofRequest, vn_index: int, n_vns: int) -> bool:
+def should_verify(sq, req: ProofRequest, vn_index: int, n_vns: int, coins=None) -> bool:
+    """The VN's sampling decision: ``rand.Float64() <= Threshold`` from the
+    VN's own coins (structs_proofs.go:160-161), or the sharding extension."""
     a = assigned_vns(sq, req, n_vns)
     if a is not None:
         return vn_index in a
-    return random.random() <= sq.Threshold
+    return (coins.random() if coins is not None else random.random()) <= sq.Threshold
 
 
 class VerifierCache:
@@ -461,54 +493,67 @@ def _range_lists(req: ProofRequest, device) -> list:
     return req.decoded
 
 
-def verify_range_many(reqs: list, idxs: list, sq, device, cache: VerifierCache, part=None) -> dict:
+def verify_range_many(reqs: list, idxs: list, sq, device, cache: VerifierCache, part=None, coins=None) -> dict:
     """Range-proof requests of one VN as ONE batched verification (see
     ``verify_range_many_multi``).  -> {request index: bool}"""
-    return verify_range_many_multi(reqs, {"vn": idxs}, sq, device, cache, part)["vn"]
+    return verify_range_many_multi(reqs, {"vn": idxs}, sq, device, cache, part, {"vn": coins})["vn"]
 
 
-def verify_range_many_multi(reqs: list, vn_idxs: dict, sq, device, cache: VerifierCache, part=None) -> dict:
+def verify_range_many_multi(reqs: list, vn_idxs: dict, sq, device, cache: VerifierCache, part=None,
+                            coins: dict | None = None) -> dict:
     """Range-proof requests of several VNs hosted on this rank: the sampled
     prefix of every list (reference RangeProofThreshold semantics) of every
     request, grouped by (u, l), folded into one pairing batch per VN with that
-    VN's own random weights; VNs that sample the same requests share the
-    decode and the weight-free work (``rp.verify_range_proof_list_multi``).
-    If a VN's batch fails, each request is re-checked alone for that VN so the
-    bitmap blames exactly the bad ones.  ``part = (k, W)`` checks only the
-    k-th of W equal slices of every sampled prefix (the pooled verification of
-    a multi-GPU node).  vn_idxs: {vn: [request index]} -> {vn: {index: bool}}"""
+    VN's own random weights (``coins[vn]``); VNs that sample the same requests
+    share the decode and the weight-free work (``rp.verify_range_proof_list_multi``).
+    If a VN's batch fails, the failing requests are located by bisection over
+    that VN's own re-checks (``_blame``) so the bitmap blames exactly the bad
+    ones.  ``part = (k, W)`` checks only the k-th of W equal slices of every
+    sampled prefix (the pooled verification of a multi-GPU node); a helper
+    copy that already holds only its slice (``slice_of``) is checked whole.
+    vn_idxs: {vn: [request index]} -> {vn: {index: bool}}"""
+    coins = coins or {}
     by_set: dict = {}
     for vn, idxs in vn_idxs.items():
         by_set.setdefault(tuple(sorted(idxs)), []).append(vn)
     out = {}
     for idxs, group in by_set.items():
-        res = _verify_range_group(reqs, list(idxs), sq, device, cache, part, len(group))
+        res = _verify_range_group(reqs, list(idxs), sq, device, cache, part, [coins.get(vn) for vn in group])
         for vn, rv in zip(group, res):
             out[vn] = rv
     return out
 
 
-def _verify_range_group(reqs, idxs, sq, device, cache, part, n_vn) -> list:
-    P = sq.RosterServers.aggregate()
+def sampled_bounds(sq, n: int, part=None) -> tuple:
+    """[lo, hi) of a list of n proofs that a verifier checks: the sampled
+    prefix ceil(RangeProofThreshold * n) (range_proof.go:486), or its k-th of
+    W equal slices for ``part = (k, W)``."""
+    k = int(math.ceil(sq.RangeProofThreshold * n))
+    if part is None:
+        return 0, k
+    return (k * part[0]) // part[1], (k * (part[0] + 1)) // part[1]
+
+
+def _range_parts(reqs, idxs, sq, device, part):
+    """Decode + query-consistency checks of every request's lists, cut to the
+    part this rank checks -> (base verdicts {i: bool}, parts {i: [lists]})."""
     sigs = sq.Query.IVSigs.InputValidationSigs
-    mode = int(getattr(sq, "RangeProofMode", 0) or 0)
     base, parts = {}, {}
     with timers.span("rp.verify.unpack_many"):
         _prefetch_range_lists(reqs, idxs, device)
     for i in idxs:
         try:
             lists = []
-            with timers.span("rp.verify.unpack"):
-                unpacked = _range_lists(reqs[i], device)
+            unpacked = _range_lists(reqs[i], device)
             for r in unpacked:
                 if not r.has_rp:
                     continue
                 if sigs is None or not _ranges_ok(sq, r):
                     raise ValueError("ranges / signatures do not match the query")
-                k = int(math.ceil(sq.RangeProofThreshold * len(r)))
-                lo, hi = 0, k
-                if part is not None:
-                    lo, hi = (k * part[0]) // part[1], (k * (part[0] + 1)) // part[1]
+                if reqs[i].slice_of is not None:
+                    lo, hi = 0, len(r)  # a helper's copy: already this rank's slice
+                else:
+                    lo, hi = sampled_bounds(sq, len(r), part)
                 if hi > lo:
                     lists.append(r if (lo, hi) == (0, len(r)) else rp.rpl_range(r, lo, hi))
             parts[i] = lists
@@ -516,11 +561,120 @@ def _verify_range_group(reqs, idxs, sq, device, cache, part, n_vn) -> list:
         except Exception as e:
             log.warning(f"range proof from {reqs[i].sender_id} rejected: {e}")
             base[i] = False
+    return base, parts
+
+
+_RPL_FIELDS = ("challenge", "zr", "D", "zphi", "zv", "V", "A")
+
+
+def lists_digests(entries: list) -> list:
+    """Digest of each entry (a list of RangeProofLists, e.g. one request's
+    slice for one pooled part) over its header values and the raw limbs of
+    every field, computed from VIEWS of the lists (no packing copy): every
+    field region of every entry in ONE segmented SHA-256 launch, one copy to
+    the host.  A helper rank reports the digest of the slice it verified; the
+    VN recomputes it from its own signed payload, so a helper's verdict only
+    counts for exactly the bytes the VN received."""
+    tens, spans, metas = [], [], []
+    for lists in entries:
+        a = len(tens)
+        meta = []
+        for r in lists:
+            meta += [len(r), r.u, r.l, r.S] + [int(o) for o in r.offset] + [int(c) for c in r.cols]
+            tens += [r.commit.K, r.commit.C]
+            if r.has_rp and len(r):
+                tens += [getattr(r, f) for f in _RPL_FIELDS]
+        spans.append((a, len(tens)))
+        metas.append(np.asarray(meta, dtype="<i8").tobytes())
+    if tens:
+        devs = {t.device for t in tens}
+        if len(devs) == 1:
+            parts = payload_digest.digest_many([t.contiguous() for t in tens])
+        else:
+            parts = [payload_digest.digest_tensor(t) for t in tens]
+    else:
+        parts = []
+    out = []
+    for (a, b), meta in zip(spans, metas):
+        h = hashlib.sha256(b"drynx_amd/range-slice" + meta)
+        for d in parts[a:b]:
+            h.update(d)
+        out.append(h.digest())
+    return out
+
+
+def slice_lists(lists: list, sq, part) -> list:
+    """The lists of one bundle cut to what rank ``part[0]`` of ``part[1]``
+    checks (empty slices dropped)."""
+    out = []
+    for r in lists:
+        if not r.has_rp:
+            continue
+        lo, hi = sampled_bounds(sq, len(r), part)
+        if hi > lo:
+            out.append(r if (lo, hi) == (0, len(r)) else rp.rpl_range(r, lo, hi))
+    return out
+
+
+def _verify_range_group(reqs, idxs, sq, device, cache, part, coins_list: list) -> list:
+    P = sq.RosterServers.aggregate()
+    mode = int(getattr(sq, "RangeProofMode", 0) or 0)
+    n_vn = len(coins_list)
+    base, parts = _range_parts(reqs, idxs, sq, device, part)
     outs = [dict(base) for _ in range(n_vn)]
     live = [i for i in idxs if base[i] and parts[i]]
     if not live:
         return outs
     sigmat = cache.sigmat(sq, device)
+    oks = _check_lists(live, parts, sigmat, P, device, mode, coins_list)
+    for k in range(n_vn):
+        if oks[k] or len(live) == 1:
+            for i in live:
+                outs[k][i] = oks[k]
+            continue
+        with timers.span("rp.verify.blame"):
+            bad = _blame(live, parts, sigmat, P, device, mode, coins_list[k])
+        for i in live:
+            outs[k][i] = i not in bad
+    return outs
+
+
+def verify_range_pool_part(reqs: list, vn_idxs: dict, sq, device, cache: VerifierCache, part, coins: dict):
+    """One rank's share of a pooled range verification: part ``part`` of the
+    sampled prefix of every request, checked for every VN with that VN's
+    coins for this part.  -> ({vn: {index: bool}}, {index: slice digest})"""
+    union = sorted({i for idxs in vn_idxs.values() for i in idxs})
+    base, parts = _range_parts(reqs, union, sq, device, part)
+    with timers.span("rp.verify.slice_digests"):
+        ok_idx = [i for i in union if base[i]]
+        digests = dict(zip(ok_idx, lists_digests([parts[i] for i in ok_idx])))
+    P = sq.RosterServers.aggregate()
+    mode = int(getattr(sq, "RangeProofMode", 0) or 0)
+    by_set: dict = {}
+    for vn, idxs in vn_idxs.items():
+        by_set.setdefault(tuple(sorted(idxs)), []).append(vn)
+    out = {}
+    for idxs, group in by_set.items():
+        live = [i for i in idxs if base[i] and parts[i]]
+        res = [{i: base[i] for i in idxs} for _ in group]
+        if live:
+            sigmat = cache.sigmat(sq, device)
+            cl = [coins.get(vn) for vn in group]
+            oks = _check_lists(live, parts, sigmat, P, device, mode, cl)
+            for k, vn in enumerate(group):
+                bad = set() if oks[k] else (_blame(live, parts, sigmat, P, device, mode, cl[k])
+                                            if len(live) > 1 else set(live))
+                for i in live:
+                    res[k][i] = i not in bad
+        for vn, rv in zip(group, res):
+            out[vn] = rv
+    return out, digests
+
+
+def _check_lists(live, parts, sigmat, P, device, mode, coins_list) -> list:
+    """One batch per (u, l, S) group over the requests ``live``, every VN's
+    verdict from its own weights -> [bool] per VN."""
+    n_vn = len(coins_list)
     groups: dict = {}
     for i in live:
         for r in parts[i]:
@@ -530,22 +684,33 @@ def _verify_range_group(reqs, idxs, sq, device, cache, part, n_vn) -> list:
         with timers.span("rp.verify.cat"):
             cats = [rp.rpl_cat(g) for g in groups.values()]
         for c in cats:
-            for k, ok in enumerate(rp.verify_range_proof_list_multi(c, sigmat, P, n_vn, device, mode)):
+            for k, ok in enumerate(rp.verify_range_proof_list_multi(c, sigmat, P, n_vn, device, mode,
+                                                                    coins=coins_list)):
                 oks[k] = oks[k] and ok
     except Exception as e:
         log.warning(f"batched range verification failed: {e}")
         oks = [False] * n_vn
-    for k in range(n_vn):
-        if oks[k] or len(live) == 1:
-            for i in live:
-                outs[k][i] = oks[k]
+    return oks
+
+
+def _blame(live, parts, sigmat, P, device, mode, coins) -> set:
+    """The requests of a failed batch that fail on their own, found by
+    bisection: a half that passes as one batch is cleared at once, so k bad
+    requests among m cost O(k log m) batches instead of m re-checks (each
+    batch drawn afresh from the VN's own coins)."""
+    bad: set = set()
+    stack = [list(live)]
+    while stack:
+        grp = stack.pop()
+        if len(grp) == 1:
+            if not _check_lists(grp, parts, sigmat, P, device, mode, [coins])[0]:
+                bad.add(grp[0])
             continue
-        for i in live:  # attribute the failure (this VN's own re-check, request by request)
-            try:
-                outs[k][i] = all(rp.verify_range_proof_list(r, sigmat, P, 1.0, device, mode) for r in parts[i])
-            except Exception:
-                outs[k][i] = False
-    return outs
+        if _check_lists(grp, parts, sigmat, P, device, mode, [coins])[0]:
+            continue
+        h = len(grp) // 2
+        stack += [grp[h:], grp[:h]]
+    return bad
 
 
 _DECODERS = {"keyswitch": lambda b, d: sigma.KeySwitchProof.from_bytes(b, d),
@@ -555,51 +720,105 @@ _DECODERS = {"keyswitch": lambda b, d: sigma.KeySwitchProof.from_bytes(b, d),
 
 
 def _decode(req: ProofRequest, device):
-    """Unmarshal the signed bytes (cached per request across the VNs of a rank)."""
+    """Unmarshal the SIGNED payload (packed tensor or bytes), never the
+    prover's in-memory object; cached per request across the VNs of a rank
+    (decoded data, not a verdict)."""
     if req.decoded is None:
-        req.decoded = _DECODERS[req.kind](req.data, device)
+        t = None
+        if req.kind in PACKED_KINDS:
+            if req.tensor is not None and req._data is None:
+                t = req.tensor.to(device)
+            elif _is_packed(req.kind, req.data):  # a packed payload that travelled as bytes
+                t = torch.from_numpy(np.frombuffer(req.data, dtype=np.int32).copy()).to(device)
+        if t is not None:
+            req.decoded = (ags.AggregationProof.unpack(t) if req.kind == "aggregation"
+                           else sigma.unpack_many(req.kind, [t])[0])
+        else:
+            req.decoded = _DECODERS[req.kind](req.data, device)
+    if isinstance(req.decoded, Exception):
+        raise req.decoded
     return req.decoded
 
 
-_SIG_BATCH_MIN = 16  # inboxes at least this long check their envelope signatures in one batch
+_PACKED_MAGIC = {"aggregation": ags.AGG_MAGIC, "keyswitch": sigma.KS_MAGIC, "obfuscation": sigma.OBF_MAGIC}
+
+
+def _is_packed(kind: str, b: bytes) -> bool:
+    return len(b) >= 4 and len(b) % 4 == 0 and int.from_bytes(b[:4], "little") == _PACKED_MAGIC[kind]
+
+
+def export_reference_bytes(kind: str, value: bytes) -> bytes:
+    """A stored payload in the reference-style byte layout (GetProofs): packed
+    raw-limb payloads are decoded and re-encoded; anything else is served as
+    stored.  A packed payload that does not decode raises."""
+    if kind == "range":
+        from . import range_wire
+
+        if value and range_wire.is_raw_bundle(value):
+            return range_wire.encode_bundle(range_bundle_from_bytes(value, "cpu"))
+        return value
+    if kind in PACKED_KINDS and _is_packed(kind, value):
+        t = torch.from_numpy(np.frombuffer(value, dtype=np.int32).copy())
+        pr = ags.AggregationProof.unpack(t) if kind == "aggregation" else sigma.unpack_many(kind, [t])[0]
+        if isinstance(pr, Exception):
+            raise pr
+        return pr.to_bytes()
+    return value
+
+
+def _prefetch_packed(reqs: list, idxs: list, device):
+    """Decode the packed per-CN proofs of an inbox with one header copy per kind."""
+    by_kind: dict = {}
+    for i in idxs:
+        r = reqs[i]
+        if r.decoded is None and r.kind in PACKED_KINDS and r.tensor is not None and r._data is None:
+            by_kind.setdefault(r.kind, []).append(i)
+    for kind, ii in by_kind.items():
+        ts = [reqs[i].tensor.to(device) for i in ii]
+        dec = ags.unpack_many(ts) if kind == "aggregation" else sigma.unpack_many(kind, ts)
+        for i, d in zip(ii, dec):
+            reqs[i].decoded = d
+
+
+def prefetch_digests(reqs: list):
+    """Envelope digests (decoded data: a function of the signed payload) of
+    every tensor payload of an inbox in ONE segmented launch per device."""
+    todo = [r for r in reqs if not r.data_digest and r.tensor is not None and r._data is None]
+    by_dev: dict = {}
+    for r in todo:
+        by_dev.setdefault(r.tensor.device, []).append(r)
+    for rs in by_dev.values():
+        for r, d in zip(rs, payload_digest.digest_many([r.tensor for r in rs])):
+            r.data_digest = d
 
 
 def verify_requests(reqs: list, sq, vn_id: str, vn_index: int, n_vns: int, device, cache: VerifierCache,
-                    range_pooled=None, defer: bool = False):
-    """VerifyProof for a VN's whole inbox.  Signatures and sampling per request;
-    the content of the short per-CN proofs (key switch, obfuscation) is verified
-    in one batched launch per kind; range proofs are already one batch each.
+                    range_pooled=None, defer: bool = False, coins=None):
+    """VerifyProof for a VN's whole inbox, with the VN's own verdicts: its
+    Schnorr checks of every envelope (one batch), its sampling decisions and
+    random weights (``coins``, crypto/coins.py), its Fiat-Shamir checks.
+    Only decoded data is shared with co-hosted VNs (envelope digests,
+    unpacked proofs, transcript digests).  The per-CN proofs are verified in
+    one batched launch sequence per kind (aggregation sums as device booleans
+    read back together); range proofs are one batch each.
     ``range_pooled``: {base_key: None (not sampled) | bool} -- this VN's range
-    results from the pooled verification (``pool_sampling`` decided the
-    sampling on this VN's rank beforehand; a dict or a Future of one).
+    results from the pooled verification (a dict or a Future of one).
     ``defer``: return a callable that waits for the pooled range results and
     returns the codes (everything else is already checked)."""
     codes = [None] * len(reqs)
     todo: dict = {}
     pooled_idx: list = []
-    if len(reqs) >= _SIG_BATCH_MIN:
-        # each envelope's Schnorr check is a deterministic function of the signed
-        # bytes and the roster key: done once per rank, read by every co-hosted VN
-        keys = [(sq.IDtoPublic.get(r.sender_id), r.digest(), r.signature) for r in reqs]
-        fresh = [i for i, r in enumerate(reqs) if r.sig_ok is None or r.sig_ok[0] != keys[i]]
-        if fresh:
-            with timers.span("verify.signature.batch"):
-                for i, v in zip(fresh, sigma.schnorr_verify_batch([keys[i] for i in fresh], device)):
-                    reqs[i].sig_ok = (keys[i], v)
-        sigs_ok = [r.sig_ok[1] for r in reqs]
-    else:
-        sigs_ok = None
+    with timers.span("verify.digests"):
+        prefetch_digests(reqs)
+    keys = [(sq.IDtoPublic.get(r.sender_id), r.digest(), r.signature) for r in reqs]
+    with timers.span("verify.signature.batch"):
+        sigs_ok = sigma.schnorr_verify_batch(keys, device) if reqs else []
     for i, req in enumerate(reqs):
-        if sigs_ok is not None:
-            sig_ok = sigs_ok[i]
-        else:
-            with timers.span(f"verify.signature.{req.kind}"):
-                sig_ok = verify_signature(req, sq.IDtoPublic.get(req.sender_id))
-        if not sig_ok:
+        if not sigs_ok[i]:
             codes[i] = PROOF_FALSE_SIGN
         elif range_pooled is not None and req.kind == "range" and not req.header_only:
             pooled_idx.append(i)  # resolved below: the pooled batch may still be running
-        elif not should_verify(sq, req, vn_index, n_vns):
+        elif not should_verify(sq, req, vn_index, n_vns, coins):
             codes[i] = PROOF_RECEIVED
         else:
             todo.setdefault(req.kind, []).append(i)
@@ -618,18 +837,28 @@ def verify_requests(reqs: list, sq, vn_id: str, vn_index: int, n_vns: int, devic
         # their own HIP stream while this thread checks the short per-CN proofs
         idxs = todo.pop("range")
         range_future = _side_pool().submit(_verify_range_side, reqs, idxs, sq, vn_id, device, cache,
-                                           torch.cuda.current_stream(torch.device(device)))
+                                           torch.cuda.current_stream(torch.device(device)), coins)
+    _prefetch_packed(reqs, [i for k in PACKED_KINDS for i in todo.get(k, [])], device)
     pre = cache.ks_pre.pop((sq.SurveyID, vn_id), None)
     if pre is not None and "keyswitch" in todo and all(i in pre for i in todo["keyswitch"]):
         with timers.timed(f"{vn_id}_{TIMER['keyswitch']}"):
             for i in todo.pop("keyswitch"):
                 codes[i] = PROOF_TRUE if pre[i] else PROOF_FALSE
+    dev_flags = []  # (request index, device bool): read back with ONE copy
     for kind, idxs in todo.items():
         with timers.timed(f"{vn_id}_{TIMER[kind]}"):
             if kind == "range":
-                for i, ok in verify_range_many(reqs, idxs, sq, device, cache).items():
+                for i, ok in verify_range_many(reqs, idxs, sq, device, cache, coins=coins).items():
                     codes[i] = PROOF_TRUE if ok else PROOF_FALSE
-            elif kind in ("keyswitch", "obfuscation") and len(idxs) > 1:
+            elif kind == "aggregation":
+                for i in idxs:
+                    try:
+                        dev_flags.append((i, ags.aggregation_check(_decode(reqs[i], device),
+                                                                   sq.AggregationProofThreshold)))
+                    except Exception as e:
+                        log.warning(f"{vn_id}: aggregation proof from {reqs[i].sender_id} rejected: {e}")
+                        codes[i] = PROOF_FALSE
+            elif kind in ("keyswitch", "obfuscation"):
                 objs, valid = [], []
                 for i in idxs:
                     try:
@@ -644,9 +873,9 @@ def verify_requests(reqs: list, sq, vn_id: str, vn_index: int, n_vns: int, devic
                         log.warning(f"{vn_id}: {kind} proof from {reqs[i].sender_id} rejected: {e}")
                         codes[i] = PROOF_FALSE
                 if kind == "keyswitch":
-                    res = sigma.key_switch_batch_verification(objs, sq.KeySwitchingProofThreshold)
+                    res = sigma.key_switch_batch_verification(objs, sq.KeySwitchingProofThreshold, coins=coins)
                 else:
-                    res = sigma.obfuscation_batch_verification(objs, sq.ObfuscationProofThreshold)
+                    res = sigma.obfuscation_batch_verification(objs, sq.ObfuscationProofThreshold, coins=coins)
                 for i, r in zip(valid, res):
                     codes[i] = PROOF_TRUE if r else PROOF_FALSE
             else:
@@ -657,6 +886,11 @@ def verify_requests(reqs: list, sq, vn_id: str, vn_index: int, n_vns: int, devic
                         log.warning(f"{vn_id}: {kind} proof from {reqs[i].sender_id} rejected: {e}")
                         ok = False
                     codes[i] = PROOF_TRUE if ok else PROOF_FALSE
+    if dev_flags:
+        with timers.span("verify.flags"):
+            flags = torch.stack([f.reshape(()) for _, f in dev_flags]).cpu().tolist()
+        for (i, _), ok in zip(dev_flags, flags):
+            codes[i] = PROOF_TRUE if ok else PROOF_FALSE
     if range_future is not None:
         for i, code in range_future.result():
             codes[i] = code
@@ -664,6 +898,7 @@ def verify_requests(reqs: list, sq, vn_id: str, vn_index: int, n_vns: int, devic
         with timers.span("rp.verify.early_wait"):
             for i, (fut, j) in early.items():
                 codes[i] = PROOF_TRUE if fut.result()[j] else PROOF_FALSE
+
     def resolve():
         if pooled_idx:
             with timers.span("rp.verify.pooled_wait"):
@@ -729,7 +964,7 @@ def _side_pool():
     return _pool
 
 
-def _verify_range_side(reqs, idxs, sq, vn_id, device, cache, main) -> list:
+def _verify_range_side(reqs, idxs, sq, vn_id, device, cache, main, coins=None) -> list:
     dev = torch.device(device)
     side = _streams.get(str(dev))
     if side is None:
@@ -737,18 +972,19 @@ def _verify_range_side(reqs, idxs, sq, vn_id, device, cache, main) -> list:
     side.wait_stream(main)  # payloads / decoded lists are ready
     out = []
     with torch.cuda.stream(side), timers.timed(f"{vn_id}_{TIMER['range']}"):
-        for i, ok in verify_range_many(reqs, idxs, sq, device, cache).items():
+        for i, ok in verify_range_many(reqs, idxs, sq, device, cache, coins=coins).items():
             out.append((i, PROOF_TRUE if ok else PROOF_FALSE))
     side.synchronize()
     return out
 
 
-def verify_proof(req: ProofRequest, sq, vn_id: str, vn_index: int, n_vns: int, device, cache: VerifierCache) -> int:
+def verify_proof(req: ProofRequest, sq, vn_id: str, vn_index: int, n_vns: int, device, cache: VerifierCache,
+                 coins=None) -> int:
     """<Kind>ProofRequest.VerifyProof -> bitmap code."""
     with timers.timed(f"{vn_id}_{TIMER[req.kind]}"):
         if not verify_signature(req, sq.IDtoPublic.get(req.sender_id)):
             return PROOF_FALSE_SIGN
-        if not should_verify(sq, req, vn_index, n_vns):
+        if not should_verify(sq, req, vn_index, n_vns, coins):
             return PROOF_RECEIVED
         try:
             ok = verify_content(req, sq, device, cache)

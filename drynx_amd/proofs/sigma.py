@@ -38,50 +38,103 @@ def _aff_bytes(jac: torch.Tensor) -> bytes:
     return bn.g1_aff_to_bytes(nt.g1_to_affine(jac.contiguous().view(-1, 24))).tobytes()
 
 
+def pts_be(jac: torch.Tensor) -> torch.Tensor:
+    """[m, 24] Jacobian -> [m, 64] uint8 kyber encodings (affine x || y, big
+    endian, infinity = zeros) computed where the points live (HBM on a GPU)."""
+    aff = nt.g1_to_affine(jac.contiguous().view(-1, 24))
+    xy = nt.fp_from_mont(aff.reshape(-1, 8))
+    return xy.view(torch.uint8).view(-1, 32).flip(1).reshape(-1, 64)
+
+
+def points_digests(groups: list) -> list:
+    """Per group (a list of Jacobian point tensors / CipherVectors) the chunked
+    digest (crypto/digest.py) of the kyber encodings of all its points, in
+    order: ONE normalisation launch, one encoding pass, one segmented SHA-256
+    launch and ONE device-to-host copy for every group together (a
+    transcript is 3-6 vectors of thousands of points)."""
+    from ..crypto import digest as dg
+
+    flat, sizes = [], []
+    for grp in groups:
+        m = 0
+        for p in grp:
+            ts = (p.K, p.C) if isinstance(p, CipherVector) else (p,)
+            for t in ts:
+                t = t.contiguous().view(-1, 24)
+                flat.append(t)
+                m += t.shape[0]
+        sizes.append(m)
+    if not flat:
+        return [dg.digest_bytes(b"") for _ in groups]
+    be = pts_be(torch.cat(flat) if len(flat) > 1 else flat[0])
+    views, o = [], 0
+    for m in sizes:
+        views.append(be[o: o + m])
+        o += m
+    return dg.digest_many(views)
+
+
+def fs_hash(context: str, raw: tuple, pts_digest: bytes) -> int:
+    """Fiat-Shamir challenge: SHA-256(context || raw parts || digest of the
+    point encodings) mod r."""
+    h = hashlib.sha256(context.encode())
+    for r in raw:
+        h.update(r)
+    h.update(pts_digest)
+    return int.from_bytes(h.digest(), "big") % O.R
+
+
 def fs_challenge(context: str, *parts) -> int:
-    """SHA-256 Fiat–Shamir challenge over the context and the affine encodings
-    of every point: all point tensors are normalised in ONE batched launch
-    (a transcript is 4-7 vectors of thousands of points)."""
+    """Challenge of one transcript: raw (bytes) parts in order, then the digest
+    of every point part (tensors / CipherVectors) in order."""
     return fs_challenges([(context, parts)])[0]
 
 
 def fs_challenges(specs) -> list:
-    """Challenges of several transcripts [(context, parts), ...] with ONE
-    to_affine launch for all their points (short vectors are latency-bound)."""
-    jacs, layouts = [], []
+    """Challenges of several transcripts [(context, parts), ...]; the point
+    parts of all of them are encoded and digested on the device together."""
+    groups, raws = [], []
     for context, parts in specs:
-        layout = [("raw", context.encode())]
-        for p in parts:
-            if isinstance(p, torch.Tensor):
-                jacs.append(p.contiguous().view(-1, 24))
-                layout.append(("pts", jacs[-1].shape[0]))
-            elif isinstance(p, CipherVector):
-                for t in (p.K, p.C):
-                    jacs.append(t.contiguous().view(-1, 24))
-                    layout.append(("pts", jacs[-1].shape[0]))
-            else:
-                layout.append(("raw", p if isinstance(p, (bytes, bytearray)) else str(p).encode()))
-        layouts.append(layout)
-    allb = _aff_bytes(torch.cat(jacs)) if jacs else b""
-    out, o = [], 0
-    for layout in layouts:
-        h = hashlib.sha256()
-        for kind, v in layout:
-            if kind == "pts":
-                h.update(allb[o: o + 64 * v])
-                o += 64 * v
-            else:
-                h.update(v)
-        out.append(int.from_bytes(h.digest(), "big") % O.R)
-    return out
+        pts = [p for p in parts if isinstance(p, (torch.Tensor, CipherVector))]
+        raw = tuple(p if isinstance(p, (bytes, bytearray)) else str(p).encode()
+                    for p in parts if not isinstance(p, (torch.Tensor, CipherVector)))
+        groups.append(pts)
+        raws.append((context, raw))
+    dgs = points_digests(groups)
+    return [fs_hash(ctx, raw, d) for (ctx, raw), d in zip(raws, dgs)]
 
 
-def _rand64(n: int, device) -> torch.Tensor:
-    """Random nonzero 64-bit batch weights (device CSPRNG), unknown to provers."""
+def _rand64(n: int, device, coins=None) -> torch.Tensor:
+    """Random nonzero 64-bit batch weights, unknown to provers: the verifier's
+    own ``coins`` (crypto/coins.py) or fresh device CSPRNG output."""
+    if coins is not None:
+        return coins.bits(n, device, 64, odd=True)
     r = bn.random_scalars(n, device)
     r[:, 2:] = 0
     r[:, 0] |= 1
     return r
+
+
+def _points_ok(tensors: list) -> torch.Tensor:
+    """Device bool: every row of every [m, 24] Jacobian tensor has canonical
+    limbs and is on the curve (a received raw payload is untrusted)."""
+    flat = torch.cat([t.reshape(-1, 24) for t in tensors]) if len(tensors) > 1 else tensors[0].reshape(-1, 24)
+    if flat.shape[0] == 0:
+        return torch.ones((), dtype=torch.bool, device=flat.device)
+    return nt.limbs_canonical(flat.reshape(-1, 8)).bool().all() & nt.g1j_on_curve(flat).bool().all()
+
+
+def _scalars_ok(t: torch.Tensor) -> torch.Tensor:
+    if t.numel() == 0:
+        return torch.ones((), dtype=torch.bool, device=t.device)
+    return nt.limbs_canonical(t.reshape(-1, 8), fr=True).bool().all()
+
+
+def _head_words(tensors: list, width: int) -> list:
+    """The first ``width`` words of every packed payload, ONE device-to-host copy."""
+    if not tensors:
+        return []
+    return torch.nn.utils.rnn.pad_sequence([t[:width] for t in tensors], batch_first=True).cpu().tolist()
 
 
 def _msm_is_zero(points: list, scalars: list) -> bool:
@@ -191,6 +244,10 @@ def schnorr_verify_batch(items: list, device="cpu") -> list:
 
 
 # ----------------------------------------------------------------------------- obfuscation (DLEQ)
+OBF_MAGIC = 0x4F425031  # "OBP1"
+_OBF_HEAD = 10          # magic, n, c (8 limbs)
+
+
 @dataclass
 class ObfuscationProof:
     C: CipherVector     # before
@@ -198,7 +255,9 @@ class ObfuscationProof:
     T: CipherVector     # commitments (a_i K_i, a_i C_i)
     c: int
     z: torch.Tensor     # [n, 8]
+    pts_digest: bytes = b""  # decoded data: digest of the transcript's point encodings
 
+    # reference-style export (kyber affine encodings): ledger / GetProofs
     def to_bytes(self) -> bytes:
         return b"".join([len(self.C).to_bytes(8, "little"), self.C.to_bytes(), self.Co.to_bytes(), self.T.to_bytes(),
                          O.scalar_to_bytes(self.c), bn.scalars_to_bytes(self.z).tobytes()])
@@ -206,6 +265,8 @@ class ObfuscationProof:
     @staticmethod
     def from_bytes(b: bytes, device="cpu") -> "ObfuscationProof":
         n = int.from_bytes(b[:8], "little")
+        if len(b) != 8 + 3 * 128 * n + 32 + 32 * n:
+            raise ValueError("obfuscation proof length does not match its header")
         o = 8
         cvs = []
         for _ in range(3):
@@ -215,6 +276,34 @@ class ObfuscationProof:
         o += 32
         z = bn.scalars_from_bytes(np.frombuffer(b[o: o + 32 * n], dtype=np.uint8), device)
         return ObfuscationProof(cvs[0], cvs[1], cvs[2], c, z)
+
+    # intra-cluster payload: raw Montgomery limbs, no host marshalling
+    def pack(self) -> torch.Tensor:
+        dev = self.C.device
+        n = len(self.C)
+        head = torch.cat([torch.tensor([OBF_MAGIC, n], dtype=torch.int32),
+                          bn.scalars_tensor([self.c], "cpu").reshape(-1)])
+        pts = [t.reshape(-1) for cv in (self.C, self.Co, self.T) for t in (cv.K, cv.C)]
+        return torch.cat([bn.h2d(head, dev)] + pts + [self.z.reshape(-1)])
+
+    @staticmethod
+    def unpack(t: torch.Tensor, head: list | None = None) -> "ObfuscationProof":
+        if head is None:
+            head = t[:_OBF_HEAD].cpu().tolist()
+        if head[0] != OBF_MAGIC or head[1] < 0:
+            raise ValueError("not a packed obfuscation proof")
+        n = head[1]
+        if t.numel() != _OBF_HEAD + 6 * 24 * n + 8 * n:
+            raise ValueError("packed obfuscation proof length does not match its header")
+        c = bn.scalars_from_tensor(torch.tensor(head[2:10], dtype=torch.int32).view(1, 8))[0]
+        o = _OBF_HEAD
+        parts = []
+        for _ in range(6):
+            parts.append(t[o: o + 24 * n].view(n, 24))
+            o += 24 * n
+        z = t[o: o + 8 * n].view(n, 8)
+        return ObfuscationProof(CipherVector(parts[0], parts[1]), CipherVector(parts[2], parts[3]),
+                                CipherVector(parts[4], parts[5]), c, z)
 
 
 def obfuscation_list_proof_creation(C: CipherVector, Co: CipherVector, s: torch.Tensor) -> ObfuscationProof:
@@ -227,6 +316,15 @@ def obfuscation_list_proof_creation(C: CipherVector, Co: CipherVector, s: torch.
     return ObfuscationProof(C, Co, T, c, z)
 
 
+def _obf_fs_ok(proofs: list) -> list:
+    """Each proof's Fiat-Shamir check: the challenge recomputed from the
+    transcript's point digest (decoded data, computed once per proof)."""
+    todo = [pr for pr in proofs if not pr.pts_digest]
+    for pr, d in zip(todo, points_digests([[pr.C, pr.Co, pr.T] for pr in todo])):
+        pr.pts_digest = d
+    return [fs_hash("proofTest/obfuscation", (), pr.pts_digest) == pr.c for pr in proofs]
+
+
 def obfuscation_list_proof_verification(pr: ObfuscationProof, threshold: float = 1.0) -> bool:
     """ObfuscationListProofVerification(percent): z K == T1 + c Ko and z C == T2 + c Co
     for the first ceil(threshold * n) elements (reference sampling)."""
@@ -234,7 +332,7 @@ def obfuscation_list_proof_verification(pr: ObfuscationProof, threshold: float =
     k = _first(n, threshold)
     if k == 0:
         return True
-    if fs_challenge("proofTest/obfuscation", pr.C, pr.Co, pr.T) != pr.c:
+    if not _obf_fs_ok([pr])[0]:
         return False
     dev = pr.C.device
     c = _sc([pr.c], dev)
@@ -245,6 +343,10 @@ def obfuscation_list_proof_verification(pr: ObfuscationProof, threshold: float =
 
 
 # ----------------------------------------------------------------------------- key switching
+KS_MAGIC = 0x4B535031   # "KSP1"
+_KS_HEAD = 2 + 3 * 16 + 2 * 8  # magic, n, X / Q / T3 affine, c, zb
+
+
 @dataclass
 class KeySwitchProof:
     X: tuple                 # CN public key
@@ -257,20 +359,21 @@ class KeySwitchProof:
     c: int
     za: torch.Tensor         # [n, 8]
     zb: int
+    pts_digest: bytes = b""  # decoded data: digest of the transcript's point encodings
 
+    # reference-style export (kyber affine encodings): ledger / GetProofs
     def to_bytes(self) -> bytes:
         n = self.K.shape[0]
-        cached = getattr(self, "_aff", None)  # affine encodings kept from the prover's transcript
-        Kb, shb, t1b, t2b = cached if cached is not None else (
-            _aff_bytes(self.K), self.share.to_bytes(), _aff_bytes(self.T1), _aff_bytes(self.T2))
-        return b"".join([n.to_bytes(8, "little"), O.g1_to_bytes(self.X), O.g1_to_bytes(self.Q), Kb, shb, t1b, t2b,
-                         self.T3,
+        return b"".join([n.to_bytes(8, "little"), O.g1_to_bytes(self.X), O.g1_to_bytes(self.Q), _aff_bytes(self.K),
+                         self.share.to_bytes(), _aff_bytes(self.T1), _aff_bytes(self.T2), self.T3,
                          O.scalar_to_bytes(self.c), bn.scalars_to_bytes(self.za).tobytes(),
                          O.scalar_to_bytes(self.zb)])
 
     @staticmethod
     def from_bytes(b: bytes, device="cpu") -> "KeySwitchProof":
         n = int.from_bytes(b[:8], "little")
+        if len(b) != 8 + 128 + 64 * n + 128 * n + 128 * n + 64 + 32 + 32 * n + 32:
+            raise ValueError("key-switch proof length does not match its header")
         o = 8
         X = O.g1_from_bytes(b[o: o + 64]); o += 64
         Q = O.g1_from_bytes(b[o: o + 64]); o += 64
@@ -290,6 +393,57 @@ class KeySwitchProof:
         zb = int.from_bytes(b[o: o + 32], "big")
         return KeySwitchProof(X, Q, K, share, T1, T2, T3, c, za, zb)
 
+    # intra-cluster payload: raw Montgomery limbs, no host marshalling
+    def pack(self) -> torch.Tensor:
+        dev = self.K.device
+        n = self.K.shape[0]
+        head = torch.cat([torch.tensor([KS_MAGIC, n], dtype=torch.int32),
+                          bn.g1_aff_tensor([self.X, self.Q, O.g1_from_bytes(self.T3)], "cpu").reshape(-1),
+                          bn.scalars_tensor([self.c, self.zb], "cpu").reshape(-1)])
+        body = [t.reshape(-1) for t in (self.K, self.share.K, self.share.C, self.T1, self.T2, self.za)]
+        return torch.cat([bn.h2d(head, dev)] + body)
+
+    @staticmethod
+    def unpack(t: torch.Tensor, head: list | None = None) -> "KeySwitchProof":
+        if head is None:
+            head = t[:_KS_HEAD].cpu().tolist()
+        if head[0] != KS_MAGIC or head[1] < 0:
+            raise ValueError("not a packed key-switch proof")
+        n = head[1]
+        if t.numel() != _KS_HEAD + 5 * 24 * n + 8 * n:
+            raise ValueError("packed key-switch proof length does not match its header")
+        hp = torch.tensor(head[2:50], dtype=torch.int32).view(3, 16)
+        lim = bn.limbs_to_ints(hp.numpy().reshape(-1, 8))
+        if any(v >= O.P for v in lim):
+            raise ValueError("non-canonical coordinate in a key-switch proof header")
+        X, Q, T3 = bn.g1_points_from_aff(hp)
+        for pt in (X, Q, T3):
+            if not O.g1_on_curve(pt):
+                raise ValueError("key-switch proof header point not on the curve")
+        c, zb = bn.scalars_from_tensor(torch.tensor(head[50:66], dtype=torch.int32).view(2, 8))
+        o = _KS_HEAD
+        rows = []
+        for _ in range(5):
+            rows.append(t[o: o + 24 * n].view(n, 24))
+            o += 24 * n
+        za = t[o: o + 8 * n].view(n, 8)
+        return KeySwitchProof(X, Q, rows[0], CipherVector(rows[1], rows[2]), rows[3], rows[4], O.g1_to_bytes(T3),
+                              c, za, zb)
+
+
+def unpack_many(kind: str, tensors: list) -> list:
+    """Unpack many packed proofs of one kind with ONE header copy; an entry is
+    the proof or the exception that rejects it."""
+    cls, width = {"keyswitch": (KeySwitchProof, _KS_HEAD), "obfuscation": (ObfuscationProof, _OBF_HEAD)}[kind]
+    heads = _head_words(tensors, width)
+    out = []
+    for t, h in zip(tensors, heads):
+        try:
+            out.append(cls.unpack(t, h[: min(width, t.numel())] if t.numel() >= width else t.cpu().tolist()))
+        except Exception as e:  # noqa: BLE001 -- a malformed payload is a rejected proof
+            out.append(e)
+    return out
+
 
 def key_switch_share(x: int, K: torch.Tensor, Q_point, v: torch.Tensor | None = None):
     """One CN's key-switching share: (v_i B, v_i Q - x K_i)."""
@@ -306,9 +460,28 @@ def key_switch_share(x: int, K: torch.Tensor, Q_point, v: torch.Tensor | None = 
     return share, v
 
 
+@dataclass
+class KeySwitchPending:
+    """What a batch of co-located CNs needs to finish their key-switch proofs
+    (challenge + responses) off the query's critical path."""
+    secrets: list
+    publics: list
+    Q: tuple
+    K: torch.Tensor
+    shares: CipherVector
+    T1: torch.Tensor
+    T2: torch.Tensor
+    a: torch.Tensor
+    v: torch.Tensor
+    bs: list
+
+
 def key_switch_shares_batch(secrets: list, publics: list, K: torch.Tensor, Q_point, with_proofs: bool):
-    """Key-switching shares (and proofs) of several co-located CNs over the same
-    K vector in a handful of launches sized (#CNs x n) instead of per CN."""
+    """Key-switching shares of several co-located CNs over the same K vector
+    in a handful of launches sized (#CNs x n) instead of per CN.  -> (list of
+    shares, KeySwitchPending or None): the shares need no host round trip;
+    ``finish_keyswitch_proofs`` completes the proofs (one device-to-host copy
+    for the challenges of every CN)."""
     from ..crypto.elgamal import pk_table
 
     dev = K.device
@@ -319,6 +492,7 @@ def key_switch_shares_batch(secrets: list, publics: list, K: torch.Tensor, Q_poi
     x_rep = torch.cat([_sc([x], dev).expand(n, 8) for x in secrets]).contiguous()
     v = bn.random_scalars(c * n, dev)
     scal = [x_rep]
+    bs = None
     if with_proofs:
         bs = [O.random_scalar() for _ in secrets]
         scal.append(torch.cat([_sc([b], dev).expand(n, 8) for b in bs]).contiguous())
@@ -329,43 +503,37 @@ def key_switch_shares_batch(secrets: list, publics: list, K: torch.Tensor, Q_poi
         vB = nt.g1_fb_mul(tabB, v)
         vQ = nt.g1_fb_mul(tabQ, v)
         shares_all = CipherVector(vB, nt.g1_add(vQ, xK, subtract=True))
-    out = []
-    if with_proofs:
-        with timers.span("ks.commit"):
-            a = bn.random_scalars(c * n, dev)
-            T1 = nt.g1_fb_mul(tabB, a)
-            T2 = nt.g1_add(nt.g1_fb_mul(tabQ, a), prods[c * n:].contiguous(), subtract=True)
+    shares = [shares_all[j * n:(j + 1) * n] for j in range(c)]
     if not with_proofs:
-        return [(shares_all[j * n:(j + 1) * n], None) for j in range(c)]
-    # every CN's transcript in ONE normalisation launch; the affine encodings are
-    # kept on the proofs so marshalling them later needs no further launch
-    T3s = [O.g1_to_bytes(bn.g1_mul_point(b)) for b in bs]
-    with timers.span("ks.affine"):
-        aff = _aff_bytes(torch.cat([K, shares_all.K, shares_all.C, T1, T2]))
-    seg = 64 * n
-    Kb = aff[:seg]
+        return shares, None
+    with timers.span("ks.commit"):
+        a = bn.random_scalars(c * n, dev)
+        T1 = nt.g1_fb_mul(tabB, a)
+        T2 = nt.g1_add(nt.g1_fb_mul(tabQ, a), prods[c * n:].contiguous(), subtract=True)
+    return shares, KeySwitchPending(list(secrets), list(publics), Q_point, K, shares_all, T1, T2, a, v, bs)
 
-    def part(block, j):
-        o = seg * (1 + block * c + j)
-        return aff[o: o + seg]
 
-    Qb = O.g1_to_bytes(Q_point)
-    for j in range(c):
+def finish_keyswitch_proofs(p: KeySwitchPending) -> list:
+    """Challenges (every CN's transcript digested on the device, ONE copy to
+    the host) and responses za = a + c v (one launch) of a pending batch."""
+    dev = p.K.device
+    c_n = len(p.secrets)
+    n = p.K.shape[0]
+    T3s = [O.g1_to_bytes(bn.g1_mul_point(b)) for b in p.bs]
+    Qb = O.g1_to_bytes(p.Q)
+    groups = [[p.K, p.shares[j * n:(j + 1) * n], p.T1[j * n:(j + 1) * n], p.T2[j * n:(j + 1) * n]]
+              for j in range(c_n)]
+    with timers.span("ks.transcript"):
+        dgs = points_digests(groups)
+    chs = [fs_hash("proofTest/keyswitch", (O.g1_to_bytes(p.publics[j]), Qb, T3s[j]), dgs[j]) for j in range(c_n)]
+    c_rep = torch.cat([_sc([ch], dev).expand(n, 8) for ch in chs]).contiguous()
+    za = nt.fr_arith(nt.FR_ADD, p.a, nt.fr_arith(nt.FR_MUL, p.v, c_rep))
+    out = []
+    for j in range(c_n):
         sl = slice(j * n, (j + 1) * n)
-        share = shares_all[sl]
-        t1, t2 = T1[sl].contiguous(), T2[sl].contiguous()
-        sKb, sCb, t1b, t2b = part(0, j), part(1, j), part(2, j), part(3, j)
-        with timers.span("ks.hash"):
-            h = hashlib.sha256()
-            for piece in (b"proofTest/keyswitch", O.g1_to_bytes(publics[j]), Qb, Kb, sKb, sCb, t1b, t2b, T3s[j]):
-                h.update(piece)
-        ch = int.from_bytes(h.digest(), "big") % O.R
-        za = nt.fr_arith(nt.FR_ADD, a[sl].contiguous(), nt.fr_arith(nt.FR_MUL, v[sl].contiguous(), _sc([ch], dev)))
-        pr = KeySwitchProof(publics[j], Q_point, K, share, t1, t2, T3s[j], ch, za, (bs[j] + ch * secrets[j]) % O.R)
-        shb = np.concatenate([np.frombuffer(sKb, np.uint8).reshape(n, 64),
-                              np.frombuffer(sCb, np.uint8).reshape(n, 64)], axis=1).tobytes()
-        pr._aff = (Kb, shb, t1b, t2b)
-        out.append((share, pr))
+        out.append(KeySwitchProof(p.publics[j], p.Q, p.K, p.shares[sl], p.T1[sl].contiguous(), p.T2[sl].contiguous(),
+                                  T3s[j], chs[j], za[sl].contiguous(), (p.bs[j] + chs[j] * p.secrets[j]) % O.R,
+                                  dgs[j]))
     return out
 
 
@@ -382,15 +550,38 @@ def key_switch_list_proof_creation(x: int, X, Q_point, K: torch.Tensor, share: C
     T1 = nt.g1_fb_mul(tabB, a)
     T2 = nt.g1_add(nt.g1_fb_mul(tabQ, a), nt.g1_mul(K.contiguous(), _sc([b], dev)), subtract=True)
     T3 = O.g1_to_bytes(bn.g1_mul_point(b))
-    c = fs_challenge("proofTest/keyswitch", O.g1_to_bytes(X), O.g1_to_bytes(Q_point), K, share, T1, T2, T3)
+    c = fs_challenge("proofTest/keyswitch", O.g1_to_bytes(X), O.g1_to_bytes(Q_point), T3, K, share, T1, T2)
     za = nt.fr_arith(nt.FR_ADD, a, nt.fr_arith(nt.FR_MUL, v, _sc([c], dev)))
     zb = (b + c * x) % O.R
     return KeySwitchProof(X, Q_point, K, share, T1, T2, T3, c, za, zb)
 
 
-def key_switch_batch_verification(proofs: list, threshold: float = 1.0, combine: bool = True) -> list:
+def _ks_fs_ok(proofs: list) -> list:
+    """Each proof's weight-free checks, done by the verifier itself: the
+    challenge recomputed from the transcript (point digests are decoded data,
+    computed once per proof) and zb B == T3 + c X."""
+    todo = [pr for pr in proofs if not pr.pts_digest]
+    if todo:
+        with timers.span("ks.verify.transcripts"):
+            for pr, d in zip(todo, points_digests([[pr.K, pr.share, pr.T1, pr.T2] for pr in todo])):
+                pr.pts_digest = d
+    out = []
+    for pr in proofs:
+        c = fs_hash("proofTest/keyswitch", (O.g1_to_bytes(pr.X), O.g1_to_bytes(pr.Q), pr.T3), pr.pts_digest)
+        ok = c == pr.c
+        if ok:
+            try:
+                ok = bn.g1_mul_point(pr.zb) == O.g1_add(O.g1_from_bytes(pr.T3), bn.g1_mul_point(c, pr.X))
+            except ValueError:
+                ok = False
+        out.append(ok)
+    return out
+
+
+def key_switch_batch_verification(proofs: list, threshold: float = 1.0, combine: bool = True, coins=None) -> list:
     """Verify several CNs' key-switch proofs (same querier key) as ONE random
-    linear combination: with fresh 64-bit weights rho_i, sig_i per element,
+    linear combination: with 64-bit weights rho_i, sig_i per element drawn
+    from the verifier's ``coins``,
       (sum rho za) B + (sum sig za) Q - sum rho T1 - sum c rho (vB)
         - sum zb sig K - sum sig T2 - sum c sig (vQ - xK) == O
     is one Pippenger MSM (no per-element 256-step chains; soundness error
@@ -398,69 +589,56 @@ def key_switch_batch_verification(proofs: list, threshold: float = 1.0, combine:
     bitmap blames exactly the bad ones."""
     if not proofs:
         return []
-    # weight-free part (recomputed challenge, the x-part T3 check): a property
-    # of the proof data, computed once per decoded proof and shared by the
-    # verifying nodes co-hosted on this rank (each keeps its own random weights)
-    todo = [pr for pr in proofs if getattr(pr, "_fs_ok", None) is None]
-    if todo:
-        with timers.span("ks.verify.challenges"):
-            cs = fs_challenges([("proofTest/keyswitch", (O.g1_to_bytes(pr.X), O.g1_to_bytes(pr.Q), pr.K, pr.share,
-                                                         pr.T1, pr.T2, pr.T3)) for pr in todo])
-            for pr, c in zip(todo, cs):
-                pr._fs_ok = c == pr.c and bn.g1_mul_point(pr.zb) == O.g1_add(O.g1_from_bytes(pr.T3),
-                                                                             bn.g1_mul_point(c, pr.X))
-    ok, live = [], []
-    for pr in proofs:
-        k = _first(pr.K.shape[0], threshold)
-        ok.append(pr._fs_ok)
-        if pr._fs_ok and k > 0:
-            live.append((len(ok) - 1, pr, k))
+    ok = _ks_fs_ok(proofs)
+    live = [(i, pr, _first(pr.K.shape[0], threshold)) for i, pr in enumerate(proofs)]
+    live = [(i, pr, k) for i, pr, k in live if ok[i] and k > 0]
     if not live or not combine:
         return ok
     with timers.span("ks.verify.msm"):
-        if _ks_combined(live)[0]:
+        if _ks_combined(live, 1, [coins])[0]:
             return ok
     for idx, pr, k in live:
-        ok[idx] = _ks_combined([(idx, pr, k)])[0]
+        ok[idx] = _ks_combined([(idx, pr, k)], 1, [coins])[0]
     return ok
 
 
-def key_switch_batch_verification_multi(proofs: list, threshold: float, n_vn: int) -> list:
-    """``key_switch_batch_verification`` for ``n_vn`` verifying nodes hosted on
-    one rank: the weight-free part once, every VN's random combination in ONE
-    grouped MSM (one bucket plan and host sync instead of one per VN), each
-    VN's verdict from its own weights.  -> [per-VN list of bools]."""
+def key_switch_batch_verification_multi(proofs: list, threshold: float, coins_list: list) -> list:
+    """``key_switch_batch_verification`` for several verifying nodes hosted on
+    one rank: every VN runs its own Fiat-Shamir / T3 checks and its own random
+    combination (weights from its own coins); the combinations share ONE
+    grouped MSM launch.  -> [per-VN list of bools]."""
+    n_vn = len(coins_list)
     if not proofs:
         return [[] for _ in range(n_vn)]
-    ok = key_switch_batch_verification(proofs, threshold, combine=False)
-    live = [(i, pr, _first(pr.K.shape[0], threshold)) for i, pr in enumerate(proofs)]
-    live = [(i, pr, k) for i, pr, k in live if ok[i] and k > 0]
-    if not live:
-        return [list(ok) for _ in range(n_vn)]
-    with timers.span("ks.verify.msm_multi"):
-        verdicts = _ks_combined(live, n_vn)
-    out = []
+    oks = [_ks_fs_ok(proofs) for _ in range(n_vn)]
+    lives = [[(i, pr, _first(pr.K.shape[0], threshold)) for i, pr in enumerate(proofs) if ok[i]] for ok in oks]
+    lives = [[x for x in lv if x[2] > 0] for lv in lives]
+    out = [list(ok) for ok in oks]
+    if all(lv == lives[0] for lv in lives) and lives[0]:
+        with timers.span("ks.verify.msm_multi"):
+            verdicts = _ks_combined(lives[0], n_vn, coins_list)
+    else:
+        verdicts = [(_ks_combined(lv, 1, [c])[0] if lv else True) for lv, c in zip(lives, coins_list)]
     for v in range(n_vn):
-        res = list(ok)
         if not verdicts[v]:  # this VN's own per-proof re-check blames the bad ones
-            for idx, pr, k in live:
-                res[idx] = _ks_combined([(idx, pr, k)])[0]
-        out.append(res)
+            for idx, pr, k in lives[v]:
+                out[v][idx] = _ks_combined([(idx, pr, k)], 1, [coins_list[v]])[0]
     return out
 
 
-def _ks_combined(live, n_vn: int = 1):
+def _ks_combined(live, n_vn: int = 1, coins=None):
     """Grouped MSM: every per-element weight stays 64 bit (8 bucket additions
     per point instead of 32); the per-proof challenges c, zb multiply the five
-    group sums of each proof on the host.  ``n_vn`` independent combinations
-    (fresh weights each) share the one MSM launch -> [bool] per combination."""
+    group sums of each proof on the host.  -> [bool] (``n_vn`` independent
+    combinations, fresh weights each, sharing the one MSM launch)."""
     dev = live[0][1].K.device
     nl = len(live)
     pts, scs, grp = [], [], []
     sB, sQ = [], []
+    cl = coins if isinstance(coins, (list, tuple)) else [coins] * n_vn
     for v in range(n_vn):
         for j, (_, pr, k) in enumerate(live):
-            rho, sig = _rand64(k, dev), _rand64(k, dev)
+            rho, sig = _rand64(k, dev, cl[v]), _rand64(k, dev, cl[v])
             za = pr.za[:k].contiguous()
             # group 5j+0: rho T1, +1: rho vB, +2: sig K (x zb), +3: sig T2, +4: sig (vQ - xK) (x c)
             for gi, (pt, w) in enumerate(((pr.T1, rho), (pr.share.K, rho), (pr.K, sig), (pr.T2, sig),
@@ -489,39 +667,31 @@ def _ks_combined(live, n_vn: int = 1):
     return out
 
 
-def obfuscation_batch_verification(proofs: list, threshold: float = 1.0) -> list:
+def obfuscation_batch_verification(proofs: list, threshold: float = 1.0, coins=None) -> list:
     """Several CNs' obfuscation proofs as one random linear combination:
       sum rho (z K - T1 - c Ko) + sum sig (z C - T2 - c Co) == O
     (one MSM; per-proof re-check only if the combination fails)."""
     if not proofs:
         return []
-    todo = [pr for pr in proofs if getattr(pr, "_fs_ok", None) is None]   # shared by co-hosted VNs
-    if todo:
-        for pr, c in zip(todo, fs_challenges([("proofTest/obfuscation", (pr.C, pr.Co, pr.T)) for pr in todo])):
-            pr._fs_ok = c == pr.c
-    ok, live = [], []
-    for pr in proofs:
-        k = _first(len(pr.C), threshold)
-        good = pr._fs_ok
-        ok.append(good)
-        if good and k > 0:
-            live.append((len(ok) - 1, pr, k))
+    ok = _obf_fs_ok(proofs)
+    live = [(i, pr, _first(len(pr.C), threshold)) for i, pr in enumerate(proofs)]
+    live = [(i, pr, k) for i, pr, k in live if ok[i] and k > 0]
     if not live:
         return ok
-    if _obf_combined(live):
+    if _obf_combined(live, coins):
         return ok
     for idx, pr, k in live:
-        ok[idx] = _obf_combined([(idx, pr, k)])
+        ok[idx] = _obf_combined([(idx, pr, k)], coins)
     return ok
 
 
-def _obf_combined(live) -> bool:
+def _obf_combined(live, coins=None) -> bool:
     """Grouped MSM: rho z K + sig z C (full-size weights), rho T1 + sig T2
     and rho Ko + sig Co (64-bit weights, the latter times c on the host)."""
     dev = live[0][1].C.device
     pts, scs, grp = [], [], []
     for j, (_, pr, k) in enumerate(live):
-        rho, sig = _rand64(k, dev), _rand64(k, dev)
+        rho, sig = _rand64(k, dev, coins), _rand64(k, dev, coins)
         z = pr.z[:k].contiguous()
         terms = ((pr.C.K, nt.fr_arith(nt.FR_MUL, rho, z), 0), (pr.C.C, nt.fr_arith(nt.FR_MUL, sig, z), 0),
                  (pr.T.K, rho, 1), (pr.T.C, sig, 1), (pr.Co.K, rho, 2), (pr.Co.C, sig, 2))
@@ -550,18 +720,12 @@ def key_switch_list_proof_verification(pr: KeySwitchProof, threshold: float = 1.
     k = _first(n, threshold)
     if k == 0:
         return True
-    c = fs_challenge("proofTest/keyswitch", O.g1_to_bytes(pr.X), O.g1_to_bytes(pr.Q), pr.K, pr.share, pr.T1, pr.T2,
-                     pr.T3)
-    if c != pr.c:
-        return False
-    # zb B == T3 + c X
-    T3 = O.g1_from_bytes(pr.T3)
-    if bn.g1_mul_point(pr.zb) != O.g1_add(T3, bn.g1_mul_point(c, pr.X)):
+    if not _ks_fs_ok([pr])[0]:
         return False
     dev = pr.K.device
     tabB = bn.base_table(dev)
     tabQ = pk_table(pr.Q, dev).tabP
-    cs = _sc([c], dev)
+    cs = _sc([pr.c], dev)
     za = pr.za[:k].contiguous()
     # za B == T1 + c (vB)
     ok1 = nt.g1_eq(nt.g1_fb_mul(tabB, za),

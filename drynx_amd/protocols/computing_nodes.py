@@ -38,18 +38,24 @@ def _root_rank(ctx, sq) -> int:
 
 def collective_aggregation(ctx, sq, cn_sums: dict, cn_inputs: dict, n_rows: int, proofs: list):
     """Sum every CN's DP aggregate onto the root CN; each CN publishes an
-    aggregation proof (its inputs + its claimed sum)."""
+    aggregation proof (its inputs + its claimed sum).  The proofs (packed
+    device tensors, digest, signature) are finished on the node's proof worker
+    while the aggregation proceeds (the reference's ProofFunc runs in its own
+    goroutine, service.go:533-560)."""
     root = _root_rank(ctx, sq)
-    local = []
+    local, items = [], []
+    roster = {s.id for s in sq.RosterServers.list}
     for cn in ctx.cluster.local(ctx.rank, "cn"):
-        if cn.id not in {s.id for s in sq.RosterServers.list}:
+        if cn.id not in roster:
             continue
         with timers.timed(f"{cn.id}_AggregationPhase"):
             s = cn_sums.get(cn.id) or eg.CipherVector.zeros(n_rows, ctx.device)
             local.append(s)
             if sq.Query.Proofs:
                 pr = ags.aggregation_list_proof_creation(list(cn_inputs.get(cn.id, {}).values()), s)
-                proofs.append(prq.new_proof_request("aggregation", pr, sq.SurveyID, cn.id, "", cn.keypair.secret))
+                items.append(("aggregation", pr, cn.id, "", cn.keypair.secret))
+    if items:
+        proofs.append(ctx.defer_proofs(prq.new_proof_requests, items, sq.SurveyID))
     with timers.timed("CollectiveAggregation"):
         return ec.sum_to_root(ctx.comm, local, n_rows, root)
 
@@ -57,15 +63,20 @@ def collective_aggregation(ctx, sq, cn_sums: dict, cn_inputs: dict, n_rows: int,
 def obfuscation(ctx, sq, agg, n_rows: int, proofs: list):
     root = _root_rank(ctx, sq)
     agg = ec.broadcast_cv(ctx.comm, agg, n_rows, root)
-    local = []
+    local, pend = [], []
     for cn in ctx.cluster.local(ctx.rank, "cn"):
         with timers.timed(f"{cn.id}_ObfuscationPhase"):
             s = bn.random_scalars(n_rows, ctx.device)
             co = agg.mul_scalars(s)
             local.append(co)
             if sq.Query.Proofs:
-                pr = sigma.obfuscation_list_proof_creation(agg, co, s)
-                proofs.append(prq.new_proof_request("obfuscation", pr, sq.SurveyID, cn.id, "", cn.keypair.secret))
+                pend.append((cn, co, s))
+    if pend:
+        def finish(agg=agg, pend=pend):
+            items = [("obfuscation", sigma.obfuscation_list_proof_creation(agg, co, s), cn.id, "", cn.keypair.secret)
+                     for cn, co, s in pend]
+            return prq.new_proof_requests(items, sq.SurveyID)
+        proofs.append(ctx.defer_proofs(finish))
     return ec.sum_to_root(ctx.comm, local, n_rows, root)
 
 
@@ -128,14 +139,17 @@ def key_switching(ctx, sq, agg, n_groups: int, n_out: int, noise, proofs: list):
     local_K = []
     cns = [cn for cn in ctx.cluster.local(ctx.rank, "cn") if cn.id in {s.id for s in sq.RosterServers.list}]
     if cns:
-        # all co-located CNs in one batch of launches (short vectors are latency-bound)
+        # all co-located CNs in one batch of launches (short vectors are latency-bound);
+        # the proofs' challenges / responses / envelopes finish on the proof worker
         with timers.timed("KeySwitchingPhase"):
-            res = sigma.key_switch_shares_batch([c.keypair.secret for c in cns], [c.public for c in cns], agg.K, Q,
-                                                bool(sq.Query.Proofs))
-            for cn, (share, pr) in zip(cns, res):
-                local_K.append(share)
-                if pr is not None:
-                    proofs.append(prq.new_proof_request("keyswitch", pr, sq.SurveyID, cn.id, "", cn.keypair.secret))
+            local_K, pend = sigma.key_switch_shares_batch([c.keypair.secret for c in cns], [c.public for c in cns],
+                                                          agg.K, Q, bool(sq.Query.Proofs))
+        if pend is not None:
+            def finish(pend=pend, cns=cns):
+                prs = sigma.finish_keyswitch_proofs(pend)
+                return prq.new_proof_requests([("keyswitch", pr, cn.id, "", cn.keypair.secret)
+                                               for cn, pr in zip(cns, prs)], sq.SurveyID)
+            proofs.append(ctx.defer_proofs(finish))
     total = ec.sum_to_root(ctx.comm, local_K, n_rows, root)
     if ctx.rank != root:
         return None

@@ -24,6 +24,7 @@ import torch
 
 from ..ledger import skipchain as skc
 from ..parallel.comm import bytes_to_obj, obj_to_bytes
+from ..crypto.coins import Coins
 from ..proofs import requests as prq
 from ..query import query_to_proofs_nbrs
 from ..utils import timers
@@ -39,52 +40,74 @@ def expected_counts(sq) -> dict:
 
 
 def use_pool(ctx) -> bool:
-    """Pooled range verification: every rank checks a 1/world slice of every
-    range-proof list on behalf of every VN (so three VNs keep eight GPUs busy;
-    on one GPU the co-hosted VNs' batches share the decode and run back to
-    back); the VN's own rank keeps the signature checks, the sampling
-    decision, the bitmap and the ledger.  ``DRYNX_VN_POOL=0`` leaves each VN's
-    range checks to the VN's own rank, one VN at a time."""
-    return os.environ.get("DRYNX_VN_POOL", "1") != "0"
+    """Pooled range verification (single-operator deployments only): every
+    rank checks a 1/world slice of every range-proof list on behalf of every
+    VN, with THAT VN's coins (a per-survey seed the VN hands out), so three
+    VNs keep eight GPUs busy; the VN's own rank keeps the signature checks,
+    the sampling decisions, the bitmap and the ledger, and accepts a helper's
+    slice verdict only if the helper's digest of the slice it checked equals
+    the VN's own digest of that slice of its signed payload.  On one GPU the
+    co-hosted VNs' batches share the decode and run back to back.
+    ``ctx.pool_policy`` (or DRYNX_VN_POOL) "0" leaves each VN's range checks
+    to the VN's own rank; a multi-party deployment (services/server.py)
+    forces that."""
+    pol = getattr(ctx, "pool_policy", None)
+    if pol is None:
+        pol = os.environ.get("DRYNX_VN_POOL", "1")
+    return str(pol) != "0"
 
 
-def fan_out(ctx, sq, local_requests: list, all_ranks: bool = False) -> list:
-    """All requests, on every rank that hosts a VN (others get nothing), or on
-    every rank (``all_ranks``: pooled verification)."""
+def fan_out(ctx, sq, local_requests: list, pool: bool = False) -> list:
+    """Every request to the ranks that host a VN; with ``pool``, the other
+    ranks get only THEIR slice of every range bundle (what they check for
+    the pool, ~1/W of the payload) plus the envelope header.  Payload
+    tensors (range bundles, packed per-CN proofs) travel as raw limbs in one
+    all-to-all with sizes announced by the control message (no size round);
+    envelopes and byte payloads ride on the control message."""
     vns = [ctx.cluster.by_id(si.id) for si in sq.Query.RosterVNs.list]
-    vn_ranks = list(range(ctx.comm.world)) if all_ranks else sorted({v.rank for v in vns})
-    if ctx.comm.world == 1:
+    W = ctx.comm.world
+    vn_ranks = sorted({v.rank for v in vns})
+    dests = list(range(W)) if pool else vn_ranks
+    if W == 1:
         return list(local_requests)
-    # sharded verification: ship the payload only to ranks hosting an assigned
-    # VN; the others get the signed header (signature + digest) and record 2
-    # range-proof payloads (tens of MB per DP) go as raw limb tensors over RCCL;
-    # envelopes and small proofs as pickled control messages
-    per_rank = {d: [] for d in vn_ranks}
-    per_rank_t = {d: [] for d in vn_ranks}
+    per_rank = {d: [] for d in dests}
+    per_rank_t = {d: [] for d in dests}
     packed = {}
     for idx, r in enumerate(local_requests):
         assigned = prq.assigned_vns(sq, r, len(vns))
-        full_ranks = vn_ranks if (assigned is None or all_ranks) else {vns[i].rank for i in assigned}
-        for d in vn_ranks:
+        full_ranks = set(vn_ranks) if (assigned is None or pool) else {vns[i].rank for i in assigned}
+        for d in dests:
+            if d == ctx.rank:
+                continue
             if d not in full_ranks:
-                per_rank[d].append(r.header().to_wire())
-            elif r.kind == "range" and r.obj is not None and d != ctx.rank:
+                if pool and r.kind == "range" and r.obj is not None and d not in vn_ranks:
+                    # a helper: its slice of the bundle (the pool's part d of W)
+                    sl = _helper_slice(r.obj, sq, (d, W))
+                    w = r.header().to_wire()
+                    if sl:
+                        t = prq.range_bundle_pack(sl).to(ctx.device)
+                        w["tensor"], w["slice"] = t.numel(), [d, W]
+                        per_rank_t[d].append(t)
+                    per_rank[d].append(w)
+                else:
+                    per_rank[d].append(r.header().to_wire())
+            elif r.tensor is not None and r._data is None:
                 if idx not in packed:
-                    packed[idx] = (r.tensor if r.tensor is not None else prq.range_bundle_pack(r.obj)).to(ctx.device)
+                    packed[idx] = r.tensor.to(ctx.device)
                 w = r.header().to_wire()
                 w["digest"], w["tensor"] = b"", packed[idx].numel()
                 per_rank[d].append(w)
                 per_rank_t[d].append(packed[idx])
             else:
                 per_rank[d].append(r.to_wire())
-    got = ctx.comm.exchange_bytes({d: obj_to_bytes(per_rank[d]) for d in vn_ranks})
+    got = ctx.comm.exchange_bytes({d: obj_to_bytes(per_rank[d]) for d in dests if d != ctx.rank})
     wires = {src: bytes_to_obj(b) for src, b in got.items()}
-    tens = {d: torch.cat(per_rank_t[d]) for d in vn_ranks if per_rank_t[d]}
+    tens = {d: torch.cat(per_rank_t[d]) for d in dests if per_rank_t[d]}
     # the envelopes announced every tensor's size: no size round for the payloads
-    sizes = {src: sum(w.get("tensor") or 0 for w in ws) for src, ws in wires.items() if src != ctx.rank}
+    sizes = {src: sum(w.get("tensor") or 0 for w in ws) for src, ws in wires.items()}
     got_t = ctx.comm.exchange(tens, recv_sizes={s_: n_ for s_, n_ in sizes.items() if n_})
     out = []
-    for src in sorted(got):
+    for src in sorted(set(wires) | {ctx.rank}):
         if src == ctx.rank:
             out += list(local_requests)  # keep decoded objects for locally produced proofs
             continue
@@ -95,40 +118,118 @@ def fan_out(ctx, sq, local_requests: list, all_ranks: bool = False) -> list:
             if n:
                 t = got_t[src][off: off + n]
                 off += n
-                req.set_tensor(t)  # signed bytes: the VN re-hashes and decodes them on its device
+                if w.get("slice"):
+                    # helper copy: the payload is this slice; the digest stays the signed one
+                    req._data, req.tensor, req.slice_of = None, t, tuple(w["slice"])
+                else:
+                    req.set_tensor(t)  # signed bytes: the VN re-hashes and decodes them on its device
             out.append(req)
     return out
 
 
+def _helper_slice(lists, sq, part) -> list:
+    """What the prover sends pool helper ``part[0]`` (tests substitute an
+    equivocating prover here)."""
+    return prq.slice_lists(lists, sq, part)
+
+
 def pool_verify_ranges(ctx, sq, reqs: list, vns: list) -> dict:
-    """Pooled range verification (see ``use_pool``).  Sampling is decided by
-    each VN's own rank (reference ``rand.Float64() <= Threshold``, or the
-    sharding extension) and shared; rank k then checks slice k/W of the
-    sampled prefix of every list, one batch per VN with that VN's own random
-    weights; the slice verdicts are all-gathered and AND-ed.
+    """Pooled range verification (see ``use_pool``).  Each VN's rank decides
+    that VN's sampling (reference ``rand.Float64() <= Threshold``, from the
+    VN's own coins, or the sharding extension) and draws a per-survey seed;
+    rank k checks slice k/W of the sampled prefix of every list for every VN
+    with coins derived from that VN's seed, and reports its verdicts with
+    the digest of each slice it checked.  Each VN's rank then accepts a
+    helper's slice verdict only when the digest matches its own digest of
+    that slice of the signed payload, and re-checks any other slice itself.
     -> {vn_id: {base_key: None (not sampled) | bool}} on every rank."""
     W, k = ctx.comm.world, ctx.comm.rank
     rng = [i for i, r in enumerate(reqs) if r.kind == "range" and not r.header_only]
     local = {}
     for vi, vn in enumerate(vns):
         if vn.rank == ctx.rank:
-            local[vn.id] = {reqs[i].base_key(): prq.should_verify(sq, reqs[i], vi, len(vns)) for i in rng}
-    sampled = {}
+            c = ctx.vn_coins(vn.id)
+            local[vn.id] = ({reqs[i].base_key(): prq.should_verify(sq, reqs[i], vi, len(vns), c) for i in rng},
+                            c.seed())
+    sampled, seeds = {}, {}
     for d in ctx.comm.all_gather_object(local):
-        sampled.update(d)
+        for vid, (smp, seed) in d.items():
+            sampled[vid], seeds[vid] = smp, seed
     vn_idxs = {vn.id: [i for i in rng if sampled[vn.id].get(reqs[i].base_key())] for vn in vns}
+    part_coins = {vn.id: Coins(seeds[vn.id]).derive(("slice", k, W)) for vn in vns}
     t0 = time.perf_counter()
-    res = prq.verify_range_many_multi(reqs, vn_idxs, sq, ctx.device, ctx.verifier_cache, part=(k, W))
-    dt = time.perf_counter() - t0
-    mine = {}
-    for vn in vns:
-        timers.record(f"{vn.id}_VerifyRange", dt)  # one shared pass for the co-hosted VNs
-        mine[vn.id] = {reqs[i].base_key(): bool(ok) for i, ok in res.get(vn.id, {}).items()}
-    verdicts = ctx.comm.all_gather_object(mine)
+    res, digests = prq.verify_range_pool_part(reqs, vn_idxs, sq, ctx.device, ctx.verifier_cache, (k, W), part_coins)
+    mine = {vn.id: {reqs[i].base_key(): bool(ok) for i, ok in res.get(vn.id, {}).items()} for vn in vns}
+    mydig = {reqs[i].base_key(): d for i, d in digests.items()}
+    gathered = ctx.comm.all_gather_object((mine, mydig))
     out = {}
+    local_vns = [vn for vn in vns if vn.rank == ctx.rank]
+    if local_vns:
+        trusted = _check_helper_digests(ctx, sq, reqs, vn_idxs, local_vns, gathered)
     for vn in vns:
-        out[vn.id] = {key: (None if not smp else all(v[vn.id].get(key, False) for v in verdicts))
-                      for key, smp in sampled[vn.id].items()}
+        if vn.rank != ctx.rank:
+            continue
+        verdict = {}
+        for key, smp in sampled[vn.id].items():
+            if not smp:
+                verdict[key] = None
+                continue
+            verdict[key] = all(gathered[j][0][vn.id].get(key, False) for j in range(W)
+                               if (key, j) in trusted[vn.id])
+        # slices whose helper digest did not match: this VN checks them itself
+        redo = trusted[vn.id].get("redo", {})
+        if redo:
+            with timers.span("rp.verify.pool_redo"):
+                c = ctx.vn_coins(vn.id)
+                for j, idxs in redo.items():
+                    r2, _ = prq.verify_range_pool_part(reqs, {vn.id: idxs}, sq, ctx.device, ctx.verifier_cache,
+                                                       (j, W), {vn.id: c})
+                    for i, ok in r2[vn.id].items():
+                        key = reqs[i].base_key()
+                        verdict[key] = bool(verdict.get(key)) and bool(ok)
+        out[vn.id] = verdict
+        timers.record(f"{vn.id}_VerifyRange", time.perf_counter() - t0)
+    return out
+
+
+def _check_helper_digests(ctx, sq, reqs, vn_idxs: dict, local_vns: list, gathered: list) -> dict:
+    """For each local VN: the (base_key, part) pairs whose helper-reported
+    slice digest equals the digest of that slice of the VN's own signed
+    payload, and the mismatches to redo ({part: [request index]})."""
+    W = ctx.comm.world
+    need = sorted({i for vn in local_vns for i in vn_idxs[vn.id]})
+    expected: dict = {}
+    empty: set = set()  # (request, part) whose slice is empty: nothing to check there
+    with timers.span("rp.verify.expected_digests"):
+        entries, keys = [], []
+        for i in need:
+            try:
+                lists = prq._range_lists(reqs[i], ctx.device)
+            except Exception:  # noqa: BLE001 -- undecodable: every slice is redone (and fails)
+                continue
+            for j in range(W):
+                sl = prq.slice_lists(lists, sq, (j, W))
+                if not sl:
+                    empty.add((i, j))
+                    continue
+                entries.append(sl)
+                keys.append((i, j))
+        for key, d in zip(keys, prq.lists_digests(entries)):
+            expected[key] = d
+    out = {}
+    for vn in local_vns:
+        ok_pairs, redo = set(), {}
+        for i in vn_idxs[vn.id]:
+            bk = reqs[i].base_key()
+            for j in range(W):
+                if (i, j) in empty or (expected.get((i, j)) is not None
+                                       and gathered[j][1].get(bk) == expected[(i, j)]):
+                    ok_pairs.add((bk, j))
+                else:
+                    redo.setdefault(j, []).append(i)
+        ok_pairs_d = {p_: True for p_ in ok_pairs}
+        ok_pairs_d["redo"] = redo
+        out[vn.id] = ok_pairs_d
     return out
 
 
@@ -171,7 +272,7 @@ def check_requests(ctx, sq, vn, vn_index: int, n_vns: int, requests: list, range
     codes are left pending (``codes`` holds a resolver) so the VN's short
     per-CN checks run while the pooled batch is still on the GPU."""
     return prq.verify_requests(requests, sq, vn.id, vn_index, n_vns, ctx.device, ctx.verifier_cache, range_pooled,
-                               defer=True)
+                               defer=True, coins=ctx.vn_coins(vn.id))
 
 
 def store_verdicts(ctx, sq, vn, requests: list, pending) -> dict:
@@ -204,14 +305,15 @@ def proof_collection(ctx, sq, local_requests: list):
     vns = [ctx.cluster.by_id(si.id) for si in sq.Query.RosterVNs.list]
     pool = use_pool(ctx)
     with timers.timed("ProofFanOut"):
-        reqs = fan_out(ctx, sq, local_requests, all_ranks=pool)
+        reqs = fan_out(ctx, sq, local_requests, pool=pool)
     bitmaps = {}
     with timers.timed("ProofVerification"):
         pooled = _pool_async(ctx, sq, reqs, vns) if pool else None
         local_vns = [vn.id for vn in vns if vn.rank == ctx.rank]
         if len(local_vns) > 1:  # co-hosted VNs: one grouped key-switch MSM for all of them
             with timers.span("verify.keyswitch.multi"):
-                prq.prewarm_keyswitch(reqs, sq, local_vns, ctx.device, ctx.verifier_cache)
+                prq.prewarm_keyswitch(reqs, sq, local_vns, ctx.device, ctx.verifier_cache,
+                                      {v: ctx.vn_coins(v) for v in local_vns})
         pending = {vn.id: check_requests(ctx, sq, vn, idx, len(vns), reqs, pooled)
                    for idx, vn in enumerate(vns) if vn.rank == ctx.rank}
         for vn in vns:

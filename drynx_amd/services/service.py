@@ -85,6 +85,19 @@ class DrynxNode:
         self._end_blocks: dict = {}
 
     # ------------------------------------------------------------------ VN API
+    def vn_coins(self, vn_id: str):
+        """The VN's private coins (crypto/coins.py): its sampling decisions and
+        the random weights of all of its batched checks, never shared with
+        another VN hosted on this rank."""
+        if not hasattr(self, "_vn_coins"):
+            self._vn_coins = {}
+        c = self._vn_coins.get(vn_id)
+        if c is None:
+            from ..crypto.coins import Coins
+
+            c = self._vn_coins[vn_id] = Coins()
+        return c
+
     def register_vn_survey(self, sq: SurveyQuery):
         """HandleSurveyQueryToVN: the VNs learn the survey (expected proof
         counts, DB, chain) before any proof arrives.  A survey that reaches the
@@ -129,9 +142,9 @@ class DrynxNode:
         fresh: dict = {}
         skip = os.environ.get("DRYNX_LEDGER_RANGE", "on") == "off"  # A/B runs only
         for i, req in enumerate(reqs):
-            if req.kind != "range" or req.header_only or req.tensor is None or req._data is not None:
+            if req.header_only or req.tensor is None or req._data is not None:
                 out[i] = req.payload()
-            elif skip:
+            elif skip and req.kind == "range":
                 out[i] = b""
             else:
                 fresh.setdefault(req.digest().hex(), []).append(i)
@@ -250,6 +263,8 @@ class DrynxNode:
         client_future = None
         if on_result is not None and result is not None:
             client_future = self._submit_client(on_result, SurveyResult(sq.SurveyID, result, n_groups, n_out))
+        with timers.span("cn.proofs.wait"):
+            proofs = self._resolve_proofs(proofs)
         if range_future is not None:
             proofs.extend(range_future.result())
             if hasattr(self, "_prove_stream"):
@@ -263,6 +278,45 @@ class DrynxNode:
         out = SurveyResult(sq.SurveyID, result, n_groups, n_out, block, clear)
         if client_future is not None:
             out.client_out = client_future.result()
+        return out
+
+    def defer_proofs(self, fn, *args):
+        """Run ``fn(*args) -> [ProofRequest]`` (proof finishing: transcript
+        digests, responses, packing, envelope signatures -- each needs one
+        device-to-host copy) on the node's CN-proof worker with its own HIP
+        stream, ordered after the work queued so far; the query's critical
+        path does not wait for it.  -> Future (resolved before proof
+        collection)."""
+        import concurrent.futures as cf
+
+        if self.device.type != "cuda":
+            fut = cf.Future()
+            fut.set_result(fn(*args))
+            return fut
+        if not hasattr(self, "_cnp_pool"):
+            self._cnp_pool = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="drynx-cn-proofs")
+            self._cnp_stream = torch.cuda.Stream(self.device)
+        side = self._cnp_stream
+        side.wait_stream(torch.cuda.current_stream(self.device))
+
+        def run():
+            with torch.cuda.stream(side):
+                out = fn(*args)
+            side.synchronize()  # packed payloads are complete before anyone reads them
+            return out
+
+        return self._cnp_pool.submit(run)
+
+    @staticmethod
+    def _resolve_proofs(proofs: list) -> list:
+        out = []
+        for p in proofs:
+            if hasattr(p, "result"):
+                out.extend(p.result())
+            elif isinstance(p, list):
+                out.extend(p)
+            else:
+                out.append(p)
         return out
 
     def _submit_client(self, fn, partial: SurveyResult):
@@ -477,21 +531,16 @@ class DrynxNode:
 
     def get_proofs(self, vn_id: str, survey_id: str) -> dict:
         """HandleGetProofs (service_skipchain.go:240-320): the VN's stored proofs;
-        range bundles in the reference layout network.Marshal(&RangeProofListBytes)."""
-        from ..proofs import range_wire
-
+        range bundles in the reference layout network.Marshal(&RangeProofListBytes),
+        the per-CN proofs in their kyber-encoding export."""
         st = self.store(vn_id)
         st.flush()
-        sq = self.surveys.get(survey_id)
         out = {}
         for kind in prq.VN_ORDER:
             for k, v in st.bucket(f"{survey_id}/{kind}").items():
-                if kind == "range" and v:
-                    try:
-                        v = range_wire.encode_bundle(prq.range_bundle_from_bytes(v, "cpu"))
-                    except Exception:
-                        pass  # not a raw bundle (already reference bytes / malformed): as stored
-                out[k] = v
+                # raw-limb payloads are served in the reference layout; one
+                # that does not decode is an error, not silently raw bytes
+                out[k] = prq.export_reference_bytes(kind, v)
         return out
 
     def get_bitmap(self, vn_id: str, survey_id: str) -> dict:

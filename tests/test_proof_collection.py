@@ -2,7 +2,6 @@
 protocols/proof_collection_protocol_test.go:43-294 — one prover, 3 VNs,
 nbrProofs of each kind, every bitmap entry must be ProofTrue) plus a
 tampered-envelope case."""
-import pytest
 
 from drynx_amd.proofs import requests as prq
 from drynx_amd.protocols import proof_collection as pcp
@@ -42,9 +41,7 @@ def test_all_good_proofs_recorded_true(tmp_path):
     node.close(remove=True)
 
 
-@pytest.mark.parametrize("sig_batch_min", [10**9, 1])
-def test_tampered_payload_is_a_bad_signature(tmp_path, monkeypatch, sig_batch_min):
-    monkeypatch.setattr(prq, "_SIG_BATCH_MIN", sig_batch_min)  # per-envelope and batched signature checks
+def test_tampered_payload_is_a_bad_signature(tmp_path):
     cl, node, sq = _setup(tmp_path)
     data = create_random_good_test_data(sq.RosterServers.aggregate(), sq.ClientPubKey,
                                         sq.Query.IVSigs.InputValidationSigs, 1, entity=cl.cns[0].keypair)

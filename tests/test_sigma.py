@@ -123,10 +123,13 @@ def test_batched_keyswitch_and_obfuscation_verification():
     P = eg.aggregate_keys(X)
     cv, _ = eg.encrypt_ints(eg.pk_table(P), [4, -9, 16])
     q = eg.KeyPair.generate()
-    res = sigma.key_switch_shares_batch(xs, X, cv.K, q.public, True)
-    prs = [pr for _, pr in res]
+    shares, pend = sigma.key_switch_shares_batch(xs, X, cv.K, q.public, True)
+    prs = sigma.finish_keyswitch_proofs(pend)
     assert sigma.key_switch_batch_verification(prs) == [True, True, True]
-    tot = eg.CipherVector.sum([s for s, _ in res])
+    # the packed (raw-limb) payload round trip verifies too, with fresh decoded digests
+    back = [sigma.KeySwitchProof.unpack(pr.pack()) for pr in prs]
+    assert sigma.key_switch_batch_verification(back) == [True, True, True]
+    tot = eg.CipherVector.sum(shares)
     out = eg.CipherVector(tot.K, __import__("drynx_amd").native.g1_add(cv.C, tot.C))
     assert eg.decrypt_ints(q.secret, out) == [4, -9, 16]
     prs[1].za[0, 0] ^= 1  # break one element of one proof
@@ -203,8 +206,63 @@ def test_multi_vn_keyswitch_verification_matches_single():
     for kp in kps:
         share, v = sigma.key_switch_share(kp.secret, cv.K, q.public)
         ks.append(sigma.key_switch_list_proof_creation(kp.secret, kp.public, q.public, cv.K, share, v))
-    assert sigma.key_switch_batch_verification_multi(ks, 1.0, 3) == [[True] * 3] * 3
+    from drynx_amd.crypto.coins import Coins
+
+    assert sigma.key_switch_batch_verification_multi(ks, 1.0, [Coins() for _ in range(3)]) == [[True] * 3] * 3
     ks[2].za = ks[2].za.clone()
     ks[2].za[1, 0] ^= 1
-    assert sigma.key_switch_batch_verification_multi(ks, 1.0, 2) == [[True, True, False]] * 2
-    assert sigma.key_switch_batch_verification_multi([], 1.0, 2) == [[], []]
+    assert sigma.key_switch_batch_verification_multi(ks, 1.0, [Coins(), Coins()]) == [[True, True, False]] * 2
+    assert sigma.key_switch_batch_verification_multi([], 1.0, [Coins(), Coins()]) == [[], []]
+
+
+class _ZeroCoins:
+    """Sabotaged coins: every batch weight is 0 (a verifier with these coins
+    accepts any combination).  Used to show that one VN's coins cannot change
+    another VN's verdicts."""
+
+    def bits(self, n, device, bits=64, odd=False):
+        import torch
+
+        return torch.zeros((n, 8), dtype=torch.int32, device=device)
+
+    def random(self):
+        return 0.0
+
+
+def test_one_vns_coins_cannot_change_anothers_keyswitch_verdict():
+    from drynx_amd.crypto.coins import Coins
+
+    kps = [eg.KeyPair.generate() for _ in range(2)]
+    q = eg.KeyPair.generate()
+    cv, _ = eg.encrypt_ints(eg.pk_table(eg.aggregate_keys([k.public for k in kps])), [1, 2])
+    ks = []
+    for kp in kps:
+        share, v = sigma.key_switch_share(kp.secret, cv.K, q.public)
+        ks.append(sigma.key_switch_list_proof_creation(kp.secret, kp.public, q.public, cv.K, share, v))
+    ks[0].za = ks[0].za.clone()
+    ks[0].za[0, 0] ^= 1  # forged response
+    res = sigma.key_switch_batch_verification_multi(ks, 1.0, [Coins(), _ZeroCoins()])
+    assert res[0] == [False, True]  # the honest VN blames the forged proof, whatever VN 1's coins are
+
+
+def test_packed_payloads_round_trip():
+    """Raw-limb payloads (the intra-cluster format) of the per-CN proofs."""
+    kp, pk, a = _cv([1, 2, 3])
+    b, _ = eg.encrypt_ints(pk, [4, 5, 6])
+    agg = ags.aggregation_list_proof_creation([a, b], a.add(b))
+    back = ags.AggregationProof.unpack(agg.pack())
+    assert ags.aggregation_list_proof_verification(back)
+    assert ags.AggregationProof.from_bytes(back.to_bytes()).result.to_bytes() == agg.result.to_bytes()
+    bad = agg.pack().clone()
+    bad[-1] ^= 1  # corrupt a limb of the claimed sum
+    assert not ags.aggregation_list_proof_verification(ags.AggregationProof.unpack(bad))
+    s = bn.random_scalars(3)
+    ob = sigma.obfuscation_list_proof_creation(a, a.mul_scalars(s), s)
+    ob2 = sigma.ObfuscationProof.unpack(ob.pack())
+    assert sigma.obfuscation_batch_verification([ob2]) == [True]
+    assert sigma.obfuscation_list_proof_verification(sigma.ObfuscationProof.from_bytes(ob2.to_bytes()))
+    import pytest
+
+    with pytest.raises(ValueError):
+        sigma.ObfuscationProof.unpack(ob.pack()[:-1])
+
