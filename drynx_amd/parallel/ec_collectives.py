@@ -98,13 +98,16 @@ def sum_local(cvs: list) -> CipherVector:
 
 def sum_to_root(comm: Comm, local_cvs: list, n_rows: int, root: int = 0,
                 shard_threshold: int = 1 << 16) -> CipherVector | None:
-    """Homomorphically sum CipherVectors held by all ranks onto ``root``."""
+    """Homomorphically sum CipherVectors held by all ranks onto ``root``.
+    Every rank contributes exactly ``n_rows`` rows (zeros if it hosts no
+    contributor), so every receive size is known: no size round."""
     local = CipherVector.sum(local_cvs) if local_cvs else CipherVector.zeros(n_rows, comm.device)
     if comm.world == 1:
         return local
     W = comm.world
     if n_rows < shard_threshold:
-        got = comm.exchange({root: cv_to_rows(local)})
+        known = {s: n_rows * ROW for s in range(W)} if comm.rank == root else {}
+        got = comm.exchange({root: cv_to_rows(local)}, recv_sizes=known)
         if comm.rank != root:
             return None
         parts = [rows_to_cv(got[s]) for s in sorted(got)]
@@ -112,42 +115,50 @@ def sum_to_root(comm: Comm, local_cvs: list, n_rows: int, root: int = 0,
     # reduce-scatter by ownership then gather shards at root
     bounds = [(n_rows * i) // W for i in range(W + 1)]
     rows = cv_to_rows(local)
-    got = comm.exchange({d: rows[bounds[d]: bounds[d + 1]] for d in range(W)})
-    mine = CipherVector.sum([rows_to_cv(got[s]) for s in sorted(got)])
-    got2 = comm.exchange({root: cv_to_rows(mine)})
+    mine_n = bounds[comm.rank + 1] - bounds[comm.rank]
+    got = comm.exchange({d: rows[bounds[d]: bounds[d + 1]] for d in range(W)},
+                        recv_sizes={s: mine_n * ROW for s in range(W)})
+    mine = CipherVector.sum([rows_to_cv(got[s]) for s in sorted(got)]) if mine_n else None
+    known = {s: (bounds[s + 1] - bounds[s]) * ROW for s in range(W)} if comm.rank == root else {}
+    got2 = comm.exchange({root: cv_to_rows(mine)} if mine is not None else {}, recv_sizes=known)
     if comm.rank != root:
         return None
-    return CipherVector.cat([rows_to_cv(got2[s]) for s in range(W)])
+    return CipherVector.cat([rows_to_cv(got2[s]) for s in range(W) if s in got2])
 
 
 def all_reduce_cv(comm: Comm, local_cvs: list, n_rows: int) -> CipherVector:
     """Homomorphic all-reduce: reduce-scatter by row ownership (rank d sums
     rows [b_d, b_{d+1}) of every rank's vector with the K5 kernel), then an
     all-gather of the W reduced shards.  Each rank sends and receives about
-    2 (W-1)/W of the vector over one hop of the xGMI mesh: no ring."""
+    2 (W-1)/W of the vector over one hop of the xGMI mesh: no ring, and no
+    size round (every size follows from ``n_rows``)."""
     local = CipherVector.sum(local_cvs) if local_cvs else CipherVector.zeros(n_rows, comm.device)
     if comm.world == 1:
         return local
     W = comm.world
     bounds = [(n_rows * i) // W for i in range(W + 1)]
     rows = cv_to_rows(local)
-    got = comm.exchange({d: rows[bounds[d]: bounds[d + 1]] for d in range(W) if bounds[d + 1] > bounds[d]})
-    if bounds[comm.rank + 1] > bounds[comm.rank]:
+    mine_n = bounds[comm.rank + 1] - bounds[comm.rank]
+    got = comm.exchange({d: rows[bounds[d]: bounds[d + 1]] for d in range(W) if bounds[d + 1] > bounds[d]},
+                        recv_sizes={s: mine_n * ROW for s in range(W)})
+    known = {s: (bounds[s + 1] - bounds[s]) * ROW for s in range(W)}
+    if mine_n:
         mine = cv_to_rows(CipherVector.sum([rows_to_cv(got[s]) for s in sorted(got)]))
-        got2 = comm.exchange({d: mine for d in range(W)})
+        got2 = comm.exchange({d: mine for d in range(W)}, recv_sizes=known)
     else:
-        got2 = comm.exchange({})
+        got2 = comm.exchange({}, recv_sizes=known)
     return CipherVector.cat([rows_to_cv(got2[s]) for s in range(W) if s in got2])
 
 
 def broadcast_cv(comm: Comm, cv: CipherVector | None, n_rows: int, root: int = 0) -> CipherVector:
     if comm.world == 1:
         return cv
+    known = {root: n_rows * ROW}
     if comm.rank == root:
         rows = cv_to_rows(cv)
-        got = comm.exchange({d: rows for d in range(comm.world)})
+        got = comm.exchange({d: rows for d in range(comm.world)}, recv_sizes=known)
     else:
-        got = comm.exchange({})
+        got = comm.exchange({}, recv_sizes=known)
     return rows_to_cv(got[root])
 
 

@@ -197,6 +197,16 @@ class SigMaterial:
         self._ptab[key] = mode
         return mode
 
+    def table_bytes(self) -> int:
+        """HBM held by this set's prover tables (all devices)."""
+        tot = 0
+        for v in self._ptab.values():
+            if isinstance(v, tuple):
+                tot += sum(t.numel() * t.element_size() for t in v if isinstance(t, torch.Tensor))
+            elif isinstance(v, dict):
+                tot += sum(t.numel() * t.element_size() for t in (v.get("g2"), v.get("gt")) if t is not None)
+        return tot
+
     @property
     def n_distinct(self) -> int:
         if not hasattr(self, "_n_distinct"):

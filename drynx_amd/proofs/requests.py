@@ -390,27 +390,7 @@ class VerifierCache:
 
     def __init__(self):
         self._sig = {}
-        self._early: dict = {}  # SurveyID -> {id(lists): (lists, future, index)}
         self.ks_pre: dict = {}  # (SurveyID, vn_id) -> {request index: bool} (prewarm_keyswitch)
-
-    def put_early(self, survey_id: str, objs: list, fut):
-        if len(self._early) > 8:
-            self._early.clear()
-        self._early[survey_id] = {id(o): (o, fut, i) for i, o in enumerate(objs)}
-
-    def take_early(self, survey_id: str, req):
-        """The speculative content check started for this exact proof object
-        (consumed once: a second VN on the same rank verifies on its own)."""
-        m = self._early.get(survey_id)
-        if not m or req.obj is None:
-            return None
-        e = m.get(id(req.obj))
-        if e is None or e[0] is not req.obj:
-            return None
-        del m[id(req.obj)]
-        if not m:
-            self._early.pop(survey_id, None)
-        return e[1], e[2]
 
     def sigmat(self, sq, device):
         """Keyed by a digest of the signature set, so repeated surveys over the
@@ -822,15 +802,6 @@ def verify_requests(reqs: list, sq, vn_id: str, vn_index: int, n_vns: int, devic
             codes[i] = PROOF_RECEIVED
         else:
             todo.setdefault(req.kind, []).append(i)
-    early = {}
-    for i in todo.get("range", []):
-        e = cache.take_early(sq.SurveyID, reqs[i])
-        if e is not None:
-            early[i] = e
-    if early:
-        todo["range"] = [i for i in todo["range"] if i not in early]
-        if not todo["range"]:
-            del todo["range"]
     range_future = None
     if "range" in todo and len(todo) > 1 and torch.device(device).type == "cuda":
         # the range lists (the heavy pairing work) verify on a worker thread with
@@ -894,10 +865,6 @@ def verify_requests(reqs: list, sq, vn_id: str, vn_index: int, n_vns: int, devic
     if range_future is not None:
         for i, code in range_future.result():
             codes[i] = code
-    if early:
-        with timers.span("rp.verify.early_wait"):
-            for i, (fut, j) in early.items():
-                codes[i] = PROOF_TRUE if fut.result()[j] else PROOF_FALSE
 
     def resolve():
         if pooled_idx:
@@ -910,45 +877,6 @@ def verify_requests(reqs: list, sq, vn_id: str, vn_index: int, n_vns: int, devic
         return codes
 
     return resolve if defer else resolve()
-
-
-class _EarlyReq:
-    """The prover's own lists, checked speculatively (opt-in DRYNX_EARLY_RANGE);
-    the result is only used for the request whose payload packs these lists."""
-    __slots__ = ("obj", "sender_id", "decoded")
-
-    def __init__(self, obj, sender_id):
-        self.obj, self.sender_id, self.decoded = obj, sender_id, obj
-
-
-def start_early_range_verification(items: list, sq, device, cache: VerifierCache, ready_event=None):
-    """Speculative content check of range-proof lists produced on THIS rank for
-    a VN hosted on this rank: queued on the range worker (own HIP stream) as
-    soon as the prover kernels are queued, so the pairing fold overlaps the CN
-    phases (aggregation, key switching) instead of starting after them.  The
-    reference fires proofs asynchronously and VNs verify on arrival
-    (data_collection_protocol.go:278-348, proof_collection_protocol.go:150-200);
-    here arrival is the moment the proof tensors exist.  The envelope
-    signature and sampling are still checked by ``verify_requests``, which
-    takes the result only for the very same proof object.
-    items: [(dp_id, lists)] -> future of {index: bool}."""
-    reqs = [_EarlyReq(lists, dp_id) for dp_id, lists in items]
-    fut = _side_pool().submit(_verify_range_early, reqs, sq, device, cache, ready_event)
-    cache.put_early(sq.SurveyID, [r.obj for r in reqs], fut)
-    return fut
-
-
-def _verify_range_early(reqs, sq, device, cache, ready_event) -> dict:
-    dev = torch.device(device)
-    side = _streams.get(str(dev))
-    if side is None:
-        side = _streams[str(dev)] = torch.cuda.Stream(dev)
-    if ready_event is not None:
-        side.wait_event(ready_event)  # the prover's kernels have produced the lists
-    with torch.cuda.stream(side), timers.span("rp.verify.early"):
-        out = verify_range_many(reqs, list(range(len(reqs))), sq, device, cache)
-    side.synchronize()
-    return out
 
 
 _pool = None

@@ -27,6 +27,7 @@ class DrynxClient:
         self.device = device
         self.decrypt_bound = decrypt_bound
         self._table = None
+        self.last_plaintexts: list = []  # the decrypted aggregate of the last logistic-regression query, per group
 
     @property
     def table(self) -> eg.DecryptionTable:
@@ -70,6 +71,7 @@ class DrynxClient:
 
         def decode_all(partial):
             groups, values = [], []
+            self.last_plaintexts = []
             with timers.timed("Decode"):
                 for g, cv in enumerate(partial.groups()):
                     groups.append(str(g))
@@ -85,6 +87,7 @@ class DrynxClient:
         if op.NameOp == "logistic regression":
             with timers.timed("Decryption"):
                 vals = [int(v) for v in eg.decrypt_auto(self.keypair.secret, cv, self.decrypt_bound).cpu().tolist()]
+            self.last_plaintexts.append(vals)
             from ..models.logistic_regression import decode_logistic_regression_values
 
             return decode_logistic_regression_values(vals, op.LRParameters)

@@ -377,7 +377,20 @@ class DrynxNode:
 
     def _range_proofs(self, sq, dp_results: dict, proofs: list):
         """Synchronous variant (kept for callers/tests that patch it)."""
-        proofs.extend(self._sign_range(sq, self._prove_range(sq, dp_results)))
+        t0 = time.perf_counter()
+        reqs = self._sign_range(sq, self._prove_range(sq, dp_results))
+        self._record_all_proofs(reqs, time.perf_counter() - t0)
+        proofs.extend(reqs)
+
+    @staticmethod
+    def _record_all_proofs(reqs: list, dt: float):
+        """<dp>_AllProofs (data_collection_protocol.go:280): the whole proving
+        of the DP's range proofs, from the start of proving until its signed
+        envelopes exist (device work included: measured after the prover
+        stream has drained).  The DPs of a rank prove as one batch, so they
+        share that span."""
+        for r in reqs:
+            timers.record(f"{r.sender_id}_AllProofs", dt)
 
     def _prove_range(self, sq, dp_results: dict) -> list:
         """Range proofs of every DP hosted here as ONE prover batch per (u, l)
@@ -397,7 +410,6 @@ class DrynxNode:
                 out[dp_id].append(rp.RangeProofList(0, 0, 0, [0] * len(res["cv"]), list(range(len(res["cv"]))),
                                                     res["cv"]))
         if batches:
-            t0 = time.perf_counter()
             sigmat = self.verifier_cache.sigmat(sq, self.device)
             big = dcp_batch_cat(batches)
             lists = rp.create_range_proofs(big, sigmat, P, self.device, sq.RangeProofMode)  # one list per (u, l)
@@ -410,9 +422,6 @@ class DrynxNode:
                     a = cursor.get(gi, 0)
                     out[dp_id].append(rp.rpl_range(lists[gi], a, a + cnt))
                     cursor[gi] = a + cnt
-            dt = time.perf_counter() - t0
-            for dp_id in {o[0] for o in owners}:
-                timers.record(f"{dp_id}_AllProofs", dt)
         return list(out.items())
 
     def _sign_range(self, sq, proved: list) -> list:
@@ -421,26 +430,6 @@ class DrynxNode:
         items = list(proved)
         secrets = [self.cluster.by_id(dp_id).keypair.secret for dp_id, _ in items]
         return prq.new_range_requests(items, sq.SurveyID, secrets, self.device)
-
-    def _early_range_verification(self, sq, proved: list, stream):
-        """When every VN of the survey lives on this rank, start the VN's range
-        content check now, beside the CN phases (``prq.start_early_range_verification``).
-        Opt-in (DRYNX_EARLY_RANGE=1); off under fault injection (proofs are
-        altered after proving).  On one MI355X it is neutral (62 ms per LR query
-        either way): the GPU is already saturated, so the fold started early
-        stretches the CN phases (JustExecution 22 -> 38-43 ms) by what it saves
-        on the VN side (ProofVerification 36 -> 16 ms)."""
-        if os.environ.get("DRYNX_EARLY_RANGE", "0") != "1" or self.fault_plan or not sq.Query.Proofs:
-            return
-        vns = sq.Query.RosterVNs.list if sq.Query.RosterVNs is not None else []
-        if not vns or any(self.cluster.by_id(si.id).rank != self.rank for si in vns):
-            return
-        items = [(dp_id, lists) for dp_id, lists in proved if any(r.has_rp for r in lists)]
-        if not items:
-            return
-        ev = torch.cuda.Event()
-        ev.record(stream)
-        prq.start_early_range_verification(items, sq, self.device, self.verifier_cache, ev)
 
     def _range_proofs_async(self, sq, dp_results: dict):
         import concurrent.futures as cf
@@ -454,9 +443,15 @@ class DrynxNode:
             fut = cf.Future()
             fut.set_result(lst)
             return fut
+        t0 = time.perf_counter()
         if self.device.type != "cuda":
             proved = self._prove_range(sq, dp_results)
-            return self._pool.submit(self._sign_range, sq, proved)
+
+            def sign_host():
+                reqs = self._sign_range(sq, proved)
+                self._record_all_proofs(reqs, time.perf_counter() - t0)
+                return reqs
+            return self._pool.submit(sign_host)
         # proving runs on its own HIP stream so the CN phases (aggregation, key
         # switching: short latency-bound launches) overlap it on the GPU instead
         # of queueing behind ~20 ms of range-proof kernels
@@ -470,12 +465,12 @@ class DrynxNode:
         side.wait_stream(main)  # the DP ciphertexts / randomness are ready
         with torch.cuda.stream(side):
             proved = self._prove_range(sq, dp_results)
-        self._early_range_verification(sq, proved, side)
 
         def sign():
             with torch.cuda.stream(side):
                 reqs = self._sign_range(sq, proved)  # packing + digest kernels follow the proofs on `side`
             side.synchronize()
+            self._record_all_proofs(reqs, time.perf_counter() - t0)
             return reqs
 
         return self._pool.submit(sign)

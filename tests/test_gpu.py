@@ -232,31 +232,6 @@ def test_every_operation_on_gpu(gpu_device, tmp_path, op):
     node.close(remove=True)
 
 
-def test_survey_early_range_gpu(gpu_device, tmp_path, monkeypatch):
-    """The opt-in schedule (per-VN range checks, the VN's check started at
-    proving time) gives the same result and bitmap."""
-    from drynx_amd.proofs import requests as prq
-    from drynx_amd.services.api import DrynxClient
-    from drynx_amd.services.local import local_cluster, make_survey
-
-    monkeypatch.setenv("DRYNX_EARLY_RANGE", "1")
-    monkeypatch.setenv("DRYNX_VN_POOL", "0")
-    started = []
-    orig = prq.start_early_range_verification
-    monkeypatch.setattr(prq, "start_early_range_verification",
-                        lambda *a, **k: started.append(1) or orig(*a, **k))
-    cl, node = local_cluster(2, 3, 1, device=gpu_device, workdir=str(tmp_path))
-    client = DrynxClient(node, device=gpu_device)
-    sq = make_survey(client, cl, "sum", query_min=0, query_max=40, rows=50, proofs=1, ranges=[16, 4],
-                     sig_device=gpu_device)
-    _, vals, res = client.send_survey_query(sq)
-    assert int(vals[0][0]) == sum(v[0][0] for v in res.clear_dp.values())
-    assert started, "early range verification did not run"
-    assert set(res.block.data_block().Proofs.values()) == {1}
-    assert not node.verifier_cache._early  # consumed
-    node.close(remove=True)
-
-
 @pytest.mark.parametrize("variant", ["ni", "inl"])
 def test_two_phase_fold_matches_oracle(gpu_device, variant):
     """Line image + K-item multi-Miller accumulation == product of the
