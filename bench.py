@@ -178,10 +178,12 @@ def main():
     if device.type == "cuda":
         torch.cuda.synchronize()
     t0 = time.perf_counter()
-    blocks, checks = [], []
+    blocks, checks, step_ms = [], [], []
     prof = _torch_profiler(rank)
     for _ in range(args.steps):
+        ts = time.perf_counter()
         res, weights = one_step()
+        step_ms.append(round(1000 * (time.perf_counter() - ts), 1))
         blocks.append(res.block)
         checks.append((weights, res.clear_dp))
     node.flush_stores()  # proof persistence overlaps the next step; the tail is timed too
@@ -238,6 +240,7 @@ def main():
             "setup_s": round(setup_s, 3),
             "first_query_s": round(first_s, 3),
             "prover_table_bytes": int(table_bytes),
+            "step_ms_rank0": step_ms,
             "phase_s": {k: round(v, 4) for k, v in sorted(phase.items()) if not k.startswith("dp") or "AllProofs" in k},
         }
         print(json.dumps(line), flush=True)

@@ -625,9 +625,11 @@ def verify_range_pool_part(reqs: list, vn_idxs: dict, sq, device, cache: Verifie
     coins for this part.  -> ({vn: {index: bool}}, {index: slice digest})"""
     union = sorted({i for idxs in vn_idxs.values() for i in idxs})
     base, parts = _range_parts(reqs, union, sq, device, part)
-    with timers.span("rp.verify.slice_digests"):
-        ok_idx = [i for i in union if base[i]]
-        digests = dict(zip(ok_idx, lists_digests([parts[i] for i in ok_idx])))
+    digests = {}
+    if part[1] > 1:  # only helpers' verdicts need binding to the bytes they checked
+        with timers.span("rp.verify.slice_digests"):
+            ok_idx = [i for i in union if base[i]]
+            digests = dict(zip(ok_idx, lists_digests([parts[i] for i in ok_idx])))
     P = sq.RosterServers.aggregate()
     mode = int(getattr(sq, "RangeProofMode", 0) or 0)
     by_set: dict = {}

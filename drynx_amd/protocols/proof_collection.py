@@ -196,8 +196,8 @@ def _check_helper_digests(ctx, sq, reqs, vn_idxs: dict, local_vns: list, gathere
     """For each local VN: the (base_key, part) pairs whose helper-reported
     slice digest equals the digest of that slice of the VN's own signed
     payload, and the mismatches to redo ({part: [request index]})."""
-    W = ctx.comm.world
-    need = sorted({i for vn in local_vns for i in vn_idxs[vn.id]})
+    W, me = ctx.comm.world, ctx.comm.rank
+    need = sorted({i for vn in local_vns for i in vn_idxs[vn.id]}) if W > 1 else []
     expected: dict = {}
     empty: set = set()  # (request, part) whose slice is empty: nothing to check there
     with timers.span("rp.verify.expected_digests"):
@@ -208,6 +208,8 @@ def _check_helper_digests(ctx, sq, reqs, vn_idxs: dict, local_vns: list, gathere
             except Exception:  # noqa: BLE001 -- undecodable: every slice is redone (and fails)
                 continue
             for j in range(W):
+                if j == me:
+                    continue  # this rank's own part was checked from this very payload
                 sl = prq.slice_lists(lists, sq, (j, W))
                 if not sl:
                     empty.add((i, j))
@@ -222,7 +224,7 @@ def _check_helper_digests(ctx, sq, reqs, vn_idxs: dict, local_vns: list, gathere
         for i in vn_idxs[vn.id]:
             bk = reqs[i].base_key()
             for j in range(W):
-                if (i, j) in empty or (expected.get((i, j)) is not None
+                if j == me or (i, j) in empty or (expected.get((i, j)) is not None
                                        and gathered[j][1].get(bk) == expected[(i, j)]):
                     ok_pairs.add((bk, j))
                 else:

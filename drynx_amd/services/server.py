@@ -64,10 +64,17 @@ def send_env(sock: socket.socket, env: bytes):
     sock.sendall(struct.pack("<Q", len(env)) + env)
 
 
-def recv_env(sock: socket.socket, limit: int = 1 << 34) -> bytes:
+# an unauthenticated peer's first frame (Ping, Join, SurveyQuery, VN calls) is a
+# control message: capped well below anything that could exhaust host memory;
+# only replies the caller asked for (proof maps, blocks) may be larger
+CONTROL_FRAME_LIMIT = 64 << 20
+REPLY_FRAME_LIMIT = 1 << 34
+
+
+def recv_env(sock: socket.socket, limit: int = CONTROL_FRAME_LIMIT) -> bytes:
     (n,) = struct.unpack("<Q", _recv_exact(sock, 8))
     if n > limit:
-        raise ValueError(f"frame of {n} bytes exceeds the limit")
+        raise ValueError(f"frame of {n} bytes exceeds the limit of {limit}")
     return _recv_exact(sock, n)
 
 
@@ -87,7 +94,7 @@ def request(address: str, go_type: str, fields: dict, timeout: float = 3600.0) -
     host, port = address.rsplit(":", 1)
     with socket.create_connection((host, int(port)), timeout=timeout) as s:
         send_env(s, onet.marshal(go_type, fields))
-        name, d = onet.unmarshal(recv_env(s))
+        name, d = onet.unmarshal(recv_env(s, REPLY_FRAME_LIMIT))
     if name == "drynx_amd.Error":
         raise RuntimeError(d["Message"])
     return name, d
@@ -140,6 +147,13 @@ def cluster_from_roster(roles: dict, rank_of: dict, publics: dict, my_addr: str,
 def _join_digest(d: dict) -> bytes:
     body = onet.marshal("drynx_amd.Join", dict(d, Signature=b""))
     return hashlib.sha256(b"drynx_amd/join/v1" + body).digest()
+
+
+def _abort_digest(nonce: bytes, address: str) -> bytes:
+    return hashlib.sha256(b"drynx_amd/join-abort/v1" + nonce + address.encode()).digest()
+
+
+JOIN_TIMEOUT_S = 120.0  # a joined node that never sees the rendezvous complete resets after this
 
 
 def _ack_digest(nonce: bytes, address: str) -> bytes:
@@ -217,6 +231,8 @@ class NodeServer:
             return "drynx_amd.PingReply", {"Address": self.address, "Public": O.g1_to_bytes(self.key.public)}
         if name == "drynx_amd.Join":
             return self._accept_join(d)
+        if name == "drynx_amd.JoinAbort":
+            return self._abort_join(d)
         if name == "drynx_amd.Shutdown" and peer[0] not in ("127.0.0.1", "::1"):
             raise PermissionError("shutdown is accepted from the local host only")
         if name == "libdrynx.SurveyQueryToVN":
@@ -262,9 +278,26 @@ class NodeServer:
             if not sigma.schnorr_verify(root_pub, _join_digest(d), d["Signature"]):
                 raise PermissionError("bad root signature on join")
             self._join_info = d
+            self._join_time = __import__("time").monotonic()
         self._join_event.set()
         return "drynx_amd.JoinReply", {"Signature": sigma.schnorr_sign(self.key.secret,
                                                                        _ack_digest(d["Nonce"], self.address))}
+
+    def _abort_join(self, d: dict) -> tuple[str, dict]:
+        """The root gave up forming the cluster it invited this node to (signed
+        by that root, bound to the join's nonce): forget the join."""
+        with self._join_lock:
+            info = self._join_info
+            if info is None or self.rank is not None:
+                return "drynx_amd.Ack", {"OK": False}
+            if d["Root"] != info["Root"] or bytes(d["Nonce"]) != bytes(info["Nonce"]):
+                raise PermissionError("abort does not match the pending join")
+            root_pub = O.g1_from_bytes(bytes(info["Publics"][0]))
+            if not sigma.schnorr_verify(root_pub, _abort_digest(bytes(d["Nonce"]), self.address), d["Signature"]):
+                raise PermissionError("bad root signature on join abort")
+            self._join_info = None
+            self._join_event.clear()
+        return "drynx_amd.Ack", {"OK": True}
 
     def _form_cluster_as_root(self, sq):
         roles, pubs = roster_of_survey(sq)
@@ -274,6 +307,13 @@ class NodeServer:
         if self.address in pubs and pubs[self.address] != self.key.public:
             raise PermissionError("the query names this node with another key")
         pubs[self.address] = self.key.public
+        # the entry node applies its own group file to the client's roster
+        # before contacting anyone: a client cannot make it form a (lasting)
+        # process group with nodes it does not trust
+        if not self.trusted and not self.trust_any:
+            raise PermissionError("no group file: this node forms no cluster")
+        if self.trusted and not {O.g1_to_bytes(pubs[a]) for a in addrs} <= self.trusted:
+            raise PermissionError("the query's roster contains keys this node does not trust")
         host = self.address.rsplit(":", 1)[0]
         host = "127.0.0.1" if host == "localhost" else host
         s = socket.socket()
@@ -283,16 +323,40 @@ class NodeServer:
         backend = "nccl" if self.device.type == "cuda" else "gloo"
         base = {"World": len(addrs), "Master": f"{host}:{mport}", "Backend": backend, "Addrs": addrs,
                 "Publics": [O.g1_to_bytes(pubs[a]) for a in addrs], "Root": self.address}
-        for r, a in enumerate(addrs[1:], start=1):
-            d = dict(base, Rank=r, Nonce=os.urandom(32))
-            d["Signature"] = sigma.schnorr_sign(self.key.secret, _join_digest(d))
-            name, rep = request(a, "drynx_amd.Join", d, timeout=60)
-            if name != "drynx_amd.JoinReply" or not sigma.schnorr_verify(pubs[a], _ack_digest(d["Nonce"], a),
-                                                                          rep["Signature"]):
-                raise PermissionError(f"node {a} did not prove its roster key")
+        accepted = []
+        try:
+            for r, a in enumerate(addrs[1:], start=1):
+                d = dict(base, Rank=r, Nonce=os.urandom(32))
+                d["Signature"] = sigma.schnorr_sign(self.key.secret, _join_digest(d))
+                name, rep = request(a, "drynx_amd.Join", d, timeout=60)
+                accepted.append((a, d["Nonce"]))
+                if name != "drynx_amd.JoinReply" or not sigma.schnorr_verify(pubs[a], _ack_digest(d["Nonce"], a),
+                                                                              rep["Signature"]):
+                    raise PermissionError(f"node {a} did not prove its roster key")
+        except Exception:
+            # the rendezvous will never complete: release the peers that accepted
+            for a, nonce in accepted:
+                abort = {"Root": self.address, "Nonce": nonce}
+                abort["Signature"] = sigma.schnorr_sign(self.key.secret, _abort_digest(nonce, a))
+                try:
+                    request(a, "drynx_amd.JoinAbort", abort, timeout=10)
+                except Exception:  # noqa: BLE001 -- best effort; the peer's join timeout covers the rest
+                    pass
+            raise
         self._init_group(dict(base, Rank=0), 0)
 
-    def _init_group(self, info, rank):
+    def _init_group_or_reset(self, info):
+        """Join the rendezvous; if it does not complete within JOIN_TIMEOUT_S
+        (the root died or aborted), forget the join so a later one is accepted."""
+        try:
+            self._init_group(info, info["Rank"], timeout=JOIN_TIMEOUT_S)
+        except Exception as e:  # noqa: BLE001 -- the rendezvous failed: back to waiting
+            log.warning(f"cluster rendezvous failed ({type(e).__name__}: {e}); waiting for a new join")
+            with self._join_lock:
+                self._join_info = None
+                self._join_event.clear()
+
+    def _init_group(self, info, rank, timeout: float | None = None):
         import torch.distributed as dist
 
         from ..parallel.comm import DistComm
@@ -300,8 +364,13 @@ class NodeServer:
         host, port = info["Master"].rsplit(":", 1)
         if info["Backend"] == "nccl":
             torch.cuda.set_device(self.device)
-        dist.init_process_group(info["Backend"], init_method=f"tcp://{host}:{port}", rank=rank,
-                                world_size=info["World"])
+        import datetime
+
+        # the rendezvous (not the later collectives) is bounded: a member whose
+        # root never completes it gives up after ``timeout``
+        store = dist.TCPStore(host, int(port), info["World"], rank == 0,
+                              timeout=datetime.timedelta(seconds=timeout or 1800))
+        dist.init_process_group(info["Backend"], store=store, rank=rank, world_size=info["World"])
         self.comm = DistComm(self.device if info["Backend"] == "nccl" else "cpu")
         self.rank = rank
         self.addrs = list(info["Addrs"])
@@ -329,7 +398,10 @@ class NodeServer:
                     self._dispatch_root(name, d, reply)
                     continue
                 if self._join_event.is_set():
-                    self._init_group(self._join_info, self._join_info["Rank"])
+                    with self._join_lock:
+                        info = self._join_info
+                    if info is not None:
+                        self._init_group_or_reset(info)
                 continue
             if self.rank == 0:
                 name, d, reply = self.cmds.get()
@@ -370,6 +442,9 @@ class NodeServer:
             for p in cl.vns:
                 p.bls_public = O.g2_from_bytes(allb[p.id])
             self.node = DrynxNode(cl, self.comm, self.workdir, self.comm.device)
+            # every rank is a separate party here: each VN verifies on its own
+            # rank, never through another party's pooled slice verdicts
+            self.node.pool_policy = "0"
             for sq in self._pending_vn.values():
                 self.node.register_vn_survey(sq)
             self._pending_vn.clear()

@@ -58,6 +58,55 @@ def test_join_requires_group_file_and_root_signature():
         n._accept_join(_join(a, addrs, [a.public, b.public], 1))
 
 
+def test_join_abort_releases_the_node():
+    a, b, evil = KeyPair.generate(), KeyPair.generate(), KeyPair.generate()
+    addrs = ["127.0.0.1:7000", "127.0.0.1:7001"]
+    n = srv.NodeServer(dict(_cfg(addrs[1], b), Trusted=[O.g1_to_bytes(k.public).hex() for k in (a, b)]),
+                       device="cpu")
+    d = _join(a, addrs, [a.public, b.public], 1)
+    n._accept_join(d)
+    forged = {"Root": addrs[0], "Nonce": d["Nonce"],
+              "Signature": sigma.schnorr_sign(evil.secret, srv._abort_digest(d["Nonce"], addrs[1]))}
+    with pytest.raises(PermissionError):  # only the inviting root can abort
+        n._abort_join(forged)
+    ok = {"Root": addrs[0], "Nonce": d["Nonce"],
+          "Signature": sigma.schnorr_sign(a.secret, srv._abort_digest(d["Nonce"], addrs[1]))}
+    assert n._abort_join(ok)[1]["OK"]
+    assert n._join_info is None
+    n._accept_join(_join(a, addrs, [a.public, b.public], 1))  # a new join is accepted again
+
+
+def test_entry_node_checks_the_client_roster():
+    """A client cannot make the entry node form a process group with nodes
+    outside the entry node's own group file."""
+    from drynx_amd.query import Operation, Query, Roster, ServerIdentity, SurveyQuery
+
+    a, b, evil = KeyPair.generate(), KeyPair.generate(), KeyPair.generate()
+    root = srv.NodeServer(dict(_cfg("127.0.0.1:7000", a), Trusted=[O.g1_to_bytes(k.public).hex() for k in (a, b)]),
+                          device="cpu")
+    si = lambda addr, kp: ServerIdentity(f"cn:{addr}", kp.public, addr)  # noqa: E731
+    sq = SurveyQuery(SurveyID="s", RosterServers=Roster([si("127.0.0.1:7000", a), si("127.0.0.1:7666", evil)]),
+                     ClientPubKey=b.public, ServerToDP={}, Query=Query(Operation=Operation()))
+    with pytest.raises(PermissionError):
+        root._form_cluster_as_root(sq)
+    root2 = srv.NodeServer(dict(_cfg("127.0.0.1:7000", a)), device="cpu")  # no group file at all
+    with pytest.raises(PermissionError):
+        root2._form_cluster_as_root(sq)
+
+
+def test_control_frames_are_bounded():
+    import struct
+
+    r, w = socket.socketpair()
+    try:
+        w.sendall(struct.pack("<Q", srv.CONTROL_FRAME_LIMIT + 1))
+        with pytest.raises(ValueError):
+            srv.recv_env(r)
+    finally:
+        r.close()
+        w.close()
+
+
 def _port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
