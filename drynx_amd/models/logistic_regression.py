@@ -57,9 +57,44 @@ def standardise(X: torch.Tensor) -> torch.Tensor:
     return (X - m) / s
 
 
+def standardise_with_train(X_test: torch.Tensor, X_train: torch.Tensor) -> torch.Tensor:
+    """StandardiseWithTrain (logistic_regression.go:943-965): the test matrix
+    standardised with the TRAINING matrix's column means and (population)
+    standard deviations."""
+    m, s = compute_means_sds(X_train.to(torch.float64))
+    return (X_test.to(torch.float64) - m) / s
+
+
 def normalize(X: torch.Tensor) -> torch.Tensor:
-    mn, mx = X.min(0).values, X.max(0).values
-    return (X - mn) / (mx - mn)
+    """Normalize (:985): column-wise min-max scaling with the matrix's own range."""
+    return normalize_with(X, X)
+
+
+def normalize_with(X_test: torch.Tensor, X_train: torch.Tensor) -> torch.Tensor:
+    """NormalizeWith (:990-1012): the test matrix min-max scaled with the
+    training matrix's column minima and maxima."""
+    tr = X_train.to(torch.float64)
+    mn, mx = tr.min(0).values, tr.max(0).values
+    return (X_test.to(torch.float64) - mn) / (mx - mn)
+
+
+def partition_dataset(X: torch.Tensor, y: torch.Tensor, ratio: float, shuffle: bool = False, seed: int = 0):
+    """PartitionDataset (:1389-1420): the first int(n * ratio) records (after an
+    optional seeded shuffle) for training, the rest for testing.  -> (X_train,
+    y_train, X_test, y_test).  The shuffle order comes from numpy's seeded
+    generator, not Go's math/rand (parity of the order itself is unpinned; the
+    split sizes and the no-shuffle split are the reference's)."""
+    import numpy as np
+
+    n = X.shape[0]
+    n_train = int(float(n) * ratio)
+    idx = np.arange(n)
+    if shuffle:
+        idx = np.random.RandomState(seed).permutation(n)
+    tr = torch.as_tensor(idx[:n_train], dtype=torch.long, device=X.device)
+    te = torch.as_tensor(idx[n_train:], dtype=torch.long, device=X.device)
+    return X.index_select(0, tr), y.index_select(0, tr.to(y.device)), X.index_select(0, te), \
+        y.index_select(0, te.to(y.device))
 
 
 def augment(X: torch.Tensor) -> torch.Tensor:
@@ -266,6 +301,20 @@ def _find_minimum_weights_k2(approx, initial_weights, N, lam, step, max_iter, ti
     return min_w.tolist()
 
 
+def find_minimum_weights_with_encryption(encrypted: list, secret: int, initial_weights, N: int, lam: float,
+                                         step: float, max_iter: int, precision: float):
+    """FindMinimumWeightsWithEncryption (:746-766): the client decrypts the
+    encrypted approximation coefficients (one CipherVector per level, with
+    negatives), rescales them by ``precision`` and runs FindMinimumWeights.
+    -> (weights, approx coefficients as lists of floats)."""
+    approx = []
+    for cv in encrypted:
+        vals = eg.decrypt_auto(secret, cv).cpu().to(torch.float64)
+        approx.append(vals / precision)
+    w = find_minimum_weights(approx, initial_weights, N, lam, step, max_iter)
+    return w, [a.tolist() for a in approx]
+
+
 def decode_logistic_regression_values(vals, params: LogisticRegressionParameters) -> list:
     with timers.timed("GradientDescent", sync=False):
         approx = [a / params.PrecisionApproxCoefficients for a in unpack(vals, params.NbrFeatures, params.K)]
@@ -281,6 +330,55 @@ def predict(X: torch.Tensor, weights, means=None, sds=None) -> torch.Tensor:
     Xa = augment(X)
     w = torch.as_tensor(weights, dtype=torch.float64, device=X.device)
     return torch.sigmoid(Xa @ w)
+
+
+def predict_in_clear(x, weights) -> float:
+    """PredictInClear (:808-817): sigmoid(w0 + sum_i w_{i+1} x_i) for one record."""
+    s_ = sum(float(w) * float(v) for w, v in zip(list(weights)[1:], x))
+    return 1.0 / (1.0 + math.exp(-float(weights[0]) - s_))
+
+
+def predict_encrypted(encrypted_data: eg.CipherVector, weights, secret: int, precision_weights: float,
+                      precision_data: float) -> float:
+    """Predict (:820-852) for ONE encrypted record (Enc(round(x_i *
+    precision_data)) per feature): the weighted sum with integer weights
+    round(w_{i+1} * precision_weights) is evaluated homomorphically (the
+    reference adds the ciphertext |w| times; here one scalar multiplication
+    per feature, negatives as r - |w|, and one K5 reduction), decrypted with
+    negatives, rescaled, and the sigmoid taken with the clear bias w0."""
+    from ..crypto import bn254 as bn
+
+    wi = [int(round_precision(torch.tensor([float(w)], dtype=torch.float64), precision_weights)[0])
+          for w in list(weights)[1:]]
+    n = len(encrypted_data)
+    if n != len(wi):
+        raise ValueError(f"{n} encrypted features for {len(wi)} weights")
+    dev = encrypted_data.device
+    sc = bn.scalars_tensor([w % bn.R for w in wi], dev)
+    prod = encrypted_data.mul_scalars(sc)
+    tot = eg.CipherVector(nt.g1_sum(prod.K.view(n, 1, 24)), nt.g1_sum(prod.C.view(n, 1, 24)))
+    bound = sum(abs(w) for w in wi) * int(precision_data * 1e3 + 1) + 1
+    dot = int(eg.decrypt_auto(secret, tot, bound=min(bound, 1 << 20)).cpu()[0])
+    val = dot / (precision_weights * precision_data)
+    return 1.0 / (1.0 + math.exp(-float(weights[0]) - val))
+
+
+def logistic_regression_cost(weights, X: torch.Tensor, y: torch.Tensor, N: int, lam: float) -> float:
+    """LogisticRegressionCost (:769-794) on clear data, including the
+    reference's regulariser precedence (lambda / 2 * N, not lambda / (2N);
+    a test-only helper)."""
+    w = torch.as_tensor(weights, dtype=torch.float64)
+    s1 = X.to(torch.float64) @ w
+    cost = float((torch.log1p(torch.exp(s1)) - y.to(torch.float64) * s1).sum())
+    return cost + float((w * w).sum()) * (lam / 2 * float(N))
+
+
+def logistic_regression_gradient(weights, X: torch.Tensor, y: torch.Tensor, N: int, lam: float) -> list:
+    """LogisticRegressionGradient (:797-817) on clear data."""
+    w = torch.as_tensor(weights, dtype=torch.float64)
+    X = X.to(torch.float64)
+    g = X.T @ (torch.sigmoid(X @ w) - y.to(torch.float64)) + (lam / float(N)) * w
+    return g.tolist()
 
 
 def predict_homomorphic(X: torch.Tensor, weights, pk: eg.PublicKeyTable, secret: int, precision: float = 1e2):

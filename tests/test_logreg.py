@@ -141,3 +141,48 @@ def test_cartesian_coefficients_expand_distinct(y):
         flat = cart[j - 1].tolist()
         for pos, idx in enumerate(itertools.product(range(n), repeat=j)):
             assert abs(flat[pos]) == pytest.approx(abs(lookup[tuple(sorted(idx))]))
+
+
+def test_lr_evaluation_helpers():
+    """FindMinimumWeightsWithEncryption, Predict on an encrypted record,
+    StandardiseWithTrain / NormalizeWith and PartitionDataset
+    (lib/encoding/logistic_regression.go:746, :820, :943-1012, :1389)."""
+    import torch
+
+    from drynx_amd.crypto import elgamal as eg
+    from drynx_amd.models import logistic_regression as lr
+
+    g = torch.Generator().manual_seed(5)
+    X = torch.rand((60, 3), generator=g, dtype=torch.float64) * 4
+    y = (X[:, 0] + 0.5 * X[:, 1] > 2.5).to(torch.int64)
+    Xtr, ytr, Xte, yte = lr.partition_dataset(X, y, 0.75, shuffle=False)
+    assert Xtr.shape[0] == 45 and Xte.shape[0] == 15 and torch.equal(Xtr, X[:45]) and torch.equal(yte, y[45:])
+    a = lr.partition_dataset(X, y, 0.8, shuffle=True, seed=7)
+    b = lr.partition_dataset(X, y, 0.8, shuffle=True, seed=7)
+    assert torch.equal(a[0], b[0]) and a[0].shape[0] == 48 and not torch.equal(a[0], X[:48])
+    st = lr.standardise_with_train(Xte, Xtr)
+    m, s = lr.compute_means_sds(Xtr)
+    assert torch.allclose(st, (Xte - m) / s)
+    nw = lr.normalize_with(Xte, Xtr)
+    assert torch.allclose(nw, (Xte - Xtr.min(0).values) / (Xtr.max(0).values - Xtr.min(0).values))
+    assert torch.allclose(lr.normalize(Xtr).min(0).values, torch.zeros(3, dtype=torch.float64))
+    # training on encrypted coefficients == training on the clear ones
+    from drynx_amd.query import LogisticRegressionParameters
+
+    p = LogisticRegressionParameters(NbrRecords=45, NbrFeatures=3, Lambda=1.0, Step=0.1, MaxIterations=50,
+                                     InitialWeights=[0.1] * 4, K=2, PrecisionApproxCoefficients=100.0)
+    vals = lr.encode_coefficients_int(Xtr, ytr, p)
+    kp = eg.KeyPair.generate()
+    pk = eg.pk_table(kp.public)
+    lv1, lv2 = vals[:4], vals[4:]
+    enc = [eg.encrypt_ints(pk, lv1)[0], eg.encrypt_ints(pk, lv2)[0]]
+    w, approx = lr.find_minimum_weights_with_encryption(enc, kp.secret, p.InitialWeights, 45, 1.0, 0.1, 50, 100.0)
+    assert w == lr.decode_logistic_regression_values(vals.tolist(), p)
+    assert approx[0] == [v / 100.0 for v in lv1.tolist()]
+    # Predict on one encrypted record vs PredictInClear
+    x = [1.5, 0.25, 3.0]
+    cv, _ = eg.encrypt_ints(pk, [round(v * 100) for v in x])
+    pe = lr.predict_encrypted(cv, w, kp.secret, 100.0, 100.0)
+    assert abs(pe - lr.predict_in_clear(x, w)) < 1e-2
+    c = lr.logistic_regression_cost(w, lr.augment(Xtr), ytr, 45, 1.0)
+    assert c > 0 and len(lr.logistic_regression_gradient(w, lr.augment(Xtr), ytr, 45, 1.0)) == 4
