@@ -16,24 +16,52 @@ int dx_fp_from_mont(int on_gpu, void *stream, const uint32_t *in, uint32_t *out,
   return run(on_gpu, stream, n, op, false, "fp_from_mont");
 }
 
+}  // extern "C"
+
 // Fr arithmetic on canonical scalars. op: 0 add, 1 sub, 2 mul, 3 neg(a), 4 inv(a), 5 reduce(a)
-int dx_fr_arith(int on_gpu, void *stream, int opc, const uint32_t *a, const uint32_t *b, uint32_t *out, int64_t n,
-                int b_bcast) {
+
+namespace {
+// One kernel per operation (the op code is a template parameter): a switch
+// over all five ops compiled the binary-GCD inversion into every launch of
+// the hot add / mul paths (VGPR pressure, scratch).  The product of two
+// canonical scalars is one Montgomery multiplication with one operand in
+// Montgomery form: x * (yR) * R^-1 = x y.
+template <int OPC>
+int fr_arith_t(int on_gpu, void *stream, const uint32_t *a, const uint32_t *b, uint32_t *out, int64_t n,
+               int b_bcast) {
   auto op = [=] __host__ __device__(int64_t i) {
     Fr x = reduce_256<FrParams>(a + 8 * i);
-    Fr y = b ? reduce_256<FrParams>(b + 8 * (b_bcast ? 0 : i)) : Fr::zero();
     Fr r;
-    switch (opc) {
-      case 0: r = fadd(x, y); break;
-      case 1: r = fsub(x, y); break;
-      case 2: r = from_mont(fmul(to_mont(x), to_mont(y))); break;
-      case 3: r = fneg(x); break;
-      case 4: r = from_mont(finv(to_mont(x))); break;
-      default: r = x; break;
+    if constexpr (OPC == 0 || OPC == 1 || OPC == 2) {
+      Fr y = b ? reduce_256<FrParams>(b + 8 * (b_bcast ? 0 : i)) : Fr::zero();
+      if constexpr (OPC == 0) r = fadd(x, y);
+      else if constexpr (OPC == 1) r = fsub(x, y);
+      else r = fmul(x, to_mont(y));
+    } else if constexpr (OPC == 3) {
+      r = fneg(x);
+    } else if constexpr (OPC == 4) {
+      r = from_mont(finv(to_mont(x)));
+    } else {
+      r = x;
     }
     at<Fr>(out, i) = r;
   };
   return run(on_gpu, stream, n, op, false, "fr_arith");
+}
+}  // namespace
+
+extern "C" {
+
+int dx_fr_arith(int on_gpu, void *stream, int opc, const uint32_t *a, const uint32_t *b, uint32_t *out, int64_t n,
+                int b_bcast) {
+  switch (opc) {
+    case 0: return fr_arith_t<0>(on_gpu, stream, a, b, out, n, b_bcast);
+    case 1: return fr_arith_t<1>(on_gpu, stream, a, b, out, n, b_bcast);
+    case 2: return fr_arith_t<2>(on_gpu, stream, a, b, out, n, b_bcast);
+    case 3: return fr_arith_t<3>(on_gpu, stream, a, b, out, n, b_bcast);
+    case 4: return fr_arith_t<4>(on_gpu, stream, a, b, out, n, b_bcast);
+    default: return fr_arith_t<5>(on_gpu, stream, a, b, out, n, b_bcast);
+  }
 }
 
 // Chunked Fr dot products / sums of canonical scalars, per group of m rows:

@@ -147,8 +147,13 @@ class SigMaterial:
 
     def y_tables(self, device):
         """(comb tables [n_distinct*8192, 16], slot per y index) or None when
-        there are too many distinct keys (0.5 MiB of HBM per table, <= 256)."""
-        if not self.y_distinct or len(self.y_distinct) > 256:
+        the distinct keys' tables exceed the budget (0.5 MiB each: on a GPU up
+        to ``DRYNX_Y_TABLES_MB``, default 16 GiB of HBM -- the reference's
+        random per-CN, per-column keys of a SPECTF query are 6210 keys, 3 GiB
+        -- so the verifier's c * y_i are fixed-base; 256 keys on the host)."""
+        dev = torch.device(device)
+        cap = (int(os.environ.get("DRYNX_Y_TABLES_MB", 16384)) << 20) // (8192 * 64) if dev.type == "cuda" else 256
+        if not self.y_distinct or len(self.y_distinct) > cap:
             return None
         key = str(torch.device(device))
         if key not in self._ytab:
@@ -198,9 +203,9 @@ class SigMaterial:
         return mode
 
     def table_bytes(self) -> int:
-        """HBM held by this set's prover tables (all devices)."""
+        """HBM held by this set's prover and verifier (c * y_i) tables."""
         tot = 0
-        for v in self._ptab.values():
+        for v in list(self._ptab.values()) + list(self._ytab.values()):
             if isinstance(v, tuple):
                 tot += sum(t.numel() * t.element_size() for t in v if isinstance(t, torch.Tensor))
             elif isinstance(v, dict):
