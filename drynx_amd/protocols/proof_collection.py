@@ -23,6 +23,8 @@ import time
 import torch
 
 from ..ledger import skipchain as skc
+from ..parallel.netem import CT_BYTES, POINT_BYTES, SCALAR_BYTES, SIG_BYTES, range_proof_bytes
+from .data_collection import all_possible_groups as dcp_groups
 from ..parallel.comm import bytes_to_obj, obj_to_bytes
 from ..crypto.coins import Coins
 from ..proofs import requests as prq
@@ -37,6 +39,28 @@ def expected_counts(sq) -> dict:
     """QueryToProofsNbrs reordered to the VN order (service_skipchain.go:57-63)."""
     q = query_to_proofs_nbrs(sq)
     return dict(zip(prq.QUERY_ORDER, q))
+
+
+def _net_proofs(ctx, sq, reqs: list, vns: list):
+    """Every proof envelope from its prover to every VN (one hop, the
+    reference wire sizes of SURVEY 2.4)."""
+    n_rows = len(dcp_groups(sq.Query.DPDataGen.GroupByValues)) * sq.Query.Operation.NbrOutput
+    S = len(sq.RosterServers.list)
+    sizes = {}
+    for r in reqs:
+        if r.kind == "range":
+            rg = sq.Query.Ranges or []
+            nb = sum(range_proof_bytes(int(x[0]), int(x[1]), S) for x in rg) * len(dcp_groups(sq.Query.DPDataGen.GroupByValues))
+        elif r.kind == "aggregation":
+            nb = (len((sq.ServerToDP or {}).get(r.sender_id) or []) + 1) * n_rows * CT_BYTES
+        elif r.kind == "keyswitch":
+            nb = n_rows * (POINT_BYTES + CT_BYTES + 2 * POINT_BYTES + SCALAR_BYTES) + 4 * POINT_BYTES
+        elif r.kind == "obfuscation":
+            nb = n_rows * (3 * CT_BYTES + SCALAR_BYTES)
+        else:
+            nb = int(sq.Query.DiffP.NoiseListSize) * 3 * CT_BYTES
+        sizes[r.base_key()] = (r.sender_id, nb + SIG_BYTES)
+    ctx.net.step("proofs_to_vns", [(src, v.id, nb) for src, nb in sizes.values() for v in vns], hops=1)
 
 
 def use_pool(ctx) -> bool:
@@ -308,6 +332,8 @@ def proof_collection(ctx, sq, local_requests: list):
     pool = use_pool(ctx)
     with timers.timed("ProofFanOut"):
         reqs = fan_out(ctx, sq, local_requests, pool=pool)
+    if getattr(ctx, "net", None) is not None:
+        _net_proofs(ctx, sq, reqs, vns)
     bitmaps = {}
     with timers.timed("ProofVerification"):
         pooled = _pool_async(ctx, sq, reqs, vns) if pool else None
@@ -376,5 +402,12 @@ def proof_collection(ctx, sq, local_requests: list):
             st.update_async("mapping", sq.SurveyID, block.Hash.encode())
     ctx.last_block = block
     timers.end_timer(t)
+    if getattr(ctx, "net", None) is not None:
+        ids = [v.id for v in vns]
+        bsz = len(block.to_bytes())
+        ctx.net.step("bitmaps", [(i, ids[0], 64 * len(allbm.get(i, {})) + 64) for i in ids[1:]], hops=1)
+        ctx.net.step("skipchain", [(ids[0], i, bsz) for i in ids[1:]] + [(i, ids[0], SIG_BYTES) for i in ids[1:]],
+                     hops=2)
+        ctx.net.step("end_verification", [(ids[0], "client", bsz)], hops=1)
     ctx.end_verification(sq.SurveyID, block)  # EndVerificationChannel <- block (service_skipchain.go:158)
     return block

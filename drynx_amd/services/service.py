@@ -31,6 +31,7 @@ from ..ops.encoding import cat_proof_batches as dcp_batch_cat
 from ..ledger.store import Store
 from ..parallel.comm import Comm, LocalComm
 from ..parallel.ec_collectives import KeyIndex
+from ..parallel.netem import CT_BYTES, POINT_BYTES, tree_depth, tree_edges
 from ..parallel.topology import Cluster
 from ..proofs import range_proof as rp
 from ..proofs import requests as prq
@@ -78,6 +79,9 @@ class DrynxNode:
         self.last_block: SkipBlock | None = None
         self.surveys: dict = {}
         self.fault_plan = FaultPlan.from_env()  # misbehaving parties (tests / simulations)
+        from ..parallel.netem import NetEmulator
+
+        self.net = NetEmulator.from_env()  # emulated party-to-party links (simulation Bandwidth / Delay)
         # VN side of the API (service_skipchain.go:31-166): surveys announced to
         # the VNs (SurveyQueryToVN) and the EndVerificationChannel per survey
         self.vn_surveys: dict = {}
@@ -239,7 +243,13 @@ class DrynxNode:
         n_groups = len(dcp.all_possible_groups(q.DPDataGen.GroupByValues))
         n_out = q.Operation.NbrOutput
         t_exec = timers.start_timer("JustExecution")
+        if self.net is not None:
+            self._net_dissemination(sq)
         noise = cnp.dro_phase(self, sq, proofs)
+        if self.net is not None and noise is not None:
+            cns = [si.id for si in sq.RosterServers.list]
+            nb = int(sq.Query.DiffP.NoiseListSize) * 3 * CT_BYTES
+            self.net.step("dro", [(a, b, nb) for a, b in zip(cns, cns[1:] + cns[:1])], hops=len(cns))
         cn_sums, cn_inputs, dp_results = dcp.data_collection(self, sq)
         # range proofs start right after encoding (the reference fires them
         # asynchronously, data_collection_protocol.go:278-348): proving is queued
@@ -250,10 +260,27 @@ class DrynxNode:
             n_out = len(next(iter(dp_results.values()))["cv"]) // n_groups
         n_out = max(self.comm.all_gather_object(n_out if dp_results else 0)) or n_out
         n_rows = n_groups * n_out
+        net = self.net
+        cn_ids = [si.id for si in sq.RosterServers.list]
+        if net is not None:
+            net.step("data_collection", [(si.id, cn, n_rows * CT_BYTES) for cn, dps in (sq.ServerToDP or {}).items()
+                                         for si in (dps or [])], hops=2)
         agg = cnp.collective_aggregation(self, sq, cn_sums, cn_inputs, n_rows, proofs)
+        if net is not None:
+            net.step("aggregation", [(c, p, n_rows * CT_BYTES) for c, p in tree_edges(cn_ids)],
+                     hops=2 * tree_depth(len(cn_ids)))
         if q.Obfuscation:
             agg = cnp.obfuscation(self, sq, agg, n_rows, proofs)
+            if net is not None:
+                e = tree_edges(cn_ids)
+                net.step("obfuscation", [(p, c, n_rows * CT_BYTES) for c, p in e] +
+                         [(c, p, n_rows * CT_BYTES) for c, p in e], hops=2 * tree_depth(len(cn_ids)))
         result = cnp.key_switching(self, sq, agg, n_groups, n_out, noise, proofs)
+        if net is not None:
+            e = tree_edges(cn_ids)
+            net.step("key_switching", [(p, c, n_rows * POINT_BYTES) for c, p in e] +
+                     [(c, p, n_rows * CT_BYTES) for c, p in e], hops=2 * tree_depth(len(cn_ids)))
+            net.step("result", [(cn_ids[0], "client", n_rows * CT_BYTES)], hops=1)
         if q.CuttingFactor and result is not None:
             # CN truncates the replicated response (service.go:760-761)
             per = n_out // q.CuttingFactor
@@ -279,6 +306,17 @@ class DrynxNode:
         if client_future is not None:
             out.client_out = client_future.result()
         return out
+
+    def _net_dissemination(self, sq):
+        """Client -> root CN -> other CNs -> DPs (service.go:263-339): three
+        sequential hops carrying the query and its input-validation keys."""
+        sigs = sq.Query.IVSigs.InputValidationSigs or []
+        size = 1024 + sum(len(x.Public) + len(x.Signature) for row in sigs for x in row)
+        cns = [si.id for si in sq.RosterServers.list]
+        self.net.step("query_client", [("client", cns[0], size)], hops=1)
+        self.net.step("query_cns", [(cns[0], c, size) for c in cns[1:]], hops=1)
+        self.net.step("query_dps", [(cn, si.id, size) for cn, dps in (sq.ServerToDP or {}).items()
+                                    for si in (dps or [])], hops=1)
 
     def defer_proofs(self, fn, *args):
         """Run ``fn(*args) -> [ProofRequest]`` (proof finishing: transcript

@@ -79,12 +79,19 @@ def ranges_for(code: int, n_out: int):
     raise ValueError(f"unknown Ranges preset {code}")
 
 
-def run_row(glob: dict, row: dict, comm, device, workdir):
+def run_row(glob: dict, row: dict, comm, device, workdir, netem: str = "sleep"):
     n_cn, n_vn, n_dp = int(row["NbrServers"]), int(row.get("NbrVNs", 0)), int(row["NbrDPs"])
     proofs = int(row.get("Proofs", 0))
     if proofs and n_vn == 0:
         n_vn = 1
     cl, node = local_cluster(n_cn, n_dp, max(n_vn, 1), comm=comm, device=device, workdir=workdir)
+    # the runfile's emulated links (drynx.toml:6-7): per-row Bandwidth / Delay
+    # columns override the global keys (the reference's Bandwith sheet sweeps them)
+    bw, dl = row.get("Bandwidth", glob.get("Bandwidth")), row.get("Delay", glob.get("Delay"))
+    if netem != "off" and bw and dl is not None:
+        from ..parallel.netem import NetEmulator
+
+        node.net = NetEmulator(float(bw), float(dl), netem)
     # NbrDPsPerServer: the first CNs get that many DPs each (drynx_simul.go:317-333)
     per = int(row.get("NbrDPsPerServer", 0)) or max(1, n_dp // n_cn)
     op_name = str(row["OperationName"])
@@ -145,6 +152,9 @@ def main(argv=None):
     ap.add_argument("runfile")
     ap.add_argument("--csv", default=None)
     ap.add_argument("--device", default=None)
+    ap.add_argument("--netem", default="sleep", choices=["sleep", "account", "off"],
+                    help="apply the runfile's Bandwidth/Delay: wait where messages flow (sleep), only "
+                         "record them (account), or ignore them (off)")
     a = ap.parse_args(argv)
     init_distributed()
     comm = make_comm(a.device)
@@ -153,12 +163,16 @@ def main(argv=None):
     for i, row in enumerate(rows):
         timers.reset()
         with tempfile.TemporaryDirectory() as wd:
-            res = run_row(glob, row, comm, comm.device, wd)
+            res = run_row(glob, row, comm, comm.device, wd, a.netem)
         summ = timers.summary()
         if comm.rank == 0:
+            net = summ.get("NetworkEmulated", {}).get("sum", 0.0) / max(1, int(glob.get("Rounds", 1)))
             log.info(f"row {i}: {row.get('OperationName')} -> {res[-1] if res else None} "
-                     f"(Simulation {summ['Simulation']['mean']:.3f}s)")
-            out_rows.append({"row": i, **{k: v["mean"] for k, v in summ.items()}})
+                     f"(Simulation {summ['Simulation']['mean']:.3f}s, of which emulated network {net:.3f}s)")
+            rounds = max(1, int(glob.get("Rounds", 1)))
+            # timers recorded once per run: the mean; network steps: their total per run
+            out_rows.append({"row": i, **{k: (v["sum"] / rounds if k.startswith(("net_", "NetworkEmulated"))
+                                              else v["mean"]) for k, v in summ.items()}})
     if comm.rank == 0 and a.csv:
         keys = sorted({k for r in out_rows for k in r})
         with open(a.csv, "w", newline="") as f:

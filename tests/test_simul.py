@@ -22,3 +22,32 @@ def test_simulation_run_writes_timers(tmp_path):
     assert simul.main([str(rf), "--csv", str(out), "--device", "cpu"]) == 0
     t = simul.parse_time_data(str(out), ["Simulation", "JustExecution", "VerifyRange"])
     assert t["Simulation"][0] > 0 and any("VerifyRange" in k for k in t)
+
+
+def test_network_emulation_model():
+    from drynx_amd.parallel.netem import NetEmulator, range_proof_bytes, tree_depth, tree_edges
+
+    net = NetEmulator(100, 20, "account")  # 100 Mbps = 12.5 MB/s, 20 ms
+    # two parallel 1.25 MB messages into one receiver: its interface carries 2.5 MB
+    assert abs(net.step_time([("a", "c", 1_250_000), ("b", "c", 1_250_000)], hops=2) - (0.04 + 0.2)) < 1e-9
+    assert net.step_time([("a", "a", 10**9)]) == 0.02  # in-party traffic is free
+    assert tree_depth(1) == 0 and tree_depth(3) == 1 and tree_depth(4) == 2
+    assert tree_edges(["r", "x", "y"]) == [("x", "r"), ("y", "r")]
+    assert range_proof_bytes(16, 16, 3) == 256 + 512 + 544 * 48 and range_proof_bytes(0, 0, 3) == 128
+
+
+def test_simulation_applies_runfile_links(tmp_path):
+    """Bandwidth / Delay columns (simul/runfiles/drynx.toml:6-7) are charged per
+    protocol step: a longer delay adds at least hops * delta to the query."""
+    rf = tmp_path / "r.toml"
+    rf.write_text('Rounds = 1\nGroupByValues = [1]\n\nNbrServers, NbrVNs, NbrDPs, NbrDPsPerServer, Proofs, Ranges, '
+                  'Obfuscation, OperationName, NbrInput, NbrOutput, DPRows, MinData, MaxData, ThresholdGeneral, '
+                  'ThresholdOther, CuttingFactor, Bandwidth, Delay\n'
+                  '2, 1, 2, 1, 1, 1, false, "sum", 1, 1, 2, 0, 1, 1.0, 1.0, 0, 100, 1\n'
+                  '2, 1, 2, 1, 1, 1, false, "sum", 1, 1, 2, 0, 1, 1.0, 1.0, 0, 100, 11\n')
+    out = tmp_path / "t.csv"
+    assert simul.main([str(rf), "--csv", str(out), "--device", "cpu", "--netem", "account"]) == 0
+    t = simul.parse_time_data(str(out), ["NetworkEmulated", "net_"])
+    n = t["NetworkEmulated"]
+    assert len(n) == 2 and n[1] - n[0] >= 10 * 0.010 - 1e-9  # >= 10 hops on the query + verification path
+    assert any(k.startswith("net_proofs_to_vns") for k in t)
