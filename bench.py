@@ -61,12 +61,14 @@ import torch.distributed as dist  # noqa: E402
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from drynx_amd.parallel.comm import init_distributed, make_comm  # noqa: E402
-from drynx_amd.query import LogisticRegressionParameters, new_survey_id  # noqa: E402
+from drynx_amd.query import LogisticRegressionParameters, QueryDiffP, new_survey_id  # noqa: E402
 from drynx_amd.services.api import DrynxClient  # noqa: E402
 from drynx_amd.services.local import local_cluster, make_survey  # noqa: E402
 from drynx_amd.utils import timers  # noqa: E402
 
 REFERENCE_LR_SPECTF_S = 196.77  # AllResults.xlsx LogRegr row 7
+REFERENCE_DIFFPRI_10K_S = 82.0  # AllResults.xlsx DiifPri row 6: query with a 10k-entry noise list
+DRO_LAP_SCALE, DRO_LIMIT = 2.0, 50.0  # noise list parameters of the config-4 line
 REFERENCE_VERIFICATIONS_PER_S = 10 * 2070 * 3 / REFERENCE_LR_SPECTF_S  # 10 DPs x 2070 proofs x 3 VNs
 # AllOps totals (AllResults.xlsx rows 6, 7, 16) and this bench's shape for them
 QUERY_CONFIGS = {
@@ -96,14 +98,19 @@ def parse():
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--range-mode", type=int, default=0,
                     help="SurveyQuery.RangeProofMode: 0 reference semantics, 1 recomputed challenge + V in G2")
-    ap.add_argument("--query", default="lr", choices=["lr", *QUERY_CONFIGS],
-                    help="lr = the headline; mean/variance/lin_reg = BASELINE.json configs 2 and 3")
+    ap.add_argument("--query", default="lr", choices=["lr", "lr_dro", *QUERY_CONFIGS],
+                    help="lr = the headline; lr_dro = BASELINE.json config 4; mean/variance/lin_reg = configs 2 and 3")
+    ap.add_argument("--dro", type=int, default=None,
+                    help="differential-privacy noise list size (DRO shuffle by every CN, with shuffle proofs); "
+                         "--query lr_dro sets 10000 (the reference's DiffPri 10k row)")
     return ap.parse_args()
 
 
 def main():
     args = parse()
-    if args.query != "lr":
+    if args.query == "lr_dro" and args.dro is None:
+        args.dro = 10_000
+    if args.query not in ("lr", "lr_dro"):
         return main_query(args)
     init_distributed()
     comm = make_comm(args.device)
@@ -145,9 +152,16 @@ def main():
     client = DrynxClient(node, device=device) if rank == 0 else None
     template = None
     t_setup = time.perf_counter()
+    diffp = None
+    if args.dro:
+        # config 4: the DP noise list (discretised Laplace, unlynx GenerateNoiseValuesScale) is
+        # encrypted by the root CN, shuffled + re-randomised by every CN in turn with a proof of
+        # shuffle (DRO, service.go:619-665), and added to the aggregate before key switching
+        diffp = QueryDiffP(LapMean=0.0, LapScale=DRO_LAP_SCALE, NoiseListSize=args.dro, Quanta=1.0, Scale=1.0,
+                           Limit=DRO_LIMIT)
     if rank == 0:  # CN input-validation keys are set up once, before the queries (as in the reference simulation)
         template = make_survey(client, cl, "logistic regression", proofs=1, ranges=[args.u, args.l, offset],
-                               lr_params=lp, thresholds=[1.0, 1.0, 1.0, 0.0, 1.0], verification_sharding=0,
+                               lr_params=lp, thresholds=[1.0, 1.0, 1.0, 0.0, 1.0], verification_sharding=0, diffp=diffp,
                                sig_device=device, deterministic_sigs=args.deterministic_sigs,
                                range_proof_mode=args.range_mode)
 
@@ -199,13 +213,25 @@ def main():
     ms = 1000.0 * elapsed / args.steps
     value = verifs_per_step * args.steps / elapsed
     ok = all(b is not None and all(v == 1 for v in b.data_block().Proofs.values()) for b in blocks)
-    result_ok = _check_lr_results(comm, checks, lp)
+    result_ok = _check_lr_results(comm, checks, lp, diffp)
     allt = comm.all_gather_object(timers.summary())
     if rank == 0:
         phase = {}
         for t in allt:
             for k, v in t.items():
                 phase[k] = max(phase.get(k, 0.0), v["sum"] / args.steps)
+        if args.dro:
+            config4 = {
+                "metric": "end-to-end verifiable LR query latency with DP noise (DRO shuffle) + key switching",
+                "value": round(ms / 1000.0, 5), "unit": "s per query (whole job)", "higher_is_better": False,
+                "vs_baseline": round((ms / 1000.0) / REFERENCE_LR_SPECTF_S, 6),
+                "speedup_vs_reference_lr_spectf": round(REFERENCE_LR_SPECTF_S / (ms / 1000.0), 1),
+                "speedup_vs_reference_diffpri_10k": round(REFERENCE_DIFFPRI_10K_S / (ms / 1000.0), 1),
+                "obfuscation": "DRO: encrypted Laplace noise list shuffled + re-randomised by every CN with a "
+                               "proof of shuffle, added to the aggregate before key switching (the reference's "
+                               "Obfuscation protocol is only legal for bit operations, structs.go:450-462)",
+                "noise_list": {"size": args.dro, "lap_scale": DRO_LAP_SCALE, "limit": DRO_LIMIT},
+            }
         line = {
             "metric": "end-to-end query latency + range-proof verifications/sec, logreg on 1e6 records",
             "value": round(value, 3),
@@ -243,6 +269,9 @@ def main():
             "step_ms_rank0": step_ms,
             "phase_s": {k: round(v, 4) for k, v in sorted(phase.items()) if not k.startswith("dp") or "AllProofs" in k},
         }
+        if args.dro:  # config 4: latency is the metric (one JSON line, same harness)
+            line.update(config4)
+            line["config"]["model"] = f"logistic regression k=2, d={d} + DRO noise + key switching, verifiable"
         print(json.dumps(line), flush=True)
         if args.json_out:
             with open(args.json_out, "w") as f:
@@ -255,12 +284,16 @@ def main():
         sys.exit("bench: a proof was rejected or the decrypted result is wrong (see all_proofs_valid / result_ok)")
 
 
-def _check_lr_results(comm, checks: list, lp) -> bool:
+def _check_lr_results(comm, checks: list, lp, diffp=None) -> bool:
     """Outside the timed region: for every timed query, the querier's
     decrypted aggregate must equal the clear sum of every DP's coefficient
-    vector (all ranks' DPs), and its weights the gradient descent run on that
-    clear sum."""
+    vector (all ranks' DPs) -- plus, with DP noise, one distinct entry of the
+    (shuffled) noise list per output -- and its weights the gradient descent
+    run on what was decrypted."""
+    from collections import Counter
+
     from drynx_amd.models.logistic_regression import decode_logistic_regression_values
+    from drynx_amd.proofs.aggregation_shuffle import generate_noise_values_scale
 
     sums = []
     for _, clear in checks:
@@ -280,10 +313,18 @@ def _check_lr_results(comm, checks: list, lp) -> bool:
             if s_ is not None:
                 clear_sum = s_ if clear_sum is None else [a + b for a, b in zip(clear_sum, s_)]
         (w, plain) = weights
-        if plain != clear_sum:
+        if diffp is not None:
+            noise = Counter(generate_noise_values_scale(diffp.NoiseListSize, diffp.LapMean, diffp.LapScale,
+                                                        diffp.Quanta, diffp.Scale or 1.0, diffp.Limit))
+            k = min(len(plain), diffp.NoiseListSize)
+            used = Counter(p_ - c_ for p_, c_ in zip(plain[:k], clear_sum[:k]))
+            if any(noise[v] < c for v, c in used.items()) or plain[k:] != clear_sum[k:]:
+                good = False
+                continue
+        elif plain != clear_sum:
             good = False
             continue
-        w_clear = decode_logistic_regression_values(clear_sum, lp)
+        w_clear = decode_logistic_regression_values(plain, lp)
         good = good and all(abs(a - b) <= 1e-9 * max(1.0, abs(b)) for a, b in zip(w, w_clear))
     return good
 
