@@ -680,19 +680,21 @@ def _gt_in_subgroup_each(g: torch.Tensor) -> list:
     return [bool(v) for v in nt.gt_eq(a, b).tolist()]
 
 
-def validate_list(r: RangeProofList, mode: int = 0) -> bool:
+def validate_list(r: RangeProofList, mode: int = 0, subgroup: bool | None = None) -> bool:
     """Decoding checks of a (raw-limb or kyber-layout) proof list before any
     arithmetic on it: every coordinate below p and every scalar below r; the
-    commitment (K, C) and D on G1; V on the twist (in G2 when ``mode`` >= 1);
-    every a_ij non-zero and in the cyclotomic subgroup.  The prime-order part
-    of a_ij is enforced by the batch equation plus one independent random
-    combination tested in GT (``verify_range_proof_list``)."""
+    commitment (K, C) and D on G1; V in G2 (``subgroup``, default: mode >= 1)
+    or only on the twist; every a_ij non-zero and in the cyclotomic subgroup.
+    The prime-order part of a_ij is enforced by the batch equation plus each
+    VN's independent random combination tested in GT."""
+    if subgroup is None:
+        subgroup = mode >= 1
     fp = lambda t: nt.limbs_canonical(t.reshape(-1, 8))  # noqa: E731
     fr = lambda t: nt.limbs_canonical(t.reshape(-1, 8), fr=True)  # noqa: E731
     flags = [fp(r.commit.K), fp(r.commit.C), nt.g1j_on_curve(r.commit.K), nt.g1j_on_curve(r.commit.C)]
     if r.has_rp and len(r):
         flags += [fp(r.D), nt.g1j_on_curve(r.D), fr(r.challenge), fr(r.zr), fr(r.zphi), fr(r.zv), fp(r.V), fp(r.A),
-                  nt.g2_subgroup(r.V) if mode >= 1 else nt.g2_on_curve(r.V), nt.gt_cyclotomic(r.A)]
+                  nt.g2_subgroup(r.V) if subgroup else nt.g2_on_curve(r.V), nt.gt_cyclotomic(r.A)]
     return bool(torch.stack([f.bool().all() for f in flags]).all())
 
 
@@ -741,8 +743,12 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
     if r.zphi.shape[0] != n * l or r.zv.shape[0] != n * S * l or r.V.shape[0] != n * S * l \
             or r.A.shape[0] != n * S * l or r.challenge.shape[0] != n:
         return [False] * n_vn
+    glv = os.environ.get("DRYNX_RHO", "glv") == "glv"
+    use_msm = glv and os.environ.get("DRYNX_RPV", "msm") == "msm"
     with timers.span("rp.verify.validate"):
-        if not validate_list(r, mode):
+        # the bilinearity regrouping ("msm") is only valid for V in G2: every V
+        # passes the exact subgroup test there, whatever the mode
+        if not validate_list(r, mode, subgroup=mode >= 1 or use_msm):
             return [False] * n_vn
     if mode >= 1:
         with timers.span("rp.verify.challenge"):
@@ -775,7 +781,6 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
     # pairing-equation weights: rho = a + b lambda (GLV, a and b 32-bit: 2^64
     # distinct residues, so the same 2^-64 soundness as uniform 64-bit weights;
     # csrc/kernels/dx_glv.hip) or, with DRYNX_RHO=64, uniform 64-bit
-    glv = os.environ.get("DRYNX_RHO", "glv") == "glv"
     if glv:
         pairs = [c.glv(m, device) if c is not None else nt.glv_weights(m, device) for c in cl]
         ab_all = torch.cat([p_[0] for p_ in pairs]) if G > 1 else pairs[0][0]
@@ -790,7 +795,6 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
     # pairing side: "msm" regroups the product by bilinearity (one G2 MSM and
     # n*S L-point combinations per VN, n*S + 1 Miller loops); "fold" runs one
     # Miller loop per item (the two-phase shared-V fold)
-    use_msm = glv and os.environ.get("DRYNX_RPV", "msm") == "msm"
     aux = _aux_stream(device) if device.type == "cuda" else None
     if aux is not None:
         # the pairing work (~all of the GPU time) is queued FIRST on this

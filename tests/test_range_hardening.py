@@ -148,3 +148,43 @@ def test_raw_limb_payload_checks(setup):
             t[row, 3] ^= val        # off the curve
         assert not rp.validate_list(bad), field
         assert not rp.verify_range_proof_list(bad, sm, P)
+
+
+def _g2_mul_full(k: int, Q):
+    """k * Q on the whole twist group (the oracle's g2_mul reduces k mod r)."""
+    acc, add = None, Q
+    while k:
+        if k & 1:
+            acc = O.g2_add(acc, add)
+        add = O.g2_add(add, add)
+        k >>= 1
+    return acc
+
+
+def test_g2_subgroup_rejects_every_torsion_order():
+    """The fast membership test [u+1]Q + psi([u]Q) + psi^2([u]Q) == psi^3([2u]Q)
+    (dx_g2_subgroup) against adversarial V = G + T, T of each prime order
+    dividing the twist cofactor 2p - r: every such V is rejected, every G2
+    point accepted (the msm verifier's regrouping requires V in G2)."""
+    import random
+
+    h = 2 * O.P - O.R
+    primes = [10069, 5864401, 1875725156269, 197620364512881247228717050342013327560683201906968909]
+    assert h == primes[0] * primes[1] * primes[2] * primes[3]
+    rnd = random.Random(11)
+    G = O.g2_mul(123456789, O.G2_GEN)
+    pts, want = [G, O.G2_GEN], [1, 1]
+    for q in primes:
+        while True:
+            x = O.Fp2(rnd.randrange(O.P), rnd.randrange(O.P))
+            y = _fp2_sqrt(x * x * x + O.B2)
+            if y is None:
+                continue
+            T = _g2_mul_full(h // q * O.R, (x, y))
+            if T is not None:
+                break
+        assert _g2_mul_full(q, T) is None
+        pts += [T, O.g2_add(G, T)]
+        want += [0, 0]
+    got = nt.g2_subgroup(bn.g2_aff_tensor(pts)).tolist()
+    assert got == want
