@@ -680,13 +680,14 @@ def _gt_in_subgroup_each(g: torch.Tensor) -> list:
     return [bool(v) for v in nt.gt_eq(a, b).tolist()]
 
 
-def validate_list(r: RangeProofList, mode: int = 0, subgroup: bool | None = None) -> bool:
+def validate_list(r: RangeProofList, mode: int = 0, subgroup: bool | None = None, lazy: bool = False):
     """Decoding checks of a (raw-limb or kyber-layout) proof list before any
     arithmetic on it: every coordinate below p and every scalar below r; the
     commitment (K, C) and D on G1; V in G2 (``subgroup``, default: mode >= 1)
     or only on the twist; every a_ij non-zero and in the cyclotomic subgroup.
     The prime-order part of a_ij is enforced by the batch equation plus each
-    VN's independent random combination tested in GT."""
+    VN's independent random combination tested in GT.  ``lazy``: return the
+    verdict as a device bool (no host sync)."""
     if subgroup is None:
         subgroup = mode >= 1
     fp = lambda t: nt.limbs_canonical(t.reshape(-1, 8))  # noqa: E731
@@ -695,7 +696,8 @@ def validate_list(r: RangeProofList, mode: int = 0, subgroup: bool | None = None
     if r.has_rp and len(r):
         flags += [fp(r.D), nt.g1j_on_curve(r.D), fr(r.challenge), fr(r.zr), fr(r.zphi), fr(r.zv), fp(r.V), fp(r.A),
                   nt.g2_subgroup(r.V) if subgroup else nt.g2_on_curve(r.V), nt.gt_cyclotomic(r.A)]
-    return bool(torch.stack([f.bool().all() for f in flags]).all())
+    ok = torch.stack([f.bool().all() for f in flags]).all()
+    return ok if lazy else bool(ok)
 
 
 def verify_range_proof_list(rpl: RangeProofList, sigmat: SigMaterial, P_point, threshold: float = 1.0,
@@ -743,13 +745,26 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
     if r.zphi.shape[0] != n * l or r.zv.shape[0] != n * S * l or r.V.shape[0] != n * S * l \
             or r.A.shape[0] != n * S * l or r.challenge.shape[0] != n:
         return [False] * n_vn
-    glv = os.environ.get("DRYNX_RHO", "glv") == "glv"
-    use_msm = glv and os.environ.get("DRYNX_RPV", "msm") == "msm"
+    # pairing side: "msm" regroups the product by bilinearity (one G2 MSM and
+    # n*S L-point combinations per VN, n*S + 1 Miller loops); "fold"
+    # (DRYNX_RPV=fold) runs one Miller loop per item, as the reference's
+    # per-equation check
+    use_msm = os.environ.get("DRYNX_RPV", "msm") == "msm"
     with timers.span("rp.verify.validate"):
         # the bilinearity regrouping ("msm") is only valid for V in G2: every V
-        # passes the exact subgroup test there, whatever the mode
-        if not validate_list(r, mode, subgroup=mode >= 1 or use_msm):
+        # passes the exact subgroup test there, whatever the mode.  On a GPU
+        # the checks run on their own stream, filling the gaps the verifier's
+        # host-side plans leave, and are read back with the verdicts (work
+        # done meanwhile on invalid data is discarded)
+        vstream = _val_stream(device) if device.type == "cuda" else None
+        if vstream is not None:
+            vstream.wait_stream(torch.cuda.current_stream(device))
+            with torch.cuda.stream(vstream):
+                valid = validate_list(r, mode, subgroup=mode >= 1 or use_msm, lazy=True)
+        elif not validate_list(r, mode, subgroup=mode >= 1 or use_msm):
             return [False] * n_vn
+        else:
+            valid = True
     if mode >= 1:
         with timers.span("rp.verify.challenge"):
             if not torch.equal(challenges(r.commit.C, r.cols, sigmat, device, mode, r.D, r.V, r.A, S, l),
@@ -780,21 +795,13 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
     w_all = _cat_draw(lambda c: c.bits(n, device, 64) if c is not None else _rand64(n, device))  # D-equation weights
     # pairing-equation weights: rho = a + b lambda (GLV, a and b 32-bit: 2^64
     # distinct residues, so the same 2^-64 soundness as uniform 64-bit weights;
-    # csrc/kernels/dx_glv.hip) or, with DRYNX_RHO=64, uniform 64-bit
-    if glv:
-        pairs = [c.glv(m, device) if c is not None else nt.glv_weights(m, device) for c in cl]
-        ab_all = torch.cat([p_[0] for p_ in pairs]) if G > 1 else pairs[0][0]
-        rho_all = torch.cat([p_[1] for p_ in pairs]) if G > 1 else pairs[0][1]
-    else:
-        ab_all, rho_all = None, _cat_draw(lambda c: c.bits(m, device, 64) if c is not None else _rand64(m, device))
+    # csrc/kernels/dx_glv.hip)
+    pairs = [c.glv(m, device) if c is not None else nt.glv_weights(m, device) for c in cl]
+    ab_all = torch.cat([p_[0] for p_ in pairs]) if G > 1 else pairs[0][0]
+    rho_all = torch.cat([p_[1] for p_ in pairs]) if G > 1 else pairs[0][1]
     # GT-membership combinations: one independent 40-bit gamma set PER VN
     gam_all = _cat_draw(lambda c: c.bits(m, device, 40) if c is not None else _rand64(m, device, 40))
-    vid = torch.arange(G, device=device)
-    vns = [{"rho": rho_all[v * m:(v + 1) * m], "ab": None if ab_all is None else ab_all[v * m:(v + 1) * m]}
-           for v in range(G)]
-    # pairing side: "msm" regroups the product by bilinearity (one G2 MSM and
-    # n*S L-point combinations per VN, n*S + 1 Miller loops); "fold" runs one
-    # Miller loop per item (the two-phase shared-V fold)
+    vns = [{"rho": rho_all[v * m:(v + 1) * m], "ab": ab_all[v * m:(v + 1) * m]} for v in range(G)]
     aux = _aux_stream(device) if device.type == "cuda" else None
     if aux is not None:
         # the pairing work (~all of the GPU time) is queued FIRST on this
@@ -813,7 +820,7 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
         else:
             with timers.span("rp.verify.fold_queue"):
                 for v, fb in zip(vns, _miller_fold_multi(ZB, Y, [v["rho"] for v in vns], r.V, S, l,
-                                                           [v["ab"] for v in vns] if glv else None)):
+                                                           [v["ab"] for v in vns])):
                     v["fb"] = fb
     with timers.span("rp.verify.plans"), (torch.cuda.stream(aux) if aux is not None else _nullctx()):
         # every bucket plan (one host sync each) first, then every pass: a sync
@@ -826,21 +833,19 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
         dplan = nt.g1_msm_plan(dsc, n, 2 * G)                             # group = row // n
         # groups 0..G-1: prod a^rho_v; groups G..2G-1: each VN's own GT-membership
         # combination prod a^gamma_v
-        if glv:  # prod a^rho = prod a^a' * frob^8(a)^b': 32-bit exponents over (A, frob^8 A)
-            A2 = torch.cat([r.A, nt.gt_frob8(r.A)])
-            k = torch.zeros((2 * G, 2 * m, 8), dtype=torch.int32, device=device)
-            abv = ab_all.view(G, m, 2)
-            k[:G, :m, 0] = abv[:, :, 0]
-            k[:G, m:, 0] = abv[:, :, 1]
-            k[G:, :m] = gam_all.view(G, m, 8)
-            # GPU: 11-bit windows (3 per 32-bit half, 4 for the 40-bit combinations);
-            # host: bytes (fewer buckets for the host's serial bucket products)
-            wc_ = (4, 11) if device.type == "cuda" else (5, 8)
-            k = k.view(-1, 8)
-            mplan = nt.multi_exp_plan(k, 2 * m, 2 * G, W=wc_[0], c=wc_[1])          # group = row // 2m
-            mexp = nt.multi_exp_grouped(A2, k, 2 * m, 2 * G, W=wc_[0], c=wc_[1], plan=mplan)
-        else:
-            mexp = nt.multi_exp_grouped(r.A, torch.cat([rho_all, gam_all]), m, 2 * G)
+        # prod a^rho = prod a^a' * frob^8(a)^b': 32-bit exponents over (A, frob^8 A)
+        A2 = torch.cat([r.A, nt.gt_frob8(r.A)])
+        k = torch.zeros((2 * G, 2 * m, 8), dtype=torch.int32, device=device)
+        abv = ab_all.view(G, m, 2)
+        k[:G, :m, 0] = abv[:, :, 0]
+        k[:G, m:, 0] = abv[:, :, 1]
+        k[G:, :m] = gam_all.view(G, m, 8)
+        # GPU: 11-bit windows (3 per 32-bit half, 4 for the 40-bit combinations);
+        # host: bytes (fewer buckets for the host's serial bucket products)
+        wc_ = (4, 11) if device.type == "cuda" else (5, 8)
+        k = k.view(-1, 8)
+        mplan = nt.multi_exp_plan(k, 2 * m, 2 * G, W=wc_[0], c=wc_[1])          # group = row // 2m
+        mexp = nt.multi_exp_grouped(A2, k, 2 * m, 2 * G, W=wc_[0], c=wc_[1], plan=mplan)
         if use_msm and aux is not None:
             S_R = nt.g2_msm_run(r.V, hR)                               # R window sums
         dcheck = nt.g1_msm_launch(dpts, dsc, n, 2 * G, bits=256, plan=dplan)
@@ -876,6 +881,10 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
         e_all, dfull = e_all.cpu(), dfull.cpu()
     for k, v in enumerate(vns):
         v.update(G=GG[k: k + 1], dfull=dfull[k], e=e_all[k: k + 1], dcheck=D_all[2 * k: 2 * k + 2])
+    if vstream is not None:
+        vstream.synchronize()
+        if not bool(valid):
+            return [False] * n_vn
     out = []
     # prime-order part of the a_ij: each VN's own independent 40-bit
     # combination in GT (the smallest prime factor of the cyclotomic cofactor
@@ -983,63 +992,39 @@ def fold_k(n_items: int, slots: int = 2048) -> int:
     return best_k
 
 
-def _miller_fold_multi(ZB, Y, rhos: list, V, S: int, L: int, abs_: list | None = None) -> list:
-    """GPU: for each verifier's weights rho_v, per-workgroup partial products
-    of ML(rho_it (ZB[p,j] - Y[p,i]), V_it).  The two-phase fold
-    (csrc/kernels/fold_body.h) over ALL verifiers at once: one fused G1
-    launch per verifier (gather, difference, 64-bit multiplication, affine)
-    into a shared point image whose per-verifier blocks are padded to whole
-    workgroups, then ONE line-image launch and ONE K-item accumulation (a
-    verifier's slice of a multi-GPU node is too short to fill the chip on
-    its own).  ``abs_``: the verifiers' GLV weight halves (a, b), used by the
-    point kernel instead of the full rho.  The line coefficients depend on V only, so they are computed
-    ONCE for all verifiers (``rp_fold_coeffs``) and each verifier's points
-    are evaluated inside the accumulation (``rp_fold_accum_p``).
-    ``DRYNX_FOLD=2`` selects the per-verifier line image, ``fused`` the
-    one-kernel fold (A/B); the default ``4`` normalises every line to
-    1 + (a u) w + (b v) w^3 (10 Fp2 products per line instead of 13)."""
+def _miller_fold_multi(ZB, Y, rhos: list, V, S: int, L: int, abs_: list) -> list:
+    """GPU, verifier mode "fold" (the per-item Miller product, as the
+    reference's per-equation check): for each verifier's GLV weights, the
+    per-workgroup partial products of ML(rho_it (ZB[p,j] - Y[p,i]), V_it).
+    The line coefficients depend on V only, so they are computed ONCE for all
+    verifiers, normalised to 1 + (a u) w + (b v) w^3 (``rp_fold_ncoeffs``;
+    csrc/kernels/fold_body.h); each verifier's points (fused gather,
+    difference, 32-bit GLV ladder, affine -> (x/y, 1/y)) fill its block of a
+    shared image padded to whole accumulation workgroups, and ONE K-item
+    accumulation folds every verifier (a verifier's slice of a multi-GPU
+    node is too short to fill the chip on its own)."""
     m = V.shape[0]
     G = len(rhos)
-    mode = os.environ.get("DRYNX_FOLD", "4")
-    if mode == "fused":
-        return [nt.rp_verify_fold(ZB, Y, rho, V, S, L) for rho in rhos]
     K = fold_k(G * m)
-    if mode == "4":  # normalised lines: (c1/c0, c3/c0) per V, (x/y, 1/y) per point
-        per = 64 * K * nt.FOLD_P_ALIGN
-        pad = -(-m // per) * per
-        UV = torch.zeros((G * pad, 16), dtype=torch.int32, device=V.device)
-        for v, rho in enumerate(rhos):
-            blk = UV[v * pad: v * pad + m]
-            if abs_ is not None:
-                nt.rp_fold_points_glv(ZB, Y, abs_[v], S, L, out=blk, uv=True)
-            else:
-                nt.g1_aff_to_uv_(nt.rp_fold_points(ZB, Y, rho, S, L, out=blk))
-        fb = nt.rp_fold_accum_n(nt.rp_fold_ncoeffs(V.contiguous()), UV, V.contiguous(), pad, G, K)
-        blk = pad // (64 * K)
-        return [fb[v * blk:(v + 1) * blk] for v in range(G)]
-    if mode == "3":
-        per = 64 * K * nt.FOLD_P_ALIGN
-        pad = -(-m // per) * per
-        P = torch.zeros((G * pad, 16), dtype=torch.int32, device=V.device)
-        for v, rho in enumerate(rhos):
-            if abs_ is not None:  # GLV weights: 32-bit joint ladder
-                nt.rp_fold_points_glv(ZB, Y, abs_[v], S, L, out=P[v * pad: v * pad + m])
-            else:
-                nt.rp_fold_points(ZB, Y, rho, S, L, out=P[v * pad: v * pad + m])
-        fb = nt.rp_fold_accum_p(nt.rp_fold_coeffs(V.contiguous()), P, V.contiguous(), pad, G, K)
-        blk = pad // (64 * K)
-        return [fb[v * blk:(v + 1) * blk] for v in range(G)]
-    per = 64 * K
+    per = 64 * K * nt.FOLD_P_ALIGN
     pad = -(-m // per) * per
-    P = torch.zeros((G * pad, 16), dtype=torch.int32, device=V.device)
-    for v, rho in enumerate(rhos):
-        nt.rp_fold_points(ZB, Y, rho, S, L, out=P[v * pad: v * pad + m])
-    fb = nt.rp_fold_accum(nt.rp_fold_lines(P, V, period=pad), G * pad, K)
-    blk = pad // per
+    UV = torch.zeros((G * pad, 16), dtype=torch.int32, device=V.device)
+    for v in range(G):
+        nt.rp_fold_points_glv(ZB, Y, abs_[v], S, L, out=UV[v * pad: v * pad + m], uv=True)
+    fb = nt.rp_fold_accum_n(nt.rp_fold_ncoeffs(V.contiguous()), UV, V.contiguous(), pad, G, K)
+    blk = pad // (64 * K)
     return [fb[v * blk:(v + 1) * blk] for v in range(G)]
 
 
 _aux: dict = {}
+_val: dict = {}
+
+
+def _val_stream(device):
+    key = str(device)
+    if key not in _val:
+        _val[key] = torch.cuda.Stream(device)
+    return _val[key]
 
 
 def _aux_stream(device):

@@ -44,13 +44,14 @@ def expected_counts(sq) -> dict:
 def _net_proofs(ctx, sq, reqs: list, vns: list):
     """Every proof envelope from its prover to every VN (one hop, the
     reference wire sizes of SURVEY 2.4)."""
-    n_rows = len(dcp_groups(sq.Query.DPDataGen.GroupByValues)) * sq.Query.Operation.NbrOutput
+    n_groups = len(dcp_groups(sq.Query.DPDataGen.GroupByValues))
+    n_rows = n_groups * sq.Query.Operation.NbrOutput
     S = len(sq.RosterServers.list)
     sizes = {}
     for r in reqs:
         if r.kind == "range":
             rg = sq.Query.Ranges or []
-            nb = sum(range_proof_bytes(int(x[0]), int(x[1]), S) for x in rg) * len(dcp_groups(sq.Query.DPDataGen.GroupByValues))
+            nb = sum(range_proof_bytes(int(x[0]), int(x[1]), S) for x in rg) * n_groups
         elif r.kind == "aggregation":
             nb = (len((sq.ServerToDP or {}).get(r.sender_id) or []) + 1) * n_rows * CT_BYTES
         elif r.kind == "keyswitch":

@@ -110,11 +110,9 @@ def test_lr_encode_fused_matches_torch(gpu_device):
         assert torch.allclose(g2, ref2, rtol=1e-10, atol=1e-8), (g2 - ref2).abs().max()
 
 
-@pytest.mark.parametrize("fold", ["4", "3", "2", "fused", "4-rho64"])
-def test_range_proofs_gpu(gpu_device, fold, monkeypatch):
-    if fold.endswith("-rho64"):
-        monkeypatch.setenv("DRYNX_RHO", "64")
-    monkeypatch.setenv("DRYNX_FOLD", fold.split("-")[0])
+@pytest.mark.parametrize("rpv", ["msm", "fold"])
+def test_range_proofs_gpu(gpu_device, rpv, monkeypatch):
+    monkeypatch.setenv("DRYNX_RPV", rpv)
     from drynx_amd.crypto import elgamal as eg
     from drynx_amd.ops.encoding import CreateProofBatch
     from drynx_amd.proofs import range_proof as rp
@@ -311,22 +309,19 @@ def test_fold_points_match_g1_ops(gpu_device, variant):
     assert torch.equal(got, want)
 
 
-@pytest.mark.parametrize("mode", ["2", "3", "4"])
-def test_merged_multi_verifier_fold(gpu_device, mode, monkeypatch):
-    """Several verifiers' folds in one padded line image / accumulation (mode
-    2) or over one shared coefficient image (mode 3) == each verifier's fold
-    on its own (after the final exponentiation)."""
+def test_merged_multi_verifier_fold(gpu_device):
+    """Several verifiers' folds over one shared normalised coefficient image
+    == each verifier's fold on its own (after the final exponentiation)."""
     from drynx_amd.proofs import range_proof as rp
 
-    monkeypatch.setenv("DRYNX_FOLD", mode)
     S, L, npj = 3, 4, 7
     ZB = nt.g1_fb_mul(bn.base_table(gpu_device), bn.random_scalars(npj * L, gpu_device))
     Y = nt.g1_fb_mul(bn.base_table(gpu_device), bn.random_scalars(npj * S, gpu_device))
     m = npj * S * L
     V = nt.g2_fb_mul(bn.base2_table(gpu_device), bn.random_scalars(m, gpu_device))
-    rhos = [rp._rand64(m, gpu_device) for _ in range(3)]
-    merged = rp._miller_fold_multi(ZB, Y, rhos, V, S, L)
-    for rho, fb in zip(rhos, merged):
+    ws = [nt.glv_weights(m, gpu_device) for _ in range(3)]
+    merged = rp._miller_fold_multi(ZB, Y, [w[1] for w in ws], V, S, L, [w[0] for w in ws])
+    for (ab, rho), fb in zip(ws, merged):
         P = nt.rp_fold_points(ZB, Y, rho, S, L)
         alone = nt.rp_fold_accum(nt.rp_fold_lines(P, V), m, 1)
         a = nt.final_exp(nt._finish_prod_on_host(fb))
