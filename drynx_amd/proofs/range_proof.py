@@ -751,17 +751,15 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
     # per-equation check
     use_msm = os.environ.get("DRYNX_RPV", "msm") == "msm"
     with timers.span("rp.verify.validate"):
-        # the bilinearity regrouping ("msm") is only valid for V in G2: every V
-        # passes the exact subgroup test there, whatever the mode.  On a GPU
-        # the checks run on their own stream, filling the gaps the verifier's
-        # host-side plans leave, and are read back with the verdicts (work
-        # done meanwhile on invalid data is discarded)
+        # On a GPU the checks run on their own stream, filling the gaps the
+        # verifier's host-side plans leave, and are read back with the
+        # verdicts (work done meanwhile on invalid data is discarded)
         vstream = _val_stream(device) if device.type == "cuda" else None
         if vstream is not None:
             vstream.wait_stream(torch.cuda.current_stream(device))
             with torch.cuda.stream(vstream):
-                valid = validate_list(r, mode, subgroup=mode >= 1 or use_msm, lazy=True)
-        elif not validate_list(r, mode, subgroup=mode >= 1 or use_msm):
+                valid = validate_list(r, mode, lazy=True)
+        elif not validate_list(r, mode):
             return [False] * n_vn
         else:
             valid = True
@@ -814,9 +812,9 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
             # bucket plans (host syncs) and the R passes go to the high-priority
             # aux stream, whose short plan kernels then overtake the U kernels
             with timers.span("rp.verify.msm_queue"):
-                msq = _msm_queue(Y, r.V, ab_all, G, n, S, l)
-                for v, fb in zip(vns, msq["fb"]):
-                    v["fb"] = fb
+                msq = _msm_queue(Y, r.V, ab_all, G, n, S, l, vstream)
+                for v, fb, uok in zip(vns, msq["fb"], msq["u_ok"]):
+                    v["fb"], v["u_ok"] = fb, uok
         else:
             with timers.span("rp.verify.fold_queue"):
                 for v, fb in zip(vns, _miller_fold_multi(ZB, Y, [v["rho"] for v in vns], r.V, S, l,
@@ -862,15 +860,18 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
             for v in vns:
                 v["F"] = nt._finish_prod_on_host(v["fb"])
             if use_msm:
-                for v, f in zip(vns, _msm_r_miller(hR, S_R)):
-                    v["F"] = nt.gt_mul(v["F"], f.view(1, 96))
+                fR, rok = _msm_r_miller(hR, S_R)
+                for v, f, ok in zip(vns, fR, rok):
+                    v["F"], v["r_ok"] = nt.gt_mul(v["F"], f.view(1, 96)), ok
     else:
         GG = nt.multi_exp_grouped_finish(mexp)
         if use_msm:
             hR = _msm_plan(r.zphi, r.V, rho_all, G, n, S, l)
             msq = _msm_queue(Y, r.V, ab_all, G, n, S, l)
-            for v, fb, f in zip(vns, msq["fb"], _msm_r_miller(hR, nt.g2_msm_run(r.V, hR))):
+            fR, rok = _msm_r_miller(hR, nt.g2_msm_run(r.V, hR))
+            for v, fb, f, ok, uok in zip(vns, msq["fb"], fR, rok, msq["u_ok"]):
                 v["F"] = nt.gt_mul(nt.gt_prod(fb.view(-1, 1, 96), chunk=4).view(1, 96), f.view(1, 96))
+                v["r_ok"], v["u_ok"] = ok, uok
         else:
             T = _fold_points(ZB, Y, S, l)
             for v in vns:
@@ -900,7 +901,12 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
             d_ok = bool(nt.g1_eq(nt.g1_sum(torch.stack([G0[0:1], PB[0:1], PB[1:2]])), G0[1:2])[0])
             lhs = nt.gt_mul(nt.final_exp(v["F"].cpu()), v["G"].cpu())
             eq_ok = bool(nt.gt_eq(lhs, nt.gt_fb_pow(gt_tab, v["e"].cpu())).all())
-        out.append(d_ok and m_oks[len(out)] and eq_ok)
+        # regrouped ("msm") check: the U_q and R of this VN must lie in G2 --
+        # then their torsion parts (V_it off G2 by a cofactor component) cancel
+        # and the checked equation is the one of the proof's G2 projection,
+        # where the pairing is bilinear and the regrouping exact
+        g2_ok = bool(v.get("u_ok", True)) and bool(v.get("r_ok", True))
+        out.append(d_ok and m_oks[len(out)] and eq_ok and g2_ok)
     return out
 
 
@@ -923,7 +929,7 @@ def _msm_plan(zphi, V, rho_all, G: int, n: int, S: int, L: int) -> dict:
     return nt.g2_msm_launch(V, s_r, m, G)                              # group (VN) = row // m
 
 
-def _msm_queue(Y, V, ab_all, G: int, n: int, S: int, L: int) -> dict:
+def _msm_queue(Y, V, ab_all, G: int, n: int, S: int, L: int, vstream=None) -> dict:
     """Verifier mode "msm", the U side (no host sync; csrc/kernels/dx_rpmsm.hip):
     the pairing side of G verifiers' batches regrouped by bilinearity,
         prod_it ML(rho_it (Zphi_pj B - Y_pi), V_it)
@@ -945,6 +951,14 @@ def _msm_queue(Y, V, ab_all, G: int, n: int, S: int, L: int) -> dict:
         period = -(-(G * pad) // (64 * K * nt.FOLD_P_ALIGN)) * (64 * K * nt.FOLD_P_ALIGN)
         Uall = torch.zeros((G * pad, 32), dtype=torch.int32, device=dev)
         nt.rp_u_joint(table, ab_all, nq, G, L, Uall, pad)
+        # G2 membership of every U (exact test), on the validation stream beside the fold
+        cur = torch.cuda.current_stream(dev)
+        vs = vstream if vstream is not None else cur
+        vs.wait_stream(cur)
+        with torch.cuda.stream(vs):
+            fl = nt.g2_subgroup(Uall).view(G, pad)[:, :nq].bool().all(dim=1)
+        Uall.record_stream(vs)
+        out["u_ok"] = list(fl.unbind(0))
         UV = torch.zeros((period, 16), dtype=torch.int32, device=dev)
         nt.rp_msm_uv(Y, UV, nq, G, pad)
         fb = nt.rp_fold_accum_n(nt.rp_fold_ncoeffs(Uall), UV, Uall, period, 1, K)
@@ -953,6 +967,7 @@ def _msm_queue(Y, V, ab_all, G: int, n: int, S: int, L: int) -> dict:
     else:
         Uall = torch.zeros((G * nq, 32), dtype=torch.int32, device=dev)
         nt.rp_u_joint(table, ab_all, nq, G, L, Uall, nq)
+        out["u_ok"] = [bool(x) for x in nt.g2_subgroup(Uall).view(G, nq).bool().all(dim=1).tolist()]
         negY = nt.g1_to_affine(nt.g1_add(bn.g1_infinity_jac(nq, dev), Y.contiguous(), subtract=True))
         out["fb"] = [nt.miller_loop(negY, Uall[v * nq:(v + 1) * nq].contiguous()) for v in range(G)]
     return out
@@ -960,14 +975,15 @@ def _msm_queue(Y, V, ab_all, G: int, n: int, S: int, L: int) -> dict:
 
 def _msm_r_miller(hR, S_dev) -> torch.Tensor:
     """Host tail of the R side: Horner over the window sums (one core per VN
-    beats one GPU lane at this serial chain) and ML(B, R_v) -> [G, 96] host."""
+    beats one GPU lane at this serial chain) and ML(B, R_v) -> ([G, 96] host,
+    [R_v in G2] per VN)."""
     R = nt.g2_msm_finish(S_dev.cpu(), hR)
     B = nt.g1_to_affine(bn.g1_jac_tensor([O.G1_GEN], "cpu")).repeat(R.shape[0], 1)
     f = nt.miller_loop(B, R)
     inf = ~R.bool().any(dim=1)                                         # R = O: e(B, O) = 1
     if bool(inf.any()):
         f[inf] = nt.gt_one("cpu")
-    return f
+    return f, [bool(x) for x in nt.g2_subgroup(R).tolist()]
 
 
 def _fold_points(ZB, Y, S: int, L: int) -> torch.Tensor:

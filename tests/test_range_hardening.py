@@ -188,3 +188,30 @@ def test_g2_subgroup_rejects_every_torsion_order():
         want += [0, 0]
     got = nt.g2_subgroup(bn.g2_aff_tensor(pts)).tolist()
     assert got == want
+
+
+def test_v_with_small_torsion_rejected_by_regrouped_verifier(setup, monkeypatch):
+    """V_it = G_it + T with T of order 10069 (the smallest cofactor prime):
+    the bilinearity-regrouped verifier ("msm", mode 0) rejects it through the
+    exact G2 membership of its U combinations (a torsion component survives
+    a random combination unless the weights cancel it mod 10069)."""
+    import random
+
+    monkeypatch.setenv("DRYNX_RPV", "msm")
+    sm, P = setup[4], setup[5]
+    rpl = _prove(setup, [3, 5])
+    assert rp.verify_range_proof_list(rpl, sm, P, mode=0)
+    h = 2 * O.P - O.R
+    rnd = random.Random(5)
+    while True:
+        x = O.Fp2(rnd.randrange(O.P), rnd.randrange(O.P))
+        y = _fp2_sqrt(x * x * x + O.B2)
+        if y is not None:
+            T = _g2_mul_full(h // 10069 * O.R, (x, y))
+            if T is not None:
+                break
+    G = bn.g2_points_from_aff(rpl.V[2:3].cpu())[0]
+    rpl.V = rpl.V.clone()
+    rpl.V[2] = bn.g2_aff_tensor([O.g2_add(G, T)])[0].to(rpl.V.device)
+    assert bool(nt.g2_on_curve(rpl.V[2:3]).all())
+    assert not rp.verify_range_proof_list(rpl, sm, P, mode=0)

@@ -130,7 +130,7 @@ def test_msm_pairing_product_matches_per_item_fold(device, proofs):
     ab, rho = nt.glv_weights(G * m, dev)
     hR = rp._msm_plan(r.zphi, r.V, rho, G, n, S, l)
     q = rp._msm_queue(Y, r.V, ab, G, n, S, l)
-    fR = rp._msm_r_miller(hR, nt.g2_msm_run(r.V, hR))
+    fR, _ = rp._msm_r_miller(hR, nt.g2_msm_run(r.V, hR))
     T = rp._fold_points(ZB.cpu(), Y.cpu(), S, l)
     for v in range(G):
         fbv = q["fb"][v]
