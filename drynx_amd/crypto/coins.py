@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import hashlib
 import os
+import threading
 
 import torch
 
@@ -23,17 +24,20 @@ from .. import native as nt
 
 
 class Coins:
-    __slots__ = ("key", "_n")
+    __slots__ = ("key", "_n", "_lock")
 
     def __init__(self, key: bytes | None = None):
         self.key = bytes(key) if key is not None else os.urandom(32)
         if len(self.key) != 32:
             raise ValueError("Coins key must be 32 bytes")
         self._n = 0
+        self._lock = threading.Lock()  # a VN's range pool and its per-CN checks draw from two threads
 
     def _next_key(self) -> bytes:
-        self._n += 1
-        return hashlib.sha256(b"drynx_amd/coins" + self.key + self._n.to_bytes(8, "little")).digest()
+        with self._lock:
+            self._n += 1
+            n = self._n
+        return hashlib.sha256(b"drynx_amd/coins" + self.key + n.to_bytes(8, "little")).digest()
 
     def derive(self, label) -> "Coins":
         return Coins(hashlib.sha256(b"drynx_amd/coins/derive" + self.key + str(label).encode()).digest())

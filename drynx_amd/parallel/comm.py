@@ -54,6 +54,13 @@ class Comm:
         saves the size round (and its host synchronisation)."""
         return {self.rank: outgoing[self.rank].reshape(-1)} if self.rank in outgoing else {}
 
+    def plane(self, name: str) -> "Comm":
+        """A communicator for a second thread of collectives (e.g. the pooled
+        range verification running beside the CN phases): its control
+        collectives use their own process group, so the two threads never
+        interleave operations on one group.  It carries no data plane."""
+        return self
+
     def send(self, t: torch.Tensor, dst: int):
         raise RuntimeError("single-process comm has no peers")
 
@@ -109,6 +116,11 @@ class DistComm(Comm):
         # where the data plane's all_to_all_single buffers live: HBM for RCCL,
         # host memory for gloo (whose all-to-all is CPU only)
         self._stage = self.device if self.backend == "nccl" else torch.device("cpu")
+        # control groups of the side planes (created by every rank, in this order)
+        self._planes = {name: _CtrlPlane(self, dist.new_group(backend="gloo")) for name in ("pool",)}
+
+    def plane(self, name: str) -> "Comm":
+        return self._planes[name]
 
     def barrier(self):
         if self.backend == "nccl":
@@ -117,28 +129,10 @@ class DistComm(Comm):
             dist.barrier()
 
     def broadcast_object(self, obj, src: int = 0):
-        if self.rank == src:
-            b = obj_to_bytes(obj)
-            n = torch.tensor([len(b)], dtype=torch.int64)
-        else:
-            n = torch.zeros(1, dtype=torch.int64)
-        dist.broadcast(n, src, group=self._ctrl)
-        buf = (torch.frombuffer(bytearray(b), dtype=torch.uint8) if self.rank == src
-               else torch.empty(int(n), dtype=torch.uint8))
-        dist.broadcast(buf, src, group=self._ctrl)
-        return obj if self.rank == src else bytes_to_obj(buf.numpy().tobytes())
+        return _bcast_obj(self.rank, obj, src, self._ctrl)
 
     def all_gather_object(self, obj) -> list:
-        b = obj_to_bytes(obj)
-        sizes = [torch.zeros(1, dtype=torch.int64) for _ in range(self.world)]
-        dist.all_gather(sizes, torch.tensor([len(b)], dtype=torch.int64), group=self._ctrl)
-        m = max(int(x) for x in sizes)
-        mine = torch.zeros(m, dtype=torch.uint8)
-        mine[: len(b)] = torch.frombuffer(bytearray(b), dtype=torch.uint8)
-        bufs = [torch.empty(m, dtype=torch.uint8) for _ in range(self.world)]
-        dist.all_gather(bufs, mine, group=self._ctrl)
-        return [obj if r == self.rank else bytes_to_obj(bufs[r][: int(sizes[r])].numpy().tobytes())
-                for r in range(self.world)]
+        return _gather_obj(self.rank, self.world, obj, self._ctrl)
 
     def exchange(self, outgoing: dict, recv_sizes: dict | None = None) -> dict:
         """ONE ``all_to_all_single`` whatever the backend: on RCCL the per-peer
@@ -183,6 +177,52 @@ class DistComm(Comm):
         dist.recv(t, src)
         self.bytes_recv += 4 * numel
         return t.to(self.device)
+
+
+def _bcast_obj(rank: int, obj, src: int, group):
+    """Control message from ``src`` to every rank (msgpack, no pickle)."""
+    if rank == src:
+        b = obj_to_bytes(obj)
+        n = torch.tensor([len(b)], dtype=torch.int64)
+    else:
+        n = torch.zeros(1, dtype=torch.int64)
+    dist.broadcast(n, src, group=group)
+    buf = torch.frombuffer(bytearray(b), dtype=torch.uint8) if rank == src else torch.empty(int(n), dtype=torch.uint8)
+    dist.broadcast(buf, src, group=group)
+    return obj if rank == src else bytes_to_obj(buf.numpy().tobytes())
+
+
+def _gather_obj(rank: int, world: int, obj, group) -> list:
+    b = obj_to_bytes(obj)
+    sizes = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(sizes, torch.tensor([len(b)], dtype=torch.int64), group=group)
+    m = max(int(x) for x in sizes)
+    mine = torch.zeros(m, dtype=torch.uint8)
+    mine[: len(b)] = torch.frombuffer(bytearray(b), dtype=torch.uint8)
+    bufs = [torch.empty(m, dtype=torch.uint8) for _ in range(world)]
+    dist.all_gather(bufs, mine, group=group)
+    return [obj if r == rank else bytes_to_obj(bufs[r][: int(sizes[r])].numpy().tobytes()) for r in range(world)]
+
+
+class _CtrlPlane(Comm):
+    """Control collectives of a side plane on their own gloo group (see
+    ``Comm.plane``); data-plane exchanges stay on the main thread's comm."""
+
+    def __init__(self, parent: "DistComm", group):
+        self.rank, self.world, self.device = parent.rank, parent.world, parent.device
+        self._group = group
+
+    def barrier(self):
+        dist.barrier(group=self._group)
+
+    def broadcast_object(self, obj, src: int = 0):
+        return _bcast_obj(self.rank, obj, src, self._group)
+
+    def all_gather_object(self, obj) -> list:
+        return _gather_obj(self.rank, self.world, obj, self._group)
+
+    def exchange(self, outgoing: dict, recv_sizes: dict | None = None) -> dict:
+        raise RuntimeError("a control plane carries no data-plane exchanges (use the main comm)")
 
 
 def make_comm(device=None) -> Comm:

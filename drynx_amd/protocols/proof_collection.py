@@ -158,7 +158,7 @@ def _helper_slice(lists, sq, part) -> list:
     return prq.slice_lists(lists, sq, part)
 
 
-def pool_verify_ranges(ctx, sq, reqs: list, vns: list) -> dict:
+def pool_verify_ranges(ctx, sq, reqs: list, vns: list, comm=None) -> dict:
     """Pooled range verification (see ``use_pool``).  Each VN's rank decides
     that VN's sampling (reference ``rand.Float64() <= Threshold``, from the
     VN's own coins, or the sharding extension) and draws a per-survey seed;
@@ -168,7 +168,8 @@ def pool_verify_ranges(ctx, sq, reqs: list, vns: list) -> dict:
     helper's slice verdict only when the digest matches its own digest of
     that slice of the signed payload, and re-checks any other slice itself.
     -> {vn_id: {base_key: None (not sampled) | bool}} on every rank."""
-    W, k = ctx.comm.world, ctx.comm.rank
+    comm = comm or ctx.comm
+    W, k = comm.world, comm.rank
     rng = [i for i, r in enumerate(reqs) if r.kind == "range" and not r.header_only]
     local = {}
     for vi, vn in enumerate(vns):
@@ -177,7 +178,7 @@ def pool_verify_ranges(ctx, sq, reqs: list, vns: list) -> dict:
             local[vn.id] = ({reqs[i].base_key(): prq.should_verify(sq, reqs[i], vi, len(vns), c) for i in rng},
                             c.seed())
     sampled, seeds = {}, {}
-    for d in ctx.comm.all_gather_object(local):
+    for d in comm.all_gather_object(local):
         for vid, (smp, seed) in d.items():
             sampled[vid], seeds[vid] = smp, seed
     vn_idxs = {vn.id: [i for i in rng if sampled[vn.id].get(reqs[i].base_key())] for vn in vns}
@@ -186,11 +187,11 @@ def pool_verify_ranges(ctx, sq, reqs: list, vns: list) -> dict:
     res, digests = prq.verify_range_pool_part(reqs, vn_idxs, sq, ctx.device, ctx.verifier_cache, (k, W), part_coins)
     mine = {vn.id: {reqs[i].base_key(): bool(ok) for i, ok in res.get(vn.id, {}).items()} for vn in vns}
     mydig = {reqs[i].base_key(): d for i, d in digests.items()}
-    gathered = ctx.comm.all_gather_object((mine, mydig))
+    gathered = comm.all_gather_object((mine, mydig))
     out = {}
     local_vns = [vn for vn in vns if vn.rank == ctx.rank]
     if local_vns:
-        trusted = _check_helper_digests(ctx, sq, reqs, vn_idxs, local_vns, gathered)
+        trusted = _check_helper_digests(ctx, sq, reqs, vn_idxs, local_vns, gathered, W)
     for vn in vns:
         if vn.rank != ctx.rank:
             continue
@@ -217,11 +218,11 @@ def pool_verify_ranges(ctx, sq, reqs: list, vns: list) -> dict:
     return out
 
 
-def _check_helper_digests(ctx, sq, reqs, vn_idxs: dict, local_vns: list, gathered: list) -> dict:
+def _check_helper_digests(ctx, sq, reqs, vn_idxs: dict, local_vns: list, gathered: list, W: int) -> dict:
     """For each local VN: the (base_key, part) pairs whose helper-reported
     slice digest equals the digest of that slice of the VN's own signed
     payload, and the mismatches to redo ({part: [request index]})."""
-    W, me = ctx.comm.world, ctx.comm.rank
+    me = ctx.rank
     need = sorted({i for vn in local_vns for i in vn_idxs[vn.id]}) if W > 1 else []
     expected: dict = {}
     empty: set = set()  # (request, part) whose slice is empty: nothing to check there
@@ -260,7 +261,7 @@ def _check_helper_digests(ctx, sq, reqs, vn_idxs: dict, local_vns: list, gathere
     return out
 
 
-def _pool_async(ctx, sq, reqs, vns):
+def _pool_async(ctx, sq, reqs, vns, comm=None):
     """pool_verify_ranges on a worker thread with its own HIP stream: the
     range batches (the GPU's long pole) run while this thread checks the
     short per-CN proofs of each VN.  On a multi-rank node the worker also
@@ -270,7 +271,7 @@ def _pool_async(ctx, sq, reqs, vns):
     if not hasattr(ctx, "_pool_exec"):
         ctx._pool_exec = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="drynx-vn-pool")
     if ctx.device.type != "cuda":
-        return ctx._pool_exec.submit(pool_verify_ranges, ctx, sq, reqs, vns)
+        return ctx._pool_exec.submit(pool_verify_ranges, ctx, sq, reqs, vns, comm)
     if not hasattr(ctx, "_pool_stream"):
         # DRYNX_POOL_RESERVE_CUS=k: the pool's heavy kernels (long-running
         # workgroups) leave k CUs to the short plan / per-CN-proof launches
@@ -283,7 +284,7 @@ def _pool_async(ctx, sq, reqs, vns):
 
     def run():
         with torch.cuda.stream(side):
-            out = pool_verify_ranges(ctx, sq, reqs, vns)
+            out = pool_verify_ranges(ctx, sq, reqs, vns, comm)
         side.synchronize()
         return out
 
@@ -327,17 +328,44 @@ def store_verdicts(ctx, sq, vn, requests: list, pending) -> dict:
     return bitmap
 
 
-def proof_collection(ctx, sq, local_requests: list):
-    """Returns the new SkipBlock (on every rank)."""
+def start_range_plane(ctx, sq, range_requests: list) -> dict:
+    """The range-proof plane, started as soon as this rank's range proofs are
+    signed (the reference streams them to the VNs while the CNs aggregate,
+    data_collection_protocol.go:278-348): their fan-out on the data plane
+    (main thread: every RCCL collective stays on one thread), then the pooled
+    verification on a worker with its own HIP stream and its own control
+    group (``Comm.plane("pool")``), overlapping the CN phases."""
+    vns = [ctx.cluster.by_id(si.id) for si in sq.Query.RosterVNs.list]
+    with timers.timed("RangeFanOut"):
+        reqs = fan_out(ctx, sq, range_requests, pool=True)
+    return {"reqs": reqs, "pooled": _pool_async(ctx, sq, reqs, vns, ctx.comm.plane("pool"))}
+
+
+def early_plane_ok(ctx, sq) -> bool:
+    """The range plane starts before the CN phases when verification is pooled
+    (single operator) and the survey has VNs and proofs."""
+    return bool(sq.Query.Proofs) and sq.Query.RosterVNs is not None and len(sq.Query.RosterVNs.list) > 0 \
+        and use_pool(ctx) and os.environ.get("DRYNX_RANGE_PLANE", "1") != "0"
+
+
+def proof_collection(ctx, sq, local_requests: list, early: dict | None = None):
+    """Returns the new SkipBlock (on every rank).  ``early``: the range plane
+    started by ``start_range_plane`` (its requests and pooled verdicts);
+    ``local_requests`` then holds the remaining (per-CN) proofs."""
     vns = [ctx.cluster.by_id(si.id) for si in sq.Query.RosterVNs.list]
     pool = use_pool(ctx)
     with timers.timed("ProofFanOut"):
-        reqs = fan_out(ctx, sq, local_requests, pool=pool)
+        reqs = fan_out(ctx, sq, local_requests, pool=pool and early is None)
+    if early is not None:
+        reqs = early["reqs"] + reqs
     if getattr(ctx, "net", None) is not None:
         _net_proofs(ctx, sq, reqs, vns)
     bitmaps = {}
     with timers.timed("ProofVerification"):
-        pooled = _pool_async(ctx, sq, reqs, vns) if pool else None
+        if early is not None:
+            pooled = early["pooled"]
+        else:
+            pooled = _pool_async(ctx, sq, reqs, vns) if pool else None
         local_vns = [vn.id for vn in vns if vn.rank == ctx.rank]
         if len(local_vns) > 1:  # co-hosted VNs: one grouped key-switch MSM for all of them
             with timers.span("verify.keyswitch.multi"):

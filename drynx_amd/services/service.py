@@ -259,6 +259,17 @@ class DrynxNode:
         if dp_results:
             n_out = len(next(iter(dp_results.values()))["cv"]) // n_groups
         n_out = max(self.comm.all_gather_object(n_out if dp_results else 0)) or n_out
+        early = None
+        if range_future is not None and pcp.early_plane_ok(self, sq):
+            # the range-proof plane starts now, beside the CN phases
+            with timers.span("range.plane.start"):
+                rreqs = range_future.result()
+                if hasattr(self, "_prove_stream"):
+                    torch.cuda.current_stream(self.device).wait_stream(self._prove_stream)
+                if self.fault_plan:
+                    self.fault_plan.apply(rreqs, lambda pid: self.cluster.by_id(pid).keypair.secret)
+                early = pcp.start_range_plane(self, sq, rreqs)
+            range_future = None
         n_rows = n_groups * n_out
         net = self.net
         cn_ids = [si.id for si in sq.RosterServers.list]
@@ -300,7 +311,7 @@ class DrynxNode:
             self.fault_plan.apply(proofs, lambda pid: self.cluster.by_id(pid).keypair.secret)
         block = None
         if q.Proofs and q.RosterVNs is not None and len(q.RosterVNs.list):
-            block = pcp.proof_collection(self, sq, proofs)
+            block = pcp.proof_collection(self, sq, proofs, early)
         clear = {k: v["clear"] for k, v in dp_results.items()}
         out = SurveyResult(sq.SurveyID, result, n_groups, n_out, block, clear)
         if client_future is not None:
