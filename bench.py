@@ -100,6 +100,9 @@ def parse():
                     help="SurveyQuery.RangeProofMode: 0 reference semantics, 1 recomputed challenge + V in G2")
     ap.add_argument("--query", default="lr", choices=["lr", "lr_dro", *QUERY_CONFIGS],
                     help="lr = the headline; lr_dro = BASELINE.json config 4; mean/variance/lin_reg = configs 2 and 3")
+    ap.add_argument("--fault-dp", type=int, default=None,
+                    help="fault-injected run: DP k's range-proof payload is corrupted after proving and re-signed "
+                         "(one false proof among all); the bench then checks that every VN blames exactly that DP")
     ap.add_argument("--dro", type=int, default=None,
                     help="differential-privacy noise list size (DRO shuffle by every CN, with shuffle proofs); "
                          "--query lr_dro sets 10000 (the reference's DiffPri 10k row)")
@@ -129,6 +132,10 @@ def main():
 
     pool_note = (f"pooled over {world} ranks (single operator; helper verdicts bound to slice digests)"
                  if use_pool(node) and world > 1 else "each VN verifies on its own rank")
+    if args.fault_dp is not None:
+        from drynx_amd.utils.faults import FaultPlan
+
+        node.fault_plan = FaultPlan({(cl.dps[args.fault_dp].id, "range"): "corrupt_proof"})
     rec_per_dp = max(1, args.records // n_dps)
     d = args.features
     # the DP's database: generated once on its device (synthetic, random-init)
@@ -212,7 +219,13 @@ def main():
     verifs_per_step = proofs_per_step * n_vns  # threshold 1.0: every VN checks every proof
     ms = 1000.0 * elapsed / args.steps
     value = verifs_per_step * args.steps / elapsed
-    ok = all(b is not None and all(v == 1 for v in b.data_block().Proofs.values()) for b in blocks)
+    if args.fault_dp is not None:
+        # exactly the forged DP's range proof is false (code 0) at every VN; everything else true
+        bad = f"/range/{cl.dps[args.fault_dp].id}/"
+        ok = all(b is not None and all((v == 0) if bad in k else (v == 1) for k, v in b.data_block().Proofs.items())
+                 for b in blocks)
+    else:
+        ok = all(b is not None and all(v == 1 for v in b.data_block().Proofs.values()) for b in blocks)
     result_ok = _check_lr_results(comm, checks, lp, diffp)
     allt = comm.all_gather_object(timers.summary())
     if rank == 0:
@@ -262,6 +275,8 @@ def main():
             "e2e_latency_s": round(ms / 1000.0, 4),
             "latency_vs_reference_lr_spectf": round(REFERENCE_LR_SPECTF_S / (ms / 1000.0), 2),
             "all_proofs_valid": ok,
+            **({"fault_injected": f"{cl.dps[args.fault_dp].id} range proof corrupted and re-signed",
+                "blame_ok": ok} if args.fault_dp is not None else {}),
             "result_ok": result_ok,
             "setup_s": round(setup_s, 3),
             "first_query_s": round(first_s, 3),

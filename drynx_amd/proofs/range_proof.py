@@ -172,8 +172,11 @@ class SigMaterial:
         combs, 480 KiB per point, 64 additions) or 0 (no
         tables: variable-base G2 + one pairing per item).  Budgets:
         ``DRYNX_PROVER_TABLE_MB`` (8-bit, default 8 GiB on a GPU / 96 MiB on the
-        host) and ``DRYNX_PROVER_TABLE4_MB`` (4-bit, default 60% of the free HBM
-        / 64 MiB on the host)."""
+        host) and ``DRYNX_PROVER_TABLE4_MB`` (GLS / 4-bit layouts, default: the
+        free HBM minus the verifier's reserve ``DRYNX_VERIFY_RESERVE_GB`` = 48,
+        at most 85% of it / 64 MiB on the host): a 3-CN SPECTF-shaped set
+        (99,360 points) takes the GLS-8 layout (~111 GB), a 6-CN one (198,720
+        points) the GLS-6 one (~138 GB)."""
         dev = torch.device(device)
         key = ("mode", str(dev))
         if key in self._ptab:
@@ -184,7 +187,13 @@ class SigMaterial:
         if "DRYNX_PROVER_TABLE4_MB" in os.environ:
             b4 = int(os.environ["DRYNX_PROVER_TABLE4_MB"]) << 20
         elif dev.type == "cuda":
-            b4 = int(0.6 * torch.cuda.mem_get_info(dev)[0])
+            # the tables live as long as the signature set: what the rank keeps
+            # free for everything else -- the verifier's per-query working set
+            # (line / U images, bucket plans, joint tables: ~25 GB for a 1e6-item
+            # inbox) and the ledger's staging -- is reserved first
+            free = torch.cuda.mem_get_info(dev)[0]
+            reserve = int(float(os.environ.get("DRYNX_VERIFY_RESERVE_GB", "48")) * (1 << 30))
+            b4 = max(0, min(int(0.85 * free), free - reserve))
         else:
             b4 = 64 << 20
         if forced in ("0", "4", "6", "7", "8"):
