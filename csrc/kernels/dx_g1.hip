@@ -90,6 +90,18 @@ int dx_fr_dot_chunks(int on_gpu, void *stream, const uint32_t *a, const uint32_t
   return run(on_gpu, stream, groups * n_chunks, op, false, "fr_dot_chunks");
 }
 
+// Per-segment Fr sums: out[t] = sum_{offs[t] <= i < offs[t+1]} a[i] (canonical),
+// one lane per segment (segments are a batch's per-request slices: a few
+// dozen, each a few thousand rows already reduced by fr_dot_chunks).
+int dx_fr_seg_sum(int on_gpu, void *stream, const uint32_t *a, const int64_t *offs, uint32_t *out, int64_t k) {
+  auto op = [=] __host__ __device__(int64_t t) {
+    Fr acc = Fr::zero();
+    for (int64_t i = offs[t]; i < offs[t + 1]; i++) acc = fadd(acc, reduce_256<FrParams>(a + 8 * i));
+    at<Fr>(out, t) = acc;
+  };
+  return run(on_gpu, stream, k, op, false, "fr_seg_sum");
+}
+
 // ---------------------------------------------------------------- G1
 // Comb tables for n_bases points: table[b][w*256+d] = d * 2^(8w) * base_b (affine).
 // Two phases: (1) one thread per base walks the 256 doublings 2^k * base into

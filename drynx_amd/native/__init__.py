@@ -56,6 +56,7 @@ _SIGS = {
     "dx_fp_from_mont": [_I, _P, _P, _P, _L],
     "dx_fr_arith": [_I, _P, _I, _P, _P, _P, _L, _I],
     "dx_fr_dot_chunks": [_I, _P, _P, _P, _I, _P, _L, _L, _L],
+    "dx_fr_seg_sum": [_I, _P, _P, _P, _P, _L],
     "dx_rp_challenges": [_I, _P, _P, _P, _P, _P, _P, _L],
     "dx_g1_fb_table": [_I, _P, _P, _P, _P, _L],
     "dx_g1_fb_mul": [_I, _P, _P, _P, _P, _L],
@@ -281,6 +282,18 @@ def fr_dot_rows(a: torch.Tensor, b: torch.Tensor | None, groups: int, b_periodic
         if m == 1:
             return cur
 
+
+def fr_seg_sum(a: torch.Tensor, offs: torch.Tensor) -> torch.Tensor:
+    """Per-segment Fr sums of the rows of a: out[t] = sum a[offs[t]:offs[t+1]]
+    (canonical; offs int64 [k+1] on a's device, non-decreasing, <= rows)."""
+    k = offs.numel() - 1
+    assert k >= 0 and offs.dtype == torch.int64
+    out = torch.empty((k, 8), dtype=torch.int32, device=a.device)
+    if k:
+        offs = offs.to(a.device).contiguous()
+        g, s = _ctx(a, offs, out)
+        _call("dx_fr_seg_sum", g, s, _ptr(a.contiguous()), _ptr(offs), _ptr(out), k)
+    return out
 
 # ----------------------------------------------------------------------------- G1
 def g1_fb_table(base_aff: torch.Tensor) -> torch.Tensor:

@@ -689,14 +689,21 @@ def _gt_in_subgroup_each(g: torch.Tensor) -> list:
     return [bool(v) for v in nt.gt_eq(a, b).tolist()]
 
 
-def validate_list(r: RangeProofList, mode: int = 0, subgroup: bool | None = None, lazy: bool = False):
+class RangeInvalid(list):
+    """Verdict of a segmented batch rejected at decoding: per segment, whether
+    all its proofs decode (the batch equations were not evaluated; the valid
+    segments need a batch of their own)."""
+
+
+def validate_list(r: RangeProofList, mode: int = 0, subgroup: bool | None = None, lazy: bool = False,
+                  per_proof: bool = False):
     """Decoding checks of a (raw-limb or kyber-layout) proof list before any
     arithmetic on it: every coordinate below p and every scalar below r; the
     commitment (K, C) and D on G1; V in G2 (``subgroup``, default: mode >= 1)
     or only on the twist; every a_ij non-zero and in the cyclotomic subgroup.
     The prime-order part of a_ij is enforced by the batch equation plus each
     VN's independent random combination tested in GT.  ``lazy``: return the
-    verdict as a device bool (no host sync)."""
+    verdict as a device bool (no host sync); ``per_proof``: a bool per proof."""
     if subgroup is None:
         subgroup = mode >= 1
     fp = lambda t: nt.limbs_canonical(t.reshape(-1, 8))  # noqa: E731
@@ -705,6 +712,10 @@ def validate_list(r: RangeProofList, mode: int = 0, subgroup: bool | None = None
     if r.has_rp and len(r):
         flags += [fp(r.D), nt.g1j_on_curve(r.D), fr(r.challenge), fr(r.zr), fr(r.zphi), fr(r.zv), fp(r.V), fp(r.A),
                   nt.g2_subgroup(r.V) if subgroup else nt.g2_on_curve(r.V), nt.gt_cyclotomic(r.A)]
+    if per_proof:  # every array is proof-major with a fixed number of rows per proof
+        n = len(r)
+        ok = torch.stack([f.bool().view(n, -1).all(dim=1) for f in flags]).all(dim=0)
+        return ok if lazy else ok.tolist()
     ok = torch.stack([f.bool().all() for f in flags]).all()
     return ok if lazy else bool(ok)
 
@@ -726,7 +737,7 @@ def verify_range_proof_list(rpl: RangeProofList, sigmat: SigMaterial, P_point, t
 
 
 def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_point, n_vn: int = 1, device=None,
-                                  mode: int = 0, coins: list | None = None) -> list:
+                                  mode: int = 0, coins: list | None = None, segs: list | None = None) -> list:
     """``n_vn`` independent batch verifications of one proof list -- one per
     verifying node hosted on this rank, each with its own random weights
     drawn from its own ``coins[v]`` (crypto/coins.py; fresh CSPRNG output
@@ -745,15 +756,29 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
     queued back to back (no host round trip between them) while the
     bucket-method MSM / multi-exponentiations run on a side stream; the
     closing single-element work (final exponentiations, Horner steps) runs
-    on the host, where one core beats one GPU lane.  -> [bool] per VN."""
+    on the host, where one core beats one GPU lane.  -> [bool] per VN.
+
+    ``segs`` (proof counts summing to len(r): the batch's per-request
+    slices) asks for attribution: -> per VN a [bool] per segment, None when
+    a failed batch cannot be attributed (the "fold" verifier), or a
+    ``RangeInvalid`` (per segment: decodes) when some proofs do not decode.  The U side is then laid out per segment
+    (each segment's U_q start whole accumulation workgroups, so each has its
+    own Miller partial products -- no extra pairing work), and only a VN
+    whose batch FAILS pays a second, segment-grouped pass over the cheap
+    sides (R MSM, multi-exponentiation, D-check, exponent sums) with the same
+    weights: blame costs ~one VN's MSMs, not a bisection of re-verifications."""
+    nseg = len(segs) if segs else 1
+    if segs is not None:
+        assert sum(segs) == len(r) and all(c > 0 for c in segs)
     if not r.has_rp or len(r) == 0:
-        return [True] * n_vn
+        return [True] * n_vn if segs is None else [[True] * nseg for _ in range(n_vn)]
+    fail = [False] * n_vn if segs is None else [None] * n_vn
     device = torch.device(device or r.commit.device)
     r = r.to(device)
     n, l, S, u = len(r), r.l, r.S, r.u
     if r.zphi.shape[0] != n * l or r.zv.shape[0] != n * S * l or r.V.shape[0] != n * S * l \
             or r.A.shape[0] != n * S * l or r.challenge.shape[0] != n:
-        return [False] * n_vn
+        return fail
     # pairing side: "msm" regroups the product by bilinearity (one G2 MSM and
     # n*S L-point combinations per VN, n*S + 1 Miller loops); "fold"
     # (DRYNX_RPV=fold) runs one Miller loop per item, as the reference's
@@ -764,19 +789,25 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
         # verifier's host-side plans leave, and are read back with the
         # verdicts (work done meanwhile on invalid data is discarded)
         vstream = _val_stream(device) if device.type == "cuda" else None
+        pp = segs is not None
+        chk = None
         if vstream is not None:
             vstream.wait_stream(torch.cuda.current_stream(device))
             with torch.cuda.stream(vstream):
-                valid = validate_list(r, mode, lazy=True)
-        elif not validate_list(r, mode):
-            return [False] * n_vn
+                valid = validate_list(r, mode, lazy=True, per_proof=pp)
         else:
-            valid = True
+            valid = validate_list(r, mode, lazy=True, per_proof=pp)
+            if not bool(valid.all()) and (segs is None or not use_msm):
+                return _invalid(valid, segs, n_vn)
     if mode >= 1:
         with timers.span("rp.verify.challenge"):
-            if not torch.equal(challenges(r.commit.C, r.cols, sigmat, device, mode, r.D, r.V, r.A, S, l),
-                               r.challenge):
-                return [False] * n_vn
+            ch_ok = (challenges(r.commit.C, r.cols, sigmat, device, mode, r.D, r.V, r.A, S, l)
+                     == r.challenge).all(dim=1)
+            if segs is None or not use_msm:
+                if not bool(ch_ok.all()):
+                    return _invalid(ch_ok, segs, n_vn)
+            else:
+                chk = ch_ok                    # a wrong challenge fails its own segment (attributed below)
     tabB = bn.base_table(device)
     # --- shared, weight-free inputs
     Cp = r.commit.C                                                    # C' = C + offset*B
@@ -821,9 +852,9 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
             # bucket plans (host syncs) and the R passes go to the high-priority
             # aux stream, whose short plan kernels then overtake the U kernels
             with timers.span("rp.verify.msm_queue"):
-                msq = _msm_queue(Y, r.V, ab_all, G, n, S, l, vstream)
-                for v, fb, uok in zip(vns, msq["fb"], msq["u_ok"]):
-                    v["fb"], v["u_ok"] = fb, uok
+                msq = _msm_queue(Y, r.V, ab_all, G, n, S, l, vstream, segs)
+                for v, uok in zip(vns, msq["u_ok"]):
+                    v["u_ok"] = uok
         else:
             with timers.span("rp.verify.fold_queue"):
                 for v, fb in zip(vns, _miller_fold_multi(ZB, Y, [v["rho"] for v in vns], r.V, S, l,
@@ -866,8 +897,13 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
             D_all = nt.g1_msm_finish(dcheck)                           # [2G, 24]
             e_all, dfull = e_all.cpu(), dfull.cpu()
         with timers.span("rp.verify.fold_wait"):
-            for v in vns:
-                v["F"] = nt._finish_prod_on_host(v["fb"])
+            if use_msm:
+                useg = _seg_products(msq)                              # [G, nseg, 96] host
+                for k_, v in enumerate(vns):
+                    v["F"] = nt.gt_prod(useg[k_].view(nseg, 1, 96), chunk=4).view(1, 96)
+            else:
+                for v in vns:
+                    v["F"] = nt._finish_prod_on_host(v["fb"])
             if use_msm:
                 fR, rok = _msm_r_miller(hR, S_R)
                 for v, f, ok in zip(vns, fR, rok):
@@ -876,10 +912,11 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
         GG = nt.multi_exp_grouped_finish(mexp)
         if use_msm:
             hR = _msm_plan(r.zphi, r.V, rho_all, G, n, S, l)
-            msq = _msm_queue(Y, r.V, ab_all, G, n, S, l)
+            msq = _msm_queue(Y, r.V, ab_all, G, n, S, l, None, segs)
             fR, rok = _msm_r_miller(hR, nt.g2_msm_run(r.V, hR))
-            for v, fb, f, ok, uok in zip(vns, msq["fb"], fR, rok, msq["u_ok"]):
-                v["F"] = nt.gt_mul(nt.gt_prod(fb.view(-1, 1, 96), chunk=4).view(1, 96), f.view(1, 96))
+            useg = _seg_products(msq)
+            for k_, (v, f, ok, uok) in enumerate(zip(vns, fR, rok, msq["u_ok"])):
+                v["F"] = nt.gt_mul(nt.gt_prod(useg[k_].view(nseg, 1, 96), chunk=4).view(1, 96), f.view(1, 96))
                 v["r_ok"], v["u_ok"] = ok, uok
         else:
             T = _fold_points(ZB, Y, S, l)
@@ -893,8 +930,11 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
         v.update(G=GG[k: k + 1], dfull=dfull[k], e=e_all[k: k + 1], dcheck=D_all[2 * k: 2 * k + 2])
     if vstream is not None:
         vstream.synchronize()
-        if not bool(valid):
-            return [False] * n_vn
+    if chk is not None:
+        valid = valid & chk
+    if vstream is not None:
+        if not bool(valid.all()) and (segs is None or not use_msm):
+            return _invalid(valid, segs, n_vn)
     out = []
     # prime-order part of the a_ij: each VN's own independent 40-bit
     # combination in GT (the smallest prime factor of the cyclotomic cofactor
@@ -916,7 +956,26 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
         # where the pairing is bilinear and the regrouping exact
         g2_ok = bool(v.get("u_ok", True)) and bool(v.get("r_ok", True))
         out.append(d_ok and m_oks[len(out)] and eq_ok and g2_ok)
-    return out
+    if segs is None:
+        return out
+    # attribution: a passing batch clears every segment; a failing one gets
+    # the segment-grouped second pass.  Undecodable proofs fail their own
+    # segments only: every per-segment quantity (U_q, the fold blocks, R_s,
+    # prod a^rho, the D-check) involves that segment's data alone
+    seg_valid = None if bool(valid.all()) else _seg_all(valid.view(1, -1), segs, valid.device).view(-1).tolist()
+    redo = [k_ for k_ in range(G) if not out[k_] or seg_valid is not None]
+    res = [[True] * nseg if ok else None for ok in out]
+    if redo:
+        with timers.span("rp.verify.segments"):
+            per = _segment_pass(r, segs, redo, dict(
+                A2=A2, rho=rho_all, ab=ab_all, gam=gam_all, w=w_all, Cp=Cp, z=z, useg=useg, u_seg=msq["u_seg"],
+                PB_base=PB_base, gt_tab=gt_tab, wc=wc_))
+        for k_ in redo:
+            if seg_valid is not None:
+                res[k_] = [a and b for a, b in zip(per[k_], seg_valid)]
+            else:
+                res[k_] = per[k_] if not all(per[k_]) else None  # nothing attributable: the caller bisects
+    return res
 
 
 class _nullctx:
@@ -938,7 +997,7 @@ def _msm_plan(zphi, V, rho_all, G: int, n: int, S: int, L: int) -> dict:
     return nt.g2_msm_launch(V, s_r, m, G)                              # group (VN) = row // m
 
 
-def _msm_queue(Y, V, ab_all, G: int, n: int, S: int, L: int, vstream=None) -> dict:
+def _msm_queue(Y, V, ab_all, G: int, n: int, S: int, L: int, vstream=None, segs: list | None = None) -> dict:
     """Verifier mode "msm", the U side (no host sync; csrc/kernels/dx_rpmsm.hip):
     the pairing side of G verifiers' batches regrouped by bilinearity,
         prod_it ML(rho_it (Zphi_pj B - Y_pi), V_it)
@@ -947,38 +1006,182 @@ def _msm_queue(Y, V, ab_all, G: int, n: int, S: int, L: int, vstream=None) -> di
     ladder over the 15-entry per-V table shared by the VNs) and R_v the
     Pippenger G2 MSM of ``_msm_plan`` (queued separately: ``nt.g2_msm_run``,
     finished by ``_msm_r_miller``).  GPU: the U's of all VNs form one list
-    (VN-major, blocks padded to whole accumulation workgroups) that the
-    normalised fold kernels pair with uv(-Y_q) -> each VN's per-workgroup
-    partial products ("fb"); host: per-item Miller loops over the same pairs."""
+    (VN-major; with ``segs``, each segment's U's start a whole accumulation
+    workgroup) that the normalised fold kernels pair with uv(-Y_q) -> per-
+    workgroup partial products ("fb"), reduced per (VN, segment) by
+    ``_seg_products``; host: per-item Miller loops over the same pairs.
+    "u_seg": [G, n_segments] exact G2 membership of every segment's U's."""
     dev = V.device
     nq = n * S
+    nseg = len(segs) if segs else 1
+    qoff = np.cumsum([0] + [c * S for c in segs]) if segs else np.array([0, nq])
+    cq = np.diff(qoff)
     table = nt.g2_joint_table(V)
-    out = {}
+    out = {"G": G}
     if dev.type == "cuda":
-        K = fold_k(G * (nq + 1))
-        pad = -(-(nq + 1) // (64 * K)) * (64 * K)
-        period = -(-(G * pad) // (64 * K * nt.FOLD_P_ALIGN)) * (64 * K * nt.FOLD_P_ALIGN)
+        if nseg == 1:
+            K = fold_k(G * (nq + 1))
+            rows = 64 * K
+            pad = -(-(nq + 1) // rows) * rows
+        else:
+            K = fold_k(G * nq)
+            rows = 64 * K
+            ac = -(-cq // rows) * rows                              # segments start whole workgroups
+            segbase = np.cumsum(ac) - ac
+            pad = int(ac.sum())
+        period = -(-(G * pad) // (rows * nt.FOLD_P_ALIGN)) * (rows * nt.FOLD_P_ALIGN)
         Uall = torch.zeros((G * pad, 32), dtype=torch.int32, device=dev)
-        nt.rp_u_joint(table, ab_all, nq, G, L, Uall, pad)
+        UV = torch.zeros((period, 16), dtype=torch.int32, device=dev)
+        if nseg == 1:
+            nt.rp_u_joint(table, ab_all, nq, G, L, Uall, pad)
+            nt.rp_msm_uv(Y, UV, nq, G, pad)
+            Ud = Uall
+        else:
+            Ud = torch.empty((G * nq, 32), dtype=torch.int32, device=dev)
+            nt.rp_u_joint(table, ab_all, nq, G, L, Ud, nq)
+            UVd = torch.zeros((G * (nq + 1), 16), dtype=torch.int32, device=dev)
+            nt.rp_msm_uv(Y, UVd, nq, G, nq + 1)
+            qseg = torch.repeat_interleave(torch.arange(nseg, device=dev), torch.from_numpy(cq).to(dev),
+                                           output_size=nq)
+            qpos = torch.from_numpy(segbase).to(dev)[qseg] + torch.arange(nq, device=dev) \
+                - torch.from_numpy(qoff[:-1]).to(dev)[qseg]
+            pos = (torch.arange(G, device=dev).view(G, 1) * pad + qpos.view(1, nq)).reshape(-1)
+            Uall.index_copy_(0, pos, Ud)
+            UV.index_copy_(0, pos, UVd.view(G, nq + 1, 16)[:, :nq].reshape(-1, 16))
         # G2 membership of every U (exact test), on the validation stream beside the fold
         cur = torch.cuda.current_stream(dev)
         vs = vstream if vstream is not None else cur
         vs.wait_stream(cur)
         with torch.cuda.stream(vs):
-            fl = nt.g2_subgroup(Uall).view(G, pad)[:, :nq].bool().all(dim=1)
-        Uall.record_stream(vs)
-        out["u_ok"] = list(fl.unbind(0))
-        UV = torch.zeros((period, 16), dtype=torch.int32, device=dev)
-        nt.rp_msm_uv(Y, UV, nq, G, pad)
-        fb = nt.rp_fold_accum_n(nt.rp_fold_ncoeffs(Uall), UV, Uall, period, 1, K)
-        blk = pad // (64 * K)
-        out["fb"] = [fb[v * blk:(v + 1) * blk] for v in range(G)]
+            fl = nt.g2_subgroup(Ud).view(G, -1)[:, :nq].bool()
+            out["u_seg"] = _seg_all(fl, cq, dev)
+        Ud.record_stream(vs)
+        out["u_ok"] = list(out["u_seg"].all(dim=1).unbind(0))
+        out["fb"] = nt.rp_fold_accum_n(nt.rp_fold_ncoeffs(Uall), UV, Uall, period, 1, K)
+        out["blk"] = pad // rows
+        out["sb"] = [0] if nseg == 1 else (segbase // rows).tolist()
+        out["nb"] = [pad // rows] if nseg == 1 else (ac // rows).tolist()
     else:
         Uall = torch.zeros((G * nq, 32), dtype=torch.int32, device=dev)
         nt.rp_u_joint(table, ab_all, nq, G, L, Uall, nq)
-        out["u_ok"] = [bool(x) for x in nt.g2_subgroup(Uall).view(G, nq).bool().all(dim=1).tolist()]
+        out["u_seg"] = _seg_all(nt.g2_subgroup(Uall).view(G, nq).bool(), cq, dev)
+        out["u_ok"] = [bool(x) for x in out["u_seg"].all(dim=1).tolist()]
         negY = nt.g1_to_affine(nt.g1_add(bn.g1_infinity_jac(nq, dev), Y.contiguous(), subtract=True))
-        out["fb"] = [nt.miller_loop(negY, Uall[v * nq:(v + 1) * nq].contiguous()) for v in range(G)]
+        out["fb"] = torch.cat([nt.miller_loop(negY, Uall[v * nq:(v + 1) * nq].contiguous()) for v in range(G)])
+        out["blk"], out["sb"], out["nb"] = nq, qoff[:-1].tolist(), cq.tolist()
+    return out
+
+
+def _invalid(valid: torch.Tensor, segs, n_vn: int) -> list:
+    if segs is None:
+        return [False] * n_vn
+    seg_ok = _seg_all(valid.view(1, -1), segs, valid.device).view(-1).tolist()
+    return [RangeInvalid(seg_ok) for _ in range(n_vn)]
+
+
+def _seg_all(flags: torch.Tensor, counts, dev) -> torch.Tensor:
+    """[G, k] bool: all(flags[v, run s]) for the consecutive runs of ``counts``."""
+    G, nq = flags.shape
+    k = len(counts)
+    if k == 1:
+        return flags.all(dim=1).view(G, 1)
+    sid = torch.repeat_interleave(torch.arange(k, device=dev), torch.as_tensor(counts, device=dev), output_size=nq)
+    bad = torch.zeros((G, k), dtype=torch.int32, device=dev)
+    bad.index_add_(1, sid, (~flags).to(torch.int32))
+    return bad == 0
+
+
+def _seg_products(msq: dict) -> torch.Tensor:
+    """Per-(VN, segment) products of the fold partials -> host [G, k, 96]:
+    the blocks of every (VN, segment) gathered into one [blocks, G k] image
+    (short segments padded with ones), 8-way device levels, then the host."""
+    fb, G, blk, sb, nb = msq["fb"], msq["G"], msq["blk"], msq["sb"], msq["nb"]
+    k = len(sb)
+    dev = fb.device
+    maxb = max(nb)
+    b = torch.arange(maxb, device=dev).view(maxb, 1, 1)
+    base = (torch.arange(G, device=dev).view(1, G, 1) * blk + torch.as_tensor(sb, device=dev).view(1, 1, k))
+    idx = torch.where(b < torch.as_tensor(nb, device=dev).view(1, 1, k), base + b, fb.shape[0])
+    ext = torch.cat([fb, nt.gt_one(dev)])
+    x = ext.index_select(0, idx.reshape(-1)).view(maxb, G * k, 96)
+    if dev.type == "cuda":
+        while x.shape[0] > 8:
+            x = nt._gt_prod_level(x, 8)
+    return nt.gt_prod(x.cpu(), chunk=4).view(G, k, 96)
+
+
+def _seg_c(n_entries: int, n_groups: int, bits: int = 254) -> int:
+    """Window of a grouped G2 MSM: entries x windows bucket additions plus
+    ~36 G2 operations per (group, window, digit) bucket weight."""
+    return min(range(6, 14), key=lambda c: -(-bits // c) * (n_entries + n_groups * (1 << c) * 36))
+
+
+def _segment_pass(r: RangeProofList, segs: list, redo: list, x: dict) -> dict:
+    """Second, segment-grouped pass for the VNs ``redo`` whose batch failed:
+    with the SAME weights, every side of the batch equation per (VN,
+    segment) -- R MSM, prod a^rho, sum rho Zv, D-check, GT membership -- in
+    one grouped MSM / multi-exponentiation each; the U side's per-segment products come from
+    the first pass.  -> {vn: [bool] per segment}."""
+    dev = r.V.device
+    n, S, l = len(r), r.S, r.l
+    m, nseg, Gf = n * S * l, len(segs), len(redo)
+    K = Gf * nseg
+    poff = np.cumsum([0] + list(segs))
+    pseg = torch.repeat_interleave(torch.arange(nseg, device=dev), torch.as_tensor(segs, device=dev), output_size=n)
+    iseg = pseg.repeat_interleave(S * l)
+    fi = torch.arange(Gf, device=dev).view(Gf, 1)
+    def rows(t, w):
+        return torch.cat([t[v * w:(v + 1) * w] for v in redo]) if Gf > 1 else t[redo[0] * w:(redo[0] + 1) * w]
+
+    rho, ab, w = rows(x["rho"], m), rows(x["ab"], m), rows(x["w"], n)
+    # R_(v,s) = sum_{it in s} rho_it Zphi_(p,j) V_it
+    it = torch.arange(m, device=dev)
+    zi = (it // (S * l)) * l + it % l
+    s_r = nt.fr_arith(nt.FR_MUL, rho, r.zphi.index_select(0, zi).repeat(Gf, 1).contiguous())
+    grp = (fi * nseg + iseg.view(1, m)).reshape(-1).to(torch.int32)
+    hR = nt.g2_msm_launch(r.V, s_r, grp, K, c=_seg_c(Gf * m, K))
+    S_R = nt.g2_msm_run(r.V, hR)
+    # prod a^rho per (v, s) (32-bit halves over (A, frob^8 A)) and each
+    # segment's own GT-membership combination prod a^gamma (the VN's gammas)
+    k = torch.zeros((2 * Gf, 2 * m, 8), dtype=torch.int32, device=dev)
+    abv = ab.view(Gf, m, 2)
+    k[:Gf, :m, 0] = abv[:, :, 0]
+    k[:Gf, m:, 0] = abv[:, :, 1]
+    k[Gf:, :m] = rows(x["gam"], m).view(Gf, m, 8)
+    fi2 = torch.arange(2 * Gf, device=dev).view(2 * Gf, 1)
+    grp2 = (fi2 * nseg + iseg.repeat(2).view(1, 2 * m)).reshape(-1).to(torch.int32)
+    mexp = nt.multi_exp_grouped(x["A2"], k.view(-1, 8), grp2, 2 * K, W=x["wc"][0], c=x["wc"][1])
+    # sum rho Zv, sum w Zr, sum w z per (v, s): per-proof sums, then per-segment
+    offs = torch.from_numpy((np.arange(Gf).reshape(Gf, 1) * n + poff[:-1].reshape(1, nseg)).reshape(-1))
+    offs = torch.cat([offs, torch.tensor([Gf * n])]).to(dev)
+    e = nt.fr_seg_sum(nt.fr_dot_rows(rho, r.zv.repeat(Gf, 1).contiguous(), Gf * n), offs)
+    dzr = nt.fr_seg_sum(nt.fr_arith(nt.FR_MUL, w, r.zr.repeat(Gf, 1).contiguous()), offs)
+    dz = nt.fr_seg_sum(nt.fr_arith(nt.FR_MUL, w, x["z"].repeat(Gf, 1).contiguous()), offs)
+    # D-check per (v, s): sum w c C' - sum w D (groups (v, which, s))
+    wc = nt.fr_arith(nt.FR_MUL, w, r.challenge.repeat(Gf, 1).contiguous())
+    dsc = torch.stack([wc.view(Gf, n, 8), w.view(Gf, n, 8)], 1).reshape(-1, 8).contiguous()
+    grp3 = ((fi.view(Gf, 1, 1) * 2 + torch.arange(2, device=dev).view(1, 2, 1)) * nseg
+            + pseg.view(1, 1, n)).reshape(-1).to(torch.int32)
+    dpts = torch.cat([x["Cp"].contiguous(), r.D.contiguous()]).repeat(Gf, 1)
+    dh = nt.g1_msm_launch(dpts, dsc, grp3, 2 * K, bits=256)
+    # host: Horner steps, Miller loops of B with each R_(v,s), final exps
+    GG = nt.multi_exp_grouped_finish(mexp)                             # [2K, 96]
+    m_ok = _gt_in_subgroup_each(GG[K:])
+    GG = GG[:K]
+    fR, rok = _msm_r_miller(hR, S_R)
+    D_all = nt.g1_msm_finish(dh).view(Gf, 2, nseg, 24)
+    e, dzr, dz = e.cpu(), dzr.cpu(), dz.cpu()
+    useg = torch.stack([x["useg"][v] for v in redo]).view(K, 96)
+    useg_ok = x["u_seg"].cpu()[redo].reshape(-1).tolist()
+    lhs = nt.gt_mul(nt.final_exp(nt.gt_mul(useg.contiguous(), fR.contiguous())), GG.contiguous())
+    eq = nt.gt_eq(lhs, nt.gt_fb_pow(x["gt_tab"], e)).tolist()
+    PB = nt.g1_mul(x["PB_base"].repeat(K, 1), torch.stack([dzr, dz], 1).reshape(-1, 8).contiguous()).view(K, 2, 24)
+    lhs_d = nt.g1_sum(torch.stack([D_all[:, 0].reshape(K, 24), PB[:, 0], PB[:, 1]]).contiguous())
+    d_ok = nt.g1_eq(lhs_d.contiguous(), D_all[:, 1].reshape(K, 24).contiguous()).tolist()
+    out = {}
+    for f, v in enumerate(redo):
+        out[v] = [bool(eq[f * nseg + s_]) and bool(d_ok[f * nseg + s_]) and bool(useg_ok[f * nseg + s_])
+                  and bool(rok[f * nseg + s_]) and m_ok[f * nseg + s_] for s_ in range(nseg)]
     return out
 
 

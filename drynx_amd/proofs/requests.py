@@ -606,14 +606,7 @@ def _verify_range_group(reqs, idxs, sq, device, cache, part, coins_list: list) -
     if not live:
         return outs
     sigmat = cache.sigmat(sq, device)
-    oks = _check_lists(live, parts, sigmat, P, device, mode, coins_list)
-    for k in range(n_vn):
-        if oks[k] or len(live) == 1:
-            for i in live:
-                outs[k][i] = oks[k]
-            continue
-        with timers.span("rp.verify.blame"):
-            bad = _blame(live, parts, sigmat, P, device, mode, coins_list[k])
+    for k, bad in enumerate(_bad_requests(live, parts, sigmat, P, device, mode, coins_list)):
         for i in live:
             outs[k][i] = i not in bad
     return outs
@@ -642,15 +635,80 @@ def verify_range_pool_part(reqs: list, vn_idxs: dict, sq, device, cache: Verifie
         if live:
             sigmat = cache.sigmat(sq, device)
             cl = [coins.get(vn) for vn in group]
-            oks = _check_lists(live, parts, sigmat, P, device, mode, cl)
-            for k, vn in enumerate(group):
-                bad = set() if oks[k] else (_blame(live, parts, sigmat, P, device, mode, cl[k])
-                                            if len(live) > 1 else set(live))
+            for k, bad in enumerate(_bad_requests(live, parts, sigmat, P, device, mode, cl)):
                 for i in live:
                     res[k][i] = i not in bad
         for vn, rv in zip(group, res):
             out[vn] = rv
     return out, digests
+
+
+_SEG_MAX = 64  # attribution segments per batch (more requests: chunks of requests)
+
+
+def _bad_requests(live, parts, sigmat, P, device, mode, coins_list) -> list:
+    """The requests of ``live`` each VN rejects -> [set] per VN.  One batch
+    per (u, l, S) group with per-request attribution (rp.verify_range_proof_
+    list_multi ``segs``): a passing batch clears everything at once; a
+    failing one names its bad segments from a second, segment-grouped pass of
+    the failing VN alone.  Only what attribution cannot settle (a segment
+    holding several requests when there are more than _SEG_MAX, or a batch
+    rejected before the equations) falls back to bisection."""
+    n_vn = len(coins_list)
+    if len(live) == 1:
+        return [set() if ok else set(live) for ok in _check_lists(live, parts, sigmat, P, device, mode, coins_list)]
+    units = [[i] for i in live] if len(live) <= _SEG_MAX else \
+        [list(c) for c in np.array_split(np.asarray(live), _SEG_MAX) if len(c)]
+    groups: dict = {}
+    for ui, unit in enumerate(units):
+        for i in unit:
+            for r in parts[i]:
+                if len(r):
+                    lists, cnt = groups.setdefault((r.u, r.l, r.S), ([], {}))
+                    lists.append(r)
+                    cnt[ui] = cnt.get(ui, 0) + len(r)
+    bad = [set() for _ in range(n_vn)]
+    unsure = [set() for _ in range(n_vn)]
+    recheck: set = set()
+    try:
+        for lists, cnt in groups.values():
+            with timers.span("rp.verify.cat"):
+                c = rp.rpl_cat(lists)
+            uids = list(cnt)
+            res = rp.verify_range_proof_list_multi(c, sigmat, P, n_vn, device, mode, coins=coins_list,
+                                                   segs=[cnt[u] for u in uids])
+            if isinstance(res[0], rp.RangeInvalid):
+                # some proofs do not decode: their requests are bad for every VN,
+                # the others get a batch without them
+                for u, ok in zip(uids, res[0]):
+                    if ok:
+                        recheck.update(int(i) for i in units[u])
+                    elif len(units[u]) == 1:
+                        for b in bad:
+                            b.add(int(units[u][0]))
+                    else:
+                        for us in unsure:
+                            us.update(int(i) for i in units[u])
+                continue
+            for k, rk in enumerate(res):
+                for u, ok in zip(uids, rk if rk is not None else [None] * len(uids)):
+                    if ok is None or (not ok and len(units[u]) > 1):
+                        unsure[k].update(int(i) for i in units[u])
+                    elif not ok:
+                        bad[k].add(int(units[u][0]))
+    except Exception as e:
+        log.warning(f"batched range verification failed: {e}")
+        return [set(int(i) for i in live) for _ in range(n_vn)]
+    recheck -= set().union(*bad, *unsure)
+    if recheck:  # the decodable requests of a batch that held undecodable ones
+        for b, more in zip(bad, _bad_requests(sorted(recheck), parts, sigmat, P, device, mode, coins_list)):
+            b |= more
+    for k in range(n_vn):
+        rest = sorted(unsure[k] - bad[k])
+        if rest:
+            with timers.span("rp.verify.blame"):
+                bad[k] |= _blame(rest, parts, sigmat, P, device, mode, coins_list[k])
+    return bad
 
 
 def _check_lists(live, parts, sigmat, P, device, mode, coins_list) -> list:

@@ -143,16 +143,6 @@ def _msm_is_zero(points: list, scalars: list) -> bool:
     return not bool(res[0, 16:24].any())
 
 
-def _fr_sum(x: torch.Tensor) -> torch.Tensor:
-    """[m, 8] -> [1, 8] Fr sum (pairwise tree on the device)."""
-    cur = x
-    while cur.shape[0] > 1:
-        if cur.shape[0] % 2:
-            cur = torch.cat([cur, torch.zeros((1, 8), dtype=torch.int32, device=cur.device)])
-        cur = nt.fr_arith(nt.FR_ADD, cur[0::2].contiguous(), cur[1::2].contiguous())
-    return cur
-
-
 def _sc(vals, device):
     return bn.scalars_tensor(vals, device)
 
@@ -209,6 +199,9 @@ def schnorr_verify(public, msg: bytes, sig: bytes) -> bool:
     return lhs == O.g1_add(R, bn.g1_mul_point(e, public))
 
 
+_SIG_DEVICE_MIN = 256
+
+
 def schnorr_verify_batch(items: list, device="cpu") -> list:
     """schnorr_verify over many (public, msg, sig) at once: s_i B by one
     fixed-base launch, e_i X_i by one variable-base launch, one addition and
@@ -234,7 +227,9 @@ def schnorr_verify_batch(items: list, device="cpu") -> list:
         e.append(int.from_bytes(hashlib.sha256(sig[:64] + O.g1_to_bytes(public) + msg).digest(), "big") % O.R)
     if not idx:
         return out
-    dev = torch.device(device)
+    # a VN inbox of a few dozen envelopes verifies on the host pool: a GPU
+    # launch chain plus its read-back costs more than the products themselves
+    dev = torch.device(device) if len(idx) >= _SIG_DEVICE_MIN else torch.device("cpu")
     lhs = nt.g1_fb_mul(bn.base_table(dev), _sc(s, dev))
     rhs = nt.g1_add(bn.g1_jac_tensor(R, dev), nt.g1_mul(bn.g1_jac_tensor(X, dev), _sc(e, dev)))
     ok = nt.g1_eq(lhs, rhs).cpu().tolist()
@@ -630,39 +625,36 @@ def _ks_combined(live, n_vn: int = 1, coins=None):
     """Grouped MSM: every per-element weight stays 64 bit (8 bucket additions
     per point instead of 32); the per-proof challenges c, zb multiply the five
     group sums of each proof on the host.  -> [bool] (``n_vn`` independent
-    combinations, fresh weights each, sharing the one MSM launch)."""
+    combinations, fresh weights each, sharing the one MSM launch).  Each VN's
+    weights are ONE draw from its coins ([rho | sig] over every live proof);
+    the points, the weight selection and the groups are built once."""
     dev = live[0][1].K.device
     nl = len(live)
-    pts, scs, grp = [], [], []
-    sB, sQ = [], []
     cl = coins if isinstance(coins, (list, tuple)) else [coins] * n_vn
-    for v in range(n_vn):
-        for j, (_, pr, k) in enumerate(live):
-            rho, sig = _rand64(k, dev, cl[v]), _rand64(k, dev, cl[v])
-            za = pr.za[:k].contiguous()
-            # group 5j+0: rho T1, +1: rho vB, +2: sig K (x zb), +3: sig T2, +4: sig (vQ - xK) (x c)
-            for gi, (pt, w) in enumerate(((pr.T1, rho), (pr.share.K, rho), (pr.K, sig), (pr.T2, sig),
-                                          (pr.share.C, sig))):
-                pts.append(pt[:k])
-                scs.append(w)
-                grp.append(torch.full((k,), (v * nl + j) * 5 + gi, dtype=torch.int32, device=dev))
-            sB.append(_fr_sum(nt.fr_arith(nt.FR_MUL, rho, za)))
-            sQ.append(_fr_sum(nt.fr_arith(nt.FR_MUL, sig, za)))
-    G = nt.g1_msm_grouped(torch.cat(pts).contiguous(), torch.cat(scs).contiguous(), torch.cat(grp),
+    ks = [k for _, _, k in live]
+    kt = sum(ks)
+    offs = np.cumsum([0] + ks)
+    # rows in (proof j, role gi) order -- gi 0: rho T1, 1: rho vB, 2: sig K (x zb), 3: sig T2,
+    # 4: sig (vQ - xK) (x c) -- each row's weight index in [rho | sig] and its group
+    pts = torch.cat([pt[:k] for _, pr, k in live for pt in (pr.T1, pr.share.K, pr.K, pr.T2, pr.share.C)])
+    sel = np.concatenate([(0 if gi < 2 else kt) + offs[j] + np.arange(k) for j, k in enumerate(ks) for gi in range(5)])
+    grp1 = np.concatenate([np.full(k, 5 * j + gi) for j, k in enumerate(ks) for gi in range(5)])
+    za = torch.cat([pr.za[:k] for _, pr, k in live]).contiguous()
+    W = torch.cat([_rand64(2 * kt, dev, c) for c in cl])                      # [n_vn * 2kt, 8]
+    scs = W.view(n_vn, 2 * kt, 8).index_select(1, torch.from_numpy(sel).to(dev)).reshape(-1, 8).contiguous()
+    grp = (np.arange(n_vn).reshape(-1, 1) * (5 * nl) + grp1.reshape(1, -1)).reshape(-1)
+    G = nt.g1_msm_grouped(pts.contiguous().repeat(n_vn, 1), scs, torch.from_numpy(grp.astype(np.int32)).to(dev),
                           5 * nl * n_vn, bits=64)
+    full = nt.fr_dot_rows(W, za, 2 * n_vn, b_periodic=True).cpu()           # [sum rho za, sum sig za] per VN
     Q = live[0][1].Q
+    facs = _sc([f for _, pr, _ in live for f in (1, pr.c, pr.zb, 1, pr.c)], "cpu")
+    BQ = bn.g1_jac_tensor([O.G1_GEN, Q], "cpu")
     out = []
     for v in range(n_vn):
-        full = torch.cat([_fr_sum(torch.cat(sB[v * nl:(v + 1) * nl])),
-                          _fr_sum(torch.cat(sQ[v * nl:(v + 1) * nl]))]).cpu()
         # lhs = (sum rho za) B + (sum sig za) Q; rhs = sum_j G0 + c G1 + zb G2 + G3 + c G4
-        lhs = nt.g1_add(*nt.g1_mul(bn.g1_jac_tensor([O.G1_GEN, Q], "cpu"), full).split(1))
-        facs, fpts = [], []
-        for j, (_, pr, _) in enumerate(live):
-            g = G[5 * (v * nl + j): 5 * (v * nl + j) + 5]
-            facs += [1, pr.c, pr.zb, 1, pr.c]
-            fpts.append(g)
-        rhs = nt.g1_sum(nt.g1_mul(torch.cat(fpts).contiguous(), _sc(facs, "cpu")).view(-1, 1, 24))
+        lhs = nt.g1_add(*nt.g1_mul(BQ, full[2 * v: 2 * v + 2].contiguous()).split(1))
+        g = G[5 * nl * v: 5 * nl * (v + 1)].contiguous()
+        rhs = nt.g1_sum(nt.g1_mul(g, facs).view(-1, 1, 24))
         out.append(bool(nt.g1_eq(lhs, rhs)[0]))
     return out
 

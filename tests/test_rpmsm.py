@@ -115,7 +115,8 @@ def proofs():
 
 
 @pytest.mark.parametrize("device", DEVICES)
-def test_msm_pairing_product_matches_per_item_fold(device, proofs):
+@pytest.mark.parametrize("segs", [None, [1, 2, 1]])
+def test_msm_pairing_product_matches_per_item_fold(device, proofs, segs):
     """FE(ML(B, R) prod ML(-Y_q, U_q)) == FE(prod_it ML(rho (Zphi B - Y), V_it))
     for the same weights: the regrouping is an identity, not a new check."""
     dev = _dev(device)
@@ -129,14 +130,14 @@ def test_msm_pairing_product_matches_per_item_fold(device, proofs):
     Y = nt.g1_mul(sm.y_jac.to(dev).index_select(0, y_idx).contiguous(), rp._rep(r.challenge, S))
     ab, rho = nt.glv_weights(G * m, dev)
     hR = rp._msm_plan(r.zphi, r.V, rho, G, n, S, l)
-    q = rp._msm_queue(Y, r.V, ab, G, n, S, l)
+    q = rp._msm_queue(Y, r.V, ab, G, n, S, l, None, segs)
     fR, _ = rp._msm_r_miller(hR, nt.g2_msm_run(r.V, hR))
+    useg = rp._seg_products(q)                            # per (VN, segment) U-side products
+    k = len(segs) if segs else 1
+    assert tuple(useg.shape) == (G, k, 96)
     T = rp._fold_points(ZB.cpu(), Y.cpu(), S, l)
     for v in range(G):
-        fbv = q["fb"][v]
-        F_msm = nt._finish_prod_on_host(fbv) if dev.type == "cuda" else \
-            nt.gt_prod(fbv.view(-1, 1, 96), chunk=4).view(1, 96)
-        F_msm = nt.gt_mul(F_msm.cpu(), fR[v:v + 1])
+        F_msm = nt.gt_mul(nt.gt_prod(useg[v].view(k, 1, 96), chunk=4).view(1, 96), fR[v:v + 1])
         f = nt.miller_loop(nt.g1_to_affine(nt.g1_mul(T, rho[v * m:(v + 1) * m].cpu().contiguous())), r.V.cpu())
         F_fold = nt.gt_prod(f.view(-1, 1, 96), chunk=4).view(1, 96)
         assert bool(nt.gt_eq(nt.final_exp(F_msm.cpu()), nt.final_exp(F_fold)).all()), v
@@ -153,4 +154,40 @@ def test_both_verifier_modes_accept_and_reject(device, mode, proofs, monkeypatch
     V = bad.V.clone()
     V[4] = V[5]                                           # a valid G2 point, wrong item
     bad.V = V
+    assert rp.verify_range_proof_list_multi(bad, sm, P, 2, dev) == [False] * 2
+
+
+@pytest.mark.parametrize("device", DEVICES)
+@pytest.mark.parametrize("field", ["V", "zr", "A", "A_off_gt"])
+def test_segment_attribution(device, field, proofs):
+    """segs = per-request slices: a clean batch clears every segment; a
+    tampered proof is named by the failing VN's segment-grouped second pass
+    (pairing side: V; D-equation: Zr; GT side: A), the other segments pass."""
+    dev = _dev(device)
+    rpl, sm, P = proofs
+    r = rpl.to(dev)
+    assert rp.verify_range_proof_list_multi(r, sm, P, 2, dev, segs=[1, 2, 1]) == [[True] * 3] * 2
+    bad = rpl.to(dev)
+    n, l, S = len(bad), bad.l, bad.S
+    if field == "V":                                      # proof 2 (segment 1): a valid G2 point, wrong item
+        V = bad.V.clone()
+        V[2 * S * l] = V[2 * S * l + 1]
+        bad.V = V
+        want = [True, False, True]
+    elif field == "zr":                                   # proof 3 (segment 2)
+        zr = bad.zr.clone()
+        zr[3, 0] ^= 1
+        bad.zr = zr
+        want = [True, True, False]
+    elif field == "A":                                    # proof 0 (segment 0): a_it^2 is still in GT
+        A = bad.A.clone()
+        A[1] = nt.gt_mul(A[1:2].contiguous(), A[1:2].contiguous())[0]
+        bad.A = A
+        want = [False, True, True]
+    else:                                                 # the last word flipped (FaultPlan corrupt_proof): off GT
+        A = bad.A.clone()
+        A[-1, -1] ^= 1
+        bad.A = A
+        want = [True, True, False]
+    assert rp.verify_range_proof_list_multi(bad, sm, P, 2, dev, segs=[1, 2, 1]) == [want] * 2
     assert rp.verify_range_proof_list_multi(bad, sm, P, 2, dev) == [False] * 2
