@@ -16,6 +16,7 @@
 // calls: see dx_rpmsm.hip on branch relaxation in out-of-line callees).
 #define DX_NI __host__ __device__ __forceinline__
 #include "common.h"
+#include "../bn254/gt_coop.h"
 
 using namespace dxk;
 
@@ -198,6 +199,59 @@ DX_HD void prove_e_one(const uint32_t *gphi_tables, const int32_t *tab_idx, cons
   at<Fp12>(a_out, it) = mul(gt_gls8_eval(T, e_sc + 8 * it), at<Fp12>(a_out, p * S * L + j));
 }
 
+// ---- the two prover passes on the GPU: three lanes per item (gt_coop.h)
+// x <- x * prod of the signed 8-bit windows of one 128-bit half (role operands)
+__device__ __forceinline__ void gt_half_coop(Fp6 &x, const Fp12 *T, const uint32_t *k5, const coop::Role &R) {
+  uint32_t c = 0;
+  for (int w = 0; w < kWin; w++) {
+    const int d = sdigit(k5, w, c);
+    if (d) coop::mul(x, coop::load(&T[w * kHalf + (d > 0 ? d : -d) - 1], d < 0, R), R);
+  }
+}
+
+__global__ void __launch_bounds__(kWG) DX_OCC prove_t_coop(const uint32_t *t_sc, const uint32_t *gt16, uint32_t *a_out,
+                                                          int S, int L, int64_t n_pj) {
+  const coop::Role R = coop::role();
+  const int64_t pj = (int64_t)blockIdx.x * coop::kTriples + R.g;
+  if (R.g >= coop::kTriples || pj >= n_pj) return;  // whole triples leave together
+  const Fp12 *T = reinterpret_cast<const Fp12 *>(gt16);
+  const uint32_t *k = t_sc + 8 * pj;
+  Fp6 x = coop::one(R);
+  uint32_t carry = 0;
+  for (int w = 0; w < kW16; w++) {
+    const uint32_t raw = w < 16 ? (k[w >> 1] >> (16 * (w & 1))) & 0xFFFFu : 0u;
+    const uint32_t v = raw + carry;
+    carry = v > (uint32_t)kH16 ? 1u : 0u;
+    const int d = carry ? (int)v - 65536 : (int)v;
+    if (d) coop::mul(x, coop::load(&T[w * kH16 + (d > 0 ? d : -d) - 1], d < 0, R), R);
+  }
+  const int64_t p = pj / L, j = pj % L;
+  coop::store(&at<Fp12>(a_out, p * S * L + j), x, R);
+}
+
+// server range [i_lo, i_hi): a[it] = E_phi(it)^(e[it]) * a[p*S*L + j]
+__global__ void __launch_bounds__(kWG) DX_OCC prove_e_coop(const uint32_t *gphi, const int32_t *tab_idx,
+                                                          const uint32_t *e_sc, uint32_t *a_out, int S, int L,
+                                                          int i_lo, int i_hi, int64_t n) {
+  const coop::Role R = coop::role();
+  const int64_t kk = (int64_t)blockIdx.x * coop::kTriples + R.g;
+  if (R.g >= coop::kTriples || kk >= n) return;
+  const int64_t per = (int64_t)(i_hi - i_lo) * L;
+  const int64_t p = kk / per, rr = kk % per;
+  const int64_t i = i_lo + rr / L, j = rr % L;
+  const int64_t it = (p * S + i) * L + j;
+  const Fp12 *T = reinterpret_cast<const Fp12 *>(gphi) + (int64_t)tab_idx[it] * kEnt;
+  uint32_t k0[5], k1[5];
+  split_lambda2(e_sc + 8 * it, k0, k1);
+  Fp6 x = coop::one(R);
+  gt_half_coop(x, T, k1, R);
+  coop::frob1(x, R);
+  gt_half_coop(x, T, k0, R);
+  Fp12 *slot = &at<Fp12>(a_out, p * S * L + j);
+  coop::mul(x, coop::load(slot, false, R), R);  // every role has read the shared slot before any store
+  coop::store(&at<Fp12>(a_out, it), x, R);
+}
+
 #define DX_TID() const int64_t i = (int64_t)blockIdx.x * kWG + threadIdx.x
 __global__ void __launch_bounds__(kWG) DX_OCC g2_pow_kernel(const uint32_t *b, uint32_t *w, int64_t n) {
   DX_TID();
@@ -220,47 +274,15 @@ __global__ void __launch_bounds__(kWG) DX_OCC g2_mul_kernel(const uint32_t *tabl
   DX_TID();
   if (i < n) g2_mul_one(tables, tab_idx, sc, out, i);
 }
-__global__ void __launch_bounds__(kWG) DX_OCC prove_t_kernel(const uint32_t *t_sc, const uint32_t *gt_table,
-                                                            uint32_t *a_out, int S, int L, int t16, int64_t n) {
-  DX_TID();
-  if (i < n) prove_t_one(t_sc, gt_table, a_out, S, L, t16, i);
-}
 __global__ void __launch_bounds__(kWG) DX_OCC gt16_entry_kernel(const uint32_t *pow2, uint32_t *table, int64_t n) {
   DX_TID();
   if (i < n) gt16_entry_one(pow2, table, i);
 }
-__global__ void __launch_bounds__(kWG) DX_OCC prove_e_kernel(const uint32_t *gphi, const int32_t *tab_idx,
-                                                            const uint32_t *e_sc, uint32_t *a_out, int S, int L,
-                                                            int i_lo, int i_hi, int64_t n) {
-  DX_TID();
-  if (i < n) prove_e_one(gphi, tab_idx, e_sc, a_out, S, L, i_lo, i_hi, i);
-}
-// One-wave-per-SIMD variants of the two prover kernels (A/B, DRYNX_PROVE_WAVES=1):
-// the whole register file (VGPRs + AGPRs) instead of 256 registers and scratch spills
-#define DX_OCC1 __attribute__((amdgpu_waves_per_eu(1, 1)))
-__global__ void __launch_bounds__(kWG) DX_OCC1 prove_t_kernel_w1(const uint32_t *t_sc, const uint32_t *gt_table,
-                                                               uint32_t *a_out, int S, int L, int t16, int64_t n) {
-  DX_TID();
-  if (i < n) prove_t_one(t_sc, gt_table, a_out, S, L, t16, i);
-}
-__global__ void __launch_bounds__(kWG) DX_OCC1 prove_e_kernel_w1(const uint32_t *gphi, const int32_t *tab_idx,
-                                                               const uint32_t *e_sc, uint32_t *a_out, int S, int L,
-                                                               int i_lo, int i_hi, int64_t n) {
-  DX_TID();
-  if (i < n) prove_e_one(gphi, tab_idx, e_sc, a_out, S, L, i_lo, i_hi, i);
-}
-#undef DX_OCC1
 #undef DX_TID
 
 inline dim3 grid_of(int64_t n) { return dim3((unsigned)((n + kWG - 1) / kWG)); }
+inline dim3 grid_coop(int64_t n) { return dim3((unsigned)((n + coop::kTriples - 1) / coop::kTriples)); }
 
-inline bool prove_one_wave() {
-  static const bool w1 = [] {
-    const char *e = getenv("DRYNX_PROVE_WAVES");
-    return e && e[0] == '1';
-  }();
-  return w1;
-}
 }  // namespace
 
 extern "C" {
@@ -340,21 +362,14 @@ int dx_rp_prove_a_gls8(int on_gpu, void *stream, const uint32_t *gphi_tables, co
     return 0;
   }
   hipStream_t s = (hipStream_t)stream;
-  const bool w1 = prove_one_wave();
-  if (w1)
-    hipLaunchKernelGGL(prove_t_kernel_w1, grid_of(n_pj), dim3(kWG), 0, s, t_sc, gt_table, a_out, S, L, t16, n_pj);
-  else
-    hipLaunchKernelGGL(prove_t_kernel, grid_of(n_pj), dim3(kWG), 0, s, t_sc, gt_table, a_out, S, L, t16, n_pj);
+  if (!t16) return check_hip(hipErrorInvalidValue, "rp_prove_a_gls8 (the GPU path takes the 16-bit gT table)");
+  hipLaunchKernelGGL(prove_t_coop, grid_coop(n_pj), dim3(kWG), 0, s, t_sc, gt_table, a_out, S, L, n_pj);
   for (auto &rg : ranges) {
     const int lo = rg[0], hi = rg[1];
     if (hi <= lo) continue;
     const int64_t n = n_p * (hi - lo) * L;
-    if (w1)
-      hipLaunchKernelGGL(prove_e_kernel_w1, grid_of(n), dim3(kWG), 0, s, gphi_tables, tab_idx, e_sc, a_out, S, L, lo,
-                         hi, n);
-    else
-      hipLaunchKernelGGL(prove_e_kernel, grid_of(n), dim3(kWG), 0, s, gphi_tables, tab_idx, e_sc, a_out, S, L, lo, hi,
-                         n);
+    hipLaunchKernelGGL(prove_e_coop, grid_coop(n), dim3(kWG), 0, s, gphi_tables, tab_idx, e_sc, a_out, S, L, lo, hi,
+                       n);
   }
   return check_hip(hipGetLastError(), "rp_prove_a_gls8");
 }

@@ -13,6 +13,7 @@
 //            instead of three pairings.
 // Item index: it = (p * S + i) * L + j.
 #include "common.h"
+#include "../bn254/gt_coop.h"
 
 extern "C" {
 
@@ -135,14 +136,38 @@ extern "C" int dx_rp_verify_fold(void *stream, const uint32_t *ZB_jac, const uin
 
 // Segmented GT products (bucket accumulation of a multi-exponentiation):
 //   out[s] = prod_{k < len[s]} src[idx ? idx[start[s] + k] : start[s] + k]
+// GPU: three lanes per slice (gt_coop.h).
+namespace {
+__global__ void __launch_bounds__(64) DX_OCC gt_slice_prod_coop(const uint32_t *src, const int64_t *idx,
+                                                               const int64_t *start, const int32_t *len,
+                                                               uint32_t *out, int64_t n_slices) {
+  const coop::Role R = coop::role();
+  const int64_t s = (int64_t)blockIdx.x * coop::kTriples + R.g;
+  if (R.g >= coop::kTriples || s >= n_slices) return;  // whole triples leave together
+  const int64_t b = start[s];
+  const int n = len[s];
+  const Fp12 *F = reinterpret_cast<const Fp12 *>(src);
+  Fp6 x = coop::one(R);
+  for (int k = 0; k < n; k++) coop::mul(x, coop::load(&F[idx ? idx[b + k] : b + k], false, R), R);
+  coop::store(&at<Fp12>(out, s), x, R);
+}
+}  // namespace
+
 extern "C" int dx_gt_slice_prod(int on_gpu, void *stream, const uint32_t *src, const int64_t *idx,
                                 const int64_t *start, const int32_t *len, uint32_t *out, int64_t n_slices) {
-  auto op = [=] __host__ __device__(int64_t s) {
-    const int64_t b = start[s];
-    const int n = len[s];
-    Fp12 acc = Fp12::one();
-    for (int k = 0; k < n; k++) acc = mul(acc, at<Fp12>(src, idx ? idx[b + k] : b + k));
-    at<Fp12>(out, s) = acc;
-  };
-  return run(on_gpu, stream, n_slices, op, true, "gt_slice_prod");
+  if (n_slices <= 0) return 0;
+  if (!on_gpu) {
+    host_for_each(n_slices, [=](int64_t s) {
+      const int64_t b = start[s];
+      const int n = len[s];
+      Fp12 acc = Fp12::one();
+      for (int k = 0; k < n; k++) acc = mul(acc, at<Fp12>(src, idx ? idx[b + k] : b + k));
+      at<Fp12>(out, s) = acc;
+    });
+    return 0;
+  }
+  const unsigned blocks = (unsigned)((n_slices + coop::kTriples - 1) / coop::kTriples);
+  hipLaunchKernelGGL(gt_slice_prod_coop, dim3(blocks), dim3(64), 0, (hipStream_t)stream, src, idx, start, len, out,
+                     n_slices);
+  return check_hip(hipGetLastError(), "gt_slice_prod");
 }

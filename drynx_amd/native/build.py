@@ -55,10 +55,35 @@ SAN_FLAGS = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=und
 SAN_LIB = os.path.join(ROOT, "build", "libdrynx_native_asan.so")
 
 
+def _closure(src: str) -> list:
+    """The source and every header it reaches through quoted #includes
+    (resolved next to the including file, then under csrc/)."""
+    seen, todo = [], [os.path.abspath(src)]
+    while todo:
+        f = todo.pop()
+        if f in seen or not os.path.exists(f):
+            continue
+        seen.append(f)
+        with open(f) as fh:
+            for line in fh:
+                t = line.strip()
+                if t.startswith("#include") and '"' in t:
+                    inc = t.split('"')[1]
+                    for d in (os.path.dirname(f), CSRC):
+                        cand = os.path.abspath(os.path.join(d, inc))
+                        if os.path.exists(cand):
+                            todo.append(cand)
+                            break
+    return sorted(seen)
+
+
 def _compile(src, hdr_digest, sanitize=False):
+    """``hdr_digest`` is unused for the object key: an object depends on its
+    own include closure only, so a header edit recompiles the translation
+    units that include it (the library stamp still covers every file)."""
     objdir = OBJDIR + ("_asan" if sanitize else "")
     os.makedirs(objdir, exist_ok=True)
-    key = _digest([src]) + hdr_digest + ("san" if sanitize else "")
+    key = _digest(_closure(src)) + ("san" if sanitize else "")
     obj = os.path.join(objdir, os.path.basename(src) + ".o")
     stamp = obj + ".stamp"
     if os.path.exists(obj) and os.path.exists(stamp) and open(stamp).read() == key:
