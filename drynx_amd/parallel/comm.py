@@ -225,8 +225,16 @@ class _CtrlPlane(Comm):
         raise RuntimeError("a control plane carries no data-plane exchanges (use the main comm)")
 
 
+def _force_dist() -> bool:
+    """DRYNX_FORCE_DIST=1: a world of ONE rank still runs torch.distributed and
+    the DistComm planes (RCCL data plane + gloo control groups), so a one-GPU
+    box exercises the exact multi-GPU code path (init with a device id, the
+    all_to_all_single splits on HBM tensors, side-plane groups)."""
+    return os.environ.get("DRYNX_FORCE_DIST") == "1"
+
+
 def make_comm(device=None) -> Comm:
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+    if dist.is_available() and dist.is_initialized() and (dist.get_world_size() > 1 or _force_dist()):
         return DistComm(device)
     if device is None:
         device = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0"))) if torch.cuda.is_available() else "cpu"
@@ -241,7 +249,7 @@ def init_distributed(backend: str | None = None):
     if dist.is_initialized():
         return
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world <= 1:
+    if world <= 1 and not (_force_dist() and "MASTER_ADDR" in os.environ):
         return
     if backend is None:
         # DRYNX_DIST_BACKEND=gloo rehearses the multi-rank GPU path with several
