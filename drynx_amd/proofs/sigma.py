@@ -551,26 +551,40 @@ def key_switch_list_proof_creation(x: int, X, Q_point, K: torch.Tensor, share: C
     return KeySwitchProof(X, Q_point, K, share, T1, T2, T3, c, za, zb)
 
 
-def _ks_fs_ok(proofs: list) -> list:
+def _ks_fs_ok(proofs: list, copies: int = 1):
     """Each proof's weight-free checks, done by the verifier itself: the
     challenge recomputed from the transcript (point digests are decoded data,
-    computed once per proof) and zb B == T3 + c X."""
+    computed once per proof) and zb B == T3 + c X.  ``copies`` verifying
+    nodes of one rank run their own checks in ONE native batch (zb B by one
+    fixed-base call, c X by one variable-base call) -> one list per copy
+    (copies > 1) or the list itself."""
     todo = [pr for pr in proofs if not pr.pts_digest]
     if todo:
         with timers.span("ks.verify.transcripts"):
             for pr, d in zip(todo, points_digests([[pr.K, pr.share, pr.T1, pr.T2] for pr in todo])):
                 pr.pts_digest = d
-    out = []
-    for pr in proofs:
-        c = fs_hash("proofTest/keyswitch", (O.g1_to_bytes(pr.X), O.g1_to_bytes(pr.Q), pr.T3), pr.pts_digest)
-        ok = c == pr.c
-        if ok:
+    rows, chs, idx = [], [], []
+    res = [[False] * len(proofs) for _ in range(copies)]
+    for cp in range(copies):
+        for i, pr in enumerate(proofs):
+            c = fs_hash("proofTest/keyswitch", (O.g1_to_bytes(pr.X), O.g1_to_bytes(pr.Q), pr.T3), pr.pts_digest)
+            if c != pr.c:
+                continue
             try:
-                ok = bn.g1_mul_point(pr.zb) == O.g1_add(O.g1_from_bytes(pr.T3), bn.g1_mul_point(c, pr.X))
+                T3 = O.g1_from_bytes(pr.T3)
             except ValueError:
-                ok = False
-        out.append(ok)
-    return out
+                continue
+            rows.append((pr, T3))
+            chs.append(c)
+            idx.append((cp, i))
+    if rows:
+        zb = bn.scalars_tensor([pr.zb % O.R for pr, _ in rows], "cpu")
+        lhs = nt.g1_fb_mul(bn.base_table("cpu"), zb)
+        cX = nt.g1_mul(bn.g1_jac_tensor([pr.X for pr, _ in rows], "cpu"), bn.scalars_tensor(chs, "cpu"))
+        rhs = nt.g1_add(bn.g1_jac_tensor([T3 for _, T3 in rows], "cpu"), cX)
+        for (cp, i), ok in zip(idx, nt.g1_eq(lhs, rhs).tolist()):
+            res[cp][i] = bool(ok)
+    return res if copies > 1 else res[0]
 
 
 def key_switch_batch_verification(proofs: list, threshold: float = 1.0, combine: bool = True, coins=None) -> list:
@@ -605,7 +619,7 @@ def key_switch_batch_verification_multi(proofs: list, threshold: float, coins_li
     n_vn = len(coins_list)
     if not proofs:
         return [[] for _ in range(n_vn)]
-    oks = [_ks_fs_ok(proofs) for _ in range(n_vn)]
+    oks = _ks_fs_ok(proofs, n_vn) if n_vn > 1 else [_ks_fs_ok(proofs)]
     lives = [[(i, pr, _first(pr.K.shape[0], threshold)) for i, pr in enumerate(proofs) if ok[i]] for ok in oks]
     lives = [[x for x in lv if x[2] > 0] for lv in lives]
     out = [list(ok) for ok in oks]
@@ -642,10 +656,23 @@ def _ks_combined(live, n_vn: int = 1, coins=None):
     za = torch.cat([pr.za[:k] for _, pr, k in live]).contiguous()
     W = torch.cat([_rand64(2 * kt, dev, c) for c in cl])                      # [n_vn * 2kt, 8]
     scs = W.view(n_vn, 2 * kt, 8).index_select(1, torch.from_numpy(sel).to(dev)).reshape(-1, 8).contiguous()
-    grp = (np.arange(n_vn).reshape(-1, 1) * (5 * nl) + grp1.reshape(1, -1)).reshape(-1)
-    G = nt.g1_msm_grouped(pts.contiguous().repeat(n_vn, 1), scs, torch.from_numpy(grp.astype(np.int32)).to(dev),
-                          5 * nl * n_vn, bits=64)
-    full = nt.fr_dot_rows(W, za, 2 * n_vn, b_periodic=True).cpu()           # [sum rho za, sum sig za] per VN
+    full = nt.fr_dot_rows(W, za, 2 * n_vn, b_periodic=True)                  # [sum rho za, sum sig za] per VN
+    if dev.type == "cuda" and len(set(ks)) == 1:
+        # equal-length proofs (the CNs switch the same K): every weighted point
+        # by one 64-bit variable-base launch (leading zero windows skipped) and
+        # the 5 nl n_vn group sums by a chunked tree -- no bucket plan and its
+        # host sync; group sums and za dots come back in ONE copy
+        k0 = ks[0]
+        prod = nt.g1_mul(pts.contiguous().repeat(n_vn, 1), scs).view(5 * nl * n_vn, k0, 24)
+        sums = nt.g1_sum(prod.transpose(0, 1).contiguous())
+        both = torch.cat([sums.reshape(-1), full.reshape(-1)]).cpu()
+        G = both[: sums.numel()].view(-1, 24)
+        full = both[sums.numel():].view(-1, 8)
+    else:
+        grp = (np.arange(n_vn).reshape(-1, 1) * (5 * nl) + grp1.reshape(1, -1)).reshape(-1)
+        G = nt.g1_msm_grouped(pts.contiguous().repeat(n_vn, 1), scs, torch.from_numpy(grp.astype(np.int32)).to(dev),
+                              5 * nl * n_vn, bits=64)
+        full = full.cpu()
     Q = live[0][1].Q
     facs = _sc([f for _, pr, _ in live for f in (1, pr.c, pr.zb, 1, pr.c)], "cpu")
     BQ = bn.g1_jac_tensor([O.G1_GEN, Q], "cpu")
