@@ -41,6 +41,9 @@ from ..crypto import oracle as O
 from ..crypto.elgamal import CipherVector, pk_table
 from ..query import PublishSignatureBytes
 from ..utils import timers
+from ..utils.log import get_logger
+
+log = get_logger("range_proof")
 
 G2_LEN, G1_LEN, GT_LEN, SC_LEN = 128, 64, 384, 32
 
@@ -956,6 +959,10 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
         # where the pairing is bilinear and the regrouping exact
         g2_ok = bool(v.get("u_ok", True)) and bool(v.get("r_ok", True))
         out.append(d_ok and m_oks[len(out)] and eq_ok and g2_ok)
+        if not out[-1]:
+            log.warning(f"range batch of {n} proofs failed for verifier {len(out) - 1}: D-check {d_ok}, "
+                        f"GT membership {m_oks[len(out) - 1]}, pairing equation {eq_ok}, "
+                        f"U in G2 {bool(v.get('u_ok', True))}, R in G2 {bool(v.get('r_ok', True))}")
     if segs is None:
         return out
     # attribution: a passing batch clears every segment; a failing one gets
@@ -1053,10 +1060,13 @@ def _msm_queue(Y, V, ab_all, G: int, n: int, S: int, L: int, vstream=None, segs:
         vs = vstream if vstream is not None else cur
         vs.wait_stream(cur)
         with torch.cuda.stream(vs):
+            # every read of the flags stays on the validation stream: a reduction
+            # queued on `cur` would race the membership kernels (read before they
+            # finish); the caller synchronises `vs` before looking at the verdicts
             fl = nt.g2_subgroup(Ud).view(G, -1)[:, :nq].bool()
             out["u_seg"] = _seg_all(fl, cq, dev)
+            out["u_ok"] = list(out["u_seg"].all(dim=1).unbind(0))
         Ud.record_stream(vs)
-        out["u_ok"] = list(out["u_seg"].all(dim=1).unbind(0))
         out["fb"] = nt.rp_fold_accum_n(nt.rp_fold_ncoeffs(Uall), UV, Uall, period, 1, K)
         out["blk"] = pad // rows
         out["sb"] = [0] if nseg == 1 else (segbase // rows).tolist()
