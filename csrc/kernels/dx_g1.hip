@@ -229,6 +229,21 @@ int dx_g1j_on_curve(int on_gpu, void *stream, const uint32_t *jac, uint8_t *out,
 
 // Partial sums over axis 0 of in[n_items][n_groups] (Jacobian):
 // out[c][g] = sum_{i in chunk c} in[i][g], chunk = `chunk` items.
+// Host tail of the G1 bucket MSM: out[g] = sum_w 2^(c w) S[g W + w] (Jacobian),
+// one serial Horner chain per group on the host pool -- a Python loop of
+// per-window native calls cost ~2 ms for a 32-window, 6-group D-check.
+int dx_g1_horner_host(const uint32_t *S_jac, uint32_t *out_jac, int64_t G, int W, int c) {
+  host_for_each(G, [=](int64_t g) {
+    G1J acc = at<G1J>(S_jac, g * W + W - 1);
+    for (int w = W - 2; w >= 0; w--) {
+      for (int k = 0; k < c; k++) acc = jdbl(acc);
+      acc = jadd(acc, at<G1J>(S_jac, g * W + w));
+    }
+    at<G1J>(out_jac, g) = acc;
+  }, 2);
+  return 0;
+}
+
 int dx_g1_sum_chunks(int on_gpu, void *stream, const uint32_t *in, uint32_t *out, int64_t n_items, int64_t n_groups,
                      int64_t chunk) {
   int64_t n_chunks = (n_items + chunk - 1) / chunk;

@@ -122,6 +122,21 @@ int dx_gt_cyclotomic(int on_gpu, void *stream, const uint32_t *a, uint8_t *out, 
   return run(on_gpu, stream, n, op, true, "gt_cyclotomic");
 }
 
+// Exact membership of the prime-order GT for elements of the cyclotomic
+// subgroup: p = 6u^2 (mod r), so x^r = 1 iff x^p == x^(6u^2).  x^p is ONE
+// Frobenius map; x^(6u^2) = ((x^u)^u)^6 two cyclotomic u-ladders (62
+// Granger-Scott squarings each) and three products -- instead of two generic
+// 254/127-bit exponentiations.  The caller guarantees cyclotomic inputs.
+int dx_gt_membership(int on_gpu, void *stream, const uint32_t *a, uint8_t *out, int64_t n) {
+  auto op = [=] __host__ __device__(int64_t i) {
+    const Fp12 x = at<Fp12>(a, i);
+    const Fp12 y = cyc_pow_u(cyc_pow_u(x));
+    const Fp12 y2 = cyclotomic_sqr(y);
+    out[i] = frob<1>(x) == mul(y2, cyclotomic_sqr(y2)) ? 1 : 0;
+  };
+  return run(on_gpu, stream, n, op, true, "gt_membership");
+}
+
 // product over axis 0 chunks of in[n_items][n_groups] Fp12 (same scheme as g1_sum_chunks)
 int dx_gt_prod_chunks(int on_gpu, void *stream, const uint32_t *in, uint32_t *out, int64_t n_items, int64_t n_groups,
                       int64_t chunk) {

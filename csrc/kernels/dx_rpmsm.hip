@@ -288,7 +288,7 @@ int dx_g2_horner(int on_gpu, void *stream, const uint32_t *S_jac, uint32_t *out_
                  int64_t stride, int64_t offset) {
   if (G <= 0) return 0;
   if (!on_gpu) {
-    host_for_each(G, [=](int64_t g) { horner_one(S_jac, out_aff, W, c, stride, offset, g); });
+    host_for_each(G, [=](int64_t g) { horner_one(S_jac, out_aff, W, c, stride, offset, g); }, 2);
     return 0;
   }
   hipLaunchKernelGGL(horner_kernel, grid_of(G), dim3(kWG), 0, (hipStream_t)stream, S_jac, out_aff, W, c, stride,

@@ -60,11 +60,14 @@ class HostPool {
     static HostPool *p = new HostPool(host_threads() - 1);  // never destroyed: workers outlive static teardown
     return *p;
   }
+  // min_par: smallest n worth a dispatch to the workers (heavy per-item ops
+  // -- pairings, final exponentiations, GT ladders of a few verifiers -- gain
+  // from 2 items on; cheap ones from 4)
   template <class Op>
-  void for_each(int64_t n, const Op &op) {
+  void for_each(int64_t n, const Op &op, int64_t min_par = 4) {
     const int64_t chunk = std::max<int64_t>(1, n / ((int64_t)(workers_.size() + 1) * 8));
     std::unique_lock<std::mutex> busy(job_mu_, std::try_to_lock);
-    if (!busy.owns_lock() || workers_.empty() || n < 4) {
+    if (!busy.owns_lock() || workers_.empty() || n < min_par) {
       for (int64_t i = 0; i < n; i++) op(i);
       return;
     }
@@ -121,8 +124,8 @@ class HostPool {
 };
 
 template <class Op>
-void host_for_each(int64_t n, const Op &op) {
-  HostPool::get().for_each(n, op);
+void host_for_each(int64_t n, const Op &op, int64_t min_par = 4) {
+  HostPool::get().for_each(n, op, min_par);
 }
 
 inline int check_hip(hipError_t e, const char *what) {
@@ -138,7 +141,7 @@ template <class Op>
 int run(int on_gpu, void *stream, int64_t n, const Op &op, bool heavy = false, const char *name = "op") {
   if (n <= 0) return 0;
   if (!on_gpu) {
-    host_for_each(n, op);
+    host_for_each(n, op, heavy ? 2 : 4);
     return 0;
   }
   hipStream_t s = (hipStream_t)stream;

@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import threading
 
 import numpy as np
 
@@ -103,6 +104,8 @@ _SIGS = {
     "dx_gt_fb4_table": [_I, _P, _P, _P, _P, _L],
     "dx_gt_fb4_pow": [_I, _P, _P, _P, _P, _P, _L],
     "dx_gt_cyclotomic": [_I, _P, _P, _P, _L],
+    "dx_gt_membership": [_I, _P, _P, _P, _L],
+    "dx_g1_horner_host": [_P, _P, _L, _I, _I],
     "dx_g2_subgroup": [_I, _P, _P, _P, _L],
     "dx_limbs_canonical": [_I, _P, _P, _I, _P, _L],
     "dx_g1j_on_curve": [_I, _P, _P, _P, _L],
@@ -199,10 +202,21 @@ def loaded_path() -> str:
 
 
 # ----------------------------------------------------------------------------- helpers
+_keep = threading.local()
+
+
 def _ptr(t: torch.Tensor | None):
+    """Raw pointer of a contiguous tensor for a native call.  The tensor is
+    kept alive until the calling thread's next ``_call`` returns: a temporary
+    such as ``_ptr(x.contiguous())`` would otherwise be freed before the call
+    runs (on the host path the native code would then read freed memory)."""
     if t is None:
         return None
     assert t.is_contiguous(), "native ops need contiguous tensors"
+    held = getattr(_keep, "held", None)
+    if held is None:
+        held = _keep.held = []
+    held.append(t)
     return ctypes.c_void_p(t.data_ptr())
 
 
@@ -221,7 +235,10 @@ def _ctx(*ts):
 
 
 def _call(name, *args):
-    rc = getattr(_load(), name)(*args)
+    try:
+        rc = getattr(_load(), name)(*args)
+    finally:
+        _keep.held = []
     if rc != 0:
         raise RuntimeError(f"native op {name} failed (rc={rc})")
 
@@ -427,6 +444,16 @@ def gt_cyclotomic(a: torch.Tensor) -> torch.Tensor:
     out = torch.empty((n,), dtype=torch.uint8, device=a.device)
     g, s = _ctx(a)
     _call("dx_gt_cyclotomic", g, s, _ptr(a.contiguous()), _ptr(out), n)
+    return out
+
+
+def gt_membership(a: torch.Tensor) -> torch.Tensor:
+    """[n] uint8: a_i in the prime-order GT, for a_i in the cyclotomic subgroup
+    (x^p == x^(6u^2): one Frobenius against two cyclotomic u-ladders)."""
+    n = _rows(a, 96)
+    out = torch.empty((n,), dtype=torch.uint8, device=a.device)
+    g, s = _ctx(a)
+    _call("dx_gt_membership", g, s, _ptr(a.contiguous()), _ptr(out), n)
     return out
 
 
@@ -1397,7 +1424,7 @@ def multi_exp_grouped_finish(h) -> torch.Tensor:
     G, W = h["G"], h["W"]
     if h["win"] is None:
         return gt_one("cpu").repeat(G, 1)
-    S_w = gt_prod(h["win"].cpu(), chunk=4).view(G, W, 96)
+    S_w = gt_prod(h["win"].cpu(), chunk=64).view(G, W, 96)  # host: one chain per (group, window)
     acc = S_w[:, W - 1].contiguous()
     sh = _pow2_scalar(h.get("c", _ME_C)).expand(G, 8).contiguous()
     for w in range(W - 2, -1, -1):
@@ -1491,11 +1518,11 @@ def g1_msm_finish(h: dict) -> torch.Tensor:
     rows[torch.from_numpy(gws.astype(np.int64))] = S_w
     rows = rows.view(G, W, 24)
     top = int((gws % W).max())
-    sh8 = torch.zeros((G, 8), dtype=torch.int32)
-    sh8[:, 0] = 256
-    out = rows[:, top].contiguous()
-    for w in range(top - 1, -1, -1):
-        out = g1_add(g1_mul(out, sh8), rows[:, w].contiguous())
+    out = torch.empty((G, 24), dtype=torch.int32)
+    src = rows[:, : top + 1].contiguous()  # held: the host call reads it
+    rc = _load().dx_g1_horner_host(_ptr(src), _ptr(out), G, top + 1, 8)
+    if rc:
+        raise RuntimeError(f"dx_g1_horner_host failed rc={rc}")
     return out
 
 

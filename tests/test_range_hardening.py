@@ -215,3 +215,31 @@ def test_v_with_small_torsion_rejected_by_regrouped_verifier(setup, monkeypatch)
     rpl.V[2] = bn.g2_aff_tensor([O.g2_add(G, T)])[0].to(rpl.V.device)
     assert bool(nt.g2_on_curve(rpl.V[2:3]).all())
     assert not rp.verify_range_proof_list(rpl, sm, P, mode=0)
+
+
+
+def test_gt_membership_matches_generic_pow():
+    """dx_gt_membership (x^p by Frobenius vs two cyclotomic u-ladders) agrees
+    with x^p == x^(6u^2) computed by the oracle with exact exponents, on GT
+    elements and on cyclotomic elements outside GT (the easy part of the final
+    exponentiation of random Fp12 values) -- which it must reject."""
+    import random
+
+    rng = random.Random(5)
+    g = O.pairing(O.G1_GEN, O.G2_GEN)
+    inside_vals = [g ** rng.randrange(O.R) for _ in range(3)]
+    inside = bn.gt_tensor(inside_vals, "cpu")
+    outside_vals = []
+    for _ in range(3):
+        e = O.Fp12.from_coeffs([rng.randrange(O.P) for _ in range(12)])
+        c = e.conj() * e.inv()
+        outside_vals.append(c.frob(2) * c)
+    outside = bn.gt_tensor(outside_vals, "cpu")
+    assert all(nt.gt_cyclotomic(outside).tolist())
+    # reference with the oracle's exact exponents (a scalar tensor would
+    # reduce p mod r = 6u^2 and make the comparison vacuous)
+    for vals, t in ((inside_vals, inside), (outside_vals, outside)):
+        ref = [x ** O.P == x ** (6 * O.U * O.U) for x in vals]
+        assert [bool(v) for v in nt.gt_membership(t).tolist()] == ref
+    assert all(nt.gt_membership(inside).tolist())
+    assert not any(nt.gt_membership(outside).tolist())
