@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <cstdio>
+#include <vector>
 
 typedef double dx_f64x4 __attribute__((ext_vector_type(4)));
 
@@ -143,4 +144,37 @@ extern "C" int dx_lr_encode(void *stream, const double *X, int64_t ldx, int64_t 
                             const double *sd, const double *y, double wa, double wb, double *partial, int n_blocks) {
   LrArgs a{X, ldx, N, dx, 1, mean, sd, nullptr, y, wa, wb, 1};
   return launch(stream, a, partial, n_blocks);
+}
+
+// Querier gradient descent for k = 2 (FindMinimumWeights, reference
+// lib/encoding/logistic_regression.go:693-742; the Cost accumulation quirk and
+// the "last weights with Cost >= 0" rule kept): one (d+1)x(d+1) mat-vec per
+// iteration with S = A2 + A2^T, on the host.  Runs outside the Python GIL (a
+// numpy loop of 450 iterations held it for ~2.6 ms beside the VN checks).
+extern "C" int dx_lr_gd_k2(const double *a0, const double *S, const double *w0, int d1, double N, double lam,
+                           double step, int max_iter, double C0, double C1, double C2, double *min_w) {
+  std::vector<double> w(w0, w0 + d1), Sw(d1), g(d1);
+  for (int i = 0; i < d1; i++) min_w[i] = w[i];
+  for (int it = 0; it < max_iter; it++) {
+    double wa = 0.0, wsw = 0.0, reg = 0.0;
+    for (int i = 0; i < d1; i++) {
+      double acc = 0.0;
+      for (int j = 0; j < d1; j++) acc += S[(int64_t)i * d1 + j] * w[j];
+      Sw[i] = acc;
+    }
+    for (int i = 0; i < d1; i++) {
+      wa += w[i] * a0[i];
+      wsw += w[i] * Sw[i];
+      if (i) reg += w[i] * w[i];
+    }
+    double c = (wa * C1 + 0.5 * wsw) * C2;
+    c = c / N - C0 + (lam / (2 * N)) * reg;
+    if (c >= 0.0)
+      for (int i = 0; i < d1; i++) min_w[i] = w[i];
+    for (int i = 0; i < d1; i++) {
+      g[i] = (C1 * a0[i] + C2 * Sw[i]) / N + (i ? (lam / N) * w[i] : 0.0);
+      w[i] = w[i] - step * g[i];
+    }
+  }
+  return 0;
 }

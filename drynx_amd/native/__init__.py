@@ -89,6 +89,8 @@ _SIGS = {
     "dx_version": [],
     "dx_stream_create_cu_mask": [_I, _P, _I, ctypes.POINTER(ctypes.c_void_p)],
     "dx_lr_moments": [_P, _P, _P, _L, _I, _P, _I],
+    "dx_lr_gd_k2": [_P, _P, _P, _I, ctypes.c_double, ctypes.c_double, ctypes.c_double, _I, ctypes.c_double,
+                    ctypes.c_double, ctypes.c_double, _P],
     "dx_random_scalars": [_I, _P, _P, ctypes.c_uint32, _P, _L],
     "dx_sha256_chunks": [_I, _P, _P, _L, _L, _P],
     "dx_hash_to_g1": [_I, _P, _P, _P, _L, _P, _L],
@@ -784,6 +786,23 @@ def gt_prod(x: torch.Tensor, chunk: int = 16) -> torch.Tensor:
 
 
 # ----------------------------------------------------------------------------- logistic-regression GEMM (K13)
+def lr_gd_k2(a0, S, w0, N: float, lam: float, step: float, max_iter: int, C) -> list:
+    """FindMinimumWeights for k = 2 on the host (csrc/kernels/dx_lr.hip
+    dx_lr_gd_k2; float64 numpy arrays in, the minimum weights out).  The
+    ctypes call releases the GIL for the whole descent."""
+    a0 = np.ascontiguousarray(a0, dtype=np.float64)
+    S = np.ascontiguousarray(S, dtype=np.float64)
+    w0 = np.ascontiguousarray(w0, dtype=np.float64)
+    d1 = a0.shape[0]
+    out = np.empty(d1, dtype=np.float64)
+    p = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    rc = _load().dx_lr_gd_k2(p(a0), p(S), p(w0), d1, float(N), float(lam), float(step), int(max_iter), float(C[0]),
+                             float(C[1]), float(C[2]), p(out))
+    if rc:
+        raise RuntimeError(f"dx_lr_gd_k2 failed rc={rc}")
+    return out.tolist()
+
+
 def random_scalars(n: int, device) -> torch.Tensor:
     """n uniform nonzero Fr scalars [n, 8] (plain limbs): ChaCha20 keyed with
     256 fresh bits of os.urandom per call, one block per scalar (dx_hash.hip)."""
