@@ -1319,8 +1319,8 @@ def _segment_passes_dev(counts, dev, first_slice: int | None = None):
         sl = first_slice if (first_slice and not passes) else _ME_SLICE
         n_sl = (c + sl - 1) // sl
         total = int(n_sl.sum())
-        ct = torch.from_numpy(c).to(dev)
-        nt_ = torch.from_numpy(n_sl).to(dev)
+        ct = _upload(c, dev)
+        nt_ = _upload(n_sl, dev)
         first = torch.cumsum(ct, 0) - ct
         b = torch.repeat_interleave(torch.arange(c.size, device=dev), nt_, output_size=total)
         k = torch.arange(total, device=dev) - (torch.cumsum(nt_, 0) - nt_)[b]
@@ -1516,7 +1516,7 @@ def g1_msm_launch(P_jac: torch.Tensor, k: torch.Tensor, group: torch.Tensor | No
     gws, counts = np.unique(bk // 256, return_counts=True)
     cur = weighted
     for st, ln in _segment_passes(counts):
-        cur = g1_slice_sum(cur, None, torch.from_numpy(st).to(dev), torch.from_numpy(ln.astype("int32")).to(dev))
+        cur = g1_slice_sum(cur, None, _upload(st, dev), _upload(ln.astype("int32"), dev))
     h["S_w"], h["gws"] = cur, gws
     return h
 
@@ -1625,9 +1625,9 @@ def g2_msm_launch(P_aff: torch.Tensor, k: torch.Tensor, group: torch.Tensor | No
         if not passes:  # every bucket holds one entry
             passes = [(torch.arange(bk.size, device=dev), torch.ones(bk.size, dtype=torch.int32, device=dev))]
         h["passes"] = passes
-        h["d"] = torch.from_numpy((bk & ((1 << c) - 1)).astype("int32")).to(dev)
+        h["d"] = _upload((bk & ((1 << c) - 1)).astype("int32"), dev)
         gws, gcounts = np.unique(bk >> c, return_counts=True)
-        h["gws"] = torch.from_numpy(gws.astype(np.int64)).to(dev)
+        h["gws"] = _upload(gws.astype(np.int64), dev)
         h["gpasses"] = _segment_passes_dev(gcounts, dev)
     return h
 

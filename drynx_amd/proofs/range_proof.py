@@ -1039,10 +1039,9 @@ def _msm_queue(Y, V, ab_all, G: int, n: int, S: int, L: int, vstream=None, segs:
             nt.rp_u_joint(table, ab_all, nq, G, L, Ud, nq)
             UVd = torch.zeros((G * (nq + 1), 16), dtype=torch.int32, device=dev)
             nt.rp_msm_uv(Y, UVd, nq, G, nq + 1)
-            qseg = torch.repeat_interleave(torch.arange(nseg, device=dev), torch.from_numpy(cq).to(dev),
+            qseg = torch.repeat_interleave(torch.arange(nseg, device=dev), _h2d(cq, dev),
                                            output_size=nq)
-            qpos = torch.from_numpy(segbase).to(dev)[qseg] + torch.arange(nq, device=dev) \
-                - torch.from_numpy(qoff[:-1]).to(dev)[qseg]
+            qpos = _h2d(segbase, dev)[qseg] + torch.arange(nq, device=dev) - _h2d(qoff[:-1], dev)[qseg]
             pos = (torch.arange(G, device=dev).view(G, 1) * pad + qpos.view(1, nq)).reshape(-1)
             Uall.index_copy_(0, pos, Ud)
             UV.index_copy_(0, pos, UVd.view(G, nq + 1, 16)[:, :nq].reshape(-1, 16))
@@ -1073,6 +1072,14 @@ def _msm_queue(Y, V, ab_all, G: int, n: int, S: int, L: int, vstream=None, segs:
     return out
 
 
+def _h2d(a, dev) -> torch.Tensor:
+    """A small host array (list / numpy) on ``dev`` through pinned memory: a
+    pageable copy would block this thread until every kernel already queued
+    on its stream has finished (the U-side launches of ``_msm_queue``)."""
+    t = torch.as_tensor(np.asarray(a) if not isinstance(a, torch.Tensor) else a)
+    return bn.h2d(t.contiguous(), dev)
+
+
 def _invalid(valid: torch.Tensor, segs, n_vn: int) -> list:
     if segs is None:
         return [False] * n_vn
@@ -1086,7 +1093,7 @@ def _seg_all(flags: torch.Tensor, counts, dev) -> torch.Tensor:
     k = len(counts)
     if k == 1:
         return flags.all(dim=1).view(G, 1)
-    sid = torch.repeat_interleave(torch.arange(k, device=dev), torch.as_tensor(counts, device=dev), output_size=nq)
+    sid = torch.repeat_interleave(torch.arange(k, device=dev), _h2d(counts, dev), output_size=nq)
     bad = torch.zeros((G, k), dtype=torch.int32, device=dev)
     bad.index_add_(1, sid, (~flags).to(torch.int32))
     return bad == 0
@@ -1101,8 +1108,8 @@ def _seg_products(msq: dict) -> torch.Tensor:
     dev = fb.device
     maxb = max(nb)
     b = torch.arange(maxb, device=dev).view(maxb, 1, 1)
-    base = (torch.arange(G, device=dev).view(1, G, 1) * blk + torch.as_tensor(sb, device=dev).view(1, 1, k))
-    idx = torch.where(b < torch.as_tensor(nb, device=dev).view(1, 1, k), base + b, fb.shape[0])
+    base = (torch.arange(G, device=dev).view(1, G, 1) * blk + _h2d(sb, dev).view(1, 1, k))
+    idx = torch.where(b < _h2d(nb, dev).view(1, 1, k), base + b, fb.shape[0])
     ext = torch.cat([fb, nt.gt_one(dev)])
     x = ext.index_select(0, idx.reshape(-1)).view(maxb, G * k, 96)
     if dev.type == "cuda":
@@ -1128,7 +1135,7 @@ def _segment_pass(r: RangeProofList, segs: list, redo: list, x: dict) -> dict:
     m, nseg, Gf = n * S * l, len(segs), len(redo)
     K = Gf * nseg
     poff = np.cumsum([0] + list(segs))
-    pseg = torch.repeat_interleave(torch.arange(nseg, device=dev), torch.as_tensor(segs, device=dev), output_size=n)
+    pseg = torch.repeat_interleave(torch.arange(nseg, device=dev), _h2d(segs, dev), output_size=n)
     iseg = pseg.repeat_interleave(S * l)
     fi = torch.arange(Gf, device=dev).view(Gf, 1)
     def rows(t, w):
@@ -1154,7 +1161,7 @@ def _segment_pass(r: RangeProofList, segs: list, redo: list, x: dict) -> dict:
     mexp = nt.multi_exp_grouped(x["A2"], k.view(-1, 8), grp2, 2 * K, W=x["wc"][0], c=x["wc"][1])
     # sum rho Zv, sum w Zr, sum w z per (v, s): per-proof sums, then per-segment
     offs = torch.from_numpy((np.arange(Gf).reshape(Gf, 1) * n + poff[:-1].reshape(1, nseg)).reshape(-1))
-    offs = torch.cat([offs, torch.tensor([Gf * n])]).to(dev)
+    offs = bn.h2d(torch.cat([offs, torch.tensor([Gf * n])]), dev)
     e = nt.fr_seg_sum(nt.fr_dot_rows(rho, r.zv.repeat(Gf, 1).contiguous(), Gf * n), offs)
     dzr = nt.fr_seg_sum(nt.fr_arith(nt.FR_MUL, w, r.zr.repeat(Gf, 1).contiguous()), offs)
     dz = nt.fr_seg_sum(nt.fr_arith(nt.FR_MUL, w, x["z"].repeat(Gf, 1).contiguous()), offs)
