@@ -212,13 +212,25 @@ def range_bundle_unpack_many(ts: list) -> list:
     short = [i for i, t in enumerate(ts) if t.numel() >= 7]
     if short:
         heads = torch.nn.utils.rnn.pad_sequence([ts[i][: _HEAD] for i in short], batch_first=True).cpu().tolist()
+    big = []
     for j, i in enumerate(short):
         h = heads[j]
         try:
             if h[0] == 1 and 0 <= h[3] <= 64:
                 out[i] = _unpack_one(ts[i], h[: min(len(h), ts[i].numel())])
+            elif h[0] == 1 and 64 < h[3] and 7 + 3 * h[3] <= ts[i].numel():
+                big.append((i, 7 + 3 * h[3]))
         except Exception as e:  # noqa: BLE001 -- a malformed bundle is a rejected proof
             out[i] = e
+    if big:
+        # single-list bundles of wide queries (2070 proofs per DP): every full
+        # header in ONE more device-to-host copy instead of one sync per bundle
+        full = torch.nn.utils.rnn.pad_sequence([ts[i][:w] for i, w in big], batch_first=True).cpu().numpy()
+        for (i, w), h in zip(big, full):
+            try:
+                out[i] = _unpack_one(ts[i], h[:w].tolist())
+            except Exception as e:  # noqa: BLE001
+                out[i] = e
     for i, t in enumerate(ts):
         if out[i] is None:
             try:
@@ -404,15 +416,44 @@ class VerifierCache:
         return self._sig[key]
 
 
+def _range_table(sq):
+    """The query's Ranges as int64 columns (u, l, offset) plus a validity
+    mask, built once per survey object (a Python loop over 2070 columns per
+    DP list cost ~2 ms each on the range plane's critical path)."""
+    cached = getattr(sq, "_range_table_cache", None)
+    rg = sq.Query.Ranges or []
+    if cached is not None and cached[0] is rg:
+        return cached[1]
+    n = len(rg)
+    tab = np.zeros((4, n), dtype=np.int64)
+    for c, r in enumerate(rg):
+        if r is None or len(r) < 2:
+            continue
+        off = int(r[2]) if len(r) > 2 else 0
+        if not (0 <= off < (1 << 63)):
+            continue
+        tab[:, c] = (int(r[0]), int(r[1]), off, 1)
+    try:
+        sq._range_table_cache = (rg, tab)
+    except AttributeError:
+        pass
+    return tab
+
+
 def _ranges_ok(sq, rpl) -> bool:
-    rg = sq.Query.Ranges
-    for j, col in enumerate(rpl.cols):
-        r = rg[col] if col < len(rg) else None
-        if r is None or int(r[0]) != rpl.u or int(r[1]) != rpl.l:
-            return False
-        if (int(r[2]) if len(r) > 2 else 0) != int(rpl.offset[j]):
-            return False
-    return True
+    """Every proof of the list claims its column's (u, l, offset) from the query."""
+    tab = _range_table(sq)
+    cols = np.asarray(rpl.cols, dtype=np.int64)
+    if cols.size == 0:
+        return True
+    if cols.min() < 0 or cols.max() >= tab.shape[1]:
+        return False
+    try:
+        offs = np.asarray(rpl.offset, dtype=np.int64)
+    except (OverflowError, TypeError, ValueError):
+        return False
+    t = tab[:, cols]
+    return bool(t[3].all() and (t[0] == rpl.u).all() and (t[1] == rpl.l).all() and (t[2] == offs).all())
 
 
 def verify_content(req: ProofRequest, sq, device, cache: VerifierCache) -> bool:

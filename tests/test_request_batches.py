@@ -86,3 +86,22 @@ def test_unpack_many_rejects_malformed(bundles):
     out = prq.range_bundle_unpack_many([bad_len, bad_size, bad_n, tiny, ts[3]])
     assert all(isinstance(o, Exception) for o in out[:4])
     assert isinstance(out[4], list)
+
+
+def test_unpack_many_wide_lists():
+    """Bundles of ONE list with more than 64 proofs (a wide query's DP list:
+    2070 proofs for SPECTF LR) decode through the batched header path, equal to
+    the one-bundle decode, and a truncated one is rejected alone."""
+    vals = list(range(70))
+    pk = eg.pk_table(eg.KeyPair.generate().public)
+    cv, _ = eg.encrypt_ints(pk, vals)
+    cols = [i % 5 for i in range(70)]
+    lists = [rp.RangeProofList(0, 0, 0, [7 * i for i in range(70)], cols, cv)]
+    t = prq.range_bundle_pack(lists)
+    short = t[:-24]
+    out = prq.range_bundle_unpack_many([t, t.clone(), short])
+    ref = prq.range_bundle_unpack(t)
+    for got in out[:2]:
+        assert got[0].offset == ref[0].offset and got[0].cols == ref[0].cols
+        assert torch.equal(got[0].commit.K, ref[0].commit.K) and torch.equal(got[0].commit.C, ref[0].commit.C)
+    assert isinstance(out[2], Exception)
