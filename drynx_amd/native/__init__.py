@@ -108,6 +108,7 @@ _SIGS = {
     "dx_gt_cyclotomic": [_I, _P, _P, _P, _L],
     "dx_gt_membership": [_I, _P, _P, _P, _L],
     "dx_g1_horner_host": [_P, _P, _L, _I, _I],
+    "dx_fp_sqrt_host": [_P, _P, _P, _P, _L],
     "dx_g2_subgroup": [_I, _P, _P, _P, _L],
     "dx_limbs_canonical": [_I, _P, _P, _I, _P, _L],
     "dx_g1j_on_curve": [_I, _P, _P, _P, _L],
@@ -833,6 +834,25 @@ def hash_to_g1(seed: bytes, start: int, n: int, device) -> torch.Tensor:
     _call("dx_hash_to_g1", g, s, sd.ctypes.data_as(ctypes.c_void_p), e.ctypes.data_as(ctypes.c_void_p), start,
           _ptr(out), n)
     return out
+
+
+def fp_sqrt_host(vals: list) -> list:
+    """[(sqrt or None)] of Python ints mod p (p = 3 mod 4: a^((p+1)/4)), one
+    native host batch."""
+    from ..crypto import oracle as _O
+
+    n = len(vals)
+    if n == 0:
+        return []
+    a = np.frombuffer(b"".join((int(v) % _O.P).to_bytes(32, "little") for v in vals), dtype="<u4").copy()
+    e = np.frombuffer(((_O.P + 1) // 4).to_bytes(32, "little"), dtype="<u4").copy()
+    y = np.empty(8 * n, dtype="<u4")
+    ok = np.empty(n, dtype=np.uint8)
+    p = lambda x: x.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    if _load().dx_fp_sqrt_host(p(a), p(e), p(y), p(ok), n):
+        raise RuntimeError("dx_fp_sqrt_host failed")
+    yb = y.tobytes()
+    return [int.from_bytes(yb[32 * i: 32 * i + 32], "little") if ok[i] else None for i in range(n)]
 
 
 def prg_scalars(key: bytes, n: int, device) -> torch.Tensor:
