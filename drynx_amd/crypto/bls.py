@@ -112,7 +112,8 @@ def aggregate(publics: list, partials: dict) -> tuple:
     if not items:
         return None
     # every t_i sigma_i in one native batch, then one sum
-    prods = nt.g1_mul(bn.g1_jac_tensor([s for _, s in items], "cpu"), bn.scalars_tensor([t[i] for i, _ in items], "cpu"))
+    prods = nt.g1_mul(bn.g1_jac_tensor([s for _, s in items], "cpu"),
+                      bn.scalars_tensor([t[i] for i, _ in items], "cpu"))
     return bn.g1_points_from_jac(nt.g1_sum(prods.view(-1, 1, 24)))[0]
 
 

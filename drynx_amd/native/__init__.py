@@ -1390,7 +1390,7 @@ def _bucket_plan(k: torch.Tensor, W: int, group: torch.Tensor | None = None, n_g
     sc[:, 0] = torch.from_numpy((bk & mask).astype("int32"))
     slot = torch.from_numpy((bk & mask) * W + (bk >> c))
     return {"item": item, "passes": passes, "bk": bk, "single": not passes,
-            "digit_sc": sc.to(dev), "slot": slot.to(dev), "W": W, "c": c}
+            "digit_sc": _upload(sc.numpy(), dev), "slot": _upload(slot.numpy(), dev), "W": W, "c": c}
 
 
 def _multi_exp64_run(a: torch.Tensor, plan) -> torch.Tensor:
@@ -1447,7 +1447,7 @@ def multi_exp_grouped(a: torch.Tensor, k: torch.Tensor, group, n_groups: int, W:
     bkp = gt_pow(cur, plan["digit_sc"])
     D = 1 << c
     g, w, d = bk // (W * D), (bk >> c) % W, bk & (D - 1)
-    slot = torch.from_numpy(d * (n_groups * W) + g * W + w).to(a.device)
+    slot = _upload(d * (n_groups * W) + g * W + w, a.device)
     win = gt_one(a.device).repeat(D * n_groups * W, 1)
     win[slot] = bkp
     win = win.view(D, n_groups * W, 96)
@@ -1530,7 +1530,7 @@ def g1_msm_launch(P_jac: torch.Tensor, k: torch.Tensor, group: torch.Tensor | No
         cur = g1_slice_sum(P_jac if i == 0 else cur, plan["item"] if i == 0 else None, st, ln)
     sc = torch.zeros((bk.size, 8), dtype=torch.int32)
     sc[:, 0] = torch.from_numpy((bk % 256).astype("int32"))
-    weighted = g1_mul(cur, sc.to(dev))                                   # d * B_{g,w,d}
+    weighted = g1_mul(cur, _upload(sc.numpy(), dev))                     # d * B_{g,w,d}
     # per-(group, window) sums: buckets are sorted by key = (g*W + w)*256 + d,
     # so each (group, window) is a contiguous run
     gws, counts = np.unique(bk // 256, return_counts=True)

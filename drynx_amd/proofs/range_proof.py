@@ -1142,13 +1142,14 @@ def _segment_pass(r: RangeProofList, segs: list, redo: list, x: dict) -> dict:
         return torch.cat([t[v * w:(v + 1) * w] for v in redo]) if Gf > 1 else t[redo[0] * w:(redo[0] + 1) * w]
 
     rho, ab, w = rows(x["rho"], m), rows(x["ab"], m), rows(x["w"], n)
+    # every input and every bucket plan (one host sync each) first, then the
+    # device passes: a plan's sync then never waits behind another MSM's
+    # queued passes (the first pass's schedule)
     # R_(v,s) = sum_{it in s} rho_it Zphi_(p,j) V_it
     it = torch.arange(m, device=dev)
     zi = (it // (S * l)) * l + it % l
     s_r = nt.fr_arith(nt.FR_MUL, rho, r.zphi.index_select(0, zi).repeat(Gf, 1).contiguous())
     grp = (fi * nseg + iseg.view(1, m)).reshape(-1).to(torch.int32)
-    hR = nt.g2_msm_launch(r.V, s_r, grp, K, c=_seg_c(Gf * m, K))
-    S_R = nt.g2_msm_run(r.V, hR)
     # prod a^rho per (v, s) (32-bit halves over (A, frob^8 A)) and each
     # segment's own GT-membership combination prod a^gamma (the VN's gammas)
     k = torch.zeros((2 * Gf, 2 * m, 8), dtype=torch.int32, device=dev)
@@ -1156,28 +1157,38 @@ def _segment_pass(r: RangeProofList, segs: list, redo: list, x: dict) -> dict:
     k[:Gf, :m, 0] = abv[:, :, 0]
     k[:Gf, m:, 0] = abv[:, :, 1]
     k[Gf:, :m] = rows(x["gam"], m).view(Gf, m, 8)
+    k = k.view(-1, 8)
     fi2 = torch.arange(2 * Gf, device=dev).view(2 * Gf, 1)
     grp2 = (fi2 * nseg + iseg.repeat(2).view(1, 2 * m)).reshape(-1).to(torch.int32)
-    mexp = nt.multi_exp_grouped(x["A2"], k.view(-1, 8), grp2, 2 * K, W=x["wc"][0], c=x["wc"][1])
-    # sum rho Zv, sum w Zr, sum w z per (v, s): per-proof sums, then per-segment
-    offs = torch.from_numpy((np.arange(Gf).reshape(Gf, 1) * n + poff[:-1].reshape(1, nseg)).reshape(-1))
-    offs = bn.h2d(torch.cat([offs, torch.tensor([Gf * n])]), dev)
-    e = nt.fr_seg_sum(nt.fr_dot_rows(rho, r.zv.repeat(Gf, 1).contiguous(), Gf * n), offs)
-    dzr = nt.fr_seg_sum(nt.fr_arith(nt.FR_MUL, w, r.zr.repeat(Gf, 1).contiguous()), offs)
-    dz = nt.fr_seg_sum(nt.fr_arith(nt.FR_MUL, w, x["z"].repeat(Gf, 1).contiguous()), offs)
     # D-check per (v, s): sum w c C' - sum w D (groups (v, which, s))
     wc = nt.fr_arith(nt.FR_MUL, w, r.challenge.repeat(Gf, 1).contiguous())
     dsc = torch.stack([wc.view(Gf, n, 8), w.view(Gf, n, 8)], 1).reshape(-1, 8).contiguous()
     grp3 = ((fi.view(Gf, 1, 1) * 2 + torch.arange(2, device=dev).view(1, 2, 1)) * nseg
             + pseg.view(1, 1, n)).reshape(-1).to(torch.int32)
     dpts = torch.cat([x["Cp"].contiguous(), r.D.contiguous()]).repeat(Gf, 1)
-    dh = nt.g1_msm_launch(dpts, dsc, grp3, 2 * K, bits=256)
+    with timers.span("rp.seg.plans"):
+        hR = nt.g2_msm_launch(r.V, s_r, grp, K, c=_seg_c(Gf * m, K))
+        mplan = nt.multi_exp_plan(k, grp2, 2 * K, W=x["wc"][0], c=x["wc"][1])
+        dplan = nt.g1_msm_plan(dsc, grp3, 2 * K)
+    with timers.span("rp.seg.passes"):
+        S_R = nt.g2_msm_run(r.V, hR)
+        mexp = nt.multi_exp_grouped(x["A2"], k, grp2, 2 * K, W=x["wc"][0], c=x["wc"][1], plan=mplan)
+        dh = nt.g1_msm_launch(dpts, dsc, grp3, 2 * K, bits=256, plan=dplan)
+    # sum rho Zv, sum w Zr, sum w z per (v, s): per-proof sums, then per-segment
+    offs = torch.from_numpy((np.arange(Gf).reshape(Gf, 1) * n + poff[:-1].reshape(1, nseg)).reshape(-1))
+    offs = bn.h2d(torch.cat([offs, torch.tensor([Gf * n])]), dev)
+    e = nt.fr_seg_sum(nt.fr_dot_rows(rho, r.zv.repeat(Gf, 1).contiguous(), Gf * n), offs)
+    dzr = nt.fr_seg_sum(nt.fr_arith(nt.FR_MUL, w, r.zr.repeat(Gf, 1).contiguous()), offs)
+    dz = nt.fr_seg_sum(nt.fr_arith(nt.FR_MUL, w, x["z"].repeat(Gf, 1).contiguous()), offs)
     # host: Horner steps, Miller loops of B with each R_(v,s), final exps
-    GG = nt.multi_exp_grouped_finish(mexp)                             # [2K, 96]
-    m_ok = _gt_in_subgroup_each(GG[K:])
+    with timers.span("rp.seg.gt_finish"):
+        GG = nt.multi_exp_grouped_finish(mexp)                         # [2K, 96]
+        m_ok = _gt_in_subgroup_each(GG[K:])
     GG = GG[:K]
-    fR, rok = _msm_r_miller(hR, S_R)
-    D_all = nt.g1_msm_finish(dh).view(Gf, 2, nseg, 24)
+    with timers.span("rp.seg.r_finish"):
+        fR, rok = _msm_r_miller(hR, S_R)
+    with timers.span("rp.seg.d_finish"):
+        D_all = nt.g1_msm_finish(dh).view(Gf, 2, nseg, 24)
     e, dzr, dz = e.cpu(), dzr.cpu(), dz.cpu()
     useg = torch.stack([x["useg"][v] for v in redo]).view(K, 96)
     useg_ok = x["u_seg"].cpu()[redo].reshape(-1).tolist()
