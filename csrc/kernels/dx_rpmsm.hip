@@ -175,6 +175,39 @@ DX_HD void msm_keys_one(const uint32_t *k, const int32_t *grp, int64_t gstride, 
 }
 
 #define DX_TID() const int64_t i = (int64_t)blockIdx.x * kWG + threadIdx.x
+// Bucket weights of a Pippenger window by running sums, per chunk of
+// buckets whose digits lie in one aligned range [base, base + L): with the
+// buckets sorted by digit, sum_i d_i B_i = base * sum_i B_i + sum_t A_t,
+// A_t = sum_{d_i - base >= t} B_i for t = top .. 1 -- about 2 additions per
+// bucket plus one short multiplication by base per chunk, instead of one
+// double-and-add by a c-bit digit per bucket (~20 G2 operations each).
+DX_HD void chunk_weight_one(const uint32_t *B_jac, const int32_t *d, const int64_t *start, const int32_t *len,
+                            const int32_t *base, uint32_t *out, int64_t ch) {
+  const int64_t a = start[ch];
+  const int n = len[ch];
+  const uint32_t b0 = (uint32_t)base[ch];
+  G2J acc = G2J::inf(), tot = G2J::inf();
+  int i = n - 1;
+  int t = (int)((uint32_t)d[a + i] - b0);
+  for (; t >= 1; t--) {
+    while (i >= 0 && (int)((uint32_t)d[a + i] - b0) == t) {
+      acc = jadd(acc, at<G2J>(B_jac, a + i));
+      i--;
+    }
+    tot = jadd(tot, acc);
+  }
+  for (; i >= 0; i--) acc = jadd(acc, at<G2J>(B_jac, a + i));  // offset 0: weight base only
+  if (b0) {
+    G2J m = G2J::inf();
+    for (int bit = 30; bit >= 0; bit--) {
+      m = jdbl(m);
+      if ((b0 >> bit) & 1u) m = jadd(m, acc);
+    }
+    tot = jadd(tot, m);
+  }
+  at<G2J>(out, ch) = tot;
+}
+
 __global__ void __launch_bounds__(256) msm_keys_kernel(const uint32_t *k, const int32_t *grp, int64_t gstride,
                                                        int64_t n, int c, int W, int32_t *keys, int32_t *items) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -200,6 +233,12 @@ __global__ void __launch_bounds__(kWG) DX_OCC mul_small_kernel(const uint32_t *i
                                                               int64_t n) {
   DX_TID();
   if (i < n) mul_small_one(in, d, out, i);
+}
+__global__ void __launch_bounds__(kWG) DX_OCC chunk_weight_kernel(const uint32_t *B, const int32_t *d,
+                                                                 const int64_t *start, const int32_t *len,
+                                                                 const int32_t *base, uint32_t *out, int64_t n) {
+  DX_TID();
+  if (i < n) chunk_weight_one(B, d, start, len, base, out, i);
 }
 __global__ void __launch_bounds__(kWG) DX_OCC horner_kernel(const uint32_t *S, uint32_t *out, int W, int c,
                                                            int64_t stride, int64_t offset, int64_t n) {
@@ -279,6 +318,20 @@ int dx_g2_mul_small(int on_gpu, void *stream, const uint32_t *in_jac, const int3
   }
   hipLaunchKernelGGL(mul_small_kernel, grid_of(n), dim3(kWG), 0, (hipStream_t)stream, in_jac, d, out, n);
   return check_hip(hipGetLastError(), "g2_mul_small");
+}
+
+// out[ch] = sum_{i in chunk ch} d[i] * B[i] (Jacobian; chunk = start/len over
+// digit-sorted buckets whose digits lie in [base, base + L))
+int dx_g2_chunk_weight(int on_gpu, void *stream, const uint32_t *B_jac, const int32_t *d, const int64_t *start,
+                       const int32_t *len, const int32_t *base, uint32_t *out, int64_t n) {
+  if (n <= 0) return 0;
+  if (!on_gpu) {
+    host_for_each(n, [=](int64_t i) { chunk_weight_one(B_jac, d, start, len, base, out, i); });
+    return 0;
+  }
+  hipLaunchKernelGGL(chunk_weight_kernel, grid_of(n), dim3(kWG), 0, (hipStream_t)stream, B_jac, d, start, len, base,
+                     out, n);
+  return check_hip(hipGetLastError(), "g2_chunk_weight");
 }
 
 // Per group g < G: acc = S[g*W + W-1]; acc = 2^c acc + S[g*W + w] for w = W-2..0;

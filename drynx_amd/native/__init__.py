@@ -109,6 +109,7 @@ _SIGS = {
     "dx_gt_membership": [_I, _P, _P, _P, _L],
     "dx_g1_horner_host": [_P, _P, _L, _I, _I],
     "dx_fp_sqrt_host": [_P, _P, _P, _P, _L],
+    "dx_g2_chunk_weight": [_I, _P, _P, _P, _P, _P, _P, _P, _L],
     "dx_g2_subgroup": [_I, _P, _P, _P, _L],
     "dx_limbs_canonical": [_I, _P, _P, _I, _P, _L],
     "dx_g1j_on_curve": [_I, _P, _P, _P, _L],
@@ -1605,6 +1606,24 @@ def g2_slice_sum(src: torch.Tensor, idx, start: torch.Tensor, length: torch.Tens
     return out
 
 
+G2_CHUNK = 32  # digit range of one running-sum chunk of Pippenger buckets
+
+
+def g2_chunk_weight(B_jac: torch.Tensor, d: torch.Tensor, start: torch.Tensor, length: torch.Tensor,
+                    base: torch.Tensor) -> torch.Tensor:
+    """out[ch] = sum_{i in chunk ch} d[i] B[i] over digit-sorted Jacobian
+    buckets (chunk: start/length rows whose digits lie in [base, base +
+    G2_CHUNK)) -- running sums instead of one multiplication per bucket."""
+    n = start.numel()
+    assert B_jac.shape[-1] == 48 and d.dtype == torch.int32 and start.dtype == torch.int64
+    assert length.dtype == torch.int32 and base.dtype == torch.int32 and base.numel() == n
+    out = torch.empty((n, 48), dtype=torch.int32, device=B_jac.device)
+    g, s = _ctx(B_jac, d, start, length, base)
+    _call("dx_g2_chunk_weight", g, s, _ptr(B_jac.contiguous()), _ptr(d.contiguous()), _ptr(start), _ptr(length),
+          _ptr(base), _ptr(out), n)
+    return out
+
+
 def g2_mul_small(jac: torch.Tensor, d: torch.Tensor) -> torch.Tensor:
     """d[i] * jac[i] (Jacobian G2, 0 <= d < 2^31)."""
     n = _rows(jac, 48)
@@ -1645,8 +1664,18 @@ def g2_msm_launch(P_aff: torch.Tensor, k: torch.Tensor, group: torch.Tensor | No
         if not passes:  # every bucket holds one entry
             passes = [(torch.arange(bk.size, device=dev), torch.ones(bk.size, dtype=torch.int32, device=dev))]
         h["passes"] = passes
-        h["d"] = _upload((bk & ((1 << c) - 1)).astype("int32"), dev)
-        gws, gcounts = np.unique(bk >> c, return_counts=True)
+        dig = bk & ((1 << c) - 1)
+        h["d"] = _upload(dig.astype("int32"), dev)
+        # bucket weights by running sums over chunks of digit range G2_CHUNK
+        # (csrc/kernels/dx_rpmsm.hip chunk_weight_one), then per-window sums of
+        # the chunk results
+        gw = bk >> c
+        ck = gw * ((1 << c) // G2_CHUNK + 1) + dig // G2_CHUNK
+        first = np.flatnonzero(np.r_[True, ck[1:] != ck[:-1]])
+        clen = np.diff(np.r_[first, bk.size])
+        h["chunks"] = (_upload(first.astype(np.int64), dev), _upload(clen.astype(np.int32), dev),
+                       _upload(((dig[first] // G2_CHUNK) * G2_CHUNK).astype(np.int32), dev))
+        gws, gcounts = np.unique(gw[first], return_counts=True)
         h["gws"] = _upload(gws.astype(np.int64), dev)
         h["gpasses"] = _segment_passes_dev(gcounts, dev)
     return h
@@ -1663,7 +1692,7 @@ def g2_msm_run(P_aff: torch.Tensor, h: dict) -> torch.Tensor:
         for i, (st, ln) in enumerate(h["passes"]):
             cur = g2_slice_sum(P_aff if i == 0 else cur, h["item"] if i == 0 else None, st, ln, i == 0,
                                h["m"] if i == 0 else 0)
-        cur = g2_mul_small(cur, h["d"])
+        cur = g2_chunk_weight(cur, h["d"], *h["chunks"])
         for st, ln in h["gpasses"]:
             cur = g2_slice_sum(cur, None, st, ln, False)
         S[h["gws"]] = cur

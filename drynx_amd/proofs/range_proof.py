@@ -1120,8 +1120,9 @@ def _seg_products(msq: dict) -> torch.Tensor:
 
 def _seg_c(n_entries: int, n_groups: int, bits: int = 254) -> int:
     """Window of a grouped G2 MSM: entries x windows bucket additions plus
-    ~36 G2 operations per (group, window, digit) bucket weight."""
-    return min(range(6, 14), key=lambda c: -(-bits // c) * (n_entries + n_groups * (1 << c) * 36))
+    ~3 G2 operations per (group, window, digit) bucket for its weight (running
+    sums per chunk, ``nt.g2_chunk_weight``)."""
+    return min(range(6, 14), key=lambda c: -(-bits // c) * (n_entries + n_groups * (1 << c) * 3))
 
 
 def _segment_pass(r: RangeProofList, segs: list, redo: list, x: dict) -> dict:
