@@ -116,19 +116,49 @@ class BlobSegment:
             with timers.span("ledger.encode"):
                 data = produce()
         with timers.span("ledger.write"):
-            off = self._f.seek(0, os.SEEK_END)
-            if many:
-                out = []
-                for d in data:
-                    n = memoryview(d).nbytes
-                    self._f.write(d)
-                    out.append((off, n))
-                    off += n
-                self._f.flush()
-                return out
-            self._f.write(data)
             self._f.flush()
-        return off, memoryview(data).nbytes
+            off = self._f.seek(0, os.SEEK_END)
+            bufs = [memoryview(d).cast("B") for d in (data if many else [data])]
+            out, pos = [], off
+            for b in bufs:
+                out.append((pos, b.nbytes))
+                pos += b.nbytes
+            self._pwrite_all(bufs, off)
+            self._f.seek(0, os.SEEK_END)
+        return out if many else out[0]
+
+    _PIECE = 32 << 20  # bytes per parallel write
+
+    def _pwrite_all(self, bufs: list, off: int):
+        """The buffers back to back from ``off``, in pieces written by several
+        threads with positioned writes (they release the GIL; one sequential
+        write of a query's ~540 MB of range proofs took ~50 ms)."""
+        pieces, pos = [], off
+        for b in bufs:
+            for a in range(0, b.nbytes, self._PIECE):
+                pieces.append((b[a: a + self._PIECE], pos + a))
+            pos += b.nbytes
+        if not hasattr(self, "_pfd"):
+            # positioned writes need a descriptor WITHOUT O_APPEND (Linux
+            # appends every pwrite on an O_APPEND descriptor, ignoring the offset)
+            self._pfd = os.open(self.path, os.O_WRONLY | os.O_CREAT, 0o644)
+        fd = self._pfd
+
+        def put(item):
+            view, at = item
+            while view.nbytes:
+                k = os.pwrite(fd, view, at)
+                view, at = view[k:], at + k
+
+        if len(pieces) <= 1:
+            for it in pieces:
+                put(it)
+            return
+        if not hasattr(self, "_wpool"):
+            import concurrent.futures as cf
+
+            self._wpool = cf.ThreadPoolExecutor(max_workers=4, thread_name_prefix="drynx-ledger-w")
+        list(self._wpool.map(put, pieces))
 
     def flush(self):
         with self._lock:
@@ -139,6 +169,9 @@ class BlobSegment:
     def close(self, remove: bool = False):
         self._ex.shutdown(wait=True)
         self._f.close()
+        if hasattr(self, "_pfd"):
+            os.close(self._pfd)
+            del self._pfd
         if remove:
             try:
                 os.remove(self.path)
