@@ -376,7 +376,9 @@ class DrynxNode:
         if self.device.type != "cuda":
             return self._client_pool.submit(fn, partial)
         if not hasattr(self, "_client_stream"):
-            self._client_stream = torch.cuda.Stream(self.device)
+            # high priority: the querier's decrypt/BSGS kernels are short and
+            # would otherwise queue behind the VNs' MSM passes (75 ms vs 10 ms)
+            self._client_stream = torch.cuda.Stream(self.device, priority=-1)
         side = self._client_stream
         side.wait_stream(torch.cuda.current_stream(self.device))  # result tensors are ready on `side`
 
