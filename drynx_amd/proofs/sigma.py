@@ -484,14 +484,16 @@ def key_switch_shares_batch(secrets: list, publics: list, K: torch.Tensor, Q_poi
     n, c = K.shape[0], len(secrets)
     tabB = bn.base_table(dev)
     tabQ = pk_table(Q_point, dev).tabP
-    bs = [O.random_scalar() for _ in secrets] if with_proofs else None
-    # every CN's secret (and commitment scalar b) in ONE upload, each row
-    # repeated n times on the device
-    per = _sc(list(secrets) + (bs or []), dev)
-    scal = per.repeat_interleave(n, dim=0)
+    Kt = K.repeat(c, 1).contiguous()
+    x_rep = torch.cat([_sc([x], dev).expand(n, 8) for x in secrets]).contiguous()
     v = bn.random_scalars(c * n, dev)
+    scal = [x_rep]
+    bs = None
+    if with_proofs:
+        bs = [O.random_scalar() for _ in secrets]
+        scal.append(torch.cat([_sc([b], dev).expand(n, 8) for b in bs]).contiguous())
     with timers.span("ks.varmul"):
-        prods = nt.g1_mul(K.repeat(per.shape[0], 1).contiguous(), scal)
+        prods = nt.g1_mul(torch.cat([Kt] * len(scal)).contiguous(), torch.cat(scal).contiguous())
     xK = prods[: c * n].contiguous()
     with timers.span("ks.fixedbase"):
         vB = nt.g1_fb_mul(tabB, v)
