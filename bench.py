@@ -28,8 +28,9 @@ scaling = strong: the query is fixed; N GPUs share it (DPs round robin over the
 vs_baseline = value / 315.6, the reference's verifications per second of
          end-to-end time in that run (20,700 x 3 / 196.77 s).
 
-Run: python bench.py [--gpus N --steps K --warmup W]; for N>1 under
-torch.distributed.run (one rank per GPU, RCCL over xGMI).
+Run: python bench.py [--gpus N --steps K --warmup W].  N > 1 runs one rank
+per GPU (RCCL over xGMI): under torch.distributed.run, or, when started
+directly, bench.py launches torch.distributed.run with N ranks itself.
 
 Other BASELINE.json configs (``--query``; same harness, one JSON line each;
 value = end-to-end latency in seconds of one verifiable query, lower is
@@ -49,6 +50,8 @@ import argparse
 import copy
 import json
 import os
+import socket
+import subprocess
 import sys
 import tempfile
 import time
@@ -109,14 +112,52 @@ def parse():
     return ap.parse_args()
 
 
+def _launch_ranks(args) -> int | None:
+    """``--gpus N`` (N > 1) run directly, not under a launcher: start N ranks
+    through torch.distributed.run as a CHILD process (this process has made
+    no GPU call yet -- nothing here may touch HIP) and hand back its exit
+    code; rank 0's JSON line reaches our stdout unchanged.  The reference
+    likewise runs every party as its own process (simul/drynx_simul.go:83-98).
+    Under a launcher (WORLD_SIZE set) returns None and the ranks run here."""
+    if "WORLD_SIZE" in os.environ or args.gpus <= 1:
+        return None
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS=os.environ.get("OMP_NUM_THREADS", "1"))
+    return subprocess.call(cmd, env=env)
+
+
+def _check_world(args, comm):
+    if comm.world != args.gpus:
+        sys.exit(f"bench: --gpus {args.gpus} but the job has {comm.world} rank(s)")
+
+
+def _rank_record(comm, cl, step_ms, elapsed, setup_s, b0) -> dict:
+    """This rank's share of the job: its parties, step times, data-plane
+    traffic over the timed steps and the range items it checked for the VN
+    pool (gathered to rank 0 into the JSON's ``ranks``)."""
+    roles = {r: [p.id for p in cl.local(comm.rank, r)] for r in ("cn", "vn", "dp")}
+    return {"rank": comm.rank, "roles": roles, "step_ms": step_ms, "elapsed_ms": round(1000 * elapsed, 1),
+            "setup_s": round(setup_s, 3), "bytes_sent": comm.bytes_sent - b0[0], "bytes_recv": comm.bytes_recv - b0[1],
+            "pool_range_items": timers.counters().get("pool.range_items", 0)}
+
+
 def main():
     args = parse()
+    rc = _launch_ranks(args)
+    if rc is not None:
+        sys.exit(rc)
     if args.query == "lr_dro" and args.dro is None:
         args.dro = 10_000
     if args.query not in ("lr", "lr_dro"):
         return main_query(args)
     init_distributed()
     comm = make_comm(args.device)
+    _check_world(args, comm)
     world, rank = comm.world, comm.rank
     device = comm.device
     if device.type == "cuda":
@@ -192,12 +233,14 @@ def main():
             first_s = time.perf_counter() - t_first
     if args.warmup == 0:
         first_s = 0.0
-    setup_s = max(comm.all_gather_object(time.perf_counter() - t_setup if args.warmup else 0.0))
+    my_setup_s = time.perf_counter() - t_setup if args.warmup else 0.0
+    setup_s = max(comm.all_gather_object(my_setup_s))
     table_bytes = sum(comm.all_gather_object(sum(sm.table_bytes() for sm in node.verifier_cache._sig.values())))
     timers.reset()
     comm.barrier()
     if device.type == "cuda":
         torch.cuda.synchronize()
+    b0 = (comm.bytes_sent, comm.bytes_recv)
     t0 = time.perf_counter()
     blocks, checks, step_ms = [], [], []
     prof = _torch_profiler(rank)
@@ -212,8 +255,9 @@ def main():
     comm.barrier()
     if device.type == "cuda":
         torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    elapsed = max(comm.all_gather_object(elapsed))
+    my_elapsed = time.perf_counter() - t0
+    elapsed = max(comm.all_gather_object(my_elapsed))
+    ranks = comm.all_gather_object(_rank_record(comm, cl, step_ms, my_elapsed, my_setup_s, b0))
     n_out = (d + 1) + (d + 1) ** 2
     proofs_per_step = n_dps * n_out
     verifs_per_step = proofs_per_step * n_vns  # threshold 1.0: every VN checks every proof
@@ -282,6 +326,8 @@ def main():
             "first_query_s": round(first_s, 3),
             "prover_table_bytes": int(table_bytes),
             "step_ms_rank0": step_ms,
+            "rccl_world": world if dist.is_initialized() and dist.get_backend() == "nccl" else 0,
+            "ranks": ranks,
             "phase_s": {k: round(v, 4) for k, v in sorted(phase.items()) if not k.startswith("dp") or "AllProofs" in k},
         }
         if args.dro:  # config 4: latency is the metric (one JSON line, same harness)
@@ -389,6 +435,7 @@ def main_query(args):
     cfg = QUERY_CONFIGS[args.query]
     init_distributed()
     comm = make_comm(args.device)
+    _check_world(args, comm)
     world, rank = comm.world, comm.rank
     device = comm.device
     if device.type == "cuda":

@@ -673,6 +673,8 @@ def verify_range_pool_part(reqs: list, vn_idxs: dict, sq, device, cache: Verifie
     for idxs, group in by_set.items():
         live = [i for i in idxs if base[i] and parts[i]]
         res = [{i: base[i] for i in idxs} for _ in group]
+        # work accounting: range items this rank checks, once per VN of the group
+        timers.count("pool.range_items", len(group) * sum(len(r) for i in live for r in parts[i]))
         if live:
             sigmat = cache.sigmat(sq, device)
             cl = [coins.get(vn) for vn in group]

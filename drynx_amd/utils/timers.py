@@ -127,9 +127,25 @@ def records() -> dict:
         return {k: list(v) for k, v in _records.items()}
 
 
+_counts: dict = defaultdict(int)
+
+
+def count(name: str, n: int = 1):
+    """Add ``n`` to a named work counter (e.g. range items this rank checked
+    for the VN pool); reported next to the timers, cleared by ``reset``."""
+    with _lock:
+        _counts[name] += int(n)
+
+
+def counters() -> dict:
+    with _lock:
+        return dict(_counts)
+
+
 def reset():
     with _lock:
         _records.clear()
+        _counts.clear()
 
 
 def summary() -> dict:

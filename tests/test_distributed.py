@@ -77,3 +77,60 @@ def test_bench_two_ranks_torchrun():
     line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
     d = json.loads(line) if (json := __import__("json")) else None
     assert d["n_gpus"] == 2 and d["all_proofs_valid"] and d["value"] > 0
+
+
+def _bench_line(r):
+    assert r.returncode == 0, r.stderr[-3000:]
+    import json
+
+    return json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+
+
+_SMALL = ["--steps", "1", "--warmup", "0", "--records", "2000", "--features", "2", "--max-iter", "5", "--device", "cpu"]
+
+
+@pytest.mark.slow
+def test_bench_self_launches_eight_ranks():
+    """``python bench.py --gpus 8`` with no launcher (the driver's BENCH form)
+    starts 8 ranks itself and runs the targeted placement: CNs on ranks 0-2,
+    VNs on 3-5, DPs round robin from rank 6 (ranks 6 and 7 host 2 DPs each),
+    every VN's range checks pooled in 1/8 slices over all ranks."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", *_SMALL],
+                       capture_output=True, text=True, timeout=900, env=env)
+    d = _bench_line(r)
+    assert d["n_gpus"] == 8 and d["all_proofs_valid"] and d["result_ok"]
+    ranks = {x["rank"]: x for x in d["ranks"]}
+    assert sorted(ranks) == list(range(8))
+    assert [ranks[k]["roles"]["cn"] for k in range(3)] == [["cn0"], ["cn1"], ["cn2"]]
+    assert [ranks[k]["roles"]["vn"] for k in range(3, 6)] == [["vn0"], ["vn1"], ["vn2"]]
+    assert sorted(ranks[6]["roles"]["dp"]) == ["dp0", "dp8"] and sorted(ranks[7]["roles"]["dp"]) == ["dp1", "dp9"]
+    assert all(len(ranks[k]["roles"]["dp"]) == 1 for k in range(6))
+    # pooled range checks: every (proof, VN) verification is done once, split in 1/8 slices
+    n_out = d["config"]["range_proof"]["proofs_per_query"] // d["config"]["dps"]
+    items = [ranks[k]["pool_range_items"] for k in range(8)]
+    assert sum(items) == d["config"]["range_proof"]["verifications_per_query"]
+    per_list_max = -(-n_out // 8)
+    assert max(items) <= per_list_max * d["config"]["dps"] * d["config"]["vns"]
+    # traffic: every rank took part in the data plane; the VN ranks receive the most
+    assert all(ranks[k]["bytes_sent"] > 0 and ranks[k]["bytes_recv"] > 0 for k in range(8))
+    assert min(ranks[k]["bytes_recv"] for k in (3, 4, 5)) > max(ranks[k]["bytes_recv"] for k in (0, 1, 2, 6, 7))
+
+
+@pytest.mark.slow
+def test_bench_self_launches_two_ranks():
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", *_SMALL],
+                       capture_output=True, text=True, timeout=600, env=env)
+    d = _bench_line(r)
+    assert d["n_gpus"] == 2 and d["all_proofs_valid"] and d["result_ok"] and len(d["ranks"]) == 2
+
+
+def test_bench_rejects_world_mismatch():
+    """Under a launcher whose world differs from --gpus the bench refuses to
+    print a number labelled with the wrong GPU count."""
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", *_SMALL],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode != 0 and "rank(s)" in r.stderr
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
