@@ -23,6 +23,17 @@ import torch
 from .. import native as nt
 
 
+def mask_bits(r: torch.Tensor, bits: int) -> torch.Tensor:
+    """Keep the low ``bits`` bits of every [n, 8] little-endian 32-bit-limb
+    scalar (in place): the words above the partial word are cleared and the
+    partial word is masked (bits = 40 keeps word 0 and the low 8 bits of word 1)."""
+    words, part = divmod(bits, 32)
+    r[:, words + (1 if part else 0):] = 0
+    if part:
+        r[:, words] &= (1 << part) - 1
+    return r
+
+
 class Coins:
     __slots__ = ("key", "_n", "_lock")
 
@@ -52,11 +63,7 @@ class Coins:
 
     def bits(self, n: int, device, bits: int = 64, odd: bool = False) -> torch.Tensor:
         """n uniform ``bits``-bit weights as [n, 8] scalars (``odd``: never 0)."""
-        r = self.scalars(n, device)
-        words = bits // 32
-        r[:, words:] = 0
-        if bits % 32:
-            r[:, words] &= (1 << (bits % 32)) - 1
+        r = mask_bits(self.scalars(n, device), bits)
         if odd:
             r[:, 0] |= 1
         return r

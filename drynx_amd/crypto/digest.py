@@ -59,21 +59,32 @@ def digest_rows(t: torch.Tensor) -> list:
     return [_finish(row_bytes, be[r].tobytes()) for r in range(t.shape[0])]
 
 
-def digest_many(tensors: list) -> list:
+def digest_many(tensors: list, flags: list | None = None):
     """``digest_tensor`` of many tensors of one device: one segmented launch
-    and ONE device-to-host copy for all of them (a VN inbox's envelopes)."""
+    and ONE device-to-host copy for all of them (a VN inbox's envelopes).
+    ``flags``: device bools (validity checks of the same payloads) read back
+    in that same copy -> (digests, [bool]) instead of the digests alone."""
     if not tensors:
-        return []
+        return ([], [bool(f) for f in flags]) if flags is not None else []
     dev = tensors[0].device
     same = all(t.device == dev for t in tensors)
     if not same:
-        return [digest_tensor(t) for t in tensors]
+        dg = [digest_tensor(t) for t in tensors]
+        return (dg, [bool(f) for f in flags]) if flags is not None else dg
     parts = nt.sha256_segments(tensors, CHUNK)
-    flat = torch.cat(parts) if len(parts) > 1 else parts[0]
-    be = flat.cpu().numpy().view(np.uint32).astype(">u4")
+    nf = len(flags) if flags else 0
+    if nf:
+        parts_f = parts + [torch.stack([f.reshape(()).to(dev) for f in flags]).to(parts[0].dtype).reshape(1, -1)]
+    else:
+        parts_f = parts
+    flat = torch.cat([p.reshape(-1) for p in parts_f]) if len(parts_f) > 1 else parts_f[0].reshape(-1)
+    host = flat.cpu().numpy()
+    be = host.view(np.uint32).astype(">u4")
     out, o = [], 0
     for t, p in zip(tensors, parts):
-        k = p.shape[0]
+        k = p.numel()
         out.append(_finish(t.numel() * t.element_size(), be[o: o + k].tobytes()))
         o += k
-    return out
+    if flags is None:
+        return out
+    return out, [bool(v) for v in host[o: o + nf]]

@@ -238,11 +238,17 @@ def _ctx(*ts):
     return 0, None
 
 
-def _call(name, *args):
+def _raw_call(name, *args) -> int:
+    """A native call whose return code the caller interprets; releases the
+    tensors ``_ptr`` held for it, like ``_call``."""
     try:
-        rc = getattr(_load(), name)(*args)
+        return getattr(_load(), name)(*args)
     finally:
         _keep.held = []
+
+
+def _call(name, *args):
+    rc = _raw_call(name, *args)
     if rc != 0:
         raise RuntimeError(f"native op {name} failed (rc={rc})")
 
@@ -363,7 +369,7 @@ def g1_mul(pts_jac: torch.Tensor, scalars: torch.Tensor) -> torch.Tensor:
     out = torch.empty((n, 24), dtype=torch.int32, device=scalars.device)
     g, s = _ctx(pts_jac, scalars)
     if g:  # gfx950: register-resident kernel with the window table in LDS (dx_g1_varmul.hip)
-        rc = _load().dx_g1_mul_fast(s, _ptr(pts_jac), _ptr(scalars), _ptr(out), n, int(np_ == 1 and n > 1),
+        rc = _raw_call("dx_g1_mul_fast", s, _ptr(pts_jac), _ptr(scalars), _ptr(out), n, int(np_ == 1 and n > 1),
                                     int(nk == 1 and n > 1))
         if rc:
             raise RuntimeError(f"dx_g1_mul_fast failed rc={rc}")
@@ -1000,7 +1006,7 @@ def lr_encode(X: torch.Tensor, y: torch.Tensor, mean: torch.Tensor, sd: torch.Te
     n_blocks = int(max(1, min(1024, (steps + 15) // 16)))
     partial = torch.empty((n_blocks, 48, 48), dtype=torch.float64, device=X.device)
     _, s = _ctx(X)
-    rc = _load().dx_lr_encode(s, _ptr(X), X.stride(0), N, dx, _ptr(mean), _ptr(sd), _ptr(y), float(wa), float(wb),
+    rc = _raw_call("dx_lr_encode", s, _ptr(X), X.stride(0), N, dx, _ptr(mean), _ptr(sd), _ptr(y), float(wa), float(wb),
                               _ptr(partial), n_blocks)
     if rc != 0:
         raise RuntimeError(f"dx_lr_encode failed rc={rc}")
@@ -1084,7 +1090,7 @@ def rp_verify_fold(ZB_jac, Y_jac, rho, V_aff, S: int, L: int) -> torch.Tensor:
     n = _rows(V_aff, 32)
     _, s = _ctx(ZB_jac, Y_jac, rho, V_aff)
     fb = torch.empty(((n + 63) // 64, 96), dtype=torch.int32, device=V_aff.device)
-    rc = _load().dx_rp_verify_fold(s, _ptr(ZB_jac), _ptr(Y_jac), _ptr(rho), _ptr(V_aff), _ptr(fb), n, S, L)
+    rc = _raw_call("dx_rp_verify_fold", s, _ptr(ZB_jac), _ptr(Y_jac), _ptr(rho), _ptr(V_aff), _ptr(fb), n, S, L)
     if rc:
         raise RuntimeError(f"dx_rp_verify_fold failed rc={rc}")
     return fb
@@ -1560,7 +1566,7 @@ def g1_msm_finish(h: dict) -> torch.Tensor:
     top = int((gws % W).max())
     out = torch.empty((G, 24), dtype=torch.int32)
     src = rows[:, : top + 1].contiguous()  # held: the host call reads it
-    rc = _load().dx_g1_horner_host(_ptr(src), _ptr(out), G, top + 1, 8)
+    rc = _raw_call("dx_g1_horner_host", _ptr(src), _ptr(out), G, top + 1, 8)
     if rc:
         raise RuntimeError(f"dx_g1_horner_host failed rc={rc}")
     return out

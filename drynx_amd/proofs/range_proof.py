@@ -659,12 +659,9 @@ def _prove_group(u, l, vals, offs, cols, r, cv, sigmat, P_point, device, mode=0,
 def _rand64(n, device, bits: int = 64) -> torch.Tensor:
     """Uniform ``bits``-bit batch weights from the ChaCha20 CSPRNG (device or
     host path), unknown to the prover."""
-    r = bn.random_scalars(n, device)
-    words = bits // 32
-    r[:, words:] = 0
-    if bits % 32:
-        r[:, words] &= (1 << (bits % 32)) - 1
-    return r
+    from ..crypto.coins import mask_bits
+
+    return mask_bits(bn.random_scalars(n, device), bits)
 
 
 def _gt_in_subgroup(g: torch.Tensor) -> bool:
@@ -967,7 +964,11 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
         with timers.span("rp.verify.segments"):
             per = _segment_pass(r, segs, redo, dict(
                 A2=A2, rho=rho_all, ab=ab_all, gam=gam_all, w=w_all, Cp=Cp, z=z, useg=useg, u_seg=msq["u_seg"],
-                PB_base=PB_base, gt_tab=gt_tab, wc=wc_, m_first=m_oks))
+                PB_base=PB_base, gt_tab=gt_tab, wc=wc_,
+                # undecodable proofs in the batch: the first pass's GT combination
+                # included a_ij not known to be cyclotomic, so it bounds nothing --
+                # every segment then gets its own combination
+                m_first=m_oks if seg_valid is None else [False] * G))
         for k_ in redo:
             if seg_valid is not None:
                 res[k_] = [a and b for a, b in zip(per[k_], seg_valid)]

@@ -46,12 +46,13 @@ def pts_be(jac: torch.Tensor) -> torch.Tensor:
     return xy.view(torch.uint8).view(-1, 32).flip(1).reshape(-1, 64)
 
 
-def points_digests(groups: list) -> list:
+def points_digests(groups: list, flags: list | None = None):
     """Per group (a list of Jacobian point tensors / CipherVectors) the chunked
     digest (crypto/digest.py) of the kyber encodings of all its points, in
     order: ONE normalisation launch, one encoding pass, one segmented SHA-256
     launch and ONE device-to-host copy for every group together (a
-    transcript is 3-6 vectors of thousands of points)."""
+    transcript is 3-6 vectors of thousands of points).  ``flags``: device
+    bools read back in the same copy -> (digests, [bool])."""
     from ..crypto import digest as dg
 
     flat, sizes = [], []
@@ -65,13 +66,14 @@ def points_digests(groups: list) -> list:
                 m += t.shape[0]
         sizes.append(m)
     if not flat:
-        return [dg.digest_bytes(b"") for _ in groups]
+        out = [dg.digest_bytes(b"") for _ in groups]
+        return (out, [bool(f) for f in flags]) if flags is not None else out
     be = pts_be(torch.cat(flat) if len(flat) > 1 else flat[0])
     views, o = [], 0
     for m in sizes:
         views.append(be[o: o + m])
         o += m
-    return dg.digest_many(views)
+    return dg.digest_many(views, flags)
 
 
 def fs_hash(context: str, raw: tuple, pts_digest: bytes) -> int:
@@ -128,6 +130,22 @@ def _scalars_ok(t: torch.Tensor) -> torch.Tensor:
     if t.numel() == 0:
         return torch.ones((), dtype=torch.bool, device=t.device)
     return nt.limbs_canonical(t.reshape(-1, 8), fr=True).bool().all()
+
+
+def _digest_checked(proofs: list, groups_of) -> None:
+    """Decoded data of received proofs, computed once per proof and shared by
+    co-hosted VNs: the transcript's point digest and the host verdict of the
+    payload's lazy well-formedness flag (every point row canonical and on the
+    curve, every response scalar canonical), read back in the digest's copy."""
+    todo = [pr for pr in proofs if not pr.pts_digest]
+    if not todo:
+        return
+    fl = [pr for pr in todo if isinstance(pr.wellformed, torch.Tensor)]
+    dgs, oks = points_digests([groups_of(pr) for pr in todo], [pr.wellformed for pr in fl])
+    for pr, d in zip(todo, dgs):
+        pr.pts_digest = d
+    for pr, ok in zip(fl, oks):
+        pr.wellformed = bool(ok)
 
 
 def _head_words(tensors: list, width: int) -> list:
@@ -239,6 +257,12 @@ def schnorr_verify_batch(items: list, device="cpu") -> list:
     return out
 
 
+# Fiat-Shamir context strings carry the transcript version: v2 = SHA-256 over
+# context || raw parts || chunked digest of the point encodings (crypto/digest.py).
+# Proofs made with another transcript layout fail the challenge check.
+OBF_CONTEXT = "proofTest/obfuscation/v2"
+KS_CONTEXT = "proofTest/keyswitch/v2"
+
 # ----------------------------------------------------------------------------- obfuscation (DLEQ)
 OBF_MAGIC = 0x4F425031  # "OBP1"
 _OBF_HEAD = 10          # magic, n, c (8 limbs)
@@ -252,6 +276,9 @@ class ObfuscationProof:
     c: int
     z: torch.Tensor     # [n, 8]
     pts_digest: bytes = b""  # decoded data: digest of the transcript's point encodings
+    # received payloads: device bool (every point canonical + on the curve, z
+    # canonical), a host bool once read back; None = built locally / decoded from bytes
+    wellformed: object = None
 
     # reference-style export (kyber affine encodings): ledger / GetProofs
     def to_bytes(self) -> bytes:
@@ -298,8 +325,10 @@ class ObfuscationProof:
             parts.append(t[o: o + 24 * n].view(n, 24))
             o += 24 * n
         z = t[o: o + 8 * n].view(n, 8)
+        if c >= O.R:
+            raise ValueError("non-canonical challenge in an obfuscation proof")
         return ObfuscationProof(CipherVector(parts[0], parts[1]), CipherVector(parts[2], parts[3]),
-                                CipherVector(parts[4], parts[5]), c, z)
+                                CipherVector(parts[4], parts[5]), c, z, wellformed=_points_ok(parts) & _scalars_ok(z))
 
 
 def obfuscation_list_proof_creation(C: CipherVector, Co: CipherVector, s: torch.Tensor) -> ObfuscationProof:
@@ -307,18 +336,17 @@ def obfuscation_list_proof_creation(C: CipherVector, Co: CipherVector, s: torch.
     dev = C.device
     a = bn.random_scalars(len(C), dev)
     T = C.mul_scalars(a)
-    c = fs_challenge("proofTest/obfuscation", C, Co, T)
+    c = fs_challenge(OBF_CONTEXT, C, Co, T)
     z = nt.fr_arith(nt.FR_ADD, a, nt.fr_arith(nt.FR_MUL, s, _sc([c], dev)))
     return ObfuscationProof(C, Co, T, c, z)
 
 
 def _obf_fs_ok(proofs: list) -> list:
     """Each proof's Fiat-Shamir check: the challenge recomputed from the
-    transcript's point digest (decoded data, computed once per proof)."""
-    todo = [pr for pr in proofs if not pr.pts_digest]
-    for pr, d in zip(todo, points_digests([[pr.C, pr.Co, pr.T] for pr in todo])):
-        pr.pts_digest = d
-    return [fs_hash("proofTest/obfuscation", (), pr.pts_digest) == pr.c for pr in proofs]
+    transcript's point digest (decoded data, computed once per proof), and
+    the payload's well-formedness."""
+    _digest_checked(proofs, lambda pr: [pr.C, pr.Co, pr.T])
+    return [pr.wellformed is not False and fs_hash(OBF_CONTEXT, (), pr.pts_digest) == pr.c for pr in proofs]
 
 
 def obfuscation_list_proof_verification(pr: ObfuscationProof, threshold: float = 1.0) -> bool:
@@ -356,6 +384,7 @@ class KeySwitchProof:
     za: torch.Tensor         # [n, 8]
     zb: int
     pts_digest: bytes = b""  # decoded data: digest of the transcript's point encodings
+    wellformed: object = None  # as ObfuscationProof.wellformed (K, share, T1, T2 rows; za)
 
     # reference-style export (kyber affine encodings): ledger / GetProofs
     def to_bytes(self) -> bytes:
@@ -387,6 +416,8 @@ class KeySwitchProof:
         c = int.from_bytes(b[o: o + 32], "big"); o += 32
         za = bn.scalars_from_bytes(np.frombuffer(b[o: o + 32 * n], dtype=np.uint8), device); o += 32 * n
         zb = int.from_bytes(b[o: o + 32], "big")
+        if c >= O.R or zb >= O.R:
+            raise ValueError("non-canonical scalar in a key-switch proof")
         return KeySwitchProof(X, Q, K, share, T1, T2, T3, c, za, zb)
 
     # intra-cluster payload: raw Montgomery limbs, no host marshalling
@@ -423,8 +454,10 @@ class KeySwitchProof:
             rows.append(t[o: o + 24 * n].view(n, 24))
             o += 24 * n
         za = t[o: o + 8 * n].view(n, 8)
+        if c >= O.R or zb >= O.R:
+            raise ValueError("non-canonical scalar in a key-switch proof header")
         return KeySwitchProof(X, Q, rows[0], CipherVector(rows[1], rows[2]), rows[3], rows[4], O.g1_to_bytes(T3),
-                              c, za, zb)
+                              c, za, zb, wellformed=_points_ok(rows) & _scalars_ok(za))
 
 
 def unpack_many(kind: str, tensors: list) -> list:
@@ -521,7 +554,7 @@ def finish_keyswitch_proofs(p: KeySwitchPending) -> list:
               for j in range(c_n)]
     with timers.span("ks.transcript"):
         dgs = points_digests(groups)
-    chs = [fs_hash("proofTest/keyswitch", (O.g1_to_bytes(p.publics[j]), Qb, T3s[j]), dgs[j]) for j in range(c_n)]
+    chs = [fs_hash(KS_CONTEXT, (O.g1_to_bytes(p.publics[j]), Qb, T3s[j]), dgs[j]) for j in range(c_n)]
     c_rep = torch.cat([_sc([ch], dev).expand(n, 8) for ch in chs]).contiguous()
     za = nt.fr_arith(nt.FR_ADD, p.a, nt.fr_arith(nt.FR_MUL, p.v, c_rep))
     out = []
@@ -546,7 +579,7 @@ def key_switch_list_proof_creation(x: int, X, Q_point, K: torch.Tensor, share: C
     T1 = nt.g1_fb_mul(tabB, a)
     T2 = nt.g1_add(nt.g1_fb_mul(tabQ, a), nt.g1_mul(K.contiguous(), _sc([b], dev)), subtract=True)
     T3 = O.g1_to_bytes(bn.g1_mul_point(b))
-    c = fs_challenge("proofTest/keyswitch", O.g1_to_bytes(X), O.g1_to_bytes(Q_point), T3, K, share, T1, T2)
+    c = fs_challenge(KS_CONTEXT, O.g1_to_bytes(X), O.g1_to_bytes(Q_point), T3, K, share, T1, T2)
     za = nt.fr_arith(nt.FR_ADD, a, nt.fr_arith(nt.FR_MUL, v, _sc([c], dev)))
     zb = (b + c * x) % O.R
     return KeySwitchProof(X, Q_point, K, share, T1, T2, T3, c, za, zb)
@@ -559,17 +592,14 @@ def _ks_fs_ok(proofs: list, copies: int = 1):
     nodes of one rank run their own checks in ONE native batch (zb B by one
     fixed-base call, c X by one variable-base call) -> one list per copy
     (copies > 1) or the list itself."""
-    todo = [pr for pr in proofs if not pr.pts_digest]
-    if todo:
-        with timers.span("ks.verify.transcripts"):
-            for pr, d in zip(todo, points_digests([[pr.K, pr.share, pr.T1, pr.T2] for pr in todo])):
-                pr.pts_digest = d
+    with timers.span("ks.verify.transcripts"):
+        _digest_checked(proofs, lambda pr: [pr.K, pr.share, pr.T1, pr.T2])
     rows, chs, idx = [], [], []
     res = [[False] * len(proofs) for _ in range(copies)]
     for cp in range(copies):
         for i, pr in enumerate(proofs):
-            c = fs_hash("proofTest/keyswitch", (O.g1_to_bytes(pr.X), O.g1_to_bytes(pr.Q), pr.T3), pr.pts_digest)
-            if c != pr.c:
+            c = fs_hash(KS_CONTEXT, (O.g1_to_bytes(pr.X), O.g1_to_bytes(pr.Q), pr.T3), pr.pts_digest)
+            if c != pr.c or pr.wellformed is False or pr.zb >= O.R:
                 continue
             try:
                 T3 = O.g1_from_bytes(pr.T3)

@@ -266,3 +266,111 @@ def test_packed_payloads_round_trip():
     with pytest.raises(ValueError):
         sigma.ObfuscationProof.unpack(ob.pack()[:-1])
 
+
+
+def _add_p_to_x(t, row: int):
+    """Row ``row`` of a packed Jacobian tensor with its X limbs replaced by
+    X + p: the same field element, non-canonical limbs."""
+    import numpy as np
+    import torch
+
+    lim = t[row, :8].numpy().reshape(1, 8)
+    x = bn.limbs_to_ints(lim)[0] + O.P
+    assert x < 2 ** 256
+    t[row, :8] = torch.from_numpy(np.asarray(bn.ints_to_limbs([x]), dtype=np.uint32).view(np.int32).reshape(8))
+
+
+def _ks_proofs(n_vals=3):
+    xs = [O.random_scalar() for _ in range(2)]
+    X = [O.g1_mul(x, O.G1_GEN) for x in xs]
+    cv, _ = eg.encrypt_ints(eg.pk_table(eg.aggregate_keys(X)), list(range(n_vals)))
+    q = eg.KeyPair.generate()
+    _, pend = sigma.key_switch_shares_batch(xs, X, cv.K, q.public, True)
+    return sigma.finish_keyswitch_proofs(pend)
+
+
+def test_packed_keyswitch_rejects_non_canonical_and_off_curve_rows():
+    """every point row and response scalar of a received
+    packed key-switch payload is checked (canonical limbs, on the curve).  A
+    non-canonical X limb encodes the same point, so the Fiat-Shamir challenge
+    and the equations would still hold: only the well-formedness check
+    rejects it."""
+    prs = _ks_proofs()
+    good = [sigma.KeySwitchProof.unpack(pr.pack()) for pr in prs]
+    assert sigma.key_switch_batch_verification(good) == [True, True]
+    for field in ("T1", "share.K", "K"):
+        prs = _ks_proofs()
+        back = [sigma.KeySwitchProof.unpack(pr.pack()) for pr in prs]
+        tgt = back[1].share.K if field == "share.K" else getattr(back[1], field)
+        tgt = tgt.clone()
+        _add_p_to_x(tgt, 0)
+        if field == "share.K":
+            back[1].share = eg.CipherVector(tgt, back[1].share.C)
+        else:
+            setattr(back[1], field, tgt)
+        back[1].wellformed = sigma._points_ok([back[1].K, back[1].share.K, back[1].share.C, back[1].T1, back[1].T2])
+        assert sigma.key_switch_batch_verification(back) == [True, False], field
+    # off-curve row straight in the packed payload
+    prs = _ks_proofs()
+    t = prs[0].pack().clone()
+    n = prs[0].K.shape[0]
+    off = sigma._KS_HEAD + 3 * 24 * n  # T1 row 0
+    t[off: off + 24] = bn.g1_jac_tensor([(1, 1)]).reshape(-1)  # y^2 = 1 != x^3 + 3
+    bad = sigma.KeySwitchProof.unpack(t)
+    assert not bool(bad.wellformed)
+    assert sigma.key_switch_batch_verification([bad]) == [False]
+    assert not sigma.key_switch_list_proof_verification(sigma.KeySwitchProof.unpack(t))
+    # non-canonical response scalar za (za + r)
+    t = prs[0].pack().clone()
+    zo = sigma._KS_HEAD + 5 * 24 * n
+    import numpy as np
+    import torch
+
+    z0 = bn.limbs_to_ints(t[zo: zo + 8].numpy().reshape(1, 8))[0] + O.R
+    t[zo: zo + 8] = torch.from_numpy(np.asarray(bn.ints_to_limbs([z0]), dtype=np.uint32).view(np.int32).reshape(8))
+    assert sigma.key_switch_batch_verification([sigma.KeySwitchProof.unpack(t)]) == [False]
+
+
+def test_packed_keyswitch_rejects_non_canonical_zb_and_c():
+    import numpy as np
+    import pytest
+    import torch
+
+    pr = _ks_proofs()[0]
+    t = pr.pack().clone()
+    for pos, v in ((58, pr.zb + O.R), (50, pr.c + O.R)):  # header words of zb and c
+        b = t.clone()
+        b[pos: pos + 8] = torch.from_numpy(np.asarray(bn.ints_to_limbs([v]), dtype=np.uint32).view(np.int32).reshape(8))
+        with pytest.raises(ValueError):
+            sigma.KeySwitchProof.unpack(b)
+
+
+def test_packed_obfuscation_rejects_non_canonical_rows():
+    kp, pk, a = _cv([1, 2, 3])
+    s = bn.random_scalars(3)
+    ob = sigma.obfuscation_list_proof_creation(a, a.mul_scalars(s), s)
+    t = ob.pack().clone()
+    assert sigma.obfuscation_batch_verification([sigma.ObfuscationProof.unpack(t)]) == [True]
+    rows = t[sigma._OBF_HEAD: sigma._OBF_HEAD + 24 * 3].view(3, 24).clone()  # C.K
+    _add_p_to_x(rows, 1)
+    t[sigma._OBF_HEAD: sigma._OBF_HEAD + 24 * 3] = rows.reshape(-1)
+    bad = sigma.ObfuscationProof.unpack(t)
+    assert sigma.obfuscation_batch_verification([bad]) == [False]
+    assert not sigma.obfuscation_list_proof_verification(sigma.ObfuscationProof.unpack(t))
+
+
+def test_coins_bits_keep_exactly_the_requested_width():
+    """40-bit weights have bits 32-39 set (somewhere) and
+    nothing at or above bit 40."""
+    from drynx_amd.crypto.coins import Coins
+
+    r = Coins().bits(4096, "cpu", 40)
+    assert int((r[:, 2:] != 0).sum()) == 0
+    w1 = r[:, 1]
+    assert int((w1 & ~0xFF).abs().sum()) == 0 and int((w1 != 0).sum()) > 4000
+    r64 = Coins().bits(64, "cpu", 64)
+    assert int((r64[:, 2:] != 0).sum()) == 0 and int((r64[:, 1] != 0).sum()) > 60
+    from drynx_amd.proofs import range_proof as rp
+
+    g = rp._rand64(4096, "cpu", 40)
+    assert int((g[:, 2:] != 0).sum()) == 0 and int((g[:, 1] & ~0xFF).abs().sum()) == 0 and int((g[:, 1] != 0).sum()) > 4000
