@@ -83,6 +83,67 @@ class NetEmulator:
         return t
 
 
+# ---------------------------------------------------------------- reference flows
+# Sequential one-way messages ("hops") on the critical path of each step of a
+# reference query, read off the reference sources; every step's messages are
+# charged with these counts (the simulation's Delay per hop).  Transport
+# overhead that the reference sources do not show (onet's websocket setup per
+# client call, tree propagation to nodes that do not know a protocol's tree)
+# is NOT in these counts: ``DRYNX_NETEM_SETUP_HOPS`` adds that many hops per
+# client call and per new protocol tree when set (default 0).
+def setup_hops() -> int:
+    return int(os.environ.get("DRYNX_NETEM_SETUP_HOPS", "0"))
+
+
+def flow_hops(step: str, n_cns: int = 3, n_vns: int = 3, cns_with_dps: int = 1, genesis: bool = False) -> int:
+    """Hops of one reference step (the table below cites the reference flow
+    of each); ``n_*`` size the CN / VN trees."""
+    d_cn, d_vn = tree_depth(n_cns), tree_depth(n_vns)
+    st = setup_hops()
+    table = {
+        # simul client -> every VN, one request/reply after the other
+        # (api_skipchain.go SendSurveyQueryToVNs loop; drynx_simul.go:382-393)
+        "query_vns": n_vns * (2 + st),
+        # client -> root CN request (api.go SendSurveyQuery; the reply is "result")
+        "query_client": 1 + st,
+        # root CN -> CNs and DPs (service.go:319-339), DPs' DPqueryReceived
+        # back (service_data_provider.go), CNs' SyncDCP (service.go:367-378,
+        # sent by the other CNs on arrival, so it is there with the DP acks)
+        "query_dissemination": 2,
+        # DataCollection star announce + reply (data_collection_protocol.go),
+        # then DPdataFinished among the CNs (service.go:391-408): one more hop
+        # when several CNs collect from DPs and finish together
+        "data_collection": 2 + st + (1 if cns_with_dps > 1 else 0),
+        # unlynx collective aggregation / obfuscation / key switching: the
+        # binary CN tree down (announcement) and up (reply)
+        # (service.go:667-700 GenerateNaryTreeWithRoot(2, root))
+        "aggregation": 2 * d_cn + st,
+        "obfuscation": 2 * d_cn + st,
+        "key_switching": 2 * d_cn + st,
+        "dro": n_cns,
+        # root CN -> client reply
+        "result": 1,
+        # the last proofs (key switch) leave their CN when the key switching
+        # ends: prover -> VN (proof_collection_protocol.go:154-165)
+        "proofs_to_vns": 1 + st,
+        # non-root VN -> root VN BitmapCollectionMessage (:360-372)
+        "bitmaps": 1,
+        # cothority skipchain store: BFT-CoSi prepare + commit over the VN tree
+        # (down + up each) for the new block, the same for the previous block's
+        # forward link, then the block's propagation to the roster (announce +
+        # ack); the genesis has no forward link (service_skipchain.go:120-150)
+        "skipchain": 4 * max(1, d_vn) * (1 if genesis else 2) + 2,
+        # root VN -> client: the pending SendEndVerification reply (:158, :164-169)
+        "end_verification": 1,
+        # simul client -> every VN CloseDB, one after the other (api_skipchain.go SendCloseDB)
+        "close_db": n_vns * (2 + st),
+        # simul client -> a VN GetLatestBlock request/reply, and that VN's
+        # skipchain GetUpdateChain request/reply (service_skipchain.go:185-200)
+        "latest_block": 4 + 2 * st,
+    }
+    return table[step]
+
+
 def tree_depth(n: int) -> int:
     """Depth of onet's binary tree over n nodes (GenerateNaryTreeWithRoot(2, root))."""
     d, cap = 0, 1

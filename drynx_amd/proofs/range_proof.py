@@ -214,6 +214,23 @@ class SigMaterial:
         self._ptab[key] = mode
         return mode
 
+    def _host_tables_pay(self, n_points: int, n_items: int | None) -> bool:
+        """Host cost model: a comb table costs thousands of G2 / GT additions
+        per distinct point (an 8-bit comb: 8192 entries), while proving one
+        item without it costs one variable-base G2 multiplication and one
+        pairing -- ~64 items per distinct point before the table breaks even.
+        Tables are built once the set's cumulative items per distinct point
+        reach that (``DRYNX_HOST_TABLE_MIN_USES``): a one-shot CPU query (the
+        simulation, BASELINE config 1) proves without them; a set reused
+        query after query gets them.  A forced ``DRYNX_PROVER_TABLE_BITS``
+        bypasses the model."""
+        if os.environ.get("DRYNX_PROVER_TABLE_BITS") is not None or getattr(self, "_host_ok", False):
+            return True  # forced, or the tables are (being) built: using them is free
+        self._host_items = getattr(self, "_host_items", 0) + int(n_items if n_items is not None else n_points)
+        need = int(os.environ.get("DRYNX_HOST_TABLE_MIN_USES", "64"))
+        self._host_ok = self._host_items >= need * max(1, self.n_distinct)
+        return self._host_ok
+
     def table_bytes(self) -> int:
         """HBM held by this set's prover and verifier (c * y_i) tables."""
         tot = 0
@@ -255,12 +272,16 @@ class SigMaterial:
             self._ptab[key] = (g2, gt, slot.to(dev))
         return self._ptab[key]
 
-    def prover_tables(self, a_idx: torch.Tensor, device):
+    def prover_tables(self, a_idx: torch.Tensor, device, n_items: int | None = None):
         """Comb tables (G2 for V = v*A, GT for e(B, A)) of the distinct signature
         points used by a proof batch, cached for the lifetime of the signature
         set.  Returns (g2_tables, gt_tables, slot[a_idx-position], wbits) or
-        None when no table layout fits the memory budget (``table_mode``)."""
+        None when no table layout fits the memory budget (``table_mode``) or,
+        on the host, while the set has not yet been used enough to repay the
+        build (``_host_tables_pay``)."""
         dev = torch.device(device)
+        if dev.type == "cpu" and not self._host_tables_pay(a_idx.numel(), n_items):
+            return None
         mode = self.table_mode(dev)
         if mode == 0:
             return None
@@ -622,7 +643,7 @@ def _prove_group(u, l, vals, offs, cols, r, cv, sigmat, P_point, device, mode=0,
                + phi_t.view(n, 1, l)).reshape(-1)
     _, gt_tab = gt_generator_table(device)
     uniq, inv = torch.unique(a_index, return_inverse=True)
-    tabs = sigmat.prover_tables(uniq, device)
+    tabs = sigmat.prover_tables(uniq, device, n_items=a_index.numel())
     if tabs is not None:
         # table-driven prover: V = v * A_phi (G2 comb), a = e(B,A_phi)^{-s v} * gT^t (GT combs) --
         # no pairing and no final exponentiation per (value, server, digit)

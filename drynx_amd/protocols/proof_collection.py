@@ -23,7 +23,7 @@ import time
 import torch
 
 from ..ledger import skipchain as skc
-from ..parallel.netem import CT_BYTES, POINT_BYTES, SCALAR_BYTES, SIG_BYTES, range_proof_bytes
+from ..parallel.netem import CT_BYTES, POINT_BYTES, SCALAR_BYTES, SIG_BYTES, flow_hops, range_proof_bytes
 from .data_collection import all_possible_groups as dcp_groups
 from ..parallel.comm import bytes_to_obj, obj_to_bytes
 from ..crypto.coins import Coins
@@ -61,7 +61,8 @@ def _net_proofs(ctx, sq, reqs: list, vns: list):
         else:
             nb = int(sq.Query.DiffP.NoiseListSize) * 3 * CT_BYTES
         sizes[r.base_key()] = (r.sender_id, nb + SIG_BYTES)
-    ctx.net.step("proofs_to_vns", [(src, v.id, nb) for src, nb in sizes.values() for v in vns], hops=1)
+    ctx.net.step("proofs_to_vns", [(src, v.id, nb) for src, nb in sizes.values() for v in vns],
+                 hops=flow_hops("proofs_to_vns"))
 
 
 def use_pool(ctx) -> bool:
@@ -434,9 +435,10 @@ def proof_collection(ctx, sq, local_requests: list, early: dict | None = None):
     if getattr(ctx, "net", None) is not None:
         ids = [v.id for v in vns]
         bsz = len(block.to_bytes())
-        ctx.net.step("bitmaps", [(i, ids[0], 64 * len(allbm.get(i, {})) + 64) for i in ids[1:]], hops=1)
+        ctx.net.step("bitmaps", [(i, ids[0], 64 * len(allbm.get(i, {})) + 64) for i in ids[1:]],
+                     hops=flow_hops("bitmaps"))
         ctx.net.step("skipchain", [(ids[0], i, bsz) for i in ids[1:]] + [(i, ids[0], SIG_BYTES) for i in ids[1:]],
-                     hops=2)
-        ctx.net.step("end_verification", [(ids[0], "client", bsz)], hops=1)
+                     hops=flow_hops("skipchain", n_vns=len(ids), genesis=block.Index == 0))
+        ctx.net.step("end_verification", [(ids[0], "client", bsz)], hops=flow_hops("end_verification"))
     ctx.end_verification(sq.SurveyID, block)  # EndVerificationChannel <- block (service_skipchain.go:158)
     return block

@@ -31,7 +31,7 @@ from ..ops.encoding import cat_proof_batches as dcp_batch_cat
 from ..ledger.store import Store
 from ..parallel.comm import Comm, LocalComm
 from ..parallel.ec_collectives import KeyIndex
-from ..parallel.netem import CT_BYTES, POINT_BYTES, tree_depth, tree_edges
+from ..parallel.netem import CT_BYTES, POINT_BYTES, flow_hops, tree_edges
 from ..parallel.topology import Cluster
 from ..proofs import range_proof as rp
 from ..proofs import requests as prq
@@ -249,7 +249,7 @@ class DrynxNode:
         if self.net is not None and noise is not None:
             cns = [si.id for si in sq.RosterServers.list]
             nb = int(sq.Query.DiffP.NoiseListSize) * 3 * CT_BYTES
-            self.net.step("dro", [(a, b, nb) for a, b in zip(cns, cns[1:] + cns[:1])], hops=len(cns))
+            self.net.step("dro", [(a, b, nb) for a, b in zip(cns, cns[1:] + cns[:1])], hops=flow_hops("dro", len(cns)))
         cn_sums, cn_inputs, dp_results = dcp.data_collection(self, sq)
         # range proofs start right after encoding (the reference fires them
         # asynchronously, data_collection_protocol.go:278-348): proving is queued
@@ -273,25 +273,27 @@ class DrynxNode:
         n_rows = n_groups * n_out
         net = self.net
         cn_ids = [si.id for si in sq.RosterServers.list]
+        nc = len(cn_ids)
         if net is not None:
+            with_dps = sum(1 for dps in (sq.ServerToDP or {}).values() if dps)
             net.step("data_collection", [(si.id, cn, n_rows * CT_BYTES) for cn, dps in (sq.ServerToDP or {}).items()
-                                         for si in (dps or [])], hops=2)
+                                         for si in (dps or [])], hops=flow_hops("data_collection", nc, cns_with_dps=with_dps))
         agg = cnp.collective_aggregation(self, sq, cn_sums, cn_inputs, n_rows, proofs)
         if net is not None:
             net.step("aggregation", [(c, p, n_rows * CT_BYTES) for c, p in tree_edges(cn_ids)],
-                     hops=2 * tree_depth(len(cn_ids)))
+                     hops=flow_hops("aggregation", nc))
         if q.Obfuscation:
             agg = cnp.obfuscation(self, sq, agg, n_rows, proofs)
             if net is not None:
                 e = tree_edges(cn_ids)
                 net.step("obfuscation", [(p, c, n_rows * CT_BYTES) for c, p in e] +
-                         [(c, p, n_rows * CT_BYTES) for c, p in e], hops=2 * tree_depth(len(cn_ids)))
+                         [(c, p, n_rows * CT_BYTES) for c, p in e], hops=flow_hops("obfuscation", nc))
         result = cnp.key_switching(self, sq, agg, n_groups, n_out, noise, proofs)
         if net is not None:
             e = tree_edges(cn_ids)
             net.step("key_switching", [(p, c, n_rows * POINT_BYTES) for c, p in e] +
-                     [(c, p, n_rows * CT_BYTES) for c, p in e], hops=2 * tree_depth(len(cn_ids)))
-            net.step("result", [(cn_ids[0], "client", n_rows * CT_BYTES)], hops=1)
+                     [(c, p, n_rows * CT_BYTES) for c, p in e], hops=flow_hops("key_switching", nc))
+            net.step("result", [(cn_ids[0], "client", n_rows * CT_BYTES)], hops=flow_hops("result"))
         if q.CuttingFactor and result is not None:
             # CN truncates the replicated response (service.go:760-761)
             per = n_out // q.CuttingFactor
@@ -319,15 +321,16 @@ class DrynxNode:
         return out
 
     def _net_dissemination(self, sq):
-        """Client -> root CN -> other CNs -> DPs (service.go:263-339): three
-        sequential hops carrying the query and its input-validation keys."""
+        """Client -> root CN, then root CN -> other CNs and its DPs with the
+        DPs' acknowledgements (service.go:263-378), carrying the query and its
+        input-validation keys (hops: ``netem.flow_hops``)."""
         sigs = sq.Query.IVSigs.InputValidationSigs or []
         size = 1024 + sum(len(x.Public) + len(x.Signature) for row in sigs for x in row)
         cns = [si.id for si in sq.RosterServers.list]
-        self.net.step("query_client", [("client", cns[0], size)], hops=1)
-        self.net.step("query_cns", [(cns[0], c, size) for c in cns[1:]], hops=1)
-        self.net.step("query_dps", [(cn, si.id, size) for cn, dps in (sq.ServerToDP or {}).items()
-                                    for si in (dps or [])], hops=1)
+        self.net.step("query_client", [("client", cns[0], size)], hops=flow_hops("query_client"))
+        self.net.step("query_dissemination", [(cns[0], c, size) for c in cns[1:]] +
+                      [(cn, si.id, size) for cn, dps in (sq.ServerToDP or {}).items() for si in (dps or [])],
+                      hops=flow_hops("query_dissemination", len(cns)))
 
     def defer_proofs(self, fn, *args):
         """Run ``fn(*args) -> [ProofRequest]`` (proof finishing: transcript

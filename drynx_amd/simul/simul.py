@@ -20,6 +20,7 @@ import sys
 import tempfile
 
 from ..parallel.comm import init_distributed, make_comm
+from ..parallel.netem import flow_hops
 from ..query import QueryDiffP, LogisticRegressionParameters
 from ..services.api import DrynxClient
 from ..services.local import local_cluster, make_survey
@@ -138,8 +139,18 @@ def run_row(glob: dict, row: dict, comm, device, workdir, netem: str = "sleep"):
             rest = ids[n_cn * per:]
             if rest:
                 sq.ServerToDP[cl.cns[0].id] += rest
+            net = node.net
+            vn_ids = [v.id for v in cl.vns]
+            if net is not None and proofs:
+                # the simulation client hands the query to every VN first (drynx_simul.go:382-393)
+                net.step("query_vns", [("client", v, 4096) for v in vn_ids], hops=flow_hops("query_vns", n_vns=n_vn))
             _, vals, res = client.send_survey_query(sq)
             results.append(vals[0])
+            if net is not None and proofs:
+                # CloseDB at every VN, then GetLatestBlock (drynx_simul.go:427-446)
+                net.step("close_db", [("client", v, 64) for v in vn_ids], hops=flow_hops("close_db", n_vns=n_vn))
+                net.step("latest_block", [("client", vn_ids[0], 1024), (vn_ids[0], "client", 4096)],
+                         hops=flow_hops("latest_block"))
         else:
             node.run_survey(None)
         timers.end_timer(t)
@@ -165,6 +176,7 @@ def main(argv=None):
         with tempfile.TemporaryDirectory() as wd:
             res = run_row(glob, row, comm, comm.device, wd, a.netem)
         summ = timers.summary()
+        timers.dump_trace()  # DRYNX_TRACE=<path>: host span trace of the runs
         if comm.rank == 0:
             net = summ.get("NetworkEmulated", {}).get("sum", 0.0) / max(1, int(glob.get("Rounds", 1)))
             log.info(f"row {i}: {row.get('OperationName')} -> {res[-1] if res else None} "
