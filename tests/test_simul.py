@@ -55,17 +55,19 @@ def test_simulation_applies_runfile_links(tmp_path):
 
 def test_reference_flow_hops(monkeypatch):
     """The per-step hop counts of the network model, read off the reference
-    flows (netem.flow_hops): 36 one-way delays for the sum query of the
-    Bandwith sheet (3 CNs, 3 VNs, depth-1 trees, one CN hosting DPs, an
-    appended block); the transport-setup knob adds hops per client call /
+    flows (netem.flow_hops): 35 one-way delays for the sum query of the
+    Bandwith sheet (3 CNs, 3 VNs, depth-1 trees, one CN hosting DPs, a
+    genesis block as in a one-round simulation; an appended block adds the
+    forward link's 4); the transport-setup knob adds hops per client call /
     new protocol tree."""
     from drynx_amd.parallel.netem import flow_hops
 
     monkeypatch.delenv("DRYNX_NETEM_SETUP_HOPS", raising=False)
     steps = ["query_vns", "query_client", "query_dissemination", "data_collection", "aggregation", "key_switching",
              "result", "proofs_to_vns", "bitmaps", "skipchain", "end_verification", "close_db", "latest_block"]
-    assert sum(flow_hops(s) for s in steps) == 36
-    assert flow_hops("skipchain", genesis=True) == 6 and flow_hops("aggregation", n_cns=7) == 4
+    assert sum(flow_hops(s) for s in steps) - flow_hops("skipchain") + flow_hops("skipchain", genesis=True) == 35
+    assert flow_hops("skipchain", genesis=True) == 6 and flow_hops("skipchain") == 10
+    assert flow_hops("aggregation", n_cns=7) == 4
     assert flow_hops("data_collection", cns_with_dps=3) == 3
     monkeypatch.setenv("DRYNX_NETEM_SETUP_HOPS", "4")
-    assert sum(flow_hops(s) for s in steps) == 36 + 52
+    assert sum(flow_hops(s) for s in steps) == 39 + 52
