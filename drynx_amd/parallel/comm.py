@@ -67,6 +67,12 @@ class Comm:
     def recv(self, numel: int, src: int) -> torch.Tensor:
         raise RuntimeError("single-process comm has no peers")
 
+    def broadcast_into(self, t: torch.Tensor, src: int):
+        """Fill contiguous ``t`` on every rank with ``src``'s content, in place
+        (sharded setup: each rank builds a slice of a large table, then every
+        slice is broadcast into the same view of the full table)."""
+        return t
+
     def exchange_bytes(self, outgoing: dict) -> dict:
         """Like exchange but for python bytes payloads (proof blobs)."""
         tens = {d: _bytes_to_i32(b, self.device) for d, b in outgoing.items()}
@@ -166,6 +172,31 @@ class DistComm(Comm):
                 out[s] = buf[off: off + recv[s]]
             off += recv[s]
         return out
+
+    _BCAST_CHUNK = 1 << 28  # elements per collective (1 GiB of int32)
+
+    def broadcast_into(self, t: torch.Tensor, src: int):
+        """``Comm.broadcast_into`` over the data plane: RCCL broadcasts straight
+        into the HBM view (chunked to 1 GiB per call, no staging copy, no
+        gathered temporary); gloo stages each chunk through host memory."""
+        assert t.is_contiguous()
+        flat = t.view(-1)
+        n = flat.numel()
+        for a in range(0, n, self._BCAST_CHUNK):
+            part = flat[a: a + self._BCAST_CHUNK]
+            if part.device == self._stage:
+                dist.broadcast(part, src)
+            else:
+                st = part.to(self._stage) if self.rank == src else torch.empty(part.shape, dtype=part.dtype,
+                                                                                 device=self._stage)
+                dist.broadcast(st, src)
+                if self.rank != src:
+                    part.copy_(st)
+            if self.rank == src:
+                self.bytes_sent += part.numel() * part.element_size()
+            else:
+                self.bytes_recv += part.numel() * part.element_size()
+        return t
 
     def send(self, t: torch.Tensor, dst: int):
         t = t.contiguous().to(self._stage)

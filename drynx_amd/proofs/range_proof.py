@@ -164,6 +164,19 @@ class SigMaterial:
             self._ytab[key] = (nt.g1_fb_table(aff), torch.tensor(self.y_slot, dtype=torch.int32, device=device))
         return self._ytab[key]
 
+    def attach_shard(self, comm, every_rank_proves: bool):
+        """Build the GLS / 4-bit prover tables sharded over ``comm``'s ranks:
+        rank k computes points [k n / W, (k+1) n / W) and every slice is then
+        broadcast over the data plane (RCCL over xGMI) into each rank's full
+        table, instead of every rank computing all of it.  Collective: only
+        when EVERY rank proves (each calls the table build in the same query
+        at the same point of its schedule); the layout choice is agreed on
+        first (``table_mode``)."""
+        if comm is not None and getattr(comm, "world", 1) > 1 and every_rank_proves:
+            self._shard = comm
+        else:
+            self._shard = None
+
     def table_mode(self, device) -> int:
         """Prover comb-table layout for this signature set on ``device``:
         8 (8-bit combs, 4 MiB per distinct point: few distinct points, e.g.
@@ -211,6 +224,11 @@ class SigMaterial:
             mode = 4
         else:
             mode = 0
+        shard = getattr(self, "_shard", None)
+        if shard is not None and forced is None:
+            # sharded builds need ONE layout on every rank: the most compact one any rank chose
+            order = [8, 7, 6, 4, 0]
+            mode = max(shard.all_gather_object(mode), key=order.index)
         self._ptab[key] = mode
         return mode
 
@@ -228,8 +246,12 @@ class SigMaterial:
             return True  # forced, or the tables are (being) built: using them is free
         self._host_items = getattr(self, "_host_items", 0) + int(n_items if n_items is not None else n_points)
         need = int(os.environ.get("DRYNX_HOST_TABLE_MIN_USES", "64"))
-        self._host_ok = self._host_items >= need * max(1, self.n_distinct)
-        return self._host_ok
+        ok = self._host_items >= need * max(1, self.n_distinct)
+        shard = getattr(self, "_shard", None)
+        if shard is not None:  # a sharded build is collective: every rank decides the same
+            ok = any(shard.all_gather_object(ok))
+        self._host_ok = ok
+        return ok
 
     def table_bytes(self) -> int:
         """HBM held by this set's prover and verifier (c * y_i) tables."""
@@ -262,13 +284,24 @@ class SigMaterial:
             gt = torch.empty((n * E, 96), dtype=torch.int32, device=dev)
             A = self.A.to(dev)
             step = 8192
+            shard = getattr(self, "_shard", None)
+            W, k = (shard.world, shard.rank) if shard is not None else (1, 0)
+            per = -(-n // W)
+            bounds = [(min(n, r * per), min(n, (r + 1) * per)) for r in range(W)]
+            lo, hi = bounds[k]
             with timers.span("rp.prove.tables4"):
-                for a in range(0, n, step):
-                    b = min(n, a + step)
+                for a in range(lo, hi, step):
+                    b = min(hi, a + step)
                     pts = A.index_select(0, uniq[a:b].to(dev)).contiguous()
                     g2_tab(pts, out=g2[a * E: b * E])
                     gphi = nt.pairing(bn.g1_generator_aff(dev).expand(b - a, 16).contiguous(), pts)
                     gt_tab(gphi, out=gt[a * E: b * E])
+            if shard is not None:
+                with timers.span("rp.prove.tables4.share"):
+                    for r, (a, b) in enumerate(bounds):
+                        if b > a:
+                            shard.broadcast_into(g2[a * E: b * E], r)
+                            shard.broadcast_into(gt[a * E: b * E], r)
             self._ptab[key] = (g2, gt, slot.to(dev))
         return self._ptab[key]
 

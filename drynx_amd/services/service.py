@@ -465,6 +465,9 @@ class DrynxNode:
                                                     res["cv"]))
         if batches:
             sigmat = self.verifier_cache.sigmat(sq, self.device)
+            if not hasattr(sigmat, "_shard"):
+                # every rank hosts DPs: the prover tables are built 1/W per rank and shared
+                sigmat.attach_shard(self.comm, all(self.cluster.local(r, "dp") for r in range(self.comm.world)))
             big = dcp_batch_cat(batches)
             lists = rp.create_range_proofs(big, sigmat, P, self.device, sq.RangeProofMode)  # one list per (u, l)
             # every DP's items of a given (u, l) are contiguous inside that list
