@@ -1,0 +1,181 @@
+"""One rank's share of the W-rank headline schedule, measured on ONE GPU.
+
+bench.py at --gpus 8 places CNs on ranks 0-2, VNs on ranks 3-5 and the 10 DPs
+round robin from rank 6 (ranks 6 and 7 host two DPs each); every VN's range
+checks are pooled, rank k checking slice k/W of every list for every VN
+(protocols/proof_collection.py).  This tool runs one real d = 44 query on one
+GPU (the bench's configuration), captures its DPs' encoded results and the
+signed range-proof inbox, and then times, alone and synchronised (median of
+``--reps``):
+
+* prove(k): range proofs + signed envelopes of exactly rank k's DPs;
+* pool(k): rank k's pooled share for all three VNs -- on a helper rank from
+  the slice payloads it would receive (unpack included), on a VN rank from
+  the full signed payloads (decode of the whole inbox included);
+* digests(k): a VN rank's recomputation of the other ranks' slice digests;
+* serial: the query's non-range critical path (CN phases, querier, per-CN
+  proofs, block), taken from a ``--u 0 --l 0`` bench JSON (``--serial-json``).
+
+The projection per rank is max(serial on rank 0, prove + pool [+ digests])
+plus the measured fan-out time; the step is the max over ranks.  Peers'
+traffic over xGMI and waits on peers are not in it (the 8-GPU run measures
+those).  Usage: python tools/rank_share.py [--world 8] [--reps 5] [--serial-json f]
+"""
+from __future__ import annotations
+
+import argparse
+import copy
+import json
+import os
+import statistics
+import sys
+import tempfile
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from drynx_amd.crypto.coins import Coins  # noqa: E402
+from drynx_amd.protocols import proof_collection as pcp  # noqa: E402
+from drynx_amd.proofs import requests as prq  # noqa: E402
+from drynx_amd.query import LogisticRegressionParameters, new_survey_id  # noqa: E402
+from drynx_amd.services.api import DrynxClient  # noqa: E402
+from drynx_amd.services.local import local_cluster, make_survey  # noqa: E402
+from drynx_amd.services.service import DrynxNode  # noqa: E402
+
+
+def _sync():
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+
+
+def timed(fn, reps):
+    fn()
+    ts = []
+    for _ in range(reps):
+        _sync()
+        t = time.perf_counter()
+        fn()
+        _sync()
+        ts.append(1e3 * (time.perf_counter() - t))
+    return round(statistics.median(ts), 2)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--world", type=int, default=8)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--features", type=int, default=44)
+    ap.add_argument("--records", type=int, default=1_000_000)
+    ap.add_argument("--serial-json", default=None, help="bench.py --u 0 --l 0 JSON (the non-range critical path)")
+    ap.add_argument("--json-out", default=None)
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
+    if dev.type == "cuda":
+        torch.cuda.set_device(dev)
+    W, n_cns, n_vns, n_dps, d = a.world, 3, 3, 10, a.features
+    cl, node = local_cluster(n_cns, n_dps, n_vns, device=dev, workdir=tempfile.mkdtemp(prefix="drynx_share_"))
+    rec = max(1, a.records // n_dps)
+    g = torch.Generator(device=dev).manual_seed(1234)
+    node.dp_data = {}
+    for dp in cl.dps:
+        X = torch.randint(0, 4, (rec, d), generator=g, device=dev).to(torch.float64)
+        X += torch.rand((rec, d), generator=g, device=dev, dtype=torch.float64)
+        node.dp_data[dp.id] = (X, torch.randint(0, 2, (rec,), generator=g, device=dev))
+    lp = LogisticRegressionParameters(NbrRecords=rec * n_dps, NbrFeatures=d, Means=[2.0] * d,
+                                      StandardDeviations=[1.15] * d, Lambda=1.0, Step=0.012, MaxIterations=450,
+                                      InitialWeights=[0.1] * (d + 1), K=2, PrecisionApproxCoefficients=100.0)
+    client = DrynxClient(node, device=dev)
+    sq0 = make_survey(client, cl, "logistic regression", proofs=1, ranges=[16, 16, 1 << 62], lr_params=lp,
+                      thresholds=[1.0, 1.0, 1.0, 0.0, 1.0], sig_device=dev)
+    cap = {}
+    orig_async, orig_plane = DrynxNode._range_proofs_async, pcp.start_range_plane
+
+    def cap_async(self, sq, dp_results):
+        cap["dp_results"], cap["sq"] = dp_results, sq
+        return orig_async(self, sq, dp_results)
+
+    def cap_plane(ctx, sq, reqs):
+        cap["reqs"] = list(reqs)
+        return orig_plane(ctx, sq, reqs)
+
+    DrynxNode._range_proofs_async, pcp.start_range_plane = cap_async, cap_plane
+    for _ in range(2):  # the first query builds the prover tables
+        sq = copy.copy(sq0)
+        sq.SurveyID = new_survey_id()
+        client.send_survey_query(sq)
+    DrynxNode._range_proofs_async, pcp.start_range_plane = orig_async, orig_plane
+    sq, reqs, dp_results = cap["sq"], cap["reqs"], cap["dp_results"]
+    rng = [i for i, r in enumerate(reqs) if r.kind == "range"]
+    vn_idxs = {vn.id: rng for vn in cl.vns}
+    cache = node.verifier_cache
+    # the bench's placement at world W
+    place = {}
+    for i, c in enumerate(cl.cns):
+        place.setdefault(i % W, []).append(c.id)
+    for i, v in enumerate(cl.vns):
+        place.setdefault((n_cns + i) % W, []).append(v.id)
+    dps_of = {k: [dp.id for i, dp in enumerate(cl.dps) if (n_cns + n_vns + i) % W == k] for k in range(W)}
+    vn_ranks = {(n_cns + i) % W for i in range(n_vns)}
+
+    def helper_reqs(part):
+        out = []
+        for i in rng:
+            r = reqs[i]
+            sl = prq.slice_lists(prq._range_lists(r, dev), sq, part)
+            c = copy.copy(r)
+            c._data, c.decoded, c.slice_of = None, None, tuple(part)
+            c.tensor = prq.range_bundle_pack(sl).to(dev)
+            out.append(c)
+        return out
+
+    def full_reqs():
+        out = []
+        for i in rng:
+            c = copy.copy(reqs[i])
+            c.decoded = None  # a VN rank decodes its signed payloads itself
+            out.append(c)
+        return out
+
+    res = {"world": W, "features": d, "placement": {k: {"parties": place.get(k, []), "dps": dps_of[k]} for k in range(W)},
+           "ranks": {}}
+    for k in range(W):
+        part = (k, W)
+        coins = {vn.id: Coins() for vn in cl.vns}
+        is_vn = k in vn_ranks
+        if is_vn:
+            t_pool = timed(lambda: prq.verify_range_pool_part(full_reqs(), {v: list(range(len(rng))) for v in vn_idxs},
+                                                              sq, dev, cache, part, coins), a.reps)
+        else:
+            t_pool = timed(lambda: prq.verify_range_pool_part(helper_reqs(part), {v: list(range(len(rng)))
+                                                                                  for v in vn_idxs},
+                                                              sq, dev, cache, part, coins), a.reps)
+        t_dig = 0.0
+        if is_vn:
+            full = [prq._range_lists(reqs[i], dev) for i in rng]
+            t_dig = timed(lambda: prq.lists_digests([prq.slice_lists(ls, sq, (j, W)) for ls in full
+                                                     for j in range(W) if j != k]), a.reps)
+        mine = {dp: dp_results[dp] for dp in dps_of[k]}
+        t_prove = timed(lambda: node._sign_range(sq, node._prove_range(sq, mine)), a.reps) if mine else 0.0
+        res["ranks"][k] = {"prove_ms": t_prove, "pool_ms": t_pool, "vn_digest_ms": t_dig, "vn_rank": is_vn,
+                           "dps": len(mine)}
+        print(json.dumps({"rank": k, **res["ranks"][k]}), flush=True)
+    if a.serial_json:
+        s = json.load(open(a.serial_json))
+        res["serial_ms"] = s["ms_per_step"]
+        res["serial_source"] = a.serial_json
+    serial = res.get("serial_ms", 0.0)
+    proj = {}
+    for k, v in res["ranks"].items():
+        rng_path = v["prove_ms"] + v["pool_ms"] + v["vn_digest_ms"]
+        proj[k] = round(max(serial if k == 0 else 0.0, rng_path), 2)
+    res["projection_ms"] = proj
+    res["projection_step_ms"] = max(proj.values())
+    print(json.dumps({"projection_ms": proj, "step_ms": res["projection_step_ms"]}), flush=True)
+    if a.json_out:
+        json.dump(res, open(a.json_out, "w"), indent=1)
+    node.close(remove=True)
+
+
+if __name__ == "__main__":
+    main()
