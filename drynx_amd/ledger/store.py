@@ -53,6 +53,14 @@ class _Item:
         return self.job.result()[self.i]
 
 
+def _copies() -> int:
+    """DRYNX_LEDGER_COPIES=k (diagnostics): every blob is also written to k-1
+    extra files, reproducing on one rank the ledger write volume of k VN ranks
+    (on an 8-GPU node each of the 3 VN ranks persists its own copy of every
+    proof, proof_collection_protocol.go:307-406)."""
+    return max(1, int(os.environ.get("DRYNX_LEDGER_COPIES", "1")))
+
+
 class BlobSegment:
     """Append-only file of large ledger values shared by the VNs of one rank:
     the same proof payload is written once, however many co-hosted VNs store
@@ -125,11 +133,15 @@ class BlobSegment:
                 pos += b.nbytes
             self._pwrite_all(bufs, off)
             self._f.seek(0, os.SEEK_END)
+            for j in range(1, _copies()):
+                # diagnostics: the write volume of several VN ranks, each
+                # persisting its own copy (DRYNX_LEDGER_COPIES, see _copies)
+                self._pwrite_all(bufs, off, f"{self.path}.copy{j}")
         return out if many else out[0]
 
     _PIECE = 32 << 20  # bytes per parallel write
 
-    def _pwrite_all(self, bufs: list, off: int):
+    def _pwrite_all(self, bufs: list, off: int, path: str | None = None):
         """The buffers back to back from ``off``, in pieces written by several
         threads with positioned writes (they release the GIL; one sequential
         write of a query's ~540 MB of range proofs took ~50 ms)."""
@@ -138,11 +150,13 @@ class BlobSegment:
             for a in range(0, b.nbytes, self._PIECE):
                 pieces.append((b[a: a + self._PIECE], pos + a))
             pos += b.nbytes
-        if not hasattr(self, "_pfd"):
+        fds = self.__dict__.setdefault("_pfds", {})
+        path = path or self.path
+        if path not in fds:
             # positioned writes need a descriptor WITHOUT O_APPEND (Linux
             # appends every pwrite on an O_APPEND descriptor, ignoring the offset)
-            self._pfd = os.open(self.path, os.O_WRONLY | os.O_CREAT, 0o644)
-        fd = self._pfd
+            fds[path] = os.open(path, os.O_WRONLY | os.O_CREAT, 0o644)
+        fd = fds[path]
 
         def put(item):
             view, at = item
@@ -169,9 +183,10 @@ class BlobSegment:
     def close(self, remove: bool = False):
         self._ex.shutdown(wait=True)
         self._f.close()
-        if hasattr(self, "_pfd"):
-            os.close(self._pfd)
-            del self._pfd
+        for path, fd in self.__dict__.pop("_pfds", {}).items():
+            os.close(fd)
+            if remove and path != self.path:
+                os.remove(path)
         if remove:
             try:
                 os.remove(self.path)
