@@ -1433,36 +1433,103 @@ def multi_exp_plan(k: torch.Tensor, group, n_groups: int, W: int = _ME_W, c: int
 
 
 def multi_exp_grouped(a: torch.Tensor, k: torch.Tensor, group, n_groups: int, W: int = _ME_W, c: int = 8,
-                      plan: dict | None = None):
+                      plan: dict | None = None, fold: int = 1):
     """Launch G independent multi-exponentiations prod_{i: group_i = g} a[i % n]^k_i
     (n = rows of a, k [m, 8] with m a multiple of n, low W c-bit windows of
     each exponent; ``group`` an int32 tensor or an int stride) as ONE bucket
     plan (one host sync for all groups, e.g. the batch weights of several
     verifying nodes).  Returns a handle for ``multi_exp_grouped_finish``;
-    device passes are queued on the current stream."""
+    device passes are queued on the current stream.  ``fold`` = k: the
+    ``n_groups`` plan groups are (group, segment) pairs g * k + s; the handle
+    finishes the n_groups / k groups (buckets combined over the segments) and
+    keeps the per-segment buckets for ``multi_exp_seg_finish``."""
     n = a.shape[0]
     if plan is None:
         plan = _bucket_plan(k, W, group, n_groups, c)
     plan["item"] = (plan["item"] % n).contiguous()
     bk = plan["bk"]
-    h = {"G": n_groups, "W": W, "c": c, "win": None}
+    h = {"G": n_groups // fold, "W": W, "c": c, "win": None}
     if bk.size == 0:
         return h
     cur = a.index_select(0, plan["item"]).contiguous() if plan["single"] else None
     for i, (st, ln) in enumerate(plan["passes"]):
         cur = gt_slice_prod(a if i == 0 else cur, plan["item"] if i == 0 else None, st, ln)
-    bkp = gt_pow(cur, plan["digit_sc"])
+    if fold > 1:
+        # per-(group, segment) buckets are kept for ``multi_exp_seg_finish``;
+        # the groups' results come from the buckets multiplied across segments
+        h["seg"] = {"cur": cur, "bk": bk, "fold": fold}
+        cur, bk = _fold_buckets(cur, bk, W << c, fold, lambda src, idx, st, ln: gt_slice_prod(src, idx, st, ln))
+    _me_windows(h, cur, bk, n_groups // fold, W, c, a.device)
+    return h
+
+
+def _fold_buckets(cur, bk, per_group: int, fold: int, slice_op):
+    """Buckets of groups g * fold + s (keys bk, values cur) combined over s:
+    one segmented slice operation (product / sum) -> (values, keys) of the
+    groups g (host-side ordering of the bucket keys; the values never leave
+    the device)."""
+    t = (bk // per_group) // fold * per_group + bk % per_group
+    order = np.argsort(t, kind="stable")
+    ts = t[order]
+    first = np.flatnonzero(np.r_[True, ts[1:] != ts[:-1]])
+    lens = np.diff(np.r_[first, ts.size])
+    dev = cur.device
+    idx = _upload(order.astype(np.int64), dev)
+    out = slice_op(cur, idx, _upload(first.astype(np.int64), dev), _upload(lens.astype(np.int32), dev))
+    return out, ts[first]
+
+
+def _me_windows(h: dict, cur, bk, n_groups: int, W: int, c: int, dev):
+    """Bucket values -> B^d (GPU) scattered into per-(group, window) rows,
+    reduced on the device down to <= 32 rows each (``multi_exp_grouped_finish``
+    ends on the host)."""
+    digit_sc = torch.zeros((bk.size, 8), dtype=torch.int32)
+    digit_sc[:, 0] = torch.from_numpy((bk & ((1 << c) - 1)).astype("int32"))
+    bkp = gt_pow(cur, _upload(digit_sc.numpy(), dev))
     D = 1 << c
     g, w, d = bk // (W * D), (bk >> c) % W, bk & (D - 1)
-    slot = _upload(d * (n_groups * W) + g * W + w, a.device)
-    win = gt_one(a.device).repeat(D * n_groups * W, 1)
+    slot = _upload(d * (n_groups * W) + g * W + w, dev)
+    win = gt_one(dev).repeat(D * n_groups * W, 1)
     win[slot] = bkp
     win = win.view(D, n_groups * W, 96)
-    if a.is_cuda:  # 8-way device levels down to <= 32 rows per (group, window): the host finishes
+    if torch.device(dev).type == "cuda":  # 8-way device levels down to <= 32 rows per (group, window)
         while win.shape[0] > 32:
             win = _gt_prod_level(win, 8)
     h["win"] = win
-    return h
+    h["G"] = n_groups
+
+
+def _seg_select(bk, per_group: int, fold: int, groups: list):
+    """Keys of the kept per-(group, segment) buckets that belong to ``groups``
+    (original group ids), renumbered group-major: (position in groups) * fold + s
+    -> (row indices into the kept values, new keys)."""
+    gs = bk // per_group
+    g, sg = gs // fold, gs % fold
+    pos = np.full(int(g.max()) + 1 if g.size else 1, -1, dtype=np.int64)
+    for i, gg in enumerate(groups):
+        if gg < pos.size:
+            pos[gg] = i
+    sel = np.flatnonzero(pos[g] >= 0)
+    nbk = (pos[g[sel]] * fold + sg[sel]) * per_group + bk[sel] % per_group
+    order = np.argsort(nbk, kind="stable")  # keys stay sorted (contiguous (group, window) runs)
+    return sel[order], nbk[order]
+
+
+def multi_exp_seg_finish(h: dict, groups: list) -> torch.Tensor:
+    """Per-(group, segment) results of a ``multi_exp_grouped(..., fold=k)``
+    run for the original groups ``groups`` -> host [len(groups) * k, 96]
+    (group-major), from the kept buckets: no new plan, no re-bucketing."""
+    sg = h.get("seg")
+    W, c = h["W"], h["c"]
+    k = sg["fold"] if sg else 1
+    out = {"G": len(groups) * k, "W": W, "c": c, "win": None}
+    if sg is None:
+        return multi_exp_grouped_finish(out)
+    sel, nbk = _seg_select(sg["bk"], W << c, k, groups)
+    if sel.size:
+        cur = sg["cur"].index_select(0, _upload(sel.astype(np.int64), sg["cur"].device))
+        _me_windows(out, cur, nbk, len(groups) * k, W, c, sg["cur"].device)
+    return multi_exp_grouped_finish(out)
 
 
 def multi_exp_grouped_finish(h) -> torch.Tensor:
@@ -1514,16 +1581,18 @@ def g1_msm_plan(k: torch.Tensor, group, n_groups: int, bits: int = 256) -> dict:
 
 
 def g1_msm_launch(P_jac: torch.Tensor, k: torch.Tensor, group: torch.Tensor | None, n_groups: int,
-                  bits: int = 256, plan: dict | None = None) -> dict:
+                  bits: int = 256, plan: dict | None = None, fold: int = 1) -> dict:
     """First half of g1_msm_grouped: the bucket plan (one host sync on k,
     unless ``plan`` comes from ``g1_msm_plan``) and every device pass, queued
     on the current stream.  g1_msm_finish waits for them and runs the Horner
-    steps on the host."""
+    steps on the host.  ``fold`` = k: plan groups are (group, segment) pairs
+    g * k + s, the handle finishes the n_groups / k groups and keeps the
+    per-segment buckets for ``g1_msm_seg_finish`` (as ``multi_exp_grouped``)."""
     assert P_jac.shape[0] == k.shape[0]
     assert group is None or isinstance(group, int) or group.numel() == k.shape[0]
     dev = P_jac.device
     W = (bits + 7) // 8
-    h = {"n_groups": n_groups, "W": W, "S_w": None}
+    h = {"n_groups": n_groups // fold, "W": W, "S_w": None}
     if P_jac.shape[0] == 0:
         return h
     if plan is None:
@@ -1535,6 +1604,31 @@ def g1_msm_launch(P_jac: torch.Tensor, k: torch.Tensor, group: torch.Tensor | No
     cur = P_jac.index_select(0, plan["item"]).contiguous() if plan["single"] else None
     for i, (st, ln) in enumerate(plan["passes"]):
         cur = g1_slice_sum(P_jac if i == 0 else cur, plan["item"] if i == 0 else None, st, ln)
+    if fold > 1:
+        h["seg"] = {"cur": cur, "bk": bk, "fold": fold}
+        cur, bk = _fold_buckets(cur, bk, W << 8, fold, g1_slice_sum)
+    _g1_windows(h, cur, bk, dev)
+    return h
+
+
+def g1_msm_seg_finish(h: dict, groups: list) -> torch.Tensor:
+    """Per-(group, segment) sums of a ``g1_msm_launch(..., fold=k)`` run for
+    the original groups ``groups`` -> host [len(groups) * k, 24], from the
+    kept buckets."""
+    sg = h.get("seg")
+    k = sg["fold"] if sg else 1
+    out = {"n_groups": len(groups) * k, "W": h["W"], "S_w": None}
+    if sg is not None:
+        sel, nbk = _seg_select(sg["bk"], h["W"] << 8, k, groups)
+        if sel.size:
+            cur = sg["cur"].index_select(0, _upload(sel.astype(np.int64), sg["cur"].device))
+            _g1_windows(out, cur, nbk, sg["cur"].device)
+    return g1_msm_finish(out)
+
+
+def _g1_windows(h: dict, cur, bk, dev):
+    """Bucket sums -> d * B_{g,w,d} (one short variable-base launch) ->
+    per-(group, window) sums on the device (``g1_msm_finish`` ends on the host)."""
     sc = torch.zeros((bk.size, 8), dtype=torch.int32)
     sc[:, 0] = torch.from_numpy((bk % 256).astype("int32"))
     weighted = g1_mul(cur, _upload(sc.numpy(), dev))                     # d * B_{g,w,d}
@@ -1545,7 +1639,6 @@ def g1_msm_launch(P_jac: torch.Tensor, k: torch.Tensor, group: torch.Tensor | No
     for st, ln in _segment_passes(counts):
         cur = g1_slice_sum(cur, None, _upload(st, dev), _upload(ln.astype("int32"), dev))
     h["S_w"], h["gws"] = cur, gws
-    return h
 
 
 def g1_msm_finish(h: dict) -> torch.Tensor:
@@ -1641,14 +1734,17 @@ def g2_mul_small(jac: torch.Tensor, d: torch.Tensor) -> torch.Tensor:
 
 
 def g2_msm_launch(P_aff: torch.Tensor, k: torch.Tensor, group: torch.Tensor | None, n_groups: int,
-                  c: int = 13, bits: int = 254, first_slice: int = 32) -> dict:
+                  c: int = 13, bits: int = 254, first_slice: int = 32, fold: int = 1) -> dict:
     """Bucket plan of G independent G2 MSMs out[g] = sum_{t: group_t = g}
     k_t P[t % m] (m = rows of P_aff, k [n, 8] with n a multiple of m; group:
     int32 tensor, or an int stride s meaning group_t = t // s):
     c-bit windows; int32 keys (g, w, d) built by one kernel (zero digits get
     a sentinel that sorts last), one radix sort, per-bucket counts by a
     binary search of the bucket boundaries -- ONE host sync (the counts).
-    ``g2_msm_run`` queues the device passes."""
+    ``g2_msm_run`` queues the device passes.  ``fold`` = k: plan groups are
+    (group, segment) pairs g * k + s; the run sums the buckets over the
+    segments before weighting them (n_groups / k results) and keeps the
+    per-segment bucket sums for ``g2_msm_seg_run``."""
     dev = P_aff.device
     n, m = k.shape[0], _rows(P_aff, 32)
     W = -(-bits // c)
@@ -1664,27 +1760,49 @@ def g2_msm_launch(P_aff: torch.Tensor, k: torch.Tensor, group: torch.Tensor | No
     offs = torch.searchsorted(keys, torch.arange(nb + 1, device=dev, dtype=torch.int32))
     counts = (offs[1:] - offs[:-1]).cpu().numpy()                       # the one host sync
     bk = counts.nonzero()[0]
-    h = {"G": n_groups, "W": W, "c": c, "m": m, "bk": bk, "item": items[: int(counts.sum())]}
+    h = {"G": n_groups // fold, "W": W, "c": c, "m": m, "bk": bk, "item": items[: int(counts.sum())]}
     if bk.size:
         passes = _segment_passes_dev(counts[bk], dev, first_slice)
         if not passes:  # every bucket holds one entry
             passes = [(torch.arange(bk.size, device=dev), torch.ones(bk.size, dtype=torch.int32, device=dev))]
         h["passes"] = passes
-        dig = bk & ((1 << c) - 1)
-        h["d"] = _upload(dig.astype("int32"), dev)
-        # bucket weights by running sums over chunks of digit range G2_CHUNK
-        # (csrc/kernels/dx_rpmsm.hip chunk_weight_one), then per-window sums of
-        # the chunk results
-        gw = bk >> c
-        ck = gw * ((1 << c) // G2_CHUNK + 1) + dig // G2_CHUNK
-        first = np.flatnonzero(np.r_[True, ck[1:] != ck[:-1]])
-        clen = np.diff(np.r_[first, bk.size])
-        h["chunks"] = (_upload(first.astype(np.int64), dev), _upload(clen.astype(np.int32), dev),
-                       _upload(((dig[first] // G2_CHUNK) * G2_CHUNK).astype(np.int32), dev))
-        gws, gcounts = np.unique(gw[first], return_counts=True)
-        h["gws"] = _upload(gws.astype(np.int64), dev)
-        h["gpasses"] = _segment_passes_dev(gcounts, dev)
+        wbk = bk
+        if fold > 1:
+            per = W << c
+            t = (bk // per) // fold * per + bk % per
+            order_ = np.argsort(t, kind="stable")
+            ts = t[order_]
+            first = np.flatnonzero(np.r_[True, ts[1:] != ts[:-1]])
+            h["fold"] = (_upload(order_.astype(np.int32), dev), _upload(first.astype(np.int64), dev),
+                         _upload(np.diff(np.r_[first, ts.size]).astype(np.int32), dev))
+            h["seg_fold"] = fold
+            wbk = ts[first]
+        h.update(_g2_weight_plan(wbk, c, dev))
     return h
+
+
+def _g2_weight_plan(bk, c: int, dev) -> dict:
+    """Bucket weights by running sums over chunks of digit range G2_CHUNK
+    (csrc/kernels/dx_rpmsm.hip chunk_weight_one), then per-window sums of the
+    chunk results, for the sorted bucket keys ``bk``."""
+    dig = bk & ((1 << c) - 1)
+    gw = bk >> c
+    ck = gw * ((1 << c) // G2_CHUNK + 1) + dig // G2_CHUNK
+    first = np.flatnonzero(np.r_[True, ck[1:] != ck[:-1]])
+    clen = np.diff(np.r_[first, bk.size])
+    gws, gcounts = np.unique(gw[first], return_counts=True)
+    return {"d": _upload(dig.astype("int32"), dev),
+            "chunks": (_upload(first.astype(np.int64), dev), _upload(clen.astype(np.int32), dev),
+                       _upload(((dig[first] // G2_CHUNK) * G2_CHUNK).astype(np.int32), dev)),
+            "gws": _upload(gws.astype(np.int64), dev), "gpasses": _segment_passes_dev(gcounts, dev)}
+
+
+def _g2_weigh(cur, wp: dict, S: torch.Tensor) -> torch.Tensor:
+    cur = g2_chunk_weight(cur, wp["d"], *wp["chunks"])
+    for st, ln in wp["gpasses"]:
+        cur = g2_slice_sum(cur, None, st, ln, False)
+    S[wp["gws"]] = cur
+    return S
 
 
 def g2_msm_run(P_aff: torch.Tensor, h: dict) -> torch.Tensor:
@@ -1698,11 +1816,30 @@ def g2_msm_run(P_aff: torch.Tensor, h: dict) -> torch.Tensor:
         for i, (st, ln) in enumerate(h["passes"]):
             cur = g2_slice_sum(P_aff if i == 0 else cur, h["item"] if i == 0 else None, st, ln, i == 0,
                                h["m"] if i == 0 else 0)
-        cur = g2_chunk_weight(cur, h["d"], *h["chunks"])
-        for st, ln in h["gpasses"]:
-            cur = g2_slice_sum(cur, None, st, ln, False)
-        S[h["gws"]] = cur
+        if "fold" in h:
+            h["seg_cur"] = cur
+            cur = g2_slice_sum(cur, *h["fold"], False)                    # buckets summed over the segments
+        _g2_weigh(cur, h, S)
     return S
+
+
+def g2_msm_seg_run(h: dict, groups: list):
+    """Per-(group, segment) window sums of a ``g2_msm_launch(..., fold=k)``
+    run (after ``g2_msm_run``) for the original groups ``groups``, from the
+    kept bucket sums -> (S [len(groups) * k * W, 48], handle for
+    ``g2_msm_finish``): weights and window sums only, no new plan."""
+    k, W, c = h.get("seg_fold", 1), h["W"], h["c"]
+    G = len(groups) * k
+    cur = h.get("seg_cur")
+    dev = cur.device if cur is not None else torch.device("cpu")
+    S = torch.zeros((G * W, 48), dtype=torch.int32, device=dev)
+    hh = {"G": G, "W": W, "c": c}
+    if cur is None:
+        return S, hh
+    sel, nbk = _seg_select(h["bk"], W << c, k, groups)
+    if sel.size:
+        _g2_weigh(cur.index_select(0, _upload(sel.astype(np.int64), dev)), _g2_weight_plan(nbk, c, dev), S)
+    return S, hh
 
 
 def g2_msm_finish(S: torch.Tensor, h: dict, out_aff: torch.Tensor | None = None, stride: int = 1,

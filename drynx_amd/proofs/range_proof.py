@@ -882,6 +882,16 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
     # GT-membership combinations: one independent 40-bit gamma set PER VN
     gam_all = _cat_draw(lambda c: c.bits(m, device, 40) if c is not None else _rand64(m, device, 40))
     vns = [{"rho": rho_all[v * m:(v + 1) * m], "ab": ab_all[v * m:(v + 1) * m]} for v in range(G)]
+    # attribution: the bucket methods group every entry by (VN, segment) and
+    # sum / multiply the buckets over the segments before weighting them, so
+    # the per-VN checks cost the same, and a failing VN's per-segment values
+    # come from the kept buckets (no second plan, no re-bucketing)
+    fold = nseg if (segs is not None and nseg > 1 and use_msm
+                    and os.environ.get("DRYNX_SEG_KEEP", "1") != "0") else 1
+    pseg = iseg = None
+    if fold > 1:
+        pseg = torch.repeat_interleave(torch.arange(nseg, device=device), _h2d(segs, device), output_size=n)
+        iseg = pseg.repeat_interleave(S * l)
     aux = _aux_stream(device) if device.type == "cuda" else None
     if aux is not None:
         # the pairing work (~all of the GPU time) is queued FIRST on this
@@ -906,11 +916,16 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
         # every bucket plan (one host sync each) first, then every pass: a sync
         # never waits behind another plan's heavy passes
         if use_msm and aux is not None:
-            hR = _msm_plan(r.zphi, r.V, rho_all, G, n, S, l)
+            hR = _msm_plan(r.zphi, r.V, rho_all, G, n, S, l, iseg, fold)
         dpts = torch.cat([Cp.contiguous(), r.D.contiguous()]).repeat(G, 1)
         wc = nt.fr_arith(nt.FR_MUL, w_all, r.challenge.repeat(G, 1))
         dsc = torch.stack([wc.view(G, n, 8), w_all.view(G, n, 8)], 1).reshape(-1, 8).contiguous()
-        dplan = nt.g1_msm_plan(dsc, n, 2 * G)                             # group = row // n
+        if fold > 1:  # group = ((v, which) row // n, segment of the proof)
+            dgrp = (torch.arange(2 * G, device=device).view(-1, 1) * fold + pseg.view(1, n)).reshape(-1).to(torch.int32)
+            dplan = nt.g1_msm_plan(dsc, dgrp, 2 * G * fold)
+        else:
+            dgrp = n
+            dplan = nt.g1_msm_plan(dsc, n, 2 * G)                         # group = row // n
         # groups 0..G-1: prod a^rho_v; groups G..2G-1: each VN's own GT-membership
         # combination prod a^gamma_v
         # prod a^rho = prod a^a' * frob^8(a)^b': 32-bit exponents over (A, frob^8 A)
@@ -924,11 +939,17 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
         # host: bytes (fewer buckets for the host's serial bucket products)
         wc_ = (4, 11) if device.type == "cuda" else (5, 8)
         k = k.view(-1, 8)
-        mplan = nt.multi_exp_plan(k, 2 * m, 2 * G, W=wc_[0], c=wc_[1])          # group = row // 2m
-        mexp = nt.multi_exp_grouped(A2, k, 2 * m, 2 * G, W=wc_[0], c=wc_[1], plan=mplan)
+        if fold > 1:  # group = (row // 2m, segment of the item)
+            mgrp = (torch.arange(2 * G, device=device).view(-1, 1) * fold
+                    + iseg.repeat(2).view(1, 2 * m)).reshape(-1).to(torch.int32)
+            mplan = nt.multi_exp_plan(k, mgrp, 2 * G * fold, W=wc_[0], c=wc_[1])
+            mexp = nt.multi_exp_grouped(A2, k, mgrp, 2 * G * fold, W=wc_[0], c=wc_[1], plan=mplan, fold=fold)
+        else:
+            mplan = nt.multi_exp_plan(k, 2 * m, 2 * G, W=wc_[0], c=wc_[1])      # group = row // 2m
+            mexp = nt.multi_exp_grouped(A2, k, 2 * m, 2 * G, W=wc_[0], c=wc_[1], plan=mplan)
         if use_msm and aux is not None:
             S_R = nt.g2_msm_run(r.V, hR)                               # R window sums
-        dcheck = nt.g1_msm_launch(dpts, dsc, n, 2 * G, bits=256, plan=dplan)
+        dcheck = nt.g1_msm_launch(dpts, dsc, dgrp, 2 * G * fold, bits=256, plan=dplan, fold=fold)
         e_all = nt.fr_dot_rows(rho_all, r.zv, G, b_periodic=True)                        # sum rho Zv per VN
         dfull = torch.stack([nt.fr_dot_rows(w_all, r.zr, G, b_periodic=True),
                              nt.fr_dot_rows(w_all, z, G, b_periodic=True)], 1)             # [G, 2, 8]
@@ -953,7 +974,7 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
     else:
         GG = nt.multi_exp_grouped_finish(mexp)
         if use_msm:
-            hR = _msm_plan(r.zphi, r.V, rho_all, G, n, S, l)
+            hR = _msm_plan(r.zphi, r.V, rho_all, G, n, S, l, iseg, fold)
             msq = _msm_queue(Y, r.V, ab_all, G, n, S, l, None, segs)
             fR, rok = _msm_r_miller(hR, nt.g2_msm_run(r.V, hR))
             useg = _seg_products(msq)
@@ -1018,7 +1039,8 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
         with timers.span("rp.verify.segments"):
             per = _segment_pass(r, segs, redo, dict(
                 A2=A2, rho=rho_all, ab=ab_all, gam=gam_all, w=w_all, Cp=Cp, z=z, useg=useg, u_seg=msq["u_seg"],
-                PB_base=PB_base, gt_tab=gt_tab, wc=wc_,
+                PB_base=PB_base, gt_tab=gt_tab, wc=wc_, G=G,
+                kept=dict(hR=hR, mexp=mexp, dcheck=dcheck) if fold > 1 else None,
                 # undecodable proofs in the batch: the first pass's GT combination
                 # included a_ij not known to be cyclotomic, so it bounds nothing --
                 # every segment then gets its own combination
@@ -1039,14 +1061,18 @@ class _nullctx:
         return False
 
 
-def _msm_plan(zphi, V, rho_all, G: int, n: int, S: int, L: int) -> dict:
+def _msm_plan(zphi, V, rho_all, G: int, n: int, S: int, L: int, iseg=None, fold: int = 1) -> dict:
     """Verifier mode "msm", step 1 (one host sync): the R-MSM bucket plan of
-    every VN, R_v = sum_it (rho_it Zphi_(p, j)) V_it."""
+    every VN, R_v = sum_it (rho_it Zphi_(p, j)) V_it (``fold`` > 1: entries
+    grouped by (VN, segment ``iseg`` of the item), see ``nt.g2_msm_launch``)."""
     dev = V.device
     m = n * S * L
     it = torch.arange(m, device=dev)
     zi = (it // (S * L)) * L + it % L
     s_r = nt.fr_arith(nt.FR_MUL, rho_all, zphi.index_select(0, zi).repeat(G, 1).contiguous())
+    if fold > 1:
+        grp = (torch.arange(G, device=dev).view(G, 1) * fold + iseg.view(1, m)).reshape(-1).to(torch.int32)
+        return nt.g2_msm_launch(V, s_r, grp, G * fold, fold=fold)
     return nt.g2_msm_launch(V, s_r, m, G)                              # group (VN) = row // m
 
 
@@ -1201,6 +1227,8 @@ def _segment_pass(r: RangeProofList, segs: list, redo: list, x: dict) -> dict:
         return torch.cat([t[v * w:(v + 1) * w] for v in redo]) if Gf > 1 else t[redo[0] * w:(redo[0] + 1) * w]
 
     rho, ab, w = rows(x["rho"], m), rows(x["ab"], m), rows(x["w"], n)
+    if x.get("kept") is not None:
+        return _segment_finish_kept(r, segs, redo, x, rows, pseg, poff, K)
     # every input and every bucket plan (one host sync each) first, then the
     # device passes: a plan's sync then never waits behind another MSM's
     # queued passes (the first pass's schedule)
@@ -1258,6 +1286,50 @@ def _segment_pass(r: RangeProofList, segs: list, redo: list, x: dict) -> dict:
     useg = torch.stack([x["useg"][v] for v in redo]).view(K, 96)
     useg_ok = x["u_seg"].cpu()[redo].reshape(-1).tolist()
     lhs = nt.gt_mul(nt.final_exp(nt.gt_mul(useg.contiguous(), fR.contiguous())), GG.contiguous())
+    eq = nt.gt_eq(lhs, nt.gt_fb_pow(x["gt_tab"], e)).tolist()
+    PB = nt.g1_mul(x["PB_base"].repeat(K, 1), torch.stack([dzr, dz], 1).reshape(-1, 8).contiguous()).view(K, 2, 24)
+    lhs_d = nt.g1_sum(torch.stack([D_all[:, 0].reshape(K, 24), PB[:, 0], PB[:, 1]]).contiguous())
+    d_ok = nt.g1_eq(lhs_d.contiguous(), D_all[:, 1].reshape(K, 24).contiguous()).tolist()
+    out = {}
+    for f, v in enumerate(redo):
+        out[v] = [bool(eq[f * nseg + s_]) and bool(d_ok[f * nseg + s_]) and bool(useg_ok[f * nseg + s_])
+                  and bool(rok[f * nseg + s_]) and m_ok[f * nseg + s_] for s_ in range(nseg)]
+    return out
+
+
+def _segment_finish_kept(r: RangeProofList, segs: list, redo: list, x: dict, rows, pseg, poff, K: int) -> dict:
+    """``_segment_pass`` from the first pass's kept per-(VN, segment)
+    buckets: the failing VNs' R window sums, multi-exponentiation windows and
+    D-check windows per segment are weighted / combined from buckets already
+    on the device (nt.g2_msm_seg_run, multi_exp_seg_finish, g1_msm_seg_finish);
+    only the Horner steps, Miller loops of B with R, final exponentiations
+    and exponent sums remain."""
+    dev = r.V.device
+    n, nseg, Gf, G = len(r), len(segs), len(redo), x["G"]
+    kept = x["kept"]
+    rho, w = rows(x["rho"], n * r.S * r.l), rows(x["w"], n)
+    with timers.span("rp.seg.kept_windows"):
+        S_R, hh = nt.g2_msm_seg_run(kept["hR"], list(redo))
+        Dk = nt.g1_msm_seg_finish(kept["dcheck"], [g for v in redo for g in (2 * v, 2 * v + 1)])
+    offs = torch.from_numpy((np.arange(Gf).reshape(Gf, 1) * n + poff[:-1].reshape(1, nseg)).reshape(-1))
+    offs = bn.h2d(torch.cat([offs, torch.tensor([Gf * n])]), dev)
+    e = nt.fr_seg_sum(nt.fr_dot_rows(rho, r.zv.repeat(Gf, 1).contiguous(), Gf * n), offs)
+    dzr = nt.fr_seg_sum(nt.fr_arith(nt.FR_MUL, w, r.zr.repeat(Gf, 1).contiguous()), offs)
+    dz = nt.fr_seg_sum(nt.fr_arith(nt.FR_MUL, w, x["z"].repeat(Gf, 1).contiguous()), offs)
+    with timers.span("rp.seg.gt_finish"):
+        GG = nt.multi_exp_seg_finish(kept["mexp"], list(redo))                 # [K, 96] prod a^rho per (v, s)
+        if any(not x["m_first"][v] for v in redo):
+            m_ok = _gt_in_subgroup_each(nt.multi_exp_seg_finish(kept["mexp"], [G + v for v in redo]))
+        else:  # the first pass's combination bounds every a_ij already
+            m_ok = [True] * K
+    with timers.span("rp.seg.r_finish"):
+        fR, rok = _msm_r_miller(hh, S_R)
+    D_all = Dk.view(Gf, 2, nseg, 24)
+    e, dzr, dz = e.cpu(), dzr.cpu(), dz.cpu()
+    useg = torch.stack([x["useg"][v] for v in redo]).view(K, 96)
+    useg_ok = x["u_seg"].cpu()[redo].reshape(-1).tolist()
+    with timers.span("rp.seg.final_exp"):
+        lhs = nt.gt_mul(nt.final_exp(nt.gt_mul(useg.contiguous(), fR.contiguous())), GG.contiguous())
     eq = nt.gt_eq(lhs, nt.gt_fb_pow(x["gt_tab"], e)).tolist()
     PB = nt.g1_mul(x["PB_base"].repeat(K, 1), torch.stack([dzr, dz], 1).reshape(-1, 8).contiguous()).view(K, 2, 24)
     lhs_d = nt.g1_sum(torch.stack([D_all[:, 0].reshape(K, 24), PB[:, 0], PB[:, 1]]).contiguous())

@@ -64,19 +64,65 @@ def _sync():
         torch.cuda.current_stream().synchronize()
 
 
+def _use_events() -> bool:
+    """Device-timed phases measure with HIP events on the phase's stream
+    (resolved when the timers are read) instead of synchronising the host at
+    both ends: a phase timer then costs the query no host-device round trip.
+    DRYNX_TIMER_SYNC=1 restores the synchronising timers."""
+    return (os.environ.get("DRYNX_TIMER_SYNC") != "1" and torch.cuda.is_available()
+            and torch.cuda.is_initialized())
+
+
+_pending: list = []  # (name, start event, end event) of event-timed phases
+
+
+def _resolve():
+    """Turn finished event pairs into recorded intervals (device time from
+    the phase's first to its last queued operation on its stream)."""
+    with _lock:
+        todo = list(_pending)
+        _pending.clear()
+    done = []
+    for name, e0, e1 in todo:
+        e1.synchronize()
+        done.append((name, e0.elapsed_time(e1) / 1e3))
+    with _lock:
+        for name, dt in done:
+            _records[name].append(dt)
+
+
 class Timer:
     def __init__(self, name: str, sync: bool = True):
         self.name = name
         self.sync = sync
         self.t0 = None
+        self.ev = None
 
     def start(self):
-        if self.sync:
+        if self.sync and _use_events():
+            self.ev = torch.cuda.Event(enable_timing=True)
+            self.ev.record()
+        elif self.sync:
             _sync()
         self.t0 = time.perf_counter()
         return self
 
     def end(self) -> float:
+        if self.ev is not None:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            t1 = time.perf_counter()
+            with _lock:
+                _pending.append((self.name, self.ev, e1))
+                if len(_pending) > 4096:
+                    todo = _pending[:2048]
+                    del _pending[:2048]
+                    for name, a, b in todo:
+                        b.synchronize()
+                        _records[name].append(a.elapsed_time(b) / 1e3)
+            if _TRACE:
+                _emit(self.name, int(self.t0 * 1e9), int(t1 * 1e9))
+            return t1 - self.t0
         if self.sync:
             _sync()
         t1 = time.perf_counter()
@@ -123,6 +169,7 @@ def record(name: str, seconds: float):
 
 
 def records() -> dict:
+    _resolve()
     with _lock:
         return {k: list(v) for k, v in _records.items()}
 
@@ -144,11 +191,13 @@ def counters() -> dict:
 
 def reset():
     with _lock:
+        _pending.clear()
         _records.clear()
         _counts.clear()
 
 
 def summary() -> dict:
+    _resolve()
     with _lock:
         return {k: {"n": len(v), "sum": sum(v), "mean": sum(v) / len(v), "max": max(v)} for k, v in _records.items()}
 

@@ -159,7 +159,7 @@ def test_both_verifier_modes_accept_and_reject(device, mode, proofs, monkeypatch
 
 @pytest.mark.parametrize("device", DEVICES)
 @pytest.mark.parametrize("field", ["V", "zr", "A", "A_off_gt"])
-def test_segment_attribution(device, field, proofs):
+def test_segment_attribution(device, field, proofs, monkeypatch):
     """segs = per-request slices: a clean batch clears every segment; a
     tampered proof is named by the failing VN's segment-grouped second pass
     (pairing side: V; D-equation: Zr; GT side: A), the other segments pass."""
@@ -189,5 +189,13 @@ def test_segment_attribution(device, field, proofs):
         A[-1, -1] ^= 1
         bad.A = A
         want = [True, True, False]
+    calls = []
+    orig = rp._segment_finish_kept
+    monkeypatch.setattr(rp, "_segment_finish_kept", lambda *a: calls.append(1) or orig(*a))
     assert rp.verify_range_proof_list_multi(bad, sm, P, 2, dev, segs=[1, 2, 1]) == [want] * 2
+    assert calls, "the failing VNs' segments come from the first pass's kept buckets"
+    # the re-bucketing second pass (DRYNX_SEG_KEEP=0) names the same segments
+    monkeypatch.setenv("DRYNX_SEG_KEEP", "0")
+    assert rp.verify_range_proof_list_multi(bad, sm, P, 2, dev, segs=[1, 2, 1]) == [want] * 2
+    assert len(calls) == 1
     assert rp.verify_range_proof_list_multi(bad, sm, P, 2, dev) == [False] * 2
