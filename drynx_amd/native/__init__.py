@@ -98,6 +98,10 @@ _SIGS = {
     "dx_g1_mul_fast": [_P, _P, _P, _P, _L, _I, _I],
     "dx_rp_verify_fold": [_P, _P, _P, _P, _P, _P, _L, _I, _I],
     "dx_gt_slice_prod": [_I, _P, _P, _P, _P, _P, _P, _L],
+    "dx_bucket_sort_tmp": [_L, _I, ctypes.POINTER(ctypes.c_uint64)],
+    "dx_bucket_sort": [_I, _P, _P, _P, _P, _P, _L, _I, _P, ctypes.c_uint64],
+    "dx_bucket_bounds": [_I, _P, _P, _L, _L, _P, _P],
+    "dx_slice_plan": [_I, _P, _P, _P, _P, _I, _L, _P, _P],
     "dx_g1_slice_sum": [_I, _P, _P, _P, _P, _P, _P, _L],
     "dx_rp_prove_a": [_I, _P, _P, _P, _P, _P, _P, _L, _I, _I],
     "dx_rp_prove_a_tab": [_I, _P, _P, _P, _P, _P, _P, _P, _L, _I, _I, _I],
@@ -1332,7 +1336,59 @@ def _multi_exp64_plan(rho: torch.Tensor):
     return _bucket_plan(rho, _ME_W)
 
 
+def _sort_buckets(keys: torch.Tensor, items: torch.Tensor, nb: int):
+    """Sort the (key, item) entries of a bucket plan by key over its low
+    bit_length(nb) bits (csrc/kernels/dx_plan.hip: rocPRIM radix sort, 4-byte
+    payload) and find every bucket's run -> (sorted items, per-bucket counts
+    on the host: the plan's one device-to-host copy)."""
+    dev = keys.device
+    n = keys.numel()
+    end_bit = max(1, int(nb).bit_length())
+    k2 = torch.empty_like(keys)
+    i2 = torch.empty_like(items)
+    g, s = _ctx(keys)
+    tmp = None
+    tb = ctypes.c_uint64(0)
+    if g:
+        rc = _raw_call("dx_bucket_sort_tmp", n, end_bit, ctypes.byref(tb))
+        if rc:
+            raise RuntimeError("dx_bucket_sort_tmp failed")
+        tmp = torch.empty(max(1, int(tb.value)), dtype=torch.uint8, device=dev)
+    _call("dx_bucket_sort", g, s, _ptr(keys), _ptr(items), _ptr(k2), _ptr(i2), n, end_bit, _ptr(tmp), tb.value)
+    bounds = torch.zeros((2, nb), dtype=torch.int64, device=dev)
+    _call("dx_bucket_bounds", g, s, _ptr(k2), n, nb, _ptr(bounds[0]), _ptr(bounds[1]))
+    fe = bounds.cpu().numpy()                                           # the one host sync
+    return i2, fe[1] - fe[0]
+
+
 def _segment_passes_dev(counts, dev, first_slice: int | None = None):
+    """``_segment_passes`` with the per-slice (start, len) arrays written on
+    the device by one thread per bucket (csrc/kernels/dx_plan.hip
+    dx_slice_plan): only the per-bucket counts (at most a few hundred
+    thousand) go through the host; the millions of slice descriptors of a wide
+    multi-exponentiation are never built by numpy or torch index kernels.
+    ``first_slice``: entries per thread in the first pass (later passes use
+    _ME_SLICE)."""
+    import numpy as _np
+
+    passes = []
+    c = _np.asarray(counts, dtype=_np.int64)
+    while c.size and c.max() > 1:
+        sl = first_slice if (first_slice and not passes) else _ME_SLICE
+        n_sl = (c + sl - 1) // sl
+        total = int(n_sl.sum())
+        meta = _np.stack([_np.cumsum(c) - c, c, _np.cumsum(n_sl) - n_sl])
+        m_dev = _upload(meta, dev)
+        start = torch.empty(total, dtype=torch.int64, device=dev)
+        ln = torch.empty(total, dtype=torch.int32, device=dev)
+        g, s = _ctx(m_dev)
+        _call("dx_slice_plan", g, s, _ptr(m_dev[0]), _ptr(m_dev[1]), _ptr(m_dev[2]), sl, c.size, _ptr(start), _ptr(ln))
+        passes.append((start, ln))
+        c = n_sl
+    return passes
+
+
+def _segment_passes_dev_torch(counts, dev, first_slice: int | None = None):
     """``_segment_passes`` with the per-slice (start, len) arrays built on the
     device: only the per-bucket counts (at most a few thousand) live on the
     host, the millions of slice descriptors of a wide multi-exponentiation
@@ -1384,11 +1440,8 @@ def _bucket_plan(k: torch.Tensor, W: int, group: torch.Tensor | None = None, n_g
     g, s = _ctx(k, keys)
     _call("dx_msm_keys", g, s, _ptr(k.contiguous()), _ptr(grp), gstride, n, c, W, _ptr(keys),  # dx_rpmsm.hip
           _ptr(item))
-    keys, order = torch.sort(keys)          # zero digits carry a sentinel key that sorts last
-    item = item.index_select(0, order).to(torch.int64)
-    offs = torch.searchsorted(keys, torch.arange(nb + 1, device=dev, dtype=torch.int32))
-    counts = (offs[1:] - offs[:-1]).cpu().numpy()                    # the one host sync
-    item = item[: int(counts.sum())]                                    # drop the zero-digit sentinels
+    item, counts = _sort_buckets(keys, item, nb)   # zero digits carry a sentinel key that sorts last
+    item = item[: int(counts.sum())].to(torch.int64)                    # drop the zero-digit sentinels
     bk = counts.nonzero()[0]
     passes = _segment_passes_dev(counts[bk], dev)
     # bucket digits and scatter slots, staged now so the run needs no host->device copy
@@ -1457,26 +1510,79 @@ def multi_exp_grouped(a: torch.Tensor, k: torch.Tensor, group, n_groups: int, W:
     if fold > 1:
         # per-(group, segment) buckets are kept for ``multi_exp_seg_finish``;
         # the groups' results come from the buckets multiplied across segments
-        h["seg"] = {"cur": cur, "bk": bk, "fold": fold}
-        cur, bk = _fold_buckets(cur, bk, W << c, fold, lambda src, idx, st, ln: gt_slice_prod(src, idx, st, ln))
+        cur, bk, h["seg"] = _fold_buckets(cur, bk, W << c, fold, n_groups, gt_one(a.device), gt_slice_prod,
+                                          torch.int64)
     _me_windows(h, cur, bk, n_groups // fold, W, c, a.device)
     return h
 
 
-def _fold_buckets(cur, bk, per_group: int, fold: int, slice_op):
-    """Buckets of groups g * fold + s (keys bk, values cur) combined over s:
-    one segmented slice operation (product / sum) -> (values, keys) of the
-    groups g (host-side ordering of the bucket keys; the values never leave
-    the device)."""
-    t = (bk // per_group) // fold * per_group + bk % per_group
-    order = np.argsort(t, kind="stable")
-    ts = t[order]
-    first = np.flatnonzero(np.r_[True, ts[1:] != ts[:-1]])
-    lens = np.diff(np.r_[first, ts.size])
+_FOLD_IDX: dict = {}
+
+
+def _fold_buckets(cur, bk, per_group: int, fold: int, n_groups: int, fill_row, slice_op, idx_dtype):
+    """Buckets of the plan groups g * fold + s (keys bk, values cur) combined
+    over s into the groups g.  Dense and host-free: the values are scattered
+    into a [n_groups * per_group] image (empty buckets = the identity
+    ``fill_row``) and every group bucket reduces its ``fold`` strided rows in
+    one slice launch; the host only derives the non-empty group buckets from
+    the plan's own key list.  -> (values, keys of the non-empty group
+    buckets, kept image + mask for the per-segment finish)."""
     dev = cur.device
-    idx = _upload(order.astype(np.int64), dev)
-    out = slice_op(cur, idx, _upload(first.astype(np.int64), dev), _upload(lens.astype(np.int32), dev))
-    return out, ts[first]
+    G = n_groups // fold
+    nbt = n_groups * per_group
+    dense = fill_row.view(1, -1).expand(nbt, fill_row.numel()).contiguous()
+    dense.index_copy_(0, _upload(bk.astype(np.int64), dev), cur)
+    key = (G, per_group, fold, str(dev), idx_dtype)
+    if key not in _FOLD_IDX:
+        if len(_FOLD_IDX) > 16:
+            _FOLD_IDX.clear()
+        gj = torch.arange(G * per_group, device=dev, dtype=torch.int64)
+        g, j = gj // per_group, gj % per_group
+        idx = ((g.view(-1, 1) * fold + torch.arange(fold, device=dev).view(1, -1)) * per_group + j.view(-1, 1))
+        _FOLD_IDX[key] = (idx.reshape(-1).to(idx_dtype).contiguous(), gj * fold,
+                          torch.full((G * per_group,), fold, dtype=torch.int32, device=dev))
+    idx, start, ln = _FOLD_IDX[key]
+    red = slice_op(dense, idx, start, ln)
+    mask = np.zeros(nbt, dtype=bool)
+    mask[bk] = True
+    bk_red = np.flatnonzero(mask.reshape(G, fold, per_group).any(axis=1).reshape(-1))
+    vals = red.index_select(0, _upload(bk_red.astype(np.int64), dev)) if bk_red.size < red.shape[0] else red
+    return vals, bk_red, {"dense": dense, "mask": mask, "fold": fold, "per": per_group}
+
+
+def _seg_rows(keep: dict, groups: list):
+    """Rows of the kept image for the original groups ``groups`` (non-empty
+    buckets only) and their keys renumbered group-major: (position in groups)
+    * fold + s -> (rows, keys), keys sorted."""
+    per, fold = keep["per"], keep["fold"]
+    m = keep["mask"].reshape(-1, fold, per)
+    rows, keys = [], []
+    for i, g in enumerate(groups):
+        if g >= m.shape[0]:
+            continue
+        s_, j_ = np.nonzero(m[g])
+        rows.append((g * fold + s_) * per + j_)
+        keys.append((i * fold + s_) * per + j_)
+    if not rows:
+        return np.zeros(0, dtype=np.int64), np.zeros(0, dtype=np.int64)
+    return np.concatenate(rows), np.concatenate(keys)
+
+
+def multi_exp_seg_finish(h: dict, groups: list) -> torch.Tensor:
+    """Per-(group, segment) results of a ``multi_exp_grouped(..., fold=k)``
+    run for the original groups ``groups`` -> host [len(groups) * k, 96]
+    (group-major), from the kept buckets: no new plan, no re-bucketing."""
+    keep = h.get("seg")
+    W, c = h["W"], h["c"]
+    k = keep["fold"] if keep else 1
+    out = {"G": len(groups) * k, "W": W, "c": c, "win": None}
+    if keep is None:
+        return multi_exp_grouped_finish(out)
+    rows, nbk = _seg_rows(keep, groups)
+    if rows.size:
+        dense = keep["dense"]
+        _me_windows(out, dense.index_select(0, _upload(rows, dense.device)), nbk, len(groups) * k, W, c, dense.device)
+    return multi_exp_grouped_finish(out)
 
 
 def _me_windows(h: dict, cur, bk, n_groups: int, W: int, c: int, dev):
@@ -1497,39 +1603,6 @@ def _me_windows(h: dict, cur, bk, n_groups: int, W: int, c: int, dev):
             win = _gt_prod_level(win, 8)
     h["win"] = win
     h["G"] = n_groups
-
-
-def _seg_select(bk, per_group: int, fold: int, groups: list):
-    """Keys of the kept per-(group, segment) buckets that belong to ``groups``
-    (original group ids), renumbered group-major: (position in groups) * fold + s
-    -> (row indices into the kept values, new keys)."""
-    gs = bk // per_group
-    g, sg = gs // fold, gs % fold
-    pos = np.full(int(g.max()) + 1 if g.size else 1, -1, dtype=np.int64)
-    for i, gg in enumerate(groups):
-        if gg < pos.size:
-            pos[gg] = i
-    sel = np.flatnonzero(pos[g] >= 0)
-    nbk = (pos[g[sel]] * fold + sg[sel]) * per_group + bk[sel] % per_group
-    order = np.argsort(nbk, kind="stable")  # keys stay sorted (contiguous (group, window) runs)
-    return sel[order], nbk[order]
-
-
-def multi_exp_seg_finish(h: dict, groups: list) -> torch.Tensor:
-    """Per-(group, segment) results of a ``multi_exp_grouped(..., fold=k)``
-    run for the original groups ``groups`` -> host [len(groups) * k, 96]
-    (group-major), from the kept buckets: no new plan, no re-bucketing."""
-    sg = h.get("seg")
-    W, c = h["W"], h["c"]
-    k = sg["fold"] if sg else 1
-    out = {"G": len(groups) * k, "W": W, "c": c, "win": None}
-    if sg is None:
-        return multi_exp_grouped_finish(out)
-    sel, nbk = _seg_select(sg["bk"], W << c, k, groups)
-    if sel.size:
-        cur = sg["cur"].index_select(0, _upload(sel.astype(np.int64), sg["cur"].device))
-        _me_windows(out, cur, nbk, len(groups) * k, W, c, sg["cur"].device)
-    return multi_exp_grouped_finish(out)
 
 
 def multi_exp_grouped_finish(h) -> torch.Tensor:
@@ -1605,8 +1678,10 @@ def g1_msm_launch(P_jac: torch.Tensor, k: torch.Tensor, group: torch.Tensor | No
     for i, (st, ln) in enumerate(plan["passes"]):
         cur = g1_slice_sum(P_jac if i == 0 else cur, plan["item"] if i == 0 else None, st, ln)
     if fold > 1:
-        h["seg"] = {"cur": cur, "bk": bk, "fold": fold}
-        cur, bk = _fold_buckets(cur, bk, W << 8, fold, g1_slice_sum)
+        from ..crypto.bn254 import g1_infinity_jac
+
+        cur, bk, h["seg"] = _fold_buckets(cur, bk, W << 8, fold, n_groups, g1_infinity_jac(1, dev).to(dev)[0],
+                                          g1_slice_sum, torch.int64)
     _g1_windows(h, cur, bk, dev)
     return h
 
@@ -1615,14 +1690,14 @@ def g1_msm_seg_finish(h: dict, groups: list) -> torch.Tensor:
     """Per-(group, segment) sums of a ``g1_msm_launch(..., fold=k)`` run for
     the original groups ``groups`` -> host [len(groups) * k, 24], from the
     kept buckets."""
-    sg = h.get("seg")
-    k = sg["fold"] if sg else 1
+    keep = h.get("seg")
+    k = keep["fold"] if keep else 1
     out = {"n_groups": len(groups) * k, "W": h["W"], "S_w": None}
-    if sg is not None:
-        sel, nbk = _seg_select(sg["bk"], h["W"] << 8, k, groups)
-        if sel.size:
-            cur = sg["cur"].index_select(0, _upload(sel.astype(np.int64), sg["cur"].device))
-            _g1_windows(out, cur, nbk, sg["cur"].device)
+    if keep is not None:
+        rows, nbk = _seg_rows(keep, groups)
+        if rows.size:
+            dense = keep["dense"]
+            _g1_windows(out, dense.index_select(0, _upload(rows, dense.device)), nbk, dense.device)
     return g1_msm_finish(out)
 
 
@@ -1734,17 +1809,14 @@ def g2_mul_small(jac: torch.Tensor, d: torch.Tensor) -> torch.Tensor:
 
 
 def g2_msm_launch(P_aff: torch.Tensor, k: torch.Tensor, group: torch.Tensor | None, n_groups: int,
-                  c: int = 13, bits: int = 254, first_slice: int = 32, fold: int = 1) -> dict:
+                  c: int = 13, bits: int = 254, first_slice: int = 32) -> dict:
     """Bucket plan of G independent G2 MSMs out[g] = sum_{t: group_t = g}
     k_t P[t % m] (m = rows of P_aff, k [n, 8] with n a multiple of m; group:
     int32 tensor, or an int stride s meaning group_t = t // s):
     c-bit windows; int32 keys (g, w, d) built by one kernel (zero digits get
-    a sentinel that sorts last), one radix sort, per-bucket counts by a
-    binary search of the bucket boundaries -- ONE host sync (the counts).
-    ``g2_msm_run`` queues the device passes.  ``fold`` = k: plan groups are
-    (group, segment) pairs g * k + s; the run sums the buckets over the
-    segments before weighting them (n_groups / k results) and keeps the
-    per-segment bucket sums for ``g2_msm_seg_run``."""
+    a sentinel that sorts last), one radix sort over the keys' bits
+    (csrc/kernels/dx_plan.hip), per-bucket runs by their boundaries -- ONE
+    host sync (the counts).  ``g2_msm_run`` queues the device passes."""
     dev = P_aff.device
     n, m = k.shape[0], _rows(P_aff, 32)
     W = -(-bits // c)
@@ -1755,29 +1827,15 @@ def g2_msm_launch(P_aff: torch.Tensor, k: torch.Tensor, group: torch.Tensor | No
     grp, gstride = _group_arg(group, n, dev)
     g, s = _ctx(k, keys)
     _call("dx_msm_keys", g, s, _ptr(k.contiguous()), _ptr(grp), gstride, n, c, W, _ptr(keys), _ptr(items))
-    keys, order = torch.sort(keys)
-    items = items.index_select(0, order).contiguous()
-    offs = torch.searchsorted(keys, torch.arange(nb + 1, device=dev, dtype=torch.int32))
-    counts = (offs[1:] - offs[:-1]).cpu().numpy()                       # the one host sync
+    items, counts = _sort_buckets(keys, items, nb)                      # the one host sync
     bk = counts.nonzero()[0]
-    h = {"G": n_groups // fold, "W": W, "c": c, "m": m, "bk": bk, "item": items[: int(counts.sum())]}
+    h = {"G": n_groups, "W": W, "c": c, "m": m, "bk": bk, "item": items[: int(counts.sum())]}
     if bk.size:
         passes = _segment_passes_dev(counts[bk], dev, first_slice)
         if not passes:  # every bucket holds one entry
             passes = [(torch.arange(bk.size, device=dev), torch.ones(bk.size, dtype=torch.int32, device=dev))]
         h["passes"] = passes
-        wbk = bk
-        if fold > 1:
-            per = W << c
-            t = (bk // per) // fold * per + bk % per
-            order_ = np.argsort(t, kind="stable")
-            ts = t[order_]
-            first = np.flatnonzero(np.r_[True, ts[1:] != ts[:-1]])
-            h["fold"] = (_upload(order_.astype(np.int32), dev), _upload(first.astype(np.int64), dev),
-                         _upload(np.diff(np.r_[first, ts.size]).astype(np.int32), dev))
-            h["seg_fold"] = fold
-            wbk = ts[first]
-        h.update(_g2_weight_plan(wbk, c, dev))
+        h.update(_g2_weight_plan(bk, c, dev))
     return h
 
 
@@ -1816,30 +1874,8 @@ def g2_msm_run(P_aff: torch.Tensor, h: dict) -> torch.Tensor:
         for i, (st, ln) in enumerate(h["passes"]):
             cur = g2_slice_sum(P_aff if i == 0 else cur, h["item"] if i == 0 else None, st, ln, i == 0,
                                h["m"] if i == 0 else 0)
-        if "fold" in h:
-            h["seg_cur"] = cur
-            cur = g2_slice_sum(cur, *h["fold"], False)                    # buckets summed over the segments
         _g2_weigh(cur, h, S)
     return S
-
-
-def g2_msm_seg_run(h: dict, groups: list):
-    """Per-(group, segment) window sums of a ``g2_msm_launch(..., fold=k)``
-    run (after ``g2_msm_run``) for the original groups ``groups``, from the
-    kept bucket sums -> (S [len(groups) * k * W, 48], handle for
-    ``g2_msm_finish``): weights and window sums only, no new plan."""
-    k, W, c = h.get("seg_fold", 1), h["W"], h["c"]
-    G = len(groups) * k
-    cur = h.get("seg_cur")
-    dev = cur.device if cur is not None else torch.device("cpu")
-    S = torch.zeros((G * W, 48), dtype=torch.int32, device=dev)
-    hh = {"G": G, "W": W, "c": c}
-    if cur is None:
-        return S, hh
-    sel, nbk = _seg_select(h["bk"], W << c, k, groups)
-    if sel.size:
-        _g2_weigh(cur.index_select(0, _upload(sel.astype(np.int64), dev)), _g2_weight_plan(nbk, c, dev), S)
-    return S, hh
 
 
 def g2_msm_finish(S: torch.Tensor, h: dict, out_aff: torch.Tensor | None = None, stride: int = 1,

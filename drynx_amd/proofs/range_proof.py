@@ -916,7 +916,7 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
         # every bucket plan (one host sync each) first, then every pass: a sync
         # never waits behind another plan's heavy passes
         if use_msm and aux is not None:
-            hR = _msm_plan(r.zphi, r.V, rho_all, G, n, S, l, iseg, fold)
+            hR = _msm_plan(r.zphi, r.V, rho_all, G, n, S, l)
         dpts = torch.cat([Cp.contiguous(), r.D.contiguous()]).repeat(G, 1)
         wc = nt.fr_arith(nt.FR_MUL, w_all, r.challenge.repeat(G, 1))
         dsc = torch.stack([wc.view(G, n, 8), w_all.view(G, n, 8)], 1).reshape(-1, 8).contiguous()
@@ -974,7 +974,7 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
     else:
         GG = nt.multi_exp_grouped_finish(mexp)
         if use_msm:
-            hR = _msm_plan(r.zphi, r.V, rho_all, G, n, S, l, iseg, fold)
+            hR = _msm_plan(r.zphi, r.V, rho_all, G, n, S, l)
             msq = _msm_queue(Y, r.V, ab_all, G, n, S, l, None, segs)
             fR, rok = _msm_r_miller(hR, nt.g2_msm_run(r.V, hR))
             useg = _seg_products(msq)
@@ -1040,7 +1040,7 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
             per = _segment_pass(r, segs, redo, dict(
                 A2=A2, rho=rho_all, ab=ab_all, gam=gam_all, w=w_all, Cp=Cp, z=z, useg=useg, u_seg=msq["u_seg"],
                 PB_base=PB_base, gt_tab=gt_tab, wc=wc_, G=G,
-                kept=dict(hR=hR, mexp=mexp, dcheck=dcheck) if fold > 1 else None,
+                kept=dict(mexp=mexp, dcheck=dcheck) if fold > 1 else None,
                 # undecodable proofs in the batch: the first pass's GT combination
                 # included a_ij not known to be cyclotomic, so it bounds nothing --
                 # every segment then gets its own combination
@@ -1061,18 +1061,14 @@ class _nullctx:
         return False
 
 
-def _msm_plan(zphi, V, rho_all, G: int, n: int, S: int, L: int, iseg=None, fold: int = 1) -> dict:
+def _msm_plan(zphi, V, rho_all, G: int, n: int, S: int, L: int) -> dict:
     """Verifier mode "msm", step 1 (one host sync): the R-MSM bucket plan of
-    every VN, R_v = sum_it (rho_it Zphi_(p, j)) V_it (``fold`` > 1: entries
-    grouped by (VN, segment ``iseg`` of the item), see ``nt.g2_msm_launch``)."""
+    every VN, R_v = sum_it (rho_it Zphi_(p, j)) V_it."""
     dev = V.device
     m = n * S * L
     it = torch.arange(m, device=dev)
     zi = (it // (S * L)) * L + it % L
     s_r = nt.fr_arith(nt.FR_MUL, rho_all, zphi.index_select(0, zi).repeat(G, 1).contiguous())
-    if fold > 1:
-        grp = (torch.arange(G, device=dev).view(G, 1) * fold + iseg.view(1, m)).reshape(-1).to(torch.int32)
-        return nt.g2_msm_launch(V, s_r, grp, G * fold, fold=fold)
     return nt.g2_msm_launch(V, s_r, m, G)                              # group (VN) = row // m
 
 
@@ -1299,17 +1295,28 @@ def _segment_pass(r: RangeProofList, segs: list, redo: list, x: dict) -> dict:
 
 def _segment_finish_kept(r: RangeProofList, segs: list, redo: list, x: dict, rows, pseg, poff, K: int) -> dict:
     """``_segment_pass`` from the first pass's kept per-(VN, segment)
-    buckets: the failing VNs' R window sums, multi-exponentiation windows and
-    D-check windows per segment are weighted / combined from buckets already
-    on the device (nt.g2_msm_seg_run, multi_exp_seg_finish, g1_msm_seg_finish);
-    only the Horner steps, Miller loops of B with R, final exponentiations
-    and exponent sums remain."""
+    buckets: the failing VNs' multi-exponentiation and D-check values per
+    segment are finished from buckets already on the device
+    (nt.multi_exp_seg_finish, g1_msm_seg_finish: no plan, no re-bucketing);
+    the G2 R side is re-bucketed per segment (its per-segment buckets would
+    be nseg x the first pass's), then Horner steps, Miller loops of B with R,
+    final exponentiations and exponent sums."""
     dev = r.V.device
     n, nseg, Gf, G = len(r), len(segs), len(redo), x["G"]
     kept = x["kept"]
     rho, w = rows(x["rho"], n * r.S * r.l), rows(x["w"], n)
+    m = n * r.S * r.l
+    # R_(v,s) = sum_{it in s} rho_it Zphi_(p,j) V_it: the one side re-bucketed
+    # per segment (a G2 plan kept per segment would hold nseg x the buckets)
+    it = torch.arange(m, device=dev)
+    zi = (it // (r.S * r.l)) * r.l + it % r.l
+    s_r = nt.fr_arith(nt.FR_MUL, rho, r.zphi.index_select(0, zi).repeat(Gf, 1).contiguous())
+    iseg = pseg.repeat_interleave(r.S * r.l)
+    grp = (torch.arange(Gf, device=dev).view(Gf, 1) * nseg + iseg.view(1, m)).reshape(-1).to(torch.int32)
+    with timers.span("rp.seg.plans"):
+        hh = nt.g2_msm_launch(r.V, s_r, grp, K, c=_seg_c(Gf * m, K))
+    S_R = nt.g2_msm_run(r.V, hh)
     with timers.span("rp.seg.kept_windows"):
-        S_R, hh = nt.g2_msm_seg_run(kept["hR"], list(redo))
         Dk = nt.g1_msm_seg_finish(kept["dcheck"], [g for v in redo for g in (2 * v, 2 * v + 1)])
     offs = torch.from_numpy((np.arange(Gf).reshape(Gf, 1) * n + poff[:-1].reshape(1, nseg)).reshape(-1))
     offs = bn.h2d(torch.cat([offs, torch.tensor([Gf * n])]), dev)

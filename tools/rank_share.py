@@ -61,6 +61,38 @@ def timed(fn, reps):
     return round(statistics.median(ts), 2)
 
 
+def _torch_glue(path, *fns):
+    """GPU time of the torch ops launched by ``fns`` (run on this thread),
+    grouped by (op, innermost framework frame), plus every kernel's total."""
+    from collections import defaultdict
+
+    from torch.profiler import ProfilerActivity, profile
+
+    for fn in fns:
+        fn()
+    _sync()
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True) as p:
+        for fn in fns:
+            fn()
+        _sync()
+    agg, cnt = defaultdict(float), defaultdict(int)
+    for e in p.events():
+        if not e.name.startswith("aten::") or e.cpu_parent is not None and e.cpu_parent.name.startswith("aten::"):
+            continue
+        t = getattr(e, "device_time_total", None) or getattr(e, "cuda_time_total", 0)
+        if t <= 0:
+            continue
+        frames = [fr for fr in (e.stack or []) if "drynx_amd" in fr or "tools/" in fr]
+        key = (e.name, frames[0] if frames else "?")
+        agg[key] += t
+        cnt[key] += 1
+    with open(path, "w") as f:
+        f.write(p.key_averages().table(sort_by="cuda_time_total", row_limit=50, max_name_column_width=60))
+        f.write("\n\n# GPU time of torch ops by (op, innermost framework frame)\n")
+        for (name, fr), t in sorted(agg.items(), key=lambda kv: -kv[1])[:80]:
+            f.write(f"{t / 1e3:9.2f} ms {cnt[(name, fr)]:5d}  {name:28s} {fr}\n")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--world", type=int, default=8)
@@ -69,6 +101,9 @@ def main():
     ap.add_argument("--records", type=int, default=1_000_000)
     ap.add_argument("--serial-json", default=None, help="bench.py --u 0 --l 0 JSON (the non-range critical path)")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--torch-prof", default=None,
+                    help="also profile the 1-GPU pooled check of the whole inbox and the proving of every DP "
+                         "(torch.profiler on this thread): the GPU time of torch ops per framework frame")
     a = ap.parse_args()
     dev = torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
     if dev.type == "cuda":
@@ -137,6 +172,10 @@ def main():
             out.append(c)
         return out
 
+    if a.torch_prof:
+        _torch_glue(a.torch_prof, lambda: prq.verify_range_pool_part(
+            full_reqs(), {v: list(range(len(rng))) for v in vn_idxs}, sq, dev, cache, (0, 1),
+            {vn.id: Coins() for vn in cl.vns}), lambda: node._sign_range(sq, node._prove_range(sq, dp_results)))
     res = {"world": W, "features": d, "placement": {k: {"parties": place.get(k, []), "dps": dps_of[k]} for k in range(W)},
            "ranks": {}}
     for k in range(W):
