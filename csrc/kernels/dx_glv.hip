@@ -82,9 +82,59 @@ __global__ void __launch_bounds__(kWG) DX_OCC rp_points_glv_kernel(const uint32_
     at<G1A>(P_aff, it) = G1A{fmul(fmul(r.x, r.z), iy), fmul(fmul(fsqr(r.z), r.z), iy)};
   }
 }
+// out_i = (a_i + b_i lambda) P_i = a_i P_i + b_i phi(P_i) (Jacobian): the same
+// joint 2-bit-window ladder over 32-bit halves, for arbitrary points (the
+// key-switch / obfuscation batch checks' weighted rows).  p1: one point for all.
+__global__ void __launch_bounds__(kWG) DX_OCC g1_mul_glv_kernel(const uint32_t *__restrict__ P,
+                                                              const uint32_t *__restrict__ ab,
+                                                              const uint32_t *__restrict__ beta_m,
+                                                              uint32_t *__restrict__ out, int64_t n, int p1) {
+  const int64_t it = (int64_t)blockIdx.x * kWG + threadIdx.x;
+  if (it >= n) return;
+  const G1J T = at<G1J>(P, p1 ? 0 : it);
+  const uint32_t a = ab[2 * it], b = ab[2 * it + 1];
+  if (T.is_inf() || (a | b) == 0u) {
+    at<G1J>(out, it) = G1J::inf();
+    return;
+  }
+  G1J T2 = T;
+  g1_dbl_i(T2);
+  G1J T3 = T2;
+  g1_add_i(T3, T);
+  const Fp z12 = fmul(T.z, T2.z);
+  Fp inv = finv(fmul(z12, T3.z));
+  const Fp i3 = fmul(inv, z12);
+  inv = fmul(inv, T3.z);
+  const G1A A1 = affine_with(T, fmul(inv, T2.z)), A2 = affine_with(T2, fmul(inv, T.z)), A3 = affine_with(T3, i3);
+  const Fp beta = Fp::from_limbs(beta_m);
+  G1J r = G1J::inf();
+  for (int w = 15; w >= 0; w--) {
+    if (w != 15) {
+      g1_dbl_i(r);
+      g1_dbl_i(r);
+    }
+    const uint32_t da = (a >> (2 * w)) & 3u, db = (b >> (2 * w)) & 3u;
+    if (da) g1_madd_i(r, da == 1u ? A1 : (da == 2u ? A2 : A3));
+    if (db) {
+      G1A q = db == 1u ? A1 : (db == 2u ? A2 : A3);
+      q.x = fmul(q.x, beta);  // phi(q) = (beta x, y)
+      g1_madd_i(r, q);
+    }
+  }
+  at<G1J>(out, it) = r;
+}
 }  // namespace
 
 extern "C" {
+int dx_g1_mul_glv(void *stream, const uint32_t *P_jac, const uint32_t *ab, const uint32_t *beta_m, uint32_t *out,
+                  int64_t n, int p1) {
+  if (n <= 0) return 0;
+  const int64_t blocks = (n + kWG - 1) / kWG;
+  hipLaunchKernelGGL(g1_mul_glv_kernel, dim3((unsigned)blocks), dim3(kWG), 0, (hipStream_t)stream, P_jac, ab, beta_m,
+                     out, n, p1);
+  return check_hip(hipGetLastError(), "g1_mul_glv");
+}
+
 // uv = 1: the points as (x/y, 1/y) (fold mode 4) instead of affine (x, y)
 int dx_rp_points_glv(void *stream, const uint32_t *ZB_jac, const uint32_t *Y_jac, const uint32_t *ab,
                      const uint32_t *beta_m, uint32_t *P_aff, int64_t n, int S, int L, int uv) {

@@ -99,6 +99,7 @@ _SIGS = {
     "dx_rp_verify_fold": [_P, _P, _P, _P, _P, _P, _L, _I, _I],
     "dx_gt_slice_prod": [_I, _P, _P, _P, _P, _P, _P, _L],
     "dx_bucket_sort_tmp": [_L, _I, ctypes.POINTER(ctypes.c_uint64)],
+    "dx_g1_mul_glv": [_P, _P, _P, _P, _P, _L, _I],
     "dx_bucket_sort": [_I, _P, _P, _P, _P, _P, _L, _I, _P, ctypes.c_uint64],
     "dx_bucket_bounds": [_I, _P, _P, _L, _L, _P, _P],
     "dx_slice_plan": [_I, _P, _P, _P, _P, _I, _L, _P, _P],
@@ -1191,6 +1192,29 @@ def glv_weights(n: int, device, raw: torch.Tensor | None = None):
     b[:, 0] = ab[:, 1]
     rho = fr_arith(FR_ADD, a, fr_arith(FR_MUL, b, _glv_const("lambda", device)))
     return ab, rho
+
+
+def g1_mul_glv(pts_jac: torch.Tensor, ab: torch.Tensor) -> torch.Tensor:
+    """(a_i + b_i GLV_LAMBDA) P_i for 32-bit halves ab [n, 2] (``glv_weights``)
+    -> Jacobian [n, 24]: 32 doublings of a joint 2-bit-window ladder over
+    (P, phi(P)) instead of 64 (csrc/kernels/dx_glv.hip).  GPU; on the host
+    the full scalars go through ``g1_mul``."""
+    n = _rows(ab, 2)
+    np_ = _rows(pts_jac, 24)
+    assert np_ in (1, n)
+    if not ab.is_cuda:
+        a = torch.zeros((n, 8), dtype=torch.int32)
+        b = torch.zeros((n, 8), dtype=torch.int32)
+        a[:, 0], b[:, 0] = ab[:, 0], ab[:, 1]
+        rho = fr_arith(FR_ADD, a, fr_arith(FR_MUL, b, _glv_const("lambda", "cpu")))
+        return g1_mul(pts_jac, rho)
+    out = torch.empty((n, 24), dtype=torch.int32, device=ab.device)
+    _, s = _ctx(pts_jac, ab)
+    rc = _raw_call("dx_g1_mul_glv", s, _ptr(pts_jac.contiguous()), _ptr(ab.contiguous()),
+                   _ptr(_glv_const("beta", ab.device)), _ptr(out), n, int(np_ == 1 and n > 1))
+    if rc:
+        raise RuntimeError(f"dx_g1_mul_glv failed rc={rc}")
+    return out
 
 
 def rp_fold_points_glv(ZB_jac: torch.Tensor, Y_jac: torch.Tensor, ab: torch.Tensor, S: int, L: int,

@@ -685,16 +685,27 @@ def _ks_combined(live, n_vn: int = 1, coins=None):
     sel = np.concatenate([(0 if gi < 2 else kt) + offs[j] + np.arange(k) for j, k in enumerate(ks) for gi in range(5)])
     grp1 = np.concatenate([np.full(k, 5 * j + gi) for j, k in enumerate(ks) for gi in range(5)])
     za = torch.cat([pr.za[:k] for _, pr, k in live]).contiguous()
-    W = torch.cat([_rand64(2 * kt, dev, c) for c in cl])                      # [n_vn * 2kt, 8]
-    scs = W.view(n_vn, 2 * kt, 8).index_select(1, torch.from_numpy(sel).to(dev)).reshape(-1, 8).contiguous()
+    sel_t = torch.from_numpy(sel).to(dev)
+    glv = dev.type == "cuda" and len(set(ks)) == 1
+    if glv:
+        # GLV weights rho = a + b lambda (a, b 32-bit: 2^64 distinct residues,
+        # the same 2^-64 soundness as uniform 64-bit weights): the weighted
+        # points take a 32-doubling joint ladder over (P, phi(P))
+        pairs = [c.glv(2 * kt, dev) if c is not None else nt.glv_weights(2 * kt, dev) for c in cl]
+        AB = torch.cat([p_[0] for p_ in pairs])                               # [n_vn * 2kt, 2]
+        W = torch.cat([p_[1] for p_ in pairs])                                # [n_vn * 2kt, 8]
+    else:
+        W = torch.cat([_rand64(2 * kt, dev, c) for c in cl])                  # [n_vn * 2kt, 8]
+        scs = W.view(n_vn, 2 * kt, 8).index_select(1, sel_t).reshape(-1, 8).contiguous()
     full = nt.fr_dot_rows(W, za, 2 * n_vn, b_periodic=True)                  # [sum rho za, sum sig za] per VN
-    if dev.type == "cuda" and len(set(ks)) == 1:
+    if glv:
         # equal-length proofs (the CNs switch the same K): every weighted point
-        # by one 64-bit variable-base launch (leading zero windows skipped) and
-        # the 5 nl n_vn group sums by a chunked tree -- no bucket plan and its
-        # host sync; group sums and za dots come back in ONE copy
+        # by one GLV variable-base launch and the 5 nl n_vn group sums by a
+        # chunked tree -- no bucket plan and its host sync; group sums and za
+        # dots come back in ONE copy
         k0 = ks[0]
-        prod = nt.g1_mul(pts.contiguous().repeat(n_vn, 1), scs).view(5 * nl * n_vn, k0, 24)
+        abs_ = AB.view(n_vn, 2 * kt, 2).index_select(1, sel_t).reshape(-1, 2).contiguous()
+        prod = nt.g1_mul_glv(pts.contiguous().repeat(n_vn, 1), abs_).view(5 * nl * n_vn, k0, 24)
         sums = nt.g1_sum(prod.transpose(0, 1).contiguous())
         both = torch.cat([sums.reshape(-1), full.reshape(-1)]).cpu()
         G = both[: sums.numel()].view(-1, 24)

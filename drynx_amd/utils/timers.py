@@ -34,16 +34,31 @@ def _emit(name: str, t0_ns: int, t1_ns: int):
                         "dur": (t1_ns - t0_ns) / 1e3})
 
 
+# DRYNX_SPAN_SYNC=1 (diagnostics, with DRYNX_TRACE): every span synchronises
+# the device on entry and exit, so its duration is its own host + GPU cost
+# with nothing overlapping (a serialized cost breakdown of a code path)
+_SPAN_SYNC = os.environ.get("DRYNX_SPAN_SYNC") == "1"
+
+
+def _dev_sync():
+    if torch.cuda.is_available() and torch.cuda.is_initialized():
+        torch.cuda.synchronize()
+
+
 @contextlib.contextmanager
 def span(name: str):
     """A no-sync traced region (free when DRYNX_TRACE is unset)."""
     if not _TRACE:
         yield
         return
+    if _SPAN_SYNC:
+        _dev_sync()
     t0 = time.perf_counter_ns()
     try:
         yield
     finally:
+        if _SPAN_SYNC:
+            _dev_sync()
         _emit(name, t0, time.perf_counter_ns())
 
 

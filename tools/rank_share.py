@@ -176,6 +176,18 @@ def main():
         _torch_glue(a.torch_prof, lambda: prq.verify_range_pool_part(
             full_reqs(), {v: list(range(len(rng))) for v in vn_idxs}, sq, dev, cache, (0, 1),
             {vn.id: Coins() for vn in cl.vns}), lambda: node._sign_range(sq, node._prove_range(sq, dp_results)))
+    if os.environ.get("DRYNX_TRACE"):
+        # a span trace of rank 3's (a VN rank) and rank 6's (a helper) pool share alone
+        from drynx_amd.utils import timers
+
+        timers._events.clear()
+        for k in (3, 6):
+            reqs_k = full_reqs() if k in vn_ranks else helper_reqs((k, W))
+            with timers.span(f"pool_part[{k}]"):
+                prq.verify_range_pool_part(reqs_k, {v: list(range(len(rng))) for v in vn_idxs}, sq, dev, cache,
+                                           (k, W), {vn.id: Coins() for vn in cl.vns})
+            _sync()
+        timers.dump_trace(os.environ["DRYNX_TRACE"])
     res = {"world": W, "features": d, "placement": {k: {"parties": place.get(k, []), "dps": dps_of[k]} for k in range(W)},
            "ranks": {}}
     for k in range(W):
