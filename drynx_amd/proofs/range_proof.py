@@ -916,20 +916,24 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
         # every bucket plan (one host sync each) first, then every pass: a sync
         # never waits behind another plan's heavy passes
         if use_msm and aux is not None:
-            hR = _msm_plan(r.zphi, r.V, rho_all, G, n, S, l)
+            with timers.span("rp.plan.R"):
+                hR = _msm_plan(r.zphi, r.V, rho_all, G, n, S, l)
         dpts = torch.cat([Cp.contiguous(), r.D.contiguous()]).repeat(G, 1)
         wc = nt.fr_arith(nt.FR_MUL, w_all, r.challenge.repeat(G, 1))
         dsc = torch.stack([wc.view(G, n, 8), w_all.view(G, n, 8)], 1).reshape(-1, 8).contiguous()
-        if fold > 1:  # group = ((v, which) row // n, segment of the proof)
-            dgrp = (torch.arange(2 * G, device=device).view(-1, 1) * fold + pseg.view(1, n)).reshape(-1).to(torch.int32)
-            dplan = nt.g1_msm_plan(dsc, dgrp, 2 * G * fold)
-        else:
-            dgrp = n
-            dplan = nt.g1_msm_plan(dsc, n, 2 * G)                         # group = row // n
+        with timers.span("rp.plan.D"):
+            if fold > 1:  # group = ((v, which) row // n, segment of the proof)
+                dgrp = (torch.arange(2 * G, device=device).view(-1, 1) * fold
+                        + pseg.view(1, n)).reshape(-1).to(torch.int32)
+                dplan = nt.g1_msm_plan(dsc, dgrp, 2 * G * fold)
+            else:
+                dgrp = n
+                dplan = nt.g1_msm_plan(dsc, n, 2 * G)                     # group = row // n
         # groups 0..G-1: prod a^rho_v; groups G..2G-1: each VN's own GT-membership
         # combination prod a^gamma_v
         # prod a^rho = prod a^a' * frob^8(a)^b': 32-bit exponents over (A, frob^8 A)
-        A2 = torch.cat([r.A, nt.gt_frob8(r.A)])
+        with timers.span("rp.frob8"):
+            A2 = torch.cat([r.A, nt.gt_frob8(r.A)])
         k = torch.zeros((2 * G, 2 * m, 8), dtype=torch.int32, device=device)
         abv = ab_all.view(G, m, 2)
         k[:G, :m, 0] = abv[:, :, 0]
@@ -939,17 +943,23 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
         # host: bytes (fewer buckets for the host's serial bucket products)
         wc_ = (4, 11) if device.type == "cuda" else (5, 8)
         k = k.view(-1, 8)
-        if fold > 1:  # group = (row // 2m, segment of the item)
-            mgrp = (torch.arange(2 * G, device=device).view(-1, 1) * fold
-                    + iseg.repeat(2).view(1, 2 * m)).reshape(-1).to(torch.int32)
-            mplan = nt.multi_exp_plan(k, mgrp, 2 * G * fold, W=wc_[0], c=wc_[1])
-            mexp = nt.multi_exp_grouped(A2, k, mgrp, 2 * G * fold, W=wc_[0], c=wc_[1], plan=mplan, fold=fold)
-        else:
-            mplan = nt.multi_exp_plan(k, 2 * m, 2 * G, W=wc_[0], c=wc_[1])      # group = row // 2m
-            mexp = nt.multi_exp_grouped(A2, k, 2 * m, 2 * G, W=wc_[0], c=wc_[1], plan=mplan)
+        with timers.span("rp.plan.ME"):
+            if fold > 1:  # group = (row // 2m, segment of the item)
+                mgrp = (torch.arange(2 * G, device=device).view(-1, 1) * fold
+                        + iseg.repeat(2).view(1, 2 * m)).reshape(-1).to(torch.int32)
+                mplan = nt.multi_exp_plan(k, mgrp, 2 * G * fold, W=wc_[0], c=wc_[1])
+            else:
+                mplan = nt.multi_exp_plan(k, 2 * m, 2 * G, W=wc_[0], c=wc_[1])  # group = row // 2m
+        with timers.span("rp.run.ME"):
+            if fold > 1:
+                mexp = nt.multi_exp_grouped(A2, k, mgrp, 2 * G * fold, W=wc_[0], c=wc_[1], plan=mplan, fold=fold)
+            else:
+                mexp = nt.multi_exp_grouped(A2, k, 2 * m, 2 * G, W=wc_[0], c=wc_[1], plan=mplan)
         if use_msm and aux is not None:
-            S_R = nt.g2_msm_run(r.V, hR)                               # R window sums
-        dcheck = nt.g1_msm_launch(dpts, dsc, dgrp, 2 * G * fold, bits=256, plan=dplan, fold=fold)
+            with timers.span("rp.run.R"):
+                S_R = nt.g2_msm_run(r.V, hR)                           # R window sums
+        with timers.span("rp.run.D"):
+            dcheck = nt.g1_msm_launch(dpts, dsc, dgrp, 2 * G * fold, bits=256, plan=dplan, fold=fold)
         e_all = nt.fr_dot_rows(rho_all, r.zv, G, b_periodic=True)                        # sum rho Zv per VN
         dfull = torch.stack([nt.fr_dot_rows(w_all, r.zr, G, b_periodic=True),
                              nt.fr_dot_rows(w_all, z, G, b_periodic=True)], 1)             # [G, 2, 8]
@@ -1091,7 +1101,8 @@ def _msm_queue(Y, V, ab_all, G: int, n: int, S: int, L: int, vstream=None, segs:
     nseg = len(segs) if segs else 1
     qoff = np.cumsum([0] + [c * S for c in segs]) if segs else np.array([0, nq])
     cq = np.diff(qoff)
-    table = nt.g2_joint_table(V)
+    with timers.span("rp.u.joint_table"):
+        table = nt.g2_joint_table(V)
     out = {"G": G}
     if dev.type == "cuda":
         if nseg == 1:
@@ -1108,12 +1119,14 @@ def _msm_queue(Y, V, ab_all, G: int, n: int, S: int, L: int, vstream=None, segs:
         Uall = torch.zeros((G * pad, 32), dtype=torch.int32, device=dev)
         UV = torch.zeros((period, 16), dtype=torch.int32, device=dev)
         if nseg == 1:
-            nt.rp_u_joint(table, ab_all, nq, G, L, Uall, pad)
+            with timers.span("rp.u.joint"):
+                nt.rp_u_joint(table, ab_all, nq, G, L, Uall, pad)
             nt.rp_msm_uv(Y, UV, nq, G, pad)
             Ud = Uall
         else:
             Ud = torch.empty((G * nq, 32), dtype=torch.int32, device=dev)
-            nt.rp_u_joint(table, ab_all, nq, G, L, Ud, nq)
+            with timers.span("rp.u.joint"):
+                nt.rp_u_joint(table, ab_all, nq, G, L, Ud, nq)
             UVd = torch.zeros((G * (nq + 1), 16), dtype=torch.int32, device=dev)
             nt.rp_msm_uv(Y, UVd, nq, G, nq + 1)
             qseg = torch.repeat_interleave(torch.arange(nseg, device=dev), _h2d(cq, dev),
@@ -1134,7 +1147,8 @@ def _msm_queue(Y, V, ab_all, G: int, n: int, S: int, L: int, vstream=None, segs:
             out["u_seg"] = _seg_all(fl, cq, dev)
             out["u_ok"] = list(out["u_seg"].all(dim=1).unbind(0))
         Ud.record_stream(vs)
-        out["fb"] = nt.rp_fold_accum_n(nt.rp_fold_ncoeffs(Uall), UV, Uall, period, 1, K)
+        with timers.span("rp.u.fold"):
+            out["fb"] = nt.rp_fold_accum_n(nt.rp_fold_ncoeffs(Uall), UV, Uall, period, 1, K)
         out["blk"] = pad // rows
         out["sb"] = [0] if nseg == 1 else (segbase // rows).tolist()
         out["nb"] = [pad // rows] if nseg == 1 else (ac // rows).tolist()

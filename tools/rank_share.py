@@ -183,11 +183,16 @@ def main():
         timers._events.clear()
         for k in (3, 6):
             reqs_k = full_reqs() if k in vn_ranks else helper_reqs((k, W))
+            _sync()
+            time.sleep(1.0)  # an idle gap: a kernel trace shows this part as its own burst (tools/kernel_bursts.py)
             with timers.span(f"pool_part[{k}]"):
                 prq.verify_range_pool_part(reqs_k, {v: list(range(len(rng))) for v in vn_idxs}, sq, dev, cache,
                                            (k, W), {vn.id: Coins() for vn in cl.vns})
             _sync()
         timers.dump_trace(os.environ["DRYNX_TRACE"])
+        if os.environ.get("RANK_SHARE_TRACE_ONLY") == "1":
+            node.close(remove=True)
+            return
     res = {"world": W, "features": d, "placement": {k: {"parties": place.get(k, []), "dps": dps_of[k]} for k in range(W)},
            "ranks": {}}
     for k in range(W):
