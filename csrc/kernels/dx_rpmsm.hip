@@ -102,6 +102,42 @@ DX_HD void u_joint_one(const uint32_t *T_aff, const uint32_t *ab, uint32_t *U_af
   at<G2A>(U_aff, v * pad + q) = to_affine(acc);
 }
 
+// The same combination split over sp threads per (v, q) (small batches: a
+// pool helper's 1/W slice gives too few (v, q) to fill 256 CUs): part p sums
+// digits [p L/sp, (p+1) L/sp) into a Jacobian partial; u_joint_reduce_one adds
+// the sp partials and normalises.
+DX_HD void u_joint_part_one(const uint32_t *T_aff, const uint32_t *ab, uint32_t *P_jac, int64_t n_groups, int L,
+                            int sp, int64_t t) {
+  const int64_t m = n_groups * L;
+  const int part = (int)(t % sp);
+  const int64_t vq = t / sp;
+  const int64_t v = vq / n_groups, q = vq % n_groups;
+  const int per = (L + sp - 1) / sp;
+  const int j0 = part * per, j1 = j0 + per < L ? j0 + per : L;
+  const G2A *T = reinterpret_cast<const G2A *>(T_aff) + q * L * kT;
+  const uint32_t *w = ab + 2 * (v * m + q * L);
+  G2J acc = G2J::inf();
+  for (int win = 15; win >= 0; win--) {
+    if (win != 15) {
+      acc = jdbl(acc);
+      acc = jdbl(acc);
+    }
+    for (int j = j0; j < j1; j++) {
+      const uint32_t e = ((w[2 * j] >> (2 * win)) & 3u) + 4u * ((w[2 * j + 1] >> (2 * win)) & 3u);
+      if (e) acc = jadd_mixed(acc, T[j * kT + e - 1]);
+    }
+  }
+  at<G2J>(P_jac, t) = acc;
+}
+
+DX_HD void u_joint_reduce_one(const uint32_t *P_jac, uint32_t *U_aff, int64_t n_groups, int sp, int64_t pad,
+                              int64_t vq) {
+  const int64_t v = vq / n_groups, q = vq % n_groups;
+  G2J acc = at<G2J>(P_jac, vq * sp);
+  for (int p = 1; p < sp; p++) acc = jadd(acc, at<G2J>(P_jac, vq * sp + p));
+  at<G2A>(U_aff, v * pad + q) = to_affine(acc);
+}
+
 DX_HD void slice_sum_one(const uint32_t *src, const int32_t *idx, const int64_t *start, const int32_t *len,
                          uint32_t *out, int src_aff, int64_t idx_mod, int64_t s) {
   const int64_t b = start[s];
@@ -222,6 +258,17 @@ __global__ void __launch_bounds__(kWG) DX_OCC u_joint_kernel(const uint32_t *T, 
   DX_TID();
   if (i < n) u_joint_one(T, ab, U, n_groups, L, pad, i);
 }
+__global__ void __launch_bounds__(kWG) DX_OCC u_joint_part_kernel(const uint32_t *T, const uint32_t *ab,
+                                                                 uint32_t *P, int64_t n_groups, int L, int sp,
+                                                                 int64_t n) {
+  DX_TID();
+  if (i < n) u_joint_part_one(T, ab, P, n_groups, L, sp, i);
+}
+__global__ void __launch_bounds__(kWG) DX_OCC u_joint_reduce_kernel(const uint32_t *P, uint32_t *U, int64_t n_groups,
+                                                                   int sp, int64_t pad, int64_t n) {
+  DX_TID();
+  if (i < n) u_joint_reduce_one(P, U, n_groups, sp, pad, i);
+}
 __global__ void __launch_bounds__(kWG) DX_OCC slice_sum_kernel(const uint32_t *src, const int32_t *idx,
                                                               const int64_t *start, const int32_t *len,
                                                               uint32_t *out, int src_aff, int64_t idx_mod,
@@ -293,6 +340,23 @@ int dx_rp_u_joint(int on_gpu, void *stream, const uint32_t *T_aff, const uint32_
   hipLaunchKernelGGL(u_joint_kernel, grid_of(n), dim3(kWG), 0, (hipStream_t)stream, T_aff, ab, U_aff, n_groups, L,
                      pad, n);
   return check_hip(hipGetLastError(), "rp_u_joint");
+}
+
+// dx_rp_u_joint with each (v, q) split over sp threads (tmp: G * n_groups * sp Jacobian rows)
+int dx_rp_u_joint_split(int on_gpu, void *stream, const uint32_t *T_aff, const uint32_t *ab, uint32_t *U_aff,
+                        int64_t n_groups, int G, int L, int64_t pad, int sp, uint32_t *tmp) {
+  const int64_t n = (int64_t)G * n_groups;
+  if (n <= 0) return 0;
+  if (!on_gpu) {
+    host_for_each(n * sp, [=](int64_t t) { u_joint_part_one(T_aff, ab, tmp, n_groups, L, sp, t); });
+    host_for_each(n, [=](int64_t t) { u_joint_reduce_one(tmp, U_aff, n_groups, sp, pad, t); });
+    return 0;
+  }
+  hipLaunchKernelGGL(u_joint_part_kernel, grid_of(n * sp), dim3(kWG), 0, (hipStream_t)stream, T_aff, ab, tmp,
+                     n_groups, L, sp, n * sp);
+  hipLaunchKernelGGL(u_joint_reduce_kernel, grid_of(n), dim3(kWG), 0, (hipStream_t)stream, tmp, U_aff, n_groups, sp,
+                     pad, n);
+  return check_hip(hipGetLastError(), "rp_u_joint_split");
 }
 
 // out[s] = sum_{k < len[s]} src[e_k], e_k = idx[start[s] + k] (mod idx_mod when

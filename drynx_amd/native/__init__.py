@@ -100,6 +100,7 @@ _SIGS = {
     "dx_gt_slice_prod": [_I, _P, _P, _P, _P, _P, _P, _L],
     "dx_bucket_sort_tmp": [_L, _I, ctypes.POINTER(ctypes.c_uint64)],
     "dx_g1_mul_glv": [_P, _P, _P, _P, _P, _L, _I],
+    "dx_rp_u_joint_split": [_I, _P, _P, _P, _P, _L, _I, _I, _L, _I, _P],
     "dx_bucket_sort": [_I, _P, _P, _P, _P, _P, _L, _I, _P, ctypes.c_uint64],
     "dx_bucket_bounds": [_I, _P, _P, _L, _L, _P, _P],
     "dx_slice_plan": [_I, _P, _P, _P, _P, _I, _L, _P, _P],
@@ -1367,6 +1368,11 @@ def _sort_buckets(keys: torch.Tensor, items: torch.Tensor, nb: int):
     on the host: the plan's one device-to-host copy)."""
     dev = keys.device
     n = keys.numel()
+    if os.environ.get("DRYNX_PLAN_SORT") == "torch":  # A/B: torch's sort + searchsorted
+        keys, order = torch.sort(keys)
+        items = items.index_select(0, order)
+        offs = torch.searchsorted(keys, torch.arange(nb + 1, device=dev, dtype=torch.int32))
+        return items, (offs[1:] - offs[:-1]).cpu().numpy()
     end_bit = max(1, int(nb).bit_length())
     k2 = torch.empty_like(keys)
     i2 = torch.empty_like(items)
@@ -1381,8 +1387,8 @@ def _sort_buckets(keys: torch.Tensor, items: torch.Tensor, nb: int):
     _call("dx_bucket_sort", g, s, _ptr(keys), _ptr(items), _ptr(k2), _ptr(i2), n, end_bit, _ptr(tmp), tb.value)
     bounds = torch.zeros((2, nb), dtype=torch.int64, device=dev)
     _call("dx_bucket_bounds", g, s, _ptr(k2), n, nb, _ptr(bounds[0]), _ptr(bounds[1]))
-    fe = bounds.cpu().numpy()                                           # the one host sync
-    return i2, fe[1] - fe[0]
+    counts = (bounds[1] - bounds[0]).to(torch.int32).cpu().numpy()      # the one host sync
+    return i2, counts.astype(np.int64)
 
 
 def _segment_passes_dev(counts, dev, first_slice: int | None = None):
@@ -1466,7 +1472,7 @@ def _bucket_plan(k: torch.Tensor, W: int, group: torch.Tensor | None = None, n_g
           _ptr(item))
     item, counts = _sort_buckets(keys, item, nb)   # zero digits carry a sentinel key that sorts last
     item = item[: int(counts.sum())].to(torch.int64)                    # drop the zero-digit sentinels
-    bk = counts.nonzero()[0]
+    bk = np.flatnonzero(counts)
     passes = _segment_passes_dev(counts[bk], dev)
     # bucket digits and scatter slots, staged now so the run needs no host->device copy
     mask = (1 << c) - 1
@@ -1786,6 +1792,16 @@ def rp_u_joint(table: torch.Tensor, ab: torch.Tensor, n_groups: int, G: int, L: 
     assert _rows(table, 32) == n_groups * L * G2_JOINT_ENTRIES and _rows(ab, 2) == G * n_groups * L
     assert _rows(out, 32) >= (G - 1) * pad + n_groups and pad >= n_groups and out.is_contiguous()
     g, s = _ctx(table, ab, out)
+    # a small batch (a pool helper's 1/W slice) splits each combination over
+    # 2 or 4 threads so the launch still fills the chip (~2 waves per SIMD)
+    n = G * n_groups
+    sp = 1 if (not g or n >= 131072) else (2 if n >= 65536 else 4)
+    sp = min(sp, L)
+    if sp > 1:
+        tmp = torch.empty((n * sp, 48), dtype=torch.int32, device=out.device)
+        _call("dx_rp_u_joint_split", g, s, _ptr(table), _ptr(ab.contiguous()), _ptr(out), n_groups, G, L, pad, sp,
+              _ptr(tmp))
+        return out
     _call("dx_rp_u_joint", g, s, _ptr(table), _ptr(ab.contiguous()), _ptr(out), n_groups, G, L, pad)
     return out
 
@@ -1852,7 +1868,7 @@ def g2_msm_launch(P_aff: torch.Tensor, k: torch.Tensor, group: torch.Tensor | No
     g, s = _ctx(k, keys)
     _call("dx_msm_keys", g, s, _ptr(k.contiguous()), _ptr(grp), gstride, n, c, W, _ptr(keys), _ptr(items))
     items, counts = _sort_buckets(keys, items, nb)                      # the one host sync
-    bk = counts.nonzero()[0]
+    bk = np.flatnonzero(counts)
     h = {"G": n_groups, "W": W, "c": c, "m": m, "bk": bk, "item": items[: int(counts.sum())]}
     if bk.size:
         passes = _segment_passes_dev(counts[bk], dev, first_slice)
@@ -1872,7 +1888,9 @@ def _g2_weight_plan(bk, c: int, dev) -> dict:
     ck = gw * ((1 << c) // G2_CHUNK + 1) + dig // G2_CHUNK
     first = np.flatnonzero(np.r_[True, ck[1:] != ck[:-1]])
     clen = np.diff(np.r_[first, bk.size])
-    gws, gcounts = np.unique(gw[first], return_counts=True)
+    gwf = gw[first]                                  # sorted: run lengths instead of np.unique's sort
+    gstart = np.flatnonzero(np.r_[True, gwf[1:] != gwf[:-1]])
+    gws, gcounts = gwf[gstart], np.diff(np.r_[gstart, gwf.size])
     return {"d": _upload(dig.astype("int32"), dev),
             "chunks": (_upload(first.astype(np.int64), dev), _upload(clen.astype(np.int32), dev),
                        _upload(((dig[first] // G2_CHUNK) * G2_CHUNK).astype(np.int32), dev)),

@@ -1079,7 +1079,16 @@ def _msm_plan(zphi, V, rho_all, G: int, n: int, S: int, L: int) -> dict:
     it = torch.arange(m, device=dev)
     zi = (it // (S * L)) * L + it % L
     s_r = nt.fr_arith(nt.FR_MUL, rho_all, zphi.index_select(0, zi).repeat(G, 1).contiguous())
-    return nt.g2_msm_launch(V, s_r, m, G)                              # group (VN) = row // m
+    return nt.g2_msm_launch(V, s_r, m, G, c=_r_window(m, G))          # group (VN) = row // m
+
+
+def _r_window(m: int, G: int) -> int:
+    """Window bits of the R MSM: ~(bucket additions per entry) x entries +
+    (weight and window-sum additions per bucket) x buckets, over 254-bit
+    scalars -- 13 bits for a 1-GPU inbox (1M items per VN), ~11 for a pool
+    helper's 1/8 slice (a fixed 13-bit plan would weigh 491k mostly-empty
+    buckets there)."""
+    return min(range(8, 14), key=lambda c: -(-254 // c) * (m + 8 * (1 << c)))
 
 
 def _msm_queue(Y, V, ab_all, G: int, n: int, S: int, L: int, vstream=None, segs: list | None = None) -> dict:
