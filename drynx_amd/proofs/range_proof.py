@@ -880,7 +880,8 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
     ab_all = torch.cat([p_[0] for p_ in pairs]) if G > 1 else pairs[0][0]
     rho_all = torch.cat([p_[1] for p_ in pairs]) if G > 1 else pairs[0][1]
     # GT-membership combinations: one independent 40-bit gamma set PER VN
-    gam_all = _cat_draw(lambda c: c.bits(m, device, 40) if c is not None else _rand64(m, device, 40))
+    gb = int(os.environ.get("DRYNX_GAMMA_BITS", "40"))  # A/B diagnostics only: below 39 bits is unsound
+    gam_all = _cat_draw(lambda c: c.bits(m, device, gb) if c is not None else _rand64(m, device, gb))
     vns = [{"rho": rho_all[v * m:(v + 1) * m], "ab": ab_all[v * m:(v + 1) * m]} for v in range(G)]
     # attribution: the bucket methods group every entry by (VN, segment) and
     # sum / multiply the buckets over the segments before weighting them, so

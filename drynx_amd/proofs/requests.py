@@ -387,6 +387,25 @@ def prewarm_keyswitch(reqs: list, sq, vn_ids: list, device, cache: "VerifierCach
         cache.ks_pre.pop(next(iter(cache.ks_pre)))
 
 
+def prewarm_signatures(reqs: list, sq, vn_ids: list, cache: "VerifierCache"):
+    """Every co-hosted VN's own Schnorr checks of the inbox's envelopes in ONE
+    host-pool batch (each VN's copy of every check is computed; the batch
+    only spreads them over the cores together); ``verify_requests`` reads its
+    VN's verdicts from ``cache.sig_pre``."""
+    if len(vn_ids) < 2 or not reqs:
+        return
+    with timers.span("verify.digests"):
+        prefetch_digests(reqs)
+    keys = [(sq.IDtoPublic.get(r.sender_id), r.digest(), r.signature) for r in reqs]
+    with timers.span(f"verify.signature.multi[{len(vn_ids)}]"):
+        ok = sigma.schnorr_verify_batch(keys * len(vn_ids), "cpu")
+    n = len(reqs)
+    for j, vn_id in enumerate(vn_ids):
+        cache.sig_pre[(sq.SurveyID, vn_id)] = (n, ok[j * n:(j + 1) * n])
+    while len(cache.sig_pre) > 64:
+        cache.sig_pre.pop(next(iter(cache.sig_pre)))
+
+
 def should_verify(sq, req: ProofRequest, vn_index: int, n_vns: int, coins=None) -> bool:
     """The VN's sampling decision: ``rand.Float64() <= Threshold`` from the
     VN's own coins (structs_proofs.go:160-161), or the sharding extension."""
@@ -403,6 +422,7 @@ class VerifierCache:
     def __init__(self):
         self._sig = {}
         self.ks_pre: dict = {}  # (SurveyID, vn_id) -> {request index: bool} (prewarm_keyswitch)
+        self.sig_pre: dict = {}  # (SurveyID, vn_id) -> (n requests, [bool]) (prewarm_signatures)
 
     def sigmat(self, sq, device):
         """Keyed by a digest of the signature set, so repeated surveys over the
@@ -891,11 +911,15 @@ def verify_requests(reqs: list, sq, vn_id: str, vn_index: int, n_vns: int, devic
     codes = [None] * len(reqs)
     todo: dict = {}
     pooled_idx: list = []
-    with timers.span("verify.digests"):
-        prefetch_digests(reqs)
-    keys = [(sq.IDtoPublic.get(r.sender_id), r.digest(), r.signature) for r in reqs]
-    with timers.span("verify.signature.batch"):
-        sigs_ok = sigma.schnorr_verify_batch(keys, device) if reqs else []
+    pre = cache.sig_pre.pop((sq.SurveyID, vn_id), None)
+    if pre is not None and pre[0] == len(reqs):
+        sigs_ok = pre[1]
+    else:
+        with timers.span("verify.digests"):
+            prefetch_digests(reqs)
+        keys = [(sq.IDtoPublic.get(r.sender_id), r.digest(), r.signature) for r in reqs]
+        with timers.span("verify.signature.batch"):
+            sigs_ok = sigma.schnorr_verify_batch(keys, device) if reqs else []
     for i, req in enumerate(reqs):
         if not sigs_ok[i]:
             codes[i] = PROOF_FALSE_SIGN

@@ -368,6 +368,8 @@ def proof_collection(ctx, sq, local_requests: list, early: dict | None = None):
         else:
             pooled = _pool_async(ctx, sq, reqs, vns) if pool else None
         local_vns = [vn.id for vn in vns if vn.rank == ctx.rank]
+        if len(local_vns) > 1:  # co-hosted VNs: their signature checks in one host batch
+            prq.prewarm_signatures(reqs, sq, local_vns, ctx.verifier_cache)
         if len(local_vns) > 1:  # co-hosted VNs: one grouped key-switch MSM for all of them
             with timers.span("verify.keyswitch.multi"):
                 prq.prewarm_keyswitch(reqs, sq, local_vns, ctx.device, ctx.verifier_cache,
