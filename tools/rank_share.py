@@ -181,7 +181,7 @@ def main():
         from drynx_amd.utils import timers
 
         timers._events.clear()
-        for k in (3, 6):
+        for k in [int(x) for x in os.environ.get("RANK_SHARE_PARTS", "3,6").split(",")]:
             reqs_k = full_reqs() if k in vn_ranks else helper_reqs((k, W))
             _sync()
             time.sleep(1.0)  # an idle gap: a kernel trace shows this part as its own burst (tools/kernel_bursts.py)
