@@ -349,18 +349,20 @@ def early_plane_ok(ctx, sq) -> bool:
         and use_pool(ctx) and os.environ.get("DRYNX_RANGE_PLANE", "1") != "0"
 
 
-def proof_collection(ctx, sq, local_requests: list, early: dict | None = None):
+def proof_collection(ctx, sq, local_requests: list, early: dict | None = None, late=None):
     """Returns the new SkipBlock (on every rank).  ``early``: the range plane
     started by ``start_range_plane`` (its requests and pooled verdicts);
-    ``local_requests`` then holds the remaining (per-CN) proofs."""
+    ``local_requests`` then holds the remaining (per-CN) proofs.  ``late``: a
+    callable returning the proofs still being finished (the key-switch proofs
+    of the last CN phase): the VNs check everything else first, then fan out
+    and check these -- as the reference's VNs verify each proof as it arrives
+    (proof_collection_protocol.go:183-305) -- and store one bitmap."""
     vns = [ctx.cluster.by_id(si.id) for si in sq.Query.RosterVNs.list]
     pool = use_pool(ctx)
     with timers.timed("ProofFanOut"):
         reqs = fan_out(ctx, sq, local_requests, pool=pool and early is None)
     if early is not None:
         reqs = early["reqs"] + reqs
-    if getattr(ctx, "net", None) is not None:
-        _net_proofs(ctx, sq, reqs, vns)
     bitmaps = {}
     with timers.timed("ProofVerification"):
         if early is not None:
@@ -368,19 +370,33 @@ def proof_collection(ctx, sq, local_requests: list, early: dict | None = None):
         else:
             pooled = _pool_async(ctx, sq, reqs, vns) if pool else None
         local_vns = [vn.id for vn in vns if vn.rank == ctx.rank]
-        if len(local_vns) > 1:  # co-hosted VNs: their signature checks in one host batch
-            prq.prewarm_signatures(reqs, sq, local_vns, ctx.verifier_cache)
-        if len(local_vns) > 1:  # co-hosted VNs: one grouped key-switch MSM for all of them
-            with timers.span("verify.keyswitch.multi"):
-                prq.prewarm_keyswitch(reqs, sq, local_vns, ctx.device, ctx.verifier_cache,
-                                      {v: ctx.vn_coins(v) for v in local_vns})
-        pending = {vn.id: check_requests(ctx, sq, vn, idx, len(vns), reqs, pooled)
-                   for idx, vn in enumerate(vns) if vn.rank == ctx.rank}
+
+        def checks(rs, range_pooled):
+            if len(local_vns) > 1:  # co-hosted VNs: their signature checks in one host batch
+                prq.prewarm_signatures(rs, sq, local_vns, ctx.verifier_cache)
+                with timers.span("verify.keyswitch.multi"):  # one grouped key-switch MSM for all of them
+                    prq.prewarm_keyswitch(rs, sq, local_vns, ctx.device, ctx.verifier_cache,
+                                          {v: ctx.vn_coins(v) for v in local_vns})
+            return {vn.id: check_requests(ctx, sq, vn, idx, len(vns), rs, range_pooled)
+                    for idx, vn in enumerate(vns) if vn.rank == ctx.rank}
+
+        pending = checks(reqs, pooled)
+        reqs2, pending2 = [], {}
+        if late is not None:
+            with timers.timed("ProofFanOut"):
+                reqs2 = fan_out(ctx, sq, late(), pool=False)
+            pending2 = checks(reqs2, None)
         for vn in vns:
             if vn.id in pending:
-                bitmaps[vn.id] = store_verdicts(ctx, sq, vn, reqs, pending[vn.id])
+                codes = pending[vn.id]()
+                if vn.id in pending2:
+                    codes = list(codes) + list(pending2[vn.id]())
+                bitmaps[vn.id] = store_verdicts(ctx, sq, vn, reqs + reqs2, codes)
         if pooled is not None:
             pooled.result()
+    reqs = reqs + reqs2
+    if getattr(ctx, "net", None) is not None:
+        _net_proofs(ctx, sq, reqs, vns)
     # bitmaps -> root VN (SharedBMChannel)
     allbm = {}
     for d in ctx.comm.all_gather_object(bitmaps):

@@ -303,17 +303,31 @@ class DrynxNode:
         client_future = None
         if on_result is not None and result is not None:
             client_future = self._submit_client(on_result, SurveyResult(sq.SurveyID, result, n_groups, n_out))
+        # the last CN phase's proofs (key switching) are still being finished:
+        # the VNs check every other proof first (pcp.proof_collection ``late``)
+        late_f = proofs.pop() if proofs and hasattr(proofs[-1], "result") else None
         with timers.span("cn.proofs.wait"):
             proofs = self._resolve_proofs(proofs)
         if range_future is not None:
             proofs.extend(range_future.result())
             if hasattr(self, "_prove_stream"):
                 torch.cuda.current_stream(self.device).wait_stream(self._prove_stream)
+        secret_of = lambda pid: self.cluster.by_id(pid).keypair.secret  # noqa: E731
         if self.fault_plan:
-            self.fault_plan.apply(proofs, lambda pid: self.cluster.by_id(pid).keypair.secret)
+            self.fault_plan.apply(proofs, secret_of)
+
+        def late():
+            with timers.span("cn.proofs.wait_late"):
+                out = self._resolve_proofs([late_f]) if late_f is not None else []
+            if self.fault_plan:
+                self.fault_plan.apply(out, secret_of)
+            return out
+
         block = None
         if q.Proofs and q.RosterVNs is not None and len(q.RosterVNs.list):
-            block = pcp.proof_collection(self, sq, proofs, early)
+            block = pcp.proof_collection(self, sq, proofs, early, late)
+        elif late_f is not None:
+            late()
         clear = {k: v["clear"] for k, v in dp_results.items()}
         out = SurveyResult(sq.SurveyID, result, n_groups, n_out, block, clear)
         if client_future is not None:
@@ -347,7 +361,10 @@ class DrynxNode:
             return fut
         if not hasattr(self, "_cnp_pool"):
             self._cnp_pool = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="drynx-cn-proofs")
-            self._cnp_stream = torch.cuda.Stream(self.device)
+            # high priority: the per-CN proofs (key switch last) gate the VNs' checks;
+            # at normal priority their short digest / response kernels queue behind
+            # the querier's high-priority decryption
+            self._cnp_stream = torch.cuda.Stream(self.device, priority=-1)
         side = self._cnp_stream
         side.wait_stream(torch.cuda.current_stream(self.device))
 

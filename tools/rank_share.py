@@ -87,7 +87,10 @@ def _torch_glue(path, *fns):
         agg[key] += t
         cnt[key] += 1
     with open(path, "w") as f:
-        f.write(p.key_averages().table(sort_by="cuda_time_total", row_limit=50, max_name_column_width=60))
+        f.write(p.key_averages().table(sort_by="device_time_total", row_limit=50, max_name_column_width=60))
+        f.write("\n\n# by call stack\n")
+        f.write(p.key_averages(group_by_stack_n=6).table(sort_by="self_device_time_total", row_limit=40,
+                                                         max_name_column_width=40, max_src_column_width=90))
         f.write("\n\n# GPU time of torch ops by (op, innermost framework frame)\n")
         for (name, fr), t in sorted(agg.items(), key=lambda kv: -kv[1])[:80]:
             f.write(f"{t / 1e3:9.2f} ms {cnt[(name, fr)]:5d}  {name:28s} {fr}\n")
