@@ -664,9 +664,10 @@ def _prove_group(u, l, vals, offs, cols, r, cv, sigmat, P_point, device, mode=0,
         v = bn.random_scalars(n * S * l, device)
     # commitments (independent of the challenge):
     # D = (sum_j u^j s_j) B + (sum_j m_j) P
-    us = nt.fr_dot_rows(s, _powers(u, l, device), n, b_periodic=True)
-    msum = nt.fr_dot_rows(m, None, n)
-    D = nt.g1_add(nt.g1_fb_mul(tabB, us), nt.g1_fb_mul(tabP, msum))
+    with timers.span("rp.prove.D"):
+        us = nt.fr_dot_rows(s, _powers(u, l, device), n, b_periodic=True)
+        msum = nt.fr_dot_rows(m, None, n)
+        D = nt.g1_add(nt.g1_fb_mul(tabB, us), nt.g1_fb_mul(tabP, msum))
     # V_ij = v_ij * A_{i, col, phi_j};  a_ij = e(-s_j B, V_ij) e(t_j B, B2)
     cols_t = bn.h2d(torch.tensor(cols, dtype=torch.long), device)
     i_idx = torch.arange(S, device=device)
@@ -675,17 +676,20 @@ def _prove_group(u, l, vals, offs, cols, r, cv, sigmat, P_point, device, mode=0,
     a_index = ((i_idx.view(1, S, 1) * sigmat.n_cols + cols_t.view(n, 1, 1)) * max(1, sigmat.umax)
                + phi_t.view(n, 1, l)).reshape(-1)
     _, gt_tab = gt_generator_table(device)
-    uniq, inv = torch.unique(a_index, return_inverse=True)
-    tabs = sigmat.prover_tables(uniq, device, n_items=a_index.numel())
+    with timers.span("rp.prove.unique"):
+        uniq, inv = torch.unique(a_index, return_inverse=True)
+        tabs = sigmat.prover_tables(uniq, device, n_items=a_index.numel())
     if tabs is not None:
         # table-driven prover: V = v * A_phi (G2 comb), a = e(B,A_phi)^{-s v} * gT^t (GT combs) --
         # no pairing and no final exponentiation per (value, server, digit)
         g2_tabs, gphi_tabs, slot, wbits = tabs
         tidx = slot.index_select(0, inv).to(torch.int32).contiguous()
-        V = {4: nt.g2_fb4_mul, 6: nt.g2_gls6_mul, 7: nt.g2_gls8_mul, 8: nt.g2_fb_mul}[wbits](g2_tabs, v, tidx)
+        with timers.span("rp.prove.V"):
+            V = {4: nt.g2_fb4_mul, 6: nt.g2_gls6_mul, 7: nt.g2_gls8_mul, 8: nt.g2_fb_mul}[wbits](g2_tabs, v, tidx)
         negs_rep = nt.fr_arith(nt.FR_NEG, s).view(n, 1, l, 8).expand(n, S, l, 8).reshape(-1, 8).contiguous()
         e = nt.fr_arith(nt.FR_MUL, negs_rep, v)
-        A = nt.rp_prove_a_tab(gphi_tabs, tidx, e, t, gt_tab, S, l, wbits)
+        with timers.span("rp.prove.A"):
+            A = nt.rp_prove_a_tab(gphi_tabs, tidx, e, t, gt_tab, S, l, wbits)
     else:
         A_sel = sigmat.A.to(device).index_select(0, a_index).contiguous()
         V = nt.g2_mul(A_sel, v)
@@ -701,10 +705,11 @@ def _prove_group(u, l, vals, offs, cols, r, cv, sigmat, P_point, device, mode=0,
         phi_sc[:, 0] = phi_t.reshape(-1).to(torch.int32)              # 0 <= phi < u < 2^31
     else:
         phi_sc = _small_scalars(phi.reshape(-1), device)
-    zphi = nt.fr_arith(nt.FR_SUB, s, nt.fr_arith(nt.FR_MUL, _rep(c, l), phi_sc))
-    zr = nt.fr_arith(nt.FR_SUB, msum, nt.fr_arith(nt.FR_MUL, c, r))
-    t_rep = t.view(n, 1, l, 8).expand(n, S, l, 8).reshape(-1, 8).contiguous()
-    zv = nt.fr_arith(nt.FR_SUB, t_rep, nt.fr_arith(nt.FR_MUL, _rep(c, S * l), v))
+    with timers.span("rp.prove.responses"):
+        zphi = nt.fr_arith(nt.FR_SUB, s, nt.fr_arith(nt.FR_MUL, _rep(c, l), phi_sc))
+        zr = nt.fr_arith(nt.FR_SUB, msum, nt.fr_arith(nt.FR_MUL, c, r))
+        t_rep = t.view(n, 1, l, 8).expand(n, S, l, 8).reshape(-1, 8).contiguous()
+        zv = nt.fr_arith(nt.FR_SUB, t_rep, nt.fr_arith(nt.FR_MUL, _rep(c, S * l), v))
     rpl.challenge, rpl.zr, rpl.D, rpl.zphi, rpl.zv, rpl.V, rpl.A = c, zr, D, zphi, zv, V, A
     return rpl
 
@@ -852,6 +857,8 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
                 chk = ch_ok                    # a wrong challenge fails its own segment (attributed below)
     tabB = bn.base_table(device)
     # --- shared, weight-free inputs
+    _sp = timers.span("rp.verify.inputs")
+    _sp.__enter__()
     Cp = r.commit.C                                                    # C' = C + offset*B
     if any(r.offset):
         Cp = nt.g1_add(Cp, nt.g1_fb_mul_i64(tabB, bn.h2d(torch.tensor(r.offset, dtype=torch.int64), device)))
@@ -864,6 +871,7 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
         Y = nt.g1_fb_mul_idx(ytabs[0], ytabs[1].index_select(0, y_idx).contiguous(), _rep(r.challenge, S))
     else:
         Y = nt.g1_mul(sigmat.y_jac.to(device).index_select(0, y_idx).contiguous(), _rep(r.challenge, S))  # [n*S]
+    _sp.__exit__(None, None, None)
     # --- per-VN weights (each from its own coins): every VN's bucket plans in ONE host sync each
     G, m = n_vn, n * S * l
     cl = list(coins) if coins is not None else [None] * G
@@ -872,6 +880,8 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
     def _cat_draw(fn):
         return torch.cat([fn(c) for c in cl]) if G > 1 else fn(cl[0])
 
+    _sw = timers.span("rp.verify.weights")
+    _sw.__enter__()
     w_all = _cat_draw(lambda c: c.bits(n, device, 64) if c is not None else _rand64(n, device))  # D-equation weights
     # pairing-equation weights: rho = a + b lambda (GLV, a and b 32-bit: 2^64
     # distinct residues, so the same 2^-64 soundness as uniform 64-bit weights;
@@ -882,7 +892,9 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
     # GT-membership combinations: one independent 40-bit gamma set PER VN
     gb = int(os.environ.get("DRYNX_GAMMA_BITS", "40"))  # A/B diagnostics only: below 39 bits is unsound
     gam_all = _cat_draw(lambda c: c.bits(m, device, gb) if c is not None else _rand64(m, device, gb))
+    _sw.__exit__(None, None, None)
     vns = [{"rho": rho_all[v * m:(v + 1) * m], "ab": ab_all[v * m:(v + 1) * m]} for v in range(G)]
+    timers.count("rp.verify.items", G * m)
     # attribution: the bucket methods group every entry by (VN, segment) and
     # sum / multiply the buckets over the segments before weighting them, so
     # the per-VN checks cost the same, and a failing VN's per-segment values

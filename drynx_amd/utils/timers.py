@@ -45,9 +45,16 @@ def _dev_sync():
         torch.cuda.synchronize()
 
 
+PROFILE_SPANS = False  # tools set this under torch.profiler: spans become record_function ranges
+
+
 @contextlib.contextmanager
 def span(name: str):
     """A no-sync traced region (free when DRYNX_TRACE is unset)."""
+    if PROFILE_SPANS:
+        with torch.profiler.record_function(name):
+            yield
+        return
     if not _TRACE:
         yield
         return

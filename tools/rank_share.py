@@ -68,13 +68,17 @@ def _torch_glue(path, *fns):
 
     from torch.profiler import ProfilerActivity, profile
 
+    from drynx_amd.utils import timers
+
     for fn in fns:
         fn()
     _sync()
+    timers.PROFILE_SPANS = True  # every framework span is a profiler range (GPU time of what it launched)
     with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True) as p:
         for fn in fns:
             fn()
         _sync()
+    timers.PROFILE_SPANS = False
     agg, cnt = defaultdict(float), defaultdict(int)
     for e in p.events():
         if not e.name.startswith("aten::") or e.cpu_parent is not None and e.cpu_parent.name.startswith("aten::"):
@@ -88,9 +92,8 @@ def _torch_glue(path, *fns):
         cnt[key] += 1
     with open(path, "w") as f:
         f.write(p.key_averages().table(sort_by="device_time_total", row_limit=50, max_name_column_width=60))
-        f.write("\n\n# by call stack\n")
-        f.write(p.key_averages(group_by_stack_n=6).table(sort_by="self_device_time_total", row_limit=40,
-                                                         max_name_column_width=40, max_src_column_width=90))
+        f.write("\n\n# framework spans and torch ops (device time incl. children)\n")
+        f.write(p.key_averages().table(sort_by="device_time_total", row_limit=80, max_name_column_width=50))
         f.write("\n\n# GPU time of torch ops by (op, innermost framework frame)\n")
         for (name, fr), t in sorted(agg.items(), key=lambda kv: -kv[1])[:80]:
             f.write(f"{t / 1e3:9.2f} ms {cnt[(name, fr)]:5d}  {name:28s} {fr}\n")
