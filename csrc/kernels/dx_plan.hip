@@ -10,9 +10,13 @@
 //    and a gather of the items.
 //  * dx_bucket_bounds: first entry and end of every bucket's run in the sorted
 //    keys (run boundaries only: coalesced reads, one write per boundary).
-//  * dx_slice_plan: one thread per bucket writes its slices (start, length)
-//    -- the descriptors of a pass never go through torch's repeat_interleave /
-//    arange / index arithmetic.
+//  * dx_bucket_hist + dx_bucket_scatter: a counting sort by bucket (the keys
+//    are small integers): one histogram pass, one scatter pass -- no
+//    comparison / radix sort, no index payload, no gather; the histogram is
+//    the plan's per-bucket counts.
+//  * dx_slice_desc: one thread per slice (binary search of its bucket)
+//    writes the pass descriptors (start, length), coalesced -- they never go
+//    through torch's repeat_interleave / arange / index arithmetic.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -47,6 +51,45 @@ __global__ void __launch_bounds__(256) slice_plan_kernel(const int64_t *first, c
     st[o + j] = f + j * sl;
     ln[o + j] = (int32_t)std::min<int64_t>(sl, c - j * sl);
   }
+}
+
+// counting sort of the entries by bucket: histogram, then each entry's slot
+// = offs[key] + (arrival order within its bucket); the order inside a bucket
+// is arbitrary (bucket reductions are sums / products of group elements)
+__global__ void __launch_bounds__(256) bucket_hist_kernel(const int32_t *keys, int64_t n, int64_t nb,
+                                                          int32_t *counts) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int32_t k = keys[i];
+  if (k >= 0 && k < nb) atomicAdd(&counts[k], 1);
+}
+
+__global__ void __launch_bounds__(256) bucket_scatter_kernel(const int32_t *keys, const int32_t *items, int64_t n,
+                                                             int64_t nb, const int64_t *offs, int32_t *cursor,
+                                                             int32_t *out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int32_t k = keys[i];
+  if (k < 0 || k >= nb) return;
+  out[offs[k] + atomicAdd(&cursor[k], 1)] = items[i];
+}
+
+// slice t of a pass: its bucket b by binary search over the slice offsets
+// (one thread per slice: coalesced writes)
+__global__ void __launch_bounds__(256) slice_desc_kernel(const int64_t *first, const int64_t *count,
+                                                         const int64_t *soff, int sl, int64_t nbk, int64_t total,
+                                                         int64_t *st, int32_t *ln) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= total) return;
+  int64_t lo = 0, hi = nbk - 1;
+  while (lo < hi) {  // last b with soff[b] <= t
+    const int64_t mid = (lo + hi + 1) >> 1;
+    if (soff[mid] <= t) lo = mid; else hi = mid - 1;
+  }
+  const int64_t j = t - soff[lo];
+  st[t] = first[lo] + j * sl;
+  const int64_t rem = count[lo] - j * sl;
+  ln[t] = (int32_t)(rem < sl ? rem : sl);
 }
 
 inline dim3 blocks(int64_t n) { return dim3((unsigned)((n + 255) / 256)); }
@@ -101,6 +144,55 @@ int dx_bucket_bounds(int on_gpu, void *stream, const int32_t *keys, int64_t n, i
   }
   hipLaunchKernelGGL(bucket_bounds_kernel, blocks(n), dim3(256), 0, (hipStream_t)stream, keys, n, nb, first, end);
   return dx::check_hip(hipGetLastError(), "bucket_bounds");
+}
+
+// counts[k] (zeroed int32 [nb]) of the entries with key k < nb
+int dx_bucket_hist(int on_gpu, void *stream, const int32_t *keys, int64_t n, int64_t nb, int32_t *counts) {
+  if (n <= 0) return 0;
+  if (!on_gpu) {
+    for (int64_t i = 0; i < n; i++)
+      if (keys[i] >= 0 && keys[i] < nb) counts[keys[i]]++;
+    return 0;
+  }
+  hipLaunchKernelGGL(bucket_hist_kernel, blocks(n), dim3(256), 0, (hipStream_t)stream, keys, n, nb, counts);
+  return dx::check_hip(hipGetLastError(), "bucket_hist");
+}
+
+// out[offs[k] + r] = items of the entries with key k (offs: exclusive prefix
+// sums of the counts; cursor zeroed int32 [nb])
+int dx_bucket_scatter(int on_gpu, void *stream, const int32_t *keys, const int32_t *items, int64_t n, int64_t nb,
+                      const int64_t *offs, int32_t *cursor, int32_t *out) {
+  if (n <= 0) return 0;
+  if (!on_gpu) {
+    for (int64_t i = 0; i < n; i++) {
+      const int32_t k = keys[i];
+      if (k >= 0 && k < nb) out[offs[k] + cursor[k]++] = items[i];
+    }
+    return 0;
+  }
+  hipLaunchKernelGGL(bucket_scatter_kernel, blocks(n), dim3(256), 0, (hipStream_t)stream, keys, items, n, nb, offs,
+                     cursor, out);
+  return dx::check_hip(hipGetLastError(), "bucket_scatter");
+}
+
+// per non-empty bucket b (count[b] entries from first[b]): its slices of <= sl
+// entries at soff[b] .. in (st, ln); total = the number of slices
+int dx_slice_desc(int on_gpu, void *stream, const int64_t *first, const int64_t *count, const int64_t *soff, int sl,
+                  int64_t nbk, int64_t total, int64_t *st, int32_t *ln) {
+  if (nbk <= 0 || total <= 0) return 0;
+  if (!on_gpu) {
+    for (int64_t b = 0; b < nbk; b++) {
+      const int64_t ns = (count[b] + sl - 1) / sl;
+      for (int64_t j = 0; j < ns; j++) {
+        st[soff[b] + j] = first[b] + j * sl;
+        ln[soff[b] + j] = (int32_t)std::min<int64_t>(sl, count[b] - j * sl);
+      }
+    }
+    return 0;
+  }
+  hipLaunchKernelGGL(slice_desc_kernel, blocks(total), dim3(256), 0, (hipStream_t)stream, first, count, soff, sl, nbk,
+                     total, st, ln);
+  return dx::check_hip(hipGetLastError(), "slice_desc");
 }
 
 // per non-empty bucket b (count[b] entries from first[b]): its slices of <= sl

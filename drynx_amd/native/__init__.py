@@ -104,6 +104,9 @@ _SIGS = {
     "dx_bucket_sort": [_I, _P, _P, _P, _P, _P, _L, _I, _P, ctypes.c_uint64],
     "dx_bucket_bounds": [_I, _P, _P, _L, _L, _P, _P],
     "dx_slice_plan": [_I, _P, _P, _P, _P, _I, _L, _P, _P],
+    "dx_bucket_hist": [_I, _P, _P, _L, _L, _P],
+    "dx_bucket_scatter": [_I, _P, _P, _P, _L, _L, _P, _P, _P],
+    "dx_slice_desc": [_I, _P, _P, _P, _P, _I, _L, _L, _P, _P],
     "dx_g1_slice_sum": [_I, _P, _P, _P, _P, _P, _P, _L],
     "dx_rp_prove_a": [_I, _P, _P, _P, _P, _P, _P, _L, _I, _I],
     "dx_rp_prove_a_tab": [_I, _P, _P, _P, _P, _P, _P, _P, _L, _I, _I, _I],
@@ -1369,7 +1372,17 @@ def _sort_buckets(keys: torch.Tensor, items: torch.Tensor, nb: int):
     dev = keys.device
     n = keys.numel()
     g, s = _ctx(keys)
-    if not g or os.environ.get("DRYNX_PLAN_SORT", "torch") == "torch":
+    mode = os.environ.get("DRYNX_PLAN_SORT", "count")
+    if mode == "count":
+        # counting sort by bucket (csrc/kernels/dx_plan.hip): histogram -> slots -> scatter
+        counts_d = torch.zeros(nb, dtype=torch.int32, device=dev)
+        _call("dx_bucket_hist", g, s, _ptr(keys), n, nb, _ptr(counts_d))
+        offs = torch.cumsum(counts_d, 0, dtype=torch.int64) - counts_d
+        cursor = torch.zeros(nb, dtype=torch.int32, device=dev)
+        i2 = torch.empty_like(items)
+        _call("dx_bucket_scatter", g, s, _ptr(keys), _ptr(items), n, nb, _ptr(offs), _ptr(cursor), _ptr(i2))
+        return i2, counts_d.cpu().numpy().astype(np.int64)                 # the one host sync
+    if not g or mode == "torch":
         # torch's onesweep radix sort (hipCUB): measured faster on gfx950 than a
         # direct rocprim::radix_sort_pairs over the keys' bits (5.9 vs ~1.1 ms
         # per 48M-entry plan); the runs then come from dx_bucket_bounds
@@ -1417,7 +1430,8 @@ def _segment_passes_dev(counts, dev, first_slice: int | None = None):
         start = torch.empty(total, dtype=torch.int64, device=dev)
         ln = torch.empty(total, dtype=torch.int32, device=dev)
         g, s = _ctx(m_dev)
-        _call("dx_slice_plan", g, s, _ptr(m_dev[0]), _ptr(m_dev[1]), _ptr(m_dev[2]), sl, c.size, _ptr(start), _ptr(ln))
+        _call("dx_slice_desc", g, s, _ptr(m_dev[0]), _ptr(m_dev[1]), _ptr(m_dev[2]), sl, c.size, total, _ptr(start),
+              _ptr(ln))
         passes.append((start, ln))
         c = n_sl
     return passes
