@@ -1372,7 +1372,12 @@ def _sort_buckets(keys: torch.Tensor, items: torch.Tensor, nb: int):
     dev = keys.device
     n = keys.numel()
     g, s = _ctx(keys)
-    mode = os.environ.get("DRYNX_PLAN_SORT", "count")
+    # "torch" (default): onesweep radix sort + run boundaries -- on the 1-GPU
+    # headline it measured fastest (profiles/r4/ab_plan_sort.txt): the plans run
+    # beside the U-side kernels, and the alternatives (a counting sort's atomic
+    # histogram / scatter, a rocPRIM pairs sort over the keys' bits) cost less
+    # alone but interfere more with the concurrent work
+    mode = os.environ.get("DRYNX_PLAN_SORT", "torch")
     if mode == "count":
         # counting sort by bucket (csrc/kernels/dx_plan.hip): histogram -> slots -> scatter
         counts_d = torch.zeros(nb, dtype=torch.int32, device=dev)

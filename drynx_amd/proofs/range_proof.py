@@ -899,8 +899,10 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
     # sum / multiply the buckets over the segments before weighting them, so
     # the per-VN checks cost the same, and a failing VN's per-segment values
     # come from the kept buckets (no second plan, no re-bucketing)
+    # (DRYNX_SEG_KEEP=1; off by default: folding costs the clean path ~9 ms of a
+    # ~200 ms query for ~40 ms on a failing one, profiles/r4/ab_plan_sort.txt)
     fold = nseg if (segs is not None and nseg > 1 and use_msm
-                    and os.environ.get("DRYNX_SEG_KEEP", "1") != "0") else 1
+                    and os.environ.get("DRYNX_SEG_KEEP", "0") == "1") else 1
     pseg = iseg = None
     if fold > 1:
         pseg = torch.repeat_interleave(torch.arange(nseg, device=device), _h2d(segs, device), output_size=n)

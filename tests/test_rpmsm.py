@@ -192,6 +192,7 @@ def test_segment_attribution(device, field, proofs, monkeypatch):
     calls = []
     orig = rp._segment_finish_kept
     monkeypatch.setattr(rp, "_segment_finish_kept", lambda *a: calls.append(1) or orig(*a))
+    monkeypatch.setenv("DRYNX_SEG_KEEP", "1")
     assert rp.verify_range_proof_list_multi(bad, sm, P, 2, dev, segs=[1, 2, 1]) == [want] * 2
     assert calls, "the failing VNs' segments come from the first pass's kept buckets"
     # the re-bucketing second pass (DRYNX_SEG_KEEP=0) names the same segments
