@@ -143,7 +143,9 @@ def _rank_record(comm, cl, step_ms, elapsed, setup_s, b0) -> dict:
     roles = {r: [p.id for p in cl.local(comm.rank, r)] for r in ("cn", "vn", "dp")}
     return {"rank": comm.rank, "roles": roles, "step_ms": step_ms, "elapsed_ms": round(1000 * elapsed, 1),
             "setup_s": round(setup_s, 3), "bytes_sent": comm.bytes_sent - b0[0], "bytes_recv": comm.bytes_recv - b0[1],
-            "pool_range_items": timers.counters().get("pool.range_items", 0)}
+            "pool_range_items": timers.counters().get("pool.range_items", 0),
+            "ctrl_collectives": timers.counters().get("comm.ctrl_collectives", 0),
+            "data_exchanges": timers.counters().get("comm.data_exchanges", 0)}
 
 
 def main():

@@ -30,6 +30,8 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
+from ..utils import timers
+
 
 class Comm:
     rank: int = 0
@@ -147,6 +149,7 @@ class DistComm(Comm):
         receive sizes cost one size round (a W-element all-to-all)."""
         W = self.world
         stage = self._stage
+        timers.count("comm.data_exchanges")
         flat = {d: t.reshape(-1).to(torch.int32) for d, t in outgoing.items()}
         send_sizes = [0] * W
         for d, t in flat.items():
@@ -212,6 +215,7 @@ class DistComm(Comm):
 
 def _bcast_obj(rank: int, obj, src: int, group):
     """Control message from ``src`` to every rank (msgpack, no pickle)."""
+    timers.count("comm.ctrl_collectives")
     if rank == src:
         b = obj_to_bytes(obj)
         n = torch.tensor([len(b)], dtype=torch.int64)
@@ -224,6 +228,7 @@ def _bcast_obj(rank: int, obj, src: int, group):
 
 
 def _gather_obj(rank: int, world: int, obj, group) -> list:
+    timers.count("comm.ctrl_collectives")
     b = obj_to_bytes(obj)
     sizes = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
     dist.all_gather(sizes, torch.tensor([len(b)], dtype=torch.int64), group=group)

@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import hashlib
 import math
+import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -191,7 +192,8 @@ def schnorr_sign_batch(secrets: list, msgs: list, device="cpu") -> list:
     # a handful of envelopes (a CN's per-phase proofs) sign on the host pool:
     # a device launch would queue behind the query's GPU work and add a
     # device-to-host round trip (verification uses the same rule)
-    dev = torch.device(device) if n >= _SIG_DEVICE_MIN else torch.device("cpu")
+    dev = torch.device(device) if n >= int(os.environ.get("DRYNX_SIGN_DEVICE_MIN", _SIG_DEVICE_MIN)) \
+        else torch.device("cpu")
     pts = nt.g1_fb_mul(bn.base_table(dev), bn.scalars_tensor(ks + [int(x) for x in secrets], dev))
     enc = bn.g1_aff_to_bytes(nt.g1_to_affine(pts))
     out = []

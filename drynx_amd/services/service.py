@@ -305,7 +305,8 @@ class DrynxNode:
             client_future = self._submit_client(on_result, SurveyResult(sq.SurveyID, result, n_groups, n_out))
         # the last CN phase's proofs (key switching) are still being finished:
         # the VNs check every other proof first (pcp.proof_collection ``late``)
-        late_f = proofs.pop() if proofs and hasattr(proofs[-1], "result") else None
+        late_f = (proofs.pop() if proofs and hasattr(proofs[-1], "result")
+                  and os.environ.get("DRYNX_PROOF_STAGES", "2") == "2" else None)
         with timers.span("cn.proofs.wait"):
             proofs = self._resolve_proofs(proofs)
         if range_future is not None:
@@ -364,7 +365,7 @@ class DrynxNode:
             # high priority: the per-CN proofs (key switch last) gate the VNs' checks;
             # at normal priority their short digest / response kernels queue behind
             # the querier's high-priority decryption
-            self._cnp_stream = torch.cuda.Stream(self.device, priority=-1)
+            self._cnp_stream = torch.cuda.Stream(self.device, priority=int(os.environ.get("DRYNX_CNP_PRIORITY", "-1")))
         side = self._cnp_stream
         side.wait_stream(torch.cuda.current_stream(self.device))
 
