@@ -27,6 +27,13 @@ int dx_gt_mul(int on_gpu, void *stream, const uint32_t *a, const uint32_t *b, ui
   return run(on_gpu, stream, n, op, true, "gt_mul");
 }
 
+// out_i = a_i^-1 in Fp12* (any non-zero element, not only the cyclotomic
+// subgroup where the conjugate is the inverse)
+int dx_gt_inv(int on_gpu, void *stream, const uint32_t *a, uint32_t *out, int64_t n) {
+  auto op = [=] __host__ __device__(int64_t i) { at<Fp12>(out, i) = inv(at<Fp12>(a, i)); };
+  return run(on_gpu, stream, n, op, true, "gt_inv");
+}
+
 int dx_gt_pow(int on_gpu, void *stream, const uint32_t *a, const uint32_t *scalars, uint32_t *out, int64_t n,
               int a_bcast) {
   auto op = [=] __host__ __device__(int64_t i) {

@@ -81,6 +81,7 @@ _SIGS = {
     "dx_final_exp": [_I, _P, _P, _P, _L],
     "dx_pairing": [_I, _P, _P, _P, _P, _L],
     "dx_gt_mul": [_I, _P, _P, _P, _P, _L],
+    "dx_gt_inv": [_I, _P, _P, _P, _L],
     "dx_gt_pow": [_I, _P, _P, _P, _P, _L, _I],
     "dx_gt_eq": [_I, _P, _P, _P, _P, _L],
     "dx_gt_fb_table": [_I, _P, _P, _P, _P, _L],
@@ -730,6 +731,15 @@ def gt_mul(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     out = torch.empty_like(a)
     g, s = _ctx(a, b)
     _call("dx_gt_mul", g, s, _ptr(a), _ptr(b), _ptr(out), n)
+    return out
+
+
+def gt_inv(a: torch.Tensor) -> torch.Tensor:
+    """Row-wise inverse in Fp12*."""
+    n = _rows(a, 96)
+    out = torch.empty_like(a)
+    g, s = _ctx(a)
+    _call("dx_gt_inv", g, s, _ptr(a.contiguous()), _ptr(out), n)
     return out
 
 
