@@ -82,6 +82,8 @@ _SIGS = {
     "dx_pairing": [_I, _P, _P, _P, _P, _L],
     "dx_gt_mul": [_I, _P, _P, _P, _P, _L],
     "dx_gt_inv": [_I, _P, _P, _P, _L],
+    "dx_batched_copy": [_I, _P, _P, _P, _I, _L],
+    "dx_rows_all": [_I, _P, _P, _P, _I, _L, _P],
     "dx_gt_pow": [_I, _P, _P, _P, _P, _L, _I],
     "dx_gt_eq": [_I, _P, _P, _P, _P, _L],
     "dx_gt_fb_table": [_I, _P, _P, _P, _P, _L],
@@ -726,6 +728,83 @@ def pairing(P_aff: torch.Tensor, Q_aff: torch.Tensor) -> torch.Tensor:
     return out
 
 
+_CHUNK_WORDS = 4096
+
+
+def batched_copy(pairs: list) -> None:
+    """``dst.copy_(src)`` for many (src, dst) pairs of one device in ONE
+    launch of 16 KB chunks (csrc/kernels/dx_copy.hip); both contiguous, the
+    same byte size, a multiple of 4 bytes."""
+    pairs = [(s_, d_) for s_, d_ in pairs if s_.numel()]
+    if not pairs:
+        return
+    dev = pairs[0][1].device
+    desc = np.empty((len(pairs), 4), dtype=np.int64)
+    c0 = 0
+    for i, (s_, d_) in enumerate(pairs):
+        nb = s_.numel() * s_.element_size()
+        assert s_.is_contiguous() and d_.is_contiguous() and s_.device == dev and d_.device == dev
+        assert nb == d_.numel() * d_.element_size() and nb % 4 == 0, (s_.shape, d_.shape)
+        w = nb // 4
+        desc[i] = (s_.data_ptr(), d_.data_ptr(), w, c0)
+        c0 += -(-w // _CHUNK_WORDS)
+    ht = torch.from_numpy(desc)
+    dd = ht.pin_memory().to(dev, non_blocking=True) if dev.type == "cuda" else ht
+    g, st = _ctx(pairs[0][1])
+    for s_, d_ in pairs:  # held until the call returns
+        _ptr(s_), _ptr(d_)
+    _call("dx_batched_copy", g, st, _ptr(dd), _ptr(ht), len(pairs), c0)
+
+
+def cat_rows(groups: list) -> list:
+    """``[torch.cat(g) for g in groups]`` (dim 0) with every copy in ONE
+    ``batched_copy`` launch.  A one-tensor group is returned as is (no copy);
+    groups whose element bytes are not a multiple of 4 use torch.cat."""
+    outs, pairs = [], []
+    for g_ in groups:
+        if len(g_) == 1:
+            outs.append(g_[0])
+            continue
+        t0 = g_[0]
+        if any(t.numel() * t.element_size() % 4 for t in g_):
+            outs.append(torch.cat(g_))
+            continue
+        out = torch.empty((sum(t.shape[0] for t in g_),) + tuple(t0.shape[1:]), dtype=t0.dtype, device=t0.device)
+        o = 0
+        for t in g_:
+            assert t.dtype == t0.dtype and tuple(t.shape[1:]) == tuple(t0.shape[1:])
+            pairs.append((t.contiguous(), out[o: o + t.shape[0]]))
+            o += t.shape[0]
+        outs.append(out)
+    batched_copy(pairs)
+    return outs
+
+
+def rows_all(flags: list, n: int) -> torch.Tensor:
+    """uint8 [n]: row p passes iff every flag array (uint8 / bool, n * k_a
+    entries, row-major) is non-zero on its k_a entries of row p -- one
+    wavefront per row (csrc/kernels/dx_copy.hip), no bool conversions or
+    reductions."""
+    fl = [f.reshape(-1).contiguous() for f in flags]
+    fl = [f.view(torch.uint8) if f.dtype == torch.bool else f for f in fl]
+    assert all(f.dtype == torch.uint8 and f.numel() % max(n, 1) == 0 for f in fl)
+    out = torch.empty((n,), dtype=torch.uint8, device=fl[0].device)
+    if n == 0:
+        return out
+    for i in range(0, len(fl), 16):
+        part = fl[i: i + 16]
+        ptrs = np.asarray([f.data_ptr() for f in part], dtype=np.int64)
+        ks = np.asarray([f.numel() // n for f in part], dtype=np.int64)
+        g, s = _ctx(out)
+        for f in part:
+            _ptr(f)
+        o = out if i == 0 else torch.empty_like(out)
+        _call("dx_rows_all", g, s, ptrs.ctypes.data, ks.ctypes.data, len(part), n, _ptr(o))
+        if i:
+            out &= o
+    return out
+
+
 def gt_mul(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     n = _rows(a, 96)
     out = torch.empty_like(a)
@@ -1286,9 +1365,11 @@ def rp_fold_accum_n(img: torch.Tensor, UV: torch.Tensor, V_aff: torch.Tensor, pe
     return fb
 
 
-def gt_frob8(a: torch.Tensor) -> torch.Tensor:
-    """a^(p^8) per row (= a^GLV_LAMBDA on GT)."""
-    out = torch.empty_like(a)
+def gt_frob8(a: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """a^(p^8) per row (= a^GLV_LAMBDA on GT); ``out``: a contiguous
+    destination of a's shape (e.g. the second half of a stacked image)."""
+    out = torch.empty_like(a) if out is None else out
+    assert out.is_contiguous() and out.shape == a.shape
     g, s = _ctx(a)
     _call("dx_gt_frob8", g, s, _ptr(a.contiguous()), _ptr(out), _rows(a, 96))
     return out

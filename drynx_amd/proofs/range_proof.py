@@ -759,11 +759,13 @@ def validate_list(r: RangeProofList, mode: int = 0, subgroup: bool | None = None
     if r.has_rp and len(r):
         flags += [fp(r.D), nt.g1j_on_curve(r.D), fr(r.challenge), fr(r.zr), fr(r.zphi), fr(r.zv), fp(r.V), fp(r.A),
                   nt.g2_subgroup(r.V) if subgroup else nt.g2_on_curve(r.V), nt.gt_cyclotomic(r.A)]
-    if per_proof:  # every array is proof-major with a fixed number of rows per proof
-        n = len(r)
-        ok = torch.stack([f.bool().view(n, -1).all(dim=1) for f in flags]).all(dim=0)
+    # every array is proof-major with a fixed number of rows per proof: one
+    # per-proof AND of all of them (nt.rows_all: a wavefront per proof)
+    n = len(r)
+    ok = nt.rows_all(flags, n).bool() if n else torch.ones((0,), dtype=torch.bool, device=r.commit.K.device)
+    if per_proof:
         return ok if lazy else ok.tolist()
-    ok = torch.stack([f.bool().all() for f in flags]).all()
+    ok = ok.all()
     return ok if lazy else bool(ok)
 
 
@@ -892,6 +894,24 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
     # GT-membership combinations: one independent 40-bit gamma set PER VN
     gb = int(os.environ.get("DRYNX_GAMMA_BITS", "40"))  # A/B diagnostics only: below 39 bits is unsound
     gam_all = _cat_draw(lambda c: c.bits(m, device, gb) if c is not None else _rand64(m, device, gb))
+    # attribution: undecodable proofs (and, mode >= 1, wrong challenges) get
+    # ZERO weights -- every weighted sum then runs over the decodable proofs
+    # only (their U_q and -c y_i become infinity, as the fold's padding), so
+    # one bad payload costs no second pass: the batch verdict IS the verdict
+    # of the decodable segments (DRYNX_RP_MASK=0: the round-3 full
+    # segment pass of every VN)
+    masked = segs is not None and use_msm and os.environ.get("DRYNX_RP_MASK", "1") == "1"
+    if masked:
+        if vstream is not None:
+            torch.cuda.current_stream(device).wait_stream(vstream)
+        vm = (valid if chk is None else valid & chk).to(torch.int32)
+        mi = vm.repeat_interleave(S * l).view(1, m, 1)
+        w_all = (w_all.view(G, n, 8) * vm.view(1, n, 1)).view(G * n, 8)
+        ab_all = (ab_all.view(G, m, 2) * mi).view(G * m, 2)
+        rho_all = (rho_all.view(G, m, 8) * mi).view(G * m, 8)
+        gam_all = (gam_all.view(G, m, 8) * mi).view(G * m, 8)
+        Y = Y.clone()
+        Y[:, 16:] *= vm.repeat_interleave(S).view(-1, 1)                # Z = 0: -c y_i at infinity
     _sw.__exit__(None, None, None)
     vns = [{"rho": rho_all[v * m:(v + 1) * m], "ab": ab_all[v * m:(v + 1) * m]} for v in range(G)]
     timers.count("rp.verify.items", G * m)
@@ -947,8 +967,10 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
         # groups 0..G-1: prod a^rho_v; groups G..2G-1: each VN's own GT-membership
         # combination prod a^gamma_v
         # prod a^rho = prod a^a' * frob^8(a)^b': 32-bit exponents over (A, frob^8 A)
-        with timers.span("rp.frob8"):
-            A2 = torch.cat([r.A, nt.gt_frob8(r.A)])
+        with timers.span("rp.frob8"):  # (A, frob^8 A) stacked: the Frobenius image written in place
+            A2 = torch.empty((2 * m, 96), dtype=torch.int32, device=device)
+            nt.batched_copy([(r.A.contiguous(), A2[:m])])
+            nt.gt_frob8(r.A.contiguous(), out=A2[m:])
         k = torch.zeros((2 * G, 2 * m, 8), dtype=torch.int32, device=device)
         abv = ab_all.view(G, m, 2)
         k[:G, :m, 0] = abv[:, :, 0]
@@ -1038,8 +1060,9 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
         with timers.span("rp.verify.finish"):
             G0 = v["dcheck"]
             PB = nt.g1_mul(PB_base, v["dfull"])
-            d_ok = bool(nt.g1_eq(nt.g1_sum(torch.stack([G0[0:1], PB[0:1], PB[1:2]])), G0[1:2])[0])
-            lhs = nt.gt_mul(fe[k_: k_ + 1].contiguous(), v["G"].cpu())
+            v["dl"] = nt.g1_sum(torch.stack([G0[0:1], PB[0:1], PB[1:2]]))
+            d_ok = bool(nt.g1_eq(v["dl"], G0[1:2])[0])
+            v["lhs"] = lhs = nt.gt_mul(fe[k_: k_ + 1].contiguous(), v["G"].cpu())
             eq_ok = bool(nt.gt_eq(lhs, nt.gt_fb_pow(gt_tab, v["e"].cpu())).all())
         # regrouped ("msm") check: the U_q and R of this VN must lie in G2 --
         # then their torsion parts (V_it off G2 by a cofactor component) cancel
@@ -1058,21 +1081,31 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
     # segments only: every per-segment quantity (U_q, the fold blocks, R_s,
     # prod a^rho, the D-check) involves that segment's data alone
     seg_valid = None if bool(valid.all()) else _seg_all(valid.view(1, -1), segs, valid.device).view(-1).tolist()
-    redo = [k_ for k_ in range(G) if not out[k_] or seg_valid is not None]
-    res = [[True] * nseg if ok else None for ok in out]
+    # masked weights: a passing batch clears every decodable segment
+    redo = [k_ for k_ in range(G) if not out[k_] or (seg_valid is not None and not masked)]
+    res = [([True] * nseg if seg_valid is None else list(seg_valid)) if ok else None for ok in out]
     if redo:
         with timers.span("rp.verify.segments"):
-            per = _segment_pass(r, segs, redo, dict(
-                A2=A2, rho=rho_all, ab=ab_all, gam=gam_all, w=w_all, Cp=Cp, z=z, useg=useg, u_seg=msq["u_seg"],
-                PB_base=PB_base, gt_tab=gt_tab, wc=wc_, G=G,
-                kept=dict(mexp=mexp, dcheck=dcheck) if fold > 1 else None,
-                # undecodable proofs in the batch: the first pass's GT combination
-                # included a_ij not known to be cyclotomic, so it bounds nothing --
-                # every segment then gets its own combination
-                m_first=m_oks if seg_valid is None else [False] * G))
+            x = dict(A2=A2, rho=rho_all, ab=ab_all, gam=gam_all, w=w_all, Cp=Cp, z=z, useg=useg, u_seg=msq["u_seg"],
+                     PB_base=PB_base, gt_tab=gt_tab, wc=wc_, G=G,
+                     kept=dict(mexp=mexp, dcheck=dcheck) if fold > 1 else None,
+                     # undecodable proofs in an UNMASKED batch: the first pass's GT
+                     # combination included a_ij not known to be cyclotomic, so it
+                     # bounds nothing -- every segment then gets its own combination
+                     m_first=m_oks if seg_valid is None or masked else [False] * G,
+                     tot=dict(lhs=[v.get("lhs") for v in vns], e=e_all, GGgam=GG[G: 2 * G],
+                              dl=[v.get("dl") for v in vns], dr=[v["dcheck"][1:2] for v in vns],
+                              r_ok=[bool(v.get("r_ok", True)) for v in vns]))
+            if x["kept"] is None and os.environ.get("DRYNX_SEG_HINT", "1") == "1" and (masked or seg_valid is None):
+                per = _attribute_hinted(r, segs, redo, x)
+            else:
+                per = _segment_pass(r, segs, redo, x)
         for k_ in redo:
             if seg_valid is not None:
-                res[k_] = [a and b for a, b in zip(per[k_], seg_valid)]
+                per_k = [a and b for a, b in zip(per[k_], seg_valid)]
+                # masked: the failing batch held decodable proofs only -- a pass
+                # of every decodable segment explains nothing (the caller bisects)
+                res[k_] = None if masked and per_k == seg_valid else per_k
             else:
                 res[k_] = per[k_] if not all(per[k_]) else None  # nothing attributable: the caller bisects
     return res
@@ -1243,12 +1276,96 @@ def _seg_c(n_entries: int, n_groups: int, bits: int = 254) -> int:
     return min(range(6, 14), key=lambda c: -(-bits // c) * (n_entries + n_groups * (1 << c) * 36))
 
 
-def _segment_pass(r: RangeProofList, segs: list, redo: list, x: dict) -> dict:
+def _attribute_hinted(r: RangeProofList, segs: list, redo: list, x: dict) -> dict:
+    """Attribution of several failing VNs: the first pays the full
+    segment-grouped pass (``_segment_pass``); its failing segments T are then
+    the hint for the others, each of which evaluates only T's segments
+    (``_segment_hinted``: ~|T|/nseg of the pass) and checks the REST of its
+    batch in one equation -- its first-pass totals divided by T's parts (the
+    pairing is bilinear on the G2 points it checks, so the rest's equation is
+    exactly the batch check of the other segments' proofs with the same
+    weights).  A rest that fails, or a hint that explains nothing, falls back
+    to the full pass.  -> {vn: [bool] per segment}."""
+    out, hint = {}, None
+    for v in redo:
+        if hint is not None:
+            with timers.span("rp.seg.hinted"):
+                got = _segment_hinted(r, segs, v, hint, x)
+            if got is not None:
+                out[v] = got
+                continue
+        out.update(_segment_pass(r, segs, [v], x))
+        bad = [s for s, ok in enumerate(out[v]) if not ok]
+        if hint is None and 0 < len(bad) < len(segs):
+            hint = bad
+    return out
+
+
+def _segment_hinted(r: RangeProofList, segs: list, v: int, T: list, x: dict):
+    """VN ``v``'s per-segment verdicts from the suspect segments ``T`` alone:
+    the segment pass over T's proofs (same weights) gives T's per-segment
+    equation sides; the rest's sides are the first-pass totals minus T's --
+      lhs_rest = lhs_all / prod_T lhs_s,   e_rest = e_all - sum_T e_s,
+      D-check: dl_all - sum_T dl_s == dr_all - sum_T dr_s,
+      GT membership (when the first-pass combination failed): GGgam_all / prod_T GGgam_s
+    with R_all and every R_s, U_q of the rest in G2.  -> [bool] per segment,
+    or None when the rest fails or T's segments all pass (no attribution from
+    the hint: the caller runs the full pass)."""
+    dev = r.V.device
+    n, S, l, G = len(r), r.S, r.l, x["G"]
+    m, tot = n * S * l, x["tot"]
+    if tot["lhs"][v] is None or tot["dl"][v] is None:
+        return None
+    poff = np.cumsum([0] + list(segs))
+    rT = rpl_cat([rpl_range(r, int(poff[s]), int(poff[s + 1])) for s in T])
+    pidx = torch.cat([torch.arange(int(poff[s]), int(poff[s + 1])) for s in T])
+    iidx = (pidx.view(-1, 1) * (S * l) + torch.arange(S * l).view(1, -1)).reshape(-1)
+    pidx, iidx = bn.h2d(pidx, dev), bn.h2d(iidx, dev)
+    sel = lambda t, w, idx: t.view(G, -1, w)[v].index_select(0, idx).contiguous()  # noqa: E731
+    Tt = bn.h2d(torch.tensor(T), x["u_seg"].device)
+    xT = dict(A2=x["A2"].index_select(0, torch.cat([iidx, iidx + m])), rho=sel(x["rho"], 8, iidx),
+              ab=sel(x["ab"], 2, iidx), gam=sel(x["gam"], 8, iidx), w=sel(x["w"], 8, pidx),
+              Cp=x["Cp"].index_select(0, pidx), z=x["z"].index_select(0, pidx),
+              useg=x["useg"][v: v + 1, T], u_seg=x["u_seg"][v: v + 1].index_select(1, Tt),
+              PB_base=x["PB_base"], gt_tab=x["gt_tab"], wc=x["wc"], G=1, kept=None, m_first=[x["m_first"][v]])
+    comp = {}
+    perT = _segment_pass(rT, [segs[s] for s in T], [0], xT, comp)[0]
+    if all(perT):
+        return None
+    # the rest, from the totals
+    inv_lhs = nt.gt_inv(nt.gt_prod(comp["lhs"].view(len(T), 1, 96), chunk=64).view(1, 96))
+    lhs_rest = nt.gt_mul(tot["lhs"][v].view(1, 96), inv_lhs)
+    e_rest = tot["e"][v: v + 1].cpu()
+    for s_ in range(len(T)):
+        e_rest = nt.fr_arith(nt.FR_SUB, e_rest, comp["e"][s_: s_ + 1].contiguous())
+    eq = bool(nt.gt_eq(lhs_rest, nt.gt_fb_pow(x["gt_tab"], e_rest)).all())
+    d1 = nt.g1_sum(torch.cat([tot["dl"][v].view(1, 1, 24), comp["dr"].view(-1, 1, 24)]))
+    d2 = nt.g1_sum(torch.cat([tot["dr"][v].view(1, 1, 24), comp["dl"].view(-1, 1, 24)]))
+    d_ok = bool(nt.g1_eq(d1, d2)[0])
+    m_ok = True
+    if not x["m_first"][v]:
+        if comp.get("GGgam") is None:
+            return None
+        gi = nt.gt_inv(nt.gt_prod(comp["GGgam"].view(len(T), 1, 96), chunk=64).view(1, 96))
+        m_ok = _gt_in_subgroup(nt.gt_mul(tot["GGgam"][v: v + 1].cpu(), gi))
+    rest = [s for s in range(len(segs)) if s not in set(T)]
+    u_ok = bool(x["u_seg"][v].cpu()[rest].all()) if rest else True
+    g2_ok = tot["r_ok"][v] and all(comp["rok"]) and u_ok
+    if not (eq and d_ok and m_ok and g2_ok):
+        return None
+    out = [True] * len(segs)
+    for s_, s in enumerate(T):
+        out[s] = perT[s_]
+    return out
+
+
+def _segment_pass(r: RangeProofList, segs: list, redo: list, x: dict, comp: dict | None = None) -> dict:
     """Second, segment-grouped pass for the VNs ``redo`` whose batch failed:
     with the SAME weights, every side of the batch equation per (VN,
     segment) -- R MSM, prod a^rho, sum rho Zv, D-check, GT membership -- in
     one grouped MSM / multi-exponentiation each; the U side's per-segment products come from
-    the first pass.  -> {vn: [bool] per segment}."""
+    the first pass.  -> {vn: [bool] per segment}; ``comp`` receives the
+    per-(VN, segment) sides (host): lhs, e, dl, dr, GGgam (when computed), rok."""
     dev = r.V.device
     n, S, l = len(r), r.S, r.l
     m, nseg, Gf = n * S * l, len(segs), len(redo)
@@ -1311,6 +1428,8 @@ def _segment_pass(r: RangeProofList, segs: list, redo: list, x: dict) -> dict:
     with timers.span("rp.seg.gt_finish"):
         GG = nt.multi_exp_grouped_finish(mexp)                         # [gam_groups * K, 96]
         m_ok = _gt_in_subgroup_each(GG[K:]) if gam_groups == 2 else [True] * K
+    if comp is not None and gam_groups == 2:
+        comp["GGgam"] = GG[K:].cpu()
     GG = GG[:K]
     with timers.span("rp.seg.r_finish"):
         fR, rok = _msm_r_miller(hR, S_R)
@@ -1324,6 +1443,8 @@ def _segment_pass(r: RangeProofList, segs: list, redo: list, x: dict) -> dict:
     PB = nt.g1_mul(x["PB_base"].repeat(K, 1), torch.stack([dzr, dz], 1).reshape(-1, 8).contiguous()).view(K, 2, 24)
     lhs_d = nt.g1_sum(torch.stack([D_all[:, 0].reshape(K, 24), PB[:, 0], PB[:, 1]]).contiguous())
     d_ok = nt.g1_eq(lhs_d.contiguous(), D_all[:, 1].reshape(K, 24).contiguous()).tolist()
+    if comp is not None:
+        comp.update(lhs=lhs, e=e, dl=lhs_d, dr=D_all[:, 1].reshape(K, 24), rok=rok)
     out = {}
     for f, v in enumerate(redo):
         out[v] = [bool(eq[f * nseg + s_]) and bool(d_ok[f * nseg + s_]) and bool(useg_ok[f * nseg + s_])
@@ -1469,10 +1590,15 @@ def rpl_cat(lists: list) -> RangeProofList:
     if len(lists) == 1:
         return r0
     assert all((r.u, r.l, r.S) == (r0.u, r0.l, r0.S) for r in lists)
-    cat = lambda f: None if getattr(r0, f) is None else torch.cat([getattr(r, f) for r in lists])  # noqa: E731
+    # every field of every list in ONE batched-copy launch (torch.cat ran each
+    # field as its own ~50-workgroup kernel: ~10 ms per inbox on the trace)
+    fields = ("challenge", "zr", "D", "zphi", "zv", "V", "A")
+    have = [f for f in fields if getattr(r0, f) is not None]
+    outs = nt.cat_rows([[r.commit.K for r in lists], [r.commit.C for r in lists]]
+                       + [[getattr(r, f) for r in lists] for f in have])
+    got = dict(zip(have, outs[2:]))
     return RangeProofList(r0.u, r0.l, r0.S, [o for r in lists for o in r.offset], [c for r in lists for c in r.cols],
-                          CipherVector.cat([r.commit for r in lists]), cat("challenge"), cat("zr"), cat("D"),
-                          cat("zphi"), cat("zv"), cat("V"), cat("A"))
+                          CipherVector(outs[0], outs[1]), *[got.get(f) for f in fields])
 
 
 def rpl_range(r: RangeProofList, a: int, b: int) -> RangeProofList:

@@ -189,10 +189,11 @@ def schnorr_sign_batch(secrets: list, msgs: list, device="cpu") -> list:
     if n == 0:
         return []
     ks = [O.random_scalar() for _ in range(n)]
-    # a handful of envelopes (a CN's per-phase proofs) sign on the host pool:
-    # a device launch would queue behind the query's GPU work and add a
-    # device-to-host round trip (verification uses the same rule)
-    dev = torch.device(device) if n >= int(os.environ.get("DRYNX_SIGN_DEVICE_MIN", _SIG_DEVICE_MIN)) \
+    # signing stays on the device even for a handful of envelopes: host
+    # fixed-base products compete with the query's host threads (same-box
+    # A/B, profiles/r4/ab_bisect.txt: host signing of the per-CN proofs cost
+    # ~9 ms of a ~200 ms query); DRYNX_SIGN_DEVICE_MIN=k signs below k on the host
+    dev = torch.device(device) if n >= int(os.environ.get("DRYNX_SIGN_DEVICE_MIN", "1")) \
         else torch.device("cpu")
     pts = nt.g1_fb_mul(bn.base_table(dev), bn.scalars_tensor(ks + [int(x) for x in secrets], dev))
     enc = bn.g1_aff_to_bytes(nt.g1_to_affine(pts))

@@ -277,7 +277,8 @@ class DrynxNode:
         if net is not None:
             with_dps = sum(1 for dps in (sq.ServerToDP or {}).values() if dps)
             net.step("data_collection", [(si.id, cn, n_rows * CT_BYTES) for cn, dps in (sq.ServerToDP or {}).items()
-                                         for si in (dps or [])], hops=flow_hops("data_collection", nc, cns_with_dps=with_dps))
+                                         for si in (dps or [])],
+                     hops=flow_hops("data_collection", nc, cns_with_dps=with_dps))
         agg = cnp.collective_aggregation(self, sq, cn_sums, cn_inputs, n_rows, proofs)
         if net is not None:
             net.step("aggregation", [(c, p, n_rows * CT_BYTES) for c, p in tree_edges(cn_ids)],
@@ -362,10 +363,10 @@ class DrynxNode:
             return fut
         if not hasattr(self, "_cnp_pool"):
             self._cnp_pool = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="drynx-cn-proofs")
-            # high priority: the per-CN proofs (key switch last) gate the VNs' checks;
-            # at normal priority their short digest / response kernels queue behind
-            # the querier's high-priority decryption
-            self._cnp_stream = torch.cuda.Stream(self.device, priority=int(os.environ.get("DRYNX_CNP_PRIORITY", "-1")))
+            # normal priority (DRYNX_CNP_PRIORITY=-1: high): the same-box A/B
+            # (profiles/r4/ab_bisect.txt) measured the high-priority stream no
+            # faster -- its kernels then delay the querier's decryption instead
+            self._cnp_stream = torch.cuda.Stream(self.device, priority=int(os.environ.get("DRYNX_CNP_PRIORITY", "0")))
         side = self._cnp_stream
         side.wait_stream(torch.cuda.current_stream(self.device))
 

@@ -189,14 +189,26 @@ def test_segment_attribution(device, field, proofs, monkeypatch):
         A[-1, -1] ^= 1
         bad.A = A
         want = [True, True, False]
-    calls = []
-    orig = rp._segment_finish_kept
+    decodes = field != "A_off_gt"
+    calls, hinted = [], []
+    orig, orig_h = rp._segment_finish_kept, rp._segment_hinted
     monkeypatch.setattr(rp, "_segment_finish_kept", lambda *a: calls.append(1) or orig(*a))
+    monkeypatch.setattr(rp, "_segment_hinted", lambda *a: hinted.append(orig_h(*a)) or hinted[-1])
     monkeypatch.setenv("DRYNX_SEG_KEEP", "1")
     assert rp.verify_range_proof_list_multi(bad, sm, P, 2, dev, segs=[1, 2, 1]) == [want] * 2
-    assert calls, "the failing VNs' segments come from the first pass's kept buckets"
-    # the re-bucketing second pass (DRYNX_SEG_KEEP=0) names the same segments
+    # a proof that does not decode gets zero weights: the batch of the others
+    # passes, no second pass at all
+    assert bool(calls) == decodes, "the failing VNs' segments come from the first pass's kept buckets"
+    # the re-bucketing second pass (DRYNX_SEG_KEEP=0) names the same segments:
+    # the first failing VN's full pass, the others' from its hint
     monkeypatch.setenv("DRYNX_SEG_KEEP", "0")
+    assert rp.verify_range_proof_list_multi(bad, sm, P, 3, dev, segs=[1, 2, 1]) == [want] * 3
+    assert len(calls) == int(decodes)
+    assert len(hinted) == (2 if decodes else 0) and all(h == want for h in hinted)
+    monkeypatch.setenv("DRYNX_SEG_HINT", "0")
     assert rp.verify_range_proof_list_multi(bad, sm, P, 2, dev, segs=[1, 2, 1]) == [want] * 2
-    assert len(calls) == 1
+    monkeypatch.setenv("DRYNX_SEG_HINT", "1")
+    monkeypatch.setenv("DRYNX_RP_MASK", "0")                # round 3: every VN's segment pass
+    assert rp.verify_range_proof_list_multi(bad, sm, P, 2, dev, segs=[1, 2, 1]) == [want] * 2
+    monkeypatch.setenv("DRYNX_RP_MASK", "1")
     assert rp.verify_range_proof_list_multi(bad, sm, P, 2, dev) == [False] * 2

@@ -373,4 +373,5 @@ def test_coins_bits_keep_exactly_the_requested_width():
     from drynx_amd.proofs import range_proof as rp
 
     g = rp._rand64(4096, "cpu", 40)
-    assert int((g[:, 2:] != 0).sum()) == 0 and int((g[:, 1] & ~0xFF).abs().sum()) == 0 and int((g[:, 1] != 0).sum()) > 4000
+    assert int((g[:, 2:] != 0).sum()) == 0 and int((g[:, 1] & ~0xFF).abs().sum()) == 0
+    assert int((g[:, 1] != 0).sum()) > 4000

@@ -199,7 +199,8 @@ def main():
         if os.environ.get("RANK_SHARE_TRACE_ONLY") == "1":
             node.close(remove=True)
             return
-    res = {"world": W, "features": d, "placement": {k: {"parties": place.get(k, []), "dps": dps_of[k]} for k in range(W)},
+    res = {"world": W, "features": d,
+           "placement": {k: {"parties": place.get(k, []), "dps": dps_of[k]} for k in range(W)},
            "ranks": {}}
     for k in range(W):
         part = (k, W)
