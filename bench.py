@@ -248,7 +248,8 @@ def main():
     prof = _torch_profiler(rank)
     for _ in range(args.steps):
         ts = time.perf_counter()
-        res, weights = one_step()
+        with timers.span("bench.step"):  # a roctx range under DRYNX_ROCTX=1 (tools/span_kernels.py)
+            res, weights = one_step()
         step_ms.append(round(1000 * (time.perf_counter() - ts), 1))
         blocks.append(res.block)
         checks.append((weights, res.clear_dp))

@@ -46,6 +46,10 @@ def _dev_sync():
 
 
 PROFILE_SPANS = False  # tools set this under torch.profiler: spans become record_function ranges
+# DRYNX_ROCTX=1: every span is also a roctx range, so a rocprofv3
+# --runtime-trace run attributes each kernel to the innermost span that
+# launched it (tools/span_kernels.py)
+_ROCTX = os.environ.get("DRYNX_ROCTX") == "1"
 
 
 @contextlib.contextmanager
@@ -54,6 +58,13 @@ def span(name: str):
     if PROFILE_SPANS:
         with torch.profiler.record_function(name):
             yield
+        return
+    if _ROCTX:
+        torch.cuda.nvtx.range_push(name)
+        try:
+            yield
+        finally:
+            torch.cuda.nvtx.range_pop()
         return
     if not _TRACE:
         yield

@@ -1,0 +1,134 @@
+"""GPU time per framework span, from one rocprofv3 --runtime-trace run.
+
+Run the bench with DRYNX_ROCTX=1 (every ``timers.span`` / ``timers.timed`` is
+a roctx range) under ``rocprofv3 --runtime-trace --output-format csv -d D -o
+run -- python bench.py ...``; then
+
+    python tools/span_kernels.py D [--queries K] [--out file]
+
+joins each kernel (kernel_trace: name, device duration) to the HIP call that
+launched it (hip_api_trace: same Correlation_Id -> host thread and launch
+time) and that call to the innermost roctx range open on its thread at that
+moment (marker_api_trace).  Only kernels launched inside the last K
+``bench.step`` ranges count (the timed queries; per-query averages).
+Prints per span: kernel time, the part in non-hand-written kernels (torch /
+ATen, rocPRIM, runtime copies and fills = "glue") and its largest glue
+kernels -- the table behind the glue budget of profiles/r4/."""
+from __future__ import annotations
+
+import argparse
+import bisect
+import csv
+import glob
+import os
+from collections import defaultdict
+
+
+def _find(d, suffix):
+    got = sorted(glob.glob(os.path.join(d, "**", f"*{suffix}"), recursive=True))
+    if not got:
+        raise SystemExit(f"no *{suffix} under {d}")
+    return got[-1]
+
+
+def _col(row, *names):
+    for n in names:
+        if n in row:
+            return row[n]
+    raise KeyError(names)
+
+
+def glue(name: str) -> bool:
+    return ("at::native" in name or "rocclr" in name or "rocprim" in name or "at::cuda" in name
+            or "elementwise_kernel_with_index" in name or name.startswith("void (anonymous namespace)::elementwise"))
+
+
+def short(name: str) -> str:
+    for key, s in (("CatArrayBatchedCopy", "aten cat"), ("copyBuffer", "rocclr copyBuffer"),
+                   ("fillBuffer", "rocclr fillBuffer"), ("direct_copy", "aten copy/convert"),
+                   ("and_kernel", "aten all()"), ("onesweep", "rocprim sort"), ("index_elementwise", "aten index"),
+                   ("scatter_gather", "aten gather/scatter"), ("reduce_kernel", "aten reduce"),
+                   ("radixSort", "aten sort"), ("vectorized_elementwise", "aten elementwise"),
+                   ("arange", "aten arange"), ("lookback_scan", "rocprim scan")):
+        if key in name:
+            return s
+    n = name.split("(")[0]
+    return n[-60:]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dir")
+    ap.add_argument("--queries", type=int, default=3)
+    ap.add_argument("--window", default="bench.step")
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    kern = {}
+    with open(_find(a.dir, "kernel_trace.csv")) as f:
+        for r in csv.DictReader(f):
+            kern[int(r["Correlation_Id"])] = (r["Kernel_Name"],
+                                              (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
+    launch = {}
+    with open(_find(a.dir, "hip_api_trace.csv")) as f:
+        for r in csv.DictReader(f):
+            c = int(r["Correlation_Id"])
+            if c in kern and c not in launch:
+                launch[c] = (r["Thread_Id"], int(r["Start_Timestamp"]))
+    ranges = defaultdict(list)  # thread -> [(start, end, name)]
+    with open(_find(a.dir, "marker_api_trace.csv")) as f:
+        for r in csv.DictReader(f):
+            name = _col(r, "Function", "Message", "Name")
+            ranges[r["Thread_Id"]].append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), name))
+    for t in ranges:
+        ranges[t].sort()
+    wins = sorted((s, e) for rs in ranges.values() for s, e, n in rs if n == a.window)[-a.queries:]
+    if not wins:
+        raise SystemExit(f"no {a.window} ranges")
+    starts = {t: [x[0] for x in rs] for t, rs in ranges.items()}
+
+    def innermost(th, ts):
+        rs = ranges.get(th, [])
+        i = bisect.bisect_right(starts.get(th, []), ts)
+        best = None
+        for j in range(i - 1, max(-1, i - 400), -1):
+            s, e, n = rs[j]
+            if s <= ts <= e and (best is None or s > best[0]):
+                best = (s, e, n)
+                break
+        return best[2] if best else "(no span)"
+
+    tot = defaultdict(float)
+    gl = defaultdict(float)
+    cnt = defaultdict(int)
+    gk = defaultdict(lambda: defaultdict(float))
+    all_k = all_g = 0.0
+    for c, (name, dur) in kern.items():
+        if c not in launch:
+            continue
+        th, ts = launch[c]
+        if not any(s <= ts <= e for s, e in wins):
+            continue
+        sp = innermost(th, ts)
+        tot[sp] += dur
+        cnt[sp] += 1
+        all_k += dur
+        if glue(name):
+            gl[sp] += dur
+            all_g += dur
+            gk[sp][short(name)] += dur
+    q = len(wins)
+    lines = [f"# kernels launched inside the last {q} '{a.window}' ranges, per query (ms, serialized device time)",
+             f"# all kernels {all_k / q:.2f} ms, glue (torch/ATen, rocPRIM, runtime copies/fills) {all_g / q:.2f} ms",
+             f"{'span':40s} {'kernel_ms':>9s} {'glue_ms':>8s} {'n':>6s}  largest glue kernels"]
+    for sp in sorted(tot, key=lambda k: -tot[k]):
+        top = ", ".join(f"{k} {v / q:.2f}" for k, v in sorted(gk[sp].items(), key=lambda kv: -kv[1])[:3])
+        lines.append(f"{sp[:40]:40s} {tot[sp] / q:9.2f} {gl[sp] / q:8.2f} {cnt[sp] / q:6.0f}  {top}")
+    txt = "\n".join(lines) + "\n"
+    print(txt)
+    if a.out:
+        with open(a.out, "w") as f:
+            f.write(txt)
+
+
+if __name__ == "__main__":
+    main()
