@@ -40,7 +40,7 @@ from ..crypto import bn254 as bn
 from ..crypto import oracle as O
 from ..crypto.elgamal import CipherVector, pk_table
 from ..query import PublishSignatureBytes
-from ..utils import timers
+from ..utils import streams, timers
 from ..utils.log import get_logger
 
 log = get_logger("range_proof")
@@ -1580,7 +1580,7 @@ def _val_stream(device):
 def _aux_stream(device):
     key = str(device)
     if key not in _aux:
-        _aux[key] = torch.cuda.Stream(device, priority=-1)  # plans: short kernels overtake the pairing side
+        _aux[key] = torch.cuda.Stream(device, priority=streams.priority(-1))  # plans: short kernels overtake the pairing side
     return _aux[key]
 
 

@@ -709,10 +709,14 @@ def _ks_combined(live, n_vn: int = 1, coins=None):
         # by one GLV variable-base launch and the 5 nl n_vn group sums by a
         # chunked tree -- no bucket plan and its host sync; group sums and za
         # dots come back in ONE copy
-        k0 = ks[0]
-        abs_ = AB.view(n_vn, 2 * kt, 2).index_select(1, sel_t).reshape(-1, 2).contiguous()
-        prod = nt.g1_mul_glv(pts.contiguous().repeat(n_vn, 1), abs_).view(5 * nl * n_vn, k0, 24)
-        sums = nt.g1_sum(prod.transpose(0, 1).contiguous())
+        k0, ng = ks[0], 5 * nl
+        # item-major [k0, n_vn * ng] layout: the group sums are g1_sum's axis-0
+        # reduction of the products as launched (no transposed copy of them)
+        pts_t = pts.view(ng, k0, 24).transpose(0, 1).unsqueeze(1).expand(k0, n_vn, ng, 24).reshape(-1, 24)
+        abs_ = AB.view(n_vn, 2 * kt, 2).index_select(1, sel_t).view(n_vn, ng, k0, 2)
+        abs_t = abs_.permute(2, 0, 1, 3).reshape(-1, 2).contiguous()
+        prod = nt.g1_mul_glv(pts_t.contiguous(), abs_t).view(k0, n_vn * ng, 24)
+        sums = nt.g1_sum(prod)
         both = torch.cat([sums.reshape(-1), full.reshape(-1)]).cpu()
         G = both[: sums.numel()].view(-1, 24)
         full = both[sums.numel():].view(-1, 8)

@@ -339,7 +339,15 @@ def start_range_plane(ctx, sq, range_requests: list) -> dict:
     vns = [ctx.cluster.by_id(si.id) for si in sq.Query.RosterVNs.list]
     with timers.timed("RangeFanOut"):
         reqs = fan_out(ctx, sq, range_requests, pool=True)
-    return {"reqs": reqs, "pooled": _pool_async(ctx, sq, reqs, vns, ctx.comm.plane("pool"))}
+    out = {"reqs": reqs, "pooled": _pool_async(ctx, sq, reqs, vns, ctx.comm.plane("pool"))}
+    if any(vn.rank == ctx.rank for vn in vns) and hasattr(ctx, "ledger_values"):
+        # the stored payloads' device-to-host copy starts now, under the pooled
+        # verification, instead of at the verdicts (store_verdicts finds them
+        # in the rank's blob segment); payloads whose digest is not known yet
+        # (received ones: a digest here would wait for the exchange) go then
+        with timers.span("ledger.prefetch"):
+            ctx.ledger_values([r for r in reqs if r.kind == "range" and r.data_digest])
+    return out
 
 
 def early_plane_ok(ctx, sq) -> bool:

@@ -39,7 +39,7 @@ from ..protocols import computing_nodes as cnp
 from ..protocols import data_collection as dcp
 from ..protocols import proof_collection as pcp
 from ..query import PublishSignatureBytes, SurveyQuery, add_diff_p, check_parameters, ivsigs_digest
-from ..utils import timers
+from ..utils import streams, timers
 
 from ..utils.faults import FaultPlan
 from ..utils.log import get_logger
@@ -176,17 +176,21 @@ class DrynxNode:
         sizes = [t.numel() for t in tensors]
         if not tensors[0].is_cuda:
             return lambda: [memoryview(t.numpy()) for t in tensors]
-        flat = torch.cat(tensors) if len(tensors) > 1 else tensors[0]
         if not hasattr(self, "_ledger_stream"):
             self._ledger_stream = torch.cuda.Stream(self.device)
         st = self._ledger_stream
         st.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(st):
-            host = torch.empty(flat.shape, dtype=torch.uint8, pin_memory=True)
-            host.copy_(flat, non_blocking=True)
+            # each payload straight into its slice of one pinned buffer (no
+            # device-side concatenation of the ~600 MB of range payloads)
+            host = torch.empty((sum(sizes),), dtype=torch.uint8, pin_memory=True)
+            o = 0
+            for t, n in zip(tensors, sizes):
+                host[o: o + n].copy_(t, non_blocking=True)
+                t.record_stream(st)
+                o += n
             ev = torch.cuda.Event()
             ev.record(st)
-        flat.record_stream(st)
 
         def produce():
             ev.synchronize()
@@ -223,7 +227,7 @@ class DrynxNode:
         if self.device.type != "cuda" or os.environ.get("DRYNX_HP_STREAM", "1") == "0":
             return self._run_survey(sq, on_result)
         if not hasattr(self, "_hp_stream"):
-            self._hp_stream = torch.cuda.Stream(self.device, priority=-1)
+            self._hp_stream = torch.cuda.Stream(self.device, priority=streams.priority(-1))
         hp, outer = self._hp_stream, torch.cuda.current_stream(self.device)
         hp.wait_stream(outer)
         with torch.cuda.stream(hp):
@@ -366,7 +370,8 @@ class DrynxNode:
             # normal priority (DRYNX_CNP_PRIORITY=-1: high): the same-box A/B
             # (profiles/r4/ab_bisect.txt) measured the high-priority stream no
             # faster -- its kernels then delay the querier's decryption instead
-            self._cnp_stream = torch.cuda.Stream(self.device, priority=int(os.environ.get("DRYNX_CNP_PRIORITY", "0")))
+            prio = streams.priority(int(os.environ.get("DRYNX_CNP_PRIORITY", "0")))
+            self._cnp_stream = torch.cuda.Stream(self.device, priority=prio)
         side = self._cnp_stream
         side.wait_stream(torch.cuda.current_stream(self.device))
 
@@ -400,7 +405,7 @@ class DrynxNode:
         if not hasattr(self, "_client_stream"):
             # high priority: the querier's decrypt/BSGS kernels are short and
             # would otherwise queue behind the VNs' MSM passes (75 ms vs 10 ms)
-            self._client_stream = torch.cuda.Stream(self.device, priority=-1)
+            self._client_stream = torch.cuda.Stream(self.device, priority=streams.priority(-1))
         side = self._client_stream
         side.wait_stream(torch.cuda.current_stream(self.device))  # result tensors are ready on `side`
 
