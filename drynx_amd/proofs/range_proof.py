@@ -1580,7 +1580,8 @@ def _val_stream(device):
 def _aux_stream(device):
     key = str(device)
     if key not in _aux:
-        _aux[key] = torch.cuda.Stream(device, priority=streams.priority(-1))  # plans: short kernels overtake the pairing side
+        # plans: short kernels overtake the pairing side
+        _aux[key] = torch.cuda.Stream(device, priority=streams.priority(-1))
     return _aux[key]
 
 

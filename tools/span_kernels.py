@@ -81,7 +81,7 @@ def main():
     # kernels running then, in proportion to their workgroups (capped at the
     # chip's resident slots) -- a one-workgroup kernel beside a full-chip one
     # is charged ~nothing for the wait, not its whole stretched duration
-    ev = sorted([(s_, 1, i) for i, (s_, e_, c_, w_) in enumerate(iv)] + [(e_, 0, i) for i, (s_, e_, c_, w_) in enumerate(iv)])
+    ev = sorted([(x[0], 1, i) for i, x in enumerate(iv)] + [(x[1], 0, i) for i, x in enumerate(iv)])
     active, wsum, last = set(), 0, None
     for t, kind, i in ev:
         if last is not None and active and t > last:
@@ -144,7 +144,8 @@ def main():
             all_g += dur
             gk[sp][short(name)] += dur
     q = len(wins)
-    lines = [f"# kernels launched inside the last {q} '{a.window}' ranges, per query (ms of device time, overlap shared by workgroups)",
+    lines = [f"# kernels launched inside the last {q} '{a.window}' ranges, per query "
+             "(ms of device time, overlap shared by workgroups)",
              f"# all kernels {all_k / q:.2f} ms, glue (torch/ATen, rocPRIM, runtime copies/fills) {all_g / q:.2f} ms",
              f"{'span':40s} {'kernel_ms':>9s} {'glue_ms':>8s} {'n':>6s}  largest glue kernels"]
     for sp in sorted(tot, key=lambda k: -tot[k]):
