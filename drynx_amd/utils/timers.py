@@ -59,25 +59,23 @@ def span(name: str):
         with torch.profiler.record_function(name):
             yield
         return
-    if _ROCTX:
-        torch.cuda.nvtx.range_push(name)
-        try:
-            yield
-        finally:
-            torch.cuda.nvtx.range_pop()
-        return
-    if not _TRACE:
+    if not _TRACE and not _ROCTX:
         yield
         return
     if _SPAN_SYNC:
         _dev_sync()
+    if _ROCTX:
+        torch.cuda.nvtx.range_push(name)
     t0 = time.perf_counter_ns()
     try:
         yield
     finally:
         if _SPAN_SYNC:
             _dev_sync()
-        _emit(name, t0, time.perf_counter_ns())
+        if _ROCTX:
+            torch.cuda.nvtx.range_pop()
+        if _TRACE:
+            _emit(name, t0, time.perf_counter_ns())
 
 
 def dump_trace(path: str | None = None):

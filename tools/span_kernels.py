@@ -144,9 +144,26 @@ def main():
             all_g += dur
             gk[sp][short(name)] += dur
     q = len(wins)
+    # wall and device-busy time of the windows (union of kernel intervals inside them)
+    wall = sum(e - s_ for s_, e in wins) / 1e6 / q
+    busy = 0
+    for ws, we in wins:
+        segs = sorted((max(x[0], ws), min(x[1], we)) for x in iv if x[1] > ws and x[0] < we)
+        cur_s = cur_e = None
+        for s_, e in segs:
+            if cur_e is None or s_ > cur_e:
+                if cur_e is not None:
+                    busy += cur_e - cur_s
+                cur_s, cur_e = s_, e
+            else:
+                cur_e = max(cur_e, e)
+        if cur_e is not None:
+            busy += cur_e - cur_s
+    busy = busy / 1e6 / q
     lines = [f"# kernels launched inside the last {q} '{a.window}' ranges, per query "
              "(ms of device time, overlap shared by workgroups)",
              f"# all kernels {all_k / q:.2f} ms, glue (torch/ATen, rocPRIM, runtime copies/fills) {all_g / q:.2f} ms",
+             f"# window wall {wall:.2f} ms, device busy {busy:.2f} ms ({100 * busy / max(wall, 1e-9):.0f}%)",
              f"{'span':40s} {'kernel_ms':>9s} {'glue_ms':>8s} {'n':>6s}  largest glue kernels"]
     for sp in sorted(tot, key=lambda k: -tot[k]):
         top = ", ".join(f"{k} {v / q:.2f}" for k, v in sorted(gk[sp].items(), key=lambda kv: -kv[1])[:3])
