@@ -884,7 +884,12 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
 
     _sw = timers.span("rp.verify.weights")
     _sw.__enter__()
-    w_all = _cat_draw(lambda c: c.bits(n, device, 64) if c is not None else _rand64(n, device))  # D-equation weights
+    # D-equation weights, GLV-shaped like rho (a + b lambda, 32-bit halves:
+    # the same 2^-64 soundness as uniform 64-bit weights), so the D-check can
+    # run as 32-doubling GLV ladders with no bucket plan
+    wpairs = [c.glv(n, device) if c is not None else nt.glv_weights(n, device) for c in cl]
+    wab_all = torch.cat([p_[0] for p_ in wpairs]) if G > 1 else wpairs[0][0]
+    w_all = torch.cat([p_[1] for p_ in wpairs]) if G > 1 else wpairs[0][1]
     # pairing-equation weights: rho = a + b lambda (GLV, a and b 32-bit: 2^64
     # distinct residues, so the same 2^-64 soundness as uniform 64-bit weights;
     # csrc/kernels/dx_glv.hip)
@@ -907,6 +912,7 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
         vm = (valid if chk is None else valid & chk).to(torch.int32)
         mi = vm.repeat_interleave(S * l).view(1, m, 1)
         w_all = (w_all.view(G, n, 8) * vm.view(1, n, 1)).view(G * n, 8)
+        wab_all = (wab_all.view(G, n, 2) * vm.view(1, n, 1)).view(G * n, 2)
         ab_all = (ab_all.view(G, m, 2) * mi).view(G * m, 2)
         rho_all = (rho_all.view(G, m, 8) * mi).view(G * m, 8)
         gam_all = (gam_all.view(G, m, 8) * mi).view(G * m, 8)
@@ -953,11 +959,20 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
         if use_msm and aux is not None:
             with timers.span("rp.plan.R"):
                 hR = _msm_plan(r.zphi, r.V, rho_all, G, n, S, l)
-        dpts = torch.cat([Cp.contiguous(), r.D.contiguous()]).repeat(G, 1)
-        wc = nt.fr_arith(nt.FR_MUL, w_all, r.challenge.repeat(G, 1))
-        dsc = torch.stack([wc.view(G, n, 8), w_all.view(G, n, 8)], 1).reshape(-1, 8).contiguous()
+        # D-check sums (sum w c C', sum w D) per VN: on a GPU without a bucket
+        # plan -- c C' once for every VN, then each VN's 32-bit GLV ladders and
+        # a chunked tree sum (no host sync: a 1/W pool slice spent ~5 ms in the
+        # plan's sort and sync); DRYNX_DCHECK=msm keeps the bucket MSM
+        dmode = os.environ.get("DRYNX_DCHECK", "auto")  # auto: direct on a GPU; direct / msm: forced
+        ddirect = fold == 1 and (dmode == "direct" or (dmode == "auto" and device.type == "cuda"))
+        if not ddirect:
+            dpts = torch.cat([Cp.contiguous(), r.D.contiguous()]).repeat(G, 1)
+            wc = nt.fr_arith(nt.FR_MUL, w_all, r.challenge.repeat(G, 1))
+            dsc = torch.stack([wc.view(G, n, 8), w_all.view(G, n, 8)], 1).reshape(-1, 8).contiguous()
         with timers.span("rp.plan.D"):
-            if fold > 1:  # group = ((v, which) row // n, segment of the proof)
+            if ddirect:
+                dplan = None
+            elif fold > 1:  # group = ((v, which) row // n, segment of the proof)
                 dgrp = (torch.arange(2 * G, device=device).view(-1, 1) * fold
                         + pseg.view(1, n)).reshape(-1).to(torch.int32)
                 dplan = nt.g1_msm_plan(dsc, dgrp, 2 * G * fold)
@@ -996,7 +1011,14 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
             with timers.span("rp.run.R"):
                 S_R = nt.g2_msm_run(r.V, hR)                           # R window sums
         with timers.span("rp.run.D"):
-            dcheck = nt.g1_msm_launch(dpts, dsc, dgrp, 2 * G * fold, bits=256, plan=dplan, fold=fold)
+            if ddirect:
+                cC = nt.g1_mul(Cp.contiguous(), r.challenge.contiguous())     # shared by the VNs
+                pts = torch.stack([cC, r.D], 1).unsqueeze(1).expand(n, G, 2, 24).reshape(-1, 24)
+                abs_ = wab_all.view(G, n, 2).permute(1, 0, 2).unsqueeze(2).expand(n, G, 2, 2).reshape(-1, 2)
+                # item-major [n, 2G]: group v * 2 + which, summed over the proofs
+                dcheck = nt.g1_sum(nt.g1_mul_glv(pts.contiguous(), abs_.contiguous()).view(n, 2 * G, 24))
+            else:
+                dcheck = nt.g1_msm_launch(dpts, dsc, dgrp, 2 * G * fold, bits=256, plan=dplan, fold=fold)
         e_all = nt.fr_dot_rows(rho_all, r.zv, G, b_periodic=True)                        # sum rho Zv per VN
         dfull = torch.stack([nt.fr_dot_rows(w_all, r.zr, G, b_periodic=True),
                              nt.fr_dot_rows(w_all, z, G, b_periodic=True)], 1)             # [G, 2, 8]
@@ -1004,7 +1026,7 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
         with timers.span("rp.verify.multiexp"):
             aux.synchronize()                                          # aux results are read on this stream/host
             GG = nt.multi_exp_grouped_finish(mexp)                     # [2G, 96]: prod a^rho_v, prod a^gamma_v
-            D_all = nt.g1_msm_finish(dcheck)                           # [2G, 24]
+            D_all = dcheck.cpu() if ddirect else nt.g1_msm_finish(dcheck)  # [2G, 24]
             e_all, dfull = e_all.cpu(), dfull.cpu()
         with timers.span("rp.verify.fold_wait"):
             if use_msm:
@@ -1034,7 +1056,7 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
                 f = nt.miller_loop(nt.g1_to_affine(nt.g1_mul(T, v["rho"])), r.V)
                 v["F"] = nt.gt_prod(f.view(-1, 1, 96), chunk=4).view(1, 96)
     if device.type != "cuda":
-        D_all = nt.g1_msm_finish(dcheck)                               # [2G, 24]
+        D_all = dcheck.cpu() if ddirect else nt.g1_msm_finish(dcheck)  # [2G, 24]
         e_all, dfull = e_all.cpu(), dfull.cpu()
     for k, v in enumerate(vns):
         v.update(G=GG[k: k + 1], dfull=dfull[k], e=e_all[k: k + 1], dcheck=D_all[2 * k: 2 * k + 2])

@@ -212,3 +212,21 @@ def test_segment_attribution(device, field, proofs, monkeypatch):
     assert rp.verify_range_proof_list_multi(bad, sm, P, 2, dev, segs=[1, 2, 1]) == [want] * 2
     monkeypatch.setenv("DRYNX_RP_MASK", "1")
     assert rp.verify_range_proof_list_multi(bad, sm, P, 2, dev) == [False] * 2
+
+
+@pytest.mark.parametrize("device", DEVICES)
+@pytest.mark.parametrize("dmode", ["direct", "msm"])
+def test_dcheck_direct_and_bucket_agree(device, dmode, proofs, monkeypatch):
+    """The D-check as GLV ladders + tree sums (no bucket plan) and as the
+    bucket MSM accept the same batch and reject a tampered Zr, with per-VN
+    attribution."""
+    dev = _dev(device)
+    monkeypatch.setenv("DRYNX_DCHECK", dmode)
+    rpl, sm, P = proofs
+    assert rp.verify_range_proof_list_multi(rpl.to(dev), sm, P, 3, dev, segs=[1, 2, 1]) == [[True] * 3] * 3
+    bad = rpl.to(dev)
+    zr = bad.zr.clone()
+    zr[1, 0] ^= 1
+    bad.zr = zr
+    assert rp.verify_range_proof_list_multi(bad, sm, P, 3, dev, segs=[1, 2, 1]) == [[True, False, True]] * 3
+    assert rp.verify_range_proof_list_multi(bad, sm, P, 2, dev) == [False] * 2
