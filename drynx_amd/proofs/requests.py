@@ -984,16 +984,27 @@ def verify_requests(reqs: list, sq, vn_id: str, vn_index: int, n_vns: int, devic
                         log.warning(f"{vn_id}: {kind} proof from {reqs[i].sender_id} rejected: {e}")
                         ok = False
                     codes[i] = PROOF_TRUE if ok else PROOF_FALSE
-    if dev_flags:
-        with timers.span("verify.flags"):
-            flags = torch.stack([f.reshape(()) for _, f in dev_flags]).cpu().tolist()
-        for (i, _), ok in zip(dev_flags, flags):
-            codes[i] = PROOF_TRUE if ok else PROOF_FALSE
-    if range_future is not None:
-        for i, code in range_future.result():
-            codes[i] = code
+    # the device verdicts (aggregation sums) are read back when the codes are
+    # resolved: co-hosted VNs then queue all their checks before the first
+    # read, and pay one device round trip between them instead of one each
+    flag_t = torch.stack([f.reshape(()) for _, f in dev_flags]) if dev_flags else None
+
+    def read_flags():
+        if flag_t is not None:
+            with timers.span("verify.flags"):
+                flags = flag_t.cpu().tolist()
+            for (i, _), ok in zip(dev_flags, flags):
+                codes[i] = PROOF_TRUE if ok else PROOF_FALSE
+        if range_future is not None:
+            for i, code in range_future.result():
+                codes[i] = code
+
+    if not defer:
+        read_flags()
 
     def resolve():
+        if defer:
+            read_flags()
         if pooled_idx:
             with timers.span("rp.verify.pooled_wait"):
                 pooled = range_pooled.result() if hasattr(range_pooled, "result") else range_pooled
