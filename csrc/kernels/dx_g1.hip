@@ -28,12 +28,13 @@ namespace {
 // Montgomery form: x * (yR) * R^-1 = x y.
 template <int OPC>
 int fr_arith_t(int on_gpu, void *stream, const uint32_t *a, const uint32_t *b, uint32_t *out, int64_t n,
-               int b_bcast) {
+               int64_t b_bcast) {
   auto op = [=] __host__ __device__(int64_t i) {
     Fr x = reduce_256<FrParams>(a + 8 * i);
     Fr r;
     if constexpr (OPC == 0 || OPC == 1 || OPC == 2) {
-      Fr y = b ? reduce_256<FrParams>(b + 8 * (b_bcast ? 0 : i)) : Fr::zero();
+      // b_bcast = k > 0: b has k rows, row i reads b[i % k] (1: one broadcast scalar)
+      Fr y = b ? reduce_256<FrParams>(b + 8 * (b_bcast ? i % b_bcast : i)) : Fr::zero();
       if constexpr (OPC == 0) r = fadd(x, y);
       else if constexpr (OPC == 1) r = fsub(x, y);
       else r = fmul(x, to_mont(y));
@@ -53,7 +54,7 @@ int fr_arith_t(int on_gpu, void *stream, const uint32_t *a, const uint32_t *b, u
 extern "C" {
 
 int dx_fr_arith(int on_gpu, void *stream, int opc, const uint32_t *a, const uint32_t *b, uint32_t *out, int64_t n,
-                int b_bcast) {
+                int64_t b_bcast) {
   switch (opc) {
     case 0: return fr_arith_t<0>(on_gpu, stream, a, b, out, n, b_bcast);
     case 1: return fr_arith_t<1>(on_gpu, stream, a, b, out, n, b_bcast);

@@ -55,7 +55,7 @@ _U64 = ctypes.c_uint64
 _SIGS = {
     "dx_fp_to_mont": [_I, _P, _P, _P, _L],
     "dx_fp_from_mont": [_I, _P, _P, _P, _L],
-    "dx_fr_arith": [_I, _P, _I, _P, _P, _P, _L, _I],
+    "dx_fr_arith": [_I, _P, _I, _P, _P, _P, _L, _L],
     "dx_fr_dot_chunks": [_I, _P, _P, _P, _I, _P, _L, _L, _L],
     "dx_fr_seg_sum": [_I, _P, _P, _P, _P, _L],
     "dx_rp_challenges": [_I, _P, _P, _P, _P, _P, _P, _L],
@@ -293,10 +293,14 @@ FR_ADD, FR_SUB, FR_MUL, FR_NEG, FR_INV, FR_REDUCE = range(6)
 
 
 def fr_arith(op: int, a: torch.Tensor, b: torch.Tensor | None = None) -> torch.Tensor:
+    """Row-wise Fr op of a [n, 8] with b: n rows, or k rows read periodically
+    (row i uses b[i % k]; k = 1 broadcasts one scalar), canonical in and out."""
     n = _rows(a, 8)
     out = torch.empty_like(a)
     bb = b.contiguous() if b is not None else None
-    bcast = 1 if (bb is not None and bb.numel() == 8 and n != 1) else 0
+    nb = _rows(bb, 8) if bb is not None else 0
+    bcast = nb if (bb is not None and nb != n) else 0
+    assert bcast == 0 or n % nb == 0, (n, nb)
     g, s = _ctx(a, bb)
     _call("dx_fr_arith", g, s, op, _ptr(a), _ptr(bb), _ptr(out), n, bcast)
     return out

@@ -967,7 +967,7 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
         ddirect = fold == 1 and (dmode == "direct" or (dmode == "auto" and device.type == "cuda"))
         if not ddirect:
             dpts = torch.cat([Cp.contiguous(), r.D.contiguous()]).repeat(G, 1)
-            wc = nt.fr_arith(nt.FR_MUL, w_all, r.challenge.repeat(G, 1))
+            wc = nt.fr_arith(nt.FR_MUL, w_all, r.challenge)
             dsc = torch.stack([wc.view(G, n, 8), w_all.view(G, n, 8)], 1).reshape(-1, 8).contiguous()
         with timers.span("rp.plan.D"):
             if ddirect:
@@ -1148,7 +1148,7 @@ def _msm_plan(zphi, V, rho_all, G: int, n: int, S: int, L: int) -> dict:
     m = n * S * L
     it = torch.arange(m, device=dev)
     zi = (it // (S * L)) * L + it % L
-    s_r = nt.fr_arith(nt.FR_MUL, rho_all, zphi.index_select(0, zi).repeat(G, 1).contiguous())
+    s_r = nt.fr_arith(nt.FR_MUL, rho_all, zphi.index_select(0, zi).contiguous())  # periodic over the VNs
     return nt.g2_msm_launch(V, s_r, m, G, c=_r_window(m, G))          # group (VN) = row // m
 
 
@@ -1408,7 +1408,7 @@ def _segment_pass(r: RangeProofList, segs: list, redo: list, x: dict, comp: dict
     # R_(v,s) = sum_{it in s} rho_it Zphi_(p,j) V_it
     it = torch.arange(m, device=dev)
     zi = (it // (S * l)) * l + it % l
-    s_r = nt.fr_arith(nt.FR_MUL, rho, r.zphi.index_select(0, zi).repeat(Gf, 1).contiguous())
+    s_r = nt.fr_arith(nt.FR_MUL, rho, r.zphi.index_select(0, zi).contiguous())
     grp = (fi * nseg + iseg.view(1, m)).reshape(-1).to(torch.int32)
     # prod a^rho per (v, s) (32-bit halves over (A, frob^8 A)) and -- only
     # for a VN whose first-pass GT-membership combination failed -- each
@@ -1427,7 +1427,7 @@ def _segment_pass(r: RangeProofList, segs: list, redo: list, x: dict, comp: dict
     fi2 = torch.arange(gam_groups * Gf, device=dev).view(gam_groups * Gf, 1)
     grp2 = (fi2 * nseg + iseg.repeat(2).view(1, 2 * m)).reshape(-1).to(torch.int32)
     # D-check per (v, s): sum w c C' - sum w D (groups (v, which, s))
-    wc = nt.fr_arith(nt.FR_MUL, w, r.challenge.repeat(Gf, 1).contiguous())
+    wc = nt.fr_arith(nt.FR_MUL, w, r.challenge.contiguous())
     dsc = torch.stack([wc.view(Gf, n, 8), w.view(Gf, n, 8)], 1).reshape(-1, 8).contiguous()
     grp3 = ((fi.view(Gf, 1, 1) * 2 + torch.arange(2, device=dev).view(1, 2, 1)) * nseg
             + pseg.view(1, 1, n)).reshape(-1).to(torch.int32)
@@ -1444,8 +1444,8 @@ def _segment_pass(r: RangeProofList, segs: list, redo: list, x: dict, comp: dict
     offs = torch.from_numpy((np.arange(Gf).reshape(Gf, 1) * n + poff[:-1].reshape(1, nseg)).reshape(-1))
     offs = bn.h2d(torch.cat([offs, torch.tensor([Gf * n])]), dev)
     e = nt.fr_seg_sum(nt.fr_dot_rows(rho, r.zv.repeat(Gf, 1).contiguous(), Gf * n), offs)
-    dzr = nt.fr_seg_sum(nt.fr_arith(nt.FR_MUL, w, r.zr.repeat(Gf, 1).contiguous()), offs)
-    dz = nt.fr_seg_sum(nt.fr_arith(nt.FR_MUL, w, x["z"].repeat(Gf, 1).contiguous()), offs)
+    dzr = nt.fr_seg_sum(nt.fr_arith(nt.FR_MUL, w, r.zr.contiguous()), offs)
+    dz = nt.fr_seg_sum(nt.fr_arith(nt.FR_MUL, w, x["z"].contiguous()), offs)
     # host: Horner steps, Miller loops of B with each R_(v,s), final exps
     with timers.span("rp.seg.gt_finish"):
         GG = nt.multi_exp_grouped_finish(mexp)                         # [gam_groups * K, 96]
@@ -1491,7 +1491,7 @@ def _segment_finish_kept(r: RangeProofList, segs: list, redo: list, x: dict, row
     # per segment (a G2 plan kept per segment would hold nseg x the buckets)
     it = torch.arange(m, device=dev)
     zi = (it // (r.S * r.l)) * r.l + it % r.l
-    s_r = nt.fr_arith(nt.FR_MUL, rho, r.zphi.index_select(0, zi).repeat(Gf, 1).contiguous())
+    s_r = nt.fr_arith(nt.FR_MUL, rho, r.zphi.index_select(0, zi).contiguous())
     iseg = pseg.repeat_interleave(r.S * r.l)
     grp = (torch.arange(Gf, device=dev).view(Gf, 1) * nseg + iseg.view(1, m)).reshape(-1).to(torch.int32)
     with timers.span("rp.seg.plans"):
@@ -1502,8 +1502,8 @@ def _segment_finish_kept(r: RangeProofList, segs: list, redo: list, x: dict, row
     offs = torch.from_numpy((np.arange(Gf).reshape(Gf, 1) * n + poff[:-1].reshape(1, nseg)).reshape(-1))
     offs = bn.h2d(torch.cat([offs, torch.tensor([Gf * n])]), dev)
     e = nt.fr_seg_sum(nt.fr_dot_rows(rho, r.zv.repeat(Gf, 1).contiguous(), Gf * n), offs)
-    dzr = nt.fr_seg_sum(nt.fr_arith(nt.FR_MUL, w, r.zr.repeat(Gf, 1).contiguous()), offs)
-    dz = nt.fr_seg_sum(nt.fr_arith(nt.FR_MUL, w, x["z"].repeat(Gf, 1).contiguous()), offs)
+    dzr = nt.fr_seg_sum(nt.fr_arith(nt.FR_MUL, w, r.zr.contiguous()), offs)
+    dz = nt.fr_seg_sum(nt.fr_arith(nt.FR_MUL, w, x["z"].contiguous()), offs)
     with timers.span("rp.seg.gt_finish"):
         GG = nt.multi_exp_seg_finish(kept["mexp"], list(redo))                 # [K, 96] prod a^rho per (v, s)
         if any(not x["m_first"][v] for v in redo):
