@@ -61,17 +61,32 @@ def _copies() -> int:
     return max(1, int(os.environ.get("DRYNX_LEDGER_COPIES", "1")))
 
 
+def _gb_env(name: str, default: float) -> float:
+    return float(os.environ.get(name, default)) * (1 << 30)
+
+
 class BlobSegment:
-    """Append-only file of large ledger values shared by the VNs of one rank:
+    """Append-only files of large ledger values shared by the VNs of one rank:
     the same proof payload is written once, however many co-hosted VNs store
     it.  Values are produced by a callable on the segment's own worker thread
     (and, on a GPU, its own HIP stream: device-to-host copies never queue on
-    the compute streams)."""
+    the compute streams).
+
+    Disk budget: a query's range proofs are ~0.55 GB per VN rank (three VN
+    ranks on an 8-GPU node write ~1.7 GB per query; a 79 GB box disk fills
+    in ~45 queries).  Values go to generation files of at most
+    DRYNX_LEDGER_SEGMENT_GB (default 4); before a write that would leave less
+    than DRYNX_LEDGER_RESERVE_GB (default 8) free, the oldest generations of
+    this rank are deleted (their proofs are no longer served by ``get_proofs``;
+    bitmaps, blocks and small proofs stay in the database).
+    DRYNX_LEDGER_RETAIN=all keeps everything (and fails when the disk is
+    full), as the reference's bbolt store."""
 
     def __init__(self, path: str, device=None):
         import concurrent.futures as cf
 
-        self.path = path
+        self.base = self.path = path
+        self._gens: list = [path]  # generation files, oldest first
         os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
         self._f = open(path, "ab")
         self._ex = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="drynx-ledger")
@@ -124,12 +139,13 @@ class BlobSegment:
             with timers.span("ledger.encode"):
                 data = produce()
         with timers.span("ledger.write"):
+            bufs = [memoryview(d).cast("B") for d in (data if many else [data])]
+            self._make_room(sum(b.nbytes for b in bufs) * _copies())
             self._f.flush()
             off = self._f.seek(0, os.SEEK_END)
-            bufs = [memoryview(d).cast("B") for d in (data if many else [data])]
             out, pos = [], off
             for b in bufs:
-                out.append((pos, b.nbytes))
+                out.append((pos, b.nbytes, self.path))  # the generation file it lands in
                 pos += b.nbytes
             self._pwrite_all(bufs, off)
             self._f.seek(0, os.SEEK_END)
@@ -140,6 +156,47 @@ class BlobSegment:
         return out if many else out[0]
 
     _PIECE = 32 << 20  # bytes per parallel write
+    pruned = 0  # generation files deleted for disk space (this process)
+
+    def _files_of(self, path: str) -> list:
+        return [path] + [f"{path}.copy{j}" for j in range(1, _copies())]
+
+    def _rotate(self):
+        """Start a new generation file (the old one stays readable)."""
+        self._f.close()
+        fds = self.__dict__.get("_pfds", {})
+        for p in self._files_of(self.path):
+            fd = fds.pop(p, None)
+            if fd is not None:
+                os.close(fd)
+        self.path = f"{self.base}.{len(self._gens)}"
+        self._gens.append(self.path)
+        self._f = open(self.path, "ab")
+
+    def _make_room(self, need: int):
+        import shutil
+
+        if self._f.seek(0, os.SEEK_END) + need > _gb_env("DRYNX_LEDGER_SEGMENT_GB", 4) and \
+                self._f.tell() > 0:
+            self._rotate()
+        if os.environ.get("DRYNX_LEDGER_RETAIN", "") == "all":
+            return
+        reserve = _gb_env("DRYNX_LEDGER_RESERVE_GB", 8)
+        d = os.path.dirname(os.path.abspath(self.path))
+        while shutil.disk_usage(d).free - need < reserve and len(self._gens) > 1 and self._gens[0] != self.path:
+            old = self._gens.pop(0)
+            for p in self._files_of(old):
+                try:
+                    os.remove(p)
+                except FileNotFoundError:
+                    pass
+            BlobSegment.pruned += 1
+            if BlobSegment.pruned == 1:
+                import logging
+
+                logging.getLogger("drynx_amd").warning(
+                    f"ledger: disk below the {reserve / (1 << 30):.0f} GB reserve, deleting the oldest proof "
+                    f"segments of {self.base} (DRYNX_LEDGER_RETAIN=all keeps them)")
 
     def _pwrite_all(self, bufs: list, off: int, path: str | None = None):
         """The buffers back to back from ``off``, in pieces written by several
@@ -185,13 +242,13 @@ class BlobSegment:
         self._f.close()
         for path, fd in self.__dict__.pop("_pfds", {}).items():
             os.close(fd)
-            if remove and path != self.path:
-                os.remove(path)
         if remove:
-            try:
-                os.remove(self.path)
-            except FileNotFoundError:
-                pass
+            for g in self._gens:
+                for p in self._files_of(g):
+                    try:
+                        os.remove(p)
+                    except FileNotFoundError:
+                        pass
 
 
 class Store:
@@ -215,8 +272,8 @@ class Store:
         """Caller holds the lock.  Large values are written straight from the
         host buffer (no bytes() copy under the GIL)."""
         if isinstance(value, BlobRef):
-            off, n = value.result()
-            return _REF2 + struct.pack("<QQ", off, n) + value.segment.path.encode()
+            off, n, path = value.result()
+            return _REF2 + struct.pack("<QQ", off, n) + path.encode()
         if hasattr(value, "cpu") and hasattr(value, "numpy"):
             buf = memoryview(value.detach().cpu().contiguous().numpy()).cast("B")
         else:
@@ -233,9 +290,14 @@ class Store:
         v = bytes(v)
         if v.startswith(_REF2):
             off, n = struct.unpack("<QQ", v[len(_REF2): len(_REF2) + 16])
-            with open(v[len(_REF2) + 16:].decode(), "rb") as f:
-                f.seek(off)
-                return f.read(n)
+            path = v[len(_REF2) + 16:].decode()
+            try:
+                with open(path, "rb") as f:
+                    f.seek(off)
+                    return f.read(n)
+            except FileNotFoundError:
+                raise FileNotFoundError(f"ledger value pruned for disk space ({path}; DRYNX_LEDGER_RETAIN=all "
+                                        f"keeps every proof)") from None
         if len(v) == len(_REF) + 16 and v.startswith(_REF):
             off, n = struct.unpack("<QQ", v[len(_REF):])
             if self._blob_f is not None:

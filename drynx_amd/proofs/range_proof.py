@@ -833,6 +833,25 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
     # (DRYNX_RPV=fold) runs one Miller loop per item, as the reference's
     # per-equation check
     use_msm = os.environ.get("DRYNX_RPV", "msm") == "msm"
+    # attribution: the bucket methods group every entry by (VN, segment) and
+    # sum / multiply the buckets over the segments before weighting them, so
+    # the per-VN checks cost the same, and a failing VN's per-segment values
+    # come from the kept buckets (no second plan, no re-bucketing)
+    # (DRYNX_SEG_KEEP=1; off by default: folding costs the clean path ~9 ms of a
+    # ~200 ms query for ~40 ms on a failing one, profiles/r4/ab_plan_sort.txt)
+    fold = nseg if (segs is not None and nseg > 1 and use_msm
+                    and os.environ.get("DRYNX_SEG_KEEP", "0") == "1") else 1
+    # D-check sums (sum w c C', sum w D) per VN: for a small batch (a pool
+    # helper's 1/W slice) without a bucket plan -- c C' once for every VN (on
+    # the validation stream, beside the U side), then each VN's 32-bit GLV
+    # ladders and a chunked tree sum, no host sync (the plan's sort and sync
+    # cost a 1/8 slice ~5 ms of wall); a full inbox keeps the bucket MSM, whose
+    # device time is lower (1.6 against 4.2 ms at 20,700 proofs x 3 VNs,
+    # profiles/r4/span_kernels_serialized.txt).  DRYNX_DCHECK=direct|msm forces one.
+    dmode = os.environ.get("DRYNX_DCHECK", "auto")
+    ddirect = fold == 1 and (dmode == "direct" or (dmode == "auto" and device.type == "cuda"
+                                                   and n * n_vn <= _DCHECK_DIRECT_MAX))
+    cC = ev_cC = None
     with timers.span("rp.verify.validate"):
         # On a GPU the checks run on their own stream, filling the gaps the
         # verifier's host-side plans leave, and are read back with the
@@ -844,6 +863,14 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
             vstream.wait_stream(torch.cuda.current_stream(device))
             with torch.cuda.stream(vstream):
                 valid = validate_list(r, mode, lazy=True, per_proof=pp)
+                if ddirect:  # c C' per proof, weight-free (undecodable rows are masked out later)
+                    cC = nt.g1_mul(r.commit.C.contiguous() if not any(r.offset) else
+                                   nt.g1_add(r.commit.C, nt.g1_fb_mul_i64(
+                                       bn.base_table(device), bn.h2d(torch.tensor(r.offset, dtype=torch.int64),
+                                                                     device))),
+                                   r.challenge.contiguous())
+                    ev_cC = torch.cuda.Event()
+                    ev_cC.record(vstream)
         else:
             valid = validate_list(r, mode, lazy=True, per_proof=pp)
             if not bool(valid.all()) and (segs is None or not use_msm):
@@ -921,14 +948,6 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
     _sw.__exit__(None, None, None)
     vns = [{"rho": rho_all[v * m:(v + 1) * m], "ab": ab_all[v * m:(v + 1) * m]} for v in range(G)]
     timers.count("rp.verify.items", G * m)
-    # attribution: the bucket methods group every entry by (VN, segment) and
-    # sum / multiply the buckets over the segments before weighting them, so
-    # the per-VN checks cost the same, and a failing VN's per-segment values
-    # come from the kept buckets (no second plan, no re-bucketing)
-    # (DRYNX_SEG_KEEP=1; off by default: folding costs the clean path ~9 ms of a
-    # ~200 ms query for ~40 ms on a failing one, profiles/r4/ab_plan_sort.txt)
-    fold = nseg if (segs is not None and nseg > 1 and use_msm
-                    and os.environ.get("DRYNX_SEG_KEEP", "0") == "1") else 1
     pseg = iseg = None
     if fold > 1:
         pseg = torch.repeat_interleave(torch.arange(nseg, device=device), _h2d(segs, device), output_size=n)
@@ -959,12 +978,6 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
         if use_msm and aux is not None:
             with timers.span("rp.plan.R"):
                 hR = _msm_plan(r.zphi, r.V, rho_all, G, n, S, l)
-        # D-check sums (sum w c C', sum w D) per VN: on a GPU without a bucket
-        # plan -- c C' once for every VN, then each VN's 32-bit GLV ladders and
-        # a chunked tree sum (no host sync: a 1/W pool slice spent ~5 ms in the
-        # plan's sort and sync); DRYNX_DCHECK=msm keeps the bucket MSM
-        dmode = os.environ.get("DRYNX_DCHECK", "auto")  # auto: direct on a GPU; direct / msm: forced
-        ddirect = fold == 1 and (dmode == "direct" or (dmode == "auto" and device.type == "cuda"))
         if not ddirect:
             dpts = torch.cat([Cp.contiguous(), r.D.contiguous()]).repeat(G, 1)
             wc = nt.fr_arith(nt.FR_MUL, w_all, r.challenge)
@@ -1012,7 +1025,10 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
                 S_R = nt.g2_msm_run(r.V, hR)                           # R window sums
         with timers.span("rp.run.D"):
             if ddirect:
-                cC = nt.g1_mul(Cp.contiguous(), r.challenge.contiguous())     # shared by the VNs
+                if cC is None:                                                 # host path
+                    cC = nt.g1_mul(Cp.contiguous(), r.challenge.contiguous())
+                elif ev_cC is not None:
+                    torch.cuda.current_stream(device).wait_event(ev_cC)
                 pts = torch.stack([cC, r.D], 1).unsqueeze(1).expand(n, G, 2, 24).reshape(-1, 24)
                 abs_ = wab_all.view(G, n, 2).permute(1, 0, 2).unsqueeze(2).expand(n, G, 2, 2).reshape(-1, 2)
                 # item-major [n, 2G]: group v * 2 + which, summed over the proofs
@@ -1139,6 +1155,9 @@ class _nullctx:
 
     def __exit__(self, *a):
         return False
+
+
+_DCHECK_DIRECT_MAX = 16384  # proofs x VNs up to which the D-check runs without a bucket plan
 
 
 def _msm_plan(zphi, V, rho_all, G: int, n: int, S: int, L: int) -> dict:

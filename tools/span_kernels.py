@@ -66,22 +66,31 @@ def main():
     ap.add_argument("--window", default="bench.step")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
+    # kernels by row (a Correlation_Id can repeat: several dispatches of one
+    # call, and ids reused across threads)
     kern = {}
     iv = []
     with open(_find(a.dir, "kernel_trace.csv")) as f:
-        for r in csv.DictReader(f):
-            c = int(r["Correlation_Id"])
+        for c, r in enumerate(csv.DictReader(f)):
             wgs = 1
             for ax in "XYZ":
                 wgs *= max(1, int(r[f"Grid_Size_{ax}"]) // max(1, int(r[f"Workgroup_Size_{ax}"])))
             iv.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), c, min(wgs, _SLOTS)))
-            kern[c] = [r["Kernel_Name"], 0.0]
+            kern[c] = [r["Kernel_Name"], 0.0, (int(r["Correlation_Id"]), r["Thread_Id"]), r["Thread_Id"],
+                       int(r["Start_Timestamp"])]
     # kernels overlap (streams, and queue-level concurrency even under
     # AMD_SERIALIZE_KERNEL): each instant of device time is shared by the
     # kernels running then, in proportion to their workgroups (capped at the
     # chip's resident slots) -- a one-workgroup kernel beside a full-chip one
     # is charged ~nothing for the wait, not its whole stretched duration
     ev = sorted([(x[0], 1, i) for i, x in enumerate(iv)] + [(x[1], 0, i) for i, x in enumerate(iv)])
+    srt = sorted(iv)
+    overlaps = sum(1 for i in range(1, len(srt)) if srt[i][0] < max(x[1] for x in srt[max(0, i - 64): i]))
+    raw = overlaps < 0.01 * max(1, len(iv))  # a serialized run: each kernel's own duration
+    if raw:
+        for s_, e_, c_, w_ in iv:
+            kern[c_][1] = (e_ - s_) / 1e6
+        ev = []
     active, wsum, last = set(), 0, None
     for t, kind, i in ev:
         if last is not None and active and t > last:
@@ -95,12 +104,15 @@ def main():
         else:
             active.discard(i)
             wsum -= iv[i][3]
+    from collections import Counter
+
+    nkey = Counter(k[2] for k in kern.values())
     launch = {}
     with open(_find(a.dir, "hip_api_trace.csv")) as f:
         for r in csv.DictReader(f):
-            c = int(r["Correlation_Id"])
-            if c in kern and c not in launch:
-                launch[c] = (r["Thread_Id"], int(r["Start_Timestamp"]))
+            key = (int(r["Correlation_Id"]), r["Thread_Id"])
+            if key in nkey and key not in launch:
+                launch[key] = (r["Thread_Id"], int(r["Start_Timestamp"]))
     ranges = defaultdict(list)  # thread -> [(start, end, name)]
     with open(_find(a.dir, "marker_api_trace.csv")) as f:
         for r in csv.DictReader(f):
@@ -129,10 +141,10 @@ def main():
     cnt = defaultdict(int)
     gk = defaultdict(lambda: defaultdict(float))
     all_k = all_g = 0.0
-    for c, (name, dur) in kern.items():
-        if c not in launch:
-            continue
-        th, ts = launch[c]
+    for c, (name, dur, key, kth, kstart) in kern.items():
+        # the launching call's time; for an ambiguous id the kernel's own start
+        # (a serialized run starts each kernel right after its launch)
+        th, ts = launch[key] if (key in launch and nkey[key] == 1) else (kth, kstart)
         if not any(s <= ts <= e for s, e in wins):
             continue
         sp = innermost(th, ts)
@@ -160,8 +172,9 @@ def main():
         if cur_e is not None:
             busy += cur_e - cur_s
     busy = busy / 1e6 / q
-    lines = [f"# kernels launched inside the last {q} '{a.window}' ranges, per query "
-             "(ms of device time, overlap shared by workgroups)",
+    lines = [f"# kernels launched inside the last {q} '{a.window}' ranges, per query (ms of device time, "
+             + ("serialized run: each kernel's own duration)" if raw else
+                f"{overlaps} overlapping kernels: overlap shared by workgroups)"),
              f"# all kernels {all_k / q:.2f} ms, glue (torch/ATen, rocPRIM, runtime copies/fills) {all_g / q:.2f} ms",
              f"# window wall {wall:.2f} ms, device busy {busy:.2f} ms ({100 * busy / max(wall, 1e-9):.0f}%)",
              f"{'span':40s} {'kernel_ms':>9s} {'glue_ms':>8s} {'n':>6s}  largest glue kernels"]
