@@ -1459,11 +1459,41 @@ def _multi_exp64_plan(rho: torch.Tensor):
     return _bucket_plan(rho, _ME_W)
 
 
-def _sort_buckets(keys: torch.Tensor, items: torch.Tensor, nb: int):
+class _Counts:
+    """Per-bucket counts of a plan still on their way to the host: a pinned
+    copy queued behind the plan's kernels, waited for by ``get``."""
+
+    def __init__(self, counts_dev: torch.Tensor):
+        self.host = torch.empty(counts_dev.shape, dtype=counts_dev.dtype, pin_memory=True)
+        self.host.copy_(counts_dev, non_blocking=True)
+        self.ev = torch.cuda.Event()
+        self.ev.record()
+        self.arr = None
+
+    def get(self) -> np.ndarray:
+        if self.arr is None:
+            self.ev.synchronize()
+            self.arr = self.host.numpy().astype(np.int64)
+        return self.arr
+
+
+def _counts_out(counts_dev: torch.Tensor, defer: bool):
+    if defer and counts_dev.is_cuda:
+        return _Counts(counts_dev)
+    return counts_dev.cpu().numpy().astype(np.int64)                       # the one host sync
+
+
+def _cget(counts) -> np.ndarray:
+    return counts.get() if isinstance(counts, _Counts) else counts
+
+
+def _sort_buckets(keys: torch.Tensor, items: torch.Tensor, nb: int, defer: bool = False):
     """Sort the (key, item) entries of a bucket plan by key over its low
     bit_length(nb) bits (csrc/kernels/dx_plan.hip: rocPRIM radix sort, 4-byte
     payload) and find every bucket's run -> (sorted items, per-bucket counts
-    on the host: the plan's one device-to-host copy)."""
+    on the host: the plan's one device-to-host copy).  ``defer``: the counts
+    come back as a ``_Counts`` whose copy is in flight (``_cget`` waits), so
+    a caller can queue other work before the plan's host sync."""
     dev = keys.device
     n = keys.numel()
     g, s = _ctx(keys)
@@ -1481,7 +1511,7 @@ def _sort_buckets(keys: torch.Tensor, items: torch.Tensor, nb: int):
         cursor = torch.zeros(nb, dtype=torch.int32, device=dev)
         i2 = torch.empty_like(items)
         _call("dx_bucket_scatter", g, s, _ptr(keys), _ptr(items), n, nb, _ptr(offs), _ptr(cursor), _ptr(i2))
-        return i2, counts_d.cpu().numpy().astype(np.int64)                 # the one host sync
+        return i2, _counts_out(counts_d, defer)
     if not g or mode == "torch":
         # torch's onesweep radix sort (hipCUB): measured faster on gfx950 than a
         # direct rocprim::radix_sort_pairs over the keys' bits (5.9 vs ~1.1 ms
@@ -1490,8 +1520,7 @@ def _sort_buckets(keys: torch.Tensor, items: torch.Tensor, nb: int):
         i2 = items.index_select(0, order)
         bounds = torch.zeros((2, nb), dtype=torch.int64, device=dev)
         _call("dx_bucket_bounds", g, s, _ptr(k2), n, nb, _ptr(bounds[0]), _ptr(bounds[1]))
-        counts = (bounds[1] - bounds[0]).to(torch.int32).cpu().numpy()  # the one host sync
-        return i2, counts.astype(np.int64)
+        return i2, _counts_out((bounds[1] - bounds[0]).to(torch.int32), defer)
     end_bit = max(1, int(nb).bit_length())
     k2 = torch.empty_like(keys)
     i2 = torch.empty_like(items)
@@ -1505,8 +1534,7 @@ def _sort_buckets(keys: torch.Tensor, items: torch.Tensor, nb: int):
     _call("dx_bucket_sort", g, s, _ptr(keys), _ptr(items), _ptr(k2), _ptr(i2), n, end_bit, _ptr(tmp), tb.value)
     bounds = torch.zeros((2, nb), dtype=torch.int64, device=dev)
     _call("dx_bucket_bounds", g, s, _ptr(k2), n, nb, _ptr(bounds[0]), _ptr(bounds[1]))
-    counts = (bounds[1] - bounds[0]).to(torch.int32).cpu().numpy()      # the one host sync
-    return i2, counts.astype(np.int64)
+    return i2, _counts_out((bounds[1] - bounds[0]).to(torch.int32), defer)
 
 
 def _segment_passes_dev(counts, dev, first_slice: int | None = None):
@@ -1574,11 +1602,13 @@ def _group_arg(group, n: int, dev):
     return group.to(device=dev, dtype=torch.int32).contiguous(), 0
 
 
-def _bucket_plan(k: torch.Tensor, W: int, group: torch.Tensor | None = None, n_groups: int = 1, c: int = 8):
+def _bucket_plan(k: torch.Tensor, W: int, group: torch.Tensor | None = None, n_groups: int = 1, c: int = 8,
+                 defer: bool = False):
     """Bucket plan of a multi-scalar product over the low W c-bit windows of
     the scalars k [n, 8]: window w, digit d -> bucket (w << c) + d (plus
     g * (W << c) for entries of group g when `group` is given); entries sorted
-    by bucket, then segmented passes down to one value per non-empty bucket."""
+    by bucket, then segmented passes down to one value per non-empty bucket.
+    ``defer``: -> a callable finishing the plan (its host sync) later."""
     dev = k.device
     n = k.shape[0]
     nb = (W << c) * n_groups
@@ -1589,17 +1619,21 @@ def _bucket_plan(k: torch.Tensor, W: int, group: torch.Tensor | None = None, n_g
     g, s = _ctx(k, keys)
     _call("dx_msm_keys", g, s, _ptr(k.contiguous()), _ptr(grp), gstride, n, c, W, _ptr(keys),  # dx_rpmsm.hip
           _ptr(item))
-    item, counts = _sort_buckets(keys, item, nb)   # zero digits carry a sentinel key that sorts last
-    item = item[: int(counts.sum())].to(torch.int64)                    # drop the zero-digit sentinels
-    bk = np.flatnonzero(counts)
-    passes = _segment_passes_dev(counts[bk], dev)
-    # bucket digits and scatter slots, staged now so the run needs no host->device copy
-    mask = (1 << c) - 1
-    sc = torch.zeros((bk.size, 8), dtype=torch.int32)
-    sc[:, 0] = torch.from_numpy((bk & mask).astype("int32"))
-    slot = torch.from_numpy((bk & mask) * W + (bk >> c))
-    return {"item": item, "passes": passes, "bk": bk, "single": not passes,
-            "digit_sc": _upload(sc.numpy(), dev), "slot": _upload(slot.numpy(), dev), "W": W, "c": c}
+    item, counts_f = _sort_buckets(keys, item, nb, defer)   # zero digits carry a sentinel key that sorts last
+
+    def finish():
+        counts = _cget(counts_f)
+        it = item[: int(counts.sum())].to(torch.int64)                  # drop the zero-digit sentinels
+        bk = np.flatnonzero(counts)
+        passes = _segment_passes_dev(counts[bk], dev)
+        # bucket digits and scatter slots, staged now so the run needs no host->device copy
+        mask = (1 << c) - 1
+        sc = torch.zeros((bk.size, 8), dtype=torch.int32)
+        sc[:, 0] = torch.from_numpy((bk & mask).astype("int32"))
+        slot = torch.from_numpy((bk & mask) * W + (bk >> c))
+        return {"item": it, "passes": passes, "bk": bk, "single": not passes,
+                "digit_sc": _upload(sc.numpy(), dev), "slot": _upload(slot.numpy(), dev), "W": W, "c": c}
+    return finish if defer else finish()
 
 
 def _multi_exp64_run(a: torch.Tensor, plan) -> torch.Tensor:
@@ -1629,9 +1663,10 @@ def _multi_exp64_run(a: torch.Tensor, plan) -> torch.Tensor:
     return acc
 
 
-def multi_exp_plan(k: torch.Tensor, group, n_groups: int, W: int = _ME_W, c: int = 8) -> dict:
-    """The bucket plan of ``multi_exp_grouped`` alone (its one host sync)."""
-    return _bucket_plan(k, W, group, n_groups, c)
+def multi_exp_plan(k: torch.Tensor, group, n_groups: int, W: int = _ME_W, c: int = 8, defer: bool = False):
+    """The bucket plan of ``multi_exp_grouped`` alone (its one host sync;
+    ``defer``: a callable that takes it later)."""
+    return _bucket_plan(k, W, group, n_groups, c, defer)
 
 
 def multi_exp_grouped(a: torch.Tensor, k: torch.Tensor, group, n_groups: int, W: int = _ME_W, c: int = 8,
@@ -1796,10 +1831,13 @@ def g1_msm_grouped(P_jac: torch.Tensor, k: torch.Tensor, group: torch.Tensor | N
     return g1_msm_finish(g1_msm_launch(P_jac, k, group, n_groups, bits))
 
 
-def g1_msm_plan(k: torch.Tensor, group, n_groups: int, bits: int = 256) -> dict:
+def g1_msm_plan(k: torch.Tensor, group, n_groups: int, bits: int = 256, defer: bool = False):
     """The bucket plan of ``g1_msm_launch`` alone (its one host sync), so a
-    caller can take every plan's sync before queueing any heavy pass."""
-    return _bucket_plan(k, (bits + 7) // 8, group, n_groups) if k.shape[0] else None
+    caller can take every plan's sync before queueing any heavy pass
+    (``defer``: a callable that takes it later)."""
+    if not k.shape[0]:
+        return (lambda: None) if defer else None
+    return _bucket_plan(k, (bits + 7) // 8, group, n_groups, defer=defer)
 
 
 def g1_msm_launch(P_jac: torch.Tensor, k: torch.Tensor, group: torch.Tensor | None, n_groups: int,
@@ -1968,7 +2006,7 @@ def g2_mul_small(jac: torch.Tensor, d: torch.Tensor) -> torch.Tensor:
 
 
 def g2_msm_launch(P_aff: torch.Tensor, k: torch.Tensor, group: torch.Tensor | None, n_groups: int,
-                  c: int = 13, bits: int = 254, first_slice: int = 32) -> dict:
+                  c: int = 13, bits: int = 254, first_slice: int = 32, defer: bool = False):
     """Bucket plan of G independent G2 MSMs out[g] = sum_{t: group_t = g}
     k_t P[t % m] (m = rows of P_aff, k [n, 8] with n a multiple of m; group:
     int32 tensor, or an int stride s meaning group_t = t // s):
@@ -1986,16 +2024,20 @@ def g2_msm_launch(P_aff: torch.Tensor, k: torch.Tensor, group: torch.Tensor | No
     grp, gstride = _group_arg(group, n, dev)
     g, s = _ctx(k, keys)
     _call("dx_msm_keys", g, s, _ptr(k.contiguous()), _ptr(grp), gstride, n, c, W, _ptr(keys), _ptr(items))
-    items, counts = _sort_buckets(keys, items, nb)                      # the one host sync
-    bk = np.flatnonzero(counts)
-    h = {"G": n_groups, "W": W, "c": c, "m": m, "bk": bk, "item": items[: int(counts.sum())]}
-    if bk.size:
-        passes = _segment_passes_dev(counts[bk], dev, first_slice)
-        if not passes:  # every bucket holds one entry
-            passes = [(torch.arange(bk.size, device=dev), torch.ones(bk.size, dtype=torch.int32, device=dev))]
-        h["passes"] = passes
-        h.update(_g2_weight_plan(bk, c, dev))
-    return h
+    items, counts_f = _sort_buckets(keys, items, nb, defer)             # the one host sync
+
+    def finish():
+        counts = _cget(counts_f)
+        bk = np.flatnonzero(counts)
+        h = {"G": n_groups, "W": W, "c": c, "m": m, "bk": bk, "item": items[: int(counts.sum())]}
+        if bk.size:
+            passes = _segment_passes_dev(counts[bk], dev, first_slice)
+            if not passes:  # every bucket holds one entry
+                passes = [(torch.arange(bk.size, device=dev), torch.ones(bk.size, dtype=torch.int32, device=dev))]
+            h["passes"] = passes
+            h.update(_g2_weight_plan(bk, c, dev))
+        return h
+    return finish if defer else finish()
 
 
 def _g2_weight_plan(bk, c: int, dev) -> dict:

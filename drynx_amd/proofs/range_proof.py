@@ -953,52 +953,35 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
         pseg = torch.repeat_interleave(torch.arange(nseg, device=device), _h2d(segs, device), output_size=n)
         iseg = pseg.repeat_interleave(S * l)
     aux = _aux_stream(device) if device.type == "cuda" else None
+    defer = aux is not None
+    # the bucket plans' keys and sorts go FIRST, on the high-priority aux
+    # stream, with their counts copied back asynchronously; then the U side
+    # (no plan, no sync) fills this stream; then the host takes the plans'
+    # syncs -- which then wait for the short sort kernels only, not behind the
+    # long U-side launches (a 1/8 pool slice waited ~9 ms for its R plan)
     if aux is not None:
-        # the pairing work (~all of the GPU time) is queued FIRST on this
-        # stream; the MSM / multi-exponentiation bucket plans (host syncs) then
-        # run on the aux stream, so their syncs wait only for aux work and the
-        # GPU never idles while the host plans
         aux.wait_stream(torch.cuda.current_stream(device))
-        if use_msm:
-            # msm: the U side (no plan, no sync) fills this stream at once; the
-            # bucket plans (host syncs) and the R passes go to the high-priority
-            # aux stream, whose short plan kernels then overtake the U kernels
-            with timers.span("rp.verify.msm_queue"):
-                msq = _msm_queue(Y, r.V, ab_all, G, n, S, l, vstream, segs)
-                for v, uok in zip(vns, msq["u_ok"]):
-                    v["u_ok"] = uok
-        else:
-            with timers.span("rp.verify.fold_queue"):
-                for v, fb in zip(vns, _miller_fold_multi(ZB, Y, [v["rho"] for v in vns], r.V, S, l,
-                                                           [v["ab"] for v in vns])):
-                    v["fb"] = fb
-    with timers.span("rp.verify.plans"), (torch.cuda.stream(aux) if aux is not None else _nullctx()):
-        # every bucket plan (one host sync each) first, then every pass: a sync
-        # never waits behind another plan's heavy passes
+    with timers.span("rp.verify.plan_start"), (torch.cuda.stream(aux) if aux is not None else _nullctx()):
         if use_msm and aux is not None:
             with timers.span("rp.plan.R"):
-                hR = _msm_plan(r.zphi, r.V, rho_all, G, n, S, l)
+                hR_f = _msm_plan(r.zphi, r.V, rho_all, G, n, S, l, defer=True)
         if not ddirect:
             dpts = torch.cat([Cp.contiguous(), r.D.contiguous()]).repeat(G, 1)
             wc = nt.fr_arith(nt.FR_MUL, w_all, r.challenge)
             dsc = torch.stack([wc.view(G, n, 8), w_all.view(G, n, 8)], 1).reshape(-1, 8).contiguous()
         with timers.span("rp.plan.D"):
             if ddirect:
-                dplan = None
+                dplan_f = None
             elif fold > 1:  # group = ((v, which) row // n, segment of the proof)
                 dgrp = (torch.arange(2 * G, device=device).view(-1, 1) * fold
                         + pseg.view(1, n)).reshape(-1).to(torch.int32)
-                dplan = nt.g1_msm_plan(dsc, dgrp, 2 * G * fold)
+                dplan_f = nt.g1_msm_plan(dsc, dgrp, 2 * G * fold, defer=defer)
             else:
                 dgrp = n
-                dplan = nt.g1_msm_plan(dsc, n, 2 * G)                     # group = row // n
+                dplan_f = nt.g1_msm_plan(dsc, n, 2 * G, defer=defer)     # group = row // n
         # groups 0..G-1: prod a^rho_v; groups G..2G-1: each VN's own GT-membership
         # combination prod a^gamma_v
         # prod a^rho = prod a^a' * frob^8(a)^b': 32-bit exponents over (A, frob^8 A)
-        with timers.span("rp.frob8"):  # (A, frob^8 A) stacked: the Frobenius image written in place
-            A2 = torch.empty((2 * m, 96), dtype=torch.int32, device=device)
-            nt.batched_copy([(r.A.contiguous(), A2[:m])])
-            nt.gt_frob8(r.A.contiguous(), out=A2[m:])
         k = torch.zeros((2 * G, 2 * m, 8), dtype=torch.int32, device=device)
         abv = ab_all.view(G, m, 2)
         k[:G, :m, 0] = abv[:, :, 0]
@@ -1012,9 +995,32 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
             if fold > 1:  # group = (row // 2m, segment of the item)
                 mgrp = (torch.arange(2 * G, device=device).view(-1, 1) * fold
                         + iseg.repeat(2).view(1, 2 * m)).reshape(-1).to(torch.int32)
-                mplan = nt.multi_exp_plan(k, mgrp, 2 * G * fold, W=wc_[0], c=wc_[1])
+                mplan_f = nt.multi_exp_plan(k, mgrp, 2 * G * fold, W=wc_[0], c=wc_[1], defer=defer)
             else:
-                mplan = nt.multi_exp_plan(k, 2 * m, 2 * G, W=wc_[0], c=wc_[1])  # group = row // 2m
+                mplan_f = nt.multi_exp_plan(k, 2 * m, 2 * G, W=wc_[0], c=wc_[1], defer=defer)  # group = row // 2m
+    if aux is not None:
+        if use_msm:
+            with timers.span("rp.verify.msm_queue"):
+                msq = _msm_queue(Y, r.V, ab_all, G, n, S, l, vstream, segs)
+                for v, uok in zip(vns, msq["u_ok"]):
+                    v["u_ok"] = uok
+        else:
+            with timers.span("rp.verify.fold_queue"):
+                for v, fb in zip(vns, _miller_fold_multi(ZB, Y, [v["rho"] for v in vns], r.V, S, l,
+                                                           [v["ab"] for v in vns])):
+                    v["fb"] = fb
+    with timers.span("rp.verify.plans"), (torch.cuda.stream(aux) if aux is not None else _nullctx()):
+        # every plan's host sync first, then every pass: a sync never waits
+        # behind another plan's heavy passes
+        with timers.span("rp.plan.sync"):
+            if use_msm and aux is not None:
+                hR = hR_f()
+            dplan = dplan_f() if callable(dplan_f) else dplan_f
+            mplan = mplan_f() if callable(mplan_f) else mplan_f
+        with timers.span("rp.frob8"):  # (A, frob^8 A) stacked: the Frobenius image written in place
+            A2 = torch.empty((2 * m, 96), dtype=torch.int32, device=device)
+            nt.batched_copy([(r.A.contiguous(), A2[:m])])
+            nt.gt_frob8(r.A.contiguous(), out=A2[m:])
         with timers.span("rp.run.ME"):
             if fold > 1:
                 mexp = nt.multi_exp_grouped(A2, k, mgrp, 2 * G * fold, W=wc_[0], c=wc_[1], plan=mplan, fold=fold)
@@ -1160,15 +1166,16 @@ class _nullctx:
 _DCHECK_DIRECT_MAX = 16384  # proofs x VNs up to which the D-check runs without a bucket plan
 
 
-def _msm_plan(zphi, V, rho_all, G: int, n: int, S: int, L: int) -> dict:
+def _msm_plan(zphi, V, rho_all, G: int, n: int, S: int, L: int, defer: bool = False):
     """Verifier mode "msm", step 1 (one host sync): the R-MSM bucket plan of
-    every VN, R_v = sum_it (rho_it Zphi_(p, j)) V_it."""
+    every VN, R_v = sum_it (rho_it Zphi_(p, j)) V_it (``defer``: a callable
+    taking the sync later)."""
     dev = V.device
     m = n * S * L
     it = torch.arange(m, device=dev)
     zi = (it // (S * L)) * L + it % L
     s_r = nt.fr_arith(nt.FR_MUL, rho_all, zphi.index_select(0, zi).contiguous())  # periodic over the VNs
-    return nt.g2_msm_launch(V, s_r, m, G, c=_r_window(m, G))          # group (VN) = row // m
+    return nt.g2_msm_launch(V, s_r, m, G, c=_r_window(m, G), defer=defer)  # group (VN) = row // m
 
 
 def _r_window(m: int, G: int) -> int:
