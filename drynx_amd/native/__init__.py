@@ -1670,7 +1670,7 @@ def multi_exp_plan(k: torch.Tensor, group, n_groups: int, W: int = _ME_W, c: int
 
 
 def multi_exp_grouped(a: torch.Tensor, k: torch.Tensor, group, n_groups: int, W: int = _ME_W, c: int = 8,
-                      plan: dict | None = None, fold: int = 1):
+                      plan: dict | None = None, fold: int = 1, item_split: tuple | None = None):
     """Launch G independent multi-exponentiations prod_{i: group_i = g} a[i % n]^k_i
     (n = rows of a, k [m, 8] with m a multiple of n, low W c-bit windows of
     each exponent; ``group`` an int32 tensor or an int stride) as ONE bucket
@@ -1679,11 +1679,18 @@ def multi_exp_grouped(a: torch.Tensor, k: torch.Tensor, group, n_groups: int, W:
     device passes are queued on the current stream.  ``fold`` = k: the
     ``n_groups`` plan groups are (group, segment) pairs g * k + s; the handle
     finishes the n_groups / k groups (buckets combined over the segments) and
-    keeps the per-segment buckets for ``multi_exp_seg_finish``."""
+    keeps the per-segment buckets for ``multi_exp_seg_finish``.
+    ``item_split`` = (s, q): entry i < s uses a[i % n], entry i >= s uses
+    a[(i - s) % q] (two exponent blocks over different row periods)."""
     n = a.shape[0]
     if plan is None:
         plan = _bucket_plan(k, W, group, n_groups, c)
-    plan["item"] = (plan["item"] % n).contiguous()
+    it = plan["item"]
+    if item_split is not None:
+        sp, q = item_split
+        plan["item"] = torch.where(it < sp, it % n, (it - sp) % q).contiguous()
+    else:
+        plan["item"] = (it % n).contiguous()
     bk = plan["bk"]
     h = {"G": n_groups // fold, "W": W, "c": c, "win": None}
     if bk.size == 0:

@@ -982,22 +982,33 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
         # groups 0..G-1: prod a^rho_v; groups G..2G-1: each VN's own GT-membership
         # combination prod a^gamma_v
         # prod a^rho = prod a^a' * frob^8(a)^b': 32-bit exponents over (A, frob^8 A)
-        k = torch.zeros((2 * G, 2 * m, 8), dtype=torch.int32, device=device)
         abv = ab_all.view(G, m, 2)
-        k[:G, :m, 0] = abv[:, :, 0]
-        k[:G, m:, 0] = abv[:, :, 1]
-        k[G:, :m] = gam_all.view(G, m, 8)
+        if fold > 1:
+            k = torch.zeros((2 * G, 2 * m, 8), dtype=torch.int32, device=device)
+            k[:G, :m, 0] = abv[:, :, 0]
+            k[:G, m:, 0] = abv[:, :, 1]
+            k[G:, :m] = gam_all.view(G, m, 8)
+            k = k.view(-1, 8)
+        else:
+            # [rho rows: G x 2m over (A, frob^8 A) | gamma rows: G x m over A] --
+            # no all-zero half for the combinations (a quarter fewer plan keys)
+            k = torch.zeros((3 * G * m, 8), dtype=torch.int32, device=device)
+            kr = k[: 2 * G * m].view(G, 2 * m, 8)
+            kr[:, :m, 0] = abv[:, :, 0]
+            kr[:, m:, 0] = abv[:, :, 1]
+            k[2 * G * m:] = gam_all
+            gv = torch.arange(G, device=device, dtype=torch.int32)
+            mgrp = torch.cat([gv.repeat_interleave(2 * m), G + gv.repeat_interleave(m)])
         # GPU: 11-bit windows (3 per 32-bit half, 4 for the 40-bit combinations);
         # host: bytes (fewer buckets for the host's serial bucket products)
         wc_ = (4, 11) if device.type == "cuda" else (5, 8)
-        k = k.view(-1, 8)
         with timers.span("rp.plan.ME"):
             if fold > 1:  # group = (row // 2m, segment of the item)
                 mgrp = (torch.arange(2 * G, device=device).view(-1, 1) * fold
                         + iseg.repeat(2).view(1, 2 * m)).reshape(-1).to(torch.int32)
                 mplan_f = nt.multi_exp_plan(k, mgrp, 2 * G * fold, W=wc_[0], c=wc_[1], defer=defer)
             else:
-                mplan_f = nt.multi_exp_plan(k, 2 * m, 2 * G, W=wc_[0], c=wc_[1], defer=defer)  # group = row // 2m
+                mplan_f = nt.multi_exp_plan(k, mgrp, 2 * G, W=wc_[0], c=wc_[1], defer=defer)
     if aux is not None:
         if use_msm:
             with timers.span("rp.verify.msm_queue"):
@@ -1025,7 +1036,8 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
             if fold > 1:
                 mexp = nt.multi_exp_grouped(A2, k, mgrp, 2 * G * fold, W=wc_[0], c=wc_[1], plan=mplan, fold=fold)
             else:
-                mexp = nt.multi_exp_grouped(A2, k, 2 * m, 2 * G, W=wc_[0], c=wc_[1], plan=mplan)
+                mexp = nt.multi_exp_grouped(A2, k, mgrp, 2 * G, W=wc_[0], c=wc_[1], plan=mplan,
+                                            item_split=(2 * G * m, m))
         if use_msm and aux is not None:
             with timers.span("rp.run.R"):
                 S_R = nt.g2_msm_run(r.V, hR)                           # R window sums
