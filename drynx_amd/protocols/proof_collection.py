@@ -185,14 +185,19 @@ def pool_verify_ranges(ctx, sq, reqs: list, vns: list, comm=None) -> dict:
     vn_idxs = {vn.id: [i for i in rng if sampled[vn.id].get(reqs[i].base_key())] for vn in vns}
     part_coins = {vn.id: Coins(seeds[vn.id]).derive(("slice", k, W)) for vn in vns}
     t0 = time.perf_counter()
+    local_vns = [vn for vn in vns if vn.rank == ctx.rank]
+    # a VN rank's digests of the other ranks' slices of its own payloads run
+    # beside this rank's pool part (their own thread and stream: the part's
+    # latency-bound kernels leave the GPU room), not after the gather
+    exp_f = _expected_async(ctx, sq, reqs, vn_idxs, local_vns, W) if local_vns and W > 1 else None
     res, digests = prq.verify_range_pool_part(reqs, vn_idxs, sq, ctx.device, ctx.verifier_cache, (k, W), part_coins)
     mine = {vn.id: {reqs[i].base_key(): bool(ok) for i, ok in res.get(vn.id, {}).items()} for vn in vns}
     mydig = {reqs[i].base_key(): d for i, d in digests.items()}
     gathered = comm.all_gather_object((mine, mydig))
     out = {}
-    local_vns = [vn for vn in vns if vn.rank == ctx.rank]
     if local_vns:
-        trusted = _check_helper_digests(ctx, sq, reqs, vn_idxs, local_vns, gathered, W)
+        trusted = _check_helper_digests(ctx, sq, reqs, vn_idxs, local_vns, gathered, W,
+                                        exp_f.result() if exp_f is not None else None)
     for vn in vns:
         if vn.rank != ctx.rank:
             continue
@@ -219,10 +224,29 @@ def pool_verify_ranges(ctx, sq, reqs: list, vns: list, comm=None) -> dict:
     return out
 
 
-def _check_helper_digests(ctx, sq, reqs, vn_idxs: dict, local_vns: list, gathered: list, W: int) -> dict:
-    """For each local VN: the (base_key, part) pairs whose helper-reported
-    slice digest equals the digest of that slice of the VN's own signed
-    payload, and the mismatches to redo ({part: [request index]})."""
+def _expected_async(ctx, sq, reqs, vn_idxs: dict, local_vns: list, W: int):
+    """``_expected_digests`` on a worker thread with its own HIP stream
+    (ordered after the caller's stream, where the payloads were received)."""
+    import concurrent.futures as cf
+
+    if not hasattr(ctx, "_dig_exec"):
+        ctx._dig_exec = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="drynx-vn-digests")
+    if ctx.device.type != "cuda":
+        return ctx._dig_exec.submit(_expected_digests, ctx, sq, reqs, vn_idxs, local_vns, W)
+    if not hasattr(ctx, "_dig_stream"):
+        ctx._dig_stream = torch.cuda.Stream(ctx.device)
+    st, cur = ctx._dig_stream, torch.cuda.current_stream(ctx.device)
+    st.wait_stream(cur)
+
+    def run():
+        with torch.cuda.stream(st):
+            return _expected_digests(ctx, sq, reqs, vn_idxs, local_vns, W)
+    return ctx._dig_exec.submit(run)
+
+
+def _expected_digests(ctx, sq, reqs, vn_idxs: dict, local_vns: list, W: int):
+    """Digests of every other rank's slice of the local VNs' signed payloads
+    -> ({(request, part): digest}, {(request, part) with an empty slice})."""
     me = ctx.rank
     need = sorted({i for vn in local_vns for i in vn_idxs[vn.id]}) if W > 1 else []
     expected: dict = {}
@@ -245,6 +269,17 @@ def _check_helper_digests(ctx, sq, reqs, vn_idxs: dict, local_vns: list, gathere
                 keys.append((i, j))
         for key, d in zip(keys, prq.lists_digests(entries)):
             expected[key] = d
+    return expected, empty
+
+
+def _check_helper_digests(ctx, sq, reqs, vn_idxs: dict, local_vns: list, gathered: list, W: int,
+                          pre=None) -> dict:
+    """For each local VN: the (base_key, part) pairs whose helper-reported
+    slice digest equals the digest of that slice of the VN's own signed
+    payload, and the mismatches to redo ({part: [request index]}).
+    ``pre``: the (expected, empty) of ``_expected_digests`` computed earlier."""
+    me = ctx.rank
+    expected, empty = pre if pre is not None else _expected_digests(ctx, sq, reqs, vn_idxs, local_vns, W)
     out = {}
     for vn in local_vns:
         ok_pairs, redo = set(), {}
