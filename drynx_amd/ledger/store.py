@@ -61,6 +61,21 @@ def _copies() -> int:
     return max(1, int(os.environ.get("DRYNX_LEDGER_COPIES", "1")))
 
 
+def _mark_pruned(path: str):
+    """Record a deleted value file next to it (readers then fail at once
+    instead of waiting for a node-shared file that will never appear)."""
+    with open(os.path.join(os.path.dirname(os.path.abspath(path)), "_pruned"), "a") as f:
+        f.write(os.path.basename(path) + "\n")
+
+
+def _was_pruned(path: str) -> bool:
+    try:
+        with open(os.path.join(os.path.dirname(os.path.abspath(path)), "_pruned")) as f:
+            return os.path.basename(path) in {ln.strip() for ln in f}
+    except FileNotFoundError:
+        return False
+
+
 def _gb_env(name: str, default: float) -> float:
     return float(os.environ.get(name, default)) * (1 << 30)
 
@@ -185,6 +200,7 @@ class BlobSegment:
         d = os.path.dirname(os.path.abspath(self.path))
         while shutil.disk_usage(d).free - need < reserve and len(self._gens) > 1 and self._gens[0] != self.path:
             old = self._gens.pop(0)
+            _mark_pruned(old)
             for p in self._files_of(old):
                 try:
                     os.remove(p)
@@ -251,6 +267,98 @@ class BlobSegment:
                         pass
 
 
+class _Done:
+    """An already-known result (a reference that needs no write)."""
+
+    def __init__(self, v):
+        self.v = v
+
+    def result(self):
+        return self.v
+
+
+class NodeBlobs(BlobSegment):
+    """Range payloads shared by the VN ranks of ONE node, content-addressed
+    (one file per payload digest under a node directory).  On an 8-GPU node
+    the three VN ranks receive the same signed payloads; only the first one
+    copies them to the host and writes them, the others store references to
+    the same files -- as the VNs co-hosted on a rank already share one
+    BlobSegment.  A payload file appears under its final name only once fully
+    written (write to .tmp, then rename), and a reader that finds it missing
+    waits for it; the disk reserve of BlobSegment applies to the writer's
+    files."""
+
+    def __init__(self, root: str, writer: bool, device=None):
+        os.makedirs(root, exist_ok=True)
+        super().__init__(os.path.join(root, f"_rank_{os.getpid()}.unused"), device)
+        self.root, self.writer = root, writer
+        self._files: list = []  # the writer's payload files, oldest first
+
+    def file_of(self, blob_id: str) -> str:
+        return os.path.join(self.root, f"{blob_id}.blob")
+
+    def put_many(self, blob_ids: list, produce_all, sizes: list | None = None) -> list:
+        if not self.writer:
+            refs = []
+            with self._lock:
+                for bid, n in zip(blob_ids, sizes):
+                    fut = self._done.setdefault(bid, _Done((0, int(n), self.file_of(bid))))
+                    refs.append(BlobRef(self, fut))
+            return refs
+        job = self._ex.submit(self._write_files, list(blob_ids), produce_all)
+        refs = []
+        with self._lock:
+            for i, bid in enumerate(blob_ids):
+                fut = self._done.get(bid)
+                if fut is None:
+                    fut = self._done[bid] = _Item(job, i)
+                refs.append(BlobRef(self, fut))
+        return refs
+
+    def _write_files(self, blob_ids: list, produce_all):
+        import shutil
+
+        import torch
+
+        dev = torch.device(self._device) if self._device is not None else None
+        if dev is not None and dev.type == "cuda":
+            if self._stream is None:
+                self._stream = torch.cuda.Stream(dev)
+            with torch.cuda.stream(self._stream), timers.span("ledger.encode"):
+                data = produce_all()
+        else:
+            with timers.span("ledger.encode"):
+                data = produce_all()
+        out = []
+        with timers.span("ledger.write"):
+            reserve = _gb_env("DRYNX_LEDGER_RESERVE_GB", 8)
+            for bid, d in zip(blob_ids, data):
+                b = memoryview(d).cast("B")
+                if os.environ.get("DRYNX_LEDGER_RETAIN", "") != "all":
+                    while shutil.disk_usage(self.root).free - b.nbytes < reserve and self._files:
+                        old = self._files.pop(0)
+                        _mark_pruned(old)
+                        try:
+                            os.remove(old)
+                        except FileNotFoundError:
+                            pass
+                        BlobSegment.pruned += 1
+                final = self.file_of(bid)
+                tmp = final + ".tmp"
+                self._pwrite_all([b], 0, tmp)
+                os.close(self._pfds.pop(tmp))
+                os.replace(tmp, final)
+                self._files.append(final)
+                out.append((0, b.nbytes, final))
+        return out
+
+    def close(self, remove: bool = False):
+        super().close(remove)
+        if remove and self.writer:
+            shutil_rm = __import__("shutil").rmtree
+            shutil_rm(self.root, ignore_errors=True)
+
+
 class Store:
     def __init__(self, path: str):
         self.path = path
@@ -291,13 +399,22 @@ class Store:
         if v.startswith(_REF2):
             off, n = struct.unpack("<QQ", v[len(_REF2): len(_REF2) + 16])
             path = v[len(_REF2) + 16:].decode()
-            try:
-                with open(path, "rb") as f:
-                    f.seek(off)
-                    return f.read(n)
-            except FileNotFoundError:
-                raise FileNotFoundError(f"ledger value pruned for disk space ({path}; DRYNX_LEDGER_RETAIN=all "
-                                        f"keeps every proof)") from None
+            import time as _t
+
+            deadline = _t.monotonic() + float(os.environ.get("DRYNX_LEDGER_WAIT_S", "60"))
+            while True:
+                try:
+                    with open(path, "rb") as f:
+                        f.seek(off)
+                        return f.read(n)
+                except FileNotFoundError:
+                    # a node-shared payload not yet written by the node's writer
+                    # rank: wait for it, unless the writer pruned it
+                    if not _was_pruned(path) and _t.monotonic() < deadline:
+                        _t.sleep(0.01)
+                        continue
+                    raise FileNotFoundError(f"ledger value pruned for disk space ({path}; "
+                                            f"DRYNX_LEDGER_RETAIN=all keeps every proof)") from None
         if len(v) == len(_REF) + 16 and v.startswith(_REF):
             off, n = struct.unpack("<QQ", v[len(_REF):])
             if self._blob_f is not None:

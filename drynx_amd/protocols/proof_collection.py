@@ -189,7 +189,8 @@ def pool_verify_ranges(ctx, sq, reqs: list, vns: list, comm=None) -> dict:
     # a VN rank's digests of the other ranks' slices of its own payloads run
     # beside this rank's pool part (their own thread and stream: the part's
     # latency-bound kernels leave the GPU room), not after the gather
-    exp_f = _expected_async(ctx, sq, reqs, vn_idxs, local_vns, W) if local_vns and W > 1 else None
+    exp_f = _expected_async(ctx, sq, reqs, vn_idxs, local_vns, W) \
+        if local_vns and W > 1 and os.environ.get("DRYNX_DIGEST_ASYNC", "1") == "1" else None
     res, digests = prq.verify_range_pool_part(reqs, vn_idxs, sq, ctx.device, ctx.verifier_cache, (k, W), part_coins)
     mine = {vn.id: {reqs[i].base_key(): bool(ok) for i, ok in res.get(vn.id, {}).items()} for vn in vns}
     mydig = {reqs[i].base_key(): d for i, d in digests.items()}

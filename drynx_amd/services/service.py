@@ -155,19 +155,40 @@ class DrynxNode:
         if not fresh:
             return out
         if not hasattr(self, "_blobs"):
-            from ..ledger.store import BlobSegment
-
-            self._blobs = BlobSegment(os.path.join(self.workdir, f"ledger_r{self.rank}.blobs"), self.device)
+            self._blobs = self._blob_store()
         refs = {k: self._blobs.get(k) for k in fresh}
         new = [k for k, v in refs.items() if v is None]
         if new:
             tensors = [reqs[fresh[k][0]].tensor.contiguous().reshape(-1).view(torch.uint8) for k in new]
-            for k, ref in zip(new, self._blobs.put_many(new, self._host_bytes(tensors))):
+            if getattr(self._blobs, "writer", True):
+                put = self._blobs.put_many(new, self._host_bytes(tensors))
+            else:  # another VN rank of this node writes them: references only, no device-to-host copy
+                put = self._blobs.put_many(new, None, [t.numel() for t in tensors])
+            for k, ref in zip(new, put):
                 refs[k] = ref
         for k, idxs in fresh.items():
             for i in idxs:
                 out[i] = refs[k]
         return out
+
+    def _blob_store(self):
+        """This rank's store of large ledger values.  On a single node with VNs
+        on several ranks (LOCAL_WORLD_SIZE == WORLD_SIZE), the VN ranks share
+        one content-addressed node directory and only the lowest VN rank copies
+        and writes the payloads (``ledger.store.NodeBlobs``: three VN ranks
+        would otherwise write ~1.7 GB per query to one disk);
+        DRYNX_LEDGER_NODE_SHARE=0 keeps one private store per rank."""
+        from ..ledger.store import BlobSegment, NodeBlobs
+
+        W = self.comm.world
+        vn_ranks = sorted({vn.rank for vn in self.cluster.vns})
+        lws = int(os.environ.get("LOCAL_WORLD_SIZE", "0") or 0)
+        run = os.environ.get("TORCHELASTIC_RUN_ID") or os.environ.get("MASTER_PORT")
+        if (W > 1 and lws == W and run and len(vn_ranks) > 1 and self.rank in vn_ranks
+                and os.environ.get("DRYNX_LEDGER_NODE_SHARE", "1") == "1"):
+            root = os.path.join(os.path.dirname(os.path.abspath(self.workdir)), f"drynx_node_ledger_{run}")
+            return NodeBlobs(root, writer=self.rank == vn_ranks[0], device=self.device)
+        return BlobSegment(os.path.join(self.workdir, f"ledger_r{self.rank}.blobs"), self.device)
 
     def _host_bytes(self, tensors: list):
         """A producer of the host bytes of ``tensors`` (run by the ledger

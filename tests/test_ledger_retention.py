@@ -45,3 +45,35 @@ def test_blob_generations_and_pruning(tmp_path, monkeypatch, retain):
     store.close()
     seg.close(remove=True)
     assert not any(p.name.startswith("ledger_r0.blobs") for p in tmp_path.iterdir())
+
+
+def test_node_shared_payloads(tmp_path):
+    """The VN ranks of one node share content-addressed payload files: the
+    writer copies and writes, a reader rank stores references only and its
+    reads wait until the writer's file is complete."""
+    from drynx_amd.ledger.store import NodeBlobs
+
+    root = str(tmp_path / "node")
+    reader = NodeBlobs(root, writer=False)
+    rstore = Store(str(tmp_path / "db_vn1.sqlite"))
+    data = np.arange(100000, dtype=np.uint32).view(np.uint8)
+    ref = reader.put_many(["d1"], None, [data.nbytes])[0]
+    rstore.update("proofs", "k", ref)               # a reference before the writer has written anything
+    writer = NodeBlobs(root, writer=True)
+    import threading
+    import time
+
+    def late_write():
+        time.sleep(0.2)
+        writer.put_many(["d1"], lambda: [memoryview(data)])
+        writer.flush()
+
+    th = threading.Thread(target=late_write)
+    th.start()
+    assert rstore.get("proofs", "k") == data.tobytes()   # waited for the writer
+    th.join()
+    assert os.path.exists(os.path.join(root, "d1.blob")) and not os.path.exists(os.path.join(root, "d1.blob.tmp"))
+    rstore.close()
+    reader.close(remove=True)
+    writer.close(remove=True)
+    assert not os.path.exists(root)
