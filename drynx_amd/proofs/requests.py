@@ -673,17 +673,49 @@ def _verify_range_group(reqs, idxs, sq, device, cache, part, coins_list: list) -
     return outs
 
 
-def verify_range_pool_part(reqs: list, vn_idxs: dict, sq, device, cache: VerifierCache, part, coins: dict):
+_dig_pool = None
+_dig_streams: dict = {}
+
+
+def _slice_digests_async(ok_idx: list, entries: list, device):
+    """``lists_digests`` of this part's slices on a worker thread with its own
+    HIP stream (ordered after the caller's stream): the digests are needed
+    only for the gather after the part, so they no longer delay its start."""
+    global _dig_pool
+    import concurrent.futures as cf
+
+    if _dig_pool is None:
+        _dig_pool = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="drynx-slice-digests")
+    dev = torch.device(device)
+    if dev.type != "cuda":
+        return _dig_pool.submit(lambda: dict(zip(ok_idx, lists_digests(entries))))
+    st = _dig_streams.get(str(dev))
+    if st is None:
+        st = _dig_streams[str(dev)] = torch.cuda.Stream(dev)
+    st.wait_stream(torch.cuda.current_stream(dev))
+
+    def run():
+        with torch.cuda.stream(st), timers.span("rp.verify.slice_digests"):
+            return dict(zip(ok_idx, lists_digests(entries)))
+    return _dig_pool.submit(run)
+
+
+def verify_range_pool_part(reqs: list, vn_idxs: dict, sq, device, cache: VerifierCache, part, coins: dict,
+                           async_digests: bool = False):
     """One rank's share of a pooled range verification: part ``part`` of the
     sampled prefix of every request, checked for every VN with that VN's
-    coins for this part.  -> ({vn: {index: bool}}, {index: slice digest})"""
+    coins for this part.  -> ({vn: {index: bool}}, {index: slice digest});
+    ``async_digests``: the digests as a Future (computed beside the part)."""
     union = sorted({i for idxs in vn_idxs.values() for i in idxs})
     base, parts = _range_parts(reqs, union, sq, device, part)
     digests = {}
     if part[1] > 1:  # only helpers' verdicts need binding to the bytes they checked
-        with timers.span("rp.verify.slice_digests"):
-            ok_idx = [i for i in union if base[i]]
-            digests = dict(zip(ok_idx, lists_digests([parts[i] for i in ok_idx])))
+        ok_idx = [i for i in union if base[i]]
+        if async_digests:
+            digests = _slice_digests_async(ok_idx, [parts[i] for i in ok_idx], device)
+        else:
+            with timers.span("rp.verify.slice_digests"):
+                digests = dict(zip(ok_idx, lists_digests([parts[i] for i in ok_idx])))
     P = sq.RosterServers.aggregate()
     mode = int(getattr(sq, "RangeProofMode", 0) or 0)
     by_set: dict = {}

@@ -191,7 +191,10 @@ def pool_verify_ranges(ctx, sq, reqs: list, vns: list, comm=None) -> dict:
     # latency-bound kernels leave the GPU room), not after the gather
     exp_f = _expected_async(ctx, sq, reqs, vn_idxs, local_vns, W) \
         if local_vns and W > 1 and os.environ.get("DRYNX_DIGEST_ASYNC", "1") == "1" else None
-    res, digests = prq.verify_range_pool_part(reqs, vn_idxs, sq, ctx.device, ctx.verifier_cache, (k, W), part_coins)
+    res, digests = prq.verify_range_pool_part(reqs, vn_idxs, sq, ctx.device, ctx.verifier_cache, (k, W), part_coins,
+                                              async_digests=True)
+    if hasattr(digests, "result"):
+        digests = digests.result()
     mine = {vn.id: {reqs[i].base_key(): bool(ok) for i, ok in res.get(vn.id, {}).items()} for vn in vns}
     mydig = {reqs[i].base_key(): d for i, d in digests.items()}
     gathered = comm.all_gather_object((mine, mydig))

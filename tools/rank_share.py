@@ -53,6 +53,13 @@ def _sync():
         torch.cuda.synchronize()
 
 
+def pool_part(*a):
+    """prq.verify_range_pool_part as pool_verify_ranges runs it (slice digests
+    beside the part), digests resolved."""
+    res, dig = prq.verify_range_pool_part(*a, async_digests=True)
+    return res, (dig.result() if hasattr(dig, "result") else dig)
+
+
 def timed(fn, reps):
     fn()
     ts = []
@@ -196,8 +203,8 @@ def main():
             _sync()
             time.sleep(1.0)  # an idle gap: a kernel trace shows this part as its own burst (tools/kernel_bursts.py)
             with timers.span(f"pool_part[{k}]"):
-                prq.verify_range_pool_part(reqs_k, {v: list(range(len(rng))) for v in vn_idxs}, sq, dev, cache,
-                                           (k, W), {vn.id: Coins() for vn in cl.vns})
+                pool_part(reqs_k, {v: list(range(len(rng))) for v in vn_idxs}, sq, dev, cache, (k, W),
+                          {vn.id: Coins() for vn in cl.vns})
             _sync()
         timers.dump_trace(os.environ["DRYNX_TRACE"])
         if os.environ.get("RANK_SHARE_TRACE_ONLY") == "1":
@@ -228,12 +235,11 @@ def main():
                 if dst is not None:
                     dst.wait_stream(torch.cuda.current_stream(dev))
                 fut = dig_pool.submit(digests_side)
-                prq.verify_range_pool_part(full_reqs(), {v: list(range(len(rng))) for v in vn_idxs}, sq, dev, cache,
-                                           part, coins)
+                pool_part(full_reqs(), {v: list(range(len(rng))) for v in vn_idxs}, sq, dev, cache, part, coins)
                 fut.result()
             t_pool = timed(vn_part, a.reps)
         else:
-            t_pool = timed(lambda: prq.verify_range_pool_part(helper_reqs(part), {v: list(range(len(rng)))
+            t_pool = timed(lambda: pool_part(helper_reqs(part), {v: list(range(len(rng)))
                                                                                   for v in vn_idxs},
                                                               sq, dev, cache, part, coins), a.reps)
         t_dig = 0.0
