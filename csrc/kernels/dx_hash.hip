@@ -154,6 +154,36 @@ extern "C" int dx_random_scalars(int on_gpu, void *stream, const uint32_t *key_h
   return run(on_gpu, stream, n, op, false, "random_scalars");
 }
 
+// GLV batch weights straight from the generator (one launch instead of the
+// generator + slicing + two Fr ops): item i's scalar x_i exactly as
+// dx_random_scalars draws it, a = limb 0 and b = limb 1 of x_i (32-bit
+// halves), rho_i = a + b * lambda mod r.  lam: lambda as 8 canonical limbs.
+extern "C" int dx_prg_glv(int on_gpu, void *stream, const uint32_t *key_host, uint32_t counter0, const uint32_t *lam_host,
+                          int32_t *ab, uint32_t *rho, int64_t n) {
+  struct K8 {
+    uint32_t k[8];
+  } kk, ll;
+  for (int i = 0; i < 8; i++) {
+    kk.k[i] = key_host[i];
+    ll.k[i] = lam_host[i];
+  }
+  auto op = [=] __host__ __device__(int64_t i) {
+    uint32_t blk[16];
+    chacha20_block(kk.k, counter0 + (uint32_t)i, blk);
+    Fr lo = reduce_256<FrParams>(blk);
+    Fr hi = reduce_256<FrParams>(blk + 8);
+    Fr x = fadd(lo, to_mont(hi));
+    if (x.is_zero()) x.v[0] = 1;
+    const uint32_t a = x.v[0], b = x.v[1];
+    ab[2 * i] = (int32_t)a;
+    ab[2 * i + 1] = (int32_t)b;
+    uint32_t wa[8] = {a, 0, 0, 0, 0, 0, 0, 0}, wb[8] = {b, 0, 0, 0, 0, 0, 0, 0};
+    const Fr A = reduce_256<FrParams>(wa), B = reduce_256<FrParams>(wb), L = reduce_256<FrParams>(ll.k);
+    at<Fr>(rho, i) = fadd(A, fmul(B, to_mont(L)));
+  };
+  return run(on_gpu, stream, n, op, false, "prg_glv");
+}
+
 // out[i] = 8 big-endian words of SHA-256(data[i*chunk, min(len, (i+1)*chunk)))
 extern "C" int dx_sha256_chunks(int on_gpu, void *stream, const uint8_t *data, int64_t len, int64_t chunk,
                                 uint32_t *out) {

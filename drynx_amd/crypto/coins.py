@@ -71,7 +71,7 @@ class Coins:
     def glv(self, n: int, device):
         """GLV batch weights rho = a + b lambda with 32-bit halves (see
         ``native.glv_weights``) drawn from this stream."""
-        return nt.glv_weights(n, device, raw=self.scalars(n, device))
+        return nt.prg_glv(self._next_key(), n, device)
 
     def random(self) -> float:
         """Uniform float in [0, 1) (sampling decisions)."""

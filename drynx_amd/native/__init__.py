@@ -82,6 +82,7 @@ _SIGS = {
     "dx_pairing": [_I, _P, _P, _P, _P, _L],
     "dx_gt_mul": [_I, _P, _P, _P, _P, _L],
     "dx_gt_inv": [_I, _P, _P, _P, _L],
+    "dx_prg_glv": [_I, _P, _P, ctypes.c_uint32, _P, _P, _P, _L],
     "dx_batched_copy": [_I, _P, _P, _P, _I, _L],
     "dx_rows_all": [_I, _P, _P, _P, _I, _L, _P],
     "dx_gt_pow": [_I, _P, _P, _P, _P, _L, _I],
@@ -1272,6 +1273,28 @@ def _glv_const(kind: str, device) -> torch.Tensor:
             v = _bn.to_tensor(_bn.ints_to_limbs([GLV_LAMBDA]), device)
         _glv_consts[key] = v.contiguous()
     return _glv_consts[key]
+
+
+def prg_glv(key: bytes, n: int, device):
+    """``glv_weights(n, device, raw=prg_scalars(key, n, device))`` in ONE
+    launch (csrc/kernels/dx_hash.hip dx_prg_glv) -> (ab [n, 2], rho [n, 8])."""
+    device = torch.device(device)
+    ab = torch.empty((max(0, n), 2), dtype=torch.int32, device=device)
+    rho = torch.empty((max(0, n), 8), dtype=torch.int32, device=device)
+    if n <= 0:
+        return ab, rho
+    k = np.frombuffer(key[:32], dtype="<u4").copy()
+    lam = np.asarray(_lambda_limbs(), dtype=np.uint32)
+    g, s = _ctx(ab)
+    _call("dx_prg_glv", g, s, k.ctypes.data_as(ctypes.c_void_p), 0, lam.ctypes.data_as(ctypes.c_void_p), _ptr(ab),
+          _ptr(rho), n)
+    return ab, rho
+
+
+def _lambda_limbs() -> list:
+    from ..crypto import bn254 as _bn
+
+    return [int(x) for x in _bn.ints_to_limbs([GLV_LAMBDA]).reshape(-1)]
 
 
 def glv_weights(n: int, device, raw: torch.Tensor | None = None):

@@ -68,3 +68,17 @@ def test_digest_many_matches_single():
     got = dg.digest_many(ts)
     for t, d in zip(ts, got):
         assert d == dg.digest_bytes(t.numpy().tobytes())
+
+
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def test_prg_glv_matches_generator_then_glv(device):
+    """The fused GLV-weight draw equals the generator's scalars turned into
+    GLV weights (32-bit halves a, b of each scalar; rho = a + b lambda)."""
+    if device == "cuda" and not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    key = bytes(range(32))
+    ab, rho = nt.prg_glv(key, 1000, device)
+    ab2, rho2 = nt.glv_weights(1000, device, raw=nt.prg_scalars(key, 1000, device))
+    assert torch.equal(ab.cpu(), ab2.cpu()) and torch.equal(rho.cpu(), rho2.cpu())
+    a, b = int(ab[7, 0]) & 0xFFFFFFFF, int(ab[7, 1]) & 0xFFFFFFFF
+    assert bn.scalars_from_tensor(rho[7:8].cpu())[0] == (a + b * nt.GLV_LAMBDA) % O.R
