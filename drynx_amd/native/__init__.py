@@ -1214,7 +1214,7 @@ def rp_fold_points(ZB_jac: torch.Tensor, Y_jac: torch.Tensor, rho: torch.Tensor,
     P = out if out is not None else torch.empty((n, 16), dtype=torch.int32, device=rho.device)
     assert P.shape == (n, 16) and P.is_contiguous()
     _, s = _ctx(ZB_jac, Y_jac, rho)
-    rc = getattr(_load(), f"dx_rp_points_{v}")(s, _ptr(ZB_jac.contiguous()), _ptr(Y_jac.contiguous()), _ptr(rho),
+    rc = _raw_call(f"dx_rp_points_{v}", s, _ptr(ZB_jac.contiguous()), _ptr(Y_jac.contiguous()), _ptr(rho),
                                                   _ptr(P), n, S, L)
     if rc:
         raise RuntimeError(f"dx_rp_points_{v} failed rc={rc}")
@@ -1236,7 +1236,7 @@ def rp_fold_lines(P_aff: torch.Tensor, V_aff: torch.Tensor, variant: str | None 
     steps = getattr(_load(), f"dx_fold_steps_{v}")()
     lines = torch.empty((steps * 12 * n * 4,), dtype=torch.int32, device=P_aff.device)
     _, s = _ctx(P_aff, V_aff)
-    rc = getattr(_load(), f"dx_rp_lines_{v}")(s, _ptr(P_aff), _ptr(V_aff), _ptr(lines), n, period, nv)
+    rc = _raw_call(f"dx_rp_lines_{v}", s, _ptr(P_aff), _ptr(V_aff), _ptr(lines), n, period, nv)
     if rc:
         raise RuntimeError(f"dx_rp_lines_{v} failed rc={rc}")
     return lines
@@ -1248,7 +1248,7 @@ def rp_fold_accum(lines: torch.Tensor, n: int, K: int = 4, variant: str | None =
     v = variant or FOLD_VARIANT
     fb = torch.empty(((n + 64 * K - 1) // (64 * K), 96), dtype=torch.int32, device=lines.device)
     _, s = _ctx(lines)
-    rc = getattr(_load(), f"dx_rp_accum_{v}")(s, _ptr(lines), _ptr(fb), n, K)
+    rc = _raw_call(f"dx_rp_accum_{v}", s, _ptr(lines), _ptr(fb), n, K)
     if rc:
         raise RuntimeError(f"dx_rp_accum_{v} failed rc={rc}")
     return fb
@@ -1369,7 +1369,7 @@ def rp_fold_ncoeffs(V_aff: torch.Tensor, variant: str | None = None) -> torch.Te
     img = torch.empty((steps * 8 * m * 4,), dtype=torch.int32, device=V_aff.device)
     scratch = torch.empty((2 * steps * 4 * m * 4,), dtype=torch.int32, device=V_aff.device)
     _, s = _ctx(V_aff)
-    rc = getattr(_load(), f"dx_rp_ncoeffs_{v}")(s, _ptr(V_aff), _ptr(img), _ptr(scratch), m)
+    rc = _raw_call(f"dx_rp_ncoeffs_{v}", s, _ptr(V_aff), _ptr(img), _ptr(scratch), m)
     if rc:
         raise RuntimeError(f"dx_rp_ncoeffs_{v} failed rc={rc}")
     return img
@@ -1386,7 +1386,7 @@ def rp_fold_accum_n(img: torch.Tensor, UV: torch.Tensor, V_aff: torch.Tensor, pe
     assert img.numel() == steps * 8 * m * 4
     fb = torch.empty((G * period // (64 * K), 96), dtype=torch.int32, device=UV.device)
     _, s = _ctx(img, UV, V_aff)
-    rc = getattr(_load(), f"dx_rp_accum_n_{v}")(s, _ptr(img), _ptr(UV), _ptr(V_aff), _ptr(fb), m, period, G, K)
+    rc = _raw_call(f"dx_rp_accum_n_{v}", s, _ptr(img), _ptr(UV), _ptr(V_aff), _ptr(fb), m, period, G, K)
     if rc:
         raise RuntimeError(f"dx_rp_accum_n_{v} failed rc={rc}")
     return fb
@@ -1412,7 +1412,7 @@ def rp_fold_coeffs(V_aff: torch.Tensor, variant: str | None = None) -> torch.Ten
     steps = getattr(_load(), f"dx_fold_steps_{v}")()
     coef = torch.empty((steps * 12 * m * 4,), dtype=torch.int32, device=V_aff.device)
     _, s = _ctx(V_aff)
-    rc = getattr(_load(), f"dx_rp_coeffs_{v}")(s, _ptr(V_aff), _ptr(coef), m)
+    rc = _raw_call(f"dx_rp_coeffs_{v}", s, _ptr(V_aff), _ptr(coef), m)
     if rc:
         raise RuntimeError(f"dx_rp_coeffs_{v} failed rc={rc}")
     return coef
@@ -1433,7 +1433,7 @@ def rp_fold_accum_p(coef: torch.Tensor, P_aff: torch.Tensor, V_aff: torch.Tensor
     assert coef.numel() == steps * 12 * m * 4
     fb = torch.empty((G * period // (64 * K), 96), dtype=torch.int32, device=P_aff.device)
     _, s = _ctx(coef, P_aff, V_aff)
-    rc = getattr(_load(), f"dx_rp_accum_p_{v}")(s, _ptr(coef), _ptr(P_aff), _ptr(V_aff), _ptr(fb), m, period, G, K)
+    rc = _raw_call(f"dx_rp_accum_p_{v}", s, _ptr(coef), _ptr(P_aff), _ptr(V_aff), _ptr(fb), m, period, G, K)
     if rc:
         raise RuntimeError(f"dx_rp_accum_p_{v} failed rc={rc}")
     return fb
