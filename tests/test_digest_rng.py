@@ -82,3 +82,24 @@ def test_prg_glv_matches_generator_then_glv(device):
     assert torch.equal(ab.cpu(), ab2.cpu()) and torch.equal(rho.cpu(), rho2.cpu())
     a, b = int(ab[7, 0]) & 0xFFFFFFFF, int(ab[7, 1]) & 0xFFFFFFFF
     assert bn.scalars_from_tensor(rho[7:8].cpu())[0] == (a + b * nt.GLV_LAMBDA) % O.R
+
+
+@pytest.mark.gpu
+def test_gpu_slice_hashes_match_hashlib(gpu_device):
+    """The LDS-staged slice hashing (csrc/kernels/dx_hash.hip sha_slices_kernel)
+    against hashlib: payloads of every tail shape (empty, < 1 block, exact
+    blocks, several 4 KiB slices with a partial last one), 4-byte-offset views,
+    many segments in one launch (more lanes than slices in the last wave) and
+    equal-length rows."""
+    rng = np.random.default_rng(5)
+    sizes = [0, 4, 60, 64, 120, 4096, 4100, 3 * 4096 + 64, 70000, 1 << 20]
+    host = [rng.integers(0, 2**31, size=(n + 3) // 4, dtype=np.int64).astype(np.int32)[: n // 4] for n in sizes]
+    ts = [torch.from_numpy(h).to(gpu_device) for h in host]
+    base = torch.from_numpy(rng.integers(0, 2**31, size=50001, dtype=np.int64).astype(np.int32)).to(gpu_device)
+    ts.append(base[1:])                                   # a view starting 4 bytes into its storage
+    host.append(base[1:].cpu().numpy())
+    for t, h in zip(ts, host):
+        assert D.digest_tensor(t) == D.digest_bytes(h.tobytes()), len(h)
+    assert D.digest_many(ts) == [D.digest_bytes(h.tobytes()) for h in host]
+    rows = torch.from_numpy(rng.integers(0, 2**31, size=(7, 3000), dtype=np.int64).astype(np.int32)).to(gpu_device)
+    assert D.digest_rows(rows) == [D.digest_bytes(r.tobytes()) for r in rows.cpu().numpy()]
