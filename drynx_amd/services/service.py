@@ -183,7 +183,9 @@ class DrynxNode:
         W = self.comm.world
         vn_ranks = sorted({vn.rank for vn in self.cluster.vns})
         lws = int(os.environ.get("LOCAL_WORLD_SIZE", "0") or 0)
-        run = os.environ.get("TORCHELASTIC_RUN_ID") or os.environ.get("MASTER_PORT")
+        # one directory per job: torchrun's run id (often "none" when standalone)
+        # plus the rendezvous port, so consecutive or concurrent jobs never share it
+        run = "_".join(x for x in (os.environ.get("TORCHELASTIC_RUN_ID"), os.environ.get("MASTER_PORT")) if x)
         if (W > 1 and lws == W and run and len(vn_ranks) > 1 and self.rank in vn_ranks
                 and os.environ.get("DRYNX_LEDGER_NODE_SHARE", "1") == "1"):
             root = os.path.join(os.path.dirname(os.path.abspath(self.workdir)), f"drynx_node_ledger_{run}")
