@@ -30,6 +30,7 @@ import hashlib
 import io
 import math
 import os
+import threading
 from dataclasses import dataclass
 
 import numpy as np
@@ -1058,6 +1059,7 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
                              nt.fr_dot_rows(w_all, z, G, b_periodic=True)], 1)             # [G, 2, 8]
     if device.type == "cuda":
         with timers.span("rp.verify.multiexp"):
+            run_idle_tasks()  # host work queued by the caller, in the GPU's busiest window
             aux.synchronize()                                          # aux results are read on this stream/host
             GG = nt.multi_exp_grouped_finish(mexp)                     # [2G, 96]: prod a^rho_v, prod a^gamma_v
             D_all = dcheck.cpu() if ddirect else nt.g1_msm_finish(dcheck)  # [2G, 24]
@@ -1165,6 +1167,43 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
             else:
                 res[k_] = per[k_] if not all(per[k_]) else None  # nothing attributable: the caller bisects
     return res
+
+
+_idle = threading.local()
+
+
+class Deferred:
+    """A host computation run once, at the first of ``run()`` (e.g. from
+    ``run_idle_tasks`` while the verifier waits for its device work) or
+    ``result()``."""
+
+    def __init__(self, fn):
+        self.fn, self.done, self.value = fn, False, None
+
+    def run(self):
+        if not self.done:
+            self.value, self.done = self.fn(), True
+
+    def result(self):
+        self.run()
+        return self.value
+
+
+def add_idle_task(d: Deferred) -> Deferred:
+    """Queue host work for this thread's next verifier wait: the batch
+    verifier runs it right before it blocks on the device (its passes then
+    keep the GPU busy for milliseconds while the host is idle), instead of a
+    second thread contending for the GIL with the verifier's host work."""
+    if not hasattr(_idle, "tasks"):
+        _idle.tasks = []
+    _idle.tasks.append(d)
+    return d
+
+
+def run_idle_tasks():
+    tasks = getattr(_idle, "tasks", None)
+    while tasks:
+        tasks.pop(0).run()
 
 
 class _nullctx:

@@ -673,22 +673,17 @@ def _verify_range_group(reqs, idxs, sq, device, cache, part, coins_list: list) -
     return outs
 
 
-_dig_pool = None
 _dig_streams: dict = {}
 
 
 def _slice_digests_async(ok_idx: list, entries: list, device):
-    """``lists_digests`` of this part's slices on a worker thread with its own
-    HIP stream (ordered after the caller's stream): the digests are needed
-    only for the gather after the part, so they no longer delay its start."""
-    global _dig_pool
-    import concurrent.futures as cf
-
-    if _dig_pool is None:
-        _dig_pool = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="drynx-slice-digests")
+    """``lists_digests`` of this part's slices as an idle task of the part's
+    verifier (run while it waits for its device passes, on a HIP stream of
+    its own ordered after the caller's): the digests are needed only for the
+    gather after the part, so they no longer delay its start."""
     dev = torch.device(device)
     if dev.type != "cuda":
-        return _dig_pool.submit(lambda: dict(zip(ok_idx, lists_digests(entries))))
+        return rp.add_idle_task(rp.Deferred(lambda: dict(zip(ok_idx, lists_digests(entries)))))
     st = _dig_streams.get(str(dev))
     if st is None:
         st = _dig_streams[str(dev)] = torch.cuda.Stream(dev)
@@ -697,7 +692,7 @@ def _slice_digests_async(ok_idx: list, entries: list, device):
     def run():
         with torch.cuda.stream(st), timers.span("rp.verify.slice_digests"):
             return dict(zip(ok_idx, lists_digests(entries)))
-    return _dig_pool.submit(run)
+    return rp.add_idle_task(rp.Deferred(run))
 
 
 def verify_range_pool_part(reqs: list, vn_idxs: dict, sq, device, cache: VerifierCache, part, coins: dict,

@@ -229,14 +229,14 @@ def pool_verify_ranges(ctx, sq, reqs: list, vns: list, comm=None) -> dict:
 
 
 def _expected_async(ctx, sq, reqs, vn_idxs: dict, local_vns: list, W: int):
-    """``_expected_digests`` on a worker thread with its own HIP stream
-    (ordered after the caller's stream, where the payloads were received)."""
-    import concurrent.futures as cf
+    """``_expected_digests`` as an idle task of this rank's pool part (run
+    while its verifier waits for the device, on a HIP stream of its own
+    ordered after the caller's, where the payloads were received): no second
+    thread contending for the GIL with the part's host work."""
+    from ..proofs import range_proof as rp
 
-    if not hasattr(ctx, "_dig_exec"):
-        ctx._dig_exec = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="drynx-vn-digests")
     if ctx.device.type != "cuda":
-        return ctx._dig_exec.submit(_expected_digests, ctx, sq, reqs, vn_idxs, local_vns, W)
+        return rp.add_idle_task(rp.Deferred(lambda: _expected_digests(ctx, sq, reqs, vn_idxs, local_vns, W)))
     if not hasattr(ctx, "_dig_stream"):
         ctx._dig_stream = torch.cuda.Stream(ctx.device)
     st, cur = ctx._dig_stream, torch.cuda.current_stream(ctx.device)
@@ -245,7 +245,7 @@ def _expected_async(ctx, sq, reqs, vn_idxs: dict, local_vns: list, W: int):
     def run():
         with torch.cuda.stream(st):
             return _expected_digests(ctx, sq, reqs, vn_idxs, local_vns, W)
-    return ctx._dig_exec.submit(run)
+    return rp.add_idle_task(rp.Deferred(run))
 
 
 def _expected_digests(ctx, sq, reqs, vn_idxs: dict, local_vns: list, W: int):

@@ -13,8 +13,8 @@ signed range-proof inbox, and then times, alone and synchronised (median of
   the slice payloads it would receive (unpack included), on a VN rank from
   the full signed payloads (decode of the whole inbox included);
 * digests(k): a VN rank's recomputation of the other ranks' slice digests
-  (run beside its pool part, on their own thread and stream, as the
-  framework does; also timed alone for reference);
+  (run inside its pool part while the verifier waits for the device, on a
+  stream of their own, as the framework does; also timed alone for reference);
 * serial: the query's non-range critical path (CN phases, querier, per-CN
   proofs, block), taken from a ``--u 0 --l 0`` bench JSON (``--serial-json``).
 
@@ -26,7 +26,6 @@ those).  Usage: python tools/rank_share.py [--world 8] [--reps 5] [--serial-json
 from __future__ import annotations
 
 import argparse
-import concurrent.futures as cf
 import contextlib
 import copy
 import json
@@ -41,6 +40,7 @@ import torch  # noqa: E402
 
 from drynx_amd.crypto.coins import Coins  # noqa: E402
 from drynx_amd.protocols import proof_collection as pcp  # noqa: E402
+from drynx_amd.proofs import range_proof as rp  # noqa: E402
 from drynx_amd.proofs import requests as prq  # noqa: E402
 from drynx_amd.query import LogisticRegressionParameters, new_survey_id  # noqa: E402
 from drynx_amd.services.api import DrynxClient  # noqa: E402
@@ -210,7 +210,6 @@ def main():
         if os.environ.get("RANK_SHARE_TRACE_ONLY") == "1":
             node.close(remove=True)
             return
-    dig_pool = cf.ThreadPoolExecutor(max_workers=1)
     res = {"world": W, "features": d,
            "placement": {k: {"parties": place.get(k, []), "dps": dps_of[k]} for k in range(W)},
            "ranks": {}}
@@ -231,10 +230,11 @@ def main():
 
             def vn_part():
                 # as proof_collection.pool_verify_ranges: the VN's digests of the
-                # other ranks' slices run on their own thread and stream beside the part
+                # other ranks' slices run on their own stream as an idle task of
+                # the part (while its verifier waits for the device)
                 if dst is not None:
                     dst.wait_stream(torch.cuda.current_stream(dev))
-                fut = dig_pool.submit(digests_side)
+                fut = rp.add_idle_task(rp.Deferred(digests_side))
                 pool_part(full_reqs(), {v: list(range(len(rng))) for v in vn_idxs}, sq, dev, cache, part, coins)
                 fut.result()
             t_pool = timed(vn_part, a.reps)
