@@ -1,0 +1,9 @@
+#!/bin/bash
+# Idle-task digests: W=8 rank shares again, with the GPU tests they touch.
+set -o pipefail
+mkdir -p gpurun_out
+export HSA_ENABLE_IPC_MODE_LEGACY=0 TMPDIR=/tmp
+step() { local name=$1; shift; timeout -k 10 "$@" > gpurun_out/$name.log 2>&1; local rc=$?; tail -1 gpurun_out/$name.log | cut -c1-300; if [ $rc -ne 0 ]; then tail -30 gpurun_out/$name.log; exit $rc; fi; }
+step d_tests 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu tests/test_digest_rng.py tests/test_pool.py tests/test_rpmsm.py
+step d_share 600 python -u tools/rank_share.py --world 8 --reps 3 --serial-json profiles/r4/checkpoint_u0l0.json --json-out gpurun_out/d_rank_share_w8.json
+step d_bench 300 python -u bench.py --steps 10 --warmup 2 --json-out gpurun_out/d_bench.json
