@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import hashlib
 import math
+import os
 import random
 from typing import Any
 
@@ -568,11 +569,40 @@ def verify_range_many_multi(reqs: list, vn_idxs: dict, sq, device, cache: Verifi
 def sampled_bounds(sq, n: int, part=None) -> tuple:
     """[lo, hi) of a list of n proofs that a verifier checks: the sampled
     prefix ceil(RangeProofThreshold * n) (range_proof.go:486), or its k-th of
-    W equal slices for ``part = (k, W)``."""
+    W equal slices for ``part = (k, W)``, or of W weighted slices for
+    ``part = (k, W, c_0, ..., c_W)`` (cumulative integer weights, c_0 = 0)."""
     k = int(math.ceil(sq.RangeProofThreshold * n))
     if part is None:
         return 0, k
+    if len(part) > 2:
+        c = part[2:]
+        return (k * c[part[0]]) // c[-1], (k * c[part[0] + 1]) // c[-1]
     return (k * part[0]) // part[1], (k * (part[0] + 1)) // part[1]
+
+
+# extra work of a rank, in units of a plain helper's pool share, that its
+# slice is shortened by: every DP it hosts beyond the fewest any rank hosts
+# (proving a 2,070-output DP: ~5.4 ms against a ~38 ms 1/8 part, whose
+# size-dependent half scales with the slice), and every VN it hosts (the
+# full-inbox decode and the digests of the other slices)
+_POOL_DP_W, _POOL_VN_W = 0.32, 0.12
+
+
+def balanced_parts(W: int, dps: list, vns: list) -> list:
+    """Pool parts for W ranks weighted so every rank's proving + checking
+    ends together: rank k's slice weight 1 - 0.32 (extra DPs) - 0.12 (VNs)
+    (floor 0.25), as (k, W, cumulative weights) tuples (``sampled_bounds``).
+    Calibrated from one-GPU measurements of each rank's share
+    (tools/rank_share.py, profiles/r4/rank_share_*)."""
+    if W <= 1 or os.environ.get("DRYNX_POOL_BALANCE", "1") == "0":
+        return [(k, W) for k in range(W)]
+    lo = min(dps)
+    w = [max(0.25, 1.0 - _POOL_DP_W * (dps[k] - lo) - _POOL_VN_W * vns[k]) for k in range(W)]
+    iw = [max(1, int(round(1000 * x))) for x in w]
+    cum = [0]
+    for x in iw:
+        cum.append(cum[-1] + x)
+    return [(k, W, *cum) for k in range(W)]
 
 
 def _range_parts(reqs, idxs, sq, device, part):

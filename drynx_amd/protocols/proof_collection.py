@@ -22,6 +22,7 @@ import time
 
 import torch
 
+from .. import native as nt
 from ..ledger import skipchain as skc
 from ..parallel.netem import CT_BYTES, POINT_BYTES, SCALAR_BYTES, SIG_BYTES, flow_hops, range_proof_bytes
 from .data_collection import all_possible_groups as dcp_groups
@@ -65,6 +66,20 @@ def _net_proofs(ctx, sq, reqs: list, vns: list):
                  hops=flow_hops("proofs_to_vns"))
 
 
+def pool_parts(ctx, sq) -> list:
+    """Every rank's pool part for this survey (``prq.balanced_parts``): ranks
+    hosting more DPs or a VN check shorter slices; identical on every rank
+    (a function of the placement only)."""
+    W = ctx.comm.world
+    dps, vns = [0] * W, [0] * W
+    for _, members in (sq.ServerToDP or {}).items():
+        for si in members or []:
+            dps[ctx.cluster.by_id(si.id).rank] += 1
+    for si in sq.Query.RosterVNs.list:
+        vns[ctx.cluster.by_id(si.id).rank] += 1
+    return prq.balanced_parts(W, dps, vns)
+
+
 def use_pool(ctx) -> bool:
     """Pooled range verification (single-operator deployments only): every
     rank checks a 1/world slice of every range-proof list on behalf of every
@@ -99,6 +114,7 @@ def fan_out(ctx, sq, local_requests: list, pool: bool = False) -> list:
     per_rank = {d: [] for d in dests}
     per_rank_t = {d: [] for d in dests}
     packed = {}
+    parts = pool_parts(ctx, sq) if pool else None
     for idx, r in enumerate(local_requests):
         assigned = prq.assigned_vns(sq, r, len(vns))
         full_ranks = set(vn_ranks) if (assigned is None or pool) else {vns[i].rank for i in assigned}
@@ -108,11 +124,11 @@ def fan_out(ctx, sq, local_requests: list, pool: bool = False) -> list:
             if d not in full_ranks:
                 if pool and r.kind == "range" and r.obj is not None and d not in vn_ranks:
                     # a helper: its slice of the bundle (the pool's part d of W)
-                    sl = _helper_slice(r.obj, sq, (d, W))
+                    sl = _helper_slice(r.obj, sq, parts[d])
                     w = r.header().to_wire()
                     if sl:
                         t = prq.range_bundle_pack(sl).to(ctx.device)
-                        w["tensor"], w["slice"] = t.numel(), [d, W]
+                        w["tensor"], w["slice"] = t.numel(), list(parts[d])
                         per_rank_t[d].append(t)
                     per_rank[d].append(w)
                 else:
@@ -128,7 +144,8 @@ def fan_out(ctx, sq, local_requests: list, pool: bool = False) -> list:
                 per_rank[d].append(r.to_wire())
     got = ctx.comm.exchange_bytes({d: obj_to_bytes(per_rank[d]) for d in dests if d != ctx.rank})
     wires = {src: bytes_to_obj(b) for src, b in got.items()}
-    tens = {d: torch.cat(per_rank_t[d]) for d in dests if per_rank_t[d]}
+    tens = {d: t for d, t in zip([d for d in dests if per_rank_t[d]],
+                                  nt.cat_rows([per_rank_t[d] for d in dests if per_rank_t[d]]))}
     # the envelopes announced every tensor's size: no size round for the payloads
     sizes = {src: sum(w.get("tensor") or 0 for w in ws) for src, ws in wires.items()}
     got_t = ctx.comm.exchange(tens, recv_sizes={s_: n_ for s_, n_ in sizes.items() if n_})
@@ -184,15 +201,16 @@ def pool_verify_ranges(ctx, sq, reqs: list, vns: list, comm=None) -> dict:
             sampled[vid], seeds[vid] = smp, seed
     vn_idxs = {vn.id: [i for i in rng if sampled[vn.id].get(reqs[i].base_key())] for vn in vns}
     part_coins = {vn.id: Coins(seeds[vn.id]).derive(("slice", k, W)) for vn in vns}
+    parts = pool_parts(ctx, sq)
     t0 = time.perf_counter()
     local_vns = [vn for vn in vns if vn.rank == ctx.rank]
     # a VN rank's digests of the other ranks' slices of its own payloads run
     # beside this rank's pool part (their own thread and stream: the part's
     # latency-bound kernels leave the GPU room), not after the gather
-    exp_f = _expected_async(ctx, sq, reqs, vn_idxs, local_vns, W) \
+    exp_f = _expected_async(ctx, sq, reqs, vn_idxs, local_vns, W, parts) \
         if local_vns and W > 1 and os.environ.get("DRYNX_DIGEST_ASYNC", "1") == "1" else None
-    res, digests = prq.verify_range_pool_part(reqs, vn_idxs, sq, ctx.device, ctx.verifier_cache, (k, W), part_coins,
-                                              async_digests=True)
+    res, digests = prq.verify_range_pool_part(reqs, vn_idxs, sq, ctx.device, ctx.verifier_cache, parts[k],
+                                              part_coins, async_digests=True)
     if hasattr(digests, "result"):
         digests = digests.result()
     mine = {vn.id: {reqs[i].base_key(): bool(ok) for i, ok in res.get(vn.id, {}).items()} for vn in vns}
@@ -201,7 +219,7 @@ def pool_verify_ranges(ctx, sq, reqs: list, vns: list, comm=None) -> dict:
     out = {}
     if local_vns:
         trusted = _check_helper_digests(ctx, sq, reqs, vn_idxs, local_vns, gathered, W,
-                                        exp_f.result() if exp_f is not None else None)
+                                        exp_f.result() if exp_f is not None else None, parts)
     for vn in vns:
         if vn.rank != ctx.rank:
             continue
@@ -219,7 +237,7 @@ def pool_verify_ranges(ctx, sq, reqs: list, vns: list, comm=None) -> dict:
                 c = ctx.vn_coins(vn.id)
                 for j, idxs in redo.items():
                     r2, _ = prq.verify_range_pool_part(reqs, {vn.id: idxs}, sq, ctx.device, ctx.verifier_cache,
-                                                       (j, W), {vn.id: c})
+                                                       parts[j], {vn.id: c})
                     for i, ok in r2[vn.id].items():
                         key = reqs[i].base_key()
                         verdict[key] = bool(verdict.get(key)) and bool(ok)
@@ -228,7 +246,7 @@ def pool_verify_ranges(ctx, sq, reqs: list, vns: list, comm=None) -> dict:
     return out
 
 
-def _expected_async(ctx, sq, reqs, vn_idxs: dict, local_vns: list, W: int):
+def _expected_async(ctx, sq, reqs, vn_idxs: dict, local_vns: list, W: int, parts: list):
     """``_expected_digests`` as an idle task of this rank's pool part (run
     while its verifier waits for the device, on a HIP stream of its own
     ordered after the caller's, where the payloads were received): no second
@@ -236,7 +254,7 @@ def _expected_async(ctx, sq, reqs, vn_idxs: dict, local_vns: list, W: int):
     from ..proofs import range_proof as rp
 
     if ctx.device.type != "cuda":
-        return rp.add_idle_task(rp.Deferred(lambda: _expected_digests(ctx, sq, reqs, vn_idxs, local_vns, W)))
+        return rp.add_idle_task(rp.Deferred(lambda: _expected_digests(ctx, sq, reqs, vn_idxs, local_vns, W, parts)))
     if not hasattr(ctx, "_dig_stream"):
         ctx._dig_stream = torch.cuda.Stream(ctx.device)
     st, cur = ctx._dig_stream, torch.cuda.current_stream(ctx.device)
@@ -244,11 +262,11 @@ def _expected_async(ctx, sq, reqs, vn_idxs: dict, local_vns: list, W: int):
 
     def run():
         with torch.cuda.stream(st):
-            return _expected_digests(ctx, sq, reqs, vn_idxs, local_vns, W)
+            return _expected_digests(ctx, sq, reqs, vn_idxs, local_vns, W, parts)
     return rp.add_idle_task(rp.Deferred(run))
 
 
-def _expected_digests(ctx, sq, reqs, vn_idxs: dict, local_vns: list, W: int):
+def _expected_digests(ctx, sq, reqs, vn_idxs: dict, local_vns: list, W: int, parts: list | None = None):
     """Digests of every other rank's slice of the local VNs' signed payloads
     -> ({(request, part): digest}, {(request, part) with an empty slice})."""
     me = ctx.rank
@@ -265,7 +283,7 @@ def _expected_digests(ctx, sq, reqs, vn_idxs: dict, local_vns: list, W: int):
             for j in range(W):
                 if j == me:
                     continue  # this rank's own part was checked from this very payload
-                sl = prq.slice_lists(lists, sq, (j, W))
+                sl = prq.slice_lists(lists, sq, parts[j] if parts is not None else (j, W))
                 if not sl:
                     empty.add((i, j))
                     continue
@@ -277,13 +295,13 @@ def _expected_digests(ctx, sq, reqs, vn_idxs: dict, local_vns: list, W: int):
 
 
 def _check_helper_digests(ctx, sq, reqs, vn_idxs: dict, local_vns: list, gathered: list, W: int,
-                          pre=None) -> dict:
+                          pre=None, parts: list | None = None) -> dict:
     """For each local VN: the (base_key, part) pairs whose helper-reported
     slice digest equals the digest of that slice of the VN's own signed
     payload, and the mismatches to redo ({part: [request index]}).
     ``pre``: the (expected, empty) of ``_expected_digests`` computed earlier."""
     me = ctx.rank
-    expected, empty = pre if pre is not None else _expected_digests(ctx, sq, reqs, vn_idxs, local_vns, W)
+    expected, empty = pre if pre is not None else _expected_digests(ctx, sq, reqs, vn_idxs, local_vns, W, parts)
     out = {}
     for vn in local_vns:
         ok_pairs, redo = set(), {}

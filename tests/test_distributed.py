@@ -106,12 +106,21 @@ def test_bench_self_launches_eight_ranks():
     assert [ranks[k]["roles"]["vn"] for k in range(3, 6)] == [["vn0"], ["vn1"], ["vn2"]]
     assert sorted(ranks[6]["roles"]["dp"]) == ["dp0", "dp8"] and sorted(ranks[7]["roles"]["dp"]) == ["dp1", "dp9"]
     assert all(len(ranks[k]["roles"]["dp"]) == 1 for k in range(6))
-    # pooled range checks: every (proof, VN) verification is done once, split in 1/8 slices
+    # pooled range checks: every (proof, VN) verification is done once, split in
+    # 8 slices weighted by each rank's other work (prq.balanced_parts: ranks 6
+    # and 7 prove two DPs, ranks 3-5 host a VN -> shorter slices)
+    from drynx_amd.proofs import requests as prq
+
     n_out = d["config"]["range_proof"]["proofs_per_query"] // d["config"]["dps"]
     items = [ranks[k]["pool_range_items"] for k in range(8)]
     assert sum(items) == d["config"]["range_proof"]["verifications_per_query"]
-    per_list_max = -(-n_out // 8)
-    assert max(items) <= per_list_max * d["config"]["dps"] * d["config"]["vns"]
+    parts = prq.balanced_parts(8, [1, 1, 1, 1, 1, 1, 2, 2], [0, 0, 0, 1, 1, 1, 0, 0])
+
+    class _Sq:
+        RangeProofThreshold = 1.0
+    for k in range(8):
+        lo, hi = prq.sampled_bounds(_Sq, n_out, parts[k])
+        assert items[k] == (hi - lo) * d["config"]["dps"] * d["config"]["vns"], k
     # traffic: every rank took part in the data plane; the VN ranks receive the most
     assert all(ranks[k]["bytes_sent"] > 0 and ranks[k]["bytes_recv"] > 0 for k in range(8))
     assert min(ranks[k]["bytes_recv"] for k in (3, 4, 5)) > max(ranks[k]["bytes_recv"] for k in (0, 1, 2, 6, 7))

@@ -90,3 +90,22 @@ def test_pool_slices_and_digests_world3(equivocate):
     # a helper receives its slices only: far less than the VN's full inbox
     for h in helpers:
         assert outs[h]["recv"] < 0.8 * outs[vn_rank]["recv"], (h, outs[h]["recv"], outs[vn_rank]["recv"])
+
+
+def test_balanced_pool_parts_partition_every_list():
+    """Weighted pool parts (prq.balanced_parts) cut every list into disjoint,
+    covering slices; ranks with more DPs or a VN get shorter ones;
+    DRYNX_POOL_BALANCE=0 gives the equal slices."""
+    from drynx_amd.proofs import requests as prq
+
+    class _Sq:
+        RangeProofThreshold = 1.0
+    dps, vns = [1, 1, 1, 1, 1, 1, 2, 2], [0, 0, 0, 1, 1, 1, 0, 0]
+    parts = prq.balanced_parts(8, dps, vns)
+    for n in (1, 7, 8, 100, 2070, 12345):
+        b = [prq.sampled_bounds(_Sq, n, p) for p in parts]
+        assert b[0][0] == 0 and b[-1][1] == n and all(b[k][1] == b[k + 1][0] for k in range(7))
+    b = [prq.sampled_bounds(_Sq, 2070, p) for p in parts]
+    size = [hi - lo for lo, hi in b]
+    assert size[6] < size[3] < size[0] and abs(size[6] - size[7]) <= 1
+    assert prq.balanced_parts(1, [10], [3]) == [(0, 1)]

@@ -169,6 +169,9 @@ def main():
         place.setdefault((n_cns + i) % W, []).append(v.id)
     dps_of = {k: [dp.id for i, dp in enumerate(cl.dps) if (n_cns + n_vns + i) % W == k] for k in range(W)}
     vn_ranks = {(n_cns + i) % W for i in range(n_vns)}
+    # the framework's weighted pool parts for this placement (prq.balanced_parts)
+    parts = prq.balanced_parts(W, [len(dps_of[k]) for k in range(W)],
+                               [sum(1 for i in range(n_vns) if (n_cns + i) % W == k) for k in range(W)])
 
     def helper_reqs(part):
         out = []
@@ -199,11 +202,11 @@ def main():
 
         timers._events.clear()
         for k in [int(x) for x in os.environ.get("RANK_SHARE_PARTS", "3,6").split(",")]:
-            reqs_k = full_reqs() if k in vn_ranks else helper_reqs((k, W))
+            reqs_k = full_reqs() if k in vn_ranks else helper_reqs(parts[k])
             _sync()
             time.sleep(1.0)  # an idle gap: a kernel trace shows this part as its own burst (tools/kernel_bursts.py)
             with timers.span(f"pool_part[{k}]"):
-                pool_part(reqs_k, {v: list(range(len(rng))) for v in vn_idxs}, sq, dev, cache, (k, W),
+                pool_part(reqs_k, {v: list(range(len(rng))) for v in vn_idxs}, sq, dev, cache, parts[k],
                           {vn.id: Coins() for vn in cl.vns})
             _sync()
         timers.dump_trace(os.environ["DRYNX_TRACE"])
@@ -214,7 +217,7 @@ def main():
            "placement": {k: {"parties": place.get(k, []), "dps": dps_of[k]} for k in range(W)},
            "ranks": {}}
     for k in range(W):
-        part = (k, W)
+        part = parts[k]
         coins = {vn.id: Coins() for vn in cl.vns}
         is_vn = k in vn_ranks
         if is_vn:
@@ -224,7 +227,7 @@ def main():
             def digests_side():
                 ctx = torch.cuda.stream(dst) if dst is not None else contextlib.nullcontext()
                 with ctx:
-                    prq.lists_digests([prq.slice_lists(ls, sq, (j, W)) for ls in full for j in range(W) if j != k])
+                    prq.lists_digests([prq.slice_lists(ls, sq, parts[j]) for ls in full for j in range(W) if j != k])
                 if dst is not None:
                     dst.synchronize()
 
@@ -244,7 +247,7 @@ def main():
                                                               sq, dev, cache, part, coins), a.reps)
         t_dig = 0.0
         if is_vn:  # alone, for reference (the pool time above already runs them alongside)
-            t_dig = timed(lambda: prq.lists_digests([prq.slice_lists(ls, sq, (j, W)) for ls in full
+            t_dig = timed(lambda: prq.lists_digests([prq.slice_lists(ls, sq, parts[j]) for ls in full
                                                      for j in range(W) if j != k]), a.reps)
         mine = {dp: dp_results[dp] for dp in dps_of[k]}
         t_prove = timed(lambda: node._sign_range(sq, node._prove_range(sq, mine)), a.reps) if mine else 0.0
