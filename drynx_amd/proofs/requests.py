@@ -582,15 +582,16 @@ def sampled_bounds(sq, n: int, part=None) -> tuple:
 
 # extra work of a rank, in units of a plain helper's pool share, that its
 # slice is shortened by: every DP it hosts beyond the fewest any rank hosts
-# (proving a 2,070-output DP: ~5.4 ms against a ~38 ms 1/8 part, whose
-# size-dependent half scales with the slice), and every VN it hosts (the
-# full-inbox decode and the digests of the other slices)
-_POOL_DP_W, _POOL_VN_W = 0.32, 0.12
+# (proving a 2,070-output DP: ~5.4 ms against a ~38 ms 1/8 part, of which
+# only a part scales with the slice: one-GPU shares 55.3 -> 50.6 ms with
+# 0.32 / 0.12, profiles/r4/rank_share_w8_balanced*.json), and every VN it
+# hosts (the full-inbox decode and the digests of the other slices)
+_POOL_DP_W, _POOL_VN_W = 0.45, 0.08
 
 
 def balanced_parts(W: int, dps: list, vns: list) -> list:
     """Pool parts for W ranks weighted so every rank's proving + checking
-    ends together: rank k's slice weight 1 - 0.32 (extra DPs) - 0.12 (VNs)
+    ends together: rank k's slice weight 1 - 0.45 (extra DPs) - 0.08 (VNs)
     (floor 0.25), as (k, W, cumulative weights) tuples (``sampled_bounds``).
     Calibrated from one-GPU measurements of each rank's share
     (tools/rank_share.py, profiles/r4/rank_share_*)."""
