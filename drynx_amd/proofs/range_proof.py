@@ -893,7 +893,9 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
     if any(r.offset):
         Cp = nt.g1_add(Cp, nt.g1_fb_mul_i64(tabB, bn.h2d(torch.tensor(r.offset, dtype=torch.int64), device)))
     z = nt.fr_dot_rows(r.zphi, _powers(u, l, device), n, b_periodic=True)   # sum_j Zphi_j u^j
-    ZB = nt.g1_fb_mul(tabB, r.zphi)                                    # [n*l]
+    # Zphi B: the per-item G1 side of the "fold" verifier only (the regrouped
+    # "msm" verifier folds Zphi into its R-MSM scalars)
+    ZB = None if use_msm else nt.g1_fb_mul(tabB, r.zphi)              # [n*l]
     cols_t = bn.h2d(torch.tensor(r.cols, dtype=torch.long), device)
     y_idx = (torch.arange(S, device=device).view(1, S) * sigmat.n_cols + cols_t.view(n, 1)).reshape(-1)
     ytabs = sigmat.y_tables(device)
