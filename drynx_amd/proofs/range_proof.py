@@ -1285,14 +1285,15 @@ def _msm_queue(Y, V, ab_all, G: int, n: int, S: int, L: int, vstream=None, segs:
             Ud = torch.empty((G * nq, 32), dtype=torch.int32, device=dev)
             with timers.span("rp.u.joint"):
                 nt.rp_u_joint(table, ab_all, nq, G, L, Ud, nq)
-            UVd = torch.zeros((G * (nq + 1), 16), dtype=torch.int32, device=dev)
-            nt.rp_msm_uv(Y, UVd, nq, G, nq + 1)
+            # uv(-Y_q) is the same for every VN: computed once, copied per VN below
+            UVd = torch.zeros((nq + 1, 16), dtype=torch.int32, device=dev)
+            nt.rp_msm_uv(Y, UVd, nq, 1, nq + 1)
             qseg = torch.repeat_interleave(torch.arange(nseg, device=dev), _h2d(cq, dev),
                                            output_size=nq)
             qpos = _h2d(segbase, dev)[qseg] + torch.arange(nq, device=dev) - _h2d(qoff[:-1], dev)[qseg]
             pos = (torch.arange(G, device=dev).view(G, 1) * pad + qpos.view(1, nq)).reshape(-1)
             Uall.index_copy_(0, pos, Ud)
-            UV.index_copy_(0, pos, UVd.view(G, nq + 1, 16)[:, :nq].reshape(-1, 16))
+            UV.index_copy_(0, pos, UVd[:nq].repeat(G, 1))
         # G2 membership of every U (exact test), on the validation stream beside the fold
         cur = torch.cuda.current_stream(dev)
         vs = vstream if vstream is not None else cur
