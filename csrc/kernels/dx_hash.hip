@@ -264,6 +264,35 @@ extern "C" int dx_prg_glv(int on_gpu, void *stream, const uint32_t *key_host, ui
   return run(on_gpu, stream, n, op, false, "prg_glv");
 }
 
+// Low-``bits`` batch weights straight from the generator: item i's scalar as
+// dx_random_scalars draws it, with every bit from ``bits`` up cleared (the
+// GT-membership combinations, 64-bit D weights) -- one launch instead of the
+// generator plus masking kernels.
+extern "C" int dx_prg_bits(int on_gpu, void *stream, const uint32_t *key_host, uint32_t counter0, int bits,
+                           uint32_t *out, int64_t n) {
+  if (bits < 0 || bits > 256) return -2;
+  struct K8 {
+    uint32_t k[8];
+  } kk;
+  for (int i = 0; i < 8; i++) kk.k[i] = key_host[i];
+  auto op = [=] __host__ __device__(int64_t i) {
+    uint32_t blk[16];
+    chacha20_block(kk.k, counter0 + (uint32_t)i, blk);
+    Fr lo = reduce_256<FrParams>(blk);
+    Fr hi = reduce_256<FrParams>(blk + 8);
+    Fr x = fadd(lo, to_mont(hi));
+    if (x.is_zero()) x.v[0] = 1;
+    for (int w = 0; w < 8; w++) {
+      const int lo_bit = 32 * w;
+      uint32_t v = x.v[w];
+      if (lo_bit >= bits) v = 0;
+      else if (bits - lo_bit < 32) v &= (1u << (bits - lo_bit)) - 1u;
+      out[8 * i + w] = v;
+    }
+  };
+  return run(on_gpu, stream, n, op, false, "prg_bits");
+}
+
 // out[i] = 8 big-endian words of SHA-256(data[i*chunk, min(len, (i+1)*chunk)))
 extern "C" int dx_sha256_chunks(int on_gpu, void *stream, const uint8_t *data, int64_t len, int64_t chunk,
                                 uint32_t *out) {

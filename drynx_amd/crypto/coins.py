@@ -63,7 +63,7 @@ class Coins:
 
     def bits(self, n: int, device, bits: int = 64, odd: bool = False) -> torch.Tensor:
         """n uniform ``bits``-bit weights as [n, 8] scalars (``odd``: never 0)."""
-        r = mask_bits(self.scalars(n, device), bits)
+        r = nt.prg_bits(self._next_key(), n, bits, device)                 # generator + mask, one launch
         if odd:
             r[:, 0] |= 1
         return r

@@ -83,6 +83,7 @@ _SIGS = {
     "dx_gt_mul": [_I, _P, _P, _P, _P, _L],
     "dx_gt_inv": [_I, _P, _P, _P, _L],
     "dx_prg_glv": [_I, _P, _P, ctypes.c_uint32, _P, _P, _P, _L],
+    "dx_prg_bits": [_I, _P, _P, ctypes.c_uint32, _I, _P, _L],
     "dx_batched_copy": [_I, _P, _P, _P, _I, _L],
     "dx_rows_all": [_I, _P, _P, _P, _I, _L, _P],
     "dx_gt_pow": [_I, _P, _P, _P, _P, _L, _I],
@@ -1289,6 +1290,18 @@ def prg_glv(key: bytes, n: int, device):
     _call("dx_prg_glv", g, s, k.ctypes.data_as(ctypes.c_void_p), 0, lam.ctypes.data_as(ctypes.c_void_p), _ptr(ab),
           _ptr(rho), n)
     return ab, rho
+
+
+def prg_bits(key: bytes, n: int, bits: int, device) -> torch.Tensor:
+    """``coins.mask_bits(prg_scalars(key, n, device), bits)`` in ONE launch."""
+    device = torch.device(device)
+    out = torch.empty((max(0, n), 8), dtype=torch.int32, device=device)
+    if n <= 0:
+        return out
+    k = np.frombuffer(key[:32], dtype="<u4").copy()
+    g, s = _ctx(out)
+    _call("dx_prg_bits", g, s, k.ctypes.data_as(ctypes.c_void_p), 0, int(bits), _ptr(out), n)
+    return out
 
 
 def _lambda_limbs() -> list:

@@ -103,3 +103,16 @@ def test_gpu_slice_hashes_match_hashlib(gpu_device):
     assert D.digest_many(ts) == [D.digest_bytes(h.tobytes()) for h in host]
     rows = torch.from_numpy(rng.integers(0, 2**31, size=(7, 3000), dtype=np.int64).astype(np.int32)).to(gpu_device)
     assert D.digest_rows(rows) == [D.digest_bytes(r.tobytes()) for r in rows.cpu().numpy()]
+
+
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+@pytest.mark.parametrize("bits", [32, 40, 64, 254])
+def test_prg_bits_matches_generator_then_mask(device, bits):
+    if device == "cuda" and not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from drynx_amd.crypto.coins import mask_bits
+
+    key = bytes(range(1, 33))
+    got = nt.prg_bits(key, 777, bits, device).cpu()
+    want = mask_bits(nt.prg_scalars(key, 777, device).cpu(), bits)
+    assert torch.equal(got, want)
