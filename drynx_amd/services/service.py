@@ -427,8 +427,10 @@ class DrynxNode:
             return self._client_pool.submit(fn, partial)
         if not hasattr(self, "_client_stream"):
             # high priority: the querier's decrypt/BSGS kernels are short and
-            # would otherwise queue behind the VNs' MSM passes (75 ms vs 10 ms)
-            self._client_stream = torch.cuda.Stream(self.device, priority=streams.priority(-1))
+            # would otherwise queue behind the VNs' MSM passes (75 ms vs 10 ms);
+            # DRYNX_CLIENT_PRIORITY=0 for A/B runs
+            prio = streams.priority(int(os.environ.get("DRYNX_CLIENT_PRIORITY", "-1")))
+            self._client_stream = torch.cuda.Stream(self.device, priority=prio)
         side = self._client_stream
         side.wait_stream(torch.cuda.current_stream(self.device))  # result tensors are ready on `side`
 
