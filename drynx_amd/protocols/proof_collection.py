@@ -176,7 +176,7 @@ def _helper_slice(lists, sq, part) -> list:
     return prq.slice_lists(lists, sq, part)
 
 
-def pool_verify_ranges(ctx, sq, reqs: list, vns: list, comm=None) -> dict:
+def pool_verify_ranges(ctx, sq, reqs: list, vns: list, comm=None, arrived: float | None = None) -> dict:
     """Pooled range verification (see ``use_pool``).  Each VN's rank decides
     that VN's sampling (reference ``rand.Float64() <= Threshold``, from the
     VN's own coins, or the sharding extension) and draws a per-survey seed;
@@ -185,6 +185,9 @@ def pool_verify_ranges(ctx, sq, reqs: list, vns: list, comm=None) -> dict:
     the digest of each slice it checked.  Each VN's rank then accepts a
     helper's slice verdict only when the digest matches its own digest of
     that slice of the signed payload, and re-checks any other slice itself.
+    ``<vn>_VerifyRange`` (structs_proofs.go:137) runs from ``arrived`` (the
+    VN's inbox: the range fan-out's end on its rank) to that VN's own verdict
+    (after its digest checks and any slice it re-checked).
     -> {vn_id: {base_key: None (not sampled) | bool}} on every rank."""
     comm = comm or ctx.comm
     W, k = comm.world, comm.rank
@@ -202,7 +205,7 @@ def pool_verify_ranges(ctx, sq, reqs: list, vns: list, comm=None) -> dict:
     vn_idxs = {vn.id: [i for i in rng if sampled[vn.id].get(reqs[i].base_key())] for vn in vns}
     part_coins = {vn.id: Coins(seeds[vn.id]).derive(("slice", k, W)) for vn in vns}
     parts = pool_parts(ctx, sq)
-    t0 = time.perf_counter()
+    t0 = arrived if arrived is not None else time.perf_counter()
     local_vns = [vn for vn in vns if vn.rank == ctx.rank]
     # a VN rank's digests of the other ranks' slices of its own payloads run
     # beside this rank's pool part (their own thread and stream: the part's
@@ -328,8 +331,9 @@ def _pool_async(ctx, sq, reqs, vns, comm=None):
 
     if not hasattr(ctx, "_pool_exec"):
         ctx._pool_exec = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="drynx-vn-pool")
+    arrived = time.perf_counter()  # the fan-out just delivered the VNs' inboxes
     if ctx.device.type != "cuda":
-        return ctx._pool_exec.submit(pool_verify_ranges, ctx, sq, reqs, vns, comm)
+        return ctx._pool_exec.submit(pool_verify_ranges, ctx, sq, reqs, vns, comm, arrived)
     if not hasattr(ctx, "_pool_stream"):
         # DRYNX_POOL_RESERVE_CUS=k: the pool's heavy kernels (long-running
         # workgroups) leave k CUs to the short plan / per-CN-proof launches
@@ -342,7 +346,7 @@ def _pool_async(ctx, sq, reqs, vns, comm=None):
 
     def run():
         with torch.cuda.stream(side):
-            out = pool_verify_ranges(ctx, sq, reqs, vns, comm)
+            out = pool_verify_ranges(ctx, sq, reqs, vns, comm, arrived)
         side.synchronize()
         return out
 
@@ -466,6 +470,13 @@ def proof_collection(ctx, sq, local_requests: list, early: dict | None = None, l
     allbm = {}
     for d in ctx.comm.all_gather_object(bitmaps):
         allbm.update(d)
+    if hasattr(ctx, "take_proof_starts"):
+        # the VNs' verdicts are back on every DP's rank: the reference's
+        # <dp>_AllProofs ends here (its proof collection's feedback channel,
+        # data_collection_protocol.go:343-345)
+        now = time.perf_counter()
+        for dp_id, t_start in ctx.take_proof_starts(sq.SurveyID).items():
+            timers.record(f"{dp_id}_AllProofs", now - t_start)
     root = vns[0]
     block = None
     t = timers.start_timer("BI", sync=False)

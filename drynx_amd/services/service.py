@@ -482,18 +482,30 @@ class DrynxNode:
         """Synchronous variant (kept for callers/tests that patch it)."""
         t0 = time.perf_counter()
         reqs = self._sign_range(sq, self._prove_range(sq, dp_results))
-        self._record_all_proofs(reqs, time.perf_counter() - t0)
+        self._record_all_proofs(sq, reqs, t0)
         proofs.extend(reqs)
 
-    @staticmethod
-    def _record_all_proofs(reqs: list, dt: float):
-        """<dp>_AllProofs (data_collection_protocol.go:280): the whole proving
-        of the DP's range proofs, from the start of proving until its signed
-        envelopes exist (device work included: measured after the prover
-        stream has drained).  The DPs of a rank prove as one batch, so they
-        share that span."""
+    def _record_all_proofs(self, sq, reqs: list, t0: float):
+        """``RangeProving``: this rank's proving batch, from the start of
+        proving until the signed envelopes exist (device work included:
+        measured after the prover stream has drained).  Each DP's proving start
+        is kept for its ``<dp>_AllProofs``, which -- as in the reference
+        (data_collection_protocol.go:280-345: the timer ends when the proof
+        collection protocol's feedback channel fires) -- runs until the VNs'
+        verdicts on that DP's proofs are back on the DP's rank
+        (``take_proof_starts``, proof_collection.py)."""
+        timers.record("RangeProving", time.perf_counter() - t0)
+        if not hasattr(self, "_proof_t0"):
+            self._proof_t0 = {}
+        if len(self._proof_t0) > 64:
+            self._proof_t0.clear()
+        starts = self._proof_t0.setdefault(sq.SurveyID, {})
         for r in reqs:
-            timers.record(f"{r.sender_id}_AllProofs", dt)
+            starts.setdefault(r.sender_id, t0)
+
+    def take_proof_starts(self, survey_id) -> dict:
+        """{dp_id: proving start} of the DPs of this rank for a survey (once)."""
+        return getattr(self, "_proof_t0", {}).pop(survey_id, {})
 
     def _prove_range(self, sq, dp_results: dict) -> list:
         """Range proofs of every DP hosted here as ONE prover batch per (u, l)
@@ -555,7 +567,7 @@ class DrynxNode:
 
             def sign_host():
                 reqs = self._sign_range(sq, proved)
-                self._record_all_proofs(reqs, time.perf_counter() - t0)
+                self._record_all_proofs(sq, reqs, t0)
                 return reqs
             return self._pool.submit(sign_host)
         # proving runs on its own HIP stream so the CN phases (aggregation, key
@@ -576,7 +588,7 @@ class DrynxNode:
             with torch.cuda.stream(side):
                 reqs = self._sign_range(sq, proved)  # packing + digest kernels follow the proofs on `side`
             side.synchronize()
-            self._record_all_proofs(reqs, time.perf_counter() - t0)
+            self._record_all_proofs(sq, reqs, t0)
             return reqs
 
         return self._pool.submit(sign)

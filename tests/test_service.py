@@ -315,3 +315,24 @@ def test_malformed_queries_give_bitmap_codes(env):
     sq.Query.Ranges = [[16, 2]]
     with pytest.raises(ValueError, match="signatures"):
         client.send_survey_query(sq)
+
+
+def test_per_party_timers(env):
+    """<dp>_AllProofs spans proving to the VNs' verdicts coming back
+    (data_collection_protocol.go:280-345), so it covers this rank's proving
+    batch (RangeProving) and ends after every VN's own VerifyRange started;
+    every VN of the roster records its own VerifyRange / VerifyKeySwitch."""
+    from drynx_amd.utils import timers
+
+    cl, node, client = env
+    timers.reset()
+    sq = make_survey(client, cl, "sum", query_min=0, query_max=3, rows=6, proofs=1, ranges=[2, 4])
+    client.send_survey_query(sq)
+    rec = timers.summary()
+    assert "RangeProving" in rec
+    for dp in cl.dps:
+        assert rec[f"{dp.id}_AllProofs"]["sum"] >= rec["RangeProving"]["sum"]
+    for vn in cl.vns:
+        assert rec[f"{vn.id}_VerifyRange"]["n"] >= 1
+        assert f"{vn.id}_VerifyKeySwitch" in rec
+    assert not node.take_proof_starts(sq.SurveyID)  # consumed at the feedback point
