@@ -261,8 +261,16 @@ def cosign_many(sb: SkipBlock, signers: list) -> tuple:
     return sigs, links
 
 
+_LINKS: dict = {}  # (prev hash, to hash, partials) -> link: co-hosted VNs each hold a copy of prev
+
+
 def add_forward_link(prev: SkipBlock, to_hash: str, partials: dict):
     """Aggregate the roster's partial signatures into prev's forward link."""
+    memo = (prev.Hash, to_hash, tuple(sorted(partials.items())))
+    if memo in _LINKS:
+        link = {**_LINKS[memo], "Sigs": dict(_LINKS[memo]["Sigs"])}
+        prev.ForwardLinks = [lk for lk in prev.ForwardLinks if lk["To"] != to_hash] + [link]
+        return
     link = {"To": to_hash, "CoSig": "", "Sigs": {}}
     keys = prev.bls_keys()
     if keys is None:
@@ -276,6 +284,9 @@ def add_forward_link(prev: SkipBlock, to_hash: str, partials: dict):
                 parts[i] = O.g1_from_bytes(bytes.fromhex(p))
         agg = bls.aggregate(keys, parts)
         link["CoSig"] = (O.g1_to_bytes(agg).hex() if agg is not None else "") + "/" + bls.mask_to_hex(mask)
+    if len(_LINKS) > 32:
+        _LINKS.clear()
+    _LINKS[memo] = {**link, "Sigs": dict(link["Sigs"])}
     prev.ForwardLinks = [lk for lk in prev.ForwardLinks if lk["To"] != to_hash] + [link]
 
 
