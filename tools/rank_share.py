@@ -118,6 +118,7 @@ def main():
     ap.add_argument("--records", type=int, default=1_000_000)
     ap.add_argument("--serial-json", default=None, help="bench.py --u 0 --l 0 JSON (the non-range critical path)")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--order", default=None, help="comma list: the order the ranks are measured in (default 0..W-1)")
     ap.add_argument("--torch-prof", default=None,
                     help="also profile the 1-GPU pooled check of the whole inbox and the proving of every DP "
                          "(torch.profiler on this thread): the GPU time of torch ops per framework frame")
@@ -216,7 +217,8 @@ def main():
     res = {"world": W, "features": d,
            "placement": {k: {"parties": place.get(k, []), "dps": dps_of[k]} for k in range(W)},
            "ranks": {}}
-    for k in range(W):
+    order = [int(x) for x in a.order.split(",")] if a.order else list(range(W))
+    for k in order:
         part = parts[k]
         coins = {vn.id: Coins() for vn in cl.vns}
         is_vn = k in vn_ranks
