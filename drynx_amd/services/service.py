@@ -297,6 +297,9 @@ class DrynxNode:
                     self.fault_plan.apply(rreqs, lambda pid: self.cluster.by_id(pid).keypair.secret)
                 early = pcp.start_range_plane(self, sq, rreqs)
             range_future = None
+        # range proofs on the GPU during this query's CN phases and querier (``_side_stream``)
+        self._range_active = bool(early is not None or range_future is not None) and \
+            any(u and ll for u, ll in (tuple(r[:2]) for r in (q.Ranges or [])))
         n_rows = n_groups * n_out
         net = self.net
         cn_ids = [si.id for si in sq.RosterServers.list]
@@ -375,6 +378,24 @@ class DrynxNode:
                       [(cn, si.id, size) for cn, dps in (sq.ServerToDP or {}).items() for si in (dps or [])],
                       hops=flow_hops("query_dissemination", len(cns)))
 
+    def _side_stream(self, attr: str, env: str, bulk: int, alone: int):
+        """The worker stream of the querier or of the CN-proof finishing, at the
+        priority that pays for the query at hand.  With range proofs on the GPU
+        (``self._range_active``: the range plane's long-running prover and
+        verifier workgroups) the querier's short decrypt/BSGS chain is the
+        step's tail and gets the high priority (75 ms vs 10 ms behind the VNs'
+        MSM passes) while the CN proofs stay normal; without them the CN
+        proofs' signing gates the VNs' checks and the querier only runs beside
+        them, so the priorities swap (same-box A/B, profiles/r4/prio_ab.txt:
+        headline 186.2 vs 192.8 ms, --u 0 --l 0 30.8-33.0 vs 28.8 ms).
+        ``env`` (DRYNX_CLIENT_PRIORITY / DRYNX_CNP_PRIORITY) pins one."""
+        pin = os.environ.get(env)
+        p = int(pin) if pin is not None else (bulk if getattr(self, "_range_active", False) else alone)
+        cache = self.__dict__.setdefault(attr, {})
+        if p not in cache:
+            cache[p] = torch.cuda.Stream(self.device, priority=streams.priority(p))
+        return cache[p]
+
     def defer_proofs(self, fn, *args):
         """Run ``fn(*args) -> [ProofRequest]`` (proof finishing: transcript
         digests, responses, packing, envelope signatures -- each needs one
@@ -390,12 +411,7 @@ class DrynxNode:
             return fut
         if not hasattr(self, "_cnp_pool"):
             self._cnp_pool = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="drynx-cn-proofs")
-            # normal priority (DRYNX_CNP_PRIORITY=-1: high): the same-box A/B
-            # (profiles/r4/ab_bisect.txt) measured the high-priority stream no
-            # faster -- its kernels then delay the querier's decryption instead
-            prio = streams.priority(int(os.environ.get("DRYNX_CNP_PRIORITY", "0")))
-            self._cnp_stream = torch.cuda.Stream(self.device, priority=prio)
-        side = self._cnp_stream
+        side = self._side_stream("_cnp_streams", "DRYNX_CNP_PRIORITY", bulk=0, alone=-1)
         side.wait_stream(torch.cuda.current_stream(self.device))
 
         def run():
@@ -425,13 +441,7 @@ class DrynxNode:
             self._client_pool = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="drynx-querier")
         if self.device.type != "cuda":
             return self._client_pool.submit(fn, partial)
-        if not hasattr(self, "_client_stream"):
-            # high priority: the querier's decrypt/BSGS kernels are short and
-            # would otherwise queue behind the VNs' MSM passes (75 ms vs 10 ms);
-            # DRYNX_CLIENT_PRIORITY=0 for A/B runs
-            prio = streams.priority(int(os.environ.get("DRYNX_CLIENT_PRIORITY", "-1")))
-            self._client_stream = torch.cuda.Stream(self.device, priority=prio)
-        side = self._client_stream
+        side = self._side_stream("_client_streams", "DRYNX_CLIENT_PRIORITY", bulk=-1, alone=0)
         side.wait_stream(torch.cuda.current_stream(self.device))  # result tensors are ready on `side`
 
         def run():
