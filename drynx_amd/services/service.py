@@ -332,7 +332,12 @@ class DrynxNode:
             n_out = per
         timers.end_timer(t_exec)
         client_future = None
-        if on_result is not None and result is not None:
+        # the querier decodes beside the VNs' checks; it starts once the CN
+        # proofs the VNs check first are signed (DRYNX_CLIENT_EARLY=1: at once):
+        # its decryption kernels otherwise hold the CUs the signing's short
+        # launches wait for, on the step's critical path
+        client_early = os.environ.get("DRYNX_CLIENT_EARLY", "0") == "1"
+        if on_result is not None and result is not None and client_early:
             client_future = self._submit_client(on_result, SurveyResult(sq.SurveyID, result, n_groups, n_out))
         # the last CN phase's proofs (key switching) are still being finished:
         # the VNs check every other proof first (pcp.proof_collection ``late``)
@@ -340,6 +345,8 @@ class DrynxNode:
                   and os.environ.get("DRYNX_PROOF_STAGES", "2") == "2" else None)
         with timers.span("cn.proofs.wait"):
             proofs = self._resolve_proofs(proofs)
+        if on_result is not None and result is not None and not client_early:
+            client_future = self._submit_client(on_result, SurveyResult(sq.SurveyID, result, n_groups, n_out))
         if range_future is not None:
             proofs.extend(range_future.result())
             if hasattr(self, "_prove_stream"):
