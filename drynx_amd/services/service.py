@@ -419,12 +419,22 @@ class DrynxNode:
         if not hasattr(self, "_cnp_pool"):
             self._cnp_pool = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="drynx-cn-proofs")
         side = self._side_stream("_cnp_streams", "DRYNX_CNP_PRIORITY", bulk=0, alone=-1)
-        side.wait_stream(torch.cuda.current_stream(self.device))
+        # the job's inputs are the work queued so far: an event recorded now and
+        # waited for when the job STARTS on the worker -- a wait_stream issued
+        # here would land on ``side`` while the previous job is still queueing
+        # its kernels, putting them behind this caller's later launches (the
+        # aggregation proofs' signing waited ~4 ms behind the key-switch proof
+        # kernels that way)
+        ready = torch.cuda.Event()
+        ready.record(torch.cuda.current_stream(self.device))
 
         def run():
+            side.wait_event(ready)
             with torch.cuda.stream(side):
                 out = fn(*args)
-            side.synchronize()  # packed payloads are complete before anyone reads them
+            done = torch.cuda.Event()
+            done.record(side)
+            done.synchronize()  # this job's packed payloads are complete before anyone reads them
             return out
 
         return self._cnp_pool.submit(run)
