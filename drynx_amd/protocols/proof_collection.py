@@ -413,8 +413,13 @@ def start_range_plane(ctx, sq, range_requests: list) -> dict:
 
 def early_plane_ok(ctx, sq) -> bool:
     """The range plane starts before the CN phases when verification is pooled
-    (single operator) and the survey has VNs and proofs."""
-    return bool(sq.Query.Proofs) and sq.Query.RosterVNs is not None and len(sq.Query.RosterVNs.list) > 0 \
+    (single operator), the survey has VNs and proofs, and there are range
+    proofs to verify: with ranges (0, 0) the DPs ship commitments only, and
+    starting the plane early would just put their signing and fan-out on the
+    CN phases' thread instead of beside them."""
+    q = sq.Query
+    return bool(q.Proofs) and q.RosterVNs is not None and len(q.RosterVNs.list) > 0 \
+        and any(r[0] and r[1] for r in (q.Ranges or [])) \
         and use_pool(ctx) and os.environ.get("DRYNX_RANGE_PLANE", "1") != "0"
 
 
