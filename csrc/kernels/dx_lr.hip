@@ -18,7 +18,8 @@
 // no extra pass over HBM (it used to be a separate rocBLAS gemv that ran on a
 // single workgroup).  Waves stride over records (grid-stride), the 4 waves of
 // a block reduce through LDS and each block writes one 48x48 partial; a tiny
-// second pass (torch.sum on the [blocks,48,48] slab) finishes deterministically.
+// second pass (dx_lr_reduce: fixed summation order over the [blocks,48,48]
+// slab, batched over the DPs of a rank) finishes deterministically.
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <cstdio>
@@ -137,6 +138,45 @@ extern "C" int dx_lr_moments(void *stream, const double *X, const double *w, int
                              int n_blocks) {
   LrArgs a{X, D, N, D, 0, nullptr, nullptr, w, nullptr, 0.0, 0.0, 0};
   return launch(stream, a, partial, n_blocks);
+}
+
+// Block partials -> totals, for many encoder launches at once: out[i][e] =
+// sum_b partial[i][b][e] in a fixed order (four interleaved accumulators over
+// b, then combined), so a DP's coefficients are the same bits whether its
+// partials are reduced alone or with the other DPs of its rank.  One thread
+// per (item, element): consecutive threads read consecutive elements.
+namespace {
+__global__ void __launch_bounds__(256) lr_reduce_kernel(const double *__restrict__ partial, int64_t nb, int64_t n_el,
+                                                        int64_t n_items, double *__restrict__ out) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n_items * n_el) return;
+  const int64_t i = t / n_el, e = t % n_el;
+  const double *p = partial + i * nb * n_el + e;
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+  int64_t b = 0;
+  for (; b + 4 <= nb; b += 4) {
+    s0 += p[(b + 0) * n_el];
+    s1 += p[(b + 1) * n_el];
+    s2 += p[(b + 2) * n_el];
+    s3 += p[(b + 3) * n_el];
+  }
+  for (; b < nb; b++) s0 += p[b * n_el];
+  out[t] = (s0 + s1) + (s2 + s3);
+}
+}  // namespace
+
+extern "C" int dx_lr_reduce(void *stream, const double *partial, int64_t nb, int64_t n_el, int64_t n_items,
+                            double *out) {
+  const int64_t n = n_items * n_el;
+  if (n <= 0 || nb <= 0) return -2;
+  hipLaunchKernelGGL(lr_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, partial,
+                     nb, n_el, n_items, out);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    fprintf(stderr, "[drynx_amd native] lr_reduce: %s\n", hipGetErrorString(e));
+    return -1;
+  }
+  return 0;
 }
 
 // Fused DP encoder: standardise + augment + level-1 (row D) + level-2 ((wa*y + wb) weights).

@@ -163,6 +163,24 @@ def round_precision(v: torch.Tensor, precision: float) -> torch.Tensor:
     return (torch.sign(x) * torch.floor(torch.abs(x) + 0.5)).to(torch.int64)
 
 
+def encode_coefficients_int_many(Xs: list, ys: list, params: LogisticRegressionParameters):
+    """``encode_coefficients_int`` of several DPs' records as one fused batch
+    (one encoder launch per DP, one reduction, one rounding pass: the same
+    values as DP by DP) -> [n_dp, n_coeffs] int64, or None when the batch
+    does not fit the fused GPU encoder (the caller then encodes per DP)."""
+    if not Xs or params.K > 2 or not (params.Means and params.StandardDeviations):
+        return None
+    d = Xs[0].shape[1] if Xs[0] is not None and Xs[0].dim() == 2 else -1
+    if d < 1 or d + 1 >= 48 or any(X is None or not X.is_cuda or X.dim() != 2 or X.shape[1] != d or len(X) == 0
+                                   for X in Xs):
+        return None
+    tot = nt.lr_encode_many([X.to(torch.float64).contiguous() for X in Xs], ys, params.Means,
+                            params.StandardDeviations, 0.0, -1.0)
+    D = d + 1
+    lv = tot[:, D, :D] if params.K == 1 else torch.cat([tot[:, D, :D], tot[:, :D, :D].reshape(len(Xs), -1)], 1)
+    return round_precision(lv, params.PrecisionApproxCoefficients)
+
+
 def encode_coefficients_int(X: torch.Tensor, y: torch.Tensor, params: LogisticRegressionParameters) -> torch.Tensor:
     """The packed int64 vector the DP encrypts (before encryption)."""
     X = X.to(torch.float64)

@@ -100,6 +100,7 @@ _SIGS = {
     "dx_sha256_chunks": [_I, _P, _P, _L, _L, _P],
     "dx_hash_to_g1": [_I, _P, _P, _P, _L, _P, _L],
     "dx_lr_encode": [_P, _P, _L, _L, _I, _P, _P, _P, ctypes.c_double, ctypes.c_double, _P, _I],
+    "dx_lr_reduce": [_P, _P, _L, _L, _L, _P],
     "dx_g1_mul_fast": [_P, _P, _P, _P, _L, _I, _I],
     "dx_rp_verify_fold": [_P, _P, _P, _P, _P, _P, _L, _I, _I],
     "dx_gt_slice_prod": [_I, _P, _P, _P, _P, _P, _P, _L],
@@ -1097,25 +1098,50 @@ def lr_encode(X: torch.Tensor, y: torch.Tensor, mean: torch.Tensor, sd: torch.Te
     """Fused DP encoder on the fp64-MFMA kernel (GPU tensors only): with
     xa_i = [1, (X_i - mean)/sd], returns (sum_i (2y_i-1) xa_i  [D],
     sum_i (wa*y_i + wb) xa_i xa_i^T  [D, D]), D = X.shape[1] + 1 <= 47."""
-    assert X.is_cuda and X.dtype == torch.float64 and X.dim() == 2 and X.stride(1) == 1
-    N, dx = X.shape
-    D = dx + 1
-    if D >= 48:
-        raise ValueError(f"lr_encode supports at most 46 features (got {dx})")
-    y = y.to(device=X.device, dtype=torch.float64).contiguous()
-    mean = mean.to(device=X.device, dtype=torch.float64).contiguous()
-    sd = sd.to(device=X.device, dtype=torch.float64).contiguous()
-    assert y.numel() == N and mean.numel() == dx and sd.numel() == dx
-    steps = (N + 3) // 4
-    n_blocks = int(max(1, min(1024, (steps + 15) // 16)))
-    partial = torch.empty((n_blocks, 48, 48), dtype=torch.float64, device=X.device)
-    _, s = _ctx(X)
-    rc = _raw_call("dx_lr_encode", s, _ptr(X), X.stride(0), N, dx, _ptr(mean), _ptr(sd), _ptr(y), float(wa), float(wb),
-                              _ptr(partial), n_blocks)
-    if rc != 0:
-        raise RuntimeError(f"dx_lr_encode failed rc={rc}")
-    tot = partial.sum(0)
+    tot = lr_encode_many([X], [y], mean, sd, wa, wb)[0]
+    D = X.shape[1] + 1
     return tot[D, :D], tot[:D, :D]
+
+
+def _lr_blocks(N: int) -> int:
+    steps = (N + 3) // 4
+    return int(max(1, min(1024, (steps + 15) // 16)))
+
+
+def lr_encode_many(Xs: list, ys: list, mean, sd, wa: float, wb: float) -> torch.Tensor:
+    """``lr_encode`` of several DPs' records with the same standardisation:
+    one encoder launch per DP into one partial slab, then ONE reduction
+    launch (dx_lr_reduce, fixed summation order: a DP's totals are the same
+    bits alone or batched) -> [n, 48, 48] totals (level 1 in row D)."""
+    X0 = Xs[0]
+    dev = X0.device
+    dx = X0.shape[1]
+    if dx + 1 >= 48:
+        raise ValueError(f"lr_encode supports at most 46 features (got {dx})")
+    mean = torch.as_tensor(mean, dtype=torch.float64).to(dev).contiguous()
+    sd = torch.as_tensor(sd, dtype=torch.float64).to(dev).contiguous()
+    assert mean.numel() == dx and sd.numel() == dx
+    nbs = [_lr_blocks(X.shape[0]) for X in Xs]
+    nb = max(nbs)
+    alloc = torch.empty if all(b == nb for b in nbs) else torch.zeros  # unused blocks must add nothing
+    partial = alloc((len(Xs), nb, 48, 48), dtype=torch.float64, device=dev)
+    _, s = _ctx(X0)
+    keep = []
+    for i, (X, y) in enumerate(zip(Xs, ys)):
+        assert X.is_cuda and X.dtype == torch.float64 and X.dim() == 2 and X.stride(1) == 1 and X.shape[1] == dx
+        N = X.shape[0]
+        y = y.to(device=dev, dtype=torch.float64).contiguous()
+        assert y.numel() == N
+        keep.append(y)
+        rc = _raw_call("dx_lr_encode", s, _ptr(X), X.stride(0), N, dx, _ptr(mean), _ptr(sd), _ptr(y), float(wa),
+                       float(wb), _ptr(partial[i]), nbs[i])
+        if rc != 0:
+            raise RuntimeError(f"dx_lr_encode failed rc={rc}")
+    out = torch.empty((len(Xs), 48, 48), dtype=torch.float64, device=dev)
+    rc = _raw_call("dx_lr_reduce", s, _ptr(partial), nb, 48 * 48, len(Xs), _ptr(out))
+    if rc != 0:
+        raise RuntimeError(f"dx_lr_reduce failed rc={rc}")
+    return out
 
 
 # ----------------------------------------------------------------------------- range proofs (K15/K16)

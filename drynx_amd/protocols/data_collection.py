@@ -152,16 +152,27 @@ def dp_encode_batch(ctx, sq, dps: list) -> dict:
 def _lr_values(ctx, sq, dps: list, device) -> torch.Tensor:
     """[n_dp, n_out] int64 coefficient vectors of every DP's logistic-regression
     data (the fused fp64-MFMA encoder per DP, no host round trip in between)."""
-    from ..models.logistic_regression import encode_coefficients_int, n_coeffs
+    from ..models.logistic_regression import encode_coefficients_int, encode_coefficients_int_many, n_coeffs
 
     op = sq.Query.Operation
     params = op.LRParameters
-    out = []
+    data = []
     for dp in dps:
         if ctx.dp_data and dp.id in ctx.dp_data:
             X, y = ctx.dp_data[dp.id]
         else:
             X, y = generate_lr_data(params, device, torch.Generator().manual_seed(_seed(sq.SurveyID, dp.id)))
+        data.append((X, y))
+    if device.type == "cuda":
+        # every DP of the rank through the fused encoder at once: one reduction and
+        # one rounding pass instead of ~20 launches per DP on the critical path
+        Xs = [torch.as_tensor(X, device=device) if X is not None else None for X, _ in data]
+        ys = [torch.as_tensor(y, device=device) if y is not None else None for _, y in data]
+        many = encode_coefficients_int_many(Xs, ys, params)
+        if many is not None:
+            return many
+    out = []
+    for X, y in data:
         if X is None or len(X) == 0:
             out.append(torch.zeros(n_coeffs(params.NbrFeatures, params.K), dtype=torch.int64, device=device))
         else:

@@ -110,6 +110,36 @@ def test_lr_encode_fused_matches_torch(gpu_device):
         assert torch.allclose(g2, ref2, rtol=1e-10, atol=1e-8), (g2 - ref2).abs().max()
 
 
+def test_lr_encode_many_matches_single(gpu_device):
+    """Several DPs through one encoder batch (one reduction launch) == each DP
+    alone, bit for bit, and == the plain torch fp64 reference; the rounded
+    coefficient vectors of the batch == encode_coefficients_int per DP."""
+    from drynx_amd.models import logistic_regression as lr
+    from drynx_amd.query import LogisticRegressionParameters
+
+    d = 44
+    Xs = [torch.rand(n, d, dtype=torch.float64, device=gpu_device) * 4 for n in (3000, 3000, 517, 80001)]
+    ys = [torch.randint(0, 2, (X.shape[0],), device=gpu_device) for X in Xs]
+    m, s = [2.0] * d, [1.15] * d
+    tot = nt.lr_encode_many(Xs, ys, m, s, 0.0, -1.0)
+    D = d + 1
+    mt = torch.tensor(m, dtype=torch.float64, device=gpu_device)
+    st = torch.tensor(s, dtype=torch.float64, device=gpu_device)
+    for i, (X, y) in enumerate(zip(Xs, ys)):
+        g1, g2 = nt.lr_encode(X, y, mt, st, 0.0, -1.0)
+        assert torch.equal(tot[i, D, :D], g1) and torch.equal(tot[i, :D, :D], g2)
+        Xa = lr.augment((X - mt) / st)
+        ref1 = Xa.T @ (2 * y.to(torch.float64) - 1)
+        assert torch.allclose(g1, ref1, rtol=1e-10, atol=1e-8), (g1 - ref1).abs().max()
+        assert torch.allclose(g2, -(Xa.T @ Xa), rtol=1e-10, atol=1e-8)
+    lp = LogisticRegressionParameters(NbrRecords=1, NbrFeatures=d, Means=m, StandardDeviations=s, Lambda=1.0,
+                                      Step=0.1, MaxIterations=5, InitialWeights=[0.1] * D, K=2,
+                                      PrecisionApproxCoefficients=100.0)
+    many = lr.encode_coefficients_int_many(Xs, ys, lp)
+    for i, (X, y) in enumerate(zip(Xs, ys)):
+        assert torch.equal(many[i], lr.encode_coefficients_int(X, y, lp))
+
+
 @pytest.mark.parametrize("rpv", ["msm", "fold"])
 def test_range_proofs_gpu(gpu_device, rpv, monkeypatch):
     monkeypatch.setenv("DRYNX_RPV", rpv)
