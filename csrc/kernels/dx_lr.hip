@@ -141,8 +141,8 @@ extern "C" int dx_lr_moments(void *stream, const double *X, const double *w, int
 }
 
 // Block partials -> totals, for many encoder launches at once: out[i][e] =
-// sum_b partial[i][b][e] in a fixed order (four interleaved accumulators over
-// b, then combined), so a DP's coefficients are the same bits whether its
+// sum_b partial[i][b][e] in a fixed order (block b into accumulator b % 4,
+// then combined), so a DP's coefficients are the same bits whether its
 // partials are reduced alone or with the other DPs of its rank.  One thread
 // per (item, element): consecutive threads read consecutive elements.
 namespace {
@@ -160,7 +160,11 @@ __global__ void __launch_bounds__(256) lr_reduce_kernel(const double *__restrict
     s2 += p[(b + 2) * n_el];
     s3 += p[(b + 3) * n_el];
   }
-  for (; b < nb; b++) s0 += p[b * n_el];
+  // block b always lands in accumulator b % 4: trailing all-zero blocks (a
+  // shorter DP in a batch padded to the longest) leave the sums unchanged
+  if (b < nb) s0 += p[b * n_el];
+  if (b + 1 < nb) s1 += p[(b + 1) * n_el];
+  if (b + 2 < nb) s2 += p[(b + 2) * n_el];
   out[t] = (s0 + s1) + (s2 + s3);
 }
 }  // namespace
