@@ -1031,6 +1031,9 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
                 hR = hR_f()
             dplan = dplan_f() if callable(dplan_f) else dplan_f
             mplan = mplan_f() if callable(mplan_f) else mplan_f
+        rs = _run_stream(device) if aux is not None and os.environ.get("DRYNX_RUN_SPLIT", "0") == "1" else None
+        if rs is not None:
+            rs.wait_stream(aux)  # the plans (and everything they read) are queued; the ME pass is not yet
         with timers.span("rp.frob8"):  # (A, frob^8 A) stacked: the Frobenius image written in place
             A2 = torch.empty((2 * m, 96), dtype=torch.int32, device=device)
             nt.batched_copy([(r.A.contiguous(), A2[:m])])
@@ -1041,10 +1044,11 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
             else:
                 mexp = nt.multi_exp_grouped(A2, k, mgrp, 2 * G, W=wc_[0], c=wc_[1], plan=mplan,
                                             item_split=(2 * G * m, m))
+        split = torch.cuda.stream(rs) if rs is not None else _nullctx()
         if use_msm and aux is not None:
-            with timers.span("rp.run.R"):
+            with timers.span("rp.run.R"), split:
                 S_R = nt.g2_msm_run(r.V, hR)                           # R window sums
-        with timers.span("rp.run.D"):
+        with timers.span("rp.run.D"), (torch.cuda.stream(rs) if rs is not None else _nullctx()):
             if ddirect:
                 if cC is None:                                                 # host path
                     cC = nt.g1_mul(Cp.contiguous(), r.challenge.contiguous())
@@ -1062,6 +1066,8 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
     if device.type == "cuda":
         with timers.span("rp.verify.multiexp"):
             run_idle_tasks()  # host work queued by the caller, in the GPU's busiest window
+            if rs is not None:
+                aux.wait_stream(rs)
             aux.synchronize()                                          # aux results are read on this stream/host
             GG = nt.multi_exp_grouped_finish(mexp)                     # [2G, 96]: prod a^rho_v, prod a^gamma_v
             D_all = dcheck.cpu() if ddirect else nt.g1_msm_finish(dcheck)  # [2G, 24]
@@ -1683,6 +1689,16 @@ def _aux_stream(device):
     key = str(device)
     if key not in _aux:
         # plans: short kernels overtake the pairing side
+        _aux[key] = torch.cuda.Stream(device, priority=streams.priority(-1))
+    return _aux[key]
+
+
+def _run_stream(device):
+    """Second pass stream (DRYNX_RUN_SPLIT=1): the R-MSM and D-check passes
+    beside the GT multi-exponentiation instead of behind it -- a pool part's
+    1/8 slice leaves each of them too few workgroups to fill the chip."""
+    key = ("run", str(device))
+    if key not in _aux:
         _aux[key] = torch.cuda.Stream(device, priority=streams.priority(-1))
     return _aux[key]
 
