@@ -213,31 +213,64 @@ class DistComm(Comm):
         return t.to(self.device)
 
 
+_CTRL_FIX = 8192  # bytes per rank in a control message's first (usually only) round
+
+
+def _frame(b: bytes) -> torch.Tensor:
+    """[8-byte length | first _CTRL_FIX - 8 bytes of the message], zero padded."""
+    t = torch.zeros(_CTRL_FIX, dtype=torch.uint8)
+    t[:8] = torch.frombuffer(bytearray(len(b).to_bytes(8, "little")), dtype=torch.uint8)
+    head = b[: _CTRL_FIX - 8]
+    if head:
+        t[8: 8 + len(head)] = torch.frombuffer(bytearray(head), dtype=torch.uint8)
+    return t
+
+
+def _unframe(t: torch.Tensor) -> tuple:
+    raw = t.numpy().tobytes()
+    n = int.from_bytes(raw[:8], "little")
+    return n, raw[8: 8 + min(n, _CTRL_FIX - 8)]
+
+
 def _bcast_obj(rank: int, obj, src: int, group):
-    """Control message from ``src`` to every rank (msgpack, no pickle)."""
+    """Control message from ``src`` to every rank (msgpack, no pickle): ONE
+    fixed-size broadcast carrying the length and the first bytes (a second
+    one only for the tail of a message over ~8 KB) -- each control collective
+    is a latency-bound round over the host TCP plane."""
     timers.count("comm.ctrl_collectives")
-    if rank == src:
-        b = obj_to_bytes(obj)
-        n = torch.tensor([len(b)], dtype=torch.int64)
-    else:
-        n = torch.zeros(1, dtype=torch.int64)
-    dist.broadcast(n, src, group=group)
-    buf = torch.frombuffer(bytearray(b), dtype=torch.uint8) if rank == src else torch.empty(int(n), dtype=torch.uint8)
-    dist.broadcast(buf, src, group=group)
-    return obj if rank == src else bytes_to_obj(buf.numpy().tobytes())
+    b = obj_to_bytes(obj) if rank == src else b""
+    t = _frame(b) if rank == src else torch.zeros(_CTRL_FIX, dtype=torch.uint8)
+    dist.broadcast(t, src, group=group)
+    n, head = _unframe(t)
+    if n > _CTRL_FIX - 8:
+        rest = n - (_CTRL_FIX - 8)
+        tail = torch.frombuffer(bytearray(b[_CTRL_FIX - 8:]), dtype=torch.uint8) if rank == src \
+            else torch.empty(rest, dtype=torch.uint8)
+        dist.broadcast(tail, src, group=group)
+        head = head + tail.numpy().tobytes()
+    return obj if rank == src else bytes_to_obj(head)
 
 
 def _gather_obj(rank: int, world: int, obj, group) -> list:
+    """All-gather of control objects: one fixed-size round (lengths + first
+    bytes of every rank's message), a second only when some message is
+    longer than it (every rank sees every length, so all agree)."""
     timers.count("comm.ctrl_collectives")
     b = obj_to_bytes(obj)
-    sizes = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
-    dist.all_gather(sizes, torch.tensor([len(b)], dtype=torch.int64), group=group)
-    m = max(int(x) for x in sizes)
-    mine = torch.zeros(m, dtype=torch.uint8)
-    mine[: len(b)] = torch.frombuffer(bytearray(b), dtype=torch.uint8)
-    bufs = [torch.empty(m, dtype=torch.uint8) for _ in range(world)]
-    dist.all_gather(bufs, mine, group=group)
-    return [obj if r == rank else bytes_to_obj(bufs[r][: int(sizes[r])].numpy().tobytes()) for r in range(world)]
+    frames = [torch.empty(_CTRL_FIX, dtype=torch.uint8) for _ in range(world)]
+    dist.all_gather(frames, _frame(b), group=group)
+    got = [_unframe(f) for f in frames]
+    m = max(n for n, _ in got) - (_CTRL_FIX - 8)
+    if m > 0:
+        mine = torch.zeros(m, dtype=torch.uint8)
+        tail = b[_CTRL_FIX - 8:]
+        if tail:
+            mine[: len(tail)] = torch.frombuffer(bytearray(tail), dtype=torch.uint8)
+        bufs = [torch.empty(m, dtype=torch.uint8) for _ in range(world)]
+        dist.all_gather(bufs, mine, group=group)
+        got = [(n, h + (bufs[r].numpy().tobytes()[: n - (_CTRL_FIX - 8)] if n > _CTRL_FIX - 8 else b""))
+               for r, (n, h) in enumerate(got)]
+    return [obj if r == rank else bytes_to_obj(got[r][1]) for r in range(world)]
 
 
 class _CtrlPlane(Comm):

@@ -86,3 +86,50 @@ def test_exchange_all_to_all_gloo(world):
         tot_s += d["sent"]
         tot_r += d["recv"]
     assert tot_s == tot_r > 0  # every byte sent to a peer is received by it
+
+
+def _ctrl_worker(rank, world, port, outdir):
+    import json
+
+    import torch.distributed as dist
+
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from drynx_amd.parallel import comm as cm
+    from drynx_amd.utils import timers
+
+    comm = cm.DistComm("cpu")
+    errors = []
+    # payload sizes around the one-round frame: empty, small, exactly the frame's
+    # payload, one byte over, and ~40 KB (two rounds); ranks differ in size
+    sizes = [0, 5, cm._CTRL_FIX - 8 - 12, cm._CTRL_FIX - 8, cm._CTRL_FIX - 7, 40_000]
+    for k, n in enumerate(sizes):
+        mine = {"r": rank, "k": k, "blob": bytes((rank + i) % 251 for i in range(n + rank))}
+        got = comm.all_gather_object(mine)
+        for r in range(world):
+            exp = {"r": r, "k": k, "blob": bytes((r + i) % 251 for i in range(n + r))}
+            if got[r] != exp:
+                errors.append(f"gather size {n}: rank {r} differs")
+        src = k % world
+        b = comm.broadcast_object({"src": src, "blob": bytes(i % 7 for i in range(n))} if rank == src else None,
+                                  src=src)
+        if b != {"src": src, "blob": bytes(i % 7 for i in range(n))}:
+            errors.append(f"broadcast size {n} from {src} differs")
+    with open(os.path.join(outdir, f"c{rank}.json"), "w") as f:
+        json.dump({"errors": errors, "ctrl": timers.counters().get("comm.ctrl_collectives", 0)}, f)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_control_objects_one_round_framing(world):
+    """Control objects travel in one fixed-size round (length + first bytes),
+    with a second round only for longer messages; every size on both sides of
+    the frame boundary arrives intact on every rank."""
+    import json
+
+    outdir = tempfile.mkdtemp()
+    mp.spawn(_ctrl_worker, args=(world, _free_port(), outdir), nprocs=world, join=True)
+    for r in range(world):
+        d = json.load(open(os.path.join(outdir, f"c{r}.json")))
+        assert d["errors"] == [], d["errors"]
