@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import copy
 import os
+import sys
 import time
 from dataclasses import dataclass, field
 
@@ -66,6 +67,11 @@ class DrynxNode:
 
     def __init__(self, cluster: Cluster, comm: Comm | None = None, workdir: str = "./drynx_db", device=None,
                  dp_data: dict | None = None):
+        sw = os.environ.get("DRYNX_SWITCH_INTERVAL")
+        if sw:
+            # the node's worker threads (ledger writers, CN-proof finishing, the
+            # pool) hand the GIL back to the query's thread sooner than the 5 ms default
+            sys.setswitchinterval(float(sw))
         self.comm = comm or LocalComm(device or ("cuda" if torch.cuda.is_available() else "cpu"))
         self.rank = self.comm.rank
         self.device = torch.device(device) if device is not None else self.comm.device
