@@ -401,8 +401,9 @@ def prewarm_signatures(reqs: list, sq, vn_ids: list, cache: "VerifierCache"):
     with timers.span("verify.digests"):
         prefetch_digests(reqs)
     keys = [(sq.IDtoPublic.get(r.sender_id), r.digest(), r.signature) for r in reqs]
+    dev = next((r.tensor.device for r in reqs if r.tensor is not None), "cpu")
     with timers.span(f"verify.signature.multi[{len(vn_ids)}]"):
-        ok = sigma.schnorr_verify_batch(keys * len(vn_ids), "cpu")
+        ok = sigma.schnorr_verify_batch(keys * len(vn_ids), dev)  # host below DRYNX_SIG_DEVICE_MIN checks
     n = len(reqs)
     for j, vn_id in enumerate(vn_ids):
         cache.sig_pre[(sq.SurveyID, vn_id)] = (n, ok[j * n:(j + 1) * n])

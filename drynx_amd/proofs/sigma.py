@@ -253,7 +253,8 @@ def schnorr_verify_batch(items: list, device="cpu") -> list:
         return out
     # a VN inbox of a few dozen envelopes verifies on the host pool: a GPU
     # launch chain plus its read-back costs more than the products themselves
-    dev = torch.device(device) if len(idx) >= _SIG_DEVICE_MIN else torch.device("cpu")
+    dev = torch.device(device) if len(idx) >= int(os.environ.get("DRYNX_SIG_DEVICE_MIN", _SIG_DEVICE_MIN)) \
+        else torch.device("cpu")
     with timers.span(f"sig.products[{len(idx)}]"):
         lhs = nt.g1_fb_mul(bn.base_table(dev), _sc(s, dev))
         rhs = nt.g1_add(bn.g1_jac_tensor(R, dev), nt.g1_mul(bn.g1_jac_tensor(X, dev), _sc(e, dev)))
