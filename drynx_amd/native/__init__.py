@@ -1087,8 +1087,7 @@ def lr_moments(X: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     n_blocks = int(max(1, min(2048, (steps + 15) // 16)))
     partial = torch.empty((n_blocks, 48, 48), dtype=torch.float64, device=X.device)
     _, s = _ctx(X)
-    lib_ = _load()
-    rc = lib_.dx_lr_moments(s, _ptr(X), _ptr(w.to(torch.float64).contiguous()), N, D, _ptr(partial), n_blocks)
+    rc = _raw_call("dx_lr_moments", s, _ptr(X), _ptr(w.to(torch.float64).contiguous()), N, D, _ptr(partial), n_blocks)
     if rc != 0:
         raise RuntimeError(f"dx_lr_moments failed rc={rc}")
     return partial.sum(0)[:D, :D]
