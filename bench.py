@@ -112,6 +112,20 @@ def parse():
     return ap.parse_args()
 
 
+def _forward_args(argv: list) -> list:
+    """The script's arguments for the launcher's command line: its own parser
+    takes abbreviations of ITS options out of them ("--l" would read as
+    --log-dir...), so the short aliases travel as their long forms."""
+    alias = {"--u": "--base", "--l": "--digits"}
+    out = []
+    for a in argv:
+        if a.startswith("--"):
+            name, eq, val = a.partition("=")
+            a = alias.get(name, name) + eq + val
+        out.append(a)
+    return out
+
+
 def _launch_ranks(args) -> int | None:
     """``--gpus N`` (N > 1) run directly, not under a launcher: start N ranks
     through torch.distributed.run as a CHILD process (this process has made
@@ -125,13 +139,9 @@ def _launch_ranks(args) -> int | None:
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
-    # the launcher's own parser takes abbreviations of ITS options out of the
-    # script's arguments ("--l" would read as --log-dir...): pass the long aliases
-    alias = {"--u": "--base", "--l": "--digits"}
-    fwd = [alias.get(a.split("=", 1)[0], a.split("=", 1)[0]) + (a[a.index("="):] if "=" in a else "")
-           if a.startswith("--") else a for a in sys.argv[1:]]
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
-           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *fwd]
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__),
+           *_forward_args(sys.argv[1:])]
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS=os.environ.get("OMP_NUM_THREADS", "1"))
     return subprocess.call(cmd, env=env)
 

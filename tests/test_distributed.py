@@ -143,3 +143,21 @@ def test_bench_rejects_world_mismatch():
                        capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode != 0 and "rank(s)" in r.stderr
     assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+
+
+def test_forwarded_args_avoid_launcher_abbreviations():
+    """bench.py's self-launch hands its arguments to torch.distributed.run,
+    whose parser would read "--l" as an abbreviation of its own --log-dir:
+    the short aliases travel in their long forms, values untouched."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    fwd = bench._forward_args(["--gpus", "8", "--u", "4", "--l=2", "--steps", "3", "--features", "12"])
+    assert fwd == ["--gpus", "8", "--base", "4", "--digits=2", "--steps", "3", "--features", "12"]
+    argv = sys.argv
+    try:
+        sys.argv = ["bench.py", *fwd]
+        a = bench.parse()
+    finally:
+        sys.argv = argv
+    assert (a.gpus, a.u, a.l, a.steps, a.features) == (8, 4, 2, 3, 12)

@@ -56,3 +56,19 @@ def test_tampered_payload_is_a_bad_signature(tmp_path):
     assert {v for k, v in codes.items() if "/aggregation/" in k} == {prq.PROOF_FALSE_SIGN}
     assert {v for k, v in codes.items() if "/aggregation/" not in k} == {prq.PROOF_TRUE}
     node.close(remove=True)
+
+
+def test_early_range_plane_only_with_range_proofs(tmp_path, monkeypatch):
+    """The range plane starts before the CN phases only when there are range
+    proofs to verify: with ranges (0, 0) the DPs ship commitments only and
+    their signing / fan-out stays off the CN phases' thread
+    (``early_plane_ok``); the pool itself is used either way."""
+    cl, node, sq = _setup(tmp_path)
+    monkeypatch.setattr(pcp, "use_pool", lambda ctx: True)
+    assert pcp.early_plane_ok(node, sq)
+    client = DrynxClient(node)
+    sq0 = make_survey(client, cl, "mean", query_min=0, query_max=10, rows=4, proofs=1, ranges=[0, 0])
+    assert not pcp.early_plane_ok(node, sq0)
+    monkeypatch.setenv("DRYNX_RANGE_PLANE", "0")
+    assert not pcp.early_plane_ok(node, sq)
+    node.close(remove=True)
