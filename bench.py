@@ -106,6 +106,13 @@ def parse():
     ap.add_argument("--fault-dp", type=int, default=None,
                     help="fault-injected run: DP k's range-proof payload is corrupted after proving and re-signed "
                          "(one false proof among all); the bench then checks that every VN blames exactly that DP")
+    ap.add_argument("--verification-sharding", type=int, default=0,
+                    help="SurveyQuery.VerificationSharding: each proof verified by exactly k VNs (0: every VN)")
+    ap.add_argument("--check-ledger", action="store_true",
+                    help="after the timed steps, read every local VN's stored proofs of the last survey back "
+                         "(GetProofs) and report ledger_readback in the rank records")
+    ap.add_argument("--table-digest", action="store_true",
+                    help="report a SHA-256 of each rank's prover tables (small configs: compares sharded builds)")
     ap.add_argument("--dro", type=int, default=None,
                     help="differential-privacy noise list size (DRO shuffle by every CN, with shuffle proofs); "
                          "--query lr_dro sets 10000 (the reference's DiffPri 10k row)")
@@ -151,16 +158,42 @@ def _check_world(args, comm):
         sys.exit(f"bench: --gpus {args.gpus} but the job has {comm.world} rank(s)")
 
 
-def _rank_record(comm, cl, step_ms, elapsed, setup_s, b0) -> dict:
+def _rank_record(comm, cl, step_ms, elapsed, setup_s, b0, extra: dict | None = None) -> dict:
     """This rank's share of the job: its parties, step times, data-plane
-    traffic over the timed steps and the range items it checked for the VN
-    pool (gathered to rank 0 into the JSON's ``ranks``)."""
+    traffic over the timed steps, the range items it checked for the VN
+    pool and the range payloads it wrote / referenced in the node's ledger
+    (gathered to rank 0 into the JSON's ``ranks``)."""
     roles = {r: [p.id for p in cl.local(comm.rank, r)] for r in ("cn", "vn", "dp")}
+    c = timers.counters()
     return {"rank": comm.rank, "roles": roles, "step_ms": step_ms, "elapsed_ms": round(1000 * elapsed, 1),
             "setup_s": round(setup_s, 3), "bytes_sent": comm.bytes_sent - b0[0], "bytes_recv": comm.bytes_recv - b0[1],
-            "pool_range_items": timers.counters().get("pool.range_items", 0),
-            "ctrl_collectives": timers.counters().get("comm.ctrl_collectives", 0),
-            "data_exchanges": timers.counters().get("comm.data_exchanges", 0)}
+            "pool_range_items": c.get("pool.range_items", 0),
+            "ctrl_collectives": c.get("comm.ctrl_collectives", 0),
+            "data_exchanges": c.get("comm.data_exchanges", 0),
+            "ledger_written": c.get("ledger.written", 0), "ledger_referenced": c.get("ledger.referenced", 0),
+            **(extra or {})}
+
+
+def _ledger_readback(node, cl, rank: int, survey_id: str) -> dict:
+    """GetProofs of every VN hosted here for ``survey_id`` (each stored value
+    read back and exported in the reference layout) -> {vn: n proofs}."""
+    node.flush_stores()
+    return {vn.id: len(node.get_proofs(vn.id, survey_id)) for vn in cl.local(rank, "vn")}
+
+
+def _table_digest(node) -> str:
+    """SHA-256 over this rank's prover tables (every signature set, every layout)."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for sm in node.verifier_cache._sig.values():
+        for key in sorted(sm._ptab, key=str):
+            v = sm._ptab[key]
+            ts = v[:2] if isinstance(v, tuple) else ((v.get("g2"), v.get("gt")) if isinstance(v, dict) else ())
+            for t in ts:
+                if isinstance(t, torch.Tensor):
+                    h.update(t.detach().cpu().contiguous().numpy().tobytes())
+    return h.hexdigest()
 
 
 def main():
@@ -168,6 +201,9 @@ def main():
     rc = _launch_ranks(args)
     if rc is not None:
         sys.exit(rc)
+    from drynx_amd.utils.streams import node_process_setup
+
+    node_process_setup()
     if args.query == "lr_dro" and args.dro is None:
         args.dro = 10_000
     if args.query not in ("lr", "lr_dro"):
@@ -226,7 +262,8 @@ def main():
                            Limit=DRO_LIMIT)
     if rank == 0:  # CN input-validation keys are set up once, before the queries (as in the reference simulation)
         template = make_survey(client, cl, "logistic regression", proofs=1, ranges=[args.u, args.l, offset],
-                               lr_params=lp, thresholds=[1.0, 1.0, 1.0, 0.0, 1.0], verification_sharding=0, diffp=diffp,
+                               lr_params=lp, thresholds=[1.0, 1.0, 1.0, 0.0, 1.0],
+                               verification_sharding=args.verification_sharding, diffp=diffp,
                                sig_device=device, deterministic_sigs=args.deterministic_sigs,
                                range_proof_mode=args.range_mode)
 
@@ -275,10 +312,18 @@ def main():
         torch.cuda.synchronize()
     my_elapsed = time.perf_counter() - t0
     elapsed = max(comm.all_gather_object(my_elapsed))
-    ranks = comm.all_gather_object(_rank_record(comm, cl, step_ms, my_elapsed, my_setup_s, b0))
+    extra = {}
+    if args.check_ledger:
+        extra["ledger_readback"] = _ledger_readback(node, cl, rank, blocks[-1].data_block().SurveyID
+                                                    if blocks and blocks[-1] is not None else "")
+    if args.table_digest:
+        extra["table_digest"] = _table_digest(node)
+    ranks = comm.all_gather_object(_rank_record(comm, cl, step_ms, my_elapsed, my_setup_s, b0, extra))
     n_out = (d + 1) + (d + 1) ** 2
     proofs_per_step = n_dps * n_out
-    verifs_per_step = proofs_per_step * n_vns  # threshold 1.0: every VN checks every proof
+    # threshold 1.0: every VN checks every proof (VerificationSharding k: exactly k VNs per proof)
+    verifs_per_step = proofs_per_step * (min(args.verification_sharding, n_vns) if args.verification_sharding
+                                         else n_vns)
     ms = 1000.0 * elapsed / args.steps
     value = verifs_per_step * args.steps / elapsed
     if args.fault_dp is not None:
@@ -286,6 +331,9 @@ def main():
         bad = f"/range/{cl.dps[args.fault_dp].id}/"
         ok = all(b is not None and all((v == 0) if bad in k else (v == 1) for k, v in b.data_block().Proofs.items())
                  for b in blocks)
+    elif args.verification_sharding:  # the VNs not assigned a proof record "received, not checked" (2)
+        ok = all(b is not None and set(b.data_block().Proofs.values()) <= {1, 2}
+                 and 1 in b.data_block().Proofs.values() for b in blocks)
     else:
         ok = all(b is not None and all(v == 1 for v in b.data_block().Proofs.values()) for b in blocks)
     result_ok = _check_lr_results(comm, checks, lp, diffp)
@@ -328,7 +376,8 @@ def main():
                 "dps": n_dps, "cns": args.cns, "vns": n_vns,
                 "records_per_dp": rec_per_dp,
                 "sigs": "deterministic" if args.deterministic_sigs else "random (per CN, per column)",
-                "verification": "every VN verifies every proof (threshold 1.0)",
+                "verification": (f"each proof verified by {args.verification_sharding} VNs (VerificationSharding)"
+                                 if args.verification_sharding else "every VN verifies every proof (threshold 1.0)"),
                 "range_proof": {"u": args.u, "l": args.l, "servers": args.cns, "proofs_per_query": proofs_per_step,
                                 "verifications_per_query": verifs_per_step},
                 "vn_independent": True,

@@ -38,6 +38,9 @@ def main(argv=None):
             group = toml_io.loads(f.read())
         cfg["Trusted"] = [n["PublicKey"] for n in group.get("Network", {}).get("Nodes", [])]
     cfg["TrustAny"] = bool(a.trust_any)
+    from ..utils.streams import node_process_setup
+
+    node_process_setup()
     srv.NodeServer(cfg, a.workdir, a.device).serve_forever()
     return 0
 

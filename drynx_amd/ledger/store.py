@@ -15,6 +15,16 @@ write instead of B-tree page churn.  Writes can be queued to a background
 writer thread so proof persistence never sits on the verification critical
 path (``flush`` joins them); a queued value may be a device tensor, copied to
 the host by the writer.
+
+Durability: as a bbolt batch is committed before ``UpdateDB`` returns
+(lib/structs.go:571-588), every blob write is fdatasync'ed by the ledger
+worker before its job completes and SQLite runs with ``synchronous=FULL`` (each
+commit syncs the WAL), so ``flush`` returning means the values are on disk.
+Retention: every proof is kept (bbolt never drops one and ``GetProofs`` serves
+all of them, services/service_skipchain.go:240-320); a full disk fails the
+write loudly.  ``DRYNX_LEDGER_RETAIN=budget`` opts into deleting the oldest
+blob generations below a disk reserve; a read of a pruned value then raises
+``PrunedError``.
 """
 from __future__ import annotations
 
@@ -80,6 +90,23 @@ def _gb_env(name: str, default: float) -> float:
     return float(os.environ.get(name, default)) * (1 << 30)
 
 
+def _budget() -> bool:
+    """Pruning below a disk reserve is opt-in (DRYNX_LEDGER_RETAIN=budget)."""
+    return os.environ.get("DRYNX_LEDGER_RETAIN", "all") == "budget"
+
+
+class PrunedError(FileNotFoundError):
+    """A ledger value deleted under DRYNX_LEDGER_RETAIN=budget."""
+
+
+def _fsync_dir(path: str):
+    fd = os.open(path, os.O_RDONLY)
+    try:
+        os.fsync(fd)
+    finally:
+        os.close(fd)
+
+
 class BlobSegment:
     """Append-only files of large ledger values shared by the VNs of one rank:
     the same proof payload is written once, however many co-hosted VNs store
@@ -87,15 +114,14 @@ class BlobSegment:
     (and, on a GPU, its own HIP stream: device-to-host copies never queue on
     the compute streams).
 
-    Disk budget: a query's range proofs are ~0.55 GB per VN rank (three VN
-    ranks on an 8-GPU node write ~1.7 GB per query; a 79 GB box disk fills
-    in ~45 queries).  Values go to generation files of at most
-    DRYNX_LEDGER_SEGMENT_GB (default 4); before a write that would leave less
-    than DRYNX_LEDGER_RESERVE_GB (default 8) free, the oldest generations of
-    this rank are deleted (their proofs are no longer served by ``get_proofs``;
-    bitmaps, blocks and small proofs stay in the database).
-    DRYNX_LEDGER_RETAIN=all keeps everything (and fails when the disk is
-    full), as the reference's bbolt store."""
+    Values go to generation files of at most DRYNX_LEDGER_SEGMENT_GB (default
+    4), each write fdatasync'ed before its job completes.  Everything is kept
+    (a full disk fails the write, as the reference's bbolt store would).
+    Opt-in disk budget (DRYNX_LEDGER_RETAIN=budget): before a write that would
+    leave less than DRYNX_LEDGER_RESERVE_GB (default 8) free, the oldest
+    generations of this rank are deleted (their proofs are no longer served
+    by ``get_proofs``, which raises ``PrunedError``; bitmaps, blocks and small
+    proofs stay in the database)."""
 
     def __init__(self, path: str, device=None):
         import concurrent.futures as cf
@@ -168,6 +194,9 @@ class BlobSegment:
                 # diagnostics: the write volume of several VN ranks, each
                 # persisting its own copy (DRYNX_LEDGER_COPIES, see _copies)
                 self._pwrite_all(bufs, off, f"{self.path}.copy{j}")
+        with timers.span("ledger.sync"):
+            for p in self._files_of(self.path):
+                os.fdatasync(self._pfds[p])
         return out if many else out[0]
 
     _PIECE = 32 << 20  # bytes per parallel write
@@ -187,6 +216,7 @@ class BlobSegment:
         self.path = f"{self.base}.{len(self._gens)}"
         self._gens.append(self.path)
         self._f = open(self.path, "ab")
+        _fsync_dir(os.path.dirname(os.path.abspath(self.path)))
 
     def _make_room(self, need: int):
         import shutil
@@ -194,7 +224,7 @@ class BlobSegment:
         if self._f.seek(0, os.SEEK_END) + need > _gb_env("DRYNX_LEDGER_SEGMENT_GB", 4) and \
                 self._f.tell() > 0:
             self._rotate()
-        if os.environ.get("DRYNX_LEDGER_RETAIN", "") == "all":
+        if not _budget():
             return
         reserve = _gb_env("DRYNX_LEDGER_RESERVE_GB", 8)
         d = os.path.dirname(os.path.abspath(self.path))
@@ -212,7 +242,7 @@ class BlobSegment:
 
                 logging.getLogger("drynx_amd").warning(
                     f"ledger: disk below the {reserve / (1 << 30):.0f} GB reserve, deleting the oldest proof "
-                    f"segments of {self.base} (DRYNX_LEDGER_RETAIN=all keeps them)")
+                    f"segments of {self.base} (DRYNX_LEDGER_RETAIN=budget)")
 
     def _pwrite_all(self, bufs: list, off: int, path: str | None = None):
         """The buffers back to back from ``off``, in pieces written by several
@@ -280,31 +310,50 @@ class _Done:
 class NodeBlobs(BlobSegment):
     """Range payloads shared by the VN ranks of ONE node, content-addressed
     (one file per payload digest under a node directory).  On an 8-GPU node
-    the three VN ranks receive the same signed payloads; only the first one
-    copies them to the host and writes them, the others store references to
-    the same files -- as the VNs co-hosted on a rank already share one
-    BlobSegment.  A payload file appears under its final name only once fully
-    written (write to .tmp, then rename), and a reader that finds it missing
-    waits for it; the disk reserve of BlobSegment applies to the writer's
-    files."""
+    several VN ranks receive the same signed payloads: the first rank to
+    CLAIM a digest (an ``O_CREAT | O_EXCL`` marker file, atomic across the
+    node's processes) copies it to the host and writes it; every other rank
+    holding the same payload stores a reference to that file and skips the
+    device-to-host copy -- as the VNs co-hosted on a rank already share one
+    BlobSegment.  Only a rank that actually holds the payload claims it, so a
+    VN rank that got a header-only envelope (``VerificationSharding``, or
+    per-CN proofs fanned out to the assigned VNs only) never leaves a
+    reference nobody writes.  A payload file appears under its final name
+    only once fully written and fdatasync'ed (write to .tmp, sync, rename,
+    directory sync); a reader that finds it missing waits for it."""
 
-    def __init__(self, root: str, writer: bool, device=None):
+    def __init__(self, root: str, device=None):
         os.makedirs(root, exist_ok=True)
         super().__init__(os.path.join(root, f"_rank_{os.getpid()}.unused"), device)
-        self.root, self.writer = root, writer
-        self._files: list = []  # the writer's payload files, oldest first
+        self.root = root
+        self._files: list = []  # this rank's payload files, oldest first
 
     def file_of(self, blob_id: str) -> str:
         return os.path.join(self.root, f"{blob_id}.blob")
 
-    def put_many(self, blob_ids: list, produce_all, sizes: list | None = None) -> list:
-        if not self.writer:
-            refs = []
-            with self._lock:
-                for bid, n in zip(blob_ids, sizes):
-                    fut = self._done.setdefault(bid, _Done((0, int(n), self.file_of(bid))))
-                    refs.append(BlobRef(self, fut))
-            return refs
+    def claim(self, blob_ids: list) -> list:
+        """[bool]: True where THIS rank writes the payload (first claimant on
+        the node), False where another rank of the node already claimed it."""
+        out = []
+        for bid in blob_ids:
+            try:
+                os.close(os.open(self.file_of(bid) + ".claim", os.O_CREAT | os.O_EXCL | os.O_WRONLY, 0o644))
+                out.append(True)
+            except FileExistsError:
+                out.append(False)
+        return out
+
+    def put_refs(self, blob_ids: list, sizes: list) -> list:
+        """References to payloads another rank of the node claimed and writes."""
+        refs = []
+        with self._lock:
+            for bid, n in zip(blob_ids, sizes):
+                fut = self._done.setdefault(bid, _Done((0, int(n), self.file_of(bid))))
+                refs.append(BlobRef(self, fut))
+        return refs
+
+    def put_many(self, blob_ids: list, produce_all) -> list:
+        """Write payloads this rank claimed (``claim``)."""
         job = self._ex.submit(self._write_files, list(blob_ids), produce_all)
         refs = []
         with self._lock:
@@ -334,7 +383,7 @@ class NodeBlobs(BlobSegment):
             reserve = _gb_env("DRYNX_LEDGER_RESERVE_GB", 8)
             for bid, d in zip(blob_ids, data):
                 b = memoryview(d).cast("B")
-                if os.environ.get("DRYNX_LEDGER_RETAIN", "") != "all":
+                if _budget():
                     while shutil.disk_usage(self.root).free - b.nbytes < reserve and self._files:
                         old = self._files.pop(0)
                         _mark_pruned(old)
@@ -346,17 +395,21 @@ class NodeBlobs(BlobSegment):
                 final = self.file_of(bid)
                 tmp = final + ".tmp"
                 self._pwrite_all([b], 0, tmp)
-                os.close(self._pfds.pop(tmp))
+                fd = self._pfds.pop(tmp)
+                with timers.span("ledger.sync"):
+                    os.fdatasync(fd)
+                os.close(fd)
                 os.replace(tmp, final)
                 self._files.append(final)
                 out.append((0, b.nbytes, final))
+            if blob_ids:
+                _fsync_dir(self.root)
         return out
 
     def close(self, remove: bool = False):
         super().close(remove)
-        if remove and self.writer:
-            shutil_rm = __import__("shutil").rmtree
-            shutil_rm(self.root, ignore_errors=True)
+        if remove:
+            __import__("shutil").rmtree(self.root, ignore_errors=True)
 
 
 class Store:
@@ -369,7 +422,7 @@ class Store:
         self._lock = threading.RLock()
         self._db = sqlite3.connect(path, check_same_thread=False, isolation_level=None)
         self._db.execute("PRAGMA journal_mode=WAL")
-        self._db.execute("PRAGMA synchronous=NORMAL")
+        self._db.execute("PRAGMA synchronous=FULL")  # every commit syncs the WAL (a committed bbolt batch)
         self._db.execute("CREATE TABLE IF NOT EXISTS kv (bucket TEXT, key TEXT, value BLOB, PRIMARY KEY(bucket, key))")
         self._q: queue.Queue = queue.Queue()
         self._writer = None
@@ -410,11 +463,13 @@ class Store:
                 except FileNotFoundError:
                     # a node-shared payload not yet written by the node's writer
                     # rank: wait for it, unless the writer pruned it
-                    if not _was_pruned(path) and _t.monotonic() < deadline:
+                    if _was_pruned(path):
+                        raise PrunedError(f"ledger value pruned for disk space ({path}; "
+                                          f"DRYNX_LEDGER_RETAIN=budget)") from None
+                    if _t.monotonic() < deadline:
                         _t.sleep(0.01)
                         continue
-                    raise FileNotFoundError(f"ledger value pruned for disk space ({path}; "
-                                            f"DRYNX_LEDGER_RETAIN=all keeps every proof)") from None
+                    raise FileNotFoundError(f"ledger value {path} was never written") from None
         if len(v) == len(_REF) + 16 and v.startswith(_REF):
             off, n = struct.unpack("<QQ", v[len(_REF):])
             if self._blob_f is not None:
@@ -428,14 +483,18 @@ class Store:
     def update(self, bucket: str, key: str, value: bytes):
         """UpdateDB(db, bucket, key, value)."""
         with self._lock:
-            self._db.execute("INSERT OR REPLACE INTO kv(bucket, key, value) VALUES (?,?,?)",
-                             (bucket, key, self._encode(value)))
+            v = self._encode(value)
+            if self._blob_f is not None:
+                self._blob_f.flush()
+                os.fdatasync(self._blob_f.fileno())
+            self._db.execute("INSERT OR REPLACE INTO kv(bucket, key, value) VALUES (?,?,?)", (bucket, key, v))
 
     def update_many(self, rows):
         with self._lock:
             enc = [(b, k, self._encode(v)) for b, k, v in rows]
             if self._blob_f is not None:
                 self._blob_f.flush()
+                os.fdatasync(self._blob_f.fileno())
             self._db.execute("BEGIN")
             self._db.executemany("INSERT OR REPLACE INTO kv(bucket, key, value) VALUES (?,?,?)", enc)
             self._db.execute("COMMIT")

@@ -49,7 +49,19 @@ log = get_logger("range_proof")
 G2_LEN, G1_LEN, GT_LEN, SC_LEN = 128, 64, 384, 32
 
 
+def _gamma_bits() -> int:
+    """Bits of the per-VN GT-membership combination weights: 40 (the
+    cyclotomic cofactor's smallest prime factor is ~2^38.8, so fewer bits
+    would let a non-GT element pass with non-negligible probability).
+    DRYNX_GAMMA_BITS may only raise it (up to 64)."""
+    gb = int(os.environ.get("DRYNX_GAMMA_BITS", "40"))
+    if not 40 <= gb <= 64:
+        raise ValueError(f"DRYNX_GAMMA_BITS={gb}: the GT-membership weights need 40..64 bits")
+    return gb
+
+
 # ----------------------------------------------------------------------------- setup (CN side)
+
 def init_range_proof_signature(u: int, secret: int | None = None, device="cpu") -> PublishSignatureBytes:
     """A CN's input-validation key for one output column: y = x*B, A_k = (x+k)^-1 * B2."""
     x = O.random_scalar() if secret is None else secret % O.R
@@ -927,7 +939,7 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
     ab_all = torch.cat([p_[0] for p_ in pairs]) if G > 1 else pairs[0][0]
     rho_all = torch.cat([p_[1] for p_ in pairs]) if G > 1 else pairs[0][1]
     # GT-membership combinations: one independent 40-bit gamma set PER VN
-    gb = int(os.environ.get("DRYNX_GAMMA_BITS", "40"))  # A/B diagnostics only: below 39 bits is unsound
+    gb = _gamma_bits()
     gam_all = _cat_draw(lambda c: c.bits(m, device, gb) if c is not None else _rand64(m, device, gb))
     # attribution: undecodable proofs (and, mode >= 1, wrong challenges) get
     # ZERO weights -- every weighted sum then runs over the decodable proofs

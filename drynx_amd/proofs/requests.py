@@ -405,10 +405,23 @@ def prewarm_signatures(reqs: list, sq, vn_ids: list, cache: "VerifierCache"):
     with timers.span(f"verify.signature.multi[{len(vn_ids)}]"):
         ok = sigma.schnorr_verify_batch(keys * len(vn_ids), dev)  # host below DRYNX_SIG_DEVICE_MIN checks
     n = len(reqs)
+    tag = _inbox_tag(reqs)
     for j, vn_id in enumerate(vn_ids):
-        cache.sig_pre[(sq.SurveyID, vn_id)] = (n, ok[j * n:(j + 1) * n])
+        cache.sig_pre[(sq.SurveyID, vn_id)] = (tag, ok[j * n:(j + 1) * n])
     while len(cache.sig_pre) > 64:
         cache.sig_pre.pop(next(iter(cache.sig_pre)))
+
+
+def _inbox_tag(reqs: list) -> bytes:
+    """Digest of an inbox's (sender, payload digest, signature) tuples:
+    cached signature verdicts apply only to exactly the envelopes they were
+    computed for (the two-stage flow checks two inboxes of one survey)."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for r in reqs:
+        h.update(r.sender_id.encode() + b"\x00" + bytes(r.digest()) + bytes(r.signature))
+    return h.digest()
 
 
 def should_verify(sq, req: ProofRequest, vn_index: int, n_vns: int, coins=None) -> bool:
@@ -427,7 +440,7 @@ class VerifierCache:
     def __init__(self):
         self._sig = {}
         self.ks_pre: dict = {}  # (SurveyID, vn_id) -> {request index: bool} (prewarm_keyswitch)
-        self.sig_pre: dict = {}  # (SurveyID, vn_id) -> (n requests, [bool]) (prewarm_signatures)
+        self.sig_pre: dict = {}  # (SurveyID, vn_id) -> (inbox tag, [bool]) (prewarm_signatures)
 
     def sigmat(self, sq, device):
         """Keyed by a digest of the signature set, so repeated surveys over the
@@ -974,12 +987,12 @@ def verify_requests(reqs: list, sq, vn_id: str, vn_index: int, n_vns: int, devic
     todo: dict = {}
     pooled_idx: list = []
     pre = cache.sig_pre.pop((sq.SurveyID, vn_id), None)
-    if pre is not None and pre[0] == len(reqs):
-        sigs_ok = pre[1]
+    with timers.span("verify.digests"):
+        prefetch_digests(reqs)
+    keys = [(sq.IDtoPublic.get(r.sender_id), r.digest(), r.signature) for r in reqs]
+    if pre is not None and pre[0] == _inbox_tag(reqs):
+        sigs_ok = pre[1]  # this VN's checks of exactly these envelopes, from the co-hosted batch
     else:
-        with timers.span("verify.digests"):
-            prefetch_digests(reqs)
-        keys = [(sq.IDtoPublic.get(r.sender_id), r.digest(), r.signature) for r in reqs]
         with timers.span("verify.signature.batch"):
             sigs_ok = sigma.schnorr_verify_batch(keys, device) if reqs else []
     for i, req in enumerate(reqs):

@@ -19,7 +19,6 @@ from __future__ import annotations
 
 import copy
 import os
-import sys
 import time
 from dataclasses import dataclass, field
 
@@ -67,14 +66,6 @@ class DrynxNode:
 
     def __init__(self, cluster: Cluster, comm: Comm | None = None, workdir: str = "./drynx_db", device=None,
                  dp_data: dict | None = None):
-        sw = float(os.environ.get("DRYNX_SWITCH_INTERVAL", "0.0005") or 0)
-        if sw > 0:
-            # the node's worker threads (ledger writers, CN-proof finishing, the
-            # pool, the querier) hand the GIL back to the query's thread after
-            # 0.5 ms instead of Python's 5 ms: --u 0 --l 0 25.8-28.2 -> 23.4-23.9 ms
-            # on one box, the headline unchanged (profiles/r4/serial/v_*.json);
-            # DRYNX_SWITCH_INTERVAL=0 keeps the interpreter's setting
-            sys.setswitchinterval(sw)
         self.comm = comm or LocalComm(device or ("cuda" if torch.cuda.is_available() else "cpu"))
         self.rank = self.comm.rank
         self.device = torch.device(device) if device is not None else self.comm.device
@@ -168,13 +159,18 @@ class DrynxNode:
         refs = {k: self._blobs.get(k) for k in fresh}
         new = [k for k, v in refs.items() if v is None]
         if new:
-            tensors = [reqs[fresh[k][0]].tensor.contiguous().reshape(-1).view(torch.uint8) for k in new]
-            if getattr(self._blobs, "writer", True):
-                put = self._blobs.put_many(new, self._host_bytes(tensors))
-            else:  # another VN rank of this node writes them: references only, no device-to-host copy
-                put = self._blobs.put_many(new, None, [t.numel() for t in tensors])
-            for k, ref in zip(new, put):
-                refs[k] = ref
+            tensors = {k: reqs[fresh[k][0]].tensor.contiguous().reshape(-1).view(torch.uint8) for k in new}
+            claims = self._blobs.claim(new) if hasattr(self._blobs, "claim") else [True] * len(new)
+            mine = [k for k, c in zip(new, claims) if c]
+            theirs = [k for k, c in zip(new, claims) if not c]
+            timers.count("ledger.written", len(mine))
+            timers.count("ledger.referenced", len(theirs))
+            if mine:
+                for k, ref in zip(mine, self._blobs.put_many(mine, self._host_bytes([tensors[k] for k in mine]))):
+                    refs[k] = ref
+            if theirs:  # another VN rank of this node claimed them: references only, no device-to-host copy
+                for k, ref in zip(theirs, self._blobs.put_refs(theirs, [tensors[k].numel() for k in theirs])):
+                    refs[k] = ref
         for k, idxs in fresh.items():
             for i in idxs:
                 out[i] = refs[k]
@@ -183,10 +179,11 @@ class DrynxNode:
     def _blob_store(self):
         """This rank's store of large ledger values.  On a single node with VNs
         on several ranks (LOCAL_WORLD_SIZE == WORLD_SIZE), the VN ranks share
-        one content-addressed node directory and only the lowest VN rank copies
-        and writes the payloads (``ledger.store.NodeBlobs``: three VN ranks
-        would otherwise write ~1.7 GB per query to one disk);
-        DRYNX_LEDGER_NODE_SHARE=0 keeps one private store per rank."""
+        one content-addressed node directory and each payload is copied and
+        written once, by the first VN rank of the node holding it that claims
+        it (``ledger.store.NodeBlobs``: three VN ranks would otherwise write
+        ~1.7 GB per query to one disk); DRYNX_LEDGER_NODE_SHARE=0 keeps one
+        private store per rank."""
         from ..ledger.store import BlobSegment, NodeBlobs
 
         W = self.comm.world
@@ -198,7 +195,7 @@ class DrynxNode:
         if (W > 1 and lws == W and run and len(vn_ranks) > 1 and self.rank in vn_ranks
                 and os.environ.get("DRYNX_LEDGER_NODE_SHARE", "1") == "1"):
             root = os.path.join(os.path.dirname(os.path.abspath(self.workdir)), f"drynx_node_ledger_{run}")
-            return NodeBlobs(root, writer=self.rank == vn_ranks[0], device=self.device)
+            return NodeBlobs(root, device=self.device)
         return BlobSegment(os.path.join(self.workdir, f"ledger_r{self.rank}.blobs"), self.device)
 
     def _host_bytes(self, tensors: list):
@@ -699,7 +696,8 @@ class DrynxNode:
         return json.loads(raw) if raw else {}
 
     def flush_stores(self):
-        """Wait until every queued ledger write is durable."""
+        """Wait until every queued ledger write is durable (blob writes are
+        fdatasync'ed by the ledger worker, SQLite commits sync the WAL)."""
         for s in self._stores.values():
             s.flush()
         if hasattr(self, "_blobs"):

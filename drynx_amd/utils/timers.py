@@ -3,9 +3,9 @@
 ``<node>_DataCollectionProtocol``, ``JustExecution``, ``<node>_AggregationPhase``,
 ``<node>_KeySwitchingPhase``, ``<name>_DPencoding``, ``<name>_AllProofs``,
 ``<VN>_VerifyRange``, ``BI``, ``Decode``, ``Decryption``, ``GradientDescent``,
-``Simulation``...).  GPU work inside a timer is synchronised at the end so the
-interval is real device time, and each timer also emits a roctx range when
-profiling under rocprofv3."""
+``Simulation``...).  A timer is wall time from the host's start of the phase
+to the completion of the device work the phase queued (see ``Timer``), and
+each timer also emits a roctx range when profiling under rocprofv3."""
 from __future__ import annotations
 
 import contextlib
@@ -88,38 +88,47 @@ def dump_trace(path: str | None = None):
         json.dump({"traceEvents": ev, "displayTimeUnit": "ms"}, f)
 
 
-def _sync():
-    # the calling thread's stream only: phases running on other threads/streams
-    # (querier decode, proof signing) keep overlapping
-    if torch.cuda.is_available() and torch.cuda.is_initialized():
-        torch.cuda.current_stream().synchronize()
+def _device_timed() -> bool:
+    return torch.cuda.is_available() and torch.cuda.is_initialized()
 
 
-def _use_events() -> bool:
-    """Device-timed phases measure with HIP events on the phase's stream
-    (resolved when the timers are read) instead of synchronising the host at
-    both ends: a phase timer then costs the query no host-device round trip.
-    DRYNX_TIMER_SYNC=1 restores the synchronising timers."""
-    return (os.environ.get("DRYNX_TIMER_SYNC") != "1" and torch.cuda.is_available()
-            and torch.cuda.is_initialized())
+# Phase timers measure WALL time from the host's start of the phase to the
+# completion of the last operation the phase queued on its stream (the
+# reference's StartTimer/EndTimer bracket goroutines that block until their
+# work is done).  ``end`` records a HIP event instead of synchronising the
+# query's thread; a watcher thread stamps the host time at which the event
+# completes (polling, 0.2 ms) and records ``completion - start``.  A phase that
+# starts behind a stream backlog therefore counts the wait, and work the phase
+# joined from other streams (wait_stream before ``end``) is covered.
+_watch: list = []          # (name, host start, end event) not yet complete
+_watch_cv = threading.Condition(_lock)
+_watcher = None
 
 
-_pending: list = []  # (name, start event, end event) of event-timed phases
+def _watch_loop():
+    while True:
+        with _watch_cv:
+            while not _watch:
+                _watch_cv.wait()
+            items = list(_watch)
+        done = []
+        for it in items:
+            if it[2].query():
+                done.append((it, time.perf_counter()))
+        with _watch_cv:
+            for it, t1 in done:
+                _watch.remove(it)
+                _records[it[0]].append(t1 - it[1])
+            if done:
+                _watch_cv.notify_all()
+        time.sleep(0.0002)
 
 
 def _resolve():
-    """Turn finished event pairs into recorded intervals (device time from
-    the phase's first to its last queued operation on its stream)."""
-    with _lock:
-        todo = list(_pending)
-        _pending.clear()
-    done = []
-    for name, e0, e1 in todo:
-        e1.synchronize()
-        done.append((name, e0.elapsed_time(e1) / 1e3))
-    with _lock:
-        for name, dt in done:
-            _records[name].append(dt)
+    """Wait until every watched phase has completed and been recorded."""
+    with _watch_cv:
+        while _watch:
+            _watch_cv.wait(0.05)
 
 
 class Timer:
@@ -127,41 +136,31 @@ class Timer:
         self.name = name
         self.sync = sync
         self.t0 = None
-        self.ev = None
 
     def start(self):
-        if self.sync and _use_events():
-            self.ev = torch.cuda.Event(enable_timing=True)
-            self.ev.record()
-        elif self.sync:
-            _sync()
         self.t0 = time.perf_counter()
         return self
 
     def end(self) -> float:
-        if self.ev is not None:
-            e1 = torch.cuda.Event(enable_timing=True)
-            e1.record()
-            t1 = time.perf_counter()
-            with _lock:
-                _pending.append((self.name, self.ev, e1))
-                if len(_pending) > 4096:
-                    todo = _pending[:2048]
-                    del _pending[:2048]
-                    for name, a, b in todo:
-                        b.synchronize()
-                        _records[name].append(a.elapsed_time(b) / 1e3)
-            if _TRACE:
-                _emit(self.name, int(self.t0 * 1e9), int(t1 * 1e9))
-            return t1 - self.t0
-        if self.sync:
-            _sync()
+        global _watcher
         t1 = time.perf_counter()
+        if _TRACE:
+            _emit(self.name, int(self.t0 * 1e9), int(t1 * 1e9))
+        if self.sync and _device_timed():
+            e1 = torch.cuda.Event()
+            e1.record()
+            if not e1.query():  # the phase's device work is still running: the watcher stamps its end
+                with _watch_cv:
+                    _watch.append((self.name, self.t0, e1))
+                    if _watcher is None:
+                        _watcher = threading.Thread(target=_watch_loop, daemon=True, name="drynx-timers")
+                        _watcher.start()
+                    _watch_cv.notify_all()
+                return t1 - self.t0
+            t1 = time.perf_counter()
         dt = t1 - self.t0
         with _lock:
             _records[self.name].append(dt)
-        if _TRACE:
-            _emit(self.name, int(self.t0 * 1e9), int(t1 * 1e9))
         return dt
 
 
@@ -221,8 +220,8 @@ def counters() -> dict:
 
 
 def reset():
+    _resolve()
     with _lock:
-        _pending.clear()
         _records.clear()
         _counts.clear()
 

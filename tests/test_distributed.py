@@ -161,3 +161,34 @@ def test_forwarded_args_avoid_launcher_abbreviations():
     finally:
         sys.argv = argv
     assert (a.gpus, a.u, a.l, a.steps, a.features) == (8, 4, 2, 3, 12)
+
+
+def _run_bench(gpus: int, extra: list, env_extra: dict | None = None, timeout: int = 900):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra or {})
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), *extra],
+                       capture_output=True, text=True, timeout=timeout, env=env)
+    return _bench_line(r)
+
+
+@pytest.mark.slow
+def test_two_ranks_sharded_tables_and_node_ledger():
+    """Two ranks on one node, VerificationSharding 2 (each proof checked by 2
+    of the 3 VNs, per-CN payloads fanned out to the assigned VNs only):
+    the prover tables are built 1/2 per rank and broadcast (GLS-8 layout
+    forced) and equal a one-rank build bit for bit; the VN ranks share
+    content-addressed ledger payloads (each written once on the node, the
+    other rank referencing it) and every VN's stored proofs read back."""
+    small = ["--steps", "1", "--warmup", "1", "--records", "2000", "--features", "2", "--max-iter", "5",
+             "--device", "cpu", "--deterministic-sigs", "--table-digest"]
+    env = {"DRYNX_PROVER_TABLE_BITS": "7"}
+    d2 = _run_bench(2, small + ["--verification-sharding", "2", "--check-ledger"], env)
+    d1 = _run_bench(1, small, env)
+    assert d2["n_gpus"] == 2 and d2["all_proofs_valid"] and d2["result_ok"]
+    ranks = d2["ranks"]
+    assert all(r["bytes_recv"] > 0 for r in ranks)
+    assert {r["table_digest"] for r in ranks} == {d1["ranks"][0]["table_digest"]}
+    # node-shared payloads: written once on the node, the other VN rank references them
+    assert sum(r["ledger_written"] for r in ranks) > 0 and sum(r["ledger_referenced"] for r in ranks) > 0
+    stored = {vn: n for r in ranks for vn, n in r["ledger_readback"].items()}
+    assert sorted(stored) == ["vn0", "vn1", "vn2"] and all(n > 0 for n in stored.values())

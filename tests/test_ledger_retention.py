@@ -1,8 +1,8 @@
-"""Ledger blob segments under a disk budget (ledger/store.py BlobSegment):
-values rotate into generation files; when a write would leave less than the
-reserve free, the oldest generations are deleted, their references fail
-loudly and everything newer still reads back; DRYNX_LEDGER_RETAIN=all keeps
-every file."""
+"""Ledger blob segments (ledger/store.py BlobSegment): values rotate into
+generation files and every file is kept by default (as bbolt keeps every
+proof); under the opt-in disk budget (DRYNX_LEDGER_RETAIN=budget) the oldest
+generations are deleted when a write would leave less than the reserve free,
+their references fail loudly and everything newer still reads back."""
 import os
 
 import numpy as np
@@ -21,8 +21,8 @@ def _put(seg, store, i, size=4096):
 @pytest.mark.parametrize("retain", ["budget", "all"])
 def test_blob_generations_and_pruning(tmp_path, monkeypatch, retain):
     monkeypatch.setenv("DRYNX_LEDGER_SEGMENT_GB", str(10000 / (1 << 30)))   # ~10 KB generations
-    if retain == "all":
-        monkeypatch.setenv("DRYNX_LEDGER_RETAIN", "all")
+    if retain == "budget":
+        monkeypatch.setenv("DRYNX_LEDGER_RETAIN", "budget")
     seg = BlobSegment(str(tmp_path / "ledger_r0.blobs"))
     store = Store(str(tmp_path / "db_vn0.sqlite"))
     want = {i: _put(seg, store, i) for i in range(3)}
@@ -40,7 +40,9 @@ def test_blob_generations_and_pruning(tmp_path, monkeypatch, retain):
         assert store.get("proofs", "k0") == want[0]
     else:
         assert not os.path.exists(gens_before[0]) and len(seg._gens) < len(gens_before) + 1
-        with pytest.raises(FileNotFoundError, match="pruned"):
+        from drynx_amd.ledger.store import PrunedError
+
+        with pytest.raises(PrunedError, match="pruned"):
             store.get("proofs", "k0")
     store.close()
     seg.close(remove=True)
@@ -49,17 +51,20 @@ def test_blob_generations_and_pruning(tmp_path, monkeypatch, retain):
 
 def test_node_shared_payloads(tmp_path):
     """The VN ranks of one node share content-addressed payload files: the
-    writer copies and writes, a reader rank stores references only and its
-    reads wait until the writer's file is complete."""
+    first rank to claim a digest copies and writes it, another rank holding
+    the same payload stores a reference only and its reads wait until the
+    claimant's file is complete."""
     from drynx_amd.ledger.store import NodeBlobs
 
     root = str(tmp_path / "node")
-    reader = NodeBlobs(root, writer=False)
+    writer = NodeBlobs(root)
+    reader = NodeBlobs(root)
+    assert writer.claim(["d1"]) == [True]
+    assert reader.claim(["d1"]) == [False]           # already claimed on the node
     rstore = Store(str(tmp_path / "db_vn1.sqlite"))
     data = np.arange(100000, dtype=np.uint32).view(np.uint8)
-    ref = reader.put_many(["d1"], None, [data.nbytes])[0]
-    rstore.update("proofs", "k", ref)               # a reference before the writer has written anything
-    writer = NodeBlobs(root, writer=True)
+    ref = reader.put_refs(["d1"], [data.nbytes])[0]
+    rstore.update("proofs", "k", ref)               # a reference before the claimant has written anything
     import threading
     import time
 
@@ -70,10 +75,57 @@ def test_node_shared_payloads(tmp_path):
 
     th = threading.Thread(target=late_write)
     th.start()
-    assert rstore.get("proofs", "k") == data.tobytes()   # waited for the writer
+    assert rstore.get("proofs", "k") == data.tobytes()   # waited for the claimant
     th.join()
     assert os.path.exists(os.path.join(root, "d1.blob")) and not os.path.exists(os.path.join(root, "d1.blob.tmp"))
     rstore.close()
     reader.close(remove=True)
     writer.close(remove=True)
     assert not os.path.exists(root)
+
+
+def test_node_blobs_claim_by_holder_only(tmp_path):
+    """Sharded fan-out: the lowest VN rank of the node may receive a
+    header-only envelope.  Whichever rank holds the payload claims and writes
+    it, so every VN's stored reference reads back (the old fixed-writer
+    scheme left the other VN waiting for a file nobody wrote)."""
+    from drynx_amd.ledger.store import NodeBlobs
+
+    root = str(tmp_path / "node")
+    low, high = NodeBlobs(root), NodeBlobs(root)      # VN ranks 3 and 4 of a node
+    data = np.full(70000, 7, dtype=np.uint8)
+    # rank 3 got only the header: it claims nothing; rank 4 holds the payload
+    assert high.claim(["p"]) == [True]
+    ref = high.put_many(["p"], lambda: [memoryview(data)])[0]
+    st = Store(str(tmp_path / "db_vn1.sqlite"))
+    st.update("proofs", "k", ref)
+    assert st.get("proofs", "k") == data.tobytes()
+    st.close()
+    low.close(remove=True)
+    high.close(remove=True)
+
+
+def test_first_survey_reads_back_after_many(tmp_path):
+    """Keep-everything default: after 100 surveys of large payloads the first
+    survey's values read back bit-identically (bbolt keeps every proof,
+    services/service_skipchain.go:240-320), and each write was synced."""
+    seg = BlobSegment(str(tmp_path / "ledger_r0.blobs"))
+    store = Store(str(tmp_path / "db_vn0.sqlite"))
+    pruned0 = BlobSegment.pruned
+    first = {}
+    for s_ in range(100):
+        rows = []
+        for j in range(2):
+            data = np.random.default_rng(s_ * 7 + j).integers(0, 256, 70000, dtype=np.uint8)
+            ref = seg.put_many([f"s{s_}p{j}"], lambda d=data: [memoryview(d)])[0]
+            rows.append((f"survey{s_}/range", f"dp{j}", ref))
+            if s_ == 0:
+                first[f"dp{j}"] = data.tobytes()
+        for b, k, r in rows:
+            store.update_async(b, k, r)
+    seg.flush()
+    store.flush()
+    assert store.bucket("survey0/range") == first
+    assert BlobSegment.pruned == pruned0
+    store.close()
+    seg.close(remove=True)
