@@ -75,15 +75,30 @@ __device__ __forceinline__ Fp6 mul6(const Fp6 &a, const Fp6 &b) {
   return {c0, c1, c2};
 }
 
-// x <- role operand of (x * y) (x, y: role operands of two GT elements)
-__device__ __forceinline__ void mul(Fp6 &x, const Fp6 &y, const Role &R) {
+// x <- role operand of the product whose role Fp6 products are t
+// (t0 = a0 b0 on role 0, t1 = a1 b1 on role 1, t2 = (a0 + a1)(b0 + b1) on role 2)
+__device__ __forceinline__ void combine(Fp6 &x, const Fp6 &t, const Role &R) {
   const int lane0 = R.base;
-  const Fp6 t = mul6(x, y);
   const Fp6 p = shfl6(t, lane0 + (R.r == 1 ? 0 : 1));  // r0, r2: t1 ; r1: t0
   const Fp6 q = shfl6(t, lane0 + 2);                   // r1: t2
   const Fp6 u = add(t, mul_v(p));                      // r0: c0 ; r2: t2 + v t1
   x = sub(sub(sel6(R.r == 1, q, u), sel6(R.r == 0, Fp6::zero(), p)), sel6(R.r == 1, t, Fp6::zero()));
 }
+
+// x <- role operand of (x * y) (x, y: role operands of two GT elements)
+__device__ __forceinline__ void mul(Fp6 &x, const Fp6 &y, const Role &R) { combine(x, mul6(x, y), R); }
+
+// Fp6 product with b.c2 = 0 (5 Fp2 products instead of 6)
+__device__ __forceinline__ Fp6 mul6_b2z(const Fp6 &a, const Fp6 &b) {
+  const Fp2 t0 = dx::mul(a.c0, b.c0), t1 = dx::mul(a.c1, b.c1);
+  return {add(t0, mul_xi(dx::mul(a.c2, b.c1))), sub(sub(dx::mul(add(a.c0, a.c1), add(b.c0, b.c1)), t0), t1),
+          add(dx::mul(a.c2, b.c0), t1)};
+}
+
+// x <- role operand of (x * y) for a y whose role operands all have c2 = 0
+// (a sparse Miller line 1 + l1 w + l3 w^3 = 1 + (l1 + l3 v) w: roles (1, 0, 0),
+// (l1, l3, 0), (1 + l1, l3, 0))
+__device__ __forceinline__ void mul_sparse(Fp6 &x, const Fp6 &y, const Role &R) { combine(x, mul6_b2z(x, y), R); }
 
 // x <- role operand of frob<1>(x): coefficient-wise on the roles 0 and 1
 // (conjugation times gamma_1[e], e = the w-exponent), role 2 re-summed

@@ -397,17 +397,5 @@ int dx_bsgs_solve(int on_gpu, void *stream, const uint32_t *targets_jac, const u
 }
 
 
-// A stream whose kernels only use the CUs set in `mask` (nwords x 32 bits,
-// logical CU ids).  A long, occupancy-filling kernel (the range-proof Miller
-// fold) runs on such a stream so a few CUs stay free for the short,
-// latency-bound launches queued beside it on other streams.
-int dx_stream_create_cu_mask(int device, const uint32_t *mask, int nwords, void **out) {
-  if (hipSetDevice(device) != hipSuccess) return 1;
-  hipStream_t s = nullptr;
-  if (hipExtStreamCreateWithCUMask(&s, (uint32_t)nwords, mask) != hipSuccess) return 2;
-  *out = (void *)s;
-  return 0;
-}
-
 int dx_version() { return 1; }
 }  // extern "C"

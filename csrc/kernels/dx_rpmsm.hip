@@ -233,9 +233,9 @@ DX_HD void chunk_weight_one(const uint32_t *B_jac, const int32_t *d, const int64
     tot = jadd(tot, acc);
   }
   for (; i >= 0; i--) acc = jadd(acc, at<G2J>(B_jac, a + i));  // offset 0: weight base only
-  if (b0) {
-    G2J m = G2J::inf();
-    for (int bit = 30; bit >= 0; bit--) {
+  if (b0) {  // base * acc, double-and-add from the base's top bit
+    G2J m = acc;
+    for (int bit = 30 - __builtin_clz(b0); bit >= 0; bit--) {
       m = jdbl(m);
       if ((b0 >> bit) & 1u) m = jadd(m, acc);
     }

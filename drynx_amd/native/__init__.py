@@ -92,7 +92,6 @@ _SIGS = {
     "dx_gt_fb_pow": [_I, _P, _P, _P, _P, _P, _L],
     "dx_gt_prod_chunks": [_I, _P, _P, _P, _L, _L, _L],
     "dx_version": [],
-    "dx_stream_create_cu_mask": [_I, _P, _I, ctypes.POINTER(ctypes.c_void_p)],
     "dx_lr_moments": [_P, _P, _P, _L, _I, _P, _I],
     "dx_lr_gd_k2": [_P, _P, _P, _I, ctypes.c_double, ctypes.c_double, ctypes.c_double, _I, ctypes.c_double,
                     ctypes.c_double, ctypes.c_double, _P],
@@ -104,15 +103,11 @@ _SIGS = {
     "dx_g1_mul_fast": [_P, _P, _P, _P, _L, _I, _I],
     "dx_rp_verify_fold": [_P, _P, _P, _P, _P, _P, _L, _I, _I],
     "dx_gt_slice_prod": [_I, _P, _P, _P, _P, _P, _P, _L],
-    "dx_bucket_sort_tmp": [_L, _I, ctypes.POINTER(ctypes.c_uint64)],
     "dx_g1_mul_glv": [_P, _P, _P, _P, _P, _L, _I],
     "dx_rp_u_joint_split": [_I, _P, _P, _P, _P, _L, _I, _I, _L, _I, _P],
-    "dx_bucket_sort": [_I, _P, _P, _P, _P, _P, _L, _I, _P, ctypes.c_uint64],
     "dx_bucket_bounds": [_I, _P, _P, _L, _L, _P, _P],
-    "dx_slice_plan": [_I, _P, _P, _P, _P, _I, _L, _P, _P],
-    "dx_bucket_hist": [_I, _P, _P, _L, _L, _P],
-    "dx_bucket_scatter": [_I, _P, _P, _P, _L, _L, _P, _P, _P],
     "dx_slice_desc": [_I, _P, _P, _P, _P, _I, _L, _L, _P, _P],
+    "dx_lane_slices": [_I, _P, _P, _P, _P, _P, _P, _L, _P, _P],
     "dx_g1_slice_sum": [_I, _P, _P, _P, _P, _P, _P, _L],
     "dx_rp_prove_a": [_I, _P, _P, _P, _P, _P, _P, _L, _I, _I],
     "dx_rp_prove_a_tab": [_I, _P, _P, _P, _P, _P, _P, _P, _L, _I, _I, _I],
@@ -150,6 +145,8 @@ _SIGS = {
     "dx_rp_accum_n_ni": [_P, _P, _P, _P, _P, _L, _L, _I, _I],
     "dx_rp_ncoeffs_inl": [_P, _P, _P, _P, _L],
     "dx_rp_accum_n_inl": [_P, _P, _P, _P, _P, _L, _L, _I, _I],
+    "dx_ufold_coop": [_P, _P, _P, _P, _P, _L, _L, _L],
+    "dx_ufold_coop_steps": [],
     "dx_gt_frob8": [_I, _P, _P, _P, _L],
     "dx_gls6_entries": [],
     "dx_g2_gls6_table": [_I, _P, _P, _P, _P, _L],
@@ -183,36 +180,6 @@ def _declare(lib):
 
 def lib():
     return _load()
-
-
-_cu_streams: dict = {}
-
-
-def cu_masked_stream(device, reserve: int):
-    """A torch stream (ExternalStream over hipExtStreamCreateWithCUMask) that
-    leaves ``reserve`` CUs free, spread evenly over the CU ids (every XCD
-    keeps a few for other streams).  None when reserve <= 0.  Cached per
-    (device, reserve); the stream lives as long as the process."""
-    if reserve <= 0:
-        return None
-    dev = torch.device(device)
-    key = (dev.index or 0, reserve)
-    if key not in _cu_streams:
-        n_cu = torch.cuda.get_device_properties(dev).multi_processor_count
-        step = max(1, n_cu // reserve)
-        off = {(k * step + step - 1) % n_cu for k in range(reserve)}
-        words = (n_cu + 31) // 32
-        mask = [0] * words
-        for c in range(n_cu):
-            if c not in off:
-                mask[c // 32] |= 1 << (c % 32)
-        arr = (ctypes.c_uint32 * words)(*mask)
-        out = ctypes.c_void_p()
-        rc = _load().dx_stream_create_cu_mask(key[0], ctypes.cast(arr, ctypes.c_void_p), words, ctypes.byref(out))
-        if rc:
-            raise RuntimeError(f"dx_stream_create_cu_mask failed rc={rc}")
-        _cu_streams[key] = torch.cuda.ExternalStream(out.value, device=dev)
-    return _cu_streams[key]
 
 
 def loaded_path() -> str:
@@ -1430,6 +1397,26 @@ def rp_fold_accum_n(img: torch.Tensor, UV: torch.Tensor, V_aff: torch.Tensor, pe
     return fb
 
 
+def rp_fold_accum_coop(img: torch.Tensor, UV: torch.Tensor, V_aff: torch.Tensor, period: int, G: int) -> torch.Tensor:
+    """``rp_fold_accum_n`` (K = 1 layout) with three lanes per item
+    (csrc/kernels/dx_ufold_coop.hip), for batches too small to fill the chip
+    one item per lane: every item's Miller value, then 64-item block
+    products -> [G * period / 64, 96].  GPU only."""
+    m = _rows(V_aff, 32)
+    n = G * period
+    assert _rows(UV, 16) == n and period >= m and period % 64 == 0
+    assert img.numel() == _load().dx_ufold_coop_steps() * 8 * m * 4
+    f = torch.empty((n, 96), dtype=torch.int32, device=UV.device)
+    _, s = _ctx(img, UV, V_aff)
+    rc = _raw_call("dx_ufold_coop", s, _ptr(img), _ptr(UV), _ptr(V_aff), _ptr(f), m, period, n)
+    if rc:
+        raise RuntimeError(f"dx_ufold_coop failed rc={rc}")
+    x = f.view(n // 64, 64, 96).transpose(0, 1)
+    while x.shape[0] > 1:
+        x = _gt_prod_level(x, 8)
+    return x.view(n // 64, 96)
+
+
 def gt_frob8(a: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
     """a^(p^8) per row (= a^GLV_LAMBDA on GT); ``out``: a contiguous
     destination of a's shape (e.g. the second half of a stacked image)."""
@@ -1520,82 +1507,27 @@ def _multi_exp64_plan(rho: torch.Tensor):
     return _bucket_plan(rho, _ME_W)
 
 
-class _Counts:
-    """Per-bucket counts of a plan still on their way to the host: a pinned
-    copy queued behind the plan's kernels, waited for by ``get``."""
-
-    def __init__(self, counts_dev: torch.Tensor):
-        self.host = torch.empty(counts_dev.shape, dtype=counts_dev.dtype, pin_memory=True)
-        self.host.copy_(counts_dev, non_blocking=True)
-        self.ev = torch.cuda.Event()
-        self.ev.record()
-        self.arr = None
-
-    def get(self) -> np.ndarray:
-        if self.arr is None:
-            self.ev.synchronize()
-            self.arr = self.host.numpy().astype(np.int64)
-        return self.arr
+def _sort_buckets(keys: torch.Tensor, items: torch.Tensor, nb: int):
+    """Sort the (key, item) entries of a bucket plan by key (torch's onesweep
+    radix sort: on gfx950 faster than a direct rocPRIM pairs sort over the
+    keys' bits, and it interferes least with the kernels running beside the
+    plan, profiles/r4/ab_plan_sort.txt) and find every bucket's run
+    (csrc/kernels/dx_plan.hip) -> (sorted items, per-bucket counts on the
+    host: the plan's one device-to-host copy)."""
+    i2, first, end = _sorted_runs(keys, items, nb)
+    return i2, (end - first).cpu().numpy().astype(np.int64)
 
 
-def _counts_out(counts_dev: torch.Tensor, defer: bool):
-    if defer and counts_dev.is_cuda:
-        return _Counts(counts_dev)
-    return counts_dev.cpu().numpy().astype(np.int64)                       # the one host sync
-
-
-def _cget(counts) -> np.ndarray:
-    return counts.get() if isinstance(counts, _Counts) else counts
-
-
-def _sort_buckets(keys: torch.Tensor, items: torch.Tensor, nb: int, defer: bool = False):
-    """Sort the (key, item) entries of a bucket plan by key over its low
-    bit_length(nb) bits (csrc/kernels/dx_plan.hip: rocPRIM radix sort, 4-byte
-    payload) and find every bucket's run -> (sorted items, per-bucket counts
-    on the host: the plan's one device-to-host copy).  ``defer``: the counts
-    come back as a ``_Counts`` whose copy is in flight (``_cget`` waits), so
-    a caller can queue other work before the plan's host sync."""
+def _sorted_runs(keys: torch.Tensor, items: torch.Tensor, nb: int):
+    """(items sorted by key, first[nb], end[nb]): every bucket's run in the
+    sorted entries, on the keys' device (empty buckets: first = end = 0)."""
     dev = keys.device
-    n = keys.numel()
-    g, s = _ctx(keys)
-    # "torch" (default): onesweep radix sort + run boundaries -- on the 1-GPU
-    # headline it measured fastest (profiles/r4/ab_plan_sort.txt): the plans run
-    # beside the U-side kernels, and the alternatives (a counting sort's atomic
-    # histogram / scatter, a rocPRIM pairs sort over the keys' bits) cost less
-    # alone but interfere more with the concurrent work
-    mode = os.environ.get("DRYNX_PLAN_SORT", "torch")
-    if mode == "count":
-        # counting sort by bucket (csrc/kernels/dx_plan.hip): histogram -> slots -> scatter
-        counts_d = torch.zeros(nb, dtype=torch.int32, device=dev)
-        _call("dx_bucket_hist", g, s, _ptr(keys), n, nb, _ptr(counts_d))
-        offs = torch.cumsum(counts_d, 0, dtype=torch.int64) - counts_d
-        cursor = torch.zeros(nb, dtype=torch.int32, device=dev)
-        i2 = torch.empty_like(items)
-        _call("dx_bucket_scatter", g, s, _ptr(keys), _ptr(items), n, nb, _ptr(offs), _ptr(cursor), _ptr(i2))
-        return i2, _counts_out(counts_d, defer)
-    if not g or mode == "torch":
-        # torch's onesweep radix sort (hipCUB): measured faster on gfx950 than a
-        # direct rocprim::radix_sort_pairs over the keys' bits (5.9 vs ~1.1 ms
-        # per 48M-entry plan); the runs then come from dx_bucket_bounds
-        k2, order = torch.sort(keys)
-        i2 = items.index_select(0, order)
-        bounds = torch.zeros((2, nb), dtype=torch.int64, device=dev)
-        _call("dx_bucket_bounds", g, s, _ptr(k2), n, nb, _ptr(bounds[0]), _ptr(bounds[1]))
-        return i2, _counts_out((bounds[1] - bounds[0]).to(torch.int32), defer)
-    end_bit = max(1, int(nb).bit_length())
-    k2 = torch.empty_like(keys)
-    i2 = torch.empty_like(items)
-    tmp = None
-    tb = ctypes.c_uint64(0)
-    if g:
-        rc = _raw_call("dx_bucket_sort_tmp", n, end_bit, ctypes.byref(tb))
-        if rc:
-            raise RuntimeError("dx_bucket_sort_tmp failed")
-        tmp = torch.empty(max(1, int(tb.value)), dtype=torch.uint8, device=dev)
-    _call("dx_bucket_sort", g, s, _ptr(keys), _ptr(items), _ptr(k2), _ptr(i2), n, end_bit, _ptr(tmp), tb.value)
+    k2, order = torch.sort(keys)
+    i2 = items.index_select(0, order)
     bounds = torch.zeros((2, nb), dtype=torch.int64, device=dev)
-    _call("dx_bucket_bounds", g, s, _ptr(k2), n, nb, _ptr(bounds[0]), _ptr(bounds[1]))
-    return i2, _counts_out((bounds[1] - bounds[0]).to(torch.int32), defer)
+    g, s = _ctx(k2)
+    _call("dx_bucket_bounds", g, s, _ptr(k2), keys.numel(), nb, _ptr(bounds[0]), _ptr(bounds[1]))
+    return i2, bounds[0], bounds[1]
 
 
 def _segment_passes_dev(counts, dev, first_slice: int | None = None):
@@ -1663,13 +1595,12 @@ def _group_arg(group, n: int, dev):
     return group.to(device=dev, dtype=torch.int32).contiguous(), 0
 
 
-def _bucket_plan(k: torch.Tensor, W: int, group: torch.Tensor | None = None, n_groups: int = 1, c: int = 8,
-                 defer: bool = False):
+def _bucket_plan(k: torch.Tensor, W: int, group: torch.Tensor | None = None, n_groups: int = 1, c: int = 8):
     """Bucket plan of a multi-scalar product over the low W c-bit windows of
     the scalars k [n, 8]: window w, digit d -> bucket (w << c) + d (plus
     g * (W << c) for entries of group g when `group` is given); entries sorted
     by bucket, then segmented passes down to one value per non-empty bucket.
-    ``defer``: -> a callable finishing the plan (its host sync) later."""
+    One host sync (the counts); ``_device_layout`` plans need none."""
     dev = k.device
     n = k.shape[0]
     nb = (W << c) * n_groups
@@ -1680,21 +1611,17 @@ def _bucket_plan(k: torch.Tensor, W: int, group: torch.Tensor | None = None, n_g
     g, s = _ctx(k, keys)
     _call("dx_msm_keys", g, s, _ptr(k.contiguous()), _ptr(grp), gstride, n, c, W, _ptr(keys),  # dx_rpmsm.hip
           _ptr(item))
-    item, counts_f = _sort_buckets(keys, item, nb, defer)   # zero digits carry a sentinel key that sorts last
-
-    def finish():
-        counts = _cget(counts_f)
-        it = item[: int(counts.sum())].to(torch.int64)                  # drop the zero-digit sentinels
-        bk = np.flatnonzero(counts)
-        passes = _segment_passes_dev(counts[bk], dev)
-        # bucket digits and scatter slots, staged now so the run needs no host->device copy
-        mask = (1 << c) - 1
-        sc = torch.zeros((bk.size, 8), dtype=torch.int32)
-        sc[:, 0] = torch.from_numpy((bk & mask).astype("int32"))
-        slot = torch.from_numpy((bk & mask) * W + (bk >> c))
-        return {"item": it, "passes": passes, "bk": bk, "single": not passes,
-                "digit_sc": _upload(sc.numpy(), dev), "slot": _upload(slot.numpy(), dev), "W": W, "c": c}
-    return finish if defer else finish()
+    item, counts = _sort_buckets(keys, item, nb)   # zero digits carry a sentinel key that sorts last
+    it = item[: int(counts.sum())].to(torch.int64)                  # drop the zero-digit sentinels
+    bk = np.flatnonzero(counts)
+    passes = _segment_passes_dev(counts[bk], dev)
+    # bucket digits and scatter slots, staged now so the run needs no host->device copy
+    mask = (1 << c) - 1
+    sc = torch.zeros((bk.size, 8), dtype=torch.int32)
+    sc[:, 0] = torch.from_numpy((bk & mask).astype("int32"))
+    slot = torch.from_numpy((bk & mask) * W + (bk >> c))
+    return {"item": it, "passes": passes, "bk": bk, "single": not passes,
+            "digit_sc": _upload(sc.numpy(), dev), "slot": _upload(slot.numpy(), dev), "W": W, "c": c}
 
 
 def _multi_exp64_run(a: torch.Tensor, plan) -> torch.Tensor:
@@ -1724,23 +1651,19 @@ def _multi_exp64_run(a: torch.Tensor, plan) -> torch.Tensor:
     return acc
 
 
-def multi_exp_plan(k: torch.Tensor, group, n_groups: int, W: int = _ME_W, c: int = 8, defer: bool = False):
-    """The bucket plan of ``multi_exp_grouped`` alone (its one host sync;
-    ``defer``: a callable that takes it later)."""
-    return _bucket_plan(k, W, group, n_groups, c, defer)
+def multi_exp_plan(k: torch.Tensor, group, n_groups: int, W: int = _ME_W, c: int = 8):
+    """The bucket plan of ``multi_exp_grouped`` alone (its one host sync)."""
+    return _bucket_plan(k, W, group, n_groups, c)
 
 
 def multi_exp_grouped(a: torch.Tensor, k: torch.Tensor, group, n_groups: int, W: int = _ME_W, c: int = 8,
-                      plan: dict | None = None, fold: int = 1, item_split: tuple | None = None):
+                      plan: dict | None = None, item_split: tuple | None = None):
     """Launch G independent multi-exponentiations prod_{i: group_i = g} a[i % n]^k_i
     (n = rows of a, k [m, 8] with m a multiple of n, low W c-bit windows of
     each exponent; ``group`` an int32 tensor or an int stride) as ONE bucket
     plan (one host sync for all groups, e.g. the batch weights of several
     verifying nodes).  Returns a handle for ``multi_exp_grouped_finish``;
-    device passes are queued on the current stream.  ``fold`` = k: the
-    ``n_groups`` plan groups are (group, segment) pairs g * k + s; the handle
-    finishes the n_groups / k groups (buckets combined over the segments) and
-    keeps the per-segment buckets for ``multi_exp_seg_finish``.
+    device passes are queued on the current stream.
     ``item_split`` = (s, q): entry i < s uses a[i % n], entry i >= s uses
     a[(i - s) % q] (two exponent blocks over different row periods)."""
     n = a.shape[0]
@@ -1753,88 +1676,14 @@ def multi_exp_grouped(a: torch.Tensor, k: torch.Tensor, group, n_groups: int, W:
     else:
         plan["item"] = (it % n).contiguous()
     bk = plan["bk"]
-    h = {"G": n_groups // fold, "W": W, "c": c, "win": None}
+    h = {"G": n_groups, "W": W, "c": c, "win": None}
     if bk.size == 0:
         return h
     cur = a.index_select(0, plan["item"]).contiguous() if plan["single"] else None
     for i, (st, ln) in enumerate(plan["passes"]):
         cur = gt_slice_prod(a if i == 0 else cur, plan["item"] if i == 0 else None, st, ln)
-    if fold > 1:
-        # per-(group, segment) buckets are kept for ``multi_exp_seg_finish``;
-        # the groups' results come from the buckets multiplied across segments
-        cur, bk, h["seg"] = _fold_buckets(cur, bk, W << c, fold, n_groups, gt_one(a.device), gt_slice_prod,
-                                          torch.int64)
-    _me_windows(h, cur, bk, n_groups // fold, W, c, a.device)
+    _me_windows(h, cur, bk, n_groups, W, c, a.device)
     return h
-
-
-_FOLD_IDX: dict = {}
-
-
-def _fold_buckets(cur, bk, per_group: int, fold: int, n_groups: int, fill_row, slice_op, idx_dtype):
-    """Buckets of the plan groups g * fold + s (keys bk, values cur) combined
-    over s into the groups g.  Dense and host-free: the values are scattered
-    into a [n_groups * per_group] image (empty buckets = the identity
-    ``fill_row``) and every group bucket reduces its ``fold`` strided rows in
-    one slice launch; the host only derives the non-empty group buckets from
-    the plan's own key list.  -> (values, keys of the non-empty group
-    buckets, kept image + mask for the per-segment finish)."""
-    dev = cur.device
-    G = n_groups // fold
-    nbt = n_groups * per_group
-    dense = fill_row.view(1, -1).expand(nbt, fill_row.numel()).contiguous()
-    dense.index_copy_(0, _upload(bk.astype(np.int64), dev), cur)
-    key = (G, per_group, fold, str(dev), idx_dtype)
-    if key not in _FOLD_IDX:
-        if len(_FOLD_IDX) > 16:
-            _FOLD_IDX.clear()
-        gj = torch.arange(G * per_group, device=dev, dtype=torch.int64)
-        g, j = gj // per_group, gj % per_group
-        idx = ((g.view(-1, 1) * fold + torch.arange(fold, device=dev).view(1, -1)) * per_group + j.view(-1, 1))
-        _FOLD_IDX[key] = (idx.reshape(-1).to(idx_dtype).contiguous(), gj * fold,
-                          torch.full((G * per_group,), fold, dtype=torch.int32, device=dev))
-    idx, start, ln = _FOLD_IDX[key]
-    red = slice_op(dense, idx, start, ln)
-    mask = np.zeros(nbt, dtype=bool)
-    mask[bk] = True
-    bk_red = np.flatnonzero(mask.reshape(G, fold, per_group).any(axis=1).reshape(-1))
-    vals = red.index_select(0, _upload(bk_red.astype(np.int64), dev)) if bk_red.size < red.shape[0] else red
-    return vals, bk_red, {"dense": dense, "mask": mask, "fold": fold, "per": per_group}
-
-
-def _seg_rows(keep: dict, groups: list):
-    """Rows of the kept image for the original groups ``groups`` (non-empty
-    buckets only) and their keys renumbered group-major: (position in groups)
-    * fold + s -> (rows, keys), keys sorted."""
-    per, fold = keep["per"], keep["fold"]
-    m = keep["mask"].reshape(-1, fold, per)
-    rows, keys = [], []
-    for i, g in enumerate(groups):
-        if g >= m.shape[0]:
-            continue
-        s_, j_ = np.nonzero(m[g])
-        rows.append((g * fold + s_) * per + j_)
-        keys.append((i * fold + s_) * per + j_)
-    if not rows:
-        return np.zeros(0, dtype=np.int64), np.zeros(0, dtype=np.int64)
-    return np.concatenate(rows), np.concatenate(keys)
-
-
-def multi_exp_seg_finish(h: dict, groups: list) -> torch.Tensor:
-    """Per-(group, segment) results of a ``multi_exp_grouped(..., fold=k)``
-    run for the original groups ``groups`` -> host [len(groups) * k, 96]
-    (group-major), from the kept buckets: no new plan, no re-bucketing."""
-    keep = h.get("seg")
-    W, c = h["W"], h["c"]
-    k = keep["fold"] if keep else 1
-    out = {"G": len(groups) * k, "W": W, "c": c, "win": None}
-    if keep is None:
-        return multi_exp_grouped_finish(out)
-    rows, nbk = _seg_rows(keep, groups)
-    if rows.size:
-        dense = keep["dense"]
-        _me_windows(out, dense.index_select(0, _upload(rows, dense.device)), nbk, len(groups) * k, W, c, dense.device)
-    return multi_exp_grouped_finish(out)
 
 
 def _me_windows(h: dict, cur, bk, n_groups: int, W: int, c: int, dev):
@@ -1870,6 +1719,207 @@ def multi_exp_grouped_finish(h) -> torch.Tensor:
     return acc
 
 
+# ----------------------------------------------------------------------------- device-resident bucket plans
+# The bucket plans above take ONE host sync each (the per-bucket counts decide
+# the slice passes).  A device-resident plan fixes its layout from the plan's
+# SHAPE instead: every bucket owns a number of lanes set by its window's
+# expected run (uniform digits: the batch weights are uniform), each lane
+# takes an equal share of the bucket's actual run (csrc/kernels/dx_plan.hip
+# dx_lane_slices), the multi-lane buckets reduce by a fixed tree and the
+# bucket weighting runs over a fixed set of buckets.  Nothing goes through the
+# host, so every pass is queued at once behind the sort.
+
+_DPLANS: dict = {}
+
+
+def _device_layout(groups: tuple, W: int, c: int, sl: int, dev) -> dict:
+    """Static layout of a device-resident plan (cached per shape).
+    ``groups`` = ((entries, scalar bits), ...) per group.  Window w of a group
+    with b = min(c, bits - w c) > 0 bits uses the buckets of digits 1 .. 2^b - 1,
+    each with ceil(entries / (2^b sl)) lanes; every other bucket keeps one lane
+    and must stay empty (``overflow`` counts entries that land there)."""
+    dev = torch.device(dev)
+    key = (groups, W, c, sl, str(dev))
+    lay = _DPLANS.get(key)
+    if lay is not None:
+        return lay
+    D = 1 << c
+    nb = len(groups) * W * D
+    lanes = np.ones(nb, dtype=np.int64)
+    used = np.zeros(nb, dtype=bool)
+    for g, (rows, bits) in enumerate(groups):
+        for w in range(W):
+            bw = min(c, int(bits) - w * c)
+            if bw <= 0:
+                continue
+            base, hi = (g * W + w) * D, 1 << bw
+            used[base + 1: base + hi] = True
+            lanes[base + 1: base + hi] = max(1, -(-int(rows) // (hi * sl)))
+    off = np.cumsum(lanes) - lanes
+    L = int(lanes.sum())
+    lane_bucket = np.repeat(np.arange(nb), lanes)
+    lane_j = np.arange(L) - off[lane_bucket]
+    multi = np.flatnonzero(lanes > 1)
+    passes = []
+    if multi.size:
+        # first level over the multi-lane buckets' lanes (in place in the lane
+        # array), then the usual segmented passes over the compacted results
+        c_ = lanes[multi]
+        n_sl = -(-c_ // _ME_SLICE)
+        b = np.repeat(np.arange(multi.size), n_sl)
+        k = np.arange(b.size) - (np.cumsum(n_sl) - n_sl)[b]
+        passes.append((off[multi][b] + k * _ME_SLICE, np.minimum(c_[b] - k * _ME_SLICE, _ME_SLICE)))
+        passes += _segment_passes(n_sl)
+    up = lambda a, dt: _upload(np.asarray(a).astype(dt), dev)  # noqa: E731
+    ubk = np.flatnonzero(used)
+    lay = {"nb": nb, "n_lanes": L, "W": W, "c": c, "used": ubk,
+           "lane_bucket": up(lane_bucket, np.int32), "lane_j": up(lane_j, np.int32), "lanes": up(lanes, np.int32),
+           "first_lane": up(off, np.int64), "multi": up(multi, np.int64),
+           "passes": [(up(st, np.int64), up(ln, np.int32)) for st, ln in passes],
+           "used_t": up(ubk, np.int64), "unused_t": up(np.flatnonzero(~used), np.int64)}
+    if len(_DPLANS) > 32:
+        _DPLANS.clear()
+    _DPLANS[key] = lay
+    return lay
+
+
+def _device_runs(k: torch.Tensor, group, n_groups: int, W: int, c: int):
+    """Bucket keys of every (entry, window) and their runs in key order, on
+    the device: (items sorted by key, first[nb], end[nb])."""
+    dev = k.device
+    n = k.shape[0]
+    nb = (W << c) * n_groups
+    assert n * W < 2 ** 31 and nb < 2 ** 31 - 1
+    keys = torch.empty(n * W, dtype=torch.int32, device=dev)
+    items = torch.empty(n * W, dtype=torch.int32, device=dev)
+    grp, gstride = _group_arg(group, n, dev)
+    g, s = _ctx(k, keys)
+    _call("dx_msm_keys", g, s, _ptr(k.contiguous()), _ptr(grp), gstride, n, c, W, _ptr(keys), _ptr(items))
+    return _sorted_runs(keys, items, nb)
+
+
+def _device_slices(first: torch.Tensor, end: torch.Tensor, lay: dict):
+    L = lay["n_lanes"]
+    st = torch.empty(L, dtype=torch.int64, device=first.device)
+    ln = torch.empty(L, dtype=torch.int32, device=first.device)
+    g, s = _ctx(first, st)
+    _call("dx_lane_slices", g, s, _ptr(first), _ptr(end), _ptr(lay["lane_bucket"]), _ptr(lay["lane_j"]),
+          _ptr(lay["lanes"]), L, _ptr(st), _ptr(ln))
+    return st, ln
+
+
+def _device_reduce(part: torch.Tensor, lay: dict, slice_op) -> torch.Tensor:
+    """Per-lane partials -> one value per USED bucket (``lay["used"]`` order)."""
+    B = part.index_select(0, lay["first_lane"])
+    if lay["passes"]:
+        cur = None
+        for i, (st, ln) in enumerate(lay["passes"]):
+            cur = slice_op(part if i == 0 else cur, st, ln)
+        B.index_copy_(0, lay["multi"], cur)
+    return B.index_select(0, lay["used_t"])
+
+
+def _overflow(first, end, lay) -> torch.Tensor:
+    """Entries in buckets outside the layout (scalars wider than declared): a device scalar."""
+    return (end - first).index_select(0, lay["unused_t"]).sum()
+
+
+def check_overflow(h: dict):
+    """Raise if a device-resident plan dropped entries (checked once the
+    results are read back, so it costs no extra host sync)."""
+    ov = h.get("overflow")
+    if ov is not None and int(ov) != 0:
+        raise RuntimeError(f"device bucket plan: {int(ov)} entries fell outside the declared scalar widths")
+
+
+def multi_exp_device(a: torch.Tensor, k: torch.Tensor, group, groups: tuple, W: int, c: int,
+                     item_split: tuple | None = None) -> dict:
+    """``multi_exp_grouped`` with a device-resident plan (no host sync):
+    ``groups`` = ((entries, exponent bits), ...) per group.  -> the handle of
+    ``multi_exp_grouped_finish``."""
+    dev = a.device
+    n = a.shape[0]
+    G = len(groups)
+    items, first, end = _device_runs(k, group, G, W, c)
+    it = items.to(torch.int64)
+    if item_split is not None:
+        sp, q = item_split
+        it = torch.where(it < sp, it % n, (it - sp) % q)
+    else:
+        it = it % n
+    lay = _device_layout(tuple(groups), W, c, _ME_SLICE, dev)
+    st, ln = _device_slices(first, end, lay)
+    part = gt_slice_prod(a, it.contiguous(), st, ln)
+    B = _device_reduce(part, lay, lambda src, s_, l_: gt_slice_prod(src, None, s_, l_))
+    h = {"G": G, "W": W, "c": c, "win": None, "overflow": _overflow(first, end, lay)}
+    if "me_win" not in lay:
+        bk = lay["used"]
+        D = 1 << c
+        dsc = np.zeros((bk.size, 8), dtype=np.int32)
+        dsc[:, 0] = bk & (D - 1)
+        gg, w, d = bk // (W * D), (bk >> c) % W, bk & (D - 1)
+        lay["me_win"] = (_upload(dsc, dev), _upload(d * (G * W) + gg * W + w, dev))
+    dsc, slot = lay["me_win"]
+    bkp = gt_pow(B, dsc)
+    D = 1 << c
+    win = gt_one(dev).repeat(D * G * W, 1)
+    win[slot] = bkp
+    win = win.view(D, G * W, 96)
+    if dev.type == "cuda":
+        while win.shape[0] > 32:
+            win = _gt_prod_level(win, 8)
+    h["win"] = win
+    return h
+
+
+def g2_msm_device(P_aff: torch.Tensor, k: torch.Tensor, group, groups: tuple, c: int = 13,
+                  bits: int = 254) -> tuple:
+    """``g2_msm_launch`` + ``g2_msm_run`` with a device-resident plan (no host
+    sync): out[g] = sum_{t: group_t = g} k_t P[t % m] -> ([G * W, 48] window
+    sums, handle for ``g2_msm_finish``)."""
+    dev = P_aff.device
+    m = _rows(P_aff, 32)
+    G = len(groups)
+    W = -(-bits // c)
+    items, first, end = _device_runs(k, group, G, W, c)
+    lay = _device_layout(tuple(groups), W, c, 32, dev)
+    st, ln = _device_slices(first, end, lay)
+    part = g2_slice_sum(P_aff, items, st, ln, True, m)
+    B = _device_reduce(part, lay, lambda src, s_, l_: g2_slice_sum(src, None, s_, l_, False))
+    if "g2w" not in lay:
+        lay["g2w"] = _g2_weight_plan(lay["used"], c, dev)
+    S = torch.zeros((G * W, 48), dtype=torch.int32, device=dev)
+    _g2_weigh(B, lay["g2w"], S)
+    return S, {"G": G, "W": W, "c": c, "overflow": _overflow(first, end, lay)}
+
+
+def g1_msm_device(P_jac: torch.Tensor, k: torch.Tensor, group, groups: tuple, bits: int = 256) -> dict:
+    """``g1_msm_launch`` with a device-resident plan (8-bit windows, no host
+    sync) -> the handle of ``g1_msm_finish``."""
+    dev = P_jac.device
+    G = len(groups)
+    W = (bits + 7) // 8
+    items, first, end = _device_runs(k, group, G, W, 8)
+    lay = _device_layout(tuple(groups), W, 8, _ME_SLICE, dev)
+    st, ln = _device_slices(first, end, lay)
+    part = g1_slice_sum(P_jac.contiguous(), items.to(torch.int64), st, ln)
+    B = _device_reduce(part, lay, lambda src, s_, l_: g1_slice_sum(src, None, s_, l_))
+    h = {"n_groups": G, "W": W, "S_w": None, "overflow": _overflow(first, end, lay)}
+    if "g1w" not in lay:
+        bk = lay["used"]
+        sc = np.zeros((bk.size, 8), dtype=np.int32)
+        sc[:, 0] = bk % 256
+        gws, counts = np.unique(bk // 256, return_counts=True)
+        lay["g1w"] = (_upload(sc, dev), [(_upload(st_, dev), _upload(ln_.astype("int32"), dev))
+                                         for st_, ln_ in _segment_passes(counts)], gws)
+    sc, wpasses, gws = lay["g1w"]
+    cur = g1_mul(B, sc)                                                  # d * B_{g,w,d}
+    for st_, ln_ in wpasses:
+        cur = g1_slice_sum(cur, None, st_, ln_)
+    h["S_w"], h["gws"] = cur, gws
+    return h
+
+
 def g1_slice_sum(src: torch.Tensor, idx, start: torch.Tensor, length: torch.Tensor) -> torch.Tensor:
     """out[s] = sum_k src[idx[start[s] + k]] (or src[start[s] + k]), k < length[s] (Jacobian)."""
     n = start.numel()
@@ -1899,28 +1949,25 @@ def g1_msm_grouped(P_jac: torch.Tensor, k: torch.Tensor, group: torch.Tensor | N
     return g1_msm_finish(g1_msm_launch(P_jac, k, group, n_groups, bits))
 
 
-def g1_msm_plan(k: torch.Tensor, group, n_groups: int, bits: int = 256, defer: bool = False):
+def g1_msm_plan(k: torch.Tensor, group, n_groups: int, bits: int = 256):
     """The bucket plan of ``g1_msm_launch`` alone (its one host sync), so a
-    caller can take every plan's sync before queueing any heavy pass
-    (``defer``: a callable that takes it later)."""
+    caller can take every plan's sync before queueing any heavy pass."""
     if not k.shape[0]:
-        return (lambda: None) if defer else None
-    return _bucket_plan(k, (bits + 7) // 8, group, n_groups, defer=defer)
+        return None
+    return _bucket_plan(k, (bits + 7) // 8, group, n_groups)
 
 
 def g1_msm_launch(P_jac: torch.Tensor, k: torch.Tensor, group: torch.Tensor | None, n_groups: int,
-                  bits: int = 256, plan: dict | None = None, fold: int = 1) -> dict:
+                  bits: int = 256, plan: dict | None = None) -> dict:
     """First half of g1_msm_grouped: the bucket plan (one host sync on k,
     unless ``plan`` comes from ``g1_msm_plan``) and every device pass, queued
     on the current stream.  g1_msm_finish waits for them and runs the Horner
-    steps on the host.  ``fold`` = k: plan groups are (group, segment) pairs
-    g * k + s, the handle finishes the n_groups / k groups and keeps the
-    per-segment buckets for ``g1_msm_seg_finish`` (as ``multi_exp_grouped``)."""
+    steps on the host."""
     assert P_jac.shape[0] == k.shape[0]
     assert group is None or isinstance(group, int) or group.numel() == k.shape[0]
     dev = P_jac.device
     W = (bits + 7) // 8
-    h = {"n_groups": n_groups // fold, "W": W, "S_w": None}
+    h = {"n_groups": n_groups, "W": W, "S_w": None}
     if P_jac.shape[0] == 0:
         return h
     if plan is None:
@@ -1932,28 +1979,8 @@ def g1_msm_launch(P_jac: torch.Tensor, k: torch.Tensor, group: torch.Tensor | No
     cur = P_jac.index_select(0, plan["item"]).contiguous() if plan["single"] else None
     for i, (st, ln) in enumerate(plan["passes"]):
         cur = g1_slice_sum(P_jac if i == 0 else cur, plan["item"] if i == 0 else None, st, ln)
-    if fold > 1:
-        from ..crypto.bn254 import g1_infinity_jac
-
-        cur, bk, h["seg"] = _fold_buckets(cur, bk, W << 8, fold, n_groups, g1_infinity_jac(1, dev).to(dev)[0],
-                                          g1_slice_sum, torch.int64)
     _g1_windows(h, cur, bk, dev)
     return h
-
-
-def g1_msm_seg_finish(h: dict, groups: list) -> torch.Tensor:
-    """Per-(group, segment) sums of a ``g1_msm_launch(..., fold=k)`` run for
-    the original groups ``groups`` -> host [len(groups) * k, 24], from the
-    kept buckets."""
-    keep = h.get("seg")
-    k = keep["fold"] if keep else 1
-    out = {"n_groups": len(groups) * k, "W": h["W"], "S_w": None}
-    if keep is not None:
-        rows, nbk = _seg_rows(keep, groups)
-        if rows.size:
-            dense = keep["dense"]
-            _g1_windows(out, dense.index_select(0, _upload(rows, dense.device)), nbk, dense.device)
-    return g1_msm_finish(out)
 
 
 def _g1_windows(h: dict, cur, bk, dev):
@@ -2074,7 +2101,7 @@ def g2_mul_small(jac: torch.Tensor, d: torch.Tensor) -> torch.Tensor:
 
 
 def g2_msm_launch(P_aff: torch.Tensor, k: torch.Tensor, group: torch.Tensor | None, n_groups: int,
-                  c: int = 13, bits: int = 254, first_slice: int = 32, defer: bool = False):
+                  c: int = 13, bits: int = 254, first_slice: int = 32):
     """Bucket plan of G independent G2 MSMs out[g] = sum_{t: group_t = g}
     k_t P[t % m] (m = rows of P_aff, k [n, 8] with n a multiple of m; group:
     int32 tensor, or an int stride s meaning group_t = t // s):
@@ -2092,29 +2119,36 @@ def g2_msm_launch(P_aff: torch.Tensor, k: torch.Tensor, group: torch.Tensor | No
     grp, gstride = _group_arg(group, n, dev)
     g, s = _ctx(k, keys)
     _call("dx_msm_keys", g, s, _ptr(k.contiguous()), _ptr(grp), gstride, n, c, W, _ptr(keys), _ptr(items))
-    items, counts_f = _sort_buckets(keys, items, nb, defer)             # the one host sync
+    items, counts = _sort_buckets(keys, items, nb)             # the one host sync
+    bk = np.flatnonzero(counts)
+    h = {"G": n_groups, "W": W, "c": c, "m": m, "bk": bk, "item": items[: int(counts.sum())]}
+    if bk.size:
+        passes = _segment_passes_dev(counts[bk], dev, first_slice)
+        if not passes:  # every bucket holds one entry
+            passes = [(torch.arange(bk.size, device=dev), torch.ones(bk.size, dtype=torch.int32, device=dev))]
+        h["passes"] = passes
+        h.update(_g2_weight_plan(bk, c, dev))
+    return h
 
-    def finish():
-        counts = _cget(counts_f)
-        bk = np.flatnonzero(counts)
-        h = {"G": n_groups, "W": W, "c": c, "m": m, "bk": bk, "item": items[: int(counts.sum())]}
-        if bk.size:
-            passes = _segment_passes_dev(counts[bk], dev, first_slice)
-            if not passes:  # every bucket holds one entry
-                passes = [(torch.arange(bk.size, device=dev), torch.ones(bk.size, dtype=torch.int32, device=dev))]
-            h["passes"] = passes
-            h.update(_g2_weight_plan(bk, c, dev))
-        return h
-    return finish if defer else finish()
+
+def _g2_chunk(n_buckets: int) -> int:
+    """Digit range of a bucket-weight chunk: 32 (about two additions per
+    bucket) while that still gives ~16k chunk lanes, shorter for a small
+    plan (a 1/8 pool slice: 8, i.e. 4x the lanes with a third of the chain)."""
+    ch = G2_CHUNK
+    while ch > 4 and n_buckets // ch < 16384:
+        ch //= 2
+    return ch
 
 
 def _g2_weight_plan(bk, c: int, dev) -> dict:
-    """Bucket weights by running sums over chunks of digit range G2_CHUNK
+    """Bucket weights by running sums over chunks of an aligned digit range
     (csrc/kernels/dx_rpmsm.hip chunk_weight_one), then per-window sums of the
     chunk results, for the sorted bucket keys ``bk``."""
+    chunk = _g2_chunk(bk.size)
     dig = bk & ((1 << c) - 1)
     gw = bk >> c
-    ck = gw * ((1 << c) // G2_CHUNK + 1) + dig // G2_CHUNK
+    ck = gw * ((1 << c) // chunk + 1) + dig // chunk
     first = np.flatnonzero(np.r_[True, ck[1:] != ck[:-1]])
     clen = np.diff(np.r_[first, bk.size])
     gwf = gw[first]                                  # sorted: run lengths instead of np.unique's sort
@@ -2122,7 +2156,7 @@ def _g2_weight_plan(bk, c: int, dev) -> dict:
     gws, gcounts = gwf[gstart], np.diff(np.r_[gstart, gwf.size])
     return {"d": _upload(dig.astype("int32"), dev),
             "chunks": (_upload(first.astype(np.int64), dev), _upload(clen.astype(np.int32), dev),
-                       _upload(((dig[first] // G2_CHUNK) * G2_CHUNK).astype(np.int32), dev)),
+                       _upload(((dig[first] // chunk) * chunk).astype(np.int32), dev)),
             "gws": _upload(gws.astype(np.int64), dev), "gpasses": _segment_passes_dev(gcounts, dev)}
 
 

@@ -822,7 +822,7 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
 
     ``segs`` (proof counts summing to len(r): the batch's per-request
     slices) asks for attribution: -> per VN a [bool] per segment, None when
-    a failed batch cannot be attributed (the "fold" verifier), or a
+    a failed batch cannot be attributed, or a
     ``RangeInvalid`` (per segment: decodes) when some proofs do not decode.  The U side is then laid out per segment
     (each segment's U_q start whole accumulation workgroups, so each has its
     own Miller partial products -- no extra pairing work), and only a VN
@@ -841,29 +841,10 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
     if r.zphi.shape[0] != n * l or r.zv.shape[0] != n * S * l or r.V.shape[0] != n * S * l \
             or r.A.shape[0] != n * S * l or r.challenge.shape[0] != n:
         return fail
-    # pairing side: "msm" regroups the product by bilinearity (one G2 MSM and
-    # n*S L-point combinations per VN, n*S + 1 Miller loops); "fold"
-    # (DRYNX_RPV=fold) runs one Miller loop per item, as the reference's
-    # per-equation check
-    use_msm = os.environ.get("DRYNX_RPV", "msm") == "msm"
-    # attribution: the bucket methods group every entry by (VN, segment) and
-    # sum / multiply the buckets over the segments before weighting them, so
-    # the per-VN checks cost the same, and a failing VN's per-segment values
-    # come from the kept buckets (no second plan, no re-bucketing)
-    # (DRYNX_SEG_KEEP=1; off by default: folding costs the clean path ~9 ms of a
-    # ~200 ms query for ~40 ms on a failing one, profiles/r4/ab_plan_sort.txt)
-    fold = nseg if (segs is not None and nseg > 1 and use_msm
-                    and os.environ.get("DRYNX_SEG_KEEP", "0") == "1") else 1
-    # D-check sums (sum w c C', sum w D) per VN: for a small batch (a pool
-    # helper's 1/W slice) without a bucket plan -- c C' once for every VN (on
-    # the validation stream, beside the U side), then each VN's 32-bit GLV
-    # ladders and a chunked tree sum, no host sync (the plan's sort and sync
-    # cost a 1/8 slice ~5 ms of wall); a full inbox keeps the bucket MSM, whose
-    # device time is lower (1.6 against 4.2 ms at 20,700 proofs x 3 VNs,
-    # profiles/r4/span_kernels_serialized.txt).  DRYNX_DCHECK=direct|msm forces one.
+    # pairing side regrouped by bilinearity: one G2 MSM and n*S L-point
+    # combinations per VN, n*S + 1 Miller loops (``_msm_queue``)
     dmode = os.environ.get("DRYNX_DCHECK", "auto")
-    ddirect = fold == 1 and (dmode == "direct" or (dmode == "auto" and device.type == "cuda"
-                                                   and n * n_vn <= _DCHECK_DIRECT_MAX))
+    ddirect = dmode == "direct" or (dmode == "auto" and device.type == "cuda" and n * n_vn <= _DCHECK_DIRECT_MAX)
     cC = ev_cC = None
     with timers.span("rp.verify.validate"):
         # On a GPU the checks run on their own stream, filling the gaps the
@@ -886,13 +867,13 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
                     ev_cC.record(vstream)
         else:
             valid = validate_list(r, mode, lazy=True, per_proof=pp)
-            if not bool(valid.all()) and (segs is None or not use_msm):
+            if not bool(valid.all()) and segs is None:
                 return _invalid(valid, segs, n_vn)
     if mode >= 1:
         with timers.span("rp.verify.challenge"):
             ch_ok = (challenges(r.commit.C, r.cols, sigmat, device, mode, r.D, r.V, r.A, S, l)
                      == r.challenge).all(dim=1)
-            if segs is None or not use_msm:
+            if segs is None:
                 if not bool(ch_ok.all()):
                     return _invalid(ch_ok, segs, n_vn)
             else:
@@ -905,9 +886,6 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
     if any(r.offset):
         Cp = nt.g1_add(Cp, nt.g1_fb_mul_i64(tabB, bn.h2d(torch.tensor(r.offset, dtype=torch.int64), device)))
     z = nt.fr_dot_rows(r.zphi, _powers(u, l, device), n, b_periodic=True)   # sum_j Zphi_j u^j
-    # Zphi B: the per-item G1 side of the "fold" verifier only (the regrouped
-    # "msm" verifier folds Zphi into its R-MSM scalars)
-    ZB = None if use_msm else nt.g1_fb_mul(tabB, r.zphi)              # [n*l]
     cols_t = bn.h2d(torch.tensor(r.cols, dtype=torch.long), device)
     y_idx = (torch.arange(S, device=device).view(1, S) * sigmat.n_cols + cols_t.view(n, 1)).reshape(-1)
     ytabs = sigmat.y_tables(device)
@@ -945,9 +923,8 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
     # ZERO weights -- every weighted sum then runs over the decodable proofs
     # only (their U_q and -c y_i become infinity, as the fold's padding), so
     # one bad payload costs no second pass: the batch verdict IS the verdict
-    # of the decodable segments (DRYNX_RP_MASK=0: the round-3 full
-    # segment pass of every VN)
-    masked = segs is not None and use_msm and os.environ.get("DRYNX_RP_MASK", "1") == "1"
+    # of the decodable segments
+    masked = segs is not None
     if masked:
         if vstream is not None:
             torch.cuda.current_stream(device).wait_stream(vstream)
@@ -963,104 +940,53 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
     _sw.__exit__(None, None, None)
     vns = [{"rho": rho_all[v * m:(v + 1) * m], "ab": ab_all[v * m:(v + 1) * m]} for v in range(G)]
     timers.count("rp.verify.items", G * m)
-    pseg = iseg = None
-    if fold > 1:
-        pseg = torch.repeat_interleave(torch.arange(nseg, device=device), _h2d(segs, device), output_size=n)
-        iseg = pseg.repeat_interleave(S * l)
+    # exponents of the GT multi-exponentiation: groups 0..G-1 prod a^rho_v =
+    # prod a^a' * frob^8(a)^b' (32-bit exponents over (A, frob^8 A)); groups
+    # G..2G-1 each VN's own GT-membership combination prod a^gamma_v (over A)
+    abv = ab_all.view(G, m, 2)
+    k = torch.zeros((3 * G * m, 8), dtype=torch.int32, device=device)
+    kr = k[: 2 * G * m].view(G, 2 * m, 8)
+    kr[:, :m, 0] = abv[:, :, 0]
+    kr[:, m:, 0] = abv[:, :, 1]
+    k[2 * G * m:] = gam_all
+    gv = torch.arange(G, device=device, dtype=torch.int32)
+    mgrp = torch.cat([gv.repeat_interleave(2 * m), G + gv.repeat_interleave(m)])
+    me_groups = ((2 * m, 32),) * G + ((m, gb),) * G
+    # GPU: 11-bit windows (3 per 32-bit half, 4 for the 40-bit combinations);
+    # host: bytes (fewer buckets for the host's serial bucket products)
+    wc_ = (4, 11) if device.type == "cuda" else (5, 8)
+    # R-MSM scalars rho_it Zphi_(p, j) (periodic over the VNs)
+    it = torch.arange(m, device=device)
+    s_r = nt.fr_arith(nt.FR_MUL, rho_all, r.zphi.index_select(0, (it // (S * l)) * l + it % l).contiguous())
+    if not ddirect:
+        dpts = torch.cat([Cp.contiguous(), r.D.contiguous()]).repeat(G, 1)
+        wc = nt.fr_arith(nt.FR_MUL, w_all, r.challenge)
+        dsc = torch.stack([wc.view(G, n, 8), w_all.view(G, n, 8)], 1).reshape(-1, 8).contiguous()
     aux = _aux_stream(device) if device.type == "cuda" else None
-    defer = aux is not None
-    # the bucket plans' keys and sorts go FIRST, on the high-priority aux
-    # stream, with their counts copied back asynchronously; then the U side
-    # (no plan, no sync) fills this stream; then the host takes the plans'
-    # syncs -- which then wait for the short sort kernels only, not behind the
-    # long U-side launches (a 1/8 pool slice waited ~9 ms for its R plan)
+    ready = None
     if aux is not None:
-        aux.wait_stream(torch.cuda.current_stream(device))
-    with timers.span("rp.verify.plan_start"), (torch.cuda.stream(aux) if aux is not None else _nullctx()):
-        if use_msm and aux is not None:
-            with timers.span("rp.plan.R"):
-                hR_f = _msm_plan(r.zphi, r.V, rho_all, G, n, S, l, defer=True)
-        if not ddirect:
-            dpts = torch.cat([Cp.contiguous(), r.D.contiguous()]).repeat(G, 1)
-            wc = nt.fr_arith(nt.FR_MUL, w_all, r.challenge)
-            dsc = torch.stack([wc.view(G, n, 8), w_all.view(G, n, 8)], 1).reshape(-1, 8).contiguous()
-        with timers.span("rp.plan.D"):
-            if ddirect:
-                dplan_f = None
-            elif fold > 1:  # group = ((v, which) row // n, segment of the proof)
-                dgrp = (torch.arange(2 * G, device=device).view(-1, 1) * fold
-                        + pseg.view(1, n)).reshape(-1).to(torch.int32)
-                dplan_f = nt.g1_msm_plan(dsc, dgrp, 2 * G * fold, defer=defer)
-            else:
-                dgrp = n
-                dplan_f = nt.g1_msm_plan(dsc, n, 2 * G, defer=defer)     # group = row // n
-        # groups 0..G-1: prod a^rho_v; groups G..2G-1: each VN's own GT-membership
-        # combination prod a^gamma_v
-        # prod a^rho = prod a^a' * frob^8(a)^b': 32-bit exponents over (A, frob^8 A)
-        abv = ab_all.view(G, m, 2)
-        if fold > 1:
-            k = torch.zeros((2 * G, 2 * m, 8), dtype=torch.int32, device=device)
-            k[:G, :m, 0] = abv[:, :, 0]
-            k[:G, m:, 0] = abv[:, :, 1]
-            k[G:, :m] = gam_all.view(G, m, 8)
-            k = k.view(-1, 8)
-        else:
-            # [rho rows: G x 2m over (A, frob^8 A) | gamma rows: G x m over A] --
-            # no all-zero half for the combinations (a quarter fewer plan keys)
-            k = torch.zeros((3 * G * m, 8), dtype=torch.int32, device=device)
-            kr = k[: 2 * G * m].view(G, 2 * m, 8)
-            kr[:, :m, 0] = abv[:, :, 0]
-            kr[:, m:, 0] = abv[:, :, 1]
-            k[2 * G * m:] = gam_all
-            gv = torch.arange(G, device=device, dtype=torch.int32)
-            mgrp = torch.cat([gv.repeat_interleave(2 * m), G + gv.repeat_interleave(m)])
-        # GPU: 11-bit windows (3 per 32-bit half, 4 for the 40-bit combinations);
-        # host: bytes (fewer buckets for the host's serial bucket products)
-        wc_ = (4, 11) if device.type == "cuda" else (5, 8)
-        with timers.span("rp.plan.ME"):
-            if fold > 1:  # group = (row // 2m, segment of the item)
-                mgrp = (torch.arange(2 * G, device=device).view(-1, 1) * fold
-                        + iseg.repeat(2).view(1, 2 * m)).reshape(-1).to(torch.int32)
-                mplan_f = nt.multi_exp_plan(k, mgrp, 2 * G * fold, W=wc_[0], c=wc_[1], defer=defer)
-            else:
-                mplan_f = nt.multi_exp_plan(k, mgrp, 2 * G, W=wc_[0], c=wc_[1], defer=defer)
-    if aux is not None:
-        if use_msm:
-            with timers.span("rp.verify.msm_queue"):
-                msq = _msm_queue(Y, r.V, ab_all, G, n, S, l, vstream, segs)
-                for v, uok in zip(vns, msq["u_ok"]):
-                    v["u_ok"] = uok
-        else:
-            with timers.span("rp.verify.fold_queue"):
-                for v, fb in zip(vns, _miller_fold_multi(ZB, Y, [v["rho"] for v in vns], r.V, S, l,
-                                                           [v["ab"] for v in vns])):
-                    v["fb"] = fb
-    with timers.span("rp.verify.plans"), (torch.cuda.stream(aux) if aux is not None else _nullctx()):
-        # every plan's host sync first, then every pass: a sync never waits
-        # behind another plan's heavy passes
-        with timers.span("rp.plan.sync"):
-            if use_msm and aux is not None:
-                hR = hR_f()
-            dplan = dplan_f() if callable(dplan_f) else dplan_f
-            mplan = mplan_f() if callable(mplan_f) else mplan_f
-        rs = _run_stream(device) if aux is not None and os.environ.get("DRYNX_RUN_SPLIT", "0") == "1" else None
-        if rs is not None:
-            rs.wait_stream(aux)  # the plans (and everything they read) are queued; the ME pass is not yet
+        ready = torch.cuda.Event()
+        ready.record(torch.cuda.current_stream(device))
+        # the U side first, on this stream: its chain of Miller-loop kernels is
+        # the critical path of a small batch (a pool slice)
+        with timers.span("rp.verify.msm_queue"):
+            msq = _msm_queue(Y, r.V, ab_all, G, n, S, l, vstream, segs)
+            for v, uok in zip(vns, msq["u_ok"]):
+                v["u_ok"] = uok
+        aux.wait_event(ready)
+    # the R MSM, the multi-exponentiation and the D-check on the aux stream
+    # with device-resident bucket plans: no host sync, every pass queued now
+    # (a plan's host sync used to wait ~6-9 ms behind the U side)
+    with timers.span("rp.verify.passes"), (torch.cuda.stream(aux) if aux is not None else _nullctx()):
+        with timers.span("rp.run.R"):
+            S_R, hR = nt.g2_msm_device(r.V, s_r, m, ((m, 254),) * G, c=_r_window(m, G))
         with timers.span("rp.frob8"):  # (A, frob^8 A) stacked: the Frobenius image written in place
             A2 = torch.empty((2 * m, 96), dtype=torch.int32, device=device)
             nt.batched_copy([(r.A.contiguous(), A2[:m])])
             nt.gt_frob8(r.A.contiguous(), out=A2[m:])
         with timers.span("rp.run.ME"):
-            if fold > 1:
-                mexp = nt.multi_exp_grouped(A2, k, mgrp, 2 * G * fold, W=wc_[0], c=wc_[1], plan=mplan, fold=fold)
-            else:
-                mexp = nt.multi_exp_grouped(A2, k, mgrp, 2 * G, W=wc_[0], c=wc_[1], plan=mplan,
-                                            item_split=(2 * G * m, m))
-        split = torch.cuda.stream(rs) if rs is not None else _nullctx()
-        if use_msm and aux is not None:
-            with timers.span("rp.run.R"), split:
-                S_R = nt.g2_msm_run(r.V, hR)                           # R window sums
-        with timers.span("rp.run.D"), (torch.cuda.stream(rs) if rs is not None else _nullctx()):
+            mexp = nt.multi_exp_device(A2, k, mgrp, me_groups, wc_[0], wc_[1], item_split=(2 * G * m, m))
+        with timers.span("rp.run.D"):
             if ddirect:
                 if cC is None:                                                 # host path
                     cC = nt.g1_mul(Cp.contiguous(), r.challenge.contiguous())
@@ -1071,49 +997,30 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
                 # item-major [n, 2G]: group v * 2 + which, summed over the proofs
                 dcheck = nt.g1_sum(nt.g1_mul_glv(pts.contiguous(), abs_.contiguous()).view(n, 2 * G, 24))
             else:
-                dcheck = nt.g1_msm_launch(dpts, dsc, dgrp, 2 * G * fold, bits=256, plan=dplan, fold=fold)
+                dcheck = nt.g1_msm_device(dpts, dsc, n, ((n, 254),) * (2 * G))     # group = row // n
         e_all = nt.fr_dot_rows(rho_all, r.zv, G, b_periodic=True)                        # sum rho Zv per VN
         dfull = torch.stack([nt.fr_dot_rows(w_all, r.zr, G, b_periodic=True),
                              nt.fr_dot_rows(w_all, z, G, b_periodic=True)], 1)             # [G, 2, 8]
-    if device.type == "cuda":
-        with timers.span("rp.verify.multiexp"):
+    if aux is None:  # host: the U side after the passes
+        msq = _msm_queue(Y, r.V, ab_all, G, n, S, l, None, segs)
+        for v, uok in zip(vns, msq["u_ok"]):
+            v["u_ok"] = uok
+    with timers.span("rp.verify.multiexp"):
+        if aux is not None:
             run_idle_tasks()  # host work queued by the caller, in the GPU's busiest window
-            if rs is not None:
-                aux.wait_stream(rs)
             aux.synchronize()                                          # aux results are read on this stream/host
-            GG = nt.multi_exp_grouped_finish(mexp)                     # [2G, 96]: prod a^rho_v, prod a^gamma_v
-            D_all = dcheck.cpu() if ddirect else nt.g1_msm_finish(dcheck)  # [2G, 24]
-            e_all, dfull = e_all.cpu(), dfull.cpu()
-        with timers.span("rp.verify.fold_wait"):
-            if use_msm:
-                useg = _seg_products(msq)                              # [G, nseg, 96] host
-                for k_, v in enumerate(vns):
-                    v["F"] = nt.gt_prod(useg[k_].view(nseg, 1, 96), chunk=64).view(1, 96)
-            else:
-                for v in vns:
-                    v["F"] = nt._finish_prod_on_host(v["fb"])
-            if use_msm:
-                fR, rok = _msm_r_miller(hR, S_R)
-                for v, f, ok in zip(vns, fR, rok):
-                    v["F"], v["r_ok"] = nt.gt_mul(v["F"], f.view(1, 96)), ok
-    else:
-        GG = nt.multi_exp_grouped_finish(mexp)
-        if use_msm:
-            hR = _msm_plan(r.zphi, r.V, rho_all, G, n, S, l)
-            msq = _msm_queue(Y, r.V, ab_all, G, n, S, l, None, segs)
-            fR, rok = _msm_r_miller(hR, nt.g2_msm_run(r.V, hR))
-            useg = _seg_products(msq)
-            for k_, (v, f, ok, uok) in enumerate(zip(vns, fR, rok, msq["u_ok"])):
-                v["F"] = nt.gt_mul(nt.gt_prod(useg[k_].view(nseg, 1, 96), chunk=64).view(1, 96), f.view(1, 96))
-                v["r_ok"], v["u_ok"] = ok, uok
-        else:
-            T = _fold_points(ZB, Y, S, l)
-            for v in vns:
-                f = nt.miller_loop(nt.g1_to_affine(nt.g1_mul(T, v["rho"])), r.V)
-                v["F"] = nt.gt_prod(f.view(-1, 1, 96), chunk=4).view(1, 96)
-    if device.type != "cuda":
+        GG = nt.multi_exp_grouped_finish(mexp)                         # [2G, 96]: prod a^rho_v, prod a^gamma_v
         D_all = dcheck.cpu() if ddirect else nt.g1_msm_finish(dcheck)  # [2G, 24]
+        for h_ in (mexp, hR) if ddirect else (mexp, hR, dcheck):
+            nt.check_overflow(h_)
         e_all, dfull = e_all.cpu(), dfull.cpu()
+    with timers.span("rp.verify.fold_wait"):
+        useg = _seg_products(msq)                                      # [G, nseg, 96] host
+        for k_, v in enumerate(vns):
+            v["F"] = nt.gt_prod(useg[k_].view(nseg, 1, 96), chunk=64).view(1, 96)
+        fR, rok = _msm_r_miller(hR, S_R)
+        for v, f, ok in zip(vns, fR, rok):
+            v["F"], v["r_ok"] = nt.gt_mul(v["F"], f.view(1, 96)), ok
     for k, v in enumerate(vns):
         v.update(G=GG[k: k + 1], dfull=dfull[k], e=e_all[k: k + 1], dcheck=D_all[2 * k: 2 * k + 2])
     if vstream is not None:
@@ -1121,7 +1028,7 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
     if chk is not None:
         valid = valid & chk
     if vstream is not None:
-        if not bool(valid.all()) and (segs is None or not use_msm):
+        if not bool(valid.all()) and segs is None:
             return _invalid(valid, segs, n_vn)
     out = []
     # prime-order part of the a_ij: each VN's own independent 40-bit
@@ -1166,7 +1073,6 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
         with timers.span("rp.verify.segments"):
             x = dict(A2=A2, rho=rho_all, ab=ab_all, gam=gam_all, w=w_all, Cp=Cp, z=z, useg=useg, u_seg=msq["u_seg"],
                      PB_base=PB_base, gt_tab=gt_tab, wc=wc_, G=G,
-                     kept=dict(mexp=mexp, dcheck=dcheck) if fold > 1 else None,
                      # undecodable proofs in an UNMASKED batch: the first pass's GT
                      # combination included a_ij not known to be cyclotomic, so it
                      # bounds nothing -- every segment then gets its own combination
@@ -1174,7 +1080,7 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
                      tot=dict(lhs=[v.get("lhs") for v in vns], e=e_all, GGgam=GG[G: 2 * G],
                               dl=[v.get("dl") for v in vns], dr=[v["dcheck"][1:2] for v in vns],
                               r_ok=[bool(v.get("r_ok", True)) for v in vns]))
-            if x["kept"] is None and os.environ.get("DRYNX_SEG_HINT", "1") == "1" and (masked or seg_valid is None):
+            if masked or seg_valid is None:
                 per = _attribute_hinted(r, segs, redo, x)
             else:
                 per = _segment_pass(r, segs, redo, x)
@@ -1235,18 +1141,6 @@ class _nullctx:
 
 
 _DCHECK_DIRECT_MAX = 16384  # proofs x VNs up to which the D-check runs without a bucket plan
-
-
-def _msm_plan(zphi, V, rho_all, G: int, n: int, S: int, L: int, defer: bool = False):
-    """Verifier mode "msm", step 1 (one host sync): the R-MSM bucket plan of
-    every VN, R_v = sum_it (rho_it Zphi_(p, j)) V_it (``defer``: a callable
-    taking the sync later)."""
-    dev = V.device
-    m = n * S * L
-    it = torch.arange(m, device=dev)
-    zi = (it // (S * L)) * L + it % L
-    s_r = nt.fr_arith(nt.FR_MUL, rho_all, zphi.index_select(0, zi).contiguous())  # periodic over the VNs
-    return nt.g2_msm_launch(V, s_r, m, G, c=_r_window(m, G), defer=defer)  # group (VN) = row // m
 
 
 def _r_window(m: int, G: int) -> int:
@@ -1325,7 +1219,12 @@ def _msm_queue(Y, V, ab_all, G: int, n: int, S: int, L: int, vstream=None, segs:
             out["u_ok"] = list(out["u_seg"].all(dim=1).unbind(0))
         Ud.record_stream(vs)
         with timers.span("rp.u.fold"):
-            out["fb"] = nt.rp_fold_accum_n(nt.rp_fold_ncoeffs(Uall), UV, Uall, period, 1, K)
+            img = nt.rp_fold_ncoeffs(Uall)
+            if K == 1 and G * pad <= _COOP_MAX_ITEMS:
+                # a small batch (a pool slice): three lanes per item fill 3x the SIMDs
+                out["fb"] = nt.rp_fold_accum_coop(img, UV, Uall, period, 1)
+            else:
+                out["fb"] = nt.rp_fold_accum_n(img, UV, Uall, period, 1, K)
         out["blk"] = pad // rows
         out["sb"] = [0] if nseg == 1 else (segbase // rows).tolist()
         out["nb"] = [pad // rows] if nseg == 1 else (ac // rows).tolist()
@@ -1447,7 +1346,7 @@ def _segment_hinted(r: RangeProofList, segs: list, v: int, T: list, x: dict):
               ab=sel(x["ab"], 2, iidx), gam=sel(x["gam"], 8, iidx), w=sel(x["w"], 8, pidx),
               Cp=x["Cp"].index_select(0, pidx), z=x["z"].index_select(0, pidx),
               useg=x["useg"][v: v + 1, T], u_seg=x["u_seg"][v: v + 1].index_select(1, Tt),
-              PB_base=x["PB_base"], gt_tab=x["gt_tab"], wc=x["wc"], G=1, kept=None, m_first=[x["m_first"][v]])
+              PB_base=x["PB_base"], gt_tab=x["gt_tab"], wc=x["wc"], G=1, m_first=[x["m_first"][v]])
     comp = {}
     perT = _segment_pass(rT, [segs[s] for s in T], [0], xT, comp)[0]
     if all(perT):
@@ -1498,8 +1397,6 @@ def _segment_pass(r: RangeProofList, segs: list, redo: list, x: dict, comp: dict
         return torch.cat([t[v * w:(v + 1) * w] for v in redo]) if Gf > 1 else t[redo[0] * w:(redo[0] + 1) * w]
 
     rho, ab, w = rows(x["rho"], m), rows(x["ab"], m), rows(x["w"], n)
-    if x.get("kept") is not None:
-        return _segment_finish_kept(r, segs, redo, x, rows, pseg, poff, K)
     # every input and every bucket plan (one host sync each) first, then the
     # device passes: a plan's sync then never waits behind another MSM's
     # queued passes (the first pass's schedule)
@@ -1572,61 +1469,6 @@ def _segment_pass(r: RangeProofList, segs: list, redo: list, x: dict, comp: dict
     return out
 
 
-def _segment_finish_kept(r: RangeProofList, segs: list, redo: list, x: dict, rows, pseg, poff, K: int) -> dict:
-    """``_segment_pass`` from the first pass's kept per-(VN, segment)
-    buckets: the failing VNs' multi-exponentiation and D-check values per
-    segment are finished from buckets already on the device
-    (nt.multi_exp_seg_finish, g1_msm_seg_finish: no plan, no re-bucketing);
-    the G2 R side is re-bucketed per segment (its per-segment buckets would
-    be nseg x the first pass's), then Horner steps, Miller loops of B with R,
-    final exponentiations and exponent sums."""
-    dev = r.V.device
-    n, nseg, Gf, G = len(r), len(segs), len(redo), x["G"]
-    kept = x["kept"]
-    rho, w = rows(x["rho"], n * r.S * r.l), rows(x["w"], n)
-    m = n * r.S * r.l
-    # R_(v,s) = sum_{it in s} rho_it Zphi_(p,j) V_it: the one side re-bucketed
-    # per segment (a G2 plan kept per segment would hold nseg x the buckets)
-    it = torch.arange(m, device=dev)
-    zi = (it // (r.S * r.l)) * r.l + it % r.l
-    s_r = nt.fr_arith(nt.FR_MUL, rho, r.zphi.index_select(0, zi).contiguous())
-    iseg = pseg.repeat_interleave(r.S * r.l)
-    grp = (torch.arange(Gf, device=dev).view(Gf, 1) * nseg + iseg.view(1, m)).reshape(-1).to(torch.int32)
-    with timers.span("rp.seg.plans"):
-        hh = nt.g2_msm_launch(r.V, s_r, grp, K, c=_seg_c(Gf * m, K))
-    S_R = nt.g2_msm_run(r.V, hh)
-    with timers.span("rp.seg.kept_windows"):
-        Dk = nt.g1_msm_seg_finish(kept["dcheck"], [g for v in redo for g in (2 * v, 2 * v + 1)])
-    offs = torch.from_numpy((np.arange(Gf).reshape(Gf, 1) * n + poff[:-1].reshape(1, nseg)).reshape(-1))
-    offs = bn.h2d(torch.cat([offs, torch.tensor([Gf * n])]), dev)
-    e = nt.fr_seg_sum(nt.fr_dot_rows(rho, r.zv.repeat(Gf, 1).contiguous(), Gf * n), offs)
-    dzr = nt.fr_seg_sum(nt.fr_arith(nt.FR_MUL, w, r.zr.contiguous()), offs)
-    dz = nt.fr_seg_sum(nt.fr_arith(nt.FR_MUL, w, x["z"].contiguous()), offs)
-    with timers.span("rp.seg.gt_finish"):
-        GG = nt.multi_exp_seg_finish(kept["mexp"], list(redo))                 # [K, 96] prod a^rho per (v, s)
-        if any(not x["m_first"][v] for v in redo):
-            m_ok = _gt_in_subgroup_each(nt.multi_exp_seg_finish(kept["mexp"], [G + v for v in redo]))
-        else:  # the first pass's combination bounds every a_ij already
-            m_ok = [True] * K
-    with timers.span("rp.seg.r_finish"):
-        fR, rok = _msm_r_miller(hh, S_R)
-    D_all = Dk.view(Gf, 2, nseg, 24)
-    e, dzr, dz = e.cpu(), dzr.cpu(), dz.cpu()
-    useg = torch.stack([x["useg"][v] for v in redo]).view(K, 96)
-    useg_ok = x["u_seg"].cpu()[redo].reshape(-1).tolist()
-    with timers.span("rp.seg.final_exp"):
-        lhs = nt.gt_mul(nt.final_exp(nt.gt_mul(useg.contiguous(), fR.contiguous())), GG.contiguous())
-    eq = nt.gt_eq(lhs, nt.gt_fb_pow(x["gt_tab"], e)).tolist()
-    PB = nt.g1_mul(x["PB_base"].repeat(K, 1), torch.stack([dzr, dz], 1).reshape(-1, 8).contiguous()).view(K, 2, 24)
-    lhs_d = nt.g1_sum(torch.stack([D_all[:, 0].reshape(K, 24), PB[:, 0], PB[:, 1]]).contiguous())
-    d_ok = nt.g1_eq(lhs_d.contiguous(), D_all[:, 1].reshape(K, 24).contiguous()).tolist()
-    out = {}
-    for f, v in enumerate(redo):
-        out[v] = [bool(eq[f * nseg + s_]) and bool(d_ok[f * nseg + s_]) and bool(useg_ok[f * nseg + s_])
-                  and bool(rok[f * nseg + s_]) and m_ok[f * nseg + s_] for s_ in range(nseg)]
-    return out
-
-
 def _msm_r_miller(hR, S_dev) -> torch.Tensor:
     """Host tail of the R side: Horner over the window sums (one core per VN
     beats one GPU lane at this serial chain) and ML(B, R_v) -> ([G, 96] host,
@@ -1638,14 +1480,6 @@ def _msm_r_miller(hR, S_dev) -> torch.Tensor:
     if bool(inf.any()):
         f[inf] = nt.gt_one("cpu")
     return f, [bool(x) for x in nt.g2_subgroup(R).tolist()]
-
-
-def _fold_points(ZB, Y, S: int, L: int) -> torch.Tensor:
-    """T_it = ZB[p*L + j] - Y[p*S + i] for every item it = (p*S + i)*L + j (Jacobian)."""
-    npj = ZB.shape[0] // L
-    zb = ZB.view(npj, 1, L, 24).expand(npj, S, L, 24).reshape(-1, 24)
-    yy = Y.view(npj, S, 1, 24).expand(npj, S, L, 24).reshape(-1, 24)
-    return nt.g1_add(zb.contiguous(), yy.contiguous(), subtract=True)
 
 
 def fold_k(n_items: int, slots: int = 2048) -> int:
@@ -1662,29 +1496,9 @@ def fold_k(n_items: int, slots: int = 2048) -> int:
     return best_k
 
 
-def _miller_fold_multi(ZB, Y, rhos: list, V, S: int, L: int, abs_: list) -> list:
-    """GPU, verifier mode "fold" (the per-item Miller product, as the
-    reference's per-equation check): for each verifier's GLV weights, the
-    per-workgroup partial products of ML(rho_it (ZB[p,j] - Y[p,i]), V_it).
-    The line coefficients depend on V only, so they are computed ONCE for all
-    verifiers, normalised to 1 + (a u) w + (b v) w^3 (``rp_fold_ncoeffs``;
-    csrc/kernels/fold_body.h); each verifier's points (fused gather,
-    difference, 32-bit GLV ladder, affine -> (x/y, 1/y)) fill its block of a
-    shared image padded to whole accumulation workgroups, and ONE K-item
-    accumulation folds every verifier (a verifier's slice of a multi-GPU
-    node is too short to fill the chip on its own)."""
-    m = V.shape[0]
-    G = len(rhos)
-    K = fold_k(G * m)
-    per = 64 * K * nt.FOLD_P_ALIGN
-    pad = -(-m // per) * per
-    UV = torch.zeros((G * pad, 16), dtype=torch.int32, device=V.device)
-    for v in range(G):
-        nt.rp_fold_points_glv(ZB, Y, abs_[v], S, L, out=UV[v * pad: v * pad + m], uv=True)
-    fb = nt.rp_fold_accum_n(nt.rp_fold_ncoeffs(V.contiguous()), UV, V.contiguous(), pad, G, K)
-    blk = pad // (64 * K)
-    return [fb[v * blk:(v + 1) * blk] for v in range(G)]
-
+# U-side items up to which the accumulation runs three lanes per item (one
+# item per lane would leave most SIMDs idle; 43008 items = 2048 coop waves)
+_COOP_MAX_ITEMS = 43008
 
 _aux: dict = {}
 _val: dict = {}
@@ -1701,16 +1515,6 @@ def _aux_stream(device):
     key = str(device)
     if key not in _aux:
         # plans: short kernels overtake the pairing side
-        _aux[key] = torch.cuda.Stream(device, priority=streams.priority(-1))
-    return _aux[key]
-
-
-def _run_stream(device):
-    """Second pass stream (DRYNX_RUN_SPLIT=1): the R-MSM and D-check passes
-    beside the GT multi-exponentiation instead of behind it -- a pool part's
-    1/8 slice leaves each of them too few workgroups to fill the chip."""
-    key = ("run", str(device))
-    if key not in _aux:
         _aux[key] = torch.cuda.Stream(device, priority=streams.priority(-1))
     return _aux[key]
 

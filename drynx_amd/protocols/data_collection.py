@@ -13,7 +13,6 @@ xGMI, and each CN sums its DPs with the K5 reduction kernel.
 from __future__ import annotations
 
 import itertools
-import os
 import time
 import zlib
 
@@ -238,7 +237,7 @@ def data_collection(ctx, sq) -> tuple:
     # thousands (ScaleDPs, one record each) the syncs serialise the encoders
     sync_timer = len(local_dps) <= 16
     batchable = sq.Query.Operation.NameOp in enc.BATCH_OPS + ("logistic regression",)
-    if local_dps and batchable and os.environ.get("DRYNX_DP_BATCH", "1") != "0":
+    if local_dps and batchable:
         # every DP of this rank in one batch; each DP's encoding latency is the batch's
         with timers.timed("DPencodingBatch", sync=sync_timer) as t:
             batch = dp_encode_batch(ctx, sq, local_dps)

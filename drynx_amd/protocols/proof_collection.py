@@ -211,7 +211,7 @@ def pool_verify_ranges(ctx, sq, reqs: list, vns: list, comm=None, arrived: float
     # beside this rank's pool part (their own thread and stream: the part's
     # latency-bound kernels leave the GPU room), not after the gather
     exp_f = _expected_async(ctx, sq, reqs, vn_idxs, local_vns, W, parts) \
-        if local_vns and W > 1 and os.environ.get("DRYNX_DIGEST_ASYNC", "1") == "1" else None
+        if local_vns and W > 1 else None
     res, digests = prq.verify_range_pool_part(reqs, vn_idxs, sq, ctx.device, ctx.verifier_cache, parts[k],
                                               part_coins, async_digests=True)
     if hasattr(digests, "result"):
@@ -335,12 +335,7 @@ def _pool_async(ctx, sq, reqs, vns, comm=None):
     if ctx.device.type != "cuda":
         return ctx._pool_exec.submit(pool_verify_ranges, ctx, sq, reqs, vns, comm, arrived)
     if not hasattr(ctx, "_pool_stream"):
-        # DRYNX_POOL_RESERVE_CUS=k: the pool's heavy kernels (long-running
-        # workgroups) leave k CUs to the short plan / per-CN-proof launches
-        from .. import native as nt
-
-        k = int(os.environ.get("DRYNX_POOL_RESERVE_CUS", "0"))
-        ctx._pool_stream = nt.cu_masked_stream(ctx.device, k) if k > 0 else torch.cuda.Stream(ctx.device)
+        ctx._pool_stream = torch.cuda.Stream(ctx.device)
     side, main = ctx._pool_stream, torch.cuda.current_stream(ctx.device)
     side.wait_stream(main)
 

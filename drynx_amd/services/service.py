@@ -144,12 +144,9 @@ class DrynxNode:
         them in the reference RangeProofListBytes layout (proofs/range_wire.py)."""
         out: list = [None] * len(reqs)
         fresh: dict = {}
-        skip = os.environ.get("DRYNX_LEDGER_RANGE", "on") == "off"  # A/B runs only
         for i, req in enumerate(reqs):
             if req.header_only or req.tensor is None or req._data is not None:
                 out[i] = req.payload()
-            elif skip and req.kind == "range":
-                out[i] = b""
             else:
                 fresh.setdefault(req.digest().hex(), []).append(i)
         if not fresh:
@@ -252,8 +249,8 @@ class DrynxNode:
         checks) launches run on a HIGH-priority stream, so the dispatcher hands
         them the next free CU slots instead of queueing them behind the
         long-running workgroups of the range prover / verifier, which keep
-        normal-priority streams (DRYNX_HP_STREAM=0 turns this off)."""
-        if self.device.type != "cuda" or os.environ.get("DRYNX_HP_STREAM", "1") == "0":
+        normal-priority streams."""
+        if self.device.type != "cuda":
             return self._run_survey(sq, on_result)
         if not hasattr(self, "_hp_stream"):
             self._hp_stream = torch.cuda.Stream(self.device, priority=streams.priority(-1))
@@ -338,20 +335,16 @@ class DrynxNode:
             n_out = per
         timers.end_timer(t_exec)
         client_future = None
-        # the querier decodes beside the VNs' checks; it starts once the CN
-        # proofs the VNs check first are signed (DRYNX_CLIENT_EARLY=1: at once):
-        # its decryption kernels otherwise hold the CUs the signing's short
-        # launches wait for, on the step's critical path
-        client_early = os.environ.get("DRYNX_CLIENT_EARLY", "0") == "1"
-        if on_result is not None and result is not None and client_early:
-            client_future = self._submit_client(on_result, SurveyResult(sq.SurveyID, result, n_groups, n_out))
         # the last CN phase's proofs (key switching) are still being finished:
         # the VNs check every other proof first (pcp.proof_collection ``late``)
-        late_f = (proofs.pop() if proofs and hasattr(proofs[-1], "result")
-                  and os.environ.get("DRYNX_PROOF_STAGES", "2") == "2" else None)
+        late_f = proofs.pop() if proofs and hasattr(proofs[-1], "result") else None
         with timers.span("cn.proofs.wait"):
             proofs = self._resolve_proofs(proofs)
-        if on_result is not None and result is not None and not client_early:
+        # the querier decodes beside the VNs' checks; it starts once the CN
+        # proofs the VNs check first are signed: its decryption kernels would
+        # otherwise hold the CUs the signing's short launches wait for, on the
+        # step's critical path
+        if on_result is not None and result is not None:
             client_future = self._submit_client(on_result, SurveyResult(sq.SurveyID, result, n_groups, n_out))
         if range_future is not None:
             proofs.extend(range_future.result())
@@ -607,11 +600,7 @@ class DrynxNode:
         # switching: short latency-bound launches) overlap it on the GPU instead
         # of queueing behind ~20 ms of range-proof kernels
         if not hasattr(self, "_prove_stream"):
-            # DRYNX_PROVE_RESERVE_CUS=k: the prover leaves k CUs to the CN phases
-            k = int(os.environ.get("DRYNX_PROVE_RESERVE_CUS", "0"))
-            from .. import native as nt
-
-            self._prove_stream = nt.cu_masked_stream(self.device, k) if k > 0 else torch.cuda.Stream(self.device)
+            self._prove_stream = torch.cuda.Stream(self.device)
         side, main = self._prove_stream, torch.cuda.current_stream(self.device)
         side.wait_stream(main)  # the DP ciphertexts / randomness are ready
         with torch.cuda.stream(side):

@@ -140,9 +140,7 @@ def test_lr_encode_many_matches_single(gpu_device):
         assert torch.equal(many[i], lr.encode_coefficients_int(X, y, lp))
 
 
-@pytest.mark.parametrize("rpv", ["msm", "fold"])
-def test_range_proofs_gpu(gpu_device, rpv, monkeypatch):
-    monkeypatch.setenv("DRYNX_RPV", rpv)
+def test_range_proofs_gpu(gpu_device):
     from drynx_amd.crypto import elgamal as eg
     from drynx_amd.ops.encoding import CreateProofBatch
     from drynx_amd.proofs import range_proof as rp
@@ -339,26 +337,6 @@ def test_fold_points_match_g1_ops(gpu_device, variant):
     assert torch.equal(got, want)
 
 
-def test_merged_multi_verifier_fold(gpu_device):
-    """Several verifiers' folds over one shared normalised coefficient image
-    == each verifier's fold on its own (after the final exponentiation)."""
-    from drynx_amd.proofs import range_proof as rp
-
-    S, L, npj = 3, 4, 7
-    ZB = nt.g1_fb_mul(bn.base_table(gpu_device), bn.random_scalars(npj * L, gpu_device))
-    Y = nt.g1_fb_mul(bn.base_table(gpu_device), bn.random_scalars(npj * S, gpu_device))
-    m = npj * S * L
-    V = nt.g2_fb_mul(bn.base2_table(gpu_device), bn.random_scalars(m, gpu_device))
-    ws = [nt.glv_weights(m, gpu_device) for _ in range(3)]
-    merged = rp._miller_fold_multi(ZB, Y, [w[1] for w in ws], V, S, L, [w[0] for w in ws])
-    for (ab, rho), fb in zip(ws, merged):
-        P = nt.rp_fold_points(ZB, Y, rho, S, L)
-        alone = nt.rp_fold_accum(nt.rp_fold_lines(P, V), m, 1)
-        a = nt.final_exp(nt._finish_prod_on_host(fb))
-        b = nt.final_exp(nt._finish_prod_on_host(alone))
-        assert bool(nt.gt_eq(a, b).all())
-
-
 def test_int_moments_gpu_matches_host(gpu_device):
     """K14 on gfx950 vs the host path: one 1e5-record DP split over many
     workgroups, thousands of one-record DPs, empty DPs, and the widest pair
@@ -445,8 +423,6 @@ def test_gpu_ops_match_oracle(gpu_device):
 def test_glv_points_match_host(gpu_device):
     """GLV point kernel == affine((a + b lambda)(ZB - Y)) computed with the
     host path's full-scalar multiplication, incl. T at infinity."""
-    from drynx_amd.proofs import range_proof as rp
-
     S, L, npj = 2, 3, 9
     ZB = nt.g1_fb_mul(bn.base_table(gpu_device), bn.random_scalars(npj * L, gpu_device))
     Y = nt.g1_fb_mul(bn.base_table(gpu_device), bn.random_scalars(npj * S, gpu_device))
@@ -454,7 +430,9 @@ def test_glv_points_match_host(gpu_device):
     m = npj * S * L
     ab, rho = nt.glv_weights(m, gpu_device)
     got = nt.rp_fold_points_glv(ZB, Y, ab, S, L).cpu()
-    T = rp._fold_points(ZB.cpu(), Y.cpu(), S, L)
+    zb = ZB.cpu().view(npj, 1, L, 24).expand(npj, S, L, 24).reshape(-1, 24).contiguous()
+    yy = Y.cpu().view(npj, S, 1, 24).expand(npj, S, L, 24).reshape(-1, 24).contiguous()
+    T = nt.g1_add(zb, yy, subtract=True)
     exp = nt.g1_to_affine(nt.g1_mul(T, rho.cpu()))
     assert torch.equal(got, exp)
 
@@ -480,3 +458,24 @@ def test_normalised_fold_matches_shared_v(gpu_device, K):
         a = nt.final_exp(nt._finish_prod_on_host(got[v * blk:(v + 1) * blk]))
         b = nt.final_exp(nt._finish_prod_on_host(ref[v * blk:(v + 1) * blk]))
         assert bool(nt.gt_eq(a, b).all()), v
+
+
+def test_ufold_coop_matches_one_lane(gpu_device):
+    """The three-lanes-per-item U-side accumulation (dx_ufold_coop.hip) ==
+    the one-lane rp_accum_n kernel block by block (exact Fp12 products, no
+    final exponentiation needed), with points / V at infinity and padding."""
+    m, G = 700, 2
+    period = -(-m // (64 * nt.FOLD_P_ALIGN)) * 64 * nt.FOLD_P_ALIGN
+    V = nt.g2_fb_mul(bn.base2_table(gpu_device), bn.random_scalars(m, gpu_device))
+    V[7] = 0
+    P = torch.zeros((G * period, 16), dtype=torch.int32, device=gpu_device)
+    for v in range(G):
+        Pv = nt.g1_to_affine(nt.g1_fb_mul(bn.base_table(gpu_device), bn.random_scalars(m, gpu_device)))
+        Pv[11 + v] = 0
+        P[v * period: v * period + m] = Pv
+    UV = nt.g1_aff_to_uv_(P)
+    img = nt.rp_fold_ncoeffs(V)
+    ref = nt.rp_fold_accum_n(img, UV, V, period, G, 1)
+    got = nt.rp_fold_accum_coop(img, UV, V, period, G)
+    assert got.shape == ref.shape
+    assert bool(nt.gt_eq(got.cpu(), ref.cpu()).all())

@@ -36,7 +36,8 @@ def test_two_ranks_on_device(gpu_device):
     assert len(ranks) == 2 and all(r["bytes_recv"] > 0 and r["bytes_sent"] > 0 for r in ranks)
     # pooled range checks: both ranks checked a slice for every VN
     assert all(r["pool_range_items"] > 0 for r in ranks)
-    assert sum(r["pool_range_items"] for r in ranks) == d2["config"]["range_proof"]["verifications_per_query"]
+    assert sum(r["pool_range_items"] for r in ranks) == \
+        d2["config"]["range_proof"]["verifications_per_query"] * d2["steps"]
     # sharded GLS-8 prover tables: bit-identical to the one-rank build
     assert {r["table_digest"] for r in ranks} == {d1["ranks"][0]["table_digest"]}
     # node-shared ledger payloads and every VN's proofs readable

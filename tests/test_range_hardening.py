@@ -197,7 +197,6 @@ def test_v_with_small_torsion_rejected_by_regrouped_verifier(setup, monkeypatch)
     a random combination unless the weights cancel it mod 10069)."""
     import random
 
-    monkeypatch.setenv("DRYNX_RPV", "msm")
     sm, P = setup[4], setup[5]
     rpl = _prove(setup, [3, 5])
     assert rp.verify_range_proof_list(rpl, sm, P, mode=0)

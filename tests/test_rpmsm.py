@@ -1,8 +1,10 @@
 """Range-proof verification by bilinearity (verifier mode "msm",
 csrc/kernels/dx_rpmsm.hip): the G2 joint table, the L-point combinations
 U, the Pippenger G2 MSM and the regrouped pairing product, each against the
-pure-Python oracle (host path here, the gfx950 kernels under -m gpu), and the
-"msm" verifier against the per-item "fold" verifier on the same proofs."""
+pure-Python oracle (host path here, the gfx950 kernels under -m gpu), the
+device-resident bucket plans (no host sync) against the oracle, and the
+regrouped pairing product against the per-item Miller product on the same
+proofs."""
 import random
 
 import pytest
@@ -100,6 +102,86 @@ def test_g2_msm_grouped(device, c):
         assert got[g * stride + off] == want, g
 
 
+@pytest.mark.parametrize("device", DEVICES)
+@pytest.mark.parametrize("skew", [False, True])
+def test_g2_msm_device_plan(device, skew):
+    """Device-resident plan (csrc/kernels/dx_plan.hip dx_lane_slices): lanes
+    per bucket fixed by the shape; skewed scalars (every entry in one bucket
+    per window) only lengthen the lanes' slices."""
+    dev = _dev(device)
+    m, G, c = 13, 2, 4
+    pts = _g2_points(m, 6)
+    pts[3] = None
+    V = bn.g2_aff_tensor(pts, dev)
+    rnd = random.Random(7)
+    ks = [(0x123456789 if skew else rnd.randrange(O.R)) for _ in range(G * m)]
+    ks[5] = 0
+    S, h = nt.g2_msm_device(V, bn.scalars_tensor(ks, dev), m, ((m, 254),) * G, c=c)
+    got = bn.g2_points_from_aff(nt.g2_msm_finish(S.cpu(), h).cpu())
+    nt.check_overflow(h)
+    for g in range(G):
+        want = None
+        for t in range(m):
+            if pts[t] is not None:
+                want = O.g2_add(want, O.g2_mul(ks[g * m + t], pts[t]))
+        assert got[g] == want, g
+
+
+@pytest.mark.parametrize("device", DEVICES)
+def test_multi_exp_and_g1_msm_device_plans(device):
+    """GT multi-exponentiation (two groups of different exponent widths,
+    two row periods) and the G1 MSM with device-resident plans against the
+    oracle; an exponent wider than declared is reported, not dropped silently."""
+    dev = _dev(device)
+    rnd = random.Random(9)
+    n = 5
+    a_pts = [O.pairing(O.g1_mul(rnd.randrange(1, O.R), O.G1_GEN), O.G2_GEN) for _ in range(n)]
+    a = bn.gt_tensor(a_pts, dev)
+    e32 = [rnd.getrandbits(32) for _ in range(2 * n)]   # group 0: rows i < 2n over a[i % n]
+    e40 = [rnd.getrandbits(40) for _ in range(n)]       # group 1: rows over a[(i - 2n) % n]
+    k = torch.zeros((3 * n, 8), dtype=torch.int64)
+    for i, e in enumerate(e32 + e40):
+        k[i, 0], k[i, 1] = e & 0xffffffff, e >> 32
+    k = k.to(torch.int32).to(dev)
+    grp = torch.tensor([0] * (2 * n) + [1] * n, dtype=torch.int32, device=dev)
+    h = nt.multi_exp_device(a, k, grp, ((2 * n, 32), (n, 40)), 4, 11, item_split=(2 * n, n))
+    got = nt.multi_exp_grouped_finish(h)
+    nt.check_overflow(h)
+    def pw(x, e):
+        r, b = O.Fp12.one(), x
+        while e:
+            if e & 1:
+                r = r * b
+            b, e = b * b, e >> 1
+        return r
+
+    want0, want1 = O.Fp12.one(), O.Fp12.one()
+    for i in range(2 * n):
+        want0 = want0 * pw(a_pts[i % n], e32[i])
+    for i in range(n):
+        want1 = want1 * pw(a_pts[i], e40[i])
+    assert bn.gt_from_tensor(got.cpu()) == [want0, want1]
+    # an exponent wider than group 0's declared 32 bits
+    k2 = k.clone()
+    k2[0, 1] = 1
+    h2 = nt.multi_exp_device(a, k2, grp, ((2 * n, 32), (n, 40)), 4, 11, item_split=(2 * n, n))
+    nt.multi_exp_grouped_finish(h2)
+    with pytest.raises(RuntimeError, match="declared scalar widths"):
+        nt.check_overflow(h2)
+    # G1: two groups of 254-bit scalars
+    pts = [O.g1_mul(rnd.randrange(1, O.R), O.G1_GEN) for _ in range(6)]
+    ks = [rnd.randrange(O.R) for _ in range(12)]
+    P = bn.g1_jac_tensor(pts + pts, dev)
+    hd = nt.g1_msm_device(P, bn.scalars_tensor(ks, dev), 6, ((6, 254), (6, 254)))
+    got = nt.g1_msm_finish(hd)
+    nt.check_overflow(hd)
+    for g in range(2):
+        want = None
+        for t in range(6):
+            want = O.g1_add(want, O.g1_mul(ks[g * 6 + t], pts[t]))
+        assert bn.g1_points_from_jac(got[g: g + 1])[0] == want, g
+
+
 @pytest.fixture(scope="module")
 def proofs():
     S, u, l = 2, 4, 3
@@ -129,13 +211,18 @@ def test_msm_pairing_product_matches_per_item_fold(device, proofs, segs):
              + torch.tensor(r.cols, device=dev).view(n, 1)).reshape(-1)
     Y = nt.g1_mul(sm.y_jac.to(dev).index_select(0, y_idx).contiguous(), rp._rep(r.challenge, S))
     ab, rho = nt.glv_weights(G * m, dev)
-    hR = rp._msm_plan(r.zphi, r.V, rho, G, n, S, l)
+    it = torch.arange(m, device=dev)
+    s_r = nt.fr_arith(nt.FR_MUL, rho, r.zphi.index_select(0, (it // (S * l)) * l + it % l).contiguous())
+    S_R, hR = nt.g2_msm_device(r.V, s_r, m, ((m, 254),) * G, c=rp._r_window(m, G))
     q = rp._msm_queue(Y, r.V, ab, G, n, S, l, None, segs)
-    fR, _ = rp._msm_r_miller(hR, nt.g2_msm_run(r.V, hR))
+    fR, _ = rp._msm_r_miller(hR, S_R)
     useg = rp._seg_products(q)                            # per (VN, segment) U-side products
     k = len(segs) if segs else 1
     assert tuple(useg.shape) == (G, k, 96)
-    T = rp._fold_points(ZB.cpu(), Y.cpu(), S, l)
+    # T_it = Zphi_(p,j) B - Y_(p,i) for item it = (p S + i) L + j
+    zb = ZB.cpu().view(n, 1, l, 24).expand(n, S, l, 24).reshape(-1, 24)
+    yy = Y.cpu().view(n, S, 1, 24).expand(n, S, l, 24).reshape(-1, 24)
+    T = nt.g1_add(zb.contiguous(), yy.contiguous(), subtract=True)
     for v in range(G):
         F_msm = nt.gt_mul(nt.gt_prod(useg[v].view(k, 1, 96), chunk=4).view(1, 96), fR[v:v + 1])
         f = nt.miller_loop(nt.g1_to_affine(nt.g1_mul(T, rho[v * m:(v + 1) * m].cpu().contiguous())), r.V.cpu())
@@ -144,10 +231,8 @@ def test_msm_pairing_product_matches_per_item_fold(device, proofs, segs):
 
 
 @pytest.mark.parametrize("device", DEVICES)
-@pytest.mark.parametrize("mode", ["msm", "fold"])
-def test_both_verifier_modes_accept_and_reject(device, mode, proofs, monkeypatch):
+def test_verifier_accepts_and_rejects(device, proofs):
     dev = _dev(device)
-    monkeypatch.setenv("DRYNX_RPV", mode)
     rpl, sm, P = proofs
     assert rp.verify_range_proof_list_multi(rpl.to(dev), sm, P, 3, dev) == [True] * 3
     bad = rpl.to(dev)
@@ -191,26 +276,15 @@ def test_segment_attribution(device, field, proofs, monkeypatch):
         want = [True, True, False]
     decodes = field != "A_off_gt"
     calls, hinted = [], []
-    orig, orig_h = rp._segment_finish_kept, rp._segment_hinted
-    monkeypatch.setattr(rp, "_segment_finish_kept", lambda *a: calls.append(1) or orig(*a))
+    orig, orig_h = rp._segment_pass, rp._segment_hinted
+    monkeypatch.setattr(rp, "_segment_pass", lambda *a: calls.append(1) or orig(*a))
     monkeypatch.setattr(rp, "_segment_hinted", lambda *a: hinted.append(orig_h(*a)) or hinted[-1])
-    monkeypatch.setenv("DRYNX_SEG_KEEP", "1")
-    assert rp.verify_range_proof_list_multi(bad, sm, P, 2, dev, segs=[1, 2, 1]) == [want] * 2
-    # a proof that does not decode gets zero weights: the batch of the others
-    # passes, no second pass at all
-    assert bool(calls) == decodes, "the failing VNs' segments come from the first pass's kept buckets"
-    # the re-bucketing second pass (DRYNX_SEG_KEEP=0) names the same segments:
-    # the first failing VN's full pass, the others' from its hint
-    monkeypatch.setenv("DRYNX_SEG_KEEP", "0")
+    # the first failing VN's full segment pass, the others' verdicts from its
+    # hint; a proof that does not decode gets zero weights: the batch of the
+    # others passes, no second pass at all
     assert rp.verify_range_proof_list_multi(bad, sm, P, 3, dev, segs=[1, 2, 1]) == [want] * 3
-    assert len(calls) == int(decodes)
+    assert len(calls) == (3 if decodes else 0)       # one full pass + each hinted VN's pass over T
     assert len(hinted) == (2 if decodes else 0) and all(h == want for h in hinted)
-    monkeypatch.setenv("DRYNX_SEG_HINT", "0")
-    assert rp.verify_range_proof_list_multi(bad, sm, P, 2, dev, segs=[1, 2, 1]) == [want] * 2
-    monkeypatch.setenv("DRYNX_SEG_HINT", "1")
-    monkeypatch.setenv("DRYNX_RP_MASK", "0")                # round 3: every VN's segment pass
-    assert rp.verify_range_proof_list_multi(bad, sm, P, 2, dev, segs=[1, 2, 1]) == [want] * 2
-    monkeypatch.setenv("DRYNX_RP_MASK", "1")
     assert rp.verify_range_proof_list_multi(bad, sm, P, 2, dev) == [False] * 2
 
 
