@@ -171,3 +171,78 @@ extern "C" int dx_gt_slice_prod(int on_gpu, void *stream, const uint32_t *src, c
                      n_slices);
   return check_hip(hipGetLastError(), "gt_slice_prod");
 }
+
+// Bucket weights of a GT multi-exponentiation window by running products,
+// per chunk of buckets whose digits lie in one aligned range [base, base + L)
+// (the multiplicative form of dx_rpmsm.hip chunk_weight_one): with the
+// buckets sorted by digit, prod_i B_i^(d_i) = (prod_i B_i)^base * prod_t A_t,
+// A_t = prod_(d_i - base >= t) B_i for t = top .. 1 -- two products per bucket
+// plus one short power per chunk, instead of a d-th power of every bucket
+// (~16 products for an 11-bit digit).  Three lanes per chunk (gt_coop.h).
+namespace {
+__global__ void __launch_bounds__(64) DX_OCC gt_chunk_weight_coop(const uint32_t *B, const int32_t *d,
+                                                                 const int64_t *start, const int32_t *len,
+                                                                 const int32_t *base, uint32_t *out,
+                                                                 int64_t n_chunks) {
+  const coop::Role R = coop::role();
+  const int64_t ch = (int64_t)blockIdx.x * coop::kTriples + R.g;
+  if (R.g >= coop::kTriples || ch >= n_chunks) return;  // whole triples leave together
+  const Fp12 *F = reinterpret_cast<const Fp12 *>(B);
+  const int64_t a = start[ch];
+  const int n = len[ch];
+  const uint32_t b0 = (uint32_t)base[ch];
+  Fp6 acc = coop::one(R), tot = coop::one(R);
+  int i = n - 1;
+  for (int t = n > 0 ? (int)((uint32_t)d[a + i] - b0) : 0; t >= 1; t--) {
+    while (i >= 0 && (int)((uint32_t)d[a + i] - b0) == t) {
+      coop::mul(acc, coop::load(&F[a + i], false, R), R);
+      i--;
+    }
+    coop::mul(tot, acc, R);
+  }
+  for (; i >= 0; i--) coop::mul(acc, coop::load(&F[a + i], false, R), R);  // offset 0: weight base only
+  if (b0) {  // acc^base from the base's top bit
+    Fp6 m = acc;
+    for (int bit = 30 - __builtin_clz(b0); bit >= 0; bit--) {
+      coop::mul(m, m, R);
+      if ((b0 >> bit) & 1u) coop::mul(m, acc, R);
+    }
+    coop::mul(tot, m, R);
+  }
+  coop::store(&at<Fp12>(out, ch), tot, R);
+}
+}  // namespace
+
+extern "C" int dx_gt_chunk_weight(int on_gpu, void *stream, const uint32_t *B, const int32_t *d,
+                                  const int64_t *start, const int32_t *len, const int32_t *base, uint32_t *out,
+                                  int64_t n_chunks) {
+  if (n_chunks <= 0) return 0;
+  if (!on_gpu) {
+    host_for_each(n_chunks, [=](int64_t ch) {
+      const int64_t a = start[ch];
+      const int n = len[ch];
+      const uint32_t b0 = (uint32_t)base[ch];
+      Fp12 acc = Fp12::one(), tot = Fp12::one();
+      int i = n - 1;
+      for (int t = n > 0 ? (int)((uint32_t)d[a + i] - b0) : 0; t >= 1; t--) {
+        while (i >= 0 && (int)((uint32_t)d[a + i] - b0) == t) acc = mul(acc, at<Fp12>(B, a + i--));
+        tot = mul(tot, acc);
+      }
+      for (; i >= 0; i--) acc = mul(acc, at<Fp12>(B, a + i));
+      if (b0) {
+        Fp12 m = acc;
+        for (int bit = 30 - __builtin_clz(b0); bit >= 0; bit--) {
+          m = mul(m, m);
+          if ((b0 >> bit) & 1u) m = mul(m, acc);
+        }
+        tot = mul(tot, m);
+      }
+      at<Fp12>(out, ch) = tot;
+    });
+    return 0;
+  }
+  const unsigned blocks = (unsigned)((n_chunks + coop::kTriples - 1) / coop::kTriples);
+  hipLaunchKernelGGL(gt_chunk_weight_coop, dim3(blocks), dim3(64), 0, (hipStream_t)stream, B, d, start, len, base,
+                     out, n_chunks);
+  return check_hip(hipGetLastError(), "gt_chunk_weight");
+}

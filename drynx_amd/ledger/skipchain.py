@@ -157,9 +157,13 @@ def roster_json(identities) -> list:
     return out
 
 
-def new_data_block(survey_id: str, bitmap: dict, vn_identities, sample: float = 0.4) -> DataBlock:
-    """DataBlock as built by the root VN (Sample hard-coded to 0.4 in the reference, :115)."""
-    return DataBlock(roster_json(vn_identities), survey_id, sample, time.time(), len(vn_identities), dict(bitmap))
+def new_data_block(survey_id: str, bitmap: dict, vn_identities, sample: float = 0.4,
+                   t: float | None = None) -> DataBlock:
+    """DataBlock as built by the root VN (Sample hard-coded to 0.4 in the
+    reference, :115); ``t``: the root VN's timestamp (every rank builds the
+    same block from it)."""
+    return DataBlock(roster_json(vn_identities), survey_id, sample, time.time() if t is None else t,
+                     len(vn_identities), dict(bitmap))
 
 
 def make_block(prev: SkipBlock | None, data: DataBlock, vn_identities) -> SkipBlock:

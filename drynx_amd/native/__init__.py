@@ -103,6 +103,7 @@ _SIGS = {
     "dx_g1_mul_fast": [_P, _P, _P, _P, _L, _I, _I],
     "dx_rp_verify_fold": [_P, _P, _P, _P, _P, _P, _L, _I, _I],
     "dx_gt_slice_prod": [_I, _P, _P, _P, _P, _P, _P, _L],
+    "dx_gt_chunk_weight": [_I, _P, _P, _P, _P, _P, _P, _P, _L],
     "dx_g1_mul_glv": [_P, _P, _P, _P, _P, _L, _I],
     "dx_rp_u_joint_split": [_I, _P, _P, _P, _P, _L, _I, _I, _L, _I, _P],
     "dx_bucket_bounds": [_I, _P, _P, _L, _L, _P, _P],
@@ -1832,14 +1833,41 @@ def check_overflow(h: dict):
         raise RuntimeError(f"device bucket plan: {int(ov)} entries fell outside the declared scalar widths")
 
 
-def multi_exp_device(a: torch.Tensor, k: torch.Tensor, group, groups: tuple, W: int, c: int,
-                     item_split: tuple | None = None) -> dict:
+def gt_chunk_weight(B: torch.Tensor, d: torch.Tensor, start: torch.Tensor, length: torch.Tensor,
+                    base: torch.Tensor) -> torch.Tensor:
+    """out[ch] = prod_{i in chunk ch} B[i]^d[i] over digit-sorted GT buckets
+    (chunk: start/length rows whose digits lie in [base, base + L)) -- running
+    products instead of one power per bucket."""
+    n = start.numel()
+    out = torch.empty((n, 96), dtype=torch.int32, device=B.device)
+    g, s = _ctx(B, d, start, length, base)
+    _call("dx_gt_chunk_weight", g, s, _ptr(B.contiguous()), _ptr(d.contiguous()), _ptr(start), _ptr(length),
+          _ptr(base), _ptr(out), n)
+    return out
+
+
+def me_window(groups: tuple, lo: int = 8, hi: int = 16) -> tuple:
+    """(W, c) of a GT multi-exponentiation over ``groups`` = ((entries,
+    exponent bits), ...): c minimises the bucket products (entries x windows)
+    plus ~3 products per bucket for the running-product weights -> 16-bit
+    windows for a whole 1-GPU inbox (2 windows per 32-bit GLV half instead of
+    3), 11 bits for a pool slice."""
+    def cost(c):
+        return sum(r * -(-b // c) for r, b in groups) + 3 * sum(-(-b // c) for _, b in groups) * (1 << c)
+    c = min(range(lo, hi + 1), key=cost)
+    return max(-(-b // c) for _, b in groups), c
+
+
+def multi_exp_device(a: torch.Tensor, k: torch.Tensor, group, groups: tuple, W: int | None = None,
+                     c: int | None = None, item_split: tuple | None = None) -> dict:
     """``multi_exp_grouped`` with a device-resident plan (no host sync):
-    ``groups`` = ((entries, exponent bits), ...) per group.  -> the handle of
-    ``multi_exp_grouped_finish``."""
+    ``groups`` = ((entries, exponent bits), ...) per group (window from
+    ``me_window`` unless given).  -> the handle of ``multi_exp_grouped_finish``."""
     dev = a.device
     n = a.shape[0]
     G = len(groups)
+    if c is None:
+        W, c = me_window(tuple(groups))
     items, first, end = _device_runs(k, group, G, W, c)
     it = items.to(torch.int64)
     if item_split is not None:
@@ -1852,23 +1880,15 @@ def multi_exp_device(a: torch.Tensor, k: torch.Tensor, group, groups: tuple, W: 
     part = gt_slice_prod(a, it.contiguous(), st, ln)
     B = _device_reduce(part, lay, lambda src, s_, l_: gt_slice_prod(src, None, s_, l_))
     h = {"G": G, "W": W, "c": c, "win": None, "overflow": _overflow(first, end, lay)}
-    if "me_win" not in lay:
-        bk = lay["used"]
-        D = 1 << c
-        dsc = np.zeros((bk.size, 8), dtype=np.int32)
-        dsc[:, 0] = bk & (D - 1)
-        gg, w, d = bk // (W * D), (bk >> c) % W, bk & (D - 1)
-        lay["me_win"] = (_upload(dsc, dev), _upload(d * (G * W) + gg * W + w, dev))
-    dsc, slot = lay["me_win"]
-    bkp = gt_pow(B, dsc)
-    D = 1 << c
-    win = gt_one(dev).repeat(D * G * W, 1)
-    win[slot] = bkp
-    win = win.view(D, G * W, 96)
-    if dev.type == "cuda":
-        while win.shape[0] > 32:
-            win = _gt_prod_level(win, 8)
-    h["win"] = win
+    if "gtw" not in lay:
+        lay["gtw"] = _g2_weight_plan(lay["used"], c, dev)
+    wp = lay["gtw"]
+    cur = gt_chunk_weight(B, wp["d"], *wp["chunks"])                     # running products per chunk
+    for st, ln in wp["gpasses"]:
+        cur = gt_slice_prod(cur, None, st, ln)                            # chunks -> (group, window)
+    win = gt_one(dev).repeat(G * W, 1)
+    win[wp["gws"]] = cur
+    h["win"] = win.view(1, G * W, 96)
     return h
 
 
@@ -2142,9 +2162,10 @@ def _g2_chunk(n_buckets: int) -> int:
 
 
 def _g2_weight_plan(bk, c: int, dev) -> dict:
-    """Bucket weights by running sums over chunks of an aligned digit range
-    (csrc/kernels/dx_rpmsm.hip chunk_weight_one), then per-window sums of the
-    chunk results, for the sorted bucket keys ``bk``."""
+    """Bucket weights by running sums (G2) / running products (GT) over
+    chunks of an aligned digit range (csrc/kernels/dx_rpmsm.hip
+    chunk_weight_one, dx_range.hip gt_chunk_weight_coop), then per-window
+    sums of the chunk results, for the sorted bucket keys ``bk``."""
     chunk = _g2_chunk(bk.size)
     dig = bk & ((1 << c) - 1)
     gw = bk >> c

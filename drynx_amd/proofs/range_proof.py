@@ -257,12 +257,16 @@ class SigMaterial:
         bypasses the model."""
         if os.environ.get("DRYNX_PROVER_TABLE_BITS") is not None or getattr(self, "_host_ok", False):
             return True  # forced, or the tables are (being) built: using them is free
-        self._host_items = getattr(self, "_host_items", 0) + int(n_items if n_items is not None else n_points)
         need = int(os.environ.get("DRYNX_HOST_TABLE_MIN_USES", "64"))
-        ok = self._host_items >= need * max(1, self.n_distinct)
-        shard = getattr(self, "_shard", None)
-        if shard is not None:  # a sharded build is collective: every rank decides the same
-            ok = any(shard.all_gather_object(ok))
+        if getattr(self, "_shard", None) is not None:
+            # a sharded build is collective, so every rank must decide the same
+            # without a control round: count the set's proving batches (every
+            # rank proves once per query) instead of this rank's own items
+            self._host_calls = getattr(self, "_host_calls", 0) + 1
+            ok = self._host_calls >= need
+        else:
+            self._host_items = getattr(self, "_host_items", 0) + int(n_items if n_items is not None else n_points)
+            ok = self._host_items >= need * max(1, self.n_distinct)
         self._host_ok = ok
         return ok
 
@@ -952,9 +956,9 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
     gv = torch.arange(G, device=device, dtype=torch.int32)
     mgrp = torch.cat([gv.repeat_interleave(2 * m), G + gv.repeat_interleave(m)])
     me_groups = ((2 * m, 32),) * G + ((m, gb),) * G
-    # GPU: 11-bit windows (3 per 32-bit half, 4 for the 40-bit combinations);
-    # host: bytes (fewer buckets for the host's serial bucket products)
-    wc_ = (4, 11) if device.type == "cuda" else (5, 8)
+    # windows by cost (nt.me_window): 16 bits for a 1-GPU inbox, 11 for a pool
+    # slice; the host keeps bytes (fewer buckets for its serial products)
+    wc_ = nt.me_window(me_groups) if device.type == "cuda" else (5, 8)
     # R-MSM scalars rho_it Zphi_(p, j) (periodic over the VNs)
     it = torch.arange(m, device=device)
     s_r = nt.fr_arith(nt.FR_MUL, rho_all, r.zphi.index_select(0, (it // (S * l)) * l + it % l).contiguous())
@@ -1072,7 +1076,9 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
     if redo:
         with timers.span("rp.verify.segments"):
             x = dict(A2=A2, rho=rho_all, ab=ab_all, gam=gam_all, w=w_all, Cp=Cp, z=z, useg=useg, u_seg=msq["u_seg"],
-                     PB_base=PB_base, gt_tab=gt_tab, wc=wc_, G=G,
+                     # the segment pass keeps host-planned 11-bit windows (its groups are
+                     # (VN, segment) pairs: 16-bit windows would mean millions of buckets)
+                     PB_base=PB_base, gt_tab=gt_tab, wc=(4, 11) if device.type == "cuda" else wc_, G=G,
                      # undecodable proofs in an UNMASKED batch: the first pass's GT
                      # combination included a_ij not known to be cyclotomic, so it
                      # bounds nothing -- every segment then gets its own combination

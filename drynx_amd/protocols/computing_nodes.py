@@ -149,7 +149,7 @@ def key_switching(ctx, sq, agg, n_groups: int, n_out: int, noise, proofs: list):
                 prs = sigma.finish_keyswitch_proofs(pend)
                 return prq.new_proof_requests([("keyswitch", pr, cn.id, "", cn.keypair.secret)
                                                for cn, pr in zip(cns, prs)], sq.SurveyID)
-            proofs.append(ctx.defer_proofs(finish))
+            proofs.append(ctx.defer_proofs(finish, lane="_late"))
     total = ec.sum_to_root(ctx.comm, local_K, n_rows, root)
     if ctx.rank != root:
         return None

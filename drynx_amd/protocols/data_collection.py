@@ -21,6 +21,7 @@ import torch
 from ..crypto import elgamal as eg
 from ..ops import encoding as enc
 from ..parallel import ec_collectives as ec
+from ..query import lr_nbr_outputs
 from ..utils import timers
 
 
@@ -28,6 +29,19 @@ def all_possible_groups(group_by_values) -> list:
     """unlynx AllPossibleGroups: every combination of category indices."""
     vals = [int(v) for v in (group_by_values or [1])]
     return [list(g) for g in itertools.product(*[range(v) for v in vals])]
+
+
+def expected_n_out(sq) -> int | None:
+    """Ciphertexts per group every DP of the survey encodes, from the query
+    alone (None when it does not say): ranks hosting no DP size the CN phases
+    with it instead of asking the others (one control round fewer)."""
+    q = sq.Query
+    op = q.Operation
+    cf = max(1, q.CuttingFactor or 1)
+    if op.NameOp == "logistic regression":
+        p = op.LRParameters
+        return None if p is None else lr_nbr_outputs(p.NbrFeatures, p.K) * cf
+    return (op.NbrOutput // cf) * cf if op.NbrOutput > 0 else None
 
 
 def _seed(survey_id: str, dp_id: str) -> int:

@@ -109,6 +109,15 @@ def fan_out(ctx, sq, local_requests: list, pool: bool = False) -> list:
     W = ctx.comm.world
     vn_ranks = sorted({v.rank for v in vns})
     dests = list(range(W)) if pool else vn_ranks
+    seeds = {}
+    if pool:
+        # each local VN's per-survey seed for its pool helpers rides on this
+        # exchange (no control round of its own): helper k derives that VN's
+        # coins for its slice from it
+        seeds = {vn.id: ctx.vn_coins(vn.id).seed() for vn in vns if vn.rank == ctx.rank}
+        ctx.__dict__.setdefault("_pool_seeds", {})[sq.SurveyID] = seeds
+        if len(ctx._pool_seeds) > 64:
+            ctx._pool_seeds.pop(next(iter(ctx._pool_seeds)))
     if W == 1:
         return list(local_requests)
     per_rank = {d: [] for d in dests}
@@ -142,8 +151,13 @@ def fan_out(ctx, sq, local_requests: list, pool: bool = False) -> list:
                 per_rank_t[d].append(packed[idx])
             else:
                 per_rank[d].append(r.to_wire())
-    got = ctx.comm.exchange_bytes({d: obj_to_bytes(per_rank[d]) for d in dests if d != ctx.rank})
-    wires = {src: bytes_to_obj(b) for src, b in got.items()}
+    got = ctx.comm.exchange_bytes({d: obj_to_bytes({"w": per_rank[d], "seeds": seeds})
+                                   for d in dests if d != ctx.rank})
+    msgs = {src: bytes_to_obj(b) for src, b in got.items()}
+    wires = {src: m["w"] for src, m in msgs.items()}
+    if pool:
+        for m in msgs.values():
+            seeds.update(m["seeds"])
     tens = {d: t for d, t in zip([d for d in dests if per_rank_t[d]],
                                   nt.cat_rows([per_rank_t[d] for d in dests if per_rank_t[d]]))}
     # the envelopes announced every tensor's size: no size round for the payloads
@@ -192,17 +206,21 @@ def pool_verify_ranges(ctx, sq, reqs: list, vns: list, comm=None, arrived: float
     comm = comm or ctx.comm
     W, k = comm.world, comm.rank
     rng = [i for i, r in enumerate(reqs) if r.kind == "range" and not r.header_only]
-    local = {}
-    for vi, vn in enumerate(vns):
-        if vn.rank == ctx.rank:
-            c = ctx.vn_coins(vn.id)
-            local[vn.id] = ({reqs[i].base_key(): prq.should_verify(sq, reqs[i], vi, len(vns), c) for i in rng},
-                            c.seed())
-    sampled, seeds = {}, {}
-    for d in comm.all_gather_object(local):
-        for vid, (smp, seed) in d.items():
-            sampled[vid], seeds[vid] = smp, seed
-    vn_idxs = {vn.id: [i for i in rng if sampled[vn.id].get(reqs[i].base_key())] for vn in vns}
+    # every VN's seed arrived with the fan-out; the helpers check every list a
+    # VN may sample (the sharding extension's assignment is public; a random
+    # Threshold sample stays the VN's own decision, applied to the verdicts
+    # below) -- no control round before the checks
+    seeds = getattr(ctx, "_pool_seeds", {}).pop(sq.SurveyID, {})
+    missing = [vn.id for vn in vns if vn.id not in seeds]
+    if missing:
+        raise RuntimeError(f"pool: no fan-out seed for {missing} (survey {sq.SurveyID})")
+
+    def may_check(i, vi):
+        a_ = prq.assigned_vns(sq, reqs[i], len(vns))
+        return a_ is None or vi in a_
+    vn_idxs = {vn.id: [i for i in rng if may_check(i, vi)] for vi, vn in enumerate(vns)}
+    sampled = {vn.id: {reqs[i].base_key(): prq.should_verify(sq, reqs[i], vi, len(vns), ctx.vn_coins(vn.id))
+                       for i in rng} for vi, vn in enumerate(vns) if vn.rank == ctx.rank}
     part_coins = {vn.id: Coins(seeds[vn.id]).derive(("slice", k, W)) for vn in vns}
     parts = pool_parts(ctx, sq)
     t0 = arrived if arrived is not None else time.perf_counter()
@@ -466,10 +484,24 @@ def proof_collection(ctx, sq, local_requests: list, early: dict | None = None, l
     reqs = reqs + reqs2
     if getattr(ctx, "net", None) is not None:
         _net_proofs(ctx, sq, reqs, vns)
-    # bitmaps -> root VN (SharedBMChannel)
-    allbm = {}
-    for d in ctx.comm.all_gather_object(bitmaps):
-        allbm.update(d)
+    # bitmaps -> root VN (SharedBMChannel): every rank gets every VN's bitmap
+    # plus the root VN's block parameters (its timestamp; its chain head when
+    # it resumed from its ledger) and builds the same block itself -- no
+    # broadcast round for the block
+    root = vns[0]
+    mine = {"bm": bitmaps}
+    if ctx.rank == root.rank:
+        resumed = None
+        if ctx.last_block is None:
+            # resume an existing chain from the root VN's ledger (restart of a
+            # node over a persisted workdir) instead of starting a new genesis
+            ctx.last_block = ctx.get_latest_block(root.id)
+            resumed = ctx.last_block.to_bytes() if ctx.last_block is not None else None
+        mine["root"] = {"time": time.time(), "prev": resumed}
+    allbm, rootp = {}, None
+    for d in ctx.comm.all_gather_object(mine):
+        allbm.update(d["bm"])
+        rootp = d.get("root", rootp)
     if hasattr(ctx, "take_proof_starts"):
         # the VNs' verdicts are back on every DP's rank: the reference's
         # <dp>_AllProofs ends here (its proof collection's feedback channel,
@@ -477,21 +509,15 @@ def proof_collection(ctx, sq, local_requests: list, early: dict | None = None, l
         now = time.perf_counter()
         for dp_id, t_start in ctx.take_proof_starts(sq.SurveyID).items():
             timers.record(f"{dp_id}_AllProofs", now - t_start)
-    root = vns[0]
-    block = None
     t = timers.start_timer("BI", sync=False)
-    if ctx.rank == root.rank:
-        merged = {}
-        for vn in vns:
-            merged.update(allbm.get(vn.id, {}))
-        data = skc.new_data_block(sq.SurveyID, merged, [v.identity() for v in vns])
-        if ctx.last_block is None:
-            # resume an existing chain from the root VN's ledger (restart of a
-            # node over a persisted workdir) instead of starting a new genesis
-            ctx.last_block = ctx.get_latest_block(root.id)
-        block = skc.make_block(ctx.last_block, data, [v.identity() for v in vns])
-    block_bytes = ctx.comm.broadcast_object(block.to_bytes() if block is not None else None, src=root.rank)
-    block = skc.SkipBlock.from_bytes(block_bytes)
+    merged = {}
+    for vn in vns:
+        merged.update(allbm.get(vn.id, {}))
+    data = skc.new_data_block(sq.SurveyID, merged, [v.identity() for v in vns], t=rootp["time"])
+    prev = ctx.last_block
+    if rootp["prev"] is not None and ctx.rank != root.rank:
+        prev = skc.SkipBlock.from_bytes(rootp["prev"])
+    block = skc.make_block(prev, data, [v.identity() for v in vns])
     # every VN runs its verifiers (verifyFuncBitmap, VerifyBase against its own
     # latest block), then signs the block and the forward link from its latest
     signers = []

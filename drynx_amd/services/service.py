@@ -286,9 +286,15 @@ class DrynxNode:
         # on the GPU now, envelope marshalling + signing runs on a worker thread
         # while the CN phases below proceed
         range_future = self._range_proofs_async(sq, dp_results) if q.Proofs else None
+        want = dcp.expected_n_out(sq)
         if dp_results:
             n_out = len(next(iter(dp_results.values()))["cv"]) // n_groups
-        n_out = max(self.comm.all_gather_object(n_out if dp_results else 0)) or n_out
+            if want is not None and n_out != want:
+                raise ValueError(f"survey {sq.SurveyID}: DPs encoded {n_out} outputs, the query announces {want}")
+        if want is None:  # ranks without DPs learn the width from the others
+            n_out = max(self.comm.all_gather_object(n_out if dp_results else 0)) or n_out
+        else:
+            n_out = want
         early = None
         if range_future is not None and pcp.early_plane_ok(self, sq):
             # the range-proof plane starts now, beside the CN phases
@@ -402,22 +408,25 @@ class DrynxNode:
             cache[p] = torch.cuda.Stream(self.device, priority=streams.priority(p))
         return cache[p]
 
-    def defer_proofs(self, fn, *args):
+    def defer_proofs(self, fn, *args, lane: str = ""):
         """Run ``fn(*args) -> [ProofRequest]`` (proof finishing: transcript
         digests, responses, packing, envelope signatures -- each needs one
         device-to-host copy) on the node's CN-proof worker with its own HIP
         stream, ordered after the work queued so far; the query's critical
-        path does not wait for it.  -> Future (resolved before proof
-        collection)."""
+        path does not wait for it.  ``lane`` = "late": the last CN phase's
+        (key-switching) proofs get a worker and stream of their own, so their
+        transcript starts when the phase ends instead of queueing behind the
+        earlier phases' signing.  -> Future (resolved before proof collection)."""
         import concurrent.futures as cf
 
         if self.device.type != "cuda":
             fut = cf.Future()
             fut.set_result(fn(*args))
             return fut
-        if not hasattr(self, "_cnp_pool"):
-            self._cnp_pool = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="drynx-cn-proofs")
-        side = self._side_stream("_cnp_streams", "DRYNX_CNP_PRIORITY", bulk=0, alone=-1)
+        attr = f"_cnp_pool{lane}"
+        if not hasattr(self, attr):
+            setattr(self, attr, cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix=f"drynx-cn-proofs{lane}"))
+        side = self._side_stream(f"_cnp_streams{lane}", "DRYNX_CNP_PRIORITY", bulk=0, alone=-1)
         # the job's inputs are the work queued so far: an event recorded now and
         # waited for when the job STARTS on the worker -- a wait_stream issued
         # here would land on ``side`` while the previous job is still queueing
@@ -436,7 +445,7 @@ class DrynxNode:
             done.synchronize()  # this job's packed payloads are complete before anyone reads them
             return out
 
-        return self._cnp_pool.submit(run)
+        return getattr(self, attr).submit(run)
 
     @staticmethod
     def _resolve_proofs(proofs: list) -> list:
@@ -470,9 +479,11 @@ class DrynxNode:
 
     def _broadcast_query(self, sq: SurveyQuery | None) -> SurveyQuery:
         """Query to every rank (the reference broadcasts it down the CN tree,
-        service.go:263-330).  The CN input-validation signatures (MBs for wide
-        queries) travel only to ranks that do not hold that set yet (digest
-        keyed), as raw bytes."""
+        service.go:263-330) in ONE control collective.  The CN input-validation
+        signatures (MBs for wide queries) ride along, as raw bytes, only the
+        first time their set is sent: every rank keeps the same bounded cache
+        of sets keyed by digest (rank 0 mirrors it), so rank 0 knows which
+        sets the others hold without asking."""
         if self.comm.world == 1:
             return sq
         if not hasattr(self, "_ivsigs"):
@@ -481,28 +492,28 @@ class DrynxNode:
         if sq is not None:
             sigs = sq.Query.IVSigs.InputValidationSigs
             dg = ivsigs_digest(sigs)
-            if sigs:
-                self._ivsigs[dg] = sigs
             lite = copy.copy(sq)
             lite.Query = copy.copy(sq.Query)
             lite.Query.IVSigs = copy.copy(sq.Query.IVSigs)
             lite.Query.IVSigs.InputValidationSigs = None
-            msg = (lite.to_dict(), dg)
-        d, dg = self.comm.broadcast_object(msg, src=0)
-        missing = any(self.comm.all_gather_object(bool(dg) and dg not in self._ivsigs))
-        if missing:
             raw = None
-            if self.rank == 0:
-                raw = [[(x.Public, x.Signature) for x in row] for row in self._ivsigs[dg]]
-            raw = self.comm.broadcast_object(raw, src=0)
-            if dg not in self._ivsigs:
-                if len(self._ivsigs) > 8:
-                    self._ivsigs.clear()
-                self._ivsigs[dg] = [[PublishSignatureBytes(p, g) for p, g in row] for row in raw]
+            if dg and dg not in self._ivsigs:
+                raw = [[(x.Public, x.Signature) for x in row] for row in sigs]
+                self._cache_ivsigs(dg, sigs)
+            msg = (lite.to_dict(), dg, raw)
+        d, dg, raw = self.comm.broadcast_object(msg, src=0)
+        if self.rank != 0 and raw is not None:
+            self._cache_ivsigs(dg, [[PublishSignatureBytes(p, g) for p, g in row] for row in raw])
         out = SurveyQuery.from_dict(d)
         if dg:
             out.Query.IVSigs.InputValidationSigs = self._ivsigs[dg]
         return out
+
+    def _cache_ivsigs(self, dg, sigs):
+        """The same insertion / eviction on every rank (see ``_broadcast_query``)."""
+        if len(self._ivsigs) >= 8:
+            self._ivsigs.pop(next(iter(self._ivsigs)))
+        self._ivsigs[dg] = sigs
 
     def _range_proofs(self, sq, dp_results: dict, proofs: list):
         """Synchronous variant (kept for callers/tests that patch it)."""

@@ -121,6 +121,19 @@ def test_bench_self_launches_eight_ranks():
     for k in range(8):
         lo, hi = prq.sampled_bounds(_Sq, n_out, parts[k])
         assert items[k] == (hi - lo) * d["config"]["dps"] * d["config"]["vns"], k
+    # control plane: at most 4 host collectives per query per rank (query
+    # broadcast, pooled verdicts, bitmaps, co-signatures); + 1 for the bench's
+    # own elapsed-time gather after the timed steps
+    assert all(ranks[k]["ctrl_collectives"] <= 4 * d["steps"] + 1 for k in range(8)), \
+        [ranks[k]["ctrl_collectives"] for k in range(8)]
+    # per-party timers: every DP's <dp>_AllProofs is measured on its own rank
+    # (proving start -> the VNs' verdicts back on that rank); DPs on different
+    # ranks get their own values, none longer than the query
+    ap = {k: v for k, v in d["phase_s"].items() if k.endswith("_AllProofs")}
+    assert sorted(ap) == sorted(f"dp{i}_AllProofs" for i in range(10))
+    by_rank = {k: [ap[f"{dp}_AllProofs"] for dp in ranks[k]["roles"]["dp"]] for k in range(8)}
+    assert len({round(v[0], 6) for v in by_rank.values()}) > 1
+    assert max(ap.values()) <= max(ranks[0]["step_ms"]) / 1000.0 + 1e-3
     # traffic: every rank took part in the data plane; the VN ranks receive the most
     assert all(ranks[k]["bytes_sent"] > 0 and ranks[k]["bytes_recv"] > 0 for k in range(8))
     assert min(ranks[k]["bytes_recv"] for k in (3, 4, 5)) > max(ranks[k]["bytes_recv"] for k in (0, 1, 2, 6, 7))

@@ -128,7 +128,8 @@ def test_g2_msm_device_plan(device, skew):
 
 
 @pytest.mark.parametrize("device", DEVICES)
-def test_multi_exp_and_g1_msm_device_plans(device):
+@pytest.mark.parametrize("wc", [(4, 11), (3, 16)])
+def test_multi_exp_and_g1_msm_device_plans(device, wc):
     """GT multi-exponentiation (two groups of different exponent widths,
     two row periods) and the G1 MSM with device-resident plans against the
     oracle; an exponent wider than declared is reported, not dropped silently."""
@@ -144,7 +145,7 @@ def test_multi_exp_and_g1_msm_device_plans(device):
         k[i, 0], k[i, 1] = e & 0xffffffff, e >> 32
     k = k.to(torch.int32).to(dev)
     grp = torch.tensor([0] * (2 * n) + [1] * n, dtype=torch.int32, device=dev)
-    h = nt.multi_exp_device(a, k, grp, ((2 * n, 32), (n, 40)), 4, 11, item_split=(2 * n, n))
+    h = nt.multi_exp_device(a, k, grp, ((2 * n, 32), (n, 40)), *wc, item_split=(2 * n, n))
     got = nt.multi_exp_grouped_finish(h)
     nt.check_overflow(h)
     def pw(x, e):
@@ -164,7 +165,7 @@ def test_multi_exp_and_g1_msm_device_plans(device):
     # an exponent wider than group 0's declared 32 bits
     k2 = k.clone()
     k2[0, 1] = 1
-    h2 = nt.multi_exp_device(a, k2, grp, ((2 * n, 32), (n, 40)), 4, 11, item_split=(2 * n, n))
+    h2 = nt.multi_exp_device(a, k2, grp, ((2 * n, 32), (n, 40)), *wc, item_split=(2 * n, n))
     nt.multi_exp_grouped_finish(h2)
     with pytest.raises(RuntimeError, match="declared scalar widths"):
         nt.check_overflow(h2)

@@ -43,6 +43,8 @@ def test_phase_behind_stream_backlog_counts_the_wait(gpu_device):
     own (queued-after) work completes: the timer covers the backlog, and the
     phase's device work that outlives ``end`` is counted too."""
     a = torch.randn(8192, 8192, device=gpu_device)
+    for _ in range(2):
+        a = a @ a / 8192                        # library warm-up (kernel selection) outside the reference time
     torch.cuda.synchronize()
     t = time.perf_counter()
     for _ in range(6):
