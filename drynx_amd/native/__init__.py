@@ -146,7 +146,7 @@ _SIGS = {
     "dx_rp_accum_n_ni": [_P, _P, _P, _P, _P, _L, _L, _I, _I],
     "dx_rp_ncoeffs_inl": [_P, _P, _P, _P, _L],
     "dx_rp_accum_n_inl": [_P, _P, _P, _P, _P, _L, _L, _I, _I],
-    "dx_ufold_coop": [_P, _P, _P, _P, _P, _L, _L, _L],
+    "dx_ufold_coop_raw": [_P, _P, _P, _P, _P, _L, _L, _L],
     "dx_ufold_coop_steps": [],
     "dx_gt_frob8": [_I, _P, _P, _P, _L],
     "dx_gls6_entries": [],
@@ -1398,20 +1398,19 @@ def rp_fold_accum_n(img: torch.Tensor, UV: torch.Tensor, V_aff: torch.Tensor, pe
     return fb
 
 
-def rp_fold_accum_coop(img: torch.Tensor, UV: torch.Tensor, V_aff: torch.Tensor, period: int, G: int) -> torch.Tensor:
-    """``rp_fold_accum_n`` (K = 1 layout) with three lanes per item
-    (csrc/kernels/dx_ufold_coop.hip), for batches too small to fill the chip
-    one item per lane: every item's Miller value, then 64-item block
-    products -> [G * period / 64, 96].  GPU only."""
+def rp_fold_accum_coop_raw(coef: torch.Tensor, P_aff: torch.Tensor, V_aff: torch.Tensor, period: int,
+                           G: int) -> torch.Tensor:
+    """``rp_fold_accum_coop`` over the RAW line coefficients (``rp_fold_coeffs``,
+    no normalising pass) and affine points P -> [G * period / 64, 96].  GPU only."""
     m = _rows(V_aff, 32)
     n = G * period
-    assert _rows(UV, 16) == n and period >= m and period % 64 == 0
-    assert img.numel() == _load().dx_ufold_coop_steps() * 8 * m * 4
-    f = torch.empty((n, 96), dtype=torch.int32, device=UV.device)
-    _, s = _ctx(img, UV, V_aff)
-    rc = _raw_call("dx_ufold_coop", s, _ptr(img), _ptr(UV), _ptr(V_aff), _ptr(f), m, period, n)
+    assert _rows(P_aff, 16) == n and period >= m and period % 64 == 0
+    assert coef.numel() == _load().dx_ufold_coop_steps() * 12 * m * 4
+    f = torch.empty((n, 96), dtype=torch.int32, device=P_aff.device)
+    _, s = _ctx(coef, P_aff, V_aff)
+    rc = _raw_call("dx_ufold_coop_raw", s, _ptr(coef), _ptr(P_aff), _ptr(V_aff), _ptr(f), m, period, n)
     if rc:
-        raise RuntimeError(f"dx_ufold_coop failed rc={rc}")
+        raise RuntimeError(f"dx_ufold_coop_raw failed rc={rc}")
     x = f.view(n // 64, 64, 96).transpose(0, 1)
     while x.shape[0] > 1:
         x = _gt_prod_level(x, 8)

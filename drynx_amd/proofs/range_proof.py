@@ -849,7 +849,12 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
     # combinations per VN, n*S + 1 Miller loops (``_msm_queue``)
     dmode = os.environ.get("DRYNX_DCHECK", "auto")
     ddirect = dmode == "direct" or (dmode == "auto" and device.type == "cuda" and n * n_vn <= _DCHECK_DIRECT_MAX)
-    cC = ev_cC = None
+    cC = ev_cC = ev_valid = table = None
+    if device.type == "cuda":
+        # the U side's joint tables depend on V alone: first on this stream, so
+        # the U chain (the critical path of a small batch) starts at once
+        with timers.span("rp.u.joint_table"):
+            table = nt.g2_joint_table(r.V)
     with timers.span("rp.verify.validate"):
         # On a GPU the checks run on their own stream, filling the gaps the
         # verifier's host-side plans leave, and are read back with the
@@ -861,6 +866,8 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
             vstream.wait_stream(torch.cuda.current_stream(device))
             with torch.cuda.stream(vstream):
                 valid = validate_list(r, mode, lazy=True, per_proof=pp)
+                ev_valid = torch.cuda.Event()
+                ev_valid.record(vstream)                      # the weight mask waits for this, not for c C'
                 if ddirect:  # c C' per proof, weight-free (undecodable rows are masked out later)
                     cC = nt.g1_mul(r.commit.C.contiguous() if not any(r.offset) else
                                    nt.g1_add(r.commit.C, nt.g1_fb_mul_i64(
@@ -930,8 +937,8 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
     # of the decodable segments
     masked = segs is not None
     if masked:
-        if vstream is not None:
-            torch.cuda.current_stream(device).wait_stream(vstream)
+        if ev_valid is not None:
+            torch.cuda.current_stream(device).wait_event(ev_valid)
         vm = (valid if chk is None else valid & chk).to(torch.int32)
         mi = vm.repeat_interleave(S * l).view(1, m, 1)
         w_all = (w_all.view(G, n, 8) * vm.view(1, n, 1)).view(G * n, 8)
@@ -974,7 +981,7 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
         # the U side first, on this stream: its chain of Miller-loop kernels is
         # the critical path of a small batch (a pool slice)
         with timers.span("rp.verify.msm_queue"):
-            msq = _msm_queue(Y, r.V, ab_all, G, n, S, l, vstream, segs)
+            msq = _msm_queue(Y, r.V, ab_all, G, n, S, l, vstream, segs, table)
             for v, uok in zip(vns, msq["u_ok"]):
                 v["u_ok"] = uok
         aux.wait_event(ready)
@@ -1158,7 +1165,8 @@ def _r_window(m: int, G: int) -> int:
     return min(range(8, 14), key=lambda c: -(-254 // c) * (m + 8 * (1 << c)))
 
 
-def _msm_queue(Y, V, ab_all, G: int, n: int, S: int, L: int, vstream=None, segs: list | None = None) -> dict:
+def _msm_queue(Y, V, ab_all, G: int, n: int, S: int, L: int, vstream=None, segs: list | None = None,
+               table=None) -> dict:
     """Verifier mode "msm", the U side (no host sync; csrc/kernels/dx_rpmsm.hip):
     the pairing side of G verifiers' batches regrouped by bilinearity,
         prod_it ML(rho_it (Zphi_pj B - Y_pi), V_it)
@@ -1177,8 +1185,9 @@ def _msm_queue(Y, V, ab_all, G: int, n: int, S: int, L: int, vstream=None, segs:
     nseg = len(segs) if segs else 1
     qoff = np.cumsum([0] + [c * S for c in segs]) if segs else np.array([0, nq])
     cq = np.diff(qoff)
-    with timers.span("rp.u.joint_table"):
-        table = nt.g2_joint_table(V)
+    if table is None:
+        with timers.span("rp.u.joint_table"):
+            table = nt.g2_joint_table(V)
     out = {"G": G}
     if dev.type == "cuda":
         if nseg == 1:
@@ -1192,26 +1201,37 @@ def _msm_queue(Y, V, ab_all, G: int, n: int, S: int, L: int, vstream=None, segs:
             segbase = np.cumsum(ac) - ac
             pad = int(ac.sum())
         period = -(-(G * pad) // (rows * nt.FOLD_P_ALIGN)) * (rows * nt.FOLD_P_ALIGN)
+        # a small batch (a pool slice) folds on three lanes per item over the
+        # raw line coefficients and affine points (-Y); a large one keeps the
+        # one-lane accumulation over normalised lines and (x/y, 1/y) points
+        coop = K == 1 and G * pad <= _COOP_MAX_ITEMS
         Uall = torch.zeros((G * pad, 32), dtype=torch.int32, device=dev)
         UV = torch.zeros((period, 16), dtype=torch.int32, device=dev)
+        negY = None
+        if coop:  # affine -Y_q, the same for every VN
+            negY = nt.g1_to_affine(nt.g1_add(bn.g1_infinity_jac(nq, dev), Y.contiguous(), subtract=True))
         if nseg == 1:
             with timers.span("rp.u.joint"):
                 nt.rp_u_joint(table, ab_all, nq, G, L, Uall, pad)
-            nt.rp_msm_uv(Y, UV, nq, G, pad)
+            if coop:
+                UV[: G * pad].view(G, pad, 16)[:, :nq] = negY
+            else:
+                nt.rp_msm_uv(Y, UV, nq, G, pad)
             Ud = Uall
         else:
             Ud = torch.empty((G * nq, 32), dtype=torch.int32, device=dev)
             with timers.span("rp.u.joint"):
                 nt.rp_u_joint(table, ab_all, nq, G, L, Ud, nq)
-            # uv(-Y_q) is the same for every VN: computed once, copied per VN below
-            UVd = torch.zeros((nq + 1, 16), dtype=torch.int32, device=dev)
-            nt.rp_msm_uv(Y, UVd, nq, 1, nq + 1)
+            if not coop:  # uv(-Y_q) is the same for every VN: computed once, copied per VN below
+                UVd = torch.zeros((nq + 1, 16), dtype=torch.int32, device=dev)
+                nt.rp_msm_uv(Y, UVd, nq, 1, nq + 1)
+                negY = UVd[:nq]
             qseg = torch.repeat_interleave(torch.arange(nseg, device=dev), _h2d(cq, dev),
                                            output_size=nq)
             qpos = _h2d(segbase, dev)[qseg] + torch.arange(nq, device=dev) - _h2d(qoff[:-1], dev)[qseg]
             pos = (torch.arange(G, device=dev).view(G, 1) * pad + qpos.view(1, nq)).reshape(-1)
             Uall.index_copy_(0, pos, Ud)
-            UV.index_copy_(0, pos, UVd[:nq].repeat(G, 1))
+            UV.index_copy_(0, pos, negY.repeat(G, 1))
         # G2 membership of every U (exact test), on the validation stream beside the fold
         cur = torch.cuda.current_stream(dev)
         vs = vstream if vstream is not None else cur
@@ -1225,12 +1245,10 @@ def _msm_queue(Y, V, ab_all, G: int, n: int, S: int, L: int, vstream=None, segs:
             out["u_ok"] = list(out["u_seg"].all(dim=1).unbind(0))
         Ud.record_stream(vs)
         with timers.span("rp.u.fold"):
-            img = nt.rp_fold_ncoeffs(Uall)
-            if K == 1 and G * pad <= _COOP_MAX_ITEMS:
-                # a small batch (a pool slice): three lanes per item fill 3x the SIMDs
-                out["fb"] = nt.rp_fold_accum_coop(img, UV, Uall, period, 1)
+            if coop:
+                out["fb"] = nt.rp_fold_accum_coop_raw(nt.rp_fold_coeffs(Uall), UV, Uall, period, 1)
             else:
-                out["fb"] = nt.rp_fold_accum_n(img, UV, Uall, period, 1, K)
+                out["fb"] = nt.rp_fold_accum_n(nt.rp_fold_ncoeffs(Uall), UV, Uall, period, 1, K)
         out["blk"] = pad // rows
         out["sb"] = [0] if nseg == 1 else (segbase // rows).tolist()
         out["nb"] = [pad // rows] if nseg == 1 else (ac // rows).tolist()

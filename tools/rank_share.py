@@ -202,14 +202,16 @@ def main():
         from drynx_amd.utils import timers
 
         timers._events.clear()
+        reps = int(os.environ.get("RANK_SHARE_TRACE_REPS", "1"))  # > 1: the last one is the steady state
         for k in [int(x) for x in os.environ.get("RANK_SHARE_PARTS", "3,6").split(",")]:
-            reqs_k = full_reqs() if k in vn_ranks else helper_reqs(parts[k])
-            _sync()
-            time.sleep(1.0)  # an idle gap: a kernel trace shows this part as its own burst (tools/kernel_bursts.py)
-            with timers.span(f"pool_part[{k}]"):
-                pool_part(reqs_k, {v: list(range(len(rng))) for v in vn_idxs}, sq, dev, cache, parts[k],
-                          {vn.id: Coins() for vn in cl.vns})
-            _sync()
+            for _ in range(reps):
+                reqs_k = full_reqs() if k in vn_ranks else helper_reqs(parts[k])
+                _sync()
+                time.sleep(1.0)  # an idle gap: a kernel trace shows this part as its own burst (tools/kernel_bursts.py)
+                with timers.span(f"pool_part[{k}]"):
+                    pool_part(reqs_k, {v: list(range(len(rng))) for v in vn_idxs}, sq, dev, cache, parts[k],
+                              {vn.id: Coins() for vn in cl.vns})
+                _sync()
         timers.dump_trace(os.environ["DRYNX_TRACE"])
         if os.environ.get("RANK_SHARE_TRACE_ONLY") == "1":
             node.close(remove=True)
