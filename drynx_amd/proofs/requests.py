@@ -598,12 +598,13 @@ def sampled_bounds(sq, n: int, part=None) -> tuple:
 
 
 # extra work of a rank, in units of a plain helper's pool share, that its
-# slice is shortened by: every DP it hosts beyond the fewest any rank hosts
-# (proving a 2,070-output DP: ~5.4 ms against a ~38 ms 1/8 part, of which
-# only a part scales with the slice: one-GPU shares 55.3 -> 50.6 ms with
-# 0.32 / 0.12, profiles/r4/rank_share_w8_balanced*.json), and every VN it
-# hosts (the full-inbox decode and the digests of the other slices)
-_POOL_DP_W, _POOL_VN_W = 0.45, 0.08
+# slice is shortened by: every DP it hosts beyond the fewest any rank hosts,
+# and every VN it hosts (the full-inbox decode and the digests of the other
+# slices).  Fitted to pool(k) = F + P share(k) from the one-GPU shares of
+# profiles/r5/it2/rank_share_w8.json (F ~ 10 ms fixed, P ~ 166 ms for the
+# whole pool, a second DP ~5.3 ms of proving, a VN ~0.4 ms): equal
+# prove + pool at weights 1 / 0.982 / 0.762
+_POOL_DP_W, _POOL_VN_W = 0.24, 0.02
 
 
 def balanced_parts(W: int, dps: list, vns: list) -> list:
