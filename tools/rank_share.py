@@ -18,10 +18,15 @@ signed range-proof inbox, and then times, alone and synchronised (median of
 * serial: the query's non-range critical path (CN phases, querier, per-CN
   proofs, block), taken from a ``--u 0 --l 0`` bench JSON (``--serial-json``).
 
-The projection per rank is max(serial on rank 0, prove + pool)
-plus the measured fan-out time; the step is the max over ranks.  Peers'
-traffic over xGMI and waits on peers are not in it (the 8-GPU run measures
-those).  Usage: python tools/rank_share.py [--world 8] [--reps 5] [--serial-json f]
+* ctrl: the query's control-plane rounds on the host TCP plane (one query
+  broadcast and three all-gathers per query per rank: verdicts, bitmaps with
+  the block seed, co-signatures), from a ``tools/ctrl_round.py`` JSON of W
+  processes (``--ctrl-json``), added in full to every rank (not overlapped).
+
+The projection per rank is max(serial on rank 0, prove + pool) + ctrl; the
+step is the max over ranks.  Peers' traffic over xGMI and waits on peers are
+not in it (the 8-GPU run measures those).
+Usage: python tools/rank_share.py [--world 8] [--reps 5] [--serial-json f] [--ctrl-json f]
 """
 from __future__ import annotations
 
@@ -117,6 +122,7 @@ def main():
     ap.add_argument("--features", type=int, default=44)
     ap.add_argument("--records", type=int, default=1_000_000)
     ap.add_argument("--serial-json", default=None, help="bench.py --u 0 --l 0 JSON (the non-range critical path)")
+    ap.add_argument("--ctrl-json", default=None, help="tools/ctrl_round.py JSON (W-process control round latency)")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--order", default=None, help="comma list: the order the ranks are measured in (default 0..W-1)")
     ap.add_argument("--torch-prof", default=None,
@@ -203,7 +209,7 @@ def main():
 
         timers._events.clear()
         reps = int(os.environ.get("RANK_SHARE_TRACE_REPS", "1"))  # > 1: the last one is the steady state
-        for k in [int(x) for x in os.environ.get("RANK_SHARE_PARTS", "3,6").split(",")]:
+        for k in [int(x) for x in os.environ.get("RANK_SHARE_PARTS", "3,6").split(",") if x]:
             for _ in range(reps):
                 reqs_k = full_reqs() if k in vn_ranks else helper_reqs(parts[k])
                 _sync()
@@ -211,6 +217,15 @@ def main():
                 with timers.span(f"pool_part[{k}]"):
                     pool_part(reqs_k, {v: list(range(len(rng))) for v in vn_idxs}, sq, dev, cache, parts[k],
                               {vn.id: Coins() for vn in cl.vns})
+                _sync()
+        for k in [int(x) for x in os.environ.get("RANK_SHARE_PROVE", "").split(",") if x]:
+            # rank k's proving (its DPs' range proofs + signed envelopes), after the pool parts
+            mine = {dp: dp_results[dp] for dp in dps_of[k]}
+            for _ in range(reps):
+                _sync()
+                time.sleep(1.0)
+                with timers.span(f"prove[{k}]"):
+                    node._sign_range(sq, node._prove_range(sq, mine))
                 _sync()
         timers.dump_trace(os.environ["DRYNX_TRACE"])
         if os.environ.get("RANK_SHARE_TRACE_ONLY") == "1":
@@ -263,10 +278,16 @@ def main():
         res["serial_ms"] = s["ms_per_step"]
         res["serial_source"] = a.serial_json
     serial = res.get("serial_ms", 0.0)
+    ctrl = 0.0
+    if a.ctrl_json:
+        c = json.load(open(a.ctrl_json))
+        ctrl = c["bcast_ms_median"] + 3 * c["gather_ms_median"]
+        res["ctrl_ms"] = round(ctrl, 3)
+        res["ctrl_source"] = a.ctrl_json
     proj = {}
     for k, v in res["ranks"].items():
         rng_path = v["prove_ms"] + v["pool_ms"]  # a VN rank's pool_ms includes its overlapped digests
-        proj[k] = round(max(serial if k == 0 else 0.0, rng_path), 2)
+        proj[k] = round(max(serial if k == 0 else 0.0, rng_path) + ctrl, 2)
     res["projection_ms"] = proj
     res["projection_step_ms"] = max(proj.values())
     print(json.dumps({"projection_ms": proj, "step_ms": res["projection_step_ms"]}), flush=True)
