@@ -68,6 +68,9 @@ __global__ void __launch_bounds__(64) DX_OCC ufold_coop_raw_kernel(const uint4 *
                                                                    const uint32_t *__restrict__ V_aff,
                                                                    uint32_t *__restrict__ f_out, int64_t m,
                                                                    int64_t period, int64_t n_items) {
+  // item t's product goes to row (t % 64) * (n_items / 64) + t / 64: the
+  // [64, n_items / 64] lane-major image the 8-way product levels read
+  // contiguously (no transposing copy between the fold and the reduction)
   const coop::Role R = coop::role();
   const int64_t t = (int64_t)blockIdx.x * coop::kTriples + R.g;
   const bool real = R.g < coop::kTriples && t < n_items;
@@ -85,7 +88,7 @@ __global__ void __launch_bounds__(64) DX_OCC ufold_coop_raw_kernel(const uint4 *
   }
   raw_line_step(x, img, m, s++, qq, P, live, R);
   raw_line_step(x, img, m, s++, qq, P, live, R);
-  if (real) coop::store(&at<Fp12>(f_out, t), x, R);
+  if (real) coop::store(&at<Fp12>(f_out, (t & 63) * (n_items >> 6) + (t >> 6)), x, R);
 }
 
 }  // namespace
@@ -95,7 +98,7 @@ extern "C" {
 // raw coefficient image (kSteps * 12 * m uint4) and affine points P [n_items]
 int dx_ufold_coop_raw(void *stream, const uint32_t *img, const uint32_t *P_aff, const uint32_t *V_aff,
                       uint32_t *f_out, int64_t m, int64_t period, int64_t n_items) {
-  if (n_items <= 0 || m <= 0 || period < m) return n_items <= 0 ? 0 : -2;
+  if (n_items <= 0 || m <= 0 || period < m || n_items % 64) return n_items <= 0 ? 0 : -2;
   const unsigned blocks = (unsigned)((n_items + coop::kTriples - 1) / coop::kTriples);
   hipLaunchKernelGGL(ufold_coop_raw_kernel, dim3(blocks), dim3(64), 0, (hipStream_t)stream,
                      reinterpret_cast<const uint4 *>(img), P_aff, V_aff, f_out, m, period, n_items);

@@ -1411,7 +1411,7 @@ def rp_fold_accum_coop_raw(coef: torch.Tensor, P_aff: torch.Tensor, V_aff: torch
     rc = _raw_call("dx_ufold_coop_raw", s, _ptr(coef), _ptr(P_aff), _ptr(V_aff), _ptr(f), m, period, n)
     if rc:
         raise RuntimeError(f"dx_ufold_coop_raw failed rc={rc}")
-    x = f.view(n // 64, 64, 96).transpose(0, 1)
+    x = f.view(64, n // 64, 96)  # written lane-major by the kernel: item t at row (t % 64, t // 64)
     while x.shape[0] > 1:
         x = _gt_prod_level(x, 8)
     return x.view(n // 64, 96)

@@ -9,8 +9,7 @@ from collections import defaultdict
 
 
 def _name(n: str) -> str:
-    if n.startswith("(anonymous namespace)::"):
-        n = n[len("(anonymous namespace)::"):]
+    n = n.replace("(anonymous namespace)::", "")
     if "for_each_kernel" in n and "<" in n:
         return n.split("<", 1)[1].split("::")[0]
     return n.split("(")[0][:70]

@@ -37,7 +37,7 @@ def main():
     print(f"burst: {len(b)} kernels, wall {span / 1e6:.2f} ms, device busy (union) {busy / 1e6:.2f} ms")
     for s, e, n, q in b:
         if (e - s) / 1e6 >= a.min_ms:
-            nm = n.split("(")[0].replace("(anonymous namespace)::", "")[:60]
+            nm = n.replace("(anonymous namespace)::", "").split("(")[0][:60]
             print(f"{(s - t0) / 1e6:8.2f} {(e - t0) / 1e6:8.2f} {(e - s) / 1e6:7.2f}  q{q:<4} {nm}")
 
 

@@ -122,6 +122,8 @@ def main():
     ap.add_argument("--features", type=int, default=44)
     ap.add_argument("--records", type=int, default=1_000_000)
     ap.add_argument("--serial-json", default=None, help="bench.py --u 0 --l 0 JSON (the non-range critical path)")
+    ap.add_argument("--torch-prof-query", default=None,
+                    help="torch.profiler of one whole 1-GPU query (every thread): GPU time per framework span / op")
     ap.add_argument("--ctrl-json", default=None, help="tools/ctrl_round.py JSON (W-process control round latency)")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--order", default=None, help="comma list: the order the ranks are measured in (default 0..W-1)")
@@ -164,6 +166,12 @@ def main():
         sq.SurveyID = new_survey_id()
         client.send_survey_query(sq)
     DrynxNode._range_proofs_async, pcp.start_range_plane = orig_async, orig_plane
+    if a.torch_prof_query:
+        def one_query():
+            q = copy.copy(sq0)
+            q.SurveyID = new_survey_id()
+            client.send_survey_query(q)
+        _torch_glue(a.torch_prof_query, one_query)
     sq, reqs, dp_results = cap["sq"], cap["reqs"], cap["dp_results"]
     rng = [i for i, r in enumerate(reqs) if r.kind == "range"]
     vn_idxs = {vn.id: rng for vn in cl.vns}
