@@ -392,71 +392,172 @@ DX_NI FieldT<PR> fpow(const FieldT<PR> &a, const uint32_t *e) {
   return r;
 }
 
-// Inverse of a Montgomery-form element (a = xR -> x^-1 R), constant time.
-// Binary extended GCD with a fixed iteration count and masked updates
-// (invariants A = U z, B = V z mod p; B odd; each step shrinks len(A)+len(B)
-// by >= 1, so 510 steps reach A = 0, B = 1 from A < p, B = p < 2^254):
-// ~510 x ~60 simple VALU ops instead of Fermat's ~310 dependent Montgomery
-// products -- the latency that sets to_affine / decryption-table times for
-// short vectors.  V = (xR)^-1 as an integer; V * R^3 (Montgomery) = x^-1 R.
+// Inverse of a Montgomery-form element (a = xR -> x^-1 R), constant time:
+// Bernstein-Yang "safegcd" with half-delta divsteps (the variant and the
+// 10 x 59 = 590-step bound for 256-bit moduli of libsecp256k1's modinv64;
+// written here from the published algorithm).  The divsteps run on the low
+// 64 bits of (f, g) alone, 59 at a time, accumulating a 2x2 transition
+// matrix scaled by 2^62; each batch then applies the matrix to the full
+// 5 x 62-bit signed limbs of f, g and of the Bezout tracker (d, e) (mod p,
+// with a p multiple that clears the low 62 bits before the shift).  Starting
+// e at R^2 mod p makes d = R^2 (xR)^-1 = x^-1 R directly.  ~590 x 16 simple
+// 64-bit ops plus 10 x 44 64x64 products: ~4x fewer VALU instructions than
+// the bitwise binary GCD it replaces (510 steps over 8-limb values).
+namespace inv62 {
+using i64 = int64_t;
+using u64 = uint64_t;
+using i128 = __int128;
+constexpr u64 M62 = ~0ull >> 2;
+
+// bits [62 k, 62 k + 62) of a little-endian 8 x 32-bit integer
+constexpr i64 limb(const uint32_t (&w)[8], int k) {
+  u64 r = 0;
+  for (int b = 0; b < 62; b++) {
+    const int bit = 62 * k + b;
+    if (bit < 256 && ((w[bit / 32] >> (bit % 32)) & 1u)) r |= 1ull << b;
+  }
+  return (i64)r;
+}
+// p^-1 mod 2^62 (Newton: each step doubles the correct low bits; p odd)
+constexpr u64 inv_mod62(const uint32_t (&w)[8]) {
+  const u64 p0 = (u64)w[0] | ((u64)w[1] << 32);
+  u64 x = p0;  // correct mod 2^3 for odd p
+  for (int i = 0; i < 6; i++) x *= 2 - p0 * x;
+  return x & M62;
+}
+
+DX_HD i64 divsteps59(i64 zeta, u64 f, u64 g, i64 &tu, i64 &tv, i64 &tq, i64 &tr) {
+  u64 u = 8, v = 0, q = 0, r = 8;  // identity x 2^3: 59 steps later the matrix carries 2^62
+  for (int i = 3; i < 62; i++) {
+    u64 m1 = (u64)(zeta >> 63);    // zeta < 0
+    const u64 m2 = 0 - (g & 1);    // g odd
+    const u64 x = (f ^ m1) - m1, y = (u ^ m1) - m1, z = (v ^ m1) - m1;
+    g += x & m2;
+    q += y & m2;
+    r += z & m2;
+    m1 &= m2;                      // zeta < 0 and g odd: swap (f <- g, zeta <- -zeta - 2)
+    zeta = (zeta ^ (i64)m1) - 1;
+    f += g & m1;
+    u += q & m1;
+    v += r & m1;
+    g >>= 1;
+    u <<= 1;
+    v <<= 1;
+  }
+  tu = (i64)u;
+  tv = (i64)v;
+  tq = (i64)q;
+  tr = (i64)r;
+  return zeta;
+}
+
+// [f, g] <- t [f, g] / 2^62 (exact)
+DX_HD void update_fg(i64 *f, i64 *g, i64 u, i64 v, i64 q, i64 r) {
+  i128 cf = (i128)u * f[0] + (i128)v * g[0];
+  i128 cg = (i128)q * f[0] + (i128)r * g[0];
+  cf >>= 62;
+  cg >>= 62;
+#pragma unroll
+  for (int k = 1; k < 5; k++) {
+    cf += (i128)u * f[k] + (i128)v * g[k];
+    cg += (i128)q * f[k] + (i128)r * g[k];
+    f[k - 1] = (i64)((u64)cf & M62);
+    g[k - 1] = (i64)((u64)cg & M62);
+    cf >>= 62;
+    cg >>= 62;
+  }
+  f[4] = (i64)cf;
+  g[4] = (i64)cg;
+}
+
+// [d, e] <- (t [d, e] + p [md, me]) / 2^62, md / me chosen so the division is exact
+// and d, e stay in (-2p, p)
+DX_HD void update_de(i64 *d, i64 *e, i64 u, i64 v, i64 q, i64 r, const i64 *P, u64 pinv) {
+  const i64 sd = d[4] >> 63, se = e[4] >> 63;
+  i64 md = (u & sd) + (v & se);
+  i64 me = (q & sd) + (r & se);
+  i128 cd = (i128)u * d[0] + (i128)v * e[0];
+  i128 ce = (i128)q * d[0] + (i128)r * e[0];
+  md -= (i64)((pinv * (u64)cd + (u64)md) & M62);
+  me -= (i64)((pinv * (u64)ce + (u64)me) & M62);
+  cd += (i128)P[0] * md;
+  ce += (i128)P[0] * me;
+  cd >>= 62;
+  ce >>= 62;
+#pragma unroll
+  for (int k = 1; k < 5; k++) {
+    cd += (i128)u * d[k] + (i128)v * e[k] + (i128)P[k] * md;
+    ce += (i128)q * d[k] + (i128)r * e[k] + (i128)P[k] * me;
+    d[k - 1] = (i64)((u64)cd & M62);
+    e[k - 1] = (i64)((u64)ce & M62);
+    cd >>= 62;
+    ce >>= 62;
+  }
+  d[4] = (i64)cd;
+  e[4] = (i64)ce;
+}
+
+// d in (-2p, p), negated if sign < 0 -> [0, p)
+DX_HD void normalize(i64 *d, i64 sign, const i64 *P) {
+  i64 c = d[4] >> 63;
+#pragma unroll
+  for (int k = 0; k < 5; k++) d[k] += P[k] & c;
+  const i64 n = sign >> 63;
+#pragma unroll
+  for (int k = 0; k < 5; k++) d[k] = (d[k] ^ n) - n;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    d[k + 1] += d[k] >> 62;
+    d[k] &= (i64)M62;
+  }
+  c = d[4] >> 63;
+#pragma unroll
+  for (int k = 0; k < 5; k++) d[k] += P[k] & c;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    d[k + 1] += d[k] >> 62;
+    d[k] &= (i64)M62;
+  }
+}
+}  // namespace inv62
+
 template <class PR>
 DX_NI FieldT<PR> finv(const FieldT<PR> &a) {
-  uint32_t A[8], B[8], U[8], V[8];
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    A[i] = a.v[i];
-    B[i] = PR::MOD[i];
-    U[i] = 0;
-    V[i] = 0;
+  using namespace inv62;
+  constexpr i64 P0 = limb(PR::MOD, 0), P1 = limb(PR::MOD, 1), P2 = limb(PR::MOD, 2), P3 = limb(PR::MOD, 3),
+                P4 = limb(PR::MOD, 4);
+  constexpr i64 E0 = limb(PR::R2, 0), E1 = limb(PR::R2, 1), E2 = limb(PR::R2, 2), E3 = limb(PR::R2, 3),
+                E4 = limb(PR::R2, 4);
+  constexpr u64 PINV = inv_mod62(PR::MOD);
+  const i64 P[5] = {P0, P1, P2, P3, P4};
+  i64 f[5] = {P0, P1, P2, P3, P4};
+  i64 e[5] = {E0, E1, E2, E3, E4};
+  i64 d[5] = {0, 0, 0, 0, 0};
+  i64 g[5];
+  const uint32_t *w = a.v;
+  g[0] = (i64)(((u64)w[0] | ((u64)w[1] << 32)) & M62);
+  g[1] = (i64)((((u64)w[1] >> 30) | ((u64)w[2] << 2) | ((u64)w[3] << 34)) & M62);
+  g[2] = (i64)((((u64)w[3] >> 28) | ((u64)w[4] << 4) | ((u64)w[5] << 36)) & M62);
+  g[3] = (i64)((((u64)w[5] >> 26) | ((u64)w[6] << 6) | ((u64)w[7] << 38)) & M62);
+  g[4] = (i64)((u64)w[7] >> 24);
+  i64 zeta = -1;  // -(delta + 1/2), delta = 1/2
+  for (int it = 0; it < 10; it++) {
+    i64 u, v, q, r;
+    zeta = divsteps59(zeta, (u64)f[0], (u64)g[0], u, v, q, r);
+    update_de(d, e, u, v, q, r, P, PINV);
+    update_fg(f, g, u, v, q, r);
   }
-  U[0] = 1;
-  for (int it = 0; it < 510; it++) {
-    const uint32_t odd = 0u - (A[0] & 1u);
-    uint32_t br = 0;
-#pragma unroll
-    for (int i = 0; i < 8; i++) (void)subb32(A[i], B[i], br);
-    const uint32_t sw = odd & (0u - br);  // A odd and A < B: swap
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-      uint32_t t = (A[i] ^ B[i]) & sw;
-      A[i] ^= t;
-      B[i] ^= t;
-      t = (U[i] ^ V[i]) & sw;
-      U[i] ^= t;
-      V[i] ^= t;
-    }
-    // if A odd: A -= B; U = U - V mod p
-    br = 0;
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-      uint32_t d = subb32(A[i], B[i], br);
-      A[i] = (d & odd) | (A[i] & ~odd);
-    }
-    br = 0;
-    uint32_t D[8];
-#pragma unroll
-    for (int i = 0; i < 8; i++) D[i] = subb32(U[i], V[i], br);
-    const uint32_t neg = 0u - br;
-    uint32_t c = 0;
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-      D[i] = addc32(D[i], PR::MOD[i] & neg, c);
-      U[i] = (D[i] & odd) | (U[i] & ~odd);
-    }
-    // A >>= 1 ; U = U / 2 mod p  (U + p < 2^255: no carry out)
-#pragma unroll
-    for (int i = 0; i < 7; i++) A[i] = (A[i] >> 1) | (A[i + 1] << 31);
-    A[7] >>= 1;
-    const uint32_t uo = 0u - (U[0] & 1u);
-    c = 0;
-#pragma unroll
-    for (int i = 0; i < 8; i++) U[i] = addc32(U[i], PR::MOD[i] & uo, c);
-#pragma unroll
-    for (int i = 0; i < 7; i++) U[i] = (U[i] >> 1) | (U[i + 1] << 31);
-    U[7] >>= 1;
-  }
-  const FieldT<PR> r2 = FieldT<PR>::from_limbs(PR::R2);
-  return fmul(fmul(FieldT<PR>::from_limbs(V), r2), r2);  // V R^4 R^-2 = x^-1 R
+  normalize(d, f[4], P);  // g = 0, f = +-1: d = +- R^2 a^-1
+  FieldT<PR> out;
+  out.v[0] = (uint32_t)d[0];
+  out.v[1] = (uint32_t)(((u64)d[0] >> 32) | ((u64)d[1] << 30));
+  out.v[2] = (uint32_t)((u64)d[1] >> 2);
+  out.v[3] = (uint32_t)(((u64)d[1] >> 34) | ((u64)d[2] << 28));
+  out.v[4] = (uint32_t)((u64)d[2] >> 4);
+  out.v[5] = (uint32_t)(((u64)d[2] >> 36) | ((u64)d[3] << 26));
+  out.v[6] = (uint32_t)((u64)d[3] >> 6);
+  out.v[7] = (uint32_t)(((u64)d[3] >> 38) | ((u64)d[4] << 24));
+  return out;
 }
 
 // canonical integer (limbs, little endian) <-> Montgomery
