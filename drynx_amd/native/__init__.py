@@ -124,16 +124,10 @@ _SIGS = {
     "dx_g2_subgroup": [_I, _P, _P, _P, _L],
     "dx_limbs_canonical": [_I, _P, _P, _I, _P, _L],
     "dx_g1j_on_curve": [_I, _P, _P, _P, _L],
-    "dx_rp_points_ni": [_P, _P, _P, _P, _P, _L, _I, _I],
     "dx_rp_points_inl": [_P, _P, _P, _P, _P, _L, _I, _I],
-    "dx_fold_steps_ni": [],
-    "dx_rp_lines_ni": [_P, _P, _P, _P, _L, _L, _L],
-    "dx_rp_accum_ni": [_P, _P, _P, _L, _I],
     "dx_fold_steps_inl": [],
     "dx_rp_lines_inl": [_P, _P, _P, _P, _L, _L, _L],
     "dx_rp_accum_inl": [_P, _P, _P, _L, _I],
-    "dx_rp_coeffs_ni": [_P, _P, _P, _L],
-    "dx_rp_accum_p_ni": [_P, _P, _P, _P, _P, _L, _L, _I, _I],
     "dx_rp_coeffs_inl": [_P, _P, _P, _L],
     "dx_rp_accum_p_inl": [_P, _P, _P, _P, _P, _L, _L, _I, _I],
     "dx_rp_verify_items": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _I],
@@ -142,8 +136,6 @@ _SIGS = {
     "dx_sha256_segments": [_I, _P, _P, _L, _L, _L, _P],
     "dx_rp_points_glv": [_P, _P, _P, _P, _P, _P, _L, _I, _I, _I],
     "dx_g1_aff_to_uv": [_I, _P, _P, _L],
-    "dx_rp_ncoeffs_ni": [_P, _P, _P, _P, _L],
-    "dx_rp_accum_n_ni": [_P, _P, _P, _P, _P, _L, _L, _I, _I],
     "dx_rp_ncoeffs_inl": [_P, _P, _P, _P, _L],
     "dx_rp_accum_n_inl": [_P, _P, _P, _P, _P, _L, _L, _I, _I],
     "dx_ufold_coop_raw": [_P, _P, _P, _P, _P, _L, _L, _L],
@@ -1195,7 +1187,7 @@ def rp_verify_fold(ZB_jac, Y_jac, rho, V_aff, S: int, L: int) -> torch.Tensor:
 
 # inl: tower force-inlined into the fold kernels (12.4M Miller loops/s on one
 # MI355X vs 10.0M for ni, the out-of-line tower; tools/fold_bench.py)
-FOLD_VARIANT = os.environ.get("DRYNX_FOLD_VARIANT", "inl")
+FOLD_VARIANT = "inl"  # dx_fold_inl.hip (force-inlined tower functions; the out-of-line build lost its A/B)
 
 
 def rp_fold_points(ZB_jac: torch.Tensor, Y_jac: torch.Tensor, rho: torch.Tensor, S: int, L: int,

@@ -258,8 +258,7 @@ def test_every_operation_on_gpu(gpu_device, tmp_path, op):
     node.close(remove=True)
 
 
-@pytest.mark.parametrize("variant", ["ni", "inl"])
-def test_two_phase_fold_matches_oracle(gpu_device, variant):
+def test_two_phase_fold_matches_oracle(gpu_device, variant="inl"):
     """Line image + K-item multi-Miller accumulation == product of the
     oracle's pairings (after one final exponentiation), for every K."""
     m = 67  # a ragged last workgroup for every K
@@ -320,8 +319,7 @@ def test_range_prover_layouts_gpu(gpu_device, bits, monkeypatch):
     assert not rp.verify_range_proof_list(rpl, sm, P, 1.0, gpu_device)
 
 
-@pytest.mark.parametrize("variant", ["ni", "inl"])
-def test_fold_points_match_g1_ops(gpu_device, variant):
+def test_fold_points_match_g1_ops(gpu_device, variant="inl"):
     """Fused gather + difference + 64-bit multiplication + affine == the same
     through the separate G1 launches (including Y = infinity rows)."""
     S, L, npj = 3, 4, 5
