@@ -55,6 +55,38 @@ __global__ void __launch_bounds__(256) batched_copy_kernel(const CopyDesc *__res
   }
 }
 
+// The ledger's device-to-host copy of a query's payloads (~540 MB) straight
+// into pinned host memory by a SMALL persistent grid: every block walks the
+// chunks c = blockIdx.x, blockIdx.x + gridDim.x, ...  The copy is PCIe-bound
+// either way; the runtime's blit kernel ran it on ~4096 waves that held their
+// CU slots while stalled on PCIe, beside the verification kernels (5 ms of the
+// headline, tools/ab_ledger_copy.py); a 32-block grid leaves them the chip.
+__global__ void __launch_bounds__(256) copy_out_kernel(const CopyDesc *__restrict__ d, int nd, int64_t chunks) {
+  for (int64_t c = blockIdx.x; c < chunks; c += gridDim.x) {
+    int lo = 0, hi = nd - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (d[mid].chunk0 <= c) lo = mid; else hi = mid - 1;
+    }
+    const uint32_t *__restrict__ src = d[lo].src;
+    uint32_t *__restrict__ dst = d[lo].dst;
+    const int64_t base = (c - d[lo].chunk0) * kChunkWords;
+    const int64_t rem = d[lo].words - base;
+    const int lim = rem < kChunkWords ? (int)rem : kChunkWords;
+    uint32_t v[kPerLane];
+#pragma unroll
+    for (int k = 0; k < kPerLane; k++) {
+      const int i = threadIdx.x + k * 256;
+      if (i < lim) v[k] = src[base + i];
+    }
+#pragma unroll
+    for (int k = 0; k < kPerLane; k++) {
+      const int i = threadIdx.x + k * 256;
+      if (i < lim) dst[base + i] = v[k];
+    }
+  }
+}
+
 struct FlagSet {
   const uint8_t *f[kMaxFlags];
   int64_t k[kMaxFlags];
@@ -95,6 +127,26 @@ int dx_batched_copy(int on_gpu, void *stream, const int64_t *desc_dev, const int
   hipLaunchKernelGGL(batched_copy_kernel, dim3((unsigned)chunks), dim3(256), 0, (hipStream_t)stream,
                      reinterpret_cast<const CopyDesc *>(desc_dev), nd);
   return dx::check_hip(hipGetLastError(), "batched_copy");
+}
+
+// the same descriptors, dst in pinned host memory (device-visible addresses
+// from dx_host_device_ptr), copied by a grid of `blocks` workgroups
+int dx_copy_out(int on_gpu, void *stream, const int64_t *desc_dev, const int64_t *desc_host, int nd, int64_t chunks,
+                int blocks) {
+  if (nd <= 0 || chunks <= 0) return 0;
+  if (!on_gpu) return dx_batched_copy(0, stream, desc_dev, desc_host, nd, chunks);
+  const unsigned g = (unsigned)(blocks < 1 ? 1 : (chunks < blocks ? chunks : blocks));
+  hipLaunchKernelGGL(copy_out_kernel, dim3(g), dim3(256), 0, (hipStream_t)stream,
+                     reinterpret_cast<const CopyDesc *>(desc_dev), nd, chunks);
+  return dx::check_hip(hipGetLastError(), "copy_out");
+}
+
+// device-visible address of pinned (hipHostMalloc'd) host memory
+int dx_host_device_ptr(void *host, int64_t *out) {
+  void *d = nullptr;
+  if (dx::check_hip(hipHostGetDevicePointer(&d, host, 0), "hipHostGetDevicePointer")) return -1;
+  *out = reinterpret_cast<int64_t>(d);
+  return 0;
 }
 
 // out[p] = AND over the nf arrays a of all(flags_a[p*k_a : (p+1)*k_a] != 0)

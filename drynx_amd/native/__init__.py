@@ -85,6 +85,8 @@ _SIGS = {
     "dx_prg_glv": [_I, _P, _P, ctypes.c_uint32, _P, _P, _P, _L],
     "dx_prg_bits": [_I, _P, _P, ctypes.c_uint32, _I, _P, _L],
     "dx_batched_copy": [_I, _P, _P, _P, _I, _L],
+    "dx_copy_out": [_I, _P, _P, _P, _I, _L, _I],
+    "dx_host_device_ptr": [_P, _P],
     "dx_rows_all": [_I, _P, _P, _P, _I, _L, _P],
     "dx_gt_pow": [_I, _P, _P, _P, _P, _L, _I],
     "dx_gt_eq": [_I, _P, _P, _P, _P, _L],
@@ -721,6 +723,44 @@ def batched_copy(pairs: list) -> None:
     for s_, d_ in pairs:  # held until the call returns
         _ptr(s_), _ptr(d_)
     _call("dx_batched_copy", g, st, _ptr(dd), _ptr(ht), len(pairs), c0)
+
+
+COPY_OUT_BLOCKS = 32
+
+
+def copy_to_host(pairs: list, host_base: torch.Tensor, blocks: int = COPY_OUT_BLOCKS) -> None:
+    """``dst.copy_(src)`` for (device src, slice of the pinned host buffer
+    ``host_base``) pairs in ONE launch of a ``blocks``-workgroup persistent
+    grid on the current stream (csrc/kernels/dx_copy.hip copy_out_kernel):
+    PCIe-bound like the runtime's blit copy, but on a few CUs instead of
+    thousands of waves beside the compute kernels.  4-byte multiples."""
+    pairs = [(s_, d_) for s_, d_ in pairs if s_.numel()]
+    if not pairs:
+        return
+    dev = pairs[0][0].device
+    assert dev.type == "cuda" and host_base.is_pinned() and host_base.is_contiguous()
+    hb = host_base.data_ptr()
+    dbase = ctypes.c_int64(0)
+    rc = _load().dx_host_device_ptr(ctypes.c_void_p(hb), ctypes.cast(ctypes.pointer(dbase), ctypes.c_void_p))
+    if rc:
+        raise RuntimeError("pinned buffer has no device mapping")
+    hend = hb + host_base.numel() * host_base.element_size()
+    desc = np.empty((len(pairs), 4), dtype=np.int64)
+    c0 = 0
+    for i, (s_, d_) in enumerate(pairs):
+        nb = s_.numel() * s_.element_size()
+        assert s_.is_contiguous() and d_.is_contiguous() and s_.device == dev and d_.device.type == "cpu"
+        assert nb == d_.numel() * d_.element_size() and nb % 4 == 0 and s_.data_ptr() % 4 == 0
+        assert hb <= d_.data_ptr() and d_.data_ptr() + nb <= hend and (d_.data_ptr() - hb) % 4 == 0
+        w = nb // 4
+        desc[i] = (s_.data_ptr(), dbase.value + (d_.data_ptr() - hb), w, c0)
+        c0 += -(-w // _CHUNK_WORDS)
+    ht = torch.from_numpy(desc)
+    dd = ht.pin_memory().to(dev, non_blocking=True)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    for s_, _ in pairs:
+        _ptr(s_)
+    _call("dx_copy_out", 1, st, _ptr(dd), _ptr(ht), len(pairs), c0, int(blocks))
 
 
 def cat_rows(groups: list) -> list:

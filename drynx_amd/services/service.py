@@ -24,6 +24,7 @@ from dataclasses import dataclass, field
 
 import torch
 
+from .. import native as nt
 from ..crypto.elgamal import CipherVector
 from ..ledger.skipchain import SkipBlock
 from ..ledger.skipchain import update_chain as skc_update_chain
@@ -208,13 +209,19 @@ class DrynxNode:
         st.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(st):
             # each payload straight into its slice of one pinned buffer (no
-            # device-side concatenation of the ~600 MB of range payloads)
+            # device-side concatenation of the ~600 MB of range payloads), by a
+            # small persistent copy grid (nt.copy_to_host) instead of the
+            # runtime's blit kernel, whose thousands of PCIe-stalled waves sat
+            # beside the verification (~5 ms per query, tools/ab_ledger_copy.py)
             host = torch.empty((sum(sizes),), dtype=torch.uint8, pin_memory=True)
-            o = 0
+            pairs, slow, o = [], [], 0
             for t, n in zip(tensors, sizes):
-                host[o: o + n].copy_(t, non_blocking=True)
                 t.record_stream(st)
+                (pairs if n % 4 == 0 and t.data_ptr() % 4 == 0 else slow).append((t, host[o: o + n]))
                 o += n
+            nt.copy_to_host(pairs, host)
+            for t, h in slow:
+                h.copy_(t, non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(st)
 

@@ -477,3 +477,24 @@ def test_ufold_coop_matches_one_lane(gpu_device):
     ref = nt.rp_fold_accum_n(nt.rp_fold_ncoeffs(V), nt.g1_aff_to_uv_(P.clone()), V, period, G, 1)
     assert got.shape == ref.shape
     assert bool(nt.gt_eq(nt.final_exp(got.cpu()), nt.final_exp(ref.cpu())).all())
+
+
+def test_copy_to_host_small_grid(gpu_device):
+    """The ledger's device-to-host payload copy (nt.copy_to_host, a 32-block
+    persistent grid writing pinned host memory) == the device bytes, for
+    regions of odd word counts at 4-byte offsets (interior views included)."""
+    g = torch.Generator(device=gpu_device).manual_seed(5)
+    words = [1, 7, 4096, 4097, 70001, 1 << 20]
+    src = [torch.randint(-2 ** 31, 2 ** 31 - 1, (w + 3,), generator=g, device=gpu_device, dtype=torch.int64)
+           .to(torch.int32)[3:] for w in words]                                # 12-byte offset views
+    total = sum(4 * w for w in words)
+    host = torch.empty(total + 64, dtype=torch.uint8, pin_memory=True)
+    pairs, o = [], 4
+    for t in src:
+        b = t.view(torch.uint8)
+        pairs.append((b, host[o: o + b.numel()]))
+        o += b.numel()
+    nt.copy_to_host(pairs, host)
+    torch.cuda.synchronize()
+    for t, (_, h) in zip(src, pairs):
+        assert torch.equal(h.view(torch.int32), t.cpu())
