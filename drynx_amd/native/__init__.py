@@ -718,6 +718,8 @@ def batched_copy(pairs: list) -> None:
         desc[i] = (s_.data_ptr(), d_.data_ptr(), w, c0)
         c0 += -(-w // _CHUNK_WORDS)
     ht = torch.from_numpy(desc)
+    if dev.type == "cuda":
+        no_capture("batched_copy")
     dd = ht.pin_memory().to(dev, non_blocking=True) if dev.type == "cuda" else ht
     g, st = _ctx(pairs[0][1])
     for s_, d_ in pairs:  # held until the call returns
@@ -756,6 +758,7 @@ def copy_to_host(pairs: list, host_base: torch.Tensor, blocks: int = COPY_OUT_BL
         desc[i] = (s_.data_ptr(), dbase.value + (d_.data_ptr() - hb), w, c0)
         c0 += -(-w // _CHUNK_WORDS)
     ht = torch.from_numpy(desc)
+    no_capture("copy_to_host")
     dd = ht.pin_memory().to(dev, non_blocking=True)
     st = torch.cuda.current_stream(dev).cuda_stream
     for s_, _ in pairs:
@@ -1019,9 +1022,17 @@ def sha256_segments(tensors: list, chunk: int) -> list:
 INT_MOMENTS_MAX_COLS = 64
 
 
+def no_capture(what: str):
+    """Host-to-device copies from temporary host buffers must not be recorded
+    into a HIP graph (a replay would read freed host memory)."""
+    if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+        raise RuntimeError(f"{what}: host upload inside a HIP graph capture")
+
+
 def _upload(a: np.ndarray, device) -> torch.Tensor:
     t = torch.from_numpy(np.ascontiguousarray(a))
     if torch.device(device).type == "cuda":
+        no_capture("upload")
         return t.pin_memory().to(device, non_blocking=True)
     return t
 

@@ -951,24 +951,10 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
     _sw.__exit__(None, None, None)
     vns = [{"rho": rho_all[v * m:(v + 1) * m], "ab": ab_all[v * m:(v + 1) * m]} for v in range(G)]
     timers.count("rp.verify.items", G * m)
-    # exponents of the GT multi-exponentiation: groups 0..G-1 prod a^rho_v =
-    # prod a^a' * frob^8(a)^b' (32-bit exponents over (A, frob^8 A)); groups
-    # G..2G-1 each VN's own GT-membership combination prod a^gamma_v (over A)
-    abv = ab_all.view(G, m, 2)
-    k = torch.zeros((3 * G * m, 8), dtype=torch.int32, device=device)
-    kr = k[: 2 * G * m].view(G, 2 * m, 8)
-    kr[:, :m, 0] = abv[:, :, 0]
-    kr[:, m:, 0] = abv[:, :, 1]
-    k[2 * G * m:] = gam_all
-    gv = torch.arange(G, device=device, dtype=torch.int32)
-    mgrp = torch.cat([gv.repeat_interleave(2 * m), G + gv.repeat_interleave(m)])
     me_groups = ((2 * m, 32),) * G + ((m, gb),) * G
     # windows by cost (nt.me_window): 16 bits for a 1-GPU inbox, 11 for a pool
     # slice; the host keeps bytes (fewer buckets for its serial products)
     wc_ = nt.me_window(me_groups) if device.type == "cuda" else (5, 8)
-    # R-MSM scalars rho_it Zphi_(p, j) (periodic over the VNs)
-    it = torch.arange(m, device=device)
-    s_r = nt.fr_arith(nt.FR_MUL, rho_all, r.zphi.index_select(0, (it // (S * l)) * l + it % l).contiguous())
     if not ddirect:
         dpts = torch.cat([Cp.contiguous(), r.D.contiguous()]).repeat(G, 1)
         wc = nt.fr_arith(nt.FR_MUL, w_all, r.challenge)
@@ -985,18 +971,15 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
             for v, uok in zip(vns, msq["u_ok"]):
                 v["u_ok"] = uok
         aux.wait_event(ready)
-    # the R MSM, the multi-exponentiation and the D-check on the aux stream
-    # with device-resident bucket plans: no host sync, every pass queued now
-    # (a plan's host sync used to wait ~6-9 ms behind the U side)
+    # the R MSM, the multi-exponentiation and the exponent sums on the aux
+    # stream with device-resident bucket plans (no host sync); a pool slice's
+    # are one HIP graph replay (``_graph_run``: ~60 launches of host work
+    # otherwise), then the D-check
     with timers.span("rp.verify.passes"), (torch.cuda.stream(aux) if aux is not None else _nullctx()):
-        with timers.span("rp.run.R"):
-            S_R, hR = nt.g2_msm_device(r.V, s_r, m, ((m, 254),) * G, c=_r_window(m, G))
-        with timers.span("rp.frob8"):  # (A, frob^8 A) stacked: the Frobenius image written in place
-            A2 = torch.empty((2 * m, 96), dtype=torch.int32, device=device)
-            nt.batched_copy([(r.A.contiguous(), A2[:m])])
-            nt.gt_frob8(r.A.contiguous(), out=A2[m:])
-        with timers.span("rp.run.ME"):
-            mexp = nt.multi_exp_device(A2, k, mgrp, me_groups, wc_[0], wc_[1], item_split=(2 * G * m, m))
+        pin = dict(V=r.V, A=r.A, zphi=r.zphi, rho=rho_all, ab=ab_all, gam=gam_all, zv=r.zv, w=w_all, zr=r.zr, z=z)
+        meta = (G, m, S, l, gb, tuple(wc_), _r_window(m, G))
+        S_R, hR, A2, mexp, e_all, dfull = _graph_run(("passes", meta), _verify_passes, pin, meta,
+                                                     G * m <= _GRAPH_MAX_ITEMS)
         with timers.span("rp.run.D"):
             if ddirect:
                 if cC is None:                                                 # host path
@@ -1009,9 +992,6 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
                 dcheck = nt.g1_sum(nt.g1_mul_glv(pts.contiguous(), abs_.contiguous()).view(n, 2 * G, 24))
             else:
                 dcheck = nt.g1_msm_device(dpts, dsc, n, ((n, 254),) * (2 * G))     # group = row // n
-        e_all = nt.fr_dot_rows(rho_all, r.zv, G, b_periodic=True)                        # sum rho Zv per VN
-        dfull = torch.stack([nt.fr_dot_rows(w_all, r.zr, G, b_periodic=True),
-                             nt.fr_dot_rows(w_all, z, G, b_periodic=True)], 1)             # [G, 2, 8]
     if aux is None:  # host: the U side after the passes
         msq = _msm_queue(Y, r.V, ab_all, G, n, S, l, None, segs)
         for v, uok in zip(vns, msq["u_ok"]):
@@ -1151,6 +1131,107 @@ class _nullctx:
 
     def __exit__(self, *a):
         return False
+
+
+def _verify_passes(V, A, zphi, rho, ab, gam, zv, w, zr, z, meta):
+    """The weight-dependent device passes of ``verify_range_proof_list_multi``
+    on the current stream, no host sync: R = sum (rho Zphi) V per VN (G2
+    Pippenger, device plan), the GT multi-exponentiation over (A, frob^8 A)
+    with the GLV halves of rho and the 40-bit membership combinations, and
+    the Fr exponent sums.  -> (S_R, hR, A2, mexp, e_all, dfull)."""
+    G, m, S, l, gb, wc, cR = meta
+    dev = V.device
+    it = torch.arange(m, device=dev)
+    s_r = nt.fr_arith(nt.FR_MUL, rho, zphi.index_select(0, (it // (S * l)) * l + it % l).contiguous())
+    with timers.span("rp.run.R"):
+        S_R, hR = nt.g2_msm_device(V, s_r, m, ((m, 254),) * G, c=cR)
+    with timers.span("rp.frob8"):  # (A, frob^8 A) stacked: the Frobenius image written in place
+        A2 = torch.empty((2 * m, 96), dtype=torch.int32, device=dev)
+        A2[:m].copy_(A)
+        nt.gt_frob8(A.contiguous(), out=A2[m:])
+    # exponents: groups 0..G-1 prod a^rho_v = prod a^a' * frob^8(a)^b' (32-bit
+    # GLV halves over (A, frob^8 A)); groups G..2G-1 each VN's own GT-membership
+    # combination prod a^gamma_v (over A)
+    abv = ab.view(G, m, 2)
+    k = torch.zeros((3 * G * m, 8), dtype=torch.int32, device=dev)
+    kr = k[: 2 * G * m].view(G, 2 * m, 8)
+    kr[:, :m, 0] = abv[:, :, 0]
+    kr[:, m:, 0] = abv[:, :, 1]
+    k[2 * G * m:] = gam
+    gv = torch.arange(G, device=dev, dtype=torch.int32)
+    mgrp = torch.cat([gv.repeat_interleave(2 * m), G + gv.repeat_interleave(m)])
+    with timers.span("rp.run.ME"):
+        mexp = nt.multi_exp_device(A2, k, mgrp, ((2 * m, 32),) * G + ((m, gb),) * G, wc[0], wc[1],
+                                   item_split=(2 * G * m, m))
+    e_all = nt.fr_dot_rows(rho, zv, G, b_periodic=True)                                 # sum rho Zv per VN
+    dfull = torch.stack([nt.fr_dot_rows(w, zr, G, b_periodic=True),
+                         nt.fr_dot_rows(w, z, G, b_periodic=True)], 1)                   # [G, 2, 8]
+    return S_R, hR, A2, mexp, e_all, dfull
+
+
+# ---------------------------------------------------------------- HIP graphs
+# A pool slice's passes are ~60 short launches whose host-side queueing
+# (Python, plans, torch glue) took ~6-7 ms per part while its kernels run in
+# ~14 ms: captured once per shape and replayed (inputs copied into the graph's
+# static buffers, ~100 MB of device copies).  Shape-keyed per thread (the
+# outputs are the graph's own tensors, valid until its next replay on that
+# thread).  The first call of a shape runs eagerly (it also builds the plan
+# layouts the captured launches read), the second captures.  A 1-GPU inbox
+# (G m in the millions) stays eager: its kernels dwarf the launch work, and a
+# graph pool would pin gigabytes beside the prover tables.
+_GRAPH_MAX_ITEMS = 1 << 20
+_GRAPHS: dict = {}
+_GRAPH_LIMIT = 8
+
+
+class _Graph:
+    __slots__ = ("calls", "graph", "static", "out", "stream", "failed")
+
+    def __init__(self):
+        self.calls, self.graph, self.static, self.out, self.stream, self.failed = 0, None, None, None, None, False
+
+
+def _graph_run(key, fn, inputs: dict, meta, use: bool):
+    """``fn(**inputs, meta=meta)`` on the current stream, or its HIP graph's
+    replay (see above).  ``inputs``: device tensors whose shapes the key fixes."""
+    dev = next(iter(inputs.values())).device
+    if not use or dev.type != "cuda":
+        return fn(**inputs, meta=meta)
+    k = (key, tuple((n, tuple(t.shape), t.dtype) for n, t in inputs.items()), str(dev), threading.get_ident())
+    gr = _GRAPHS.get(k)
+    if gr is None:
+        if len(_GRAPHS) >= _GRAPH_LIMIT:
+            _GRAPHS.pop(next(iter(_GRAPHS)))
+        gr = _GRAPHS[k] = _Graph()
+    gr.calls += 1
+    if gr.failed or gr.calls == 1:
+        return fn(**inputs, meta=meta)
+    cur = torch.cuda.current_stream(dev)
+    if gr.graph is None:
+        gr.static = {n: torch.empty(t.shape, dtype=t.dtype, device=dev) for n, t in inputs.items()}
+        gr.stream = torch.cuda.Stream(dev)
+        gr.stream.wait_stream(cur)
+        g = torch.cuda.CUDAGraph()
+        try:
+            with torch.cuda.stream(gr.stream):
+                g.capture_begin(capture_error_mode="thread_local")
+                try:
+                    out = fn(**gr.static, meta=meta)
+                finally:
+                    g.capture_end()
+        except Exception as e:  # noqa: BLE001 -- a shape that cannot be captured runs eagerly from now on
+            gr.failed = True
+            log.warning(f"HIP graph capture of {key[0]} failed ({e}); running it eagerly")
+            cur.wait_stream(gr.stream)
+            return fn(**inputs, meta=meta)
+        gr.graph, gr.out = g, out
+        cur.wait_stream(gr.stream)
+        timers.count("graph.captured")
+    for n, t in inputs.items():
+        gr.static[n].copy_(t)
+    gr.graph.replay()
+    timers.count("graph.replays")
+    return gr.out
 
 
 _DCHECK_DIRECT_MAX = 16384  # proofs x VNs up to which the D-check runs without a bucket plan

@@ -305,3 +305,25 @@ def test_dcheck_direct_and_bucket_agree(device, dmode, proofs, monkeypatch):
     bad.zr = zr
     assert rp.verify_range_proof_list_multi(bad, sm, P, 3, dev, segs=[1, 2, 1]) == [[True, False, True]] * 3
     assert rp.verify_range_proof_list_multi(bad, sm, P, 2, dev) == [False] * 2
+
+
+@pytest.mark.gpu
+def test_pass_graph_replays_track_their_inputs(proofs):
+    """A small batch's weight-dependent passes are captured as a HIP graph on
+    the second call of a shape and replayed after: replays see each call's
+    own proofs and weights (valid / tampered batches interleaved) and give
+    the eager verdicts."""
+    dev = _dev("cuda")
+    rpl, sm, P = proofs
+    rp._GRAPHS.clear()
+    good = rpl.to(dev)
+    bad = rpl.to(dev)
+    V = bad.V.clone()
+    V[4] = V[5]
+    bad.V = V
+    seq = [good, good, bad, good, bad, good]
+    got = [rp.verify_range_proof_list_multi(x, sm, P, 3, dev) for x in seq]
+    assert got == [[ok] * 3 for ok in (True, True, False, True, False, True)]
+    graphs = [g for k, g in rp._GRAPHS.items() if k[0][0] == "passes"]
+    assert len(graphs) == 1 and graphs[0].graph is not None and not graphs[0].failed
+    assert graphs[0].calls == len(seq)
