@@ -1158,8 +1158,8 @@ def _verify_passes(V, A, zphi, rho, ab, gam, zv, w, zr, z, meta):
     kr[:, :m, 0] = abv[:, :, 0]
     kr[:, m:, 0] = abv[:, :, 1]
     k[2 * G * m:] = gam
-    gv = torch.arange(G, device=dev, dtype=torch.int32)
-    mgrp = torch.cat([gv.repeat_interleave(2 * m), G + gv.repeat_interleave(m)])
+    e = torch.arange(3 * G * m, device=dev)                          # entry -> group, elementwise only
+    mgrp = torch.where(e < 2 * G * m, e // (2 * m), G + (e - 2 * G * m) // m).to(torch.int32)
     with timers.span("rp.run.ME"):
         mexp = nt.multi_exp_device(A2, k, mgrp, ((2 * m, 32),) * G + ((m, gb),) * G, wc[0], wc[1],
                                    item_split=(2 * G * m, m))
