@@ -1826,8 +1826,8 @@ def _device_layout(groups: tuple, W: int, c: int, sl: int, dev) -> dict:
            "first_lane": up(off, np.int64), "multi": up(multi, np.int64),
            "passes": [(up(st, np.int64), up(ln, np.int32)) for st, ln in passes],
            "used_t": up(ubk, np.int64), "unused_t": up(np.flatnonzero(~used), np.int64)}
-    if len(_DPLANS) > 32:
-        _DPLANS.clear()
+    if len(_DPLANS) > 32:  # least recently built first (HIP graphs keep their own references)
+        _DPLANS.pop(next(iter(_DPLANS)))
     _DPLANS[key] = lay
     return lay
 

@@ -1185,10 +1185,11 @@ _GRAPH_LIMIT = 8
 
 
 class _Graph:
-    __slots__ = ("calls", "graph", "static", "out", "stream", "failed")
+    __slots__ = ("calls", "graph", "static", "out", "stream", "failed", "keep")
 
     def __init__(self):
         self.calls, self.graph, self.static, self.out, self.stream, self.failed = 0, None, None, None, None, False
+        self.keep = None
 
 
 def _graph_run(key, fn, inputs: dict, meta, use: bool):
@@ -1224,7 +1225,10 @@ def _graph_run(key, fn, inputs: dict, meta, use: bool):
             log.warning(f"HIP graph capture of {key[0]} failed ({e}); running it eagerly")
             cur.wait_stream(gr.stream)
             return fn(**inputs, meta=meta)
-        gr.graph, gr.out = g, out
+        # the captured launches read the cached plan layouts (nt._DPLANS: lane
+        # maps, weight chunks): the graph holds them, so evicting a layout from
+        # the cache can never free memory a replay reads
+        gr.graph, gr.out, gr.keep = g, out, list(nt._DPLANS.values())
         cur.wait_stream(gr.stream)
         timers.count("graph.captured")
     for n, t in inputs.items():

@@ -324,6 +324,14 @@ def test_pass_graph_replays_track_their_inputs(proofs):
     seq = [good, good, bad, good, bad, good]
     got = [rp.verify_range_proof_list_multi(x, sm, P, 3, dev) for x in seq]
     assert got == [[ok] * 3 for ok in (True, True, False, True, False, True)]
+    # the graph owns the plan layouts it reads: dropping the cache and churning
+    # the allocator (the freed blocks reused) leaves its replays intact
+    nt._DPLANS.clear()
+    churn = [torch.full((1 << 20,), -1, dtype=torch.int32, device=dev) for _ in range(64)]
+    del churn
+    seq += [bad, good]
+    got = [rp.verify_range_proof_list_multi(x, sm, P, 3, dev) for x in seq[-2:]]
+    assert got == [[False] * 3, [True] * 3]
     graphs = [g for k, g in rp._GRAPHS.items() if k[0][0] == "passes"]
     assert len(graphs) == 1 and graphs[0].graph is not None and not graphs[0].failed
     assert graphs[0].calls == len(seq)
