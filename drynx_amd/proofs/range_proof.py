@@ -972,14 +972,10 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
                 v["u_ok"] = uok
         aux.wait_event(ready)
     # the R MSM, the multi-exponentiation and the exponent sums on the aux
-    # stream with device-resident bucket plans (no host sync); a pool slice's
-    # are one HIP graph replay (``_graph_run``: ~60 launches of host work
-    # otherwise), then the D-check
+    # stream with device-resident bucket plans (no host sync), then the D-check
     with timers.span("rp.verify.passes"), (torch.cuda.stream(aux) if aux is not None else _nullctx()):
-        pin = dict(V=r.V, A=r.A, zphi=r.zphi, rho=rho_all, ab=ab_all, gam=gam_all, zv=r.zv, w=w_all, zr=r.zr, z=z)
-        meta = (G, m, S, l, gb, tuple(wc_), _r_window(m, G))
-        S_R, hR, A2, mexp, e_all, dfull = _graph_run(("passes", meta), _verify_passes, pin, meta,
-                                                     G * m <= _GRAPH_MAX_ITEMS)
+        S_R, hR, A2, mexp, e_all, dfull = _verify_passes(r.V, r.A, r.zphi, rho_all, ab_all, gam_all, r.zv, w_all,
+                                                         r.zr, z, (G, m, S, l, gb, tuple(wc_), _r_window(m, G)))
         with timers.span("rp.run.D"):
             if ddirect:
                 if cC is None:                                                 # host path
@@ -1167,75 +1163,6 @@ def _verify_passes(V, A, zphi, rho, ab, gam, zv, w, zr, z, meta):
     dfull = torch.stack([nt.fr_dot_rows(w, zr, G, b_periodic=True),
                          nt.fr_dot_rows(w, z, G, b_periodic=True)], 1)                   # [G, 2, 8]
     return S_R, hR, A2, mexp, e_all, dfull
-
-
-# ---------------------------------------------------------------- HIP graphs
-# A pool slice's passes are ~60 short launches whose host-side queueing
-# (Python, plans, torch glue) took ~6-7 ms per part while its kernels run in
-# ~14 ms: captured once per shape and replayed (inputs copied into the graph's
-# static buffers, ~100 MB of device copies).  Shape-keyed per thread (the
-# outputs are the graph's own tensors, valid until its next replay on that
-# thread).  The first call of a shape runs eagerly (it also builds the plan
-# layouts the captured launches read), the second captures.  A 1-GPU inbox
-# (G m in the millions) stays eager: its kernels dwarf the launch work, and a
-# graph pool would pin gigabytes beside the prover tables.
-_GRAPH_MAX_ITEMS = 1 << 20
-_GRAPHS: dict = {}
-_GRAPH_LIMIT = 8
-
-
-class _Graph:
-    __slots__ = ("calls", "graph", "static", "out", "stream", "failed", "keep")
-
-    def __init__(self):
-        self.calls, self.graph, self.static, self.out, self.stream, self.failed = 0, None, None, None, None, False
-        self.keep = None
-
-
-def _graph_run(key, fn, inputs: dict, meta, use: bool):
-    """``fn(**inputs, meta=meta)`` on the current stream, or its HIP graph's
-    replay (see above).  ``inputs``: device tensors whose shapes the key fixes."""
-    dev = next(iter(inputs.values())).device
-    if not use or dev.type != "cuda":
-        return fn(**inputs, meta=meta)
-    k = (key, tuple((n, tuple(t.shape), t.dtype) for n, t in inputs.items()), str(dev), threading.get_ident())
-    gr = _GRAPHS.get(k)
-    if gr is None:
-        if len(_GRAPHS) >= _GRAPH_LIMIT:
-            _GRAPHS.pop(next(iter(_GRAPHS)))
-        gr = _GRAPHS[k] = _Graph()
-    gr.calls += 1
-    if gr.failed or gr.calls == 1:
-        return fn(**inputs, meta=meta)
-    cur = torch.cuda.current_stream(dev)
-    if gr.graph is None:
-        gr.static = {n: torch.empty(t.shape, dtype=t.dtype, device=dev) for n, t in inputs.items()}
-        gr.stream = torch.cuda.Stream(dev)
-        gr.stream.wait_stream(cur)
-        g = torch.cuda.CUDAGraph()
-        try:
-            with torch.cuda.stream(gr.stream):
-                g.capture_begin(capture_error_mode="thread_local")
-                try:
-                    out = fn(**gr.static, meta=meta)
-                finally:
-                    g.capture_end()
-        except Exception as e:  # noqa: BLE001 -- a shape that cannot be captured runs eagerly from now on
-            gr.failed = True
-            log.warning(f"HIP graph capture of {key[0]} failed ({e}); running it eagerly")
-            cur.wait_stream(gr.stream)
-            return fn(**inputs, meta=meta)
-        # the captured launches read the cached plan layouts (nt._DPLANS: lane
-        # maps, weight chunks): the graph holds them, so evicting a layout from
-        # the cache can never free memory a replay reads
-        gr.graph, gr.out, gr.keep = g, out, list(nt._DPLANS.values())
-        cur.wait_stream(gr.stream)
-        timers.count("graph.captured")
-    for n, t in inputs.items():
-        gr.static[n].copy_(t)
-    gr.graph.replay()
-    timers.count("graph.replays")
-    return gr.out
 
 
 _DCHECK_DIRECT_MAX = 16384  # proofs x VNs up to which the D-check runs without a bucket plan

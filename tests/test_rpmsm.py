@@ -307,36 +307,6 @@ def test_dcheck_direct_and_bucket_agree(device, dmode, proofs, monkeypatch):
     assert rp.verify_range_proof_list_multi(bad, sm, P, 2, dev) == [False] * 2
 
 
-@pytest.mark.gpu
-def test_pass_graph_replays_track_their_inputs(proofs):
-    """A small batch's weight-dependent passes are captured as a HIP graph on
-    the second call of a shape and replayed after: replays see each call's
-    own proofs and weights (valid / tampered batches interleaved) and give
-    the eager verdicts."""
-    dev = _dev("cuda")
-    rpl, sm, P = proofs
-    rp._GRAPHS.clear()
-    good = rpl.to(dev)
-    bad = rpl.to(dev)
-    V = bad.V.clone()
-    V[4] = V[5]
-    bad.V = V
-    seq = [good, good, bad, good, bad, good]
-    got = [rp.verify_range_proof_list_multi(x, sm, P, 3, dev) for x in seq]
-    assert got == [[ok] * 3 for ok in (True, True, False, True, False, True)]
-    # the graph owns the plan layouts it reads: dropping the cache and churning
-    # the allocator (the freed blocks reused) leaves its replays intact
-    nt._DPLANS.clear()
-    churn = [torch.full((1 << 20,), -1, dtype=torch.int32, device=dev) for _ in range(64)]
-    del churn
-    seq += [bad, good]
-    got = [rp.verify_range_proof_list_multi(x, sm, P, 3, dev) for x in seq[-2:]]
-    assert got == [[False] * 3, [True] * 3]
-    graphs = [g for k, g in rp._GRAPHS.items() if k[0][0] == "passes"]
-    assert len(graphs) == 1 and graphs[0].graph is not None and not graphs[0].failed
-    assert graphs[0].calls == len(seq)
-
-
 @pytest.mark.parametrize("device", DEVICES)
 @pytest.mark.parametrize("n,nb", [(0, 5), (1000, 7), (50000, 3000), (300000, 70000)])
 def test_bucket_counting_sort(device, n, nb):
