@@ -305,26 +305,3 @@ def test_dcheck_direct_and_bucket_agree(device, dmode, proofs, monkeypatch):
     bad.zr = zr
     assert rp.verify_range_proof_list_multi(bad, sm, P, 3, dev, segs=[1, 2, 1]) == [[True, False, True]] * 3
     assert rp.verify_range_proof_list_multi(bad, sm, P, 2, dev) == [False] * 2
-
-
-@pytest.mark.parametrize("device", DEVICES)
-@pytest.mark.parametrize("n,nb", [(0, 5), (1000, 7), (50000, 3000), (300000, 70000)])
-def test_bucket_counting_sort(device, n, nb):
-    """dx_bucket_sort (the plans' counting sort): every bucket's run holds
-    exactly its entries (any order), runs in key order back to back, keys
-    outside [0, nb) (zero-digit sentinels) dropped."""
-    dev = _dev(device)
-    g = torch.Generator().manual_seed(n + nb)
-    keys = torch.randint(0, nb, (n,), generator=g, dtype=torch.int32)
-    if n:
-        keys[torch.randint(0, n, (n // 7,), generator=g)] = 0x7fffffff
-    items = torch.randperm(n, generator=g).to(torch.int32)
-    out, first, end = nt._sorted_runs(keys.to(dev), items.to(dev), nb)
-    out, first, end = out.cpu(), first.cpu(), end.cpu()
-    valid = keys < nb
-    cnt = torch.bincount(keys[valid].long(), minlength=nb)
-    assert torch.equal(end - first, cnt)
-    assert torch.equal(first[1:], end[:-1]) and int(first[0]) == 0
-    for b in torch.randint(0, nb, (min(nb, 50),), generator=g).tolist() + [0, nb - 1]:
-        got = sorted(out[int(first[b]): int(end[b])].tolist())
-        assert got == sorted(items[keys == b].tolist()), b
