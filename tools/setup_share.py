@@ -37,6 +37,7 @@ import torch  # noqa: E402
 from drynx_amd.query import LogisticRegressionParameters  # noqa: E402
 from drynx_amd.services.api import DrynxClient  # noqa: E402
 from drynx_amd.services.local import local_cluster, make_survey  # noqa: E402
+from drynx_amd.utils import timers  # noqa: E402
 
 
 def _sync():
@@ -106,7 +107,11 @@ def main():
     res = {"world": a.world, "rank": a.rank, "features": d, "table_mode": mode, "distinct_points": sm.n_distinct,
            "sigs_s": round(sigs_s, 3)}
 
-    def build():
+    def build(label):
+        with timers.span(f"setup.build[{label}]"):
+            return _build()
+
+    def _build():
         old = sm._ptab.pop((mode, str(dev)), None)
         del old  # the previous build's tables are freed before the next one allocates its own
         if dev.type == "cuda":
@@ -119,12 +124,12 @@ def main():
         return t0, time.perf_counter() - t0
 
     sm.attach_shard(None, False)
-    res["build_first_s"] = round(build()[1], 3)  # module / kernel first-use costs included
-    res["build_full_s"] = round(build()[1], 3)
+    res["build_first_s"] = round(build("first")[1], 3)  # module / kernel first-use costs included
+    res["build_full_s"] = round(build("full")[1], 3)
     res["table_bytes"] = sm.table_bytes()
     emu = EmuShard(a.world, a.rank, dev)
     sm._shard = emu  # as attach_shard does for a W-rank communicator
-    t0, total = build()
+    t0, total = build("share")
     res["landing_hbm_s"] = round(emu.landing_s, 3)
     res["build_share_s"] = round((emu.first_landing or (t0 + total)) - t0, 3)
     res["share_total_s"] = round(total, 3)
@@ -139,6 +144,7 @@ def main():
     print(json.dumps(res), flush=True)
     if a.json_out:
         json.dump(res, open(a.json_out, "w"), indent=1)
+    timers.dump_trace()  # DRYNX_TRACE=<path>: the builds' host spans
     node.close(remove=True)
 
 
