@@ -95,39 +95,40 @@ def _device_timed() -> bool:
 # Phase timers measure WALL time from the host's start of the phase to the
 # completion of the last operation the phase queued on its stream (the
 # reference's StartTimer/EndTimer bracket goroutines that block until their
-# work is done), without a host sync and without a polling thread: ``start``
-# records a timing event on an idle per-device "clock" stream (it completes
-# at once, so its device timestamp is the host's start), ``end`` records one
-# on the phase's stream, and the interval is their device elapsed time, read
-# when the timers are next summarised.  A phase that starts behind a stream
-# backlog counts the wait; work joined from other streams (wait_stream before
-# ``end``) is covered.  (A watcher thread that polled the end events every
-# 0.2 ms took the interpreter from the query's threads all query long.)
-_pending: list = []        # (name, start event, end event) whose end was still running
-_clock: dict = {}
+# work is done).  ``end`` records a HIP event instead of synchronising the
+# query's thread; a watcher thread stamps the host time at which the event
+# completes (polling, 0.2 ms) and records ``completion - start``.  A phase that
+# starts behind a stream backlog therefore counts the wait, and work the phase
+# joined from other streams (wait_stream before ``end``) is covered.
+_watch: list = []          # (name, host start, end event) not yet complete
+_watch_cv = threading.Condition(_lock)
+_watcher = None
 
 
-def _clock_event():
-    dev = torch.cuda.current_device()
-    st = _clock.get(dev)
-    if st is None:
-        with _lock:
-            st = _clock.setdefault(dev, torch.cuda.Stream(dev))
-    e = torch.cuda.Event(enable_timing=True)
-    e.record(st)
-    return e
+def _watch_loop():
+    while True:
+        with _watch_cv:
+            while not _watch:
+                _watch_cv.wait()
+            items = list(_watch)
+        done = []
+        for it in items:
+            if it[2].query():
+                done.append((it, time.perf_counter()))
+        with _watch_cv:
+            for it, t1 in done:
+                _watch.remove(it)
+                _records[it[0]].append(t1 - it[1])
+            if done:
+                _watch_cv.notify_all()
+        time.sleep(0.0002)
 
 
 def _resolve():
-    """Read every pending phase's device interval (waits for its end event)."""
-    with _lock:
-        items = list(_pending)
-        _pending.clear()
-    for name, e0, e1 in items:
-        e1.synchronize()
-        dt = max(0.0, e0.elapsed_time(e1) / 1e3)
-        with _lock:
-            _records[name].append(dt)
+    """Wait until every watched phase has completed and been recorded."""
+    with _watch_cv:
+        while _watch:
+            _watch_cv.wait(0.05)
 
 
 class Timer:
@@ -135,24 +136,26 @@ class Timer:
         self.name = name
         self.sync = sync
         self.t0 = None
-        self.e0 = None
 
     def start(self):
         self.t0 = time.perf_counter()
-        if self.sync and _device_timed():
-            self.e0 = _clock_event()
         return self
 
     def end(self) -> float:
+        global _watcher
         t1 = time.perf_counter()
         if _TRACE:
             _emit(self.name, int(self.t0 * 1e9), int(t1 * 1e9))
-        if self.e0 is not None:
-            e1 = torch.cuda.Event(enable_timing=True)
+        if self.sync and _device_timed():
+            e1 = torch.cuda.Event()
             e1.record()
-            if not e1.query():  # the phase's device work is still running: timed on the device
-                with _lock:
-                    _pending.append((self.name, self.e0, e1))
+            if not e1.query():  # the phase's device work is still running: the watcher stamps its end
+                with _watch_cv:
+                    _watch.append((self.name, self.t0, e1))
+                    if _watcher is None:
+                        _watcher = threading.Thread(target=_watch_loop, daemon=True, name="drynx-timers")
+                        _watcher.start()
+                    _watch_cv.notify_all()
                 return t1 - self.t0
             t1 = time.perf_counter()
         dt = t1 - self.t0
