@@ -1,0 +1,401 @@
+// Field, G1 and ElGamal batch ops (K1-K5, K9 of SURVEY §2.3): unlynx EncryptIntGetR,
+// IntToPoint, CipherVector.Add, DecryptIntWithNeg (BSGS).
+// C ABI consumed by drynx_amd/native (ctypes).  Every entry point takes
+// (on_gpu, stream): on_gpu launches a gfx950 kernel on that HIP stream (torch's
+// current stream), otherwise the same functor runs on the host thread pool.
+#include "common.h"
+
+extern "C" {
+// ---------------------------------------------------------------- field utils
+int dx_fp_to_mont(int on_gpu, void *stream, const uint32_t *in, uint32_t *out, int64_t n) {
+  auto op = [=] __host__ __device__(int64_t i) { at<Fp>(out, i) = to_mont(at<Fp>(in, i)); };
+  return run(on_gpu, stream, n, op, false, "fp_to_mont");
+}
+int dx_fp_from_mont(int on_gpu, void *stream, const uint32_t *in, uint32_t *out, int64_t n) {
+  auto op = [=] __host__ __device__(int64_t i) { at<Fp>(out, i) = from_mont(at<Fp>(in, i)); };
+  return run(on_gpu, stream, n, op, false, "fp_from_mont");
+}
+
+}  // extern "C"
+
+// Fr arithmetic on canonical scalars. op: 0 add, 1 sub, 2 mul, 3 neg(a), 4 inv(a), 5 reduce(a)
+
+namespace {
+// One kernel per operation (the op code is a template parameter): a switch
+// over all five ops compiled the binary-GCD inversion into every launch of
+// the hot add / mul paths (VGPR pressure, scratch).  The product of two
+// canonical scalars is one Montgomery multiplication with one operand in
+// Montgomery form: x * (yR) * R^-1 = x y.
+template <int OPC>
+int fr_arith_t(int on_gpu, void *stream, const uint32_t *a, const uint32_t *b, uint32_t *out, int64_t n,
+               int64_t b_bcast) {
+  auto op = [=] __host__ __device__(int64_t i) {
+    Fr x = reduce_256<FrParams>(a + 8 * i);
+    Fr r;
+    if constexpr (OPC == 0 || OPC == 1 || OPC == 2) {
+      // b_bcast = k > 0: b has k rows, row i reads b[i % k] (1: one broadcast scalar)
+      Fr y = b ? reduce_256<FrParams>(b + 8 * (b_bcast ? i % b_bcast : i)) : Fr::zero();
+      if constexpr (OPC == 0) r = fadd(x, y);
+      else if constexpr (OPC == 1) r = fsub(x, y);
+      else r = fmul(x, to_mont(y));
+    } else if constexpr (OPC == 3) {
+      r = fneg(x);
+    } else if constexpr (OPC == 4) {
+      r = from_mont(finv(to_mont(x)));
+    } else {
+      r = x;
+    }
+    at<Fr>(out, i) = r;
+  };
+  return run(on_gpu, stream, n, op, false, "fr_arith");
+}
+}  // namespace
+
+extern "C" {
+
+int dx_fr_arith(int on_gpu, void *stream, int opc, const uint32_t *a, const uint32_t *b, uint32_t *out, int64_t n,
+                int64_t b_bcast) {
+  switch (opc) {
+    case 0: return fr_arith_t<0>(on_gpu, stream, a, b, out, n, b_bcast);
+    case 1: return fr_arith_t<1>(on_gpu, stream, a, b, out, n, b_bcast);
+    case 2: return fr_arith_t<2>(on_gpu, stream, a, b, out, n, b_bcast);
+    case 3: return fr_arith_t<3>(on_gpu, stream, a, b, out, n, b_bcast);
+    case 4: return fr_arith_t<4>(on_gpu, stream, a, b, out, n, b_bcast);
+    default: return fr_arith_t<5>(on_gpu, stream, a, b, out, n, b_bcast);
+  }
+}
+
+// Chunked Fr dot products / sums of canonical scalars, per group of m rows:
+//   out[g * n_chunks + c] = sum_{k in chunk c} a[g*m + k] * B(g, k)
+// with B = 1 (b == null), b[g*m + k] (b_periodic == 0) or b[k] (b_periodic == 1).
+// A batch verifier's weighted sums (sum rho_i Zv_i over 10^5 items) take
+// ceil(log_chunk m) launches instead of a log2(m)-deep pairwise tree.
+int dx_fr_dot_chunks(int on_gpu, void *stream, const uint32_t *a, const uint32_t *b, int b_periodic, uint32_t *out,
+                     int64_t groups, int64_t m, int64_t chunk) {
+  const int64_t n_chunks = (m + chunk - 1) / chunk;
+  auto op = [=] __host__ __device__(int64_t t) {
+    const int64_t g = t / n_chunks, c = t % n_chunks;
+    const int64_t s = c * chunk, e = s + chunk < m ? s + chunk : m;
+    const Fr r2 = Fr::from_limbs(FrParams::R2);
+    Fr acc = Fr::zero();
+    for (int64_t k = s; k < e; k++) {
+      Fr x = reduce_256<FrParams>(a + 8 * (g * m + k));
+      if (b) {
+        const Fr y = reduce_256<FrParams>(b + 8 * (b_periodic ? k : g * m + k));
+        x = fmul(fmul(x, y), r2);  // x y R^-1 R^2 R^-1 = x y (canonical)
+      }
+      acc = fadd(acc, x);
+    }
+    at<Fr>(out, t) = acc;
+  };
+  return run(on_gpu, stream, groups * n_chunks, op, false, "fr_dot_chunks");
+}
+
+// Per-segment Fr sums: out[t] = sum_{offs[t] <= i < offs[t+1]} a[i] (canonical),
+// one lane per segment (segments are a batch's per-request slices: a few
+// dozen, each a few thousand rows already reduced by fr_dot_chunks).
+int dx_fr_seg_sum(int on_gpu, void *stream, const uint32_t *a, const int64_t *offs, uint32_t *out, int64_t k) {
+  auto op = [=] __host__ __device__(int64_t t) {
+    Fr acc = Fr::zero();
+    for (int64_t i = offs[t]; i < offs[t + 1]; i++) acc = fadd(acc, reduce_256<FrParams>(a + 8 * i));
+    at<Fr>(out, t) = acc;
+  };
+  return run(on_gpu, stream, k, op, false, "fr_seg_sum");
+}
+
+// ---------------------------------------------------------------- G1
+// Comb tables for n_bases points: table[b][w*256+d] = d * 2^(8w) * base_b (affine).
+// Two phases: (1) one thread per base walks the 256 doublings 2^k * base into
+// `work` ([n_bases][256] Jacobian); (2) one thread per entry adds the <= 8
+// powers selected by the bits of d and normalises (~400 Fp mults per entry
+// instead of a 256-bit scalar multiplication).
+int dx_g1_fb_table(int on_gpu, void *stream, const uint32_t *bases_aff, uint32_t *work, uint32_t *table,
+                   int64_t n_bases) {
+  auto p1 = [=] __host__ __device__(int64_t b) {
+    G1J acc = G1J::from_aff(at<G1A>(bases_aff, b));
+    for (int k = 0; k < 256; k++) {
+      at<G1J>(work, b * 256 + k) = acc;
+      acc = jdbl(acc);
+    }
+  };
+  int rc = run(on_gpu, stream, n_bases, p1, true, "g1_fb_table_pow2");
+  if (rc) return rc;
+  auto p2 = [=] __host__ __device__(int64_t t) {
+    int64_t b = t / 8192, i = t % 8192;
+    int w = (int)(i >> 8), d = (int)(i & 255);
+    G1J acc = G1J::inf();
+    for (int bit = 0; bit < 8; bit++)
+      if ((d >> bit) & 1) acc = jadd(acc, at<G1J>(work, b * 256 + 8 * w + bit));
+    at<G1A>(table, t) = to_affine(acc);
+  };
+  return run(on_gpu, stream, n_bases * 8192, p2, true, "g1_fb_table");
+}
+
+int dx_g1_fb_mul(int on_gpu, void *stream, const uint32_t *table, const uint32_t *scalars, uint32_t *out, int64_t n) {
+  auto op = [=] __host__ __device__(int64_t i) {
+    at<G1J>(out, i) = fixed_base_mul(reinterpret_cast<const G1A *>(table), scalars + 8 * i);
+  };
+  return run(on_gpu, stream, n, op, true, "g1_fb_mul");
+}
+
+// k_i * base_{tab_idx[i]}: fixed-base multiplication over several comb tables.
+int dx_g1_fb_mul_idx(int on_gpu, void *stream, const uint32_t *tables, const int32_t *tab_idx,
+                     const uint32_t *scalars, uint32_t *out, int64_t n) {
+  auto op = [=] __host__ __device__(int64_t i) {
+    const G1A *T = reinterpret_cast<const G1A *>(tables) + (int64_t)tab_idx[i] * 8192;
+    at<G1J>(out, i) = fixed_base_mul(T, scalars + 8 * i);
+  };
+  return run(on_gpu, stream, n, op, true, "g1_fb_mul_idx");
+}
+
+// m * base for signed 64-bit m (unlynx IntToPoint).
+int dx_g1_fb_mul_i64(int on_gpu, void *stream, const uint32_t *table, const int64_t *m, uint32_t *out, int64_t n) {
+  auto op = [=] __host__ __device__(int64_t i) {
+    uint32_t k[8];
+    bool ng;
+    signed_to_scalar(m[i], k, ng);
+    G1J r = fixed_base_mul(reinterpret_cast<const G1A *>(table), k);
+    at<G1J>(out, i) = ng ? jneg(r) : r;
+  };
+  return run(on_gpu, stream, n, op, true, "g1_fb_mul_i64");
+}
+
+// Variable base: out[i] = k[i] * P[i or 0]
+int dx_g1_mul(int on_gpu, void *stream, const uint32_t *pts_jac, const uint32_t *scalars, uint32_t *out, int64_t n,
+              int pt_bcast, int k_bcast) {
+  auto op = [=] __host__ __device__(int64_t i) {
+    at<G1J>(out, i) = scalar_mul(at<G1J>(pts_jac, pt_bcast ? 0 : i), scalars + 8 * (k_bcast ? 0 : i));
+  };
+  return run(on_gpu, stream, n, op, true, "g1_mul");
+}
+
+// out = a +/- b (b may be broadcast)
+int dx_g1_add(int on_gpu, void *stream, const uint32_t *a, const uint32_t *b, uint32_t *out, int64_t n, int subtract,
+              int b_bcast) {
+  auto op = [=] __host__ __device__(int64_t i) {
+    G1J q = at<G1J>(b, b_bcast ? 0 : i);
+    if (subtract) q = jneg(q);
+    at<G1J>(out, i) = jadd(at<G1J>(a, i), q);
+  };
+  return run(on_gpu, stream, n, op, false, "g1_add");
+}
+
+int dx_g1_to_affine(int on_gpu, void *stream, const uint32_t *jac, uint32_t *aff, int64_t n) {
+  auto op = [=] __host__ __device__(int64_t i) { at<G1A>(aff, i) = to_affine(at<G1J>(jac, i)); };
+  return run(on_gpu, stream, n, op, true, "g1_to_affine");
+}
+
+int dx_g1_from_affine(int on_gpu, void *stream, const uint32_t *aff, uint32_t *jac, int64_t n) {
+  auto op = [=] __host__ __device__(int64_t i) { at<G1J>(jac, i) = G1J::from_aff(at<G1A>(aff, i)); };
+  return run(on_gpu, stream, n, op, false, "g1_from_affine");
+}
+
+int dx_g1_eq(int on_gpu, void *stream, const uint32_t *a, const uint32_t *b, uint8_t *out, int64_t n) {
+  auto op = [=] __host__ __device__(int64_t i) { out[i] = jeq(at<G1J>(a, i), at<G1J>(b, i)) ? 1 : 0; };
+  return run(on_gpu, stream, n, op, false, "g1_eq");
+}
+
+int dx_g1_on_curve(int on_gpu, void *stream, const uint32_t *aff, uint8_t *out, int64_t n) {
+  auto op = [=] __host__ __device__(int64_t i) { out[i] = on_curve(at<G1A>(aff, i)) ? 1 : 0; };
+  return run(on_gpu, stream, n, op, false, "g1_on_curve");
+}
+
+// Decoding checks of raw-limb payloads (RangeProofList.unpack): every 8-limb
+// row below its modulus (Fp for coordinates in Montgomery form, Fr for
+// scalars), and Jacobian G1 points on the curve (Y^2 = X^3 + b Z^6; Z = 0 is
+// the point at infinity).
+int dx_limbs_canonical(int on_gpu, void *stream, const uint32_t *x, int fr, uint8_t *out, int64_t n) {
+  auto op = [=] __host__ __device__(int64_t i) {
+    const uint32_t *v = x + 8 * i;
+    const uint32_t *m = fr ? FrParams::MOD : FpParams::MOD;
+    uint32_t br = 0;
+    for (int k = 0; k < 8; k++) (void)subb32(v[k], m[k], br);
+    out[i] = br ? 1 : 0;  // borrow: v < m
+  };
+  return run(on_gpu, stream, n, op, false, "limbs_canonical");
+}
+
+int dx_g1j_on_curve(int on_gpu, void *stream, const uint32_t *jac, uint8_t *out, int64_t n) {
+  auto op = [=] __host__ __device__(int64_t i) {
+    const G1J p = at<G1J>(jac, i);
+    if (p.is_inf()) {
+      out[i] = 1;
+      return;
+    }
+    const Fp z2 = fsqr(p.z), z6 = fmul(fsqr(z2), z2);
+    out[i] = fsqr(p.y) == fadd(fmul(fsqr(p.x), p.x), fmul(Fp::from_limbs(Curve::B1), z6)) ? 1 : 0;
+  };
+  return run(on_gpu, stream, n, op, false, "g1j_on_curve");
+}
+
+// Partial sums over axis 0 of in[n_items][n_groups] (Jacobian):
+// out[c][g] = sum_{i in chunk c} in[i][g], chunk = `chunk` items.
+// Square roots in Fp on the host pool: y = a^((p+1)/4) (p = 3 mod 4) and
+// whether y^2 == a, canonical little-endian limbs in and out.  The BLS
+// try-and-increment map to G1 spent ~0.2 ms per Python pow on the block
+// co-signing path.
+int dx_fp_sqrt_host(const uint32_t *a_canon, const uint32_t *exp_le, uint32_t *y_canon, uint8_t *ok, int64_t n) {
+  uint32_t e[8];
+  for (int i = 0; i < 8; i++) e[i] = exp_le[i];
+  host_for_each(n, [=](int64_t i) {
+    const Fp a = to_mont(reduce_256<FpParams>(a_canon + 8 * i));
+    const Fp y = fpow(a, e);
+    ok[i] = fsqr(y) == a ? 1 : 0;
+    const Fp yc = from_mont(y);
+    for (int k = 0; k < 8; k++) y_canon[8 * i + k] = yc.v[k];
+  }, 2);
+  return 0;
+}
+
+// Host tail of the G1 bucket MSM: out[g] = sum_w 2^(c w) S[g W + w] (Jacobian),
+// one serial Horner chain per group on the host pool -- a Python loop of
+// per-window native calls cost ~2 ms for a 32-window, 6-group D-check.
+int dx_g1_horner_host(const uint32_t *S_jac, uint32_t *out_jac, int64_t G, int W, int c) {
+  host_for_each(G, [=](int64_t g) {
+    G1J acc = at<G1J>(S_jac, g * W + W - 1);
+    for (int w = W - 2; w >= 0; w--) {
+      for (int k = 0; k < c; k++) acc = jdbl(acc);
+      acc = jadd(acc, at<G1J>(S_jac, g * W + w));
+    }
+    at<G1J>(out_jac, g) = acc;
+  }, 2);
+  return 0;
+}
+
+int dx_g1_sum_chunks(int on_gpu, void *stream, const uint32_t *in, uint32_t *out, int64_t n_items, int64_t n_groups,
+                     int64_t chunk) {
+  int64_t n_chunks = (n_items + chunk - 1) / chunk;
+  auto op = [=] __host__ __device__(int64_t t) {
+    int64_t c = t / n_groups, g = t % n_groups;
+    int64_t s = c * chunk, e = s + chunk < n_items ? s + chunk : n_items;
+    G1J acc = G1J::inf();
+    for (int64_t i = s; i < e; i++) acc = jadd(acc, at<G1J>(in, i * n_groups + g));
+    at<G1J>(out, t) = acc;
+  };
+  return run(on_gpu, stream, n_chunks * n_groups, op, true, "g1_sum_chunks");
+}
+
+// Segmented Jacobian sums (bucket accumulation of a multi-scalar multiplication):
+//   out[s] = sum_{k < len[s]} src[idx ? idx[start[s] + k] : start[s] + k]
+int dx_g1_slice_sum(int on_gpu, void *stream, const uint32_t *src, const int64_t *idx, const int64_t *start,
+                    const int32_t *len, uint32_t *out, int64_t n_slices) {
+  auto op = [=] __host__ __device__(int64_t s) {
+    const int64_t b = start[s];
+    const int n = len[s];
+    G1J acc = G1J::inf();
+    for (int k = 0; k < n; k++) acc = jadd(acc, at<G1J>(src, idx ? idx[b + k] : b + k));
+    at<G1J>(out, s) = acc;
+  };
+  return run(on_gpu, stream, n_slices, op, true, "g1_slice_sum");
+}
+
+// ---------------------------------------------------------------- ElGamal
+// K = r*B, C = m*B + r*P  (unlynx EncryptIntGetR with caller-provided r)
+int dx_elgamal_encrypt(int on_gpu, void *stream, const uint32_t *tabB, const uint32_t *tabP, const int64_t *m,
+                       const uint32_t *r, uint32_t *outK, uint32_t *outC, int64_t n) {
+  auto op = [=] __host__ __device__(int64_t i) {
+    const G1A *TB = reinterpret_cast<const G1A *>(tabB);
+    const G1A *TP = reinterpret_cast<const G1A *>(tabP);
+    uint32_t k[8];
+    bool ng;
+    signed_to_scalar(m[i], k, ng);
+    G1J mB = fixed_base_mul(TB, k);
+    if (ng) mB = jneg(mB);
+    at<G1J>(outK, i) = fixed_base_mul(TB, r + 8 * i);
+    at<G1J>(outC, i) = jadd(mB, fixed_base_mul(TP, r + 8 * i));
+  };
+  return run(on_gpu, stream, n, op, true, "elgamal_encrypt");
+}
+
+// ---------------------------------------------------------------- BSGS dlog
+// Open-addressing table (cap = power of two): keys[] u64 (0 = empty), vals[] i32.
+int dx_bsgs_build(int on_gpu, void *stream, const uint32_t *tabB, int64_t m_baby, uint64_t *keys, int32_t *vals,
+                  int64_t cap) {
+  auto op = [=] __host__ __device__(int64_t j) {
+    uint32_t k[8] = {(uint32_t)j, (uint32_t)((uint64_t)j >> 32), 0, 0, 0, 0, 0, 0};
+    G1A a = to_affine(fixed_base_mul(reinterpret_cast<const G1A *>(tabB), k));
+    uint64_t key = j == 0 ? 1ull : point_key(a);  // j==0: infinity, handled by the solver
+    if (j == 0) return;
+    uint64_t h = mix64(key) & (uint64_t)(cap - 1);
+    int32_t val = (int32_t)((j << 1) | (a.y.v[0] & 1u));  // y parity disambiguates +/-j
+    for (int64_t probe = 0; probe < cap; probe++) {
+      uint64_t old;
+      if (cas64(&keys[h], 0ull, key, old) || old == key) {
+        vals[h] = val;
+        return;
+      }
+      h = (h + 1) & (uint64_t)(cap - 1);
+    }
+  };
+  return run(on_gpu, stream, m_baby, op, true, "bsgs_build");
+}
+
+// For each target T_i (affine, = m_i*B + offset*B with m_i + offset in [0, m_baby*n_giant)),
+// find m = j + g*m_baby with T - g*(m_baby*B) = +/- j*B. Outputs value-offset.
+int dx_bsgs_solve(int on_gpu, void *stream, const uint32_t *targets_jac, const uint32_t *giant_aff, const uint64_t *keys,
+                  const int32_t *vals, int64_t cap, int64_t m_baby, int64_t n_giant, int64_t offset, int64_t *out,
+                  uint8_t *found, int64_t n) {
+  // Giant steps are taken CH at a time in Jacobian coordinates and normalised
+  // with ONE field inversion (Montgomery's simultaneous-inversion trick):
+  // ~20 Fp multiplications per giant step instead of ~300.
+  constexpr int CH = 8;
+  auto op = [=] __host__ __device__(int64_t i) {
+    G1J cur = at<G1J>(targets_jac, i);
+    G1A gneg = aneg(at<G1A>(giant_aff, 0));
+    found[i] = 0;
+    out[i] = 0;
+    for (int64_t g0 = 0; g0 < n_giant; g0 += CH) {
+      G1J pts[CH];
+      Fp pre[CH];
+      Fp acc = Fp::one();
+      for (int c = 0; c < CH; c++) {
+        pts[c] = cur;
+        Fp z = cur.is_inf() ? Fp::one() : cur.z;
+        acc = fmul(acc, z);
+        pre[c] = acc;
+        cur = jadd_mixed(cur, gneg);
+      }
+      Fp inv = finv(acc);
+      int64_t best = -1;
+      int64_t best_val = 0;
+      for (int c = CH - 1; c >= 0; c--) {
+        Fp z = pts[c].is_inf() ? Fp::one() : pts[c].z;
+        Fp zi = c ? fmul(inv, pre[c - 1]) : inv;
+        inv = fmul(inv, z);
+        int64_t g = g0 + c;
+        if (g >= n_giant) continue;
+        if (pts[c].is_inf()) {
+          best = g;
+          best_val = g * m_baby - offset;
+          continue;
+        }
+        Fp zi2 = fsqr(zi);
+        G1A a = {fmul(pts[c].x, zi2), fmul(fmul(pts[c].y, zi2), zi)};
+        uint64_t key = point_key(a);
+        uint64_t h = mix64(key) & (uint64_t)(cap - 1);
+        for (int64_t probe = 0; probe < cap; probe++) {
+          uint64_t kk = keys[h];
+          if (kk == 0) break;
+          if (kk == key) {
+            int64_t j = vals[h] >> 1;
+            bool same = (uint32_t)(vals[h] & 1) == (a.y.v[0] & 1u);
+            best = g;
+            best_val = g * m_baby + (same ? j : -j) - offset;
+            break;
+          }
+          h = (h + 1) & (uint64_t)(cap - 1);
+        }
+      }
+      if (best >= 0) {
+        out[i] = best_val;
+        found[i] = 1;
+        return;
+      }
+    }
+  };
+  return run(on_gpu, stream, n, op, true, "bsgs_solve");
+}
+
+
+int dx_version() { return 1; }
+}  // extern "C"

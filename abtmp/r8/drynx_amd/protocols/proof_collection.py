@@ -1,0 +1,564 @@
+"""ProofCollection: every proof request reaches the verifying nodes, which
+verify (sampled), persist, fill their bitmaps and append a ledger block.
+
+Reference: protocols/proof_collection_protocol.go — star tree prover root +
+all VNs (:84-305): each VN verifies, stores the proof in bbolt
+(``storeProof`` :307-406; bucket surveyID/type, key
+surveyID/type/sender/differInfo/VN; shuffle proofs are not stored), updates
+the bitmap, decrements the expected count; when done it persists its bitmap
+(bucket <VN>, key surveyID/map) and forwards it to the root VN, which builds
+the DataBlock and appends the skipchain (services/service_skipchain.go:96-158).
+
+MI355X mapping: the per-proof star broadcasts collapse into one personalised
+exchange of all requests to the ranks hosting VNs (xGMI all-to-all); each VN
+verifies every request it is assigned as one device batch; bitmaps and the
+block travel on the control plane.
+"""
+from __future__ import annotations
+
+import json
+import os
+import time
+
+import torch
+
+from .. import native as nt
+from ..ledger import skipchain as skc
+from ..parallel.netem import CT_BYTES, POINT_BYTES, SCALAR_BYTES, SIG_BYTES, flow_hops, range_proof_bytes
+from .data_collection import all_possible_groups as dcp_groups
+from ..parallel.comm import bytes_to_obj, obj_to_bytes
+from ..crypto.coins import Coins
+from ..proofs import requests as prq
+from ..query import query_to_proofs_nbrs
+from ..utils import timers
+from ..utils.log import get_logger
+
+log = get_logger("proof_collection")
+
+
+def expected_counts(sq) -> dict:
+    """QueryToProofsNbrs reordered to the VN order (service_skipchain.go:57-63)."""
+    q = query_to_proofs_nbrs(sq)
+    return dict(zip(prq.QUERY_ORDER, q))
+
+
+def _net_proofs(ctx, sq, reqs: list, vns: list):
+    """Every proof envelope from its prover to every VN (one hop, the
+    reference wire sizes of SURVEY 2.4)."""
+    n_groups = len(dcp_groups(sq.Query.DPDataGen.GroupByValues))
+    n_rows = n_groups * sq.Query.Operation.NbrOutput
+    S = len(sq.RosterServers.list)
+    sizes = {}
+    for r in reqs:
+        if r.kind == "range":
+            rg = sq.Query.Ranges or []
+            nb = sum(range_proof_bytes(int(x[0]), int(x[1]), S) for x in rg) * n_groups
+        elif r.kind == "aggregation":
+            nb = (len((sq.ServerToDP or {}).get(r.sender_id) or []) + 1) * n_rows * CT_BYTES
+        elif r.kind == "keyswitch":
+            nb = n_rows * (POINT_BYTES + CT_BYTES + 2 * POINT_BYTES + SCALAR_BYTES) + 4 * POINT_BYTES
+        elif r.kind == "obfuscation":
+            nb = n_rows * (3 * CT_BYTES + SCALAR_BYTES)
+        else:
+            nb = int(sq.Query.DiffP.NoiseListSize) * 3 * CT_BYTES
+        sizes[r.base_key()] = (r.sender_id, nb + SIG_BYTES)
+    ctx.net.step("proofs_to_vns", [(src, v.id, nb) for src, nb in sizes.values() for v in vns],
+                 hops=flow_hops("proofs_to_vns"))
+
+
+def pool_parts(ctx, sq) -> list:
+    """Every rank's pool part for this survey (``prq.balanced_parts``): ranks
+    hosting more DPs or a VN check shorter slices; identical on every rank
+    (a function of the placement only)."""
+    W = ctx.comm.world
+    dps, vns = [0] * W, [0] * W
+    for _, members in (sq.ServerToDP or {}).items():
+        for si in members or []:
+            dps[ctx.cluster.by_id(si.id).rank] += 1
+    for si in sq.Query.RosterVNs.list:
+        vns[ctx.cluster.by_id(si.id).rank] += 1
+    return prq.balanced_parts(W, dps, vns)
+
+
+def use_pool(ctx) -> bool:
+    """Pooled range verification (single-operator deployments only): every
+    rank checks a 1/world slice of every range-proof list on behalf of every
+    VN, with THAT VN's coins (a per-survey seed the VN hands out), so three
+    VNs keep eight GPUs busy; the VN's own rank keeps the signature checks,
+    the sampling decisions, the bitmap and the ledger, and accepts a helper's
+    slice verdict only if the helper's digest of the slice it checked equals
+    the VN's own digest of that slice of its signed payload.  On one GPU the
+    co-hosted VNs' batches share the decode and run back to back.
+    ``ctx.pool_policy`` (or DRYNX_VN_POOL) "0" leaves each VN's range checks
+    to the VN's own rank; a multi-party deployment (services/server.py)
+    forces that."""
+    pol = getattr(ctx, "pool_policy", None)
+    if pol is None:
+        pol = os.environ.get("DRYNX_VN_POOL", "1")
+    return str(pol) != "0"
+
+
+def fan_out(ctx, sq, local_requests: list, pool: bool = False) -> list:
+    """Every request to the ranks that host a VN; with ``pool``, the other
+    ranks get only THEIR slice of every range bundle (what they check for
+    the pool, ~1/W of the payload) plus the envelope header.  Payload
+    tensors (range bundles, packed per-CN proofs) travel as raw limbs in one
+    all-to-all with sizes announced by the control message (no size round);
+    envelopes and byte payloads ride on the control message."""
+    vns = [ctx.cluster.by_id(si.id) for si in sq.Query.RosterVNs.list]
+    W = ctx.comm.world
+    vn_ranks = sorted({v.rank for v in vns})
+    dests = list(range(W)) if pool else vn_ranks
+    seeds = {}
+    if pool:
+        # each local VN's per-survey seed for its pool helpers rides on this
+        # exchange (no control round of its own): helper k derives that VN's
+        # coins for its slice from it
+        seeds = {vn.id: ctx.vn_coins(vn.id).seed() for vn in vns if vn.rank == ctx.rank}
+        ctx.__dict__.setdefault("_pool_seeds", {})[sq.SurveyID] = seeds
+        if len(ctx._pool_seeds) > 64:
+            ctx._pool_seeds.pop(next(iter(ctx._pool_seeds)))
+    if W == 1:
+        return list(local_requests)
+    per_rank = {d: [] for d in dests}
+    per_rank_t = {d: [] for d in dests}
+    packed = {}
+    parts = pool_parts(ctx, sq) if pool else None
+    for idx, r in enumerate(local_requests):
+        assigned = prq.assigned_vns(sq, r, len(vns))
+        full_ranks = set(vn_ranks) if (assigned is None or pool) else {vns[i].rank for i in assigned}
+        for d in dests:
+            if d == ctx.rank:
+                continue
+            if d not in full_ranks:
+                if pool and r.kind == "range" and r.obj is not None and d not in vn_ranks:
+                    # a helper: its slice of the bundle (the pool's part d of W)
+                    sl = _helper_slice(r.obj, sq, parts[d])
+                    w = r.header().to_wire()
+                    if sl:
+                        t = prq.range_bundle_pack(sl).to(ctx.device)
+                        w["tensor"], w["slice"] = t.numel(), list(parts[d])
+                        per_rank_t[d].append(t)
+                    per_rank[d].append(w)
+                else:
+                    per_rank[d].append(r.header().to_wire())
+            elif r.tensor is not None and r._data is None:
+                if idx not in packed:
+                    packed[idx] = r.tensor.to(ctx.device)
+                w = r.header().to_wire()
+                w["digest"], w["tensor"] = b"", packed[idx].numel()
+                per_rank[d].append(w)
+                per_rank_t[d].append(packed[idx])
+            else:
+                per_rank[d].append(r.to_wire())
+    got = ctx.comm.exchange_bytes({d: obj_to_bytes({"w": per_rank[d], "seeds": seeds})
+                                   for d in dests if d != ctx.rank})
+    msgs = {src: bytes_to_obj(b) for src, b in got.items()}
+    wires = {src: m["w"] for src, m in msgs.items()}
+    if pool:
+        for m in msgs.values():
+            seeds.update(m["seeds"])
+    tens = {d: t for d, t in zip([d for d in dests if per_rank_t[d]],
+                                  nt.cat_rows([per_rank_t[d] for d in dests if per_rank_t[d]]))}
+    # the envelopes announced every tensor's size: no size round for the payloads
+    sizes = {src: sum(w.get("tensor") or 0 for w in ws) for src, ws in wires.items()}
+    got_t = ctx.comm.exchange(tens, recv_sizes={s_: n_ for s_, n_ in sizes.items() if n_})
+    out = []
+    for src in sorted(set(wires) | {ctx.rank}):
+        if src == ctx.rank:
+            out += list(local_requests)  # keep decoded objects for locally produced proofs
+            continue
+        off = 0
+        for w in wires[src]:
+            req = prq.ProofRequest.from_wire(w)
+            n = w.get("tensor")
+            if n:
+                t = got_t[src][off: off + n]
+                off += n
+                if w.get("slice"):
+                    # helper copy: the payload is this slice; the digest stays the signed one
+                    req._data, req.tensor, req.slice_of = None, t, tuple(w["slice"])
+                else:
+                    req.set_tensor(t)  # signed bytes: the VN re-hashes and decodes them on its device
+            out.append(req)
+    return out
+
+
+def _helper_slice(lists, sq, part) -> list:
+    """What the prover sends pool helper ``part[0]`` (tests substitute an
+    equivocating prover here)."""
+    return prq.slice_lists(lists, sq, part)
+
+
+def pool_verify_ranges(ctx, sq, reqs: list, vns: list, comm=None, arrived: float | None = None) -> dict:
+    """Pooled range verification (see ``use_pool``).  Each VN's rank decides
+    that VN's sampling (reference ``rand.Float64() <= Threshold``, from the
+    VN's own coins, or the sharding extension) and draws a per-survey seed;
+    rank k checks slice k/W of the sampled prefix of every list for every VN
+    with coins derived from that VN's seed, and reports its verdicts with
+    the digest of each slice it checked.  Each VN's rank then accepts a
+    helper's slice verdict only when the digest matches its own digest of
+    that slice of the signed payload, and re-checks any other slice itself.
+    ``<vn>_VerifyRange`` (structs_proofs.go:137) runs from ``arrived`` (the
+    VN's inbox: the range fan-out's end on its rank) to that VN's own verdict
+    (after its digest checks and any slice it re-checked).
+    -> {vn_id: {base_key: None (not sampled) | bool}} on every rank."""
+    comm = comm or ctx.comm
+    W, k = comm.world, comm.rank
+    rng = [i for i, r in enumerate(reqs) if r.kind == "range" and not r.header_only]
+    # every VN's seed arrived with the fan-out; the helpers check every list a
+    # VN may sample (the sharding extension's assignment is public; a random
+    # Threshold sample stays the VN's own decision, applied to the verdicts
+    # below) -- no control round before the checks
+    seeds = getattr(ctx, "_pool_seeds", {}).pop(sq.SurveyID, {})
+    missing = [vn.id for vn in vns if vn.id not in seeds]
+    if missing:
+        raise RuntimeError(f"pool: no fan-out seed for {missing} (survey {sq.SurveyID})")
+
+    def may_check(i, vi):
+        a_ = prq.assigned_vns(sq, reqs[i], len(vns))
+        return a_ is None or vi in a_
+    vn_idxs = {vn.id: [i for i in rng if may_check(i, vi)] for vi, vn in enumerate(vns)}
+    sampled = {vn.id: {reqs[i].base_key(): prq.should_verify(sq, reqs[i], vi, len(vns), ctx.vn_coins(vn.id))
+                       for i in rng} for vi, vn in enumerate(vns) if vn.rank == ctx.rank}
+    part_coins = {vn.id: Coins(seeds[vn.id]).derive(("slice", k, W)) for vn in vns}
+    parts = pool_parts(ctx, sq)
+    t0 = arrived if arrived is not None else time.perf_counter()
+    local_vns = [vn for vn in vns if vn.rank == ctx.rank]
+    # a VN rank's digests of the other ranks' slices of its own payloads run
+    # beside this rank's pool part (their own thread and stream: the part's
+    # latency-bound kernels leave the GPU room), not after the gather
+    exp_f = _expected_async(ctx, sq, reqs, vn_idxs, local_vns, W, parts) \
+        if local_vns and W > 1 else None
+    res, digests = prq.verify_range_pool_part(reqs, vn_idxs, sq, ctx.device, ctx.verifier_cache, parts[k],
+                                              part_coins, async_digests=True)
+    if hasattr(digests, "result"):
+        digests = digests.result()
+    mine = {vn.id: {reqs[i].base_key(): bool(ok) for i, ok in res.get(vn.id, {}).items()} for vn in vns}
+    mydig = {reqs[i].base_key(): d for i, d in digests.items()}
+    gathered = comm.all_gather_object((mine, mydig))
+    out = {}
+    if local_vns:
+        trusted = _check_helper_digests(ctx, sq, reqs, vn_idxs, local_vns, gathered, W,
+                                        exp_f.result() if exp_f is not None else None, parts)
+    for vn in vns:
+        if vn.rank != ctx.rank:
+            continue
+        verdict = {}
+        for key, smp in sampled[vn.id].items():
+            if not smp:
+                verdict[key] = None
+                continue
+            verdict[key] = all(gathered[j][0][vn.id].get(key, False) for j in range(W)
+                               if (key, j) in trusted[vn.id])
+        # slices whose helper digest did not match: this VN checks them itself
+        redo = trusted[vn.id].get("redo", {})
+        if redo:
+            with timers.span("rp.verify.pool_redo"):
+                c = ctx.vn_coins(vn.id)
+                for j, idxs in redo.items():
+                    r2, _ = prq.verify_range_pool_part(reqs, {vn.id: idxs}, sq, ctx.device, ctx.verifier_cache,
+                                                       parts[j], {vn.id: c})
+                    for i, ok in r2[vn.id].items():
+                        key = reqs[i].base_key()
+                        verdict[key] = bool(verdict.get(key)) and bool(ok)
+        out[vn.id] = verdict
+        timers.record(f"{vn.id}_VerifyRange", time.perf_counter() - t0)
+    return out
+
+
+def _expected_async(ctx, sq, reqs, vn_idxs: dict, local_vns: list, W: int, parts: list):
+    """``_expected_digests`` as an idle task of this rank's pool part (run
+    while its verifier waits for the device, on a HIP stream of its own
+    ordered after the caller's, where the payloads were received): no second
+    thread contending for the GIL with the part's host work."""
+    from ..proofs import range_proof as rp
+
+    if ctx.device.type != "cuda":
+        return rp.add_idle_task(rp.Deferred(lambda: _expected_digests(ctx, sq, reqs, vn_idxs, local_vns, W, parts)))
+    if not hasattr(ctx, "_dig_stream"):
+        ctx._dig_stream = torch.cuda.Stream(ctx.device)
+    st, cur = ctx._dig_stream, torch.cuda.current_stream(ctx.device)
+    st.wait_stream(cur)
+
+    def run():
+        with torch.cuda.stream(st):
+            return _expected_digests(ctx, sq, reqs, vn_idxs, local_vns, W, parts)
+    return rp.add_idle_task(rp.Deferred(run))
+
+
+def _expected_digests(ctx, sq, reqs, vn_idxs: dict, local_vns: list, W: int, parts: list | None = None):
+    """Digests of every other rank's slice of the local VNs' signed payloads
+    -> ({(request, part): digest}, {(request, part) with an empty slice})."""
+    me = ctx.rank
+    need = sorted({i for vn in local_vns for i in vn_idxs[vn.id]}) if W > 1 else []
+    expected: dict = {}
+    empty: set = set()  # (request, part) whose slice is empty: nothing to check there
+    with timers.span("rp.verify.expected_digests"):
+        entries, keys = [], []
+        for i in need:
+            try:
+                lists = prq._range_lists(reqs[i], ctx.device)
+            except Exception:  # noqa: BLE001 -- undecodable: every slice is redone (and fails)
+                continue
+            for j in range(W):
+                if j == me:
+                    continue  # this rank's own part was checked from this very payload
+                sl = prq.slice_lists(lists, sq, parts[j] if parts is not None else (j, W))
+                if not sl:
+                    empty.add((i, j))
+                    continue
+                entries.append(sl)
+                keys.append((i, j))
+        for key, d in zip(keys, prq.lists_digests(entries)):
+            expected[key] = d
+    return expected, empty
+
+
+def _check_helper_digests(ctx, sq, reqs, vn_idxs: dict, local_vns: list, gathered: list, W: int,
+                          pre=None, parts: list | None = None) -> dict:
+    """For each local VN: the (base_key, part) pairs whose helper-reported
+    slice digest equals the digest of that slice of the VN's own signed
+    payload, and the mismatches to redo ({part: [request index]}).
+    ``pre``: the (expected, empty) of ``_expected_digests`` computed earlier."""
+    me = ctx.rank
+    expected, empty = pre if pre is not None else _expected_digests(ctx, sq, reqs, vn_idxs, local_vns, W, parts)
+    out = {}
+    for vn in local_vns:
+        ok_pairs, redo = set(), {}
+        for i in vn_idxs[vn.id]:
+            bk = reqs[i].base_key()
+            for j in range(W):
+                if j == me or (i, j) in empty or (expected.get((i, j)) is not None
+                                       and gathered[j][1].get(bk) == expected[(i, j)]):
+                    ok_pairs.add((bk, j))
+                else:
+                    redo.setdefault(j, []).append(i)
+        ok_pairs_d = {p_: True for p_ in ok_pairs}
+        ok_pairs_d["redo"] = redo
+        out[vn.id] = ok_pairs_d
+    return out
+
+
+def _pool_async(ctx, sq, reqs, vns, comm=None):
+    """pool_verify_ranges on a worker thread with its own HIP stream: the
+    range batches (the GPU's long pole) run while this thread checks the
+    short per-CN proofs of each VN.  On a multi-rank node the worker also
+    owns the pool's collectives (the main thread issues none meanwhile)."""
+    import concurrent.futures as cf
+
+    if not hasattr(ctx, "_pool_exec"):
+        ctx._pool_exec = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="drynx-vn-pool")
+    arrived = time.perf_counter()  # the fan-out just delivered the VNs' inboxes
+    if ctx.device.type != "cuda":
+        return ctx._pool_exec.submit(pool_verify_ranges, ctx, sq, reqs, vns, comm, arrived)
+    if not hasattr(ctx, "_pool_stream"):
+        ctx._pool_stream = torch.cuda.Stream(ctx.device)
+    side, main = ctx._pool_stream, torch.cuda.current_stream(ctx.device)
+    side.wait_stream(main)
+
+    def run():
+        with torch.cuda.stream(side):
+            out = pool_verify_ranges(ctx, sq, reqs, vns, comm, arrived)
+        side.synchronize()
+        return out
+
+    return ctx._pool_exec.submit(run)
+
+
+def verify_and_store(ctx, sq, vn, vn_index: int, n_vns: int, requests: list, range_pooled=None) -> dict:
+    return store_verdicts(ctx, sq, vn, requests, check_requests(ctx, sq, vn, vn_index, n_vns, requests, range_pooled))
+
+
+def check_requests(ctx, sq, vn, vn_index: int, n_vns: int, requests: list, range_pooled=None):
+    """VerifyProof over one VN's inbox; with pooled range checks the range
+    codes are left pending (``codes`` holds a resolver) so the VN's short
+    per-CN checks run while the pooled batch is still on the GPU."""
+    return prq.verify_requests(requests, sq, vn.id, vn_index, n_vns, ctx.device, ctx.verifier_cache, range_pooled,
+                               defer=True, coins=ctx.vn_coins(vn.id))
+
+
+def store_verdicts(ctx, sq, vn, requests: list, pending) -> dict:
+    """storeProof for every request of the inbox: bitmap entry, ledger write
+    (surveyID/type bucket, shuffle proofs not stored), expected-count check
+    and the VN's bitmap (proof_collection_protocol.go:307-406)."""
+    codes = pending() if callable(pending) else pending
+    store = ctx.store(vn.id)
+    bitmap = {}
+    counts = {k: 0 for k in prq.VN_ORDER}
+    stored = [req for req in requests if req.kind != "shuffle"]  # storeProof skips shuffle proofs (:318-331)
+    values = dict(zip(map(id, stored), ctx.ledger_values(stored)))
+    for req, code in zip(requests, codes):
+        key = req.key(vn.id)
+        bitmap[key] = code
+        counts[req.kind] += 1
+        if req.kind != "shuffle":
+            store.update_async(f"{sq.SurveyID}/{req.kind}", key, values[id(req)])
+    exp = expected_counts(sq)
+    for k in prq.VN_ORDER:
+        if counts[k] != exp[k]:
+            log.warning(f"{vn.id}: received {counts[k]} {k} proofs, expected {exp[k]}")
+    store.update_async(vn.id, f"{sq.SurveyID}/map", json.dumps(bitmap, sort_keys=True).encode())
+    ctx.local_bitmaps[(sq.SurveyID, vn.id)] = bitmap
+    return bitmap
+
+
+def start_range_plane(ctx, sq, range_requests: list) -> dict:
+    """The range-proof plane, started as soon as this rank's range proofs are
+    signed (the reference streams them to the VNs while the CNs aggregate,
+    data_collection_protocol.go:278-348): their fan-out on the data plane
+    (main thread: every RCCL collective stays on one thread), then the pooled
+    verification on a worker with its own HIP stream and its own control
+    group (``Comm.plane("pool")``), overlapping the CN phases."""
+    vns = [ctx.cluster.by_id(si.id) for si in sq.Query.RosterVNs.list]
+    with timers.timed("RangeFanOut"):
+        reqs = fan_out(ctx, sq, range_requests, pool=True)
+    out = {"reqs": reqs, "pooled": _pool_async(ctx, sq, reqs, vns, ctx.comm.plane("pool"))}
+    if any(vn.rank == ctx.rank for vn in vns) and hasattr(ctx, "ledger_values"):
+        # the stored payloads' device-to-host copy starts now, under the pooled
+        # verification, instead of at the verdicts (store_verdicts finds them
+        # in the rank's blob segment); payloads whose digest is not known yet
+        # (received ones: a digest here would wait for the exchange) go then
+        with timers.span("ledger.prefetch"):
+            ctx.ledger_values([r for r in reqs if r.kind == "range" and r.data_digest])
+    return out
+
+
+def early_plane_ok(ctx, sq) -> bool:
+    """The range plane starts before the CN phases when verification is pooled
+    (single operator), the survey has VNs and proofs, and there are range
+    proofs to verify: with ranges (0, 0) the DPs ship commitments only, and
+    starting the plane early would just put their signing and fan-out on the
+    CN phases' thread instead of beside them."""
+    q = sq.Query
+    return bool(q.Proofs) and q.RosterVNs is not None and len(q.RosterVNs.list) > 0 \
+        and any(r[0] and r[1] for r in (q.Ranges or [])) \
+        and use_pool(ctx) and os.environ.get("DRYNX_RANGE_PLANE", "1") != "0"
+
+
+def proof_collection(ctx, sq, local_requests: list, early: dict | None = None, late=None):
+    """Returns the new SkipBlock (on every rank).  ``early``: the range plane
+    started by ``start_range_plane`` (its requests and pooled verdicts);
+    ``local_requests`` then holds the remaining (per-CN) proofs.  ``late``: a
+    callable returning the proofs still being finished (the key-switch proofs
+    of the last CN phase): the VNs check everything else first, then fan out
+    and check these -- as the reference's VNs verify each proof as it arrives
+    (proof_collection_protocol.go:183-305) -- and store one bitmap."""
+    vns = [ctx.cluster.by_id(si.id) for si in sq.Query.RosterVNs.list]
+    pool = use_pool(ctx)
+    with timers.timed("ProofFanOut"):
+        reqs = fan_out(ctx, sq, local_requests, pool=pool and early is None)
+    if early is not None:
+        reqs = early["reqs"] + reqs
+    bitmaps = {}
+    with timers.timed("ProofVerification"):
+        if early is not None:
+            pooled = early["pooled"]
+        else:
+            pooled = _pool_async(ctx, sq, reqs, vns) if pool else None
+        local_vns = [vn.id for vn in vns if vn.rank == ctx.rank]
+
+        def checks(rs, range_pooled):
+            if len(local_vns) > 1:  # co-hosted VNs: their signature checks in one host batch
+                prq.prewarm_signatures(rs, sq, local_vns, ctx.verifier_cache)
+                with timers.span("verify.keyswitch.multi"):  # one grouped key-switch MSM for all of them
+                    prq.prewarm_keyswitch(rs, sq, local_vns, ctx.device, ctx.verifier_cache,
+                                          {v: ctx.vn_coins(v) for v in local_vns})
+            return {vn.id: check_requests(ctx, sq, vn, idx, len(vns), rs, range_pooled)
+                    for idx, vn in enumerate(vns) if vn.rank == ctx.rank}
+
+        pending = checks(reqs, pooled)
+        reqs2, pending2 = [], {}
+        if late is not None:
+            with timers.timed("ProofFanOut"):
+                reqs2 = fan_out(ctx, sq, late(), pool=False)
+            pending2 = checks(reqs2, None)
+        for vn in vns:
+            if vn.id in pending:
+                codes = pending[vn.id]()
+                if vn.id in pending2:
+                    codes = list(codes) + list(pending2[vn.id]())
+                bitmaps[vn.id] = store_verdicts(ctx, sq, vn, reqs + reqs2, codes)
+        if pooled is not None:
+            pooled.result()
+    reqs = reqs + reqs2
+    if getattr(ctx, "net", None) is not None:
+        _net_proofs(ctx, sq, reqs, vns)
+    # bitmaps -> root VN (SharedBMChannel): every rank gets every VN's bitmap
+    # plus the root VN's block parameters (its timestamp; its chain head when
+    # it resumed from its ledger) and builds the same block itself -- no
+    # broadcast round for the block
+    root = vns[0]
+    mine = {"bm": bitmaps}
+    if ctx.rank == root.rank:
+        resumed = None
+        if ctx.last_block is None:
+            # resume an existing chain from the root VN's ledger (restart of a
+            # node over a persisted workdir) instead of starting a new genesis
+            ctx.last_block = ctx.get_latest_block(root.id)
+            resumed = ctx.last_block.to_bytes() if ctx.last_block is not None else None
+        mine["root"] = {"time": time.time(), "prev": resumed}
+    allbm, rootp = {}, None
+    for d in ctx.comm.all_gather_object(mine):
+        allbm.update(d["bm"])
+        rootp = d.get("root", rootp)
+    if hasattr(ctx, "take_proof_starts"):
+        # the VNs' verdicts are back on every DP's rank: the reference's
+        # <dp>_AllProofs ends here (its proof collection's feedback channel,
+        # data_collection_protocol.go:343-345)
+        now = time.perf_counter()
+        for dp_id, t_start in ctx.take_proof_starts(sq.SurveyID).items():
+            timers.record(f"{dp_id}_AllProofs", now - t_start)
+    t = timers.start_timer("BI", sync=False)
+    merged = {}
+    for vn in vns:
+        merged.update(allbm.get(vn.id, {}))
+    data = skc.new_data_block(sq.SurveyID, merged, [v.identity() for v in vns], t=rootp["time"])
+    prev = ctx.last_block
+    if rootp["prev"] is not None and ctx.rank != root.rank:
+        prev = skc.SkipBlock.from_bytes(rootp["prev"])
+    block = skc.make_block(prev, data, [v.identity() for v in vns])
+    # every VN runs its verifiers (verifyFuncBitmap, VerifyBase against its own
+    # latest block), then signs the block and the forward link from its latest
+    signers = []
+    for vn in vns:
+        if vn.rank == ctx.rank:
+            prev = ctx.vn_latest(vn.id)
+            if skc.verify_bitmap(block, ctx.local_bitmaps.get((sq.SurveyID, vn.id), {}), vn.id) \
+                    and skc.verify_base(prev, block):
+                signers.append((vn.id, vn.keypair.secret, prev))
+            else:
+                log.warning(f"{vn.id} refused block for survey {sq.SurveyID}")
+    sigs, links = skc.cosign_many(block, signers)  # the co-hosted VNs' partials in one batch
+    for d, fl in ctx.comm.all_gather_object((sigs, links)):
+        block.ForwardSignatures.update(d)
+        links.update(fl)
+    skc.finalize_cosig(block)  # BLS collective signature of the VN roster
+    for vn in vns:
+        if vn.rank == ctx.rank:
+            # proof blobs keep persisting on the store's writer thread (GetProofs /
+            # CloseDB flush); the block only depends on the bitmap
+            st = ctx.store(vn.id)
+            prev = ctx.vn_latest(vn.id)
+            if prev is not None and links:
+                skc.add_forward_link(prev, block.Hash, links)   # stored with the previous block
+                st.update_async("skipchain", prev.Hash, prev.to_bytes())
+            ctx.set_vn_latest(vn.id, block)
+            raw = block.to_bytes()
+            st.update_async("skipchain", block.Hash, raw)
+            st.update_async("skipchain", "latest", raw)
+            if block.Index == 0:
+                st.update_async("genesis", "genesis", raw)
+            st.update_async("mapping", sq.SurveyID, block.Hash.encode())
+    ctx.last_block = block
+    timers.end_timer(t)
+    if getattr(ctx, "net", None) is not None:
+        ids = [v.id for v in vns]
+        bsz = len(block.to_bytes())
+        ctx.net.step("bitmaps", [(i, ids[0], 64 * len(allbm.get(i, {})) + 64) for i in ids[1:]],
+                     hops=flow_hops("bitmaps"))
+        ctx.net.step("skipchain", [(ids[0], i, bsz) for i in ids[1:]] + [(i, ids[0], SIG_BYTES) for i in ids[1:]],
+                     hops=flow_hops("skipchain", n_vns=len(ids), genesis=block.Index == 0))
+        ctx.net.step("end_verification", [(ids[0], "client", bsz)], hops=flow_hops("end_verification"))
+    ctx.end_verification(sq.SurveyID, block)  # EndVerificationChannel <- block (service_skipchain.go:158)
+    return block

@@ -1,0 +1,30 @@
+"""Stream priorities of the framework's HIP streams.
+
+``priority(p)`` is the priority a stream asks for; DRYNX_STREAM_PRIO=0 turns
+every request into the normal priority.  ROCm gives each priority level its
+own hardware queue, so only then does a measurement run with
+GPU_MAX_HW_QUEUES=1 and AMD_SERIALIZE_KERNEL=3 put every stream on ONE queue
+and run every kernel alone on the chip (tools/gpu/r4_spans.sh: per-kernel
+costs with no overlap inflation)."""
+from __future__ import annotations
+
+import os
+
+
+def priority(p: int) -> int:
+    return 0 if os.environ.get("DRYNX_STREAM_PRIO", "1") == "0" else int(p)
+
+
+NODE_SWITCH_INTERVAL = 0.0005
+
+
+def node_process_setup():
+    """Process-wide settings for a process whose job is to run a node (bench,
+    ``server run``; a library user's process is left alone): a 0.5 ms GIL
+    switch interval, so the node's worker threads (ledger writers, CN-proof
+    finishing, the pool, the querier) hand the interpreter back to the
+    query's thread sooner than Python's 5 ms (--u 0 --l 0 25.8-28.2 ->
+    23.4-23.9 ms on one box, the headline unchanged: profiles/r4/serial/v_*.json)."""
+    import sys
+
+    sys.setswitchinterval(NODE_SWITCH_INTERVAL)

@@ -1,0 +1,1 @@
+"""onet wire format: dedis/protobuf codec, message envelopes, struct converters."""
