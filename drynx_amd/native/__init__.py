@@ -107,7 +107,7 @@ _SIGS = {
     "dx_gt_slice_prod": [_I, _P, _P, _P, _P, _P, _P, _L],
     "dx_gt_chunk_weight": [_I, _P, _P, _P, _P, _P, _P, _P, _L],
     "dx_g1_mul_glv": [_P, _P, _P, _P, _P, _L, _I],
-    "dx_rp_u_joint_split": [_I, _P, _P, _P, _P, _L, _I, _I, _L, _I, _P],
+    "dx_rp_u_joint_split": [_I, _P, _P, _P, _P, _L, _I, _I, _L, _I, _P, _P],
     "dx_bucket_bounds": [_I, _P, _P, _L, _L, _P, _P],
     "dx_slice_desc": [_I, _P, _P, _P, _P, _I, _L, _L, _P, _P],
     "dx_lane_slices": [_I, _P, _P, _P, _P, _P, _P, _L, _P, _P],
@@ -150,7 +150,7 @@ _SIGS = {
     "dx_gt_gls6_pow": [_I, _P, _P, _P, _P, _P, _L],
     "dx_rp_prove_a_gls6": [_I, _P, _P, _P, _P, _P, _P, _P, _L, _I, _I],
     "dx_g2_joint_table": [_I, _P, _P, _P, _L],
-    "dx_rp_u_joint": [_I, _P, _P, _P, _P, _L, _I, _I, _L],
+    "dx_rp_u_joint": [_I, _P, _P, _P, _P, _L, _I, _I, _L, _P],
     "dx_g2_slice_sum": [_I, _P, _P, _P, _P, _P, _P, _L, _I, _L],
     "dx_g2_mul_small": [_I, _P, _P, _P, _P, _L],
     "dx_g2_horner": [_I, _P, _P, _P, _I, _I, _I, _L, _L],
@@ -2102,11 +2102,16 @@ def g2_joint_table(V_aff: torch.Tensor) -> torch.Tensor:
 
 
 def rp_u_joint(table: torch.Tensor, ab: torch.Tensor, n_groups: int, G: int, L: int, out: torch.Tensor,
-               pad: int) -> torch.Tensor:
+               pad: int, pos: torch.Tensor | None = None) -> torch.Tensor:
     """out[v*pad + q] = affine(sum_j (a + b lambda)_{v, q*L+j} V_{q*L+j}) for every
-    verifier v < G and group q < n_groups (ab [G * n_groups * L, 2] int32)."""
+    verifier v < G and group q < n_groups (ab [G * n_groups * L, 2] int32);
+    ``pos`` (int64 [G * n_groups], rows of ``out``): the row of (v, q) instead."""
     assert _rows(table, 32) == n_groups * L * G2_JOINT_ENTRIES and _rows(ab, 2) == G * n_groups * L
-    assert _rows(out, 32) >= (G - 1) * pad + n_groups and pad >= n_groups and out.is_contiguous()
+    assert out.is_contiguous() and pad >= n_groups
+    if pos is None:
+        assert _rows(out, 32) >= (G - 1) * pad + n_groups
+    else:
+        assert pos.dtype == torch.int64 and pos.numel() == G * n_groups and pos.device == out.device
     g, s = _ctx(table, ab, out)
     # a small batch (a pool helper's 1/W slice) splits each combination over
     # 2 or 4 threads so the launch still fills the chip (~2 waves per SIMD)
@@ -2116,9 +2121,9 @@ def rp_u_joint(table: torch.Tensor, ab: torch.Tensor, n_groups: int, G: int, L: 
     if sp > 1:
         tmp = torch.empty((n * sp, 48), dtype=torch.int32, device=out.device)
         _call("dx_rp_u_joint_split", g, s, _ptr(table), _ptr(ab.contiguous()), _ptr(out), n_groups, G, L, pad, sp,
-              _ptr(tmp))
+              _ptr(tmp), _ptr(pos))
         return out
-    _call("dx_rp_u_joint", g, s, _ptr(table), _ptr(ab.contiguous()), _ptr(out), n_groups, G, L, pad)
+    _call("dx_rp_u_joint", g, s, _ptr(table), _ptr(ab.contiguous()), _ptr(out), n_groups, G, L, pad, _ptr(pos))
     return out
 
 

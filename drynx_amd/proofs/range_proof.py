@@ -960,22 +960,26 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
         wc = nt.fr_arith(nt.FR_MUL, w_all, r.challenge)
         dsc = torch.stack([wc.view(G, n, 8), w_all.view(G, n, 8)], 1).reshape(-1, 8).contiguous()
     aux = _aux_stream(device) if device.type == "cuda" else None
-    ready = None
+    meta = (G, m, S, l, gb, tuple(wc_), _r_window(m, G))
+    # GPU: the R MSM's launches first on the aux stream (its device chain --
+    # plan, bucket sums, weights -- is as long as the U side's), then the U
+    # side on this stream (the Miller-loop chain), then the multi-exponentiation
+    # and the D-check behind the R MSM: both chains start within ~2 ms of the
+    # weights instead of the aux one waiting ~7 ms for its host launches
     if aux is not None:
         ready = torch.cuda.Event()
         ready.record(torch.cuda.current_stream(device))
-        # the U side first, on this stream: its chain of Miller-loop kernels is
-        # the critical path of a small batch (a pool slice)
+        aux.wait_event(ready)
+        with timers.span("rp.verify.passes"), torch.cuda.stream(aux):
+            S_R, hR = _pass_r(r.V, r.zphi, rho_all, meta)
         with timers.span("rp.verify.msm_queue"):
             msq = _msm_queue(Y, r.V, ab_all, G, n, S, l, vstream, segs, table)
             for v, uok in zip(vns, msq["u_ok"]):
                 v["u_ok"] = uok
-        aux.wait_event(ready)
-    # the R MSM, the multi-exponentiation and the exponent sums on the aux
-    # stream with device-resident bucket plans (no host sync), then the D-check
+    else:
+        S_R, hR = _pass_r(r.V, r.zphi, rho_all, meta)
     with timers.span("rp.verify.passes"), (torch.cuda.stream(aux) if aux is not None else _nullctx()):
-        S_R, hR, A2, mexp, e_all, dfull = _verify_passes(r.V, r.A, r.zphi, rho_all, ab_all, gam_all, r.zv, w_all,
-                                                         r.zr, z, (G, m, S, l, gb, tuple(wc_), _r_window(m, G)))
+        A2, mexp, e_all, dfull = _pass_me(r.A, ab_all, gam_all, rho_all, r.zv, w_all, r.zr, z, meta)
         with timers.span("rp.run.D"):
             if ddirect:
                 if cC is None:                                                 # host path
@@ -1129,25 +1133,26 @@ class _nullctx:
         return False
 
 
-def _verify_passes(V, A, zphi, rho, ab, gam, zv, w, zr, z, meta):
-    """The weight-dependent device passes of ``verify_range_proof_list_multi``
-    on the current stream, no host sync: R = sum (rho Zphi) V per VN (G2
-    Pippenger, device plan), the GT multi-exponentiation over (A, frob^8 A)
-    with the GLV halves of rho and the 40-bit membership combinations, and
-    the Fr exponent sums.  -> (S_R, hR, A2, mexp, e_all, dfull)."""
+def _pass_r(V, zphi, rho, meta):
+    """R = sum_it (rho_it Zphi_(p, j)) V_it per VN: the G2 Pippenger MSM with a
+    device plan, queued on the current stream (no host sync) -> (S_R, hR)."""
     G, m, S, l, gb, wc, cR = meta
-    dev = V.device
-    it = torch.arange(m, device=dev)
+    it = torch.arange(m, device=V.device)
     s_r = nt.fr_arith(nt.FR_MUL, rho, zphi.index_select(0, (it // (S * l)) * l + it % l).contiguous())
     with timers.span("rp.run.R"):
-        S_R, hR = nt.g2_msm_device(V, s_r, m, ((m, 254),) * G, c=cR)
+        return nt.g2_msm_device(V, s_r, m, ((m, 254),) * G, c=cR)
+
+
+def _pass_me(A, ab, gam, rho, zv, w, zr, z, meta):
+    """The GT multi-exponentiation over (A, frob^8 A) with the GLV halves of
+    rho (groups 0..G-1) and each VN's 40-bit membership combination (G..2G-1),
+    and the Fr exponent sums, on the current stream -> (A2, mexp, e_all, dfull)."""
+    G, m, S, l, gb, wc, cR = meta
+    dev = A.device
     with timers.span("rp.frob8"):  # (A, frob^8 A) stacked: the Frobenius image written in place
         A2 = torch.empty((2 * m, 96), dtype=torch.int32, device=dev)
         A2[:m].copy_(A)
         nt.gt_frob8(A.contiguous(), out=A2[m:])
-    # exponents: groups 0..G-1 prod a^rho_v = prod a^a' * frob^8(a)^b' (32-bit
-    # GLV halves over (A, frob^8 A)); groups G..2G-1 each VN's own GT-membership
-    # combination prod a^gamma_v (over A)
     abv = ab.view(G, m, 2)
     k = torch.zeros((3 * G * m, 8), dtype=torch.int32, device=dev)
     kr = k[: 2 * G * m].view(G, 2 * m, 8)
@@ -1162,7 +1167,7 @@ def _verify_passes(V, A, zphi, rho, ab, gam, zv, w, zr, z, meta):
     e_all = nt.fr_dot_rows(rho, zv, G, b_periodic=True)                                 # sum rho Zv per VN
     dfull = torch.stack([nt.fr_dot_rows(w, zr, G, b_periodic=True),
                          nt.fr_dot_rows(w, z, G, b_periodic=True)], 1)                   # [G, 2, 8]
-    return S_R, hR, A2, mexp, e_all, dfull
+    return A2, mexp, e_all, dfull
 
 
 _DCHECK_DIRECT_MAX = 16384  # proofs x VNs up to which the D-check runs without a bucket plan
@@ -1219,31 +1224,31 @@ def _msm_queue(Y, V, ab_all, G: int, n: int, S: int, L: int, vstream=None, segs:
         coop = K == 1 and G * pad <= _COOP_MAX_ITEMS
         Uall = torch.zeros((G * pad, 32), dtype=torch.int32, device=dev)
         UV = torch.zeros((period, 16), dtype=torch.int32, device=dev)
-        negY = None
+        pos = None
+        if nseg > 1:
+            # row of (VN v, group q) in the fold layout (segments start whole
+            # workgroups): host-known, one upload before the U kernels -- no
+            # index glue between the combinations and the fold's coefficients
+            qseg = np.repeat(np.arange(nseg), cq)
+            qpos = segbase[qseg] + np.arange(nq) - qoff[:-1][qseg]
+            pos = _h2d((np.arange(G).reshape(G, 1) * pad + qpos.reshape(1, nq)).reshape(-1).astype(np.int64), dev)
+        # the points of the fold (affine -Y_q, or uv(-Y_q) for the normalised
+        # lines) in place before the U combinations
         if coop:  # affine -Y_q, the same for every VN
             negY = nt.g1_to_affine(nt.g1_add(bn.g1_infinity_jac(nq, dev), Y.contiguous(), subtract=True))
+        elif nseg > 1:  # uv(-Y_q) is the same for every VN: computed once, copied per VN below
+            UVd = torch.zeros((nq + 1, 16), dtype=torch.int32, device=dev)
+            nt.rp_msm_uv(Y, UVd, nq, 1, nq + 1)
+            negY = UVd[:nq]
         if nseg == 1:
-            with timers.span("rp.u.joint"):
-                nt.rp_u_joint(table, ab_all, nq, G, L, Uall, pad)
             if coop:
                 UV[: G * pad].view(G, pad, 16)[:, :nq] = negY
             else:
                 nt.rp_msm_uv(Y, UV, nq, G, pad)
-            Ud = Uall
         else:
-            Ud = torch.empty((G * nq, 32), dtype=torch.int32, device=dev)
-            with timers.span("rp.u.joint"):
-                nt.rp_u_joint(table, ab_all, nq, G, L, Ud, nq)
-            if not coop:  # uv(-Y_q) is the same for every VN: computed once, copied per VN below
-                UVd = torch.zeros((nq + 1, 16), dtype=torch.int32, device=dev)
-                nt.rp_msm_uv(Y, UVd, nq, 1, nq + 1)
-                negY = UVd[:nq]
-            qseg = torch.repeat_interleave(torch.arange(nseg, device=dev), _h2d(cq, dev),
-                                           output_size=nq)
-            qpos = _h2d(segbase, dev)[qseg] + torch.arange(nq, device=dev) - _h2d(qoff[:-1], dev)[qseg]
-            pos = (torch.arange(G, device=dev).view(G, 1) * pad + qpos.view(1, nq)).reshape(-1)
-            Uall.index_copy_(0, pos, Ud)
             UV.index_copy_(0, pos, negY.repeat(G, 1))
+        with timers.span("rp.u.joint"):
+            nt.rp_u_joint(table, ab_all, nq, G, L, Uall, pad, pos)
         # G2 membership of every U (exact test), on the validation stream beside the fold
         cur = torch.cuda.current_stream(dev)
         vs = vstream if vstream is not None else cur
@@ -1252,10 +1257,13 @@ def _msm_queue(Y, V, ab_all, G: int, n: int, S: int, L: int, vstream=None, segs:
             # every read of the flags stays on the validation stream: a reduction
             # queued on `cur` would race the membership kernels (read before they
             # finish); the caller synchronises `vs` before looking at the verdicts
-            fl = nt.g2_subgroup(Ud).view(G, -1)[:, :nq].bool()
+            flags = nt.g2_subgroup(Uall)
+            fl = (flags.view(G, pad)[:, :nq] if pos is None else flags.index_select(0, pos).view(G, nq)).bool()
             out["u_seg"] = _seg_all(fl, cq, dev)
             out["u_ok"] = list(out["u_seg"].all(dim=1).unbind(0))
-        Ud.record_stream(vs)
+        Uall.record_stream(vs)
+        if pos is not None:
+            pos.record_stream(vs)
         with timers.span("rp.u.fold"):
             if coop:
                 out["fb"] = nt.rp_fold_accum_coop_raw(nt.rp_fold_coeffs(Uall), UV, Uall, period, 1)

@@ -73,6 +73,14 @@ def test_u_joint_combinations(device):
                     acc = O.g2_add(acc, _lam_mul(a, b, Q))
             assert got[v * pad + q] == acc, (v, q)
         assert got[v * pad + nq] is None                  # untouched rows stay infinity
+    # an explicit row per (v, q) (the segmented fold layout): the same points, permuted
+    perm = list(range(G * pad))
+    random.Random(9).shuffle(perm)
+    pos = torch.tensor(perm[: G * nq], dtype=torch.int64, device=dev)
+    out2 = torch.zeros((G * pad, 32), dtype=torch.int32, device=dev)
+    nt.rp_u_joint(nt.g2_joint_table(V), ab_t, nq, G, L, out2, pad, pos)
+    want = out.view(G, pad, 32)[:, :nq].reshape(-1, 32)
+    assert torch.equal(out2.index_select(0, pos), want)
 
 
 @pytest.mark.parametrize("device", DEVICES)
