@@ -961,24 +961,21 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
         dsc = torch.stack([wc.view(G, n, 8), w_all.view(G, n, 8)], 1).reshape(-1, 8).contiguous()
     aux = _aux_stream(device) if device.type == "cuda" else None
     meta = (G, m, S, l, gb, tuple(wc_), _r_window(m, G))
-    # GPU: the R MSM's launches first on the aux stream (its device chain --
-    # plan, bucket sums, weights -- is as long as the U side's), then the U
-    # side on this stream (the Miller-loop chain), then the multi-exponentiation
-    # and the D-check behind the R MSM: both chains start within ~2 ms of the
-    # weights instead of the aux one waiting ~7 ms for its host launches
+    # GPU: the U side first, on this stream (its chain of Miller-loop kernels
+    # is the critical path of a small batch), then the R MSM, the
+    # multi-exponentiation and the D-check on the aux stream.  (Launching the R
+    # MSM first measured neutral on the pool parts and +2.5 ms on the 1-GPU
+    # query: the two chains only slow each other down on the shared CUs.)
     if aux is not None:
         ready = torch.cuda.Event()
         ready.record(torch.cuda.current_stream(device))
-        aux.wait_event(ready)
-        with timers.span("rp.verify.passes"), torch.cuda.stream(aux):
-            S_R, hR = _pass_r(r.V, r.zphi, rho_all, meta)
         with timers.span("rp.verify.msm_queue"):
             msq = _msm_queue(Y, r.V, ab_all, G, n, S, l, vstream, segs, table)
             for v, uok in zip(vns, msq["u_ok"]):
                 v["u_ok"] = uok
-    else:
-        S_R, hR = _pass_r(r.V, r.zphi, rho_all, meta)
+        aux.wait_event(ready)
     with timers.span("rp.verify.passes"), (torch.cuda.stream(aux) if aux is not None else _nullctx()):
+        S_R, hR = _pass_r(r.V, r.zphi, rho_all, meta)
         A2, mexp, e_all, dfull = _pass_me(r.A, ab_all, gam_all, rho_all, r.zv, w_all, r.zr, z, meta)
         with timers.span("rp.run.D"):
             if ddirect:
