@@ -966,6 +966,7 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
     # multi-exponentiation and the D-check on the aux stream.  (Launching the R
     # MSM first measured neutral on the pool parts and +2.5 ms on the 1-GPU
     # query: the two chains only slow each other down on the shared CUs.)
+    ev_u = ev_r = None
     if aux is not None:
         ready = torch.cuda.Event()
         ready.record(torch.cuda.current_stream(device))
@@ -973,9 +974,14 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
             msq = _msm_queue(Y, r.V, ab_all, G, n, S, l, vstream, segs, table)
             for v, uok in zip(vns, msq["u_ok"]):
                 v["u_ok"] = uok
+        ev_u = torch.cuda.Event()                                       # the U side's fold is queued
+        ev_u.record(torch.cuda.current_stream(device))
         aux.wait_event(ready)
     with timers.span("rp.verify.passes"), (torch.cuda.stream(aux) if aux is not None else _nullctx()):
         S_R, hR = _pass_r(r.V, r.zphi, rho_all, meta)
+        if aux is not None:
+            ev_r = torch.cuda.Event()                                   # the R MSM is queued
+            ev_r.record(aux)
         A2, mexp, e_all, dfull = _pass_me(r.A, ab_all, gam_all, rho_all, r.zv, w_all, r.zr, z, meta)
         with timers.span("rp.run.D"):
             if ddirect:
@@ -993,9 +999,19 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
         msq = _msm_queue(Y, r.V, ab_all, G, n, S, l, None, segs)
         for v, uok in zip(vns, msq["u_ok"]):
             v["u_ok"] = uok
+    useg = fR = None
     with timers.span("rp.verify.multiexp"):
         if aux is not None:
             run_idle_tasks()  # host work queued by the caller, in the GPU's busiest window
+            # the host tails of the R side (Horner, ML(B, R)) and of the U side
+            # (per-segment products) as soon as their device chains are done,
+            # while the multi-exponentiation and the D-check still run
+            ev_r.synchronize()
+            with timers.span("rp.verify.r_tail"):
+                fR, rok = _msm_r_miller(hR, S_R)
+            ev_u.synchronize()
+            with timers.span("rp.verify.u_tail"):
+                useg = _seg_products(msq)                              # [G, nseg, 96] host
             aux.synchronize()                                          # aux results are read on this stream/host
         GG = nt.multi_exp_grouped_finish(mexp)                         # [2G, 96]: prod a^rho_v, prod a^gamma_v
         D_all = dcheck.cpu() if ddirect else nt.g1_msm_finish(dcheck)  # [2G, 24]
@@ -1003,10 +1019,12 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
             nt.check_overflow(h_)
         e_all, dfull = e_all.cpu(), dfull.cpu()
     with timers.span("rp.verify.fold_wait"):
-        useg = _seg_products(msq)                                      # [G, nseg, 96] host
+        if useg is None:
+            useg = _seg_products(msq)                                  # [G, nseg, 96] host
         for k_, v in enumerate(vns):
             v["F"] = nt.gt_prod(useg[k_].view(nseg, 1, 96), chunk=64).view(1, 96)
-        fR, rok = _msm_r_miller(hR, S_R)
+        if fR is None:
+            fR, rok = _msm_r_miller(hR, S_R)
         for v, f, ok in zip(vns, fR, rok):
             v["F"], v["r_ok"] = nt.gt_mul(v["F"], f.view(1, 96)), ok
     for k, v in enumerate(vns):
