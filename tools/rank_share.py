@@ -23,9 +23,12 @@ signed range-proof inbox, and then times, alone and synchronised (median of
   the block seed, co-signatures), from a ``tools/ctrl_round.py`` JSON of W
   processes (``--ctrl-json``), added in full to every rank (not overlapped).
 
-The projection per rank is max(serial on rank 0, prove + pool) + ctrl; the
-step is the max over ranks.  Peers' traffic over xGMI and waits on peers are
-not in it (the 8-GPU run measures those).
+Every rank's pool part starts when the range fan-out (ONE exchange after
+every rank has signed its proofs) completes, so the projected step is
+max(serial on rank 0, max_k prove(k) + max_k pool(k)) + ctrl
+(``projection_step_ms``); ``projection_ms`` keeps each rank's own
+prove + pool (+ ctrl), the bound without that synchronisation.  Peers'
+traffic over xGMI is not in it (the 8-GPU run measures it).
 Usage: python tools/rank_share.py [--world 8] [--reps 5] [--serial-json f] [--ctrl-json f]
 """
 from __future__ import annotations
@@ -297,8 +300,12 @@ def main():
         rng_path = v["prove_ms"] + v["pool_ms"]  # a VN rank's pool_ms includes its overlapped digests
         proj[k] = round(max(serial if k == 0 else 0.0, rng_path) + ctrl, 2)
     res["projection_ms"] = proj
-    res["projection_step_ms"] = max(proj.values())
-    print(json.dumps({"projection_ms": proj, "step_ms": res["projection_step_ms"]}), flush=True)
+    prove_max = max(v["prove_ms"] for v in res["ranks"].values())
+    pool_max = max(v["pool_ms"] for v in res["ranks"].values())
+    res["projection_step_ms"] = round(max(serial, prove_max + pool_max) + ctrl, 2)
+    res["projection_terms_ms"] = {"prove_max": prove_max, "pool_max": pool_max, "serial": serial, "ctrl": round(ctrl, 3)}
+    print(json.dumps({"projection_ms": proj, "step_ms": res["projection_step_ms"],
+                      "terms": res["projection_terms_ms"]}), flush=True)
     if a.json_out:
         json.dump(res, open(a.json_out, "w"), indent=1)
     node.close(remove=True)
