@@ -603,8 +603,9 @@ def sampled_bounds(sq, n: int, part=None) -> tuple:
 # the slowest rank's proving end -- so a rank proving an extra DP gets NO
 # discount (a discount only lengthened the other parts: profiles/r5/it15,
 # pool(share) ~ 13 ms + 122 ms x share); a VN rank's part also carries the
-# digests of the other slices (a side stream, ~0.3 ms of its part)
-_POOL_DP_W, _POOL_VN_W = 0.0, 0.02
+# digests of the other slices (a side stream: +2.2 ms of its part at equal
+# shares, profiles/r5/it16)
+_POOL_DP_W, _POOL_VN_W = 0.0, 0.14
 
 
 def balanced_parts(W: int, dps: list, vns: list) -> list:
