@@ -347,18 +347,22 @@ class DrynxNode:
             result = CipherVector.cat([result[g * n_out: g * n_out + per] for g in range(n_groups)])
             n_out = per
         timers.end_timer(t_exec)
-        client_future = None
+        client = {"f": None}
         # the last CN phase's proofs (key switching) are still being finished:
         # the VNs check every other proof first (pcp.proof_collection ``late``)
         late_f = proofs.pop() if proofs and hasattr(proofs[-1], "result") else None
         with timers.span("cn.proofs.wait"):
             proofs = self._resolve_proofs(proofs)
-        # the querier decodes beside the VNs' checks; it starts once the CN
-        # proofs the VNs check first are signed: its decryption kernels would
-        # otherwise hold the CUs the signing's short launches wait for, on the
-        # step's critical path
-        if on_result is not None and result is not None:
-            client_future = self._submit_client(on_result, SurveyResult(sq.SurveyID, result, n_groups, n_out))
+
+        def start_client():
+            # the querier decodes beside the VNs' checks; it starts once the
+            # key-switch proofs are signed: its decryption kernels would
+            # otherwise hold the CUs that the proof chain's short launches
+            # (transcript digests, signing) wait for, on the step's critical path
+            if on_result is not None and result is not None and client["f"] is None:
+                client["f"] = self._submit_client(on_result, SurveyResult(sq.SurveyID, result, n_groups, n_out))
+        if late_f is None:
+            start_client()
         if range_future is not None:
             proofs.extend(range_future.result())
             if hasattr(self, "_prove_stream"):
@@ -370,6 +374,7 @@ class DrynxNode:
         def late():
             with timers.span("cn.proofs.wait_late"):
                 out = self._resolve_proofs([late_f]) if late_f is not None else []
+            start_client()
             if self.fault_plan:
                 self.fault_plan.apply(out, secret_of)
             return out
@@ -379,10 +384,11 @@ class DrynxNode:
             block = pcp.proof_collection(self, sq, proofs, early, late)
         elif late_f is not None:
             late()
+        start_client()  # (no proofs to wait for)
         clear = {k: v["clear"] for k, v in dp_results.items()}
         out = SurveyResult(sq.SurveyID, result, n_groups, n_out, block, clear)
-        if client_future is not None:
-            out.client_out = client_future.result()
+        if client["f"] is not None:
+            out.client_out = client["f"].result()
         return out
 
     def _net_dissemination(self, sq):
