@@ -82,8 +82,9 @@ DX_HD void joint_table_one(const uint32_t *V_aff, uint32_t *T_aff, int64_t it) {
   }
 }
 
+// (pos: when given, U of (v, q) goes to row pos[v * n_groups + q] instead of v * pad + q)
 DX_HD void u_joint_one(const uint32_t *T_aff, const uint32_t *ab, uint32_t *U_aff, int64_t n_groups, int L,
-                       int64_t pad, int64_t t) {
+                       int64_t pad, const int64_t *pos, int64_t t) {
   const int64_t m = n_groups * L;
   const int64_t v = t / n_groups, q = t % n_groups;
   const G2A *T = reinterpret_cast<const G2A *>(T_aff) + q * L * kT;
@@ -99,7 +100,7 @@ DX_HD void u_joint_one(const uint32_t *T_aff, const uint32_t *ab, uint32_t *U_af
       if (e) acc = jadd_mixed(acc, T[j * kT + e - 1]);
     }
   }
-  at<G2A>(U_aff, v * pad + q) = to_affine(acc);
+  at<G2A>(U_aff, pos ? pos[t] : v * pad + q) = to_affine(acc);
 }
 
 // The same combination split over sp threads per (v, q) (small batches: a
@@ -131,11 +132,11 @@ DX_HD void u_joint_part_one(const uint32_t *T_aff, const uint32_t *ab, uint32_t 
 }
 
 DX_HD void u_joint_reduce_one(const uint32_t *P_jac, uint32_t *U_aff, int64_t n_groups, int sp, int64_t pad,
-                              int64_t vq) {
+                              const int64_t *pos, int64_t vq) {
   const int64_t v = vq / n_groups, q = vq % n_groups;
   G2J acc = at<G2J>(P_jac, vq * sp);
   for (int p = 1; p < sp; p++) acc = jadd(acc, at<G2J>(P_jac, vq * sp + p));
-  at<G2A>(U_aff, v * pad + q) = to_affine(acc);
+  at<G2A>(U_aff, pos ? pos[vq] : v * pad + q) = to_affine(acc);
 }
 
 DX_HD void slice_sum_one(const uint32_t *src, const int32_t *idx, const int64_t *start, const int32_t *len,
@@ -254,9 +255,10 @@ __global__ void __launch_bounds__(kWG) DX_OCC joint_table_kernel(const uint32_t 
   if (i < m) joint_table_one(V, T, i);
 }
 __global__ void __launch_bounds__(kWG) DX_OCC u_joint_kernel(const uint32_t *T, const uint32_t *ab, uint32_t *U,
-                                                            int64_t n_groups, int L, int64_t pad, int64_t n) {
+                                                            int64_t n_groups, int L, int64_t pad, const int64_t *pos,
+                                                            int64_t n) {
   DX_TID();
-  if (i < n) u_joint_one(T, ab, U, n_groups, L, pad, i);
+  if (i < n) u_joint_one(T, ab, U, n_groups, L, pad, pos, i);
 }
 __global__ void __launch_bounds__(kWG) DX_OCC u_joint_part_kernel(const uint32_t *T, const uint32_t *ab,
                                                                  uint32_t *P, int64_t n_groups, int L, int sp,
@@ -265,9 +267,10 @@ __global__ void __launch_bounds__(kWG) DX_OCC u_joint_part_kernel(const uint32_t
   if (i < n) u_joint_part_one(T, ab, P, n_groups, L, sp, i);
 }
 __global__ void __launch_bounds__(kWG) DX_OCC u_joint_reduce_kernel(const uint32_t *P, uint32_t *U, int64_t n_groups,
-                                                                   int sp, int64_t pad, int64_t n) {
+                                                                   int sp, int64_t pad, const int64_t *pos,
+                                                                   int64_t n) {
   DX_TID();
-  if (i < n) u_joint_reduce_one(P, U, n_groups, sp, pad, i);
+  if (i < n) u_joint_reduce_one(P, U, n_groups, sp, pad, pos, i);
 }
 __global__ void __launch_bounds__(kWG) DX_OCC slice_sum_kernel(const uint32_t *src, const int32_t *idx,
                                                               const int64_t *start, const int32_t *len,
@@ -330,32 +333,32 @@ int dx_g2_joint_table(int on_gpu, void *stream, const uint32_t *V_aff, uint32_t 
 // U[v*pad + q] = affine(sum_{j<L} (a + b lambda)_{v, q*L+j} V_{q*L+j}) for
 // v < G, q < n_groups; ab [G*m, 2] (m = n_groups * L) are the 32-bit halves.
 int dx_rp_u_joint(int on_gpu, void *stream, const uint32_t *T_aff, const uint32_t *ab, uint32_t *U_aff,
-                  int64_t n_groups, int G, int L, int64_t pad) {
+                  int64_t n_groups, int G, int L, int64_t pad, const int64_t *pos) {
   const int64_t n = (int64_t)G * n_groups;
   if (n <= 0) return 0;
   if (!on_gpu) {
-    host_for_each(n, [=](int64_t t) { u_joint_one(T_aff, ab, U_aff, n_groups, L, pad, t); });
+    host_for_each(n, [=](int64_t t) { u_joint_one(T_aff, ab, U_aff, n_groups, L, pad, pos, t); });
     return 0;
   }
   hipLaunchKernelGGL(u_joint_kernel, grid_of(n), dim3(kWG), 0, (hipStream_t)stream, T_aff, ab, U_aff, n_groups, L,
-                     pad, n);
+                     pad, pos, n);
   return check_hip(hipGetLastError(), "rp_u_joint");
 }
 
 // dx_rp_u_joint with each (v, q) split over sp threads (tmp: G * n_groups * sp Jacobian rows)
 int dx_rp_u_joint_split(int on_gpu, void *stream, const uint32_t *T_aff, const uint32_t *ab, uint32_t *U_aff,
-                        int64_t n_groups, int G, int L, int64_t pad, int sp, uint32_t *tmp) {
+                        int64_t n_groups, int G, int L, int64_t pad, int sp, uint32_t *tmp, const int64_t *pos) {
   const int64_t n = (int64_t)G * n_groups;
   if (n <= 0) return 0;
   if (!on_gpu) {
     host_for_each(n * sp, [=](int64_t t) { u_joint_part_one(T_aff, ab, tmp, n_groups, L, sp, t); });
-    host_for_each(n, [=](int64_t t) { u_joint_reduce_one(tmp, U_aff, n_groups, sp, pad, t); });
+    host_for_each(n, [=](int64_t t) { u_joint_reduce_one(tmp, U_aff, n_groups, sp, pad, pos, t); });
     return 0;
   }
   hipLaunchKernelGGL(u_joint_part_kernel, grid_of(n * sp), dim3(kWG), 0, (hipStream_t)stream, T_aff, ab, tmp,
                      n_groups, L, sp, n * sp);
   hipLaunchKernelGGL(u_joint_reduce_kernel, grid_of(n), dim3(kWG), 0, (hipStream_t)stream, tmp, U_aff, n_groups, sp,
-                     pad, n);
+                     pad, pos, n);
   return check_hip(hipGetLastError(), "rp_u_joint_split");
 }
 

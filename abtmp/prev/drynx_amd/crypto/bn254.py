@@ -50,6 +50,8 @@ def h2d(t: torch.Tensor, device) -> torch.Tensor:
     dev = torch.device(device)
     if dev.type != "cuda":
         return t
+    if torch.cuda.is_current_stream_capturing():
+        raise RuntimeError("h2d: host upload inside a HIP graph capture")
     return t.pin_memory().to(dev, non_blocking=True)
 
 

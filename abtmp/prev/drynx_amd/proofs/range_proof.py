@@ -951,52 +951,38 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
     _sw.__exit__(None, None, None)
     vns = [{"rho": rho_all[v * m:(v + 1) * m], "ab": ab_all[v * m:(v + 1) * m]} for v in range(G)]
     timers.count("rp.verify.items", G * m)
-    # exponents of the GT multi-exponentiation: groups 0..G-1 prod a^rho_v =
-    # prod a^a' * frob^8(a)^b' (32-bit exponents over (A, frob^8 A)); groups
-    # G..2G-1 each VN's own GT-membership combination prod a^gamma_v (over A)
-    abv = ab_all.view(G, m, 2)
-    k = torch.zeros((3 * G * m, 8), dtype=torch.int32, device=device)
-    kr = k[: 2 * G * m].view(G, 2 * m, 8)
-    kr[:, :m, 0] = abv[:, :, 0]
-    kr[:, m:, 0] = abv[:, :, 1]
-    k[2 * G * m:] = gam_all
-    gv = torch.arange(G, device=device, dtype=torch.int32)
-    mgrp = torch.cat([gv.repeat_interleave(2 * m), G + gv.repeat_interleave(m)])
     me_groups = ((2 * m, 32),) * G + ((m, gb),) * G
     # windows by cost (nt.me_window): 16 bits for a 1-GPU inbox, 11 for a pool
     # slice; the host keeps bytes (fewer buckets for its serial products)
     wc_ = nt.me_window(me_groups) if device.type == "cuda" else (5, 8)
-    # R-MSM scalars rho_it Zphi_(p, j) (periodic over the VNs)
-    it = torch.arange(m, device=device)
-    s_r = nt.fr_arith(nt.FR_MUL, rho_all, r.zphi.index_select(0, (it // (S * l)) * l + it % l).contiguous())
     if not ddirect:
         dpts = torch.cat([Cp.contiguous(), r.D.contiguous()]).repeat(G, 1)
         wc = nt.fr_arith(nt.FR_MUL, w_all, r.challenge)
         dsc = torch.stack([wc.view(G, n, 8), w_all.view(G, n, 8)], 1).reshape(-1, 8).contiguous()
     aux = _aux_stream(device) if device.type == "cuda" else None
-    ready = None
+    meta = (G, m, S, l, gb, tuple(wc_), _r_window(m, G))
+    # GPU: the U side first, on this stream (its chain of Miller-loop kernels
+    # is the critical path of a small batch), then the R MSM, the
+    # multi-exponentiation and the D-check on the aux stream.  (Launching the R
+    # MSM first measured neutral on the pool parts and +2.5 ms on the 1-GPU
+    # query: the two chains only slow each other down on the shared CUs.)
+    ev_u = ev_r = None
     if aux is not None:
         ready = torch.cuda.Event()
         ready.record(torch.cuda.current_stream(device))
-        # the U side first, on this stream: its chain of Miller-loop kernels is
-        # the critical path of a small batch (a pool slice)
         with timers.span("rp.verify.msm_queue"):
             msq = _msm_queue(Y, r.V, ab_all, G, n, S, l, vstream, segs, table)
             for v, uok in zip(vns, msq["u_ok"]):
                 v["u_ok"] = uok
+        ev_u = torch.cuda.Event()                                       # the U side's fold is queued
+        ev_u.record(torch.cuda.current_stream(device))
         aux.wait_event(ready)
-    # the R MSM, the multi-exponentiation and the D-check on the aux stream
-    # with device-resident bucket plans: no host sync, every pass queued now
-    # (a plan's host sync used to wait ~6-9 ms behind the U side)
     with timers.span("rp.verify.passes"), (torch.cuda.stream(aux) if aux is not None else _nullctx()):
-        with timers.span("rp.run.R"):
-            S_R, hR = nt.g2_msm_device(r.V, s_r, m, ((m, 254),) * G, c=_r_window(m, G))
-        with timers.span("rp.frob8"):  # (A, frob^8 A) stacked: the Frobenius image written in place
-            A2 = torch.empty((2 * m, 96), dtype=torch.int32, device=device)
-            nt.batched_copy([(r.A.contiguous(), A2[:m])])
-            nt.gt_frob8(r.A.contiguous(), out=A2[m:])
-        with timers.span("rp.run.ME"):
-            mexp = nt.multi_exp_device(A2, k, mgrp, me_groups, wc_[0], wc_[1], item_split=(2 * G * m, m))
+        S_R, hR = _pass_r(r.V, r.zphi, rho_all, meta)
+        if aux is not None:
+            ev_r = torch.cuda.Event()                                   # the R MSM is queued
+            ev_r.record(aux)
+        A2, mexp, e_all, dfull = _pass_me(r.A, ab_all, gam_all, rho_all, r.zv, w_all, r.zr, z, meta)
         with timers.span("rp.run.D"):
             if ddirect:
                 if cC is None:                                                 # host path
@@ -1009,16 +995,23 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
                 dcheck = nt.g1_sum(nt.g1_mul_glv(pts.contiguous(), abs_.contiguous()).view(n, 2 * G, 24))
             else:
                 dcheck = nt.g1_msm_device(dpts, dsc, n, ((n, 254),) * (2 * G))     # group = row // n
-        e_all = nt.fr_dot_rows(rho_all, r.zv, G, b_periodic=True)                        # sum rho Zv per VN
-        dfull = torch.stack([nt.fr_dot_rows(w_all, r.zr, G, b_periodic=True),
-                             nt.fr_dot_rows(w_all, z, G, b_periodic=True)], 1)             # [G, 2, 8]
     if aux is None:  # host: the U side after the passes
         msq = _msm_queue(Y, r.V, ab_all, G, n, S, l, None, segs)
         for v, uok in zip(vns, msq["u_ok"]):
             v["u_ok"] = uok
+    useg = fR = None
     with timers.span("rp.verify.multiexp"):
         if aux is not None:
             run_idle_tasks()  # host work queued by the caller, in the GPU's busiest window
+            # the host tails of the R side (Horner, ML(B, R)) and of the U side
+            # (per-segment products) as soon as their device chains are done,
+            # while the multi-exponentiation and the D-check still run
+            ev_r.synchronize()
+            with timers.span("rp.verify.r_tail"):
+                fR, rok = _msm_r_miller(hR, S_R)
+            ev_u.synchronize()
+            with timers.span("rp.verify.u_tail"):
+                useg = _seg_products(msq)                              # [G, nseg, 96] host
             aux.synchronize()                                          # aux results are read on this stream/host
         GG = nt.multi_exp_grouped_finish(mexp)                         # [2G, 96]: prod a^rho_v, prod a^gamma_v
         D_all = dcheck.cpu() if ddirect else nt.g1_msm_finish(dcheck)  # [2G, 24]
@@ -1026,10 +1019,12 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
             nt.check_overflow(h_)
         e_all, dfull = e_all.cpu(), dfull.cpu()
     with timers.span("rp.verify.fold_wait"):
-        useg = _seg_products(msq)                                      # [G, nseg, 96] host
+        if useg is None:
+            useg = _seg_products(msq)                                  # [G, nseg, 96] host
         for k_, v in enumerate(vns):
             v["F"] = nt.gt_prod(useg[k_].view(nseg, 1, 96), chunk=64).view(1, 96)
-        fR, rok = _msm_r_miller(hR, S_R)
+        if fR is None:
+            fR, rok = _msm_r_miller(hR, S_R)
         for v, f, ok in zip(vns, fR, rok):
             v["F"], v["r_ok"] = nt.gt_mul(v["F"], f.view(1, 96)), ok
     for k, v in enumerate(vns):
@@ -1153,6 +1148,43 @@ class _nullctx:
         return False
 
 
+def _pass_r(V, zphi, rho, meta):
+    """R = sum_it (rho_it Zphi_(p, j)) V_it per VN: the G2 Pippenger MSM with a
+    device plan, queued on the current stream (no host sync) -> (S_R, hR)."""
+    G, m, S, l, gb, wc, cR = meta
+    it = torch.arange(m, device=V.device)
+    s_r = nt.fr_arith(nt.FR_MUL, rho, zphi.index_select(0, (it // (S * l)) * l + it % l).contiguous())
+    with timers.span("rp.run.R"):
+        return nt.g2_msm_device(V, s_r, m, ((m, 254),) * G, c=cR)
+
+
+def _pass_me(A, ab, gam, rho, zv, w, zr, z, meta):
+    """The GT multi-exponentiation over (A, frob^8 A) with the GLV halves of
+    rho (groups 0..G-1) and each VN's 40-bit membership combination (G..2G-1),
+    and the Fr exponent sums, on the current stream -> (A2, mexp, e_all, dfull)."""
+    G, m, S, l, gb, wc, cR = meta
+    dev = A.device
+    with timers.span("rp.frob8"):  # (A, frob^8 A) stacked: the Frobenius image written in place
+        A2 = torch.empty((2 * m, 96), dtype=torch.int32, device=dev)
+        A2[:m].copy_(A)
+        nt.gt_frob8(A.contiguous(), out=A2[m:])
+    abv = ab.view(G, m, 2)
+    k = torch.zeros((3 * G * m, 8), dtype=torch.int32, device=dev)
+    kr = k[: 2 * G * m].view(G, 2 * m, 8)
+    kr[:, :m, 0] = abv[:, :, 0]
+    kr[:, m:, 0] = abv[:, :, 1]
+    k[2 * G * m:] = gam
+    e = torch.arange(3 * G * m, device=dev)                          # entry -> group, elementwise only
+    mgrp = torch.where(e < 2 * G * m, e // (2 * m), G + (e - 2 * G * m) // m).to(torch.int32)
+    with timers.span("rp.run.ME"):
+        mexp = nt.multi_exp_device(A2, k, mgrp, ((2 * m, 32),) * G + ((m, gb),) * G, wc[0], wc[1],
+                                   item_split=(2 * G * m, m))
+    e_all = nt.fr_dot_rows(rho, zv, G, b_periodic=True)                                 # sum rho Zv per VN
+    dfull = torch.stack([nt.fr_dot_rows(w, zr, G, b_periodic=True),
+                         nt.fr_dot_rows(w, z, G, b_periodic=True)], 1)                   # [G, 2, 8]
+    return A2, mexp, e_all, dfull
+
+
 _DCHECK_DIRECT_MAX = 16384  # proofs x VNs up to which the D-check runs without a bucket plan
 
 
@@ -1207,31 +1239,31 @@ def _msm_queue(Y, V, ab_all, G: int, n: int, S: int, L: int, vstream=None, segs:
         coop = K == 1 and G * pad <= _COOP_MAX_ITEMS
         Uall = torch.zeros((G * pad, 32), dtype=torch.int32, device=dev)
         UV = torch.zeros((period, 16), dtype=torch.int32, device=dev)
-        negY = None
+        pos = None
+        if nseg > 1:
+            # row of (VN v, group q) in the fold layout (segments start whole
+            # workgroups): host-known, one upload before the U kernels -- no
+            # index glue between the combinations and the fold's coefficients
+            qseg = np.repeat(np.arange(nseg), cq)
+            qpos = segbase[qseg] + np.arange(nq) - qoff[:-1][qseg]
+            pos = _h2d((np.arange(G).reshape(G, 1) * pad + qpos.reshape(1, nq)).reshape(-1).astype(np.int64), dev)
+        # the points of the fold (affine -Y_q, or uv(-Y_q) for the normalised
+        # lines) in place before the U combinations
         if coop:  # affine -Y_q, the same for every VN
             negY = nt.g1_to_affine(nt.g1_add(bn.g1_infinity_jac(nq, dev), Y.contiguous(), subtract=True))
+        elif nseg > 1:  # uv(-Y_q) is the same for every VN: computed once, copied per VN below
+            UVd = torch.zeros((nq + 1, 16), dtype=torch.int32, device=dev)
+            nt.rp_msm_uv(Y, UVd, nq, 1, nq + 1)
+            negY = UVd[:nq]
         if nseg == 1:
-            with timers.span("rp.u.joint"):
-                nt.rp_u_joint(table, ab_all, nq, G, L, Uall, pad)
             if coop:
                 UV[: G * pad].view(G, pad, 16)[:, :nq] = negY
             else:
                 nt.rp_msm_uv(Y, UV, nq, G, pad)
-            Ud = Uall
         else:
-            Ud = torch.empty((G * nq, 32), dtype=torch.int32, device=dev)
-            with timers.span("rp.u.joint"):
-                nt.rp_u_joint(table, ab_all, nq, G, L, Ud, nq)
-            if not coop:  # uv(-Y_q) is the same for every VN: computed once, copied per VN below
-                UVd = torch.zeros((nq + 1, 16), dtype=torch.int32, device=dev)
-                nt.rp_msm_uv(Y, UVd, nq, 1, nq + 1)
-                negY = UVd[:nq]
-            qseg = torch.repeat_interleave(torch.arange(nseg, device=dev), _h2d(cq, dev),
-                                           output_size=nq)
-            qpos = _h2d(segbase, dev)[qseg] + torch.arange(nq, device=dev) - _h2d(qoff[:-1], dev)[qseg]
-            pos = (torch.arange(G, device=dev).view(G, 1) * pad + qpos.view(1, nq)).reshape(-1)
-            Uall.index_copy_(0, pos, Ud)
             UV.index_copy_(0, pos, negY.repeat(G, 1))
+        with timers.span("rp.u.joint"):
+            nt.rp_u_joint(table, ab_all, nq, G, L, Uall, pad, pos)
         # G2 membership of every U (exact test), on the validation stream beside the fold
         cur = torch.cuda.current_stream(dev)
         vs = vstream if vstream is not None else cur
@@ -1240,10 +1272,13 @@ def _msm_queue(Y, V, ab_all, G: int, n: int, S: int, L: int, vstream=None, segs:
             # every read of the flags stays on the validation stream: a reduction
             # queued on `cur` would race the membership kernels (read before they
             # finish); the caller synchronises `vs` before looking at the verdicts
-            fl = nt.g2_subgroup(Ud).view(G, -1)[:, :nq].bool()
+            flags = nt.g2_subgroup(Uall)
+            fl = (flags.view(G, pad)[:, :nq] if pos is None else flags.index_select(0, pos).view(G, nq)).bool()
             out["u_seg"] = _seg_all(fl, cq, dev)
             out["u_ok"] = list(out["u_seg"].all(dim=1).unbind(0))
-        Ud.record_stream(vs)
+        Uall.record_stream(vs)
+        if pos is not None:
+            pos.record_stream(vs)
         with timers.span("rp.u.fold"):
             if coop:
                 out["fb"] = nt.rp_fold_accum_coop_raw(nt.rp_fold_coeffs(Uall), UV, Uall, period, 1)

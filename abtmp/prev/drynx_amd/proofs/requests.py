@@ -598,21 +598,22 @@ def sampled_bounds(sq, n: int, part=None) -> tuple:
 
 
 # extra work of a rank, in units of a plain helper's pool share, that its
-# slice is shortened by: every DP it hosts beyond the fewest any rank hosts,
-# and every VN it hosts (the full-inbox decode and the digests of the other
-# slices).  Fitted to pool(k) = F + P share(k) from the one-GPU shares of
-# profiles/r5/it2/rank_share_w8.json (F ~ 10 ms fixed, P ~ 166 ms for the
-# whole pool, a second DP ~5.3 ms of proving, a VN ~0.4 ms): equal
-# prove + pool at weights 1 / 0.982 / 0.762
-_POOL_DP_W, _POOL_VN_W = 0.24, 0.02
+# slice is shortened by.  Every rank's part starts at the same moment -- the
+# range fan-out is ONE exchange after every rank has signed its proofs, so at
+# the slowest rank's proving end -- so a rank proving an extra DP gets NO
+# discount (a discount only lengthened the other parts: profiles/r5/it15,
+# pool(share) ~ 13 ms + 122 ms x share); a VN rank's part also carries the
+# digests of the other slices (a side stream: +2.2 ms of its part at equal
+# shares, profiles/r5/it16)
+_POOL_DP_W, _POOL_VN_W = 0.0, 0.14
 
 
 def balanced_parts(W: int, dps: list, vns: list) -> list:
-    """Pool parts for W ranks weighted so every rank's proving + checking
-    ends together: rank k's slice weight 1 - 0.45 (extra DPs) - 0.08 (VNs)
+    """Pool parts for W ranks weighted so every rank's check ends together:
+    rank k's slice weight 1 - _POOL_DP_W (per extra DP) - _POOL_VN_W (per VN)
     (floor 0.25), as (k, W, cumulative weights) tuples (``sampled_bounds``).
     Calibrated from one-GPU measurements of each rank's share
-    (tools/rank_share.py, profiles/r4/rank_share_*)."""
+    (tools/rank_share.py)."""
     if W <= 1 or os.environ.get("DRYNX_POOL_BALANCE", "1") == "0":
         return [(k, W) for k in range(W)]
     lo = min(dps)
