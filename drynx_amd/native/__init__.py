@@ -103,6 +103,8 @@ _SIGS = {
     "dx_lr_encode": [_P, _P, _L, _L, _I, _P, _P, _P, ctypes.c_double, ctypes.c_double, _P, _I],
     "dx_lr_reduce": [_P, _P, _L, _L, _L, _P],
     "dx_g1_mul_fast": [_P, _P, _P, _P, _L, _I, _I],
+    "dx_g1_mul_glv256": [_P, _P, _P, _P, _P, _L, _I, _I],
+    "dx_glv_split": [_I, _P, _P, _P, _L],
     "dx_rp_verify_fold": [_P, _P, _P, _P, _P, _P, _L, _I, _I],
     "dx_gt_slice_prod": [_I, _P, _P, _P, _P, _P, _P, _L],
     "dx_gt_chunk_weight": [_I, _P, _P, _P, _P, _P, _P, _P, _L],
@@ -342,6 +344,19 @@ def g1_fb_mul_i64(table: torch.Tensor, m: torch.Tensor) -> torch.Tensor:
     return out
 
 
+G1_MUL_GLV = True  # A/B constant (tools/ab_patch.py --no-glv): 256-step window-3 kernel instead
+
+
+def glv_split(scalars: torch.Tensor) -> torch.Tensor:
+    """[n, 8] scalars -> [n, 9] int32 words: k1 (4), |k2| (4), k2 < 0 with
+    k = k1 + k2 GLV_LAMBDA mod r (csrc/bn254/glv_split.h; host or device)."""
+    n = _rows(scalars, 8)
+    out = torch.empty((n, 9), dtype=torch.int32, device=scalars.device)
+    g, s = _ctx(scalars)
+    _call("dx_glv_split", g, s, _ptr(scalars.contiguous()), _ptr(out), n)
+    return out
+
+
 def g1_mul(pts_jac: torch.Tensor, scalars: torch.Tensor) -> torch.Tensor:
     np_ = _rows(pts_jac, 24)
     nk = _rows(scalars, 8)
@@ -349,6 +364,12 @@ def g1_mul(pts_jac: torch.Tensor, scalars: torch.Tensor) -> torch.Tensor:
     assert np_ in (1, n) and nk in (1, n)
     out = torch.empty((n, 24), dtype=torch.int32, device=scalars.device)
     g, s = _ctx(pts_jac, scalars)
+    if g and G1_MUL_GLV:  # gfx950: in-kernel GLV split, 128-step ladder (dx_g1_varmul.hip)
+        rc = _raw_call("dx_g1_mul_glv256", s, _ptr(pts_jac), _ptr(scalars), _ptr(_glv_const("beta", out.device)),
+                       _ptr(out), n, int(np_ == 1 and n > 1), int(nk == 1 and n > 1))
+        if rc:
+            raise RuntimeError(f"dx_g1_mul_glv256 failed rc={rc}")
+        return out
     if g:  # gfx950: register-resident kernel with the window table in LDS (dx_g1_varmul.hip)
         rc = _raw_call("dx_g1_mul_fast", s, _ptr(pts_jac), _ptr(scalars), _ptr(out), n, int(np_ == 1 and n > 1),
                                     int(nk == 1 and n > 1))

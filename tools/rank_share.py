@@ -303,7 +303,8 @@ def main():
     prove_max = max(v["prove_ms"] for v in res["ranks"].values())
     pool_max = max(v["pool_ms"] for v in res["ranks"].values())
     res["projection_step_ms"] = round(max(serial, prove_max + pool_max) + ctrl, 2)
-    res["projection_terms_ms"] = {"prove_max": prove_max, "pool_max": pool_max, "serial": serial, "ctrl": round(ctrl, 3)}
+    res["projection_terms_ms"] = {"prove_max": prove_max, "pool_max": pool_max, "serial": serial,
+                                  "ctrl": round(ctrl, 3)}
     print(json.dumps({"projection_ms": proj, "step_ms": res["projection_step_ms"],
                       "terms": res["projection_terms_ms"]}), flush=True)
     if a.json_out:
