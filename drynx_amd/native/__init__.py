@@ -102,8 +102,7 @@ _SIGS = {
     "dx_hash_to_g1": [_I, _P, _P, _P, _L, _P, _L],
     "dx_lr_encode": [_P, _P, _L, _L, _I, _P, _P, _P, ctypes.c_double, ctypes.c_double, _P, _I],
     "dx_lr_reduce": [_P, _P, _L, _L, _L, _P],
-    "dx_g1_mul_fast": [_P, _P, _P, _P, _L, _I, _I],
-    "dx_g1_mul_glv256": [_P, _P, _P, _P, _P, _L, _I, _I],
+    "dx_g1_mul_glv256": [_P, _P, _P, _P, _P, _L, _I, _I, _I],
     "dx_glv_split": [_I, _P, _P, _P, _L],
     "dx_rp_verify_fold": [_P, _P, _P, _P, _P, _P, _L, _I, _I],
     "dx_gt_slice_prod": [_I, _P, _P, _P, _P, _P, _P, _L],
@@ -344,7 +343,8 @@ def g1_fb_mul_i64(table: torch.Tensor, m: torch.Tensor) -> torch.Tensor:
     return out
 
 
-G1_MUL_GLV = True  # A/B constant (tools/ab_patch.py --no-glv): 256-step window-3 kernel instead
+# rows up to which g1_mul runs two lanes per row (the latency form; tools/bench_g1mul.py)
+G1_MUL_PAIR_ROWS = 1 << 14
 
 
 def glv_split(scalars: torch.Tensor) -> torch.Tensor:
@@ -364,17 +364,11 @@ def g1_mul(pts_jac: torch.Tensor, scalars: torch.Tensor) -> torch.Tensor:
     assert np_ in (1, n) and nk in (1, n)
     out = torch.empty((n, 24), dtype=torch.int32, device=scalars.device)
     g, s = _ctx(pts_jac, scalars)
-    if g and G1_MUL_GLV:  # gfx950: in-kernel GLV split, 128-step ladder (dx_g1_varmul.hip)
+    if g:  # gfx950: in-kernel GLV split, 128-step ladder (dx_g1_varmul.hip)
         rc = _raw_call("dx_g1_mul_glv256", s, _ptr(pts_jac), _ptr(scalars), _ptr(_glv_const("beta", out.device)),
-                       _ptr(out), n, int(np_ == 1 and n > 1), int(nk == 1 and n > 1))
+                       _ptr(out), n, int(np_ == 1 and n > 1), int(nk == 1 and n > 1), int(n <= G1_MUL_PAIR_ROWS))
         if rc:
             raise RuntimeError(f"dx_g1_mul_glv256 failed rc={rc}")
-        return out
-    if g:  # gfx950: register-resident kernel with the window table in LDS (dx_g1_varmul.hip)
-        rc = _raw_call("dx_g1_mul_fast", s, _ptr(pts_jac), _ptr(scalars), _ptr(out), n, int(np_ == 1 and n > 1),
-                                    int(nk == 1 and n > 1))
-        if rc:
-            raise RuntimeError(f"dx_g1_mul_fast failed rc={rc}")
         return out
     _call("dx_g1_mul", g, s, _ptr(pts_jac), _ptr(scalars), _ptr(out), n, int(np_ == 1 and n > 1),
           int(nk == 1 and n > 1))

@@ -1,7 +1,7 @@
 """GLV decomposition of full scalars (csrc/bn254/glv_split.h): k = k1 + k2
 lambda mod r with 0 <= k1 < 2^128, |k2| < 2^128 for every k < 2^256, checked
 against Python integers on the host build; the GPU test checks the GLV
-variable-base kernel (``native.g1_mul``) against the window-3 kernel and the
+variable-base kernel (``native.g1_mul``) against the host build and the
 oracle."""
 import random
 
@@ -39,7 +39,7 @@ def test_glv_split_bounds_and_identity():
 
 
 @pytest.mark.gpu
-def test_g1_mul_glv_matches_window_kernel_gpu():
+def test_g1_mul_glv_matches_host_gpu():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     dev = "cuda"
@@ -51,14 +51,15 @@ def test_g1_mul_glv_matches_window_kernel_gpu():
     ks[:6] = [0, 1, O.R, O.R - 1, (1 << 256) - 1, 3]
     P = bn.g1_jac_tensor(pts, dev)
     K = _scalars(ks, dev)
-    assert nt.G1_MUL_GLV
-    got = nt.g1_mul(P, K)
-    nt.G1_MUL_GLV = False
+    ref = nt.g1_mul(P.cpu(), K.cpu())  # host build of the generic double-and-add
+    keep = nt.G1_MUL_PAIR_ROWS
     try:
-        ref = nt.g1_mul(P, K)
+        for rows in (0, n):  # one lane per row, two lanes per row
+            nt.G1_MUL_PAIR_ROWS = rows
+            got = nt.g1_mul(P, K)
+            assert bool(nt.g1_eq(got.cpu(), ref).all()), rows
     finally:
-        nt.G1_MUL_GLV = True
-    assert bool(nt.g1_eq(got, ref).all())
+        nt.G1_MUL_PAIR_ROWS = keep
     for i in (0, 1, 2, 3, 4, 5, 100, 776):
         want = O.g1_mul(ks[i], pts[i]) if pts[i] is not None else None
         assert bn.g1_points_from_jac(got[i:i + 1].cpu())[0] == want

@@ -1,8 +1,8 @@
 """A/B diagnostic: bench.py with one verifier parameter overridden in-process
 (no switch in the framework): ``--r-window c`` fixes the R MSM's window
 bits (``range_proof._r_window``), ``--me-window c`` the GT
-multi-exponentiation's (``native.me_window``), ``--no-glv`` the window-3 variable-base
-kernel instead of the GLV one (``native.G1_MUL_GLV``).  Everything after ``--`` goes
+multi-exponentiation's (``native.me_window``), ``--g1-pair-rows n`` the row count up to which
+the variable-base G1 kernel runs two lanes per row (``native.G1_MUL_PAIR_ROWS``).  Everything after ``--`` goes
 to bench.py.  Usage: python tools/ab_patch.py --r-window 15 -- --steps 20 --warmup 5
 """
 import argparse
@@ -19,13 +19,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--r-window", type=int, default=0)
     ap.add_argument("--me-window", type=int, default=0)
-    ap.add_argument("--no-glv", action="store_true", help="g1_mul through the 256-step window-3 kernel")
+    ap.add_argument("--g1-pair-rows", type=int, default=-1, help="native.G1_MUL_PAIR_ROWS")
     a = ap.parse_args(own)
     from drynx_amd import native as nt
     from drynx_amd.proofs import range_proof as rp
 
-    if a.no_glv:
-        nt.G1_MUL_GLV = False
+    if a.g1_pair_rows >= 0:
+        nt.G1_MUL_PAIR_ROWS = a.g1_pair_rows
     if a.r_window:
         rp._r_window = lambda m, G, c=a.r_window: c
     if a.me_window:
