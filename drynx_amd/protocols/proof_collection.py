@@ -436,6 +436,9 @@ def early_plane_ok(ctx, sq) -> bool:
         and use_pool(ctx) and os.environ.get("DRYNX_RANGE_PLANE", "1") != "0"
 
 
+LEDGER_PREFETCH = True  # A/B constant (tools/ab_patch.py --no-ledger-prefetch)
+
+
 def proof_collection(ctx, sq, local_requests: list, early: dict | None = None, late=None):
     """Returns the new SkipBlock (on every rank).  ``early``: the range plane
     started by ``start_range_plane`` (its requests and pooled verdicts);
@@ -467,11 +470,22 @@ def proof_collection(ctx, sq, local_requests: list, early: dict | None = None, l
             return {vn.id: check_requests(ctx, sq, vn, idx, len(vns), rs, range_pooled)
                     for idx, vn in enumerate(vns) if vn.rank == ctx.rank}
 
+        def prefetch(rs):
+            # the stored payloads' host copy and blob write run under their
+            # verification instead of after the verdicts (store_verdicts finds
+            # them in the rank's blob segment); payloads whose digest is known
+            if LEDGER_PREFETCH and local_vns and hasattr(ctx, "ledger_values"):
+                with timers.span("ledger.prefetch"):
+                    ctx.ledger_values([r for r in rs if r.kind != "shuffle" and r.data_digest
+                                       and r.tensor is not None])
+
+        prefetch(reqs)
         pending = checks(reqs, pooled)
         reqs2, pending2 = [], {}
         if late is not None:
             with timers.timed("ProofFanOut"):
                 reqs2 = fan_out(ctx, sq, late(), pool=False)
+            prefetch(reqs2)
             pending2 = checks(reqs2, None)
         for vn in vns:
             if vn.id in pending:

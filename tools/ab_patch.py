@@ -20,12 +20,17 @@ def main():
     ap.add_argument("--r-window", type=int, default=0)
     ap.add_argument("--me-window", type=int, default=0)
     ap.add_argument("--g1-pair-rows", type=int, default=-1, help="native.G1_MUL_PAIR_ROWS")
+    ap.add_argument("--no-ledger-prefetch", action="store_true", help="proof_collection.LEDGER_PREFETCH off")
     a = ap.parse_args(own)
     from drynx_amd import native as nt
     from drynx_amd.proofs import range_proof as rp
 
     if a.g1_pair_rows >= 0:
         nt.G1_MUL_PAIR_ROWS = a.g1_pair_rows
+    if a.no_ledger_prefetch:
+        from drynx_amd.protocols import proof_collection as pc
+
+        pc.LEDGER_PREFETCH = False
     if a.r_window:
         rp._r_window = lambda m, G, c=a.r_window: c
     if a.me_window:
