@@ -124,7 +124,11 @@ def main():
         return t0, time.perf_counter() - t0
 
     sm.attach_shard(None, False)
-    res["build_first_s"] = round(build("first")[1], 3)  # module / kernel first-use costs included
+    # the full 1-rank build (module / kernel first-use costs included, as in
+    # bench.py's setup_s), then this rank's share.  Only two builds: the third
+    # ~110 GB allocation of a process stalls 3-6 s before its build starts
+    # whichever build it is (profiles/r5/final/setup_host_trace.txt,
+    # profiles/r5/setup/setup_host_trace.txt), and a real rank allocates once
     res["build_full_s"] = round(build("full")[1], 3)
     res["table_bytes"] = sm.table_bytes()
     emu = EmuShard(a.world, a.rank, dev)
