@@ -1566,15 +1566,19 @@ _val: dict = {}
 def _val_stream(device):
     key = str(device)
     if key not in _val:
-        _val[key] = torch.cuda.Stream(device)
+        _val[key] = torch.cuda.Stream(device, priority=streams.priority(VAL_PRIORITY))
     return _val[key]
+
+
+AUX_PRIORITY = -1  # A/B constants (tools/ab_patch.py --aux-priority / --val-priority)
+VAL_PRIORITY = 0
 
 
 def _aux_stream(device):
     key = str(device)
     if key not in _aux:
         # plans: short kernels overtake the pairing side
-        _aux[key] = torch.cuda.Stream(device, priority=streams.priority(-1))
+        _aux[key] = torch.cuda.Stream(device, priority=streams.priority(AUX_PRIORITY))
     return _aux[key]
 
 

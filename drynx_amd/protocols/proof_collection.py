@@ -30,7 +30,7 @@ from ..parallel.comm import bytes_to_obj, obj_to_bytes
 from ..crypto.coins import Coins
 from ..proofs import requests as prq
 from ..query import query_to_proofs_nbrs
-from ..utils import timers
+from ..utils import streams, timers
 from ..utils.log import get_logger
 
 log = get_logger("proof_collection")
@@ -353,7 +353,7 @@ def _pool_async(ctx, sq, reqs, vns, comm=None):
     if ctx.device.type != "cuda":
         return ctx._pool_exec.submit(pool_verify_ranges, ctx, sq, reqs, vns, comm, arrived)
     if not hasattr(ctx, "_pool_stream"):
-        ctx._pool_stream = torch.cuda.Stream(ctx.device)
+        ctx._pool_stream = torch.cuda.Stream(ctx.device, priority=streams.priority(POOL_PRIORITY))
     side, main = ctx._pool_stream, torch.cuda.current_stream(ctx.device)
     side.wait_stream(main)
 
@@ -436,7 +436,8 @@ def early_plane_ok(ctx, sq) -> bool:
         and use_pool(ctx) and os.environ.get("DRYNX_RANGE_PLANE", "1") != "0"
 
 
-LEDGER_PREFETCH = True  # A/B constant (tools/ab_patch.py --no-ledger-prefetch)
+LEDGER_PREFETCH = True  # A/B constants (tools/ab_patch.py --no-ledger-prefetch / --pool-priority)
+POOL_PRIORITY = 0
 
 
 def proof_collection(ctx, sq, local_requests: list, early: dict | None = None, late=None):

@@ -21,6 +21,9 @@ def main():
     ap.add_argument("--me-window", type=int, default=0)
     ap.add_argument("--g1-pair-rows", type=int, default=-1, help="native.G1_MUL_PAIR_ROWS")
     ap.add_argument("--no-ledger-prefetch", action="store_true", help="proof_collection.LEDGER_PREFETCH off")
+    ap.add_argument("--aux-priority", type=int, default=None, help="range_proof.AUX_PRIORITY")
+    ap.add_argument("--val-priority", type=int, default=None, help="range_proof.VAL_PRIORITY")
+    ap.add_argument("--pool-priority", type=int, default=None, help="proof_collection.POOL_PRIORITY")
     a = ap.parse_args(own)
     from drynx_amd import native as nt
     from drynx_amd.proofs import range_proof as rp
@@ -31,6 +34,14 @@ def main():
         from drynx_amd.protocols import proof_collection as pc
 
         pc.LEDGER_PREFETCH = False
+    if a.aux_priority is not None:
+        rp.AUX_PRIORITY = a.aux_priority
+    if a.val_priority is not None:
+        rp.VAL_PRIORITY = a.val_priority
+    if a.pool_priority is not None:
+        from drynx_amd.protocols import proof_collection as pc
+
+        pc.POOL_PRIORITY = a.pool_priority
     if a.r_window:
         rp._r_window = lambda m, G, c=a.r_window: c
     if a.me_window:

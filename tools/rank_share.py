@@ -61,11 +61,30 @@ def _sync():
         torch.cuda.synchronize()
 
 
+_PSTREAM: dict = {}
+
+
 def pool_part(*a):
     """prq.verify_range_pool_part as pool_verify_ranges runs it (slice digests
-    beside the part), digests resolved."""
-    res, dig = prq.verify_range_pool_part(*a, async_digests=True)
-    return res, (dig.result() if hasattr(dig, "result") else dig)
+    beside the part, on a stream of proof_collection.POOL_PRIORITY), digests
+    resolved."""
+    dev = a[3]
+    if not isinstance(dev, torch.device) or dev.type != "cuda":
+        res, dig = prq.verify_range_pool_part(*a, async_digests=True)
+        return res, (dig.result() if hasattr(dig, "result") else dig)
+    from drynx_amd.protocols import proof_collection as pc
+    from drynx_amd.utils import streams
+
+    key = (str(dev), pc.POOL_PRIORITY)
+    if key not in _PSTREAM:
+        _PSTREAM[key] = torch.cuda.Stream(dev, priority=streams.priority(pc.POOL_PRIORITY))
+    st = _PSTREAM[key]
+    st.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(st):
+        res, dig = prq.verify_range_pool_part(*a, async_digests=True)
+        out = res, (dig.result() if hasattr(dig, "result") else dig)
+    torch.cuda.current_stream(dev).wait_stream(st)
+    return out
 
 
 def timed(fn, reps):
