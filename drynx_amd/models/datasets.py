@@ -60,3 +60,32 @@ def clean_file(dataset: str, src: str, dst: str | None = None, label_type: str =
 if __name__ == "__main__":  # python -m drynx_amd.models.datasets PCS file.txt [int|float] [out]
     a = sys.argv[1:]
     clean_file(a[0], a[1], a[3] if len(a) > 3 else None, a[2] if len(a) > 2 else "int")
+
+
+def load_dp_file(path: str, op, device="cpu"):
+    """A data provider's records for ``op`` from a file (the file loader of
+    ``server data-provider new file-loader PATH``): one record per line,
+    values separated by commas.  Logistic regression reads the cleaned
+    dataset layout ``label,f1,...,fd`` (``load_csv_dataset``, the reference's
+    GetDataForDataProvider) -> (X float64 [n, d], y int64 [n]); every other
+    operation takes the first NbrInput values of each record as int64
+    columns -> [column tensors] (the layout of ``generate_fake_data``)."""
+    import numpy as np
+    import torch
+
+    if op.NameOp == "logistic regression":
+        from .logistic_regression import load_csv_dataset
+
+        X, y = load_csv_dataset(path)
+        d = int(op.LRParameters.NbrFeatures)
+        if X.shape[1] != d:
+            raise ValueError(f"{path}: {X.shape[1]} features per record, the query has {d}")
+        return X.to(device), y.to(device)
+    data = np.loadtxt(path, delimiter=",", dtype=np.float64, ndmin=2)
+    n_in = max(1, int(op.NbrInput))
+    if data.shape[1] < n_in:
+        raise ValueError(f"{path}: {data.shape[1]} values per record, the operation reads {n_in}")
+    if not np.all(data[:, :n_in] == np.round(data[:, :n_in])):
+        raise ValueError(f"{path}: the operation {op.NameOp} reads integer values")
+    t = torch.tensor(data[:, :n_in].T.copy(), dtype=torch.int64, device=device)
+    return list(t.unbind(0))

@@ -193,6 +193,12 @@ class NodeServer:
         self._stop = threading.Event()
         self._srv = None
         self._pending_vn: dict = {}   # SurveyQueryToVN received before the group existed
+        # roles this node serves (``server computing-node / verifying-node /
+        # data-provider new``): None = any role (a config without role sections)
+        offered = {r for r, sec in (("cn", "ComputingNode"), ("vn", "VerifyingNode"), ("dp", "DataProvider"))
+                   if sec in config}
+        self.offers = offered or None
+        self.dp_source = config.get("DataProvider") or {}
 
     # --------------------------------------------------------------- TCP side
     def serve_forever(self):
@@ -426,6 +432,28 @@ class NodeServer:
             log.error(traceback.format_exc())
             reply.put(e)
 
+    def _check_roles(self, roles: dict):
+        """Refuse a survey that gives a node a role its config does not offer:
+        every rank checks its own config, one all-gather makes the refusal
+        unanimous (no rank enters the survey's collectives alone)."""
+        mine = {r for r, addrs in roles.items() if self.address in addrs}
+        bad = sorted(mine - self.offers) if self.offers is not None else []
+        msg = f"{self.address} does not serve {bad} (its server config offers {sorted(self.offers)})" if bad else ""
+        msgs = self.comm.all_gather_object(msg) if self.comm is not None and self.comm.world > 1 else [msg]
+        msgs = [m for m in msgs if m]
+        if msgs:
+            raise ValueError("; ".join(msgs))
+
+    def _load_dp_data(self, node, sq, roles: dict):
+        """A data provider configured with a file loader answers from its file
+        (``server data-provider new file-loader PATH``) instead of the query's
+        generated data: its party's records for this survey's operation."""
+        if self.address not in roles.get("dp", []) or self.dp_source.get("Source") != "file-loader":
+            return
+        from ..models.datasets import load_dp_file
+
+        node.dp_data[f"dp:{self.address}"] = load_dp_file(self.dp_source["Path"], sq.Query.Operation, node.device)
+
     def _ensure_node(self, roles: dict):
         from .service import DrynxNode
 
@@ -481,7 +509,9 @@ class NodeServer:
         if name == "libdrynx.SurveyQuery":
             sq = survey_query_from_msg(d)
             roles, _ = roster_of_survey(sq)
+            self._check_roles(roles)
             node = self._ensure_node(roles)
+            self._load_dp_data(node, sq, roles)
             res = node.run_survey(sq if self.rank == 0 else None)
             if self.rank != 0:
                 return None
