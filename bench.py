@@ -171,6 +171,7 @@ def _rank_record(comm, cl, step_ms, elapsed, setup_s, b0, extra: dict | None = N
             "ctrl_collectives": c.get("comm.ctrl_collectives", 0),
             "data_exchanges": c.get("comm.data_exchanges", 0),
             "ledger_written": c.get("ledger.written", 0), "ledger_referenced": c.get("ledger.referenced", 0),
+            "ledger_blob_bytes": c.get("ledger.blob_bytes", 0),
             **(extra or {})}
 
 

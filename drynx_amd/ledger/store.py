@@ -181,6 +181,7 @@ class BlobSegment:
                 data = produce()
         with timers.span("ledger.write"):
             bufs = [memoryview(d).cast("B") for d in (data if many else [data])]
+            timers.count("ledger.blob_bytes", sum(b.nbytes for b in bufs))
             self._make_room(sum(b.nbytes for b in bufs) * _copies())
             self._f.flush()
             off = self._f.seek(0, os.SEEK_END)
@@ -383,6 +384,7 @@ class NodeBlobs(BlobSegment):
             reserve = _gb_env("DRYNX_LEDGER_RESERVE_GB", 8)
             for bid, d in zip(blob_ids, data):
                 b = memoryview(d).cast("B")
+                timers.count("ledger.blob_bytes", b.nbytes)
                 if _budget():
                     while shutil.disk_usage(self.root).free - b.nbytes < reserve and self._files:
                         old = self._files.pop(0)
@@ -448,6 +450,13 @@ class Store:
         return _REF + struct.pack("<QQ", off, buf.nbytes)
 
     def _decode(self, v) -> bytes:
+        v = self._decode_raw(v)
+        from ..proofs import ledger_codec
+
+        # range payloads stored in their compact form: the signed bytes again
+        return ledger_codec.decompress_bytes(v) if ledger_codec.is_compressed(v) else v
+
+    def _decode_raw(self, v) -> bytes:
         v = bytes(v)
         if v.startswith(_REF2):
             off, n = struct.unpack("<QQ", v[len(_REF2): len(_REF2) + 16])

@@ -104,6 +104,8 @@ _SIGS = {
     "dx_lr_reduce": [_P, _P, _L, _L, _L, _P],
     "dx_g1_mul_glv256": [_P, _P, _P, _P, _P, _L, _I, _I, _I],
     "dx_glv_split": [_I, _P, _P, _P, _L],
+    "dx_gt_t2_compress": [_I, _P, _P, _P, _P, _L],
+    "dx_gt_t2_decompress": [_I, _P, _P, _P, _L],
     "dx_rp_verify_fold": [_P, _P, _P, _P, _P, _P, _L, _I, _I],
     "dx_gt_slice_prod": [_I, _P, _P, _P, _P, _P, _P, _L],
     "dx_gt_chunk_weight": [_I, _P, _P, _P, _P, _P, _P, _P, _L],
@@ -345,6 +347,31 @@ def g1_fb_mul_i64(table: torch.Tensor, m: torch.Tensor) -> torch.Tensor:
 
 # rows up to which g1_mul runs two lanes per row (the latency form; tools/bench_g1mul.py)
 G1_MUL_PAIR_ROWS = 1 << 14
+
+
+def gt_t2_compress(a: torch.Tensor, out: torch.Tensor | None = None):
+    """GT elements [n, 96] -> (c [n, 48] int32, ok [n] uint8): c = (1 + g) / h
+    of f = g + h w (torus T2; csrc/kernels/dx_gt_t2.hip); ok = 1 where the
+    decompression gives back exactly these limbs (canonical, unitary, h != 0).
+    ``out``: a contiguous [n, 48] destination for c; then only ok is returned."""
+    n = _rows(a, 96)
+    c = torch.empty((n, 48), dtype=torch.int32, device=a.device) if out is None else out
+    assert c.is_contiguous() and _rows(c, 48) == n
+    ok = torch.empty((n,), dtype=torch.uint8, device=a.device)
+    g, s = _ctx(a, c)
+    _call("dx_gt_t2_compress", g, s, _ptr(a.contiguous()), _ptr(c), _ptr(ok), n)
+    return ok if out is not None else (c, ok)
+
+
+def gt_t2_decompress(c: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """[n, 48] torus-compressed GT elements -> [n, 96] (``out``: a contiguous
+    destination of that shape, e.g. a slice of a payload being rebuilt)."""
+    n = _rows(c, 48)
+    out = torch.empty((n, 96), dtype=torch.int32, device=c.device) if out is None else out
+    assert out.is_contiguous() and _rows(out, 96) == n
+    g, s = _ctx(c, out)
+    _call("dx_gt_t2_decompress", g, s, _ptr(c.contiguous()), _ptr(out), n)
+    return out
 
 
 def glv_split(scalars: torch.Tensor) -> torch.Tensor:

@@ -420,8 +420,21 @@ def start_range_plane(ctx, sq, range_requests: list) -> dict:
         # in the rank's blob segment); payloads whose digest is not known yet
         # (received ones: a digest here would wait for the exchange) go then
         with timers.span("ledger.prefetch"):
-            ctx.ledger_values([r for r in reqs if r.kind == "range" and r.data_digest])
+            ctx.ledger_values([r for r in reqs if r.kind == "range" and r.data_digest], range_shape(sq))
     return out
+
+
+def range_shape(sq):
+    """(S, l) of the query's range proofs -- servers signing the digits, digits
+    per proof -- when every output has the same (u, l), else None: the ledger's
+    compact form locates the GT block of a payload from it before decoding."""
+    q = sq.Query
+    rs = {tuple(r[:2]) for r in (q.Ranges or [])}
+    sigs = q.IVSigs.InputValidationSigs if q.IVSigs is not None else None
+    if len(rs) != 1 or not sigs:
+        return None
+    u, l = next(iter(rs))
+    return (len(sigs), int(l)) if u and l else None
 
 
 def early_plane_ok(ctx, sq) -> bool:

@@ -62,6 +62,9 @@ class SurveyResult:
         return [self.result[g * self.n_out:(g + 1) * self.n_out] for g in range(self.n_groups)]
 
 
+LEDGER_GT_T2 = True  # range payloads stored in their compact form (A/B constant: tools/ab_patch.py)
+
+
 class DrynxNode:
     """Per-rank runtime hosting the logical parties placed on this rank."""
 
@@ -134,7 +137,7 @@ class DrynxNode:
     def ledger_value(self, req):
         return self.ledger_values([req])[0]
 
-    def ledger_values(self, reqs: list) -> list:
+    def ledger_values(self, reqs: list, shape: tuple | None = None) -> list:
         """What a VN stores for each proof request (storeProof,
         proof_collection_protocol.go:318-331): the signed payload.  Range
         bundles' raw-limb tensors go to the rank's shared blob segment once
@@ -164,7 +167,8 @@ class DrynxNode:
             timers.count("ledger.written", len(mine))
             timers.count("ledger.referenced", len(theirs))
             if mine:
-                for k, ref in zip(mine, self._blobs.put_many(mine, self._host_bytes([tensors[k] for k in mine]))):
+                items = [self._ledger_item(reqs[fresh[k][0]], tensors[k], shape) for k in mine]
+                for k, ref in zip(mine, self._blobs.put_many(mine, self._host_bytes(items))):
                     refs[k] = ref
             if theirs:  # another VN rank of this node claimed them: references only, no device-to-host copy
                 for k, ref in zip(theirs, self._blobs.put_refs(theirs, [tensors[k].numel() for k in theirs])):
@@ -196,30 +200,55 @@ class DrynxNode:
             return NodeBlobs(root, device=self.device)
         return BlobSegment(os.path.join(self.workdir, f"ledger_r{self.rank}.blobs"), self.device)
 
+    def _ledger_item(self, req, tensor, shape=None):
+        """What ``_host_bytes`` copies for one stored payload: a range bundle
+        on the GPU in its compact ledger form (``proofs.ledger_codec``: GT
+        elements as torus images, rebuilt bit for bit when read), anything
+        else as is."""
+        if LEDGER_GT_T2 and req.kind == "range" and tensor.is_cuda:
+            from ..proofs import ledger_codec
+
+            pend = ledger_codec.prepare(req, shape)
+            if pend is not None:
+                return pend
+        return tensor
+
     def _host_bytes(self, tensors: list):
         """A producer of the host bytes of ``tensors`` (run by the ledger
         thread): on a GPU one concatenation on the compute stream, then one
-        pinned copy on the ledger stream, so the producer only waits for it."""
-        sizes = [t.numel() for t in tensors]
-        if not tensors[0].is_cuda:
-            return lambda: [memoryview(t.numpy()) for t in tensors]
+        pinned copy on the ledger stream, so the producer only waits for it.
+        An item may be a ``ledger_codec.Pending``: the producer builds its
+        compact image on the ledger stream and copies that instead."""
+        from ..proofs.ledger_codec import Pending
+
+        items = list(tensors)
+        if not any(isinstance(t, Pending) for t in items) and not items[0].is_cuda:
+            return lambda: [memoryview(t.numpy()) for t in items]
         if not hasattr(self, "_ledger_stream"):
             self._ledger_stream = torch.cuda.Stream(self.device)
         st = self._ledger_stream
         st.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(st):
+            for t in items:
+                (t.tensor if isinstance(t, Pending) else t).record_stream(st)
+            # compact images whose GT blocks are known now are built here, on
+            # the ledger stream, and copied with the raw payloads; the others
+            # (layout from the header) are built by the producer
+            raw = [t.launch() if isinstance(t, Pending) and t.regions is not None else t for t in items]
+            raw = [t for t in raw if not isinstance(t, Pending)]
             # each payload straight into its slice of one pinned buffer (no
             # device-side concatenation of the ~600 MB of range payloads), by a
             # small persistent copy grid (nt.copy_to_host) instead of the
             # runtime's blit kernel, whose thousands of PCIe-stalled waves sat
             # beside the verification (~5 ms per query, tools/ab_ledger_copy.py)
-            host = torch.empty((sum(sizes),), dtype=torch.uint8, pin_memory=True)
+            sizes = [t.numel() for t in raw]
+            host = torch.empty((max(1, sum(sizes)),), dtype=torch.uint8, pin_memory=True)
             pairs, slow, o = [], [], 0
-            for t, n in zip(tensors, sizes):
-                t.record_stream(st)
+            for t, n in zip(raw, sizes):
                 (pairs if n % 4 == 0 and t.data_ptr() % 4 == 0 else slow).append((t, host[o: o + n]))
                 o += n
-            nt.copy_to_host(pairs, host)
+            if pairs:
+                nt.copy_to_host(pairs, host)
             for t, h in slow:
                 h.copy_(t, non_blocking=True)
             ev = torch.cuda.Event()
@@ -228,10 +257,15 @@ class DrynxNode:
         def produce():
             ev.synchronize()
             mv = memoryview(host.numpy())
-            out, o = [], 0
-            for n in sizes:
-                out.append(mv[o: o + n])
-                o += n
+            out, o, k = [], 0, 0
+            for it in items:
+                if isinstance(it, Pending) and it.image is None:
+                    out.append(it.produce(st))
+                else:
+                    v = mv[o: o + sizes[k]]
+                    out.append(it.finish(v) if isinstance(it, Pending) else v)
+                    o += sizes[k]
+                    k += 1
             return out
         return produce
 

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--aux-priority", type=int, default=None, help="range_proof.AUX_PRIORITY")
     ap.add_argument("--val-priority", type=int, default=None, help="range_proof.VAL_PRIORITY")
     ap.add_argument("--pool-priority", type=int, default=None, help="proof_collection.POOL_PRIORITY")
+    ap.add_argument("--raw-ledger", action="store_true", help="range payloads stored raw (service.LEDGER_GT_T2 off)")
     a = ap.parse_args(own)
     from drynx_amd import native as nt
     from drynx_amd.proofs import range_proof as rp
@@ -42,6 +43,10 @@ def main():
         from drynx_amd.protocols import proof_collection as pc
 
         pc.POOL_PRIORITY = a.pool_priority
+    if a.raw_ledger:
+        from drynx_amd.services import service
+
+        service.LEDGER_GT_T2 = False
     if a.r_window:
         rp._r_window = lambda m, G, c=a.r_window: c
     if a.me_window:
