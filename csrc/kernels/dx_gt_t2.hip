@@ -1,4 +1,5 @@
-// Torus (T2) compression of GT elements for the proof ledger.
+// Compact ledger form of range-proof payloads: torus (T2) compression of GT
+// elements, and x-coordinate compression of G2 points (below).
 //
 // A GT element is unitary: f = g + h w (g, h in Fp6, w^2 = v) with
 // f conj(f) = g^2 - v h^2 = 1.  For h != 0 it is determined by the single Fp6
@@ -76,9 +77,93 @@ DX_HD void decompress_chunk(const uint32_t *c, uint32_t *a, int64_t i0, int64_t 
     at<Fp12>(a, i) = Fp12{mul(add(x2, v), di), mul(add(x, x), di)};
   }
 }
+// ---- G2 points (the V_j of a range proof): x plus one flag word
+// (bit 0: parity of y's canonical c0, or of c1 when c0 = 0; bit 1: infinity).
+// A point compresses when its limbs are canonical and it is on the twist (or
+// is the all-zero infinity); y comes back as the square root of x^3 + b' with
+// the stored parity (Adj, Rodriguez-Henriquez: Fp2 square root for p = 3 mod 4).
+struct SqrtC {
+  static constexpr uint32_t E34[8] = {0xb61f3f51u, 0x4f082305u, 0x5a1c72a3u, 0x65e05aa4u,
+                                      0xa0605617u, 0x6e14116du, 0xb84c680au, 0x0c19139cu};  // (p - 3) / 4
+  static constexpr uint32_t E12[8] = {0x6c3e7ea3u, 0x9e10460bu, 0xb438e546u, 0xcbc0b548u,
+                                      0x40c0ac2eu, 0xdc2822dbu, 0x7098d014u, 0x18322739u};  // (p - 1) / 2
+};
+
+DX_HD Fp2 pow2(const Fp2 &a, const uint32_t *e) {
+  Fp2 r = Fp2::one();
+  for (int bit = 255; bit >= 0; bit--) {
+    r = sqr(r);
+    if ((e[bit >> 5] >> (bit & 31)) & 1u) r = mul(r, a);
+  }
+  return r;
+}
+
+DX_HD uint32_t y_parity(const Fp2 &y) {
+  const Fp c0 = from_mont(y.c0);
+  return (c0.is_zero() ? from_mont(y.c1).v[0] : c0.v[0]) & 1u;
+}
+
+// one square root of a (a square), else false
+DX_HD bool sqrt2(const Fp2 &a, Fp2 &out) {
+  const Fp2 a1 = pow2(a, SqrtC::E34);
+  const Fp2 alpha = mul(a1, mul(a1, a));
+  const Fp2 a0 = mul(conj(alpha), alpha);
+  const Fp2 m1 = neg(Fp2::one());
+  if (a0 == m1) return false;
+  const Fp2 x0 = mul(a1, a);
+  if (alpha == m1) {
+    out = {fneg(x0.c1), x0.c0};  // i * x0
+  } else {
+    out = mul(pow2(add(Fp2::one(), alpha), SqrtC::E12), x0);
+  }
+  return true;
+}
 }  // namespace
 
 extern "C" {
+// V [n, 32] affine G2 -> x [n, 16], flag [n] (parity | 2 * infinity), ok [n]
+int dx_g2_x_compress(int on_gpu, void *stream, const uint32_t *V, uint32_t *xo, uint32_t *flag, uint8_t *ok,
+                     int64_t n) {
+  auto op = [=] __host__ __device__(int64_t i) {
+    const uint32_t *w = V + 32 * i;
+    bool g = true;
+    for (int k = 0; k < 4; k++) g = g && fp_canonical(w + 8 * k);
+    const G2A P = at<G2A>(V, i);
+    for (int k = 0; k < 16; k++) xo[16 * i + k] = w[k];
+    if (P.is_inf()) {
+      flag[i] = 2u;
+      ok[i] = g ? 1 : 0;
+      return;
+    }
+    flag[i] = y_parity(P.y);
+    ok[i] = g && on_curve(P) ? 1 : 0;
+  };
+  return run(on_gpu, stream, n, op, true, "g2_x_compress");
+}
+
+// x [n, 16], flag [n] -> V [n, 32]; bad[i] = 1 where x^3 + b' has no root
+int dx_g2_x_decompress(int on_gpu, void *stream, const uint32_t *xi, const uint32_t *flag, uint32_t *V,
+                       uint8_t *bad, int64_t n) {
+  auto op = [=] __host__ __device__(int64_t i) {
+    bad[i] = 0;
+    if (flag[i] & 2u) {
+      at<G2A>(V, i) = G2A::inf();
+      return;
+    }
+    const Fp2 x = at<Fp2>(xi, i);
+    Fp2 y;
+    if (!sqrt2(add(mul(sqr(x), x), Fp2::from_limbs(Curve::B2)), y)) {
+      bad[i] = 1;
+      at<G2A>(V, i) = G2A::inf();
+      return;
+    }
+    if (y_parity(y) != (flag[i] & 1u)) y = neg(y);
+    at<G2A>(V, i) = G2A{x, y};
+  };
+  return run(on_gpu, stream, n, op, true, "g2_x_decompress");
+}
+
+
 // a [n, 96] GT elements (Montgomery limbs) -> c [n, 48], ok [n] (1: c round-trips to a)
 int dx_gt_t2_compress(int on_gpu, void *stream, const uint32_t *a, uint32_t *c, uint8_t *ok, int64_t n) {
   const int64_t chunks = (n + kChunk - 1) / kChunk;

@@ -105,6 +105,8 @@ _SIGS = {
     "dx_g1_mul_glv256": [_P, _P, _P, _P, _P, _L, _I, _I, _I],
     "dx_glv_split": [_I, _P, _P, _P, _L],
     "dx_gt_t2_compress": [_I, _P, _P, _P, _P, _L],
+    "dx_g2_x_compress": [_I, _P, _P, _P, _P, _P, _L],
+    "dx_g2_x_decompress": [_I, _P, _P, _P, _P, _P, _L],
     "dx_gt_t2_decompress": [_I, _P, _P, _P, _L],
     "dx_rp_verify_fold": [_P, _P, _P, _P, _P, _P, _L, _I, _I],
     "dx_gt_slice_prod": [_I, _P, _P, _P, _P, _P, _P, _L],
@@ -372,6 +374,32 @@ def gt_t2_decompress(c: torch.Tensor, out: torch.Tensor | None = None) -> torch.
     g, s = _ctx(c, out)
     _call("dx_gt_t2_decompress", g, s, _ptr(c.contiguous()), _ptr(out), n)
     return out
+
+
+def g2_x_compress(V: torch.Tensor, x_out: torch.Tensor | None = None, flag_out: torch.Tensor | None = None):
+    """Affine G2 [n, 32] -> (x [n, 16], flag [n] int32: y parity | 2 * infinity,
+    ok [n] uint8: canonical and on the twist, i.e. ``g2_x_decompress`` gives the
+    same limbs back).  ``x_out`` / ``flag_out``: contiguous destinations."""
+    n = _rows(V, 32)
+    x = torch.empty((n, 16), dtype=torch.int32, device=V.device) if x_out is None else x_out
+    f = torch.empty((n,), dtype=torch.int32, device=V.device) if flag_out is None else flag_out
+    assert x.is_contiguous() and f.is_contiguous() and x.numel() == 16 * n and f.numel() == n
+    ok = torch.empty((n,), dtype=torch.uint8, device=V.device)
+    g, s = _ctx(V, x, f)
+    _call("dx_g2_x_compress", g, s, _ptr(V.contiguous()), _ptr(x), _ptr(f), _ptr(ok), n)
+    return x, f, ok
+
+
+def g2_x_decompress(x: torch.Tensor, flag: torch.Tensor, out: torch.Tensor | None = None):
+    """(x [n, 16], flag [n]) -> (affine G2 [n, 32], bad [n] uint8: no point
+    with that x)."""
+    n = _rows(x, 16)
+    V = torch.empty((n, 32), dtype=torch.int32, device=x.device) if out is None else out
+    assert V.is_contiguous() and V.numel() == 32 * n and flag.numel() == n
+    bad = torch.empty((n,), dtype=torch.uint8, device=x.device)
+    g, s = _ctx(x, flag, V)
+    _call("dx_g2_x_decompress", g, s, _ptr(x.contiguous()), _ptr(flag.contiguous()), _ptr(V), _ptr(bad), n)
+    return V, bad
 
 
 def glv_split(scalars: torch.Tensor) -> torch.Tensor:

@@ -5,8 +5,8 @@ proof_collection_protocol.go:318-331; bbolt keeps them all).  ~68% of a
 bundle is GT elements -- the A_j commitments, 384 bytes each -- and a GT
 element is unitary, so the ledger keeps each as its torus (T2) image c =
 (1 + g) / h, 192 bytes (``native.gt_t2_compress``, csrc/kernels/dx_gt_t2.hip):
-a query's ~560 MB of range payloads become ~370 MB to copy off the GPU and
-fdatasync (verdict r4 weak #4: the W = 8 ledger is disk-bound).
+so fewer bytes to copy off the GPU and fdatasync per query (verdict r4 weak
+#4: the W = 8 ledger is disk-bound).
 
 Reading a value back rebuilds the signed payload bit for bit
 (``decompress_bytes``; ``ledger.store.Store`` does it for every blob it
@@ -15,10 +15,15 @@ list whose GT elements do not all round-trip exactly (non-canonical limbs,
 not unitary: a malformed or malicious proof) makes the whole bundle fall back
 to the raw bytes.
 
+The V_j (G2 points, 23% of a bundle) are kept as x plus one flag word (y's
+parity, infinity; ``native.g2_x_compress``): 32 -> 17 words each.  Together
+a query's ~567 MB of range payloads become ~313 MB.
+
 Blob layout (int32 words): MAGIC, ok flag (written on the device: 1 when
 every element round-trips), raw payload words (int64), region count, then
-(word offset int64, element count int64) per region, then the payload with
-each region's A block replaced by its T2 image.
+(word offset int64, element count int64, kind) per region -- kind 0: GT block
+(96 -> 48 words per element), 1: G2 block (32 -> 17: x block, then flags) --
+then the payload with each region replaced by its compact image.
 """
 from __future__ import annotations
 
@@ -29,6 +34,14 @@ from .. import native as nt
 
 MAGIC = 0x32435052  # b"RPC2" little-endian
 _HEAD = 5
+_RW = 5  # header words per region
+_GT, _G2 = 0, 1
+_FULL = {_GT: 96, _G2: 32}
+_SMALL = {_GT: 48, _G2: 17}
+
+
+def _regions(b, k: int) -> np.ndarray:
+    return np.frombuffer(bytes(b[4 * _HEAD: 4 * (_HEAD + _RW * k)]), dtype=np.int32).reshape(k, _RW)
 
 
 def is_compressed(b) -> bool:
@@ -39,11 +52,15 @@ def is_compressed(b) -> bool:
         return False
     w = np.frombuffer(bytes(b[:4 * _HEAD]), dtype=np.int32)
     k = int(w[4])
-    if int(w[1]) != 1 or k < 0 or 4 * (_HEAD + 4 * k) > len(b):
+    if int(w[1]) != 1 or k < 1 or 4 * (_HEAD + _RW * k) > len(b):
         return False
     total = int(w[2:4].view(np.int64)[0])
-    regs = np.frombuffer(bytes(b[4 * _HEAD: 4 * (_HEAD + 4 * k)]), dtype=np.int64).reshape(k, 2)
-    return bool(len(b) // 4 == _HEAD + 4 * k + total - 48 * int(regs[:, 1].sum())) if k else False
+    r = _regions(b, k)
+    if not np.isin(r[:, 4], (_GT, _G2)).all():
+        return False
+    m = r[:, 2:4].copy().view(np.int64).reshape(-1)
+    saved = sum(int(mi) * (_FULL[int(kd)] - _SMALL[int(kd)]) for mi, kd in zip(m, r[:, 4]))
+    return len(b) // 4 == _HEAD + _RW * k + total - saved
 
 
 class Pending:
@@ -79,21 +96,25 @@ class Pending:
         if dev.type == "cuda":
             t.record_stream(torch.cuda.current_stream(dev))
         head = [MAGIC, 0] + list(np.array([t.numel()], dtype=np.int64).view(np.int32)) + [len(self.regions)]
-        for off, m in self.regions:
-            head += list(np.array([off, m], dtype=np.int64).view(np.int32))
-        n_img = len(head) + t.numel() - sum(48 * m for _, m in self.regions)
+        for off, m, kind in self.regions:
+            head += list(np.array([off, m], dtype=np.int64).view(np.int32)) + [kind]
+        n_img = len(head) + t.numel() - sum(m * (_FULL[kd] - _SMALL[kd]) for _, m, kd in self.regions)
         img = torch.empty((n_img,), dtype=torch.int32, device=dev)
         hdr = torch.tensor(head, dtype=torch.int32)
         if dev.type == "cuda":
             hdr = hdr.pin_memory().to(dev, non_blocking=True)
         pairs, oks, pos, q = [(hdr, img[:len(head)])], [], 0, len(head)
-        for off, m in self.regions:
+        for off, m, kind in self.regions:
             pairs.append((t[pos:off], img[q: q + off - pos]))
             q += off - pos
-            c = img[q: q + 48 * m].view(m, 48)
-            oks.append(nt.gt_t2_compress(t[off: off + 96 * m].view(m, 96), out=c))
-            q += 48 * m
-            pos = off + 96 * m
+            src = t[off: off + _FULL[kind] * m].view(m, _FULL[kind])
+            if kind == _GT:
+                oks.append(nt.gt_t2_compress(src, out=img[q: q + 48 * m].view(m, 48)))
+            else:
+                oks.append(nt.g2_x_compress(src, x_out=img[q: q + 16 * m].view(m, 16),
+                                            flag_out=img[q + 16 * m: q + 17 * m])[2])
+            q += _SMALL[kind] * m
+            pos = off + _FULL[kind] * m
         pairs.append((t[pos:], img[q:]))
         nt.batched_copy(pairs)  # the header and every raw segment in one launch
         okall = torch.cat(oks).all() if len(oks) > 1 else oks[0].all()
@@ -135,7 +156,7 @@ def regions_from_header(t: torch.Tensor) -> list:
             if off + 96 * m != pos + ln:
                 return []
             if m:
-                regions.append((off, m))
+                regions += [(off - 32 * m, m, _G2), (off, m, _GT)]
         pos += ln
     return regions if pos == W else []
 
@@ -150,7 +171,7 @@ def regions_from_shape(words: int, S: int, l: int) -> list | None:
         return None
     n = (words - 7) // per
     m = n * S * l
-    return [(words - 96 * m, m)]
+    return [(words - 128 * m, m, _G2), (words - 96 * m, m, _GT)] if m else None
 
 
 def prepare(req, shape: tuple | None = None) -> Pending | None:
@@ -167,12 +188,12 @@ def prepare(req, shape: tuple | None = None) -> Pending | None:
     end = base + 4 * t.numel()
     regions = []
     for r in lists:
-        A = getattr(r, "A", None)
-        if A is None or A.numel() == 0:
-            continue
-        if not A.is_contiguous() or A.dtype != torch.int32 or not (base <= A.data_ptr() < end):
-            return None
-        regions.append(((A.data_ptr() - base) // 4, A.shape[0]))
+        for F, kind in ((getattr(r, "V", None), _G2), (getattr(r, "A", None), _GT)):
+            if F is None or F.numel() == 0:
+                continue
+            if not F.is_contiguous() or F.dtype != torch.int32 or not (base <= F.data_ptr() < end):
+                return None
+            regions.append(((F.data_ptr() - base) // 4, F.shape[0], kind))
     if not regions:
         return None
     regions.sort()
@@ -186,19 +207,26 @@ def decompress_bytes(b, device=None) -> bytes:
     w = np.frombuffer(bytes(b), dtype=np.int32)
     total = int(w[2:4].view(np.int64)[0])
     k = int(w[4])
-    regs = w[_HEAD: _HEAD + 4 * k].view(np.int64).reshape(k, 2) if k else np.zeros((0, 2), np.int64)
-    body = w[_HEAD + 4 * k:]
+    r = _regions(b, k)
+    body = w[_HEAD + _RW * k:]
     if device is None:
         device = "cuda" if torch.cuda.is_available() else "cpu"
     out = torch.empty((total,), dtype=torch.int32, device=device)
     src = torch.from_numpy(body.copy()).to(device)
     pos = bp = 0
-    for off, m in regs.tolist():
-        n_raw = off - pos
-        out[pos:off].copy_(src[bp: bp + n_raw])
-        bp += n_raw
-        nt.gt_t2_decompress(src[bp: bp + 48 * m].view(m, 48), out=out[off: off + 96 * m].view(m, 96))
-        bp += 48 * m
-        pos = off + 96 * m
+    for row in r:
+        off, m = (int(v) for v in row[:4].copy().view(np.int64))
+        kind = int(row[4])
+        out[pos:off].copy_(src[bp: bp + off - pos])
+        bp += off - pos
+        dst = out[off: off + _FULL[kind] * m].view(m, _FULL[kind])
+        if kind == _GT:
+            nt.gt_t2_decompress(src[bp: bp + 48 * m].view(m, 48), out=dst)
+        else:
+            _, bad = nt.g2_x_decompress(src[bp: bp + 16 * m].view(m, 16), src[bp + 16 * m: bp + 17 * m], out=dst)
+            if bool(bad.any()):
+                raise ValueError("compressed range payload holds an x with no G2 point")
+        bp += _SMALL[kind] * m
+        pos = off + _FULL[kind] * m
     out[pos:].copy_(src[bp:])
     return out.cpu().numpy().tobytes()
