@@ -13,7 +13,8 @@ step fault 300 python -u bench.py --steps 10 --warmup 3 --fault-dp 3 --json-out 
 step u0l0 300 python -u bench.py --steps 20 --warmup 5 --u 0 --l 0 --json-out $O/u0l0.json
 OMP_NUM_THREADS=1 step ctrl 300 python -u tools/ctrl_round.py --world 8 --rounds 300 --json-out $O/ctrl_w8.json
 step share 500 python -u tools/rank_share.py --world 8 --reps 3 --serial-json $O/u0l0.json --ctrl-json $O/ctrl_w8.json --json-out $O/rank_share_w8.json
-DRYNX_TRACE=$O/setup_trace.json step setup 400 python -u tools/setup_share.py --world 8 --rank 0 --bench-json $O/bench.json --json-out $O/setup_share_w8.json
+step setupf 400 python -u tools/setup_share.py --mode full --json-out $O/setup_full.json
+DRYNX_TRACE=$O/setup_trace.json step setup 400 python -u tools/setup_share.py --world 8 --rank 0 --full-json $O/setup_full.json --bench-json $O/bench.json --json-out $O/setup_share_w8.json
 python3 tools/host_trace.py $O/setup_trace.json 1 > $O/setup_host_trace.txt || true
 DRYNX_TRACE=$O/trace.json RANK_SHARE_TRACE_ONLY=1 RANK_SHARE_PARTS=6,3 RANK_SHARE_TRACE_REPS=2 step tl 400 rocprofv3 --kernel-trace --output-format csv -d $O/kt -o run -- python3 -u tools/rank_share.py --world 8 --reps 1
 T=$(find $O/kt -name "*kernel_trace.csv" -print -quit)

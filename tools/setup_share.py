@@ -86,6 +86,8 @@ def main():
                     help="assumed per-rank receive rate of the table broadcasts (GB/s): one xGMI link's worth")
     ap.add_argument("--bench-json", default=None, help="1-GPU bench.py JSON (its setup_s)")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--mode", choices=("share", "full"), default="share")
+    ap.add_argument("--full-json", default=None, help="JSON of a --mode full run (its build_full_s)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
     if dev.type == "cuda":
@@ -124,23 +126,35 @@ def main():
         return t0, time.perf_counter() - t0
 
     sm.attach_shard(None, False)
-    # the full 1-rank build (module / kernel first-use costs included, as in
-    # bench.py's setup_s), then this rank's share.  Only two builds: the third
-    # ~110 GB allocation of a process stalls 3-6 s before its build starts
-    # whichever build it is (profiles/r5/final/setup_host_trace.txt,
-    # profiles/r5/setup/setup_host_trace.txt), and a real rank allocates once
-    res["build_full_s"] = round(build("full")[1], 3)
-    res["table_bytes"] = sm.table_bytes()
+    # ONE build per process, as a real rank allocates its tables once: a
+    # second ~110 GB allocation after a free stalled 3-6 s before its build
+    # started on some boxes, whichever build it was (profiles/r5/final/,
+    # profiles/r5/final2/setup_host_trace.txt).  --mode full: the whole
+    # 1-rank build (module / kernel first-use costs included, as in bench.py's
+    # setup_s); --mode share (default): this rank's share, with build_full_s
+    # taken from a --full-json of the other mode
+    if a.mode == "full":
+        res["build_full_s"] = round(build("full")[1], 3)
+        res["table_bytes"] = sm.table_bytes()
+        print(json.dumps(res), flush=True)
+        if a.json_out:
+            json.dump(res, open(a.json_out, "w"), indent=1)
+        timers.dump_trace()
+        node.close(remove=True)
+        return
+    if a.full_json:
+        res["build_full_s"] = json.load(open(a.full_json))["build_full_s"]
     emu = EmuShard(a.world, a.rank, dev)
     sm._shard = emu  # as attach_shard does for a W-rank communicator
     t0, total = build("share")
+    res["table_bytes"] = sm.table_bytes()
     res["landing_hbm_s"] = round(emu.landing_s, 3)
     res["build_share_s"] = round((emu.first_landing or (t0 + total)) - t0, 3)
     res["share_total_s"] = round(total, 3)
     res["recv_bytes"] = emu.recv_bytes
     res["xgmi_gbs_assumed"] = a.xgmi_gbs
     res["xgmi_s"] = round(emu.recv_bytes / (a.xgmi_gbs * 1e9), 3)
-    if a.bench_json:
+    if a.bench_json and "build_full_s" in res:
         b = json.load(open(a.bench_json))
         res["bench_setup_s"] = b["setup_s"]
         res["projected_setup_s"] = round(b["setup_s"] - res["build_full_s"] + res["build_share_s"]
