@@ -25,10 +25,12 @@ signed range-proof inbox, and then times, alone and synchronised (median of
 
 Every rank's pool part starts when the range fan-out (ONE exchange after
 every rank has signed its proofs) completes, so the projected step is
-max(serial on rank 0, max_k prove(k) + max_k pool(k)) + ctrl
-(``projection_step_ms``); ``projection_ms`` keeps each rank's own
-prove + pool (+ ctrl), the bound without that synchronisation.  Peers'
-traffic over xGMI is not in it (the 8-GPU run measures it).
+max(serial on rank 0, fan-out end + max_k pool(k)) + ctrl
+(``projection_step_ms``), the fan-out ending when the last link has
+delivered: max over senders of prove(k) + its largest per-peer payload
+(full bundles to VN ranks, slices to helpers) at ``--xgmi-link-gbs`` (one
+direction of one link; the ``xgmi`` term).  ``projection_ms`` keeps each
+rank's own prove + pool (+ ctrl), the bound without that synchronisation.
 Usage: python tools/rank_share.py [--world 8] [--reps 5] [--serial-json f] [--ctrl-json f]
 """
 from __future__ import annotations
@@ -148,6 +150,8 @@ def main():
                     help="torch.profiler of one whole 1-GPU query (every thread): GPU time per framework span / op")
     ap.add_argument("--ctrl-json", default=None, help="tools/ctrl_round.py JSON (W-process control round latency)")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--xgmi-link-gbs", type=float, default=76.5,
+                    help="one direction of one xGMI link (GB/s): the fan-out term of the projection")
     ap.add_argument("--order", default=None, help="comma list: the order the ranks are measured in (default 0..W-1)")
     ap.add_argument("--torch-prof", default=None,
                     help="also profile the 1-GPU pooled check of the whole inbox and the proving of every DP "
@@ -321,8 +325,30 @@ def main():
     res["projection_ms"] = proj
     prove_max = max(v["prove_ms"] for v in res["ranks"].values())
     pool_max = max(v["pool_ms"] for v in res["ranks"].values())
-    res["projection_step_ms"] = round(max(serial, prove_max + pool_max) + ctrl, 2)
-    res["projection_terms_ms"] = {"prove_max": prove_max, "pool_max": pool_max, "serial": serial,
+    # the range fan-out over xGMI: every rank's payloads to each peer over that
+    # peer's link (full bundles to VN ranks, the helper's slice to the others);
+    # the pool parts start when the last link has delivered
+    dp_rank = {dp: k for k, ids in dps_of.items() for dp in ids}
+    link = {}
+    for i in rng:
+        r = reqs[i]
+        src = dp_rank.get(r.sender_id)
+        if src is None:
+            continue
+        full = r.tensor.numel() * r.tensor.element_size() if r.tensor is not None else len(r.data)
+        lists = prq._range_lists(r, dev)
+        for dst in range(W):
+            if dst == src:
+                continue
+            nb = full if dst in vn_ranks else prq.range_bundle_pack(prq.slice_lists(lists, sq, parts[dst])).numel() * 4
+            link[(src, dst)] = link.get((src, dst), 0) + nb
+    bw = a.xgmi_link_gbs * 1e6  # bytes per ms
+    exchange_end = max((res["ranks"][s_]["prove_ms"] + max((b for (s2, _), b in link.items() if s2 == s_),
+                                                          default=0) / bw) for s_ in res["ranks"])
+    xgmi = round(exchange_end - prove_max, 3)
+    res["xgmi_link_bytes_max"] = max(link.values(), default=0)
+    res["projection_step_ms"] = round(max(serial, exchange_end + pool_max) + ctrl, 2)
+    res["projection_terms_ms"] = {"prove_max": prove_max, "xgmi": xgmi, "pool_max": pool_max, "serial": serial,
                                   "ctrl": round(ctrl, 3)}
     print(json.dumps({"projection_ms": proj, "step_ms": res["projection_step_ms"],
                       "terms": res["projection_terms_ms"]}), flush=True)
