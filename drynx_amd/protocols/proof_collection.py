@@ -491,7 +491,7 @@ def proof_collection(ctx, sq, local_requests: list, early: dict | None = None, l
             if LEDGER_PREFETCH and local_vns and hasattr(ctx, "ledger_values"):
                 with timers.span("ledger.prefetch"):
                     ctx.ledger_values([r for r in rs if r.kind != "shuffle" and r.data_digest
-                                       and r.tensor is not None])
+                                       and r.tensor is not None], range_shape(sq))
 
         prefetch(reqs)
         pending = checks(reqs, pooled)

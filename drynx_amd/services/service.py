@@ -63,6 +63,10 @@ class SurveyResult:
 
 
 LEDGER_GT_T2 = True  # range payloads stored in their compact form (A/B constant: tools/ab_patch.py)
+# smaller payloads stay raw: a one-record DP's 27 KB bundle saves little and
+# its own launches and header reads cost more (6000 one-record DPs: 1.7 -> 9.4 s
+# per query when every bundle was compacted, profiles/r5/allops)
+LEDGER_COMPACT_MIN_BYTES = 1 << 20
 
 
 class DrynxNode:
@@ -205,7 +209,7 @@ class DrynxNode:
         on the GPU in its compact ledger form (``proofs.ledger_codec``: GT
         elements as torus images, rebuilt bit for bit when read), anything
         else as is."""
-        if LEDGER_GT_T2 and req.kind == "range" and tensor.is_cuda:
+        if LEDGER_GT_T2 and req.kind == "range" and tensor.is_cuda and tensor.numel() >= LEDGER_COMPACT_MIN_BYTES:
             from ..proofs import ledger_codec
 
             pend = ledger_codec.prepare(req, shape)
