@@ -836,6 +836,25 @@ def copy_to_host(pairs: list, host_base: torch.Tensor, blocks: int = COPY_OUT_BL
     _call("dx_copy_out", 1, st, _ptr(dd), _ptr(ht), len(pairs), c0, int(blocks))
 
 
+def _strided_rows(ts: list):
+    """[G, *shape] strided view over G equally shaped contiguous blocks that
+    sit at a constant byte step in ONE storage, else None."""
+    t0 = ts[0]
+    if len(ts) < 8 or not all(t.is_contiguous() and t.shape == t0.shape and t.dtype == t0.dtype for t in ts):
+        return None
+    st = t0.untyped_storage().data_ptr()
+    if any(t.untyped_storage().data_ptr() != st for t in ts):
+        return None
+    es = t0.element_size()
+    step = ts[1].data_ptr() - t0.data_ptr()
+    if step % es or step < t0.numel() * es:
+        return None
+    p0 = t0.data_ptr()
+    if any(t.data_ptr() != p0 + g * step for g, t in enumerate(ts)):
+        return None
+    return t0.as_strided((len(ts), t0.numel()), (step // es, 1))
+
+
 def cat_rows(groups: list) -> list:
     """``[torch.cat(g) for g in groups]`` (dim 0) with every copy in ONE
     ``batched_copy`` launch.  A one-tensor group is returned as is (no copy);
@@ -848,6 +867,13 @@ def cat_rows(groups: list) -> list:
         t0 = g_[0]
         if any(t.numel() * t.element_size() % 4 for t in g_):
             outs.append(torch.cat(g_))
+            continue
+        sv = _strided_rows(g_)
+        if sv is not None:
+            # equally shaped blocks at a constant stride in one storage (the
+            # fields of thousands of one-proof bundles packed as rows of one
+            # tensor): ONE strided copy, not one copy descriptor per block
+            outs.append(sv.clone(memory_format=torch.contiguous_format).view((-1,) + tuple(t0.shape[1:])))
             continue
         out = torch.empty((sum(t.shape[0] for t in g_),) + tuple(t0.shape[1:]), dtype=t0.dtype, device=t0.device)
         o = 0
