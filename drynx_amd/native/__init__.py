@@ -840,7 +840,9 @@ def _strided_rows(ts: list):
     """[G, *shape] strided view over G equally shaped contiguous blocks that
     sit at a constant byte step in ONE storage, else None."""
     t0 = ts[0]
-    if len(ts) < 8 or not all(t.is_contiguous() and t.shape == t0.shape and t.dtype == t0.dtype for t in ts):
+    # many small blocks only (thousands of one-record DPs): a few large ones
+    # copy faster through the batched 16 KB-chunk kernel
+    if len(ts) < 256 or not all(t.is_contiguous() and t.shape == t0.shape and t.dtype == t0.dtype for t in ts):
         return None
     st = t0.untyped_storage().data_ptr()
     if any(t.untyped_storage().data_ptr() != st for t in ts):
