@@ -105,3 +105,18 @@ def test_unpack_many_wide_lists():
         assert got[0].offset == ref[0].offset and got[0].cols == ref[0].cols
         assert torch.equal(got[0].commit.K, ref[0].commit.K) and torch.equal(got[0].commit.C, ref[0].commit.C)
     assert isinstance(out[2], Exception)
+
+
+def test_cat_rows_strided_blocks_match_cat():
+    """native.cat_rows: >= 256 equally shaped blocks at a constant stride in one
+    storage take one strided copy; the result equals torch.cat and owns its
+    memory (also when the blocks are adjacent)."""
+    from drynx_amd import native as nt
+
+    base = torch.arange(300 * 37, dtype=torch.int32).view(300, 37)
+    for blocks in ([base[i, 5:17].view(3, 4) for i in range(300)],
+                   [base.view(-1)[12 * i: 12 * (i + 1)].view(3, 4) for i in range(300)]):
+        out = nt.cat_rows([blocks])[0]
+        assert torch.equal(out, torch.cat(blocks)) and out.untyped_storage().data_ptr() != base.data_ptr()
+    few = [base[i, 5:17].view(3, 4) for i in range(10)]
+    assert torch.equal(nt.cat_rows([few])[0], torch.cat(few))
