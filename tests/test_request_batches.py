@@ -120,3 +120,27 @@ def test_cat_rows_strided_blocks_match_cat():
         assert torch.equal(out, torch.cat(blocks)) and out.untyped_storage().data_ptr() != base.data_ptr()
     few = [base[i, 5:17].view(3, 4) for i in range(10)]
     assert torch.equal(nt.cat_rows([few])[0], torch.cat(few))
+
+
+def test_unpack_many_packed_rows_fast_path(bundles):
+    """>= 64 one-list bundles packed as rows of one tensor take the unbind fast
+    path; every list equals the per-bundle unpack (fields, offsets, columns)."""
+    bs, _, _ = bundles
+    many = [bs[g % 4] for g in range(80)]
+    ts, packed = prq.range_bundle_pack_many(many)
+    assert packed is not None
+    fast = prq.range_bundle_unpack_many(ts)
+    for t, f in zip(ts, fast):
+        ref = prq.range_bundle_unpack(t)
+        assert len(f) == len(ref) == 1
+        a, b = f[0], ref[0]
+        assert (a.u, a.l, a.S, a.offset, a.cols) == (b.u, b.l, b.S, b.offset, b.cols)
+        for fld in ("challenge", "zr", "D", "zphi", "zv", "V", "A"):
+            assert torch.equal(getattr(a, fld), getattr(b, fld)), fld
+        assert torch.equal(a.commit.K, b.commit.K) and torch.equal(a.commit.C, b.commit.C)
+    # a malformed row (wrong magic) makes the batch take the per-bundle path: that bundle alone is rejected
+    bad = packed.clone()
+    bad[5, 2] = 0
+    rows = list(bad.unbind(0))
+    res = prq.range_bundle_unpack_many(rows)
+    assert isinstance(res[5], Exception) and all(isinstance(x, list) for i, x in enumerate(res) if i != 5)
