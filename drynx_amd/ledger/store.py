@@ -42,6 +42,43 @@ _REF = b"\x00DXBLOB1"
 _REF2 = b"\x00DXBLOB2"  # + offset, length (u64) + path of a shared BlobSegment
 
 
+def _addr(mv: memoryview) -> int:
+    import numpy as np
+
+    return np.frombuffer(mv, dtype=np.uint8).__array_interface__["data"][0] if mv.nbytes else 0
+
+
+def _coalesce(bufs: list) -> list:
+    """Runs of buffers that sit back to back in one exporter (the slices of
+    one pinned device-to-host buffer: thousands of small payloads of a
+    many-DP query) merged into single views, so they are written by one
+    positioned write instead of one pool task each; written bytes unchanged."""
+    if len(bufs) < 64:
+        return bufs
+    out, run = [], None  # run: (exporter, base view, base address, start, end)
+    for b in bufs:
+        b = memoryview(b).cast("B") if b.format != "B" or b.ndim != 1 else b
+        obj = b.obj
+        a = _addr(b)
+        if run is not None and obj is run[0] and a == run[2] + run[4]:
+            run = (run[0], run[1], run[2], run[3], run[4] + b.nbytes)
+            continue
+        if run is not None:
+            out.append(run[1][run[3]: run[4]])
+        try:
+            base = memoryview(obj).cast("B")
+            base_a = _addr(base)
+            if not base_a <= a <= base_a + base.nbytes - b.nbytes:
+                raise ValueError
+            run = (obj, base, base_a, a - base_a, a - base_a + b.nbytes)
+        except (TypeError, ValueError):
+            out.append(b)
+            run = None
+    if run is not None:
+        out.append(run[1][run[3]: run[4]])
+    return out
+
+
 class BlobRef:
     """A value living in a rank-level BlobSegment (written once, referenced by
     the stores of every VN hosted on the rank)."""
@@ -250,7 +287,7 @@ class BlobSegment:
         threads with positioned writes (they release the GIL; one sequential
         write of a query's ~540 MB of range proofs took ~50 ms)."""
         pieces, pos = [], off
-        for b in bufs:
+        for b in _coalesce(bufs):
             for a in range(0, b.nbytes, self._PIECE):
                 pieces.append((b[a: a + self._PIECE], pos + a))
             pos += b.nbytes

@@ -118,3 +118,19 @@ def test_g2_block_fallback(bundle):
     bad[off + 3] ^= 1  # x of the first V: (almost surely) no longer on the twist
     stored = bytes(_roundtrip(bad))
     assert not lc.is_compressed(stored) and stored == bad.cpu().numpy().tobytes()
+
+
+def test_coalesce_adjacent_blob_buffers():
+    """ledger.store._coalesce: slices of one host buffer that sit back to back
+    merge into one write; other buffers break the run; bytes unchanged."""
+    import numpy as np
+
+    from drynx_amd.ledger.store import _coalesce
+
+    mv = memoryview(np.arange(10000, dtype=np.uint8))
+    bufs = [mv[i * 100:(i + 1) * 100] for i in range(100)]
+    assert [b.nbytes for b in _coalesce(bufs)] == [10000]
+    mixed = bufs[:50] + [memoryview(b"x" * 100)] + bufs[60:]
+    out = _coalesce(mixed)
+    assert [b.nbytes for b in out] == [5000, 100, 4000]
+    assert b"".join(bytes(b) for b in out) == b"".join(bytes(b) for b in mixed)
