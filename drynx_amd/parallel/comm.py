@@ -49,11 +49,16 @@ class Comm:
     def all_gather_object(self, obj) -> list:
         return [obj]
 
-    def exchange(self, outgoing: dict, recv_sizes: dict | None = None) -> dict:
+    def exchange(self, outgoing: dict, recv_sizes: dict | None = None, abort: str | None = None) -> dict:
         """outgoing: dst_rank -> int32 tensor (any shape, on self.device).
         Returns src_rank -> flat int32 tensor received (only non-empty ones).
         ``recv_sizes`` (src -> numel), when the protocol already knows them,
-        saves the size round (and its host synchronisation)."""
+        saves the size round (and its host synchronisation).  ``abort``: this
+        rank cannot take part (e.g. its DPs' answers do not fit the query); it
+        announces a negative size to every rank in the size round, so EVERY
+        rank raises instead of the others waiting in a later collective."""
+        if abort is not None:
+            raise ExchangeAborted(f"rank {self.rank}: {abort}")
         return {self.rank: outgoing[self.rank].reshape(-1)} if self.rank in outgoing else {}
 
     def plane(self, name: str) -> "Comm":
@@ -80,6 +85,10 @@ class Comm:
         tens = {d: _bytes_to_i32(b, self.device) for d, b in outgoing.items()}
         got = self.exchange(tens)
         return {s: _i32_to_bytes(t) for s, t in got.items()}
+
+
+class ExchangeAborted(RuntimeError):
+    """A rank aborted a data-plane exchange (``Comm.exchange(abort=...)``)."""
 
 
 def _bytes_to_i32(b: bytes, device) -> torch.Tensor:
@@ -142,23 +151,31 @@ class DistComm(Comm):
     def all_gather_object(self, obj) -> list:
         return _gather_obj(self.rank, self.world, obj, self._ctrl)
 
-    def exchange(self, outgoing: dict, recv_sizes: dict | None = None) -> dict:
+    def exchange(self, outgoing: dict, recv_sizes: dict | None = None, abort: str | None = None) -> dict:
         """ONE ``all_to_all_single`` whatever the backend: on RCCL the per-peer
         splits go straight over the xGMI links from HBM; on gloo (CPU tests,
         one-GPU rehearsals) the same call runs on host-staged buffers.  Unknown
-        receive sizes cost one size round (a W-element all-to-all)."""
+        receive sizes cost one size round (a W-element all-to-all), which also
+        carries an ``abort`` (negative sizes) to every rank."""
         W = self.world
         stage = self._stage
         timers.count("comm.data_exchanges")
-        flat = {d: t.reshape(-1).to(torch.int32) for d, t in outgoing.items()}
+        flat = {d: t.reshape(-1).to(torch.int32) for d, t in outgoing.items()} if abort is None else {}
         send_sizes = [0] * W
         for d, t in flat.items():
             send_sizes[d] = t.numel()
         if recv_sizes is None:
-            ss = torch.tensor(send_sizes, dtype=torch.int64, device=stage)
+            ss = torch.tensor([-1] * W if abort is not None else send_sizes, dtype=torch.int64, device=stage)
             rs = torch.empty_like(ss)
             dist.all_to_all_single(rs, ss)
             recv = [int(v) for v in rs.tolist()]
+            if abort is not None:
+                raise ExchangeAborted(f"rank {self.rank}: {abort}")
+            bad = [s for s, v in enumerate(recv) if v < 0]
+            if bad:
+                raise ExchangeAborted(f"rank {self.rank}: exchange aborted by rank(s) {bad}")
+        elif abort is not None:
+            raise ValueError("exchange(abort=...) needs the size round (recv_sizes=None)")
         else:
             recv = [int(recv_sizes.get(s, 0)) for s in range(W)]
         parts = [flat[d].to(stage) for d in range(W) if send_sizes[d]]

@@ -37,12 +37,15 @@ def rows_to_cv(rows: torch.Tensor) -> CipherVector:
     return CipherVector(rows[:, :24].contiguous(), rows[:, 24:].contiguous())
 
 
-def route(comm: Comm, items: list, key_index) -> dict:
+def route(comm: Comm, items: list, key_index, abort: str | None = None) -> dict:
     """items: list of (dst_rank, key, CipherVector).  Returns {key: CipherVector}
     of the items addressed to this rank.  ``key_index``: key -> int and back
     (a ``KeyIndex``) shared by all ranks.  Per destination the buffer is
     [count, key_0, n_0, key_1, n_1, ..., rows_0, rows_1, ...]: the receiver
-    copies only the 1 + 2 count header words to the host."""
+    copies only the 1 + 2 count header words to the host.  ``abort``: this
+    rank cannot send (every rank raises, ``Comm.exchange``)."""
+    if abort is not None:
+        comm.exchange({}, abort=abort)
     per_dst: dict = {}
     for dst, key, cv in items:
         per_dst.setdefault(dst, []).append((key_index.encode(key), len(cv), cv_to_rows(cv).to(comm.device).reshape(-1)))

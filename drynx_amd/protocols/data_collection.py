@@ -251,22 +251,34 @@ def data_collection(ctx, sq) -> tuple:
     # thousands (ScaleDPs, one record each) the syncs serialise the encoders
     sync_timer = len(local_dps) <= 16
     batchable = sq.Query.Operation.NameOp in enc.BATCH_OPS + ("logistic regression",)
-    if local_dps and batchable:
-        # every DP of this rank in one batch; each DP's encoding latency is the batch's
-        with timers.timed("DPencodingBatch", sync=sync_timer) as t:
-            batch = dp_encode_batch(ctx, sq, local_dps)
-        dt = time.perf_counter() - t.t0
-        for dp in local_dps:
-            timers.record(f"{dp.id}_DPencoding", dt)
-    else:
-        batch = {dp.id: dp_encode(ctx, sq, dp, sync_timer) for dp in local_dps}
+    abort = None
+    try:
+        if local_dps and batchable:
+            # every DP of this rank in one batch; each DP's encoding latency is the batch's
+            with timers.timed("DPencodingBatch", sync=sync_timer) as t:
+                batch = dp_encode_batch(ctx, sq, local_dps)
+            dt = time.perf_counter() - t.t0
+            for dp in local_dps:
+                timers.record(f"{dp.id}_DPencoding", dt)
+        else:
+            batch = {dp.id: dp_encode(ctx, sq, dp, sync_timer) for dp in local_dps}
+    except Exception as e:  # noqa: BLE001 -- a DP that cannot answer aborts the survey on every rank
+        abort = f"survey {sq.SurveyID}: a DP of rank {ctx.rank} failed to encode: {type(e).__name__}: {e}"
+        batch, local_dps = {}, []
+    want = expected_n_out(sq)
+    n_groups = len(all_possible_groups(sq.Query.DPDataGen.GroupByValues))
     for dp in local_dps:
         res = batch[dp.id]
         dp_results[dp.id] = res
         cn = cl.by_id(dp_to_cn[dp.id])
         items.append((cn.rank, dp.id, res["cv"]))
+        if want is not None and len(res["cv"]) != want * n_groups and abort is None:
+            # (raised on EVERY rank by the route's size round, not only here:
+            # ranks without DPs would otherwise wait in the CN collectives)
+            abort = (f"survey {sq.SurveyID}: DP {dp.id} encoded {len(res['cv']) // max(1, n_groups)} outputs, "
+                     f"the query announces {want}")
     with timers.timed("DataCollectionRoute"):
-        got = ec.route(ctx.comm, items, ctx.key_index)
+        got = ec.route(ctx.comm, items, ctx.key_index, abort=abort)
     cn_inputs, cn_sums = {}, {}
     for cn in cl.local(ctx.rank, "cn"):
         inputs = {si.id: got[si.id] for si in (sq.ServerToDP.get(cn.id) or []) if si.id in got}

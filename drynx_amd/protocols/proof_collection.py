@@ -252,7 +252,11 @@ def pool_verify_ranges(ctx, sq, reqs: list, vns: list, comm=None, arrived: float
             verdict[key] = all(gathered[j][0][vn.id].get(key, False) for j in range(W)
                                if (key, j) in trusted[vn.id])
         # slices whose helper digest did not match: this VN checks them itself
-        redo = trusted[vn.id].get("redo", {})
+        # (only lists this VN sampled: an unsampled one keeps None = code 2,
+        # whatever a helper reported for it)
+        redo = {j: [i for i in idxs if sampled[vn.id].get(reqs[i].base_key())]
+                for j, idxs in trusted[vn.id].get("redo", {}).items()}
+        redo = {j: idxs for j, idxs in redo.items() if idxs}
         if redo:
             with timers.span("rp.verify.pool_redo"):
                 c = ctx.vn_coins(vn.id)

@@ -332,10 +332,8 @@ class DrynxNode:
         # while the CN phases below proceed
         range_future = self._range_proofs_async(sq, dp_results) if q.Proofs else None
         want = dcp.expected_n_out(sq)
-        if dp_results:
+        if dp_results:  # (a width that does not fit ``want`` aborted the route on every rank)
             n_out = len(next(iter(dp_results.values()))["cv"]) // n_groups
-            if want is not None and n_out != want:
-                raise ValueError(f"survey {sq.SurveyID}: DPs encoded {n_out} outputs, the query announces {want}")
         if want is None:  # ranks without DPs learn the width from the others
             n_out = max(self.comm.all_gather_object(n_out if dp_results else 0)) or n_out
         else:

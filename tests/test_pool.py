@@ -24,7 +24,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, outdir, equivocate):
+def _worker(rank, world, port, outdir, equivocate, threshold=1.0):
     import torch.distributed as dist
 
     sys.path.insert(0, ROOT)
@@ -55,7 +55,8 @@ def _worker(rank, world, port, outdir, equivocate):
     before = comm.bytes_recv
     if rank == 0:
         client = DrynxClient(node)
-        sq = make_survey(client, cl, "frequencyCount", query_min=0, query_max=5, rows=8, proofs=1, ranges=[2, 4])
+        sq = make_survey(client, cl, "frequencyCount", query_min=0, query_max=5, rows=8, proofs=1, ranges=[2, 4],
+                         thresholds=[threshold, 1.0, 1.0, 0.0, 1.0])
         _, vals, res = client.send_survey_query(sq)
         out["codes"] = sorted(set(res.block.data_block().Proofs.values()))
         out["vals"] = [float(v) for v in vals[0]]
@@ -71,13 +72,17 @@ def _worker(rank, world, port, outdir, equivocate):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("equivocate", [False, True])
-def test_pool_slices_and_digests_world3(equivocate):
+@pytest.mark.parametrize("equivocate,threshold", [(False, 1.0), (True, 1.0), (True, 0.0)])
+def test_pool_slices_and_digests_world3(equivocate, threshold):
+    """threshold 0: the VN samples no list; a helper digest mismatch must not
+    turn those lists into code 0 (its re-check covers only sampled lists)."""
     outdir = tempfile.mkdtemp()
-    mp.spawn(_worker, args=(3, _free_port(), outdir, equivocate), nprocs=3, join=True)
+    mp.spawn(_worker, args=(3, _free_port(), outdir, equivocate, threshold), nprocs=3, join=True)
     outs = [json.load(open(os.path.join(outdir, f"p{r}.json"))) for r in range(3)]
     o0 = outs[0]
-    assert o0["codes"] == [1]  # every proof verified (the forged helper slices were re-checked by the VN)
+    # every proof verified (the forged helper slices were re-checked by the VN);
+    # with threshold 0 every proof is received, not checked (code 2)
+    assert o0["codes"] == ([1] if threshold == 1.0 else [2]), o0["codes"]
     clear = [0] * 6
     for o in outs:
         for v in o["clear_dp"].values():
