@@ -106,6 +106,10 @@ def parse():
     ap.add_argument("--fault-dp", type=int, default=None,
                     help="fault-injected run: DP k's range-proof payload is corrupted after proving and re-signed "
                          "(one false proof among all); the bench then checks that every VN blames exactly that DP")
+    ap.add_argument("--vn-mode", default=None, choices=["pool", "local", "own"],
+                    help="who checks each VN's range proofs at W > 1 (proof_collection.verification_mode): pool = "
+                         "every rank for every VN (single operator, the default), local = ranks assigned to that "
+                         "VN only (vn-local trust), own = the VN's own rank (default: DRYNX_VN_POOL, else pool)")
     ap.add_argument("--verification-sharding", type=int, default=0,
                     help="SurveyQuery.VerificationSharding: each proof verified by exactly k VNs (0: every VN)")
     ap.add_argument("--check-ledger", action="store_true",
@@ -223,10 +227,18 @@ def main():
     # ones without a CN or VN role: N=4 -> ranks 2, 3; N=8 -> ranks 6, 7)
     offsets = {"cn": 0, "vn": args.cns % world, "dp": (args.cns + args.vns) % world}
     cl, node = local_cluster(args.cns, n_dps, n_vns, comm=comm, device=device, workdir=workdir, offsets=offsets)
-    from drynx_amd.protocols.proof_collection import use_pool
+    if args.vn_mode:
+        node.pool_policy = args.vn_mode
+    from drynx_amd.protocols import proof_collection as pcp
 
-    pool_note = (f"pooled over {world} ranks (single operator; helper verdicts bound to slice digests)"
-                 if use_pool(node) and world > 1 else "each VN verifies on its own rank")
+    trust = pcp.trust_model(node)
+    mode = pcp.verification_mode(node)
+    pool_note = {"pool": f"pooled over {world} ranks for every VN (single operator; helper verdicts bound to "
+                         f"slice digests)",
+                 "local": "each VN's lists spread over its own rank + helper ranks serving only that VN "
+                          "(helper verdicts bound to slice digests)",
+                 "own": "each VN verifies its whole inbox on its own rank"}[mode] if world > 1 \
+        else "every VN verifies its whole inbox with its own coins (co-hosted on one GPU)"
     if args.fault_dp is not None:
         from drynx_amd.utils.faults import FaultPlan
 
@@ -381,7 +393,9 @@ def main():
                                  if args.verification_sharding else "every VN verifies every proof (threshold 1.0)"),
                 "range_proof": {"u": args.u, "l": args.l, "servers": args.cns, "proofs_per_query": proofs_per_step,
                                 "verifications_per_query": verifs_per_step},
-                "vn_independent": True,
+                "vn_independent": trust == "vn-local",
+                "trust_model": trust,
+                "verification_mode": mode,
                 "vn_pool": pool_note,
             },
             "e2e_latency_s": round(ms / 1000.0, 4),

@@ -34,12 +34,31 @@ import sqlite3
 import struct
 import threading
 
-from ..utils import timers
+from ..utils import streams, timers
 
 
 BLOB_MIN = 1 << 16
 _REF = b"\x00DXBLOB1"
-_REF2 = b"\x00DXBLOB2"  # + offset, length (u64) + path of a shared BlobSegment
+_REF2 = b"\x00DXBLOB2"  # + offset, length (u64) + path of a shared BlobSegment (raw bytes)
+_REF3 = b"\x00DXBLOB3"  # the same, holding a compact range payload (proofs/ledger_codec.py)
+_REF4 = b"\x00DXBLOB4"  # + path of a node-shared payload file (its own tag word says raw / compact)
+_NODE_RAW, _NODE_COMPACT = b"DXNODER1", b"DXNODEC1"  # first bytes of a node-shared payload file
+
+
+class Compact:
+    """A produced ledger value in the compact range-payload form: the writer
+    tags it explicitly (``_REF3`` / the node file's tag), and only tagged
+    values are decompressed when read -- nothing is recognised by sniffing."""
+
+    def __init__(self, buf):
+        self.buf = buf
+
+
+def _unwrap(d) -> tuple:
+    """(bytes view, compact flag) of a produced value."""
+    if isinstance(d, Compact):
+        return memoryview(d.buf).cast("B"), True
+    return memoryview(d).cast("B"), False
 
 
 def _addr(mv: memoryview) -> int:
@@ -161,13 +180,11 @@ class BlobSegment:
     proofs stay in the database)."""
 
     def __init__(self, path: str, device=None):
-        import concurrent.futures as cf
-
         self.base = self.path = path
         self._gens: list = [path]  # generation files, oldest first
         os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
         self._f = open(path, "ab")
-        self._ex = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="drynx-ledger")
+        self._ex = streams.executor(device, 1, "drynx-ledger")
         self._done: dict = {}
         self._lock = threading.Lock()
         self._device = device
@@ -217,14 +234,15 @@ class BlobSegment:
             with timers.span("ledger.encode"):
                 data = produce()
         with timers.span("ledger.write"):
-            bufs = [memoryview(d).cast("B") for d in (data if many else [data])]
+            pairs = [_unwrap(d) for d in (data if many else [data])]
+            bufs, flags = [b for b, _ in pairs], [f for _, f in pairs]
             timers.count("ledger.blob_bytes", sum(b.nbytes for b in bufs))
             self._make_room(sum(b.nbytes for b in bufs) * _copies())
             self._f.flush()
             off = self._f.seek(0, os.SEEK_END)
             out, pos = [], off
-            for b in bufs:
-                out.append((pos, b.nbytes, self.path))  # the generation file it lands in
+            for b, fl in zip(bufs, flags):
+                out.append((pos, b.nbytes, self.path, fl))  # the generation file it lands in
                 pos += b.nbytes
             self._pwrite_all(bufs, off)
             self._f.seek(0, os.SEEK_END)
@@ -310,9 +328,7 @@ class BlobSegment:
                 put(it)
             return
         if not hasattr(self, "_wpool"):
-            import concurrent.futures as cf
-
-            self._wpool = cf.ThreadPoolExecutor(max_workers=4, thread_name_prefix="drynx-ledger-w")
+            self._wpool = streams.executor(self._device, 4, "drynx-ledger-w")
         list(self._wpool.map(put, pieces))
 
     def flush(self):
@@ -362,9 +378,12 @@ class NodeBlobs(BlobSegment):
 
     def __init__(self, root: str, device=None):
         os.makedirs(root, exist_ok=True)
-        super().__init__(os.path.join(root, f"_rank_{os.getpid()}.unused"), device)
+        super().__init__(os.path.join(root, f"_rank_{os.getpid()}_{id(self):x}.unused"), device)
         self.root = root
         self._files: list = []  # this rank's payload files, oldest first
+        # this user's open marker: the directory goes only with its last user
+        self._open_mark = os.path.join(root, f"_open_{os.getpid()}_{id(self):x}")
+        open(self._open_mark, "w").close()
 
     def file_of(self, blob_id: str) -> str:
         return os.path.join(self.root, f"{blob_id}.blob")
@@ -381,12 +400,14 @@ class NodeBlobs(BlobSegment):
                 out.append(False)
         return out
 
-    def put_refs(self, blob_ids: list, sizes: list) -> list:
-        """References to payloads another rank of the node claimed and writes."""
+    def put_refs(self, blob_ids: list, sizes: list | None = None) -> list:
+        """References to payloads another rank of the node claimed and writes
+        (the whole file: its length and form are the writer's, which may store
+        the smaller compact image; ``sizes`` is not needed)."""
         refs = []
         with self._lock:
-            for bid, n in zip(blob_ids, sizes):
-                fut = self._done.setdefault(bid, _Done((0, int(n), self.file_of(bid))))
+            for bid in blob_ids:
+                fut = self._done.setdefault(bid, _Done((0, 0, self.file_of(bid), None)))
                 refs.append(BlobRef(self, fut))
         return refs
 
@@ -420,7 +441,7 @@ class NodeBlobs(BlobSegment):
         with timers.span("ledger.write"):
             reserve = _gb_env("DRYNX_LEDGER_RESERVE_GB", 8)
             for bid, d in zip(blob_ids, data):
-                b = memoryview(d).cast("B")
+                b, compact = _unwrap(d)
                 timers.count("ledger.blob_bytes", b.nbytes)
                 if _budget():
                     while shutil.disk_usage(self.root).free - b.nbytes < reserve and self._files:
@@ -433,22 +454,39 @@ class NodeBlobs(BlobSegment):
                         BlobSegment.pruned += 1
                 final = self.file_of(bid)
                 tmp = final + ".tmp"
-                self._pwrite_all([b], 0, tmp)
+                self._pwrite_all([memoryview(_NODE_COMPACT if compact else _NODE_RAW), b], 0, tmp)
                 fd = self._pfds.pop(tmp)
                 with timers.span("ledger.sync"):
                     os.fdatasync(fd)
                 os.close(fd)
                 os.replace(tmp, final)
                 self._files.append(final)
-                out.append((0, b.nbytes, final))
+                out.append((0, 0, final, compact))
             if blob_ids:
                 _fsync_dir(self.root)
         return out
 
     def close(self, remove: bool = False):
+        """``remove``: this rank's files go; the node directory goes only with
+        its last open user (other VN ranks may still write or read there)."""
         super().close(remove)
+        try:
+            os.remove(self._open_mark)
+        except FileNotFoundError:
+            pass
         if remove:
-            __import__("shutil").rmtree(self.root, ignore_errors=True)
+            for p in self._files:
+                for q in (p, p + ".claim"):
+                    try:
+                        os.remove(q)
+                    except FileNotFoundError:
+                        pass
+            try:
+                users = [n for n in os.listdir(self.root) if n.startswith("_open_")]
+            except FileNotFoundError:
+                return
+            if not users:
+                __import__("shutil").rmtree(self.root, ignore_errors=True)
 
 
 class Store:
@@ -472,8 +510,12 @@ class Store:
         """Caller holds the lock.  Large values are written straight from the
         host buffer (no bytes() copy under the GIL)."""
         if isinstance(value, BlobRef):
-            off, n, path = value.result()
-            return _REF2 + struct.pack("<QQ", off, n) + path.encode()
+            res = value.result()
+            if isinstance(value.segment, NodeBlobs):
+                return _REF4 + res[2].encode()
+            off, n, path = res[:3]
+            compact = len(res) > 3 and bool(res[3])
+            return (_REF3 if compact else _REF2) + struct.pack("<QQ", off, n) + path.encode()
         if hasattr(value, "cpu") and hasattr(value, "numpy"):
             buf = memoryview(value.detach().cpu().contiguous().numpy()).cast("B")
         else:
@@ -487,35 +529,53 @@ class Store:
         return _REF + struct.pack("<QQ", off, buf.nbytes)
 
     def _decode(self, v) -> bytes:
-        v = self._decode_raw(v)
-        from ..proofs import ledger_codec
+        """The stored value; a payload the writer TAGGED compact (``_REF3``,
+        or a node file's compact tag) is rebuilt into the signed bytes."""
+        v = bytes(v)
+        compact = False
+        if v.startswith(_REF4):
+            raw = self._read_shared(v[len(_REF4):].decode(), 0, 0)
+            tag, v = raw[:8], raw[8:]
+            if tag not in (_NODE_RAW, _NODE_COMPACT):
+                raise ValueError("ledger: node-shared payload file without its tag")
+            compact = tag == _NODE_COMPACT
+        elif v.startswith(_REF3) or v.startswith(_REF2):
+            off, n = struct.unpack("<QQ", v[len(_REF2): len(_REF2) + 16])
+            compact = v.startswith(_REF3)
+            v = self._read_shared(v[len(_REF2) + 16:].decode(), off, n)
+        else:
+            v = self._decode_raw(v)
+        if compact:
+            from ..proofs import ledger_codec
 
-        # range payloads stored in their compact form: the signed bytes again
-        return ledger_codec.decompress_bytes(v) if ledger_codec.is_compressed(v) else v
+            return ledger_codec.decompress_bytes(v)
+        return v
+
+    @staticmethod
+    def _read_shared(path: str, off: int, n: int) -> bytes:
+        """``n`` bytes at ``off`` of a file another thread or rank writes
+        (n = 0: all of it), waiting for a node-shared file not written yet."""
+        import time as _t
+
+        deadline = _t.monotonic() + float(os.environ.get("DRYNX_LEDGER_WAIT_S", "60"))
+        while True:
+            try:
+                with open(path, "rb") as f:
+                    f.seek(off)
+                    return f.read(n) if n else f.read()
+            except FileNotFoundError:
+                # a node-shared payload not yet written by the node's writer
+                # rank: wait for it, unless the writer pruned it
+                if _was_pruned(path):
+                    raise PrunedError(f"ledger value pruned for disk space ({path}; "
+                                      f"DRYNX_LEDGER_RETAIN=budget)") from None
+                if _t.monotonic() < deadline:
+                    _t.sleep(0.01)
+                    continue
+                raise FileNotFoundError(f"ledger value {path} was never written") from None
 
     def _decode_raw(self, v) -> bytes:
         v = bytes(v)
-        if v.startswith(_REF2):
-            off, n = struct.unpack("<QQ", v[len(_REF2): len(_REF2) + 16])
-            path = v[len(_REF2) + 16:].decode()
-            import time as _t
-
-            deadline = _t.monotonic() + float(os.environ.get("DRYNX_LEDGER_WAIT_S", "60"))
-            while True:
-                try:
-                    with open(path, "rb") as f:
-                        f.seek(off)
-                        return f.read(n)
-                except FileNotFoundError:
-                    # a node-shared payload not yet written by the node's writer
-                    # rank: wait for it, unless the writer pruned it
-                    if _was_pruned(path):
-                        raise PrunedError(f"ledger value pruned for disk space ({path}; "
-                                          f"DRYNX_LEDGER_RETAIN=budget)") from None
-                    if _t.monotonic() < deadline:
-                        _t.sleep(0.01)
-                        continue
-                    raise FileNotFoundError(f"ledger value {path} was never written") from None
         if len(v) == len(_REF) + 16 and v.startswith(_REF):
             off, n = struct.unpack("<QQ", v[len(_REF):])
             if self._blob_f is not None:

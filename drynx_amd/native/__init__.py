@@ -216,8 +216,16 @@ def _ctx(*ts):
         if t is not None and t.device != dev:
             raise ValueError(f"native op mixes devices {dev} and {t.device}")
     if dev is not None and dev.type == "cuda":
+        if _CHECK_DEVICE and torch.cuda.current_device() != dev.index:
+            # DRYNX_CHECK_DEVICE=1 (the GPU suite): a thread launching on a GPU
+            # that is not its current device was never pinned to the rank's
+            raise AssertionError(f"native op on {dev} from a thread whose current device is "
+                                 f"cuda:{torch.cuda.current_device()}")
         return 1, ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
     return 0, None
+
+
+_CHECK_DEVICE = os.environ.get("DRYNX_CHECK_DEVICE", "0") == "1"
 
 
 def _raw_call(name, *args) -> int:

@@ -650,16 +650,24 @@ def sampled_bounds(sq, n: int, part=None) -> tuple:
 _POOL_DP_W, _POOL_VN_W = 0.0, 0.14
 
 
+def rank_weights(dps: list, vns: list) -> list:
+    """Each rank's share weight for the pooled checks: 1 - _POOL_DP_W (per
+    extra DP) - _POOL_VN_W (per VN) (floor 0.25); all 1 under
+    DRYNX_POOL_BALANCE=0."""
+    if os.environ.get("DRYNX_POOL_BALANCE", "1") == "0":
+        return [1.0] * len(dps)
+    lo = min(dps)
+    return [max(0.25, 1.0 - _POOL_DP_W * (dps[k] - lo) - _POOL_VN_W * vns[k]) for k in range(len(dps))]
+
+
 def balanced_parts(W: int, dps: list, vns: list) -> list:
-    """Pool parts for W ranks weighted so every rank's check ends together:
-    rank k's slice weight 1 - _POOL_DP_W (per extra DP) - _POOL_VN_W (per VN)
-    (floor 0.25), as (k, W, cumulative weights) tuples (``sampled_bounds``).
-    Calibrated from one-GPU measurements of each rank's share
-    (tools/rank_share.py)."""
+    """Pool parts for W ranks weighted so every rank's check ends together
+    (``rank_weights``), as (k, W, cumulative weights) tuples
+    (``sampled_bounds``).  Calibrated from one-GPU measurements of each
+    rank's share (tools/rank_share.py)."""
     if W <= 1 or os.environ.get("DRYNX_POOL_BALANCE", "1") == "0":
         return [(k, W) for k in range(W)]
-    lo = min(dps)
-    w = [max(0.25, 1.0 - _POOL_DP_W * (dps[k] - lo) - _POOL_VN_W * vns[k]) for k in range(W)]
+    w = rank_weights(dps, vns)
     iw = [max(1, int(round(1000 * x))) for x in w]
     cum = [0]
     for x in iw:
@@ -1056,8 +1064,8 @@ def verify_requests(reqs: list, sq, vn_id: str, vn_index: int, n_vns: int, devic
         # the range lists (the heavy pairing work) verify on a worker thread with
         # their own HIP stream while this thread checks the short per-CN proofs
         idxs = todo.pop("range")
-        range_future = _side_pool().submit(_verify_range_side, reqs, idxs, sq, vn_id, device, cache,
-                                           torch.cuda.current_stream(torch.device(device)), coins)
+        range_future = _side_pool(device).submit(_verify_range_side, reqs, idxs, sq, vn_id, device, cache,
+                                                 torch.cuda.current_stream(torch.device(device)), coins)
     _prefetch_packed(reqs, [i for k in PACKED_KINDS for i in todo.get(k, [])], device)
     pre = cache.ks_pre.pop((sq.SurveyID, vn_id), None)
     if pre is not None and "keyswitch" in todo and all(i in pre for i in todo["keyswitch"]):
@@ -1139,17 +1147,18 @@ def verify_requests(reqs: list, sq, vn_id: str, vn_index: int, n_vns: int, devic
     return resolve if defer else resolve()
 
 
-_pool = None
+_pools: dict = {}
 _streams: dict = {}
 
 
-def _side_pool():
-    global _pool
-    if _pool is None:
-        import concurrent.futures as cf
+def _side_pool(device):
+    """The VN range side worker of ``device`` (pinned to it)."""
+    from ..utils import streams
 
-        _pool = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="drynx-vn-range")
-    return _pool
+    key = str(torch.device(device))
+    if key not in _pools:
+        _pools[key] = streams.executor(device, 1, "drynx-vn-range")
+    return _pools[key]
 
 
 def _verify_range_side(reqs, idxs, sq, vn_id, device, cache, main, coins=None) -> list:

@@ -66,56 +66,119 @@ def _net_proofs(ctx, sq, reqs: list, vns: list):
                  hops=flow_hops("proofs_to_vns"))
 
 
-def pool_parts(ctx, sq) -> list:
-    """Every rank's pool part for this survey (``prq.balanced_parts``): ranks
-    hosting more DPs or a VN check shorter slices; identical on every rank
-    (a function of the placement only)."""
+def verification_mode(ctx) -> str:
+    """Who checks a VN's range proofs (``ctx.pool_policy``, else DRYNX_VN_POOL):
+
+    * ``pool`` ("1", default; single-operator deployments): every rank checks
+      a slice of every range list on behalf of EVERY VN, with that VN's coins
+      (a per-survey seed the VN hands out), so three VNs keep eight GPUs busy;
+      the VN's own rank keeps the signature checks, the sampling decisions,
+      the bitmap and the ledger, and accepts a helper's slice verdict only if
+      the helper's digest of the slice it checked equals the VN's own digest
+      of that slice of its signed payload.
+    * ``local`` ("vn-local"): the same, but each VN's lists are spread only
+      over the ranks assigned to THAT VN (its own rank plus helper ranks no
+      other VN uses): no VN's verdict depends on another VN's ranks or
+      helpers, and a helper learns only its own VN's seed.
+    * ``own`` ("0"; forced by multi-party servers, services/server.py): each
+      VN checks its whole inbox on its own rank (the reference: every VN
+      verifies what it received, lib/proof/structs_proofs.go:135-182).
+
+    Every mode runs as the range plane beside the CN phases; on one GPU the
+    co-hosted VNs' batches share the decode and run back to back."""
+    pol = getattr(ctx, "pool_policy", None)
+    if pol is None:
+        pol = os.environ.get("DRYNX_VN_POOL", "1")
+    return {"0": "own", "own": "own", "local": "local", "vn-local": "local"}.get(str(pol), "pool")
+
+
+def trust_model(ctx) -> str:
+    """What a VN's range verdict depends on, as run: ``single-operator-pool``
+    (helper ranks that serve every VN) or ``vn-local`` (only ranks assigned
+    to that VN; at one rank, or with ``own``, its own rank)."""
+    return "single-operator-pool" if verification_mode(ctx) == "pool" and ctx.comm.world > 1 else "vn-local"
+
+
+def _placement(ctx, sq) -> tuple:
+    """(DPs per rank, VNs per rank, VN ranks in roster order) of a survey."""
     W = ctx.comm.world
     dps, vns = [0] * W, [0] * W
     for _, members in (sq.ServerToDP or {}).items():
         for si in members or []:
             dps[ctx.cluster.by_id(si.id).rank] += 1
-    for si in sq.Query.RosterVNs.list:
-        vns[ctx.cluster.by_id(si.id).rank] += 1
-    return prq.balanced_parts(W, dps, vns)
+    vn_ranks = [ctx.cluster.by_id(si.id).rank for si in sq.Query.RosterVNs.list]
+    for r in vn_ranks:
+        vns[r] += 1
+    return dps, vns, vn_ranks
 
 
-def use_pool(ctx) -> bool:
-    """Pooled range verification (single-operator deployments only): every
-    rank checks a 1/world slice of every range-proof list on behalf of every
-    VN, with THAT VN's coins (a per-survey seed the VN hands out), so three
-    VNs keep eight GPUs busy; the VN's own rank keeps the signature checks,
-    the sampling decisions, the bitmap and the ledger, and accepts a helper's
-    slice verdict only if the helper's digest of the slice it checked equals
-    the VN's own digest of that slice of its signed payload.  On one GPU the
-    co-hosted VNs' batches share the decode and run back to back.
-    ``ctx.pool_policy`` (or DRYNX_VN_POOL) "0" leaves each VN's range checks
-    to the VN's own rank; a multi-party deployment (services/server.py)
-    forces that."""
-    pol = getattr(ctx, "pool_policy", None)
-    if pol is None:
-        pol = os.environ.get("DRYNX_VN_POOL", "1")
-    return str(pol) != "0"
+def verification_groups(mode: str, W: int, dps: list, vns: list, vn_ranks: list) -> tuple:
+    """-> (groups, parts): ``groups[v]`` the ranks that check VN v's range
+    lists (v's own rank first), ``parts[v][rank]`` that rank's slice of each
+    list (``prq.sampled_bounds`` part: weighted by ``prq.balanced_parts``
+    rules, a rank hosting more DPs or a VN checks a shorter slice).  A
+    function of the placement only: identical on every rank.  ``local``:
+    every rank hosting no VN serves one VN, the one whose group has the least
+    capacity so far (its ranks' weights; a rank hosting k VNs counts 1/k)."""
+    n = len(vn_ranks)
+    if W <= 1 or mode == "own":
+        return [[r] for r in vn_ranks], [{r: (0, 1)} for r in vn_ranks]
+    if mode == "pool":
+        bp = prq.balanced_parts(W, dps, vns)
+        return [list(range(W)) for _ in range(n)], [{k: bp[k] for k in range(W)} for _ in range(n)]
+    w = prq.rank_weights(dps, vns)
+    groups = [[r] for r in vn_ranks]
+    cap = [w[r] / max(1, vns[r]) for r in vn_ranks]
+    for h in (k for k in range(W) if vns[k] == 0):
+        v = min(range(n), key=lambda i: (cap[i], i))
+        groups[v].append(h)
+        cap[v] += w[h]
+    parts = []
+    for g in groups:
+        iw = [max(1, int(round(1000 * w[k]))) for k in g]
+        cum = [0]
+        for x in iw:
+            cum.append(cum[-1] + x)
+        parts.append({k: (i, len(g), *cum) if len(g) > 1 else (0, 1) for i, k in enumerate(g)})
+    return groups, parts
+
+
+def groups_of(ctx, sq) -> tuple:
+    """``verification_groups`` of this node's mode for a survey -> (groups, parts)
+    as dicts keyed by VN id."""
+    dps, vns, vn_ranks = _placement(ctx, sq)
+    groups, parts = verification_groups(verification_mode(ctx), ctx.comm.world, dps, vns, vn_ranks)
+    ids = [si.id for si in sq.Query.RosterVNs.list]
+    return dict(zip(ids, groups)), dict(zip(ids, parts))
 
 
 def fan_out(ctx, sq, local_requests: list, pool: bool = False) -> list:
-    """Every request to the ranks that host a VN; with ``pool``, the other
-    ranks get only THEIR slice of every range bundle (what they check for
-    the pool, ~1/W of the payload) plus the envelope header.  Payload
-    tensors (range bundles, packed per-CN proofs) travel as raw limbs in one
-    all-to-all with sizes announced by the control message (no size round);
-    envelopes and byte payloads ride on the control message."""
+    """Every request to the ranks that host a VN; with ``pool`` (the range
+    plane: ``verification_groups``), a helper rank gets only ITS slice of
+    every range bundle its VN(s) may check (~1/group of the payload) plus the
+    envelope header, and each local VN's per-survey seed goes to exactly the
+    ranks of that VN's group.  Payload tensors (range bundles, packed per-CN
+    proofs) travel as raw limbs in one all-to-all with sizes announced by the
+    control message (no size round); envelopes and byte payloads ride on the
+    control message."""
     vns = [ctx.cluster.by_id(si.id) for si in sq.Query.RosterVNs.list]
     W = ctx.comm.world
     vn_ranks = sorted({v.rank for v in vns})
-    dests = list(range(W)) if pool else vn_ranks
+    mode = verification_mode(ctx)
+    groups, gparts = groups_of(ctx, sq) if pool else ({}, {})
+    helpers: dict = {}  # helper rank (hosting no VN) -> (its slice part, indices of the VNs it serves)
+    for vi, v in enumerate(vns):
+        for k in groups.get(v.id, ()):
+            if k not in vn_ranks:
+                helpers.setdefault(k, (gparts[v.id][k], []))[1].append(vi)
+    dests = sorted(set(vn_ranks) | set(helpers))
     seeds = {}
     if pool:
-        # each local VN's per-survey seed for its pool helpers rides on this
+        # each local VN's per-survey seed for its group's helpers rides on this
         # exchange (no control round of its own): helper k derives that VN's
         # coins for its slice from it
         seeds = {vn.id: ctx.vn_coins(vn.id).seed() for vn in vns if vn.rank == ctx.rank}
-        ctx.__dict__.setdefault("_pool_seeds", {})[sq.SurveyID] = seeds
+        ctx.__dict__.setdefault("_pool_seeds", {})[sq.SurveyID] = dict(seeds)
         if len(ctx._pool_seeds) > 64:
             ctx._pool_seeds.pop(next(iter(ctx._pool_seeds)))
     if W == 1:
@@ -123,21 +186,24 @@ def fan_out(ctx, sq, local_requests: list, pool: bool = False) -> list:
     per_rank = {d: [] for d in dests}
     per_rank_t = {d: [] for d in dests}
     packed = {}
-    parts = pool_parts(ctx, sq) if pool else None
     for idx, r in enumerate(local_requests):
         assigned = prq.assigned_vns(sq, r, len(vns))
-        full_ranks = set(vn_ranks) if (assigned is None or pool) else {vns[i].rank for i in assigned}
+        # in the pool every VN rank checks a slice for every VN: all get the payload
+        full_ranks = set(vn_ranks) if (assigned is None or (pool and mode == "pool")) \
+            else {vns[i].rank for i in assigned}
         for d in dests:
             if d == ctx.rank:
                 continue
             if d not in full_ranks:
-                if pool and r.kind == "range" and r.obj is not None and d not in vn_ranks:
-                    # a helper: its slice of the bundle (the pool's part d of W)
-                    sl = _helper_slice(r.obj, sq, parts[d])
+                serves = helpers.get(d)
+                if (serves is not None and r.kind == "range" and r.obj is not None
+                        and (assigned is None or any(vi in assigned for vi in serves[1]))):
+                    # a helper: its slice of the bundle (its part of its group)
+                    sl = _helper_slice(r.obj, sq, serves[0])
                     w = r.header().to_wire()
                     if sl:
                         t = prq.range_bundle_pack(sl).to(ctx.device)
-                        w["tensor"], w["slice"] = t.numel(), list(parts[d])
+                        w["tensor"], w["slice"] = t.numel(), list(serves[0])
                         per_rank_t[d].append(t)
                     per_rank[d].append(w)
                 else:
@@ -151,13 +217,16 @@ def fan_out(ctx, sq, local_requests: list, pool: bool = False) -> list:
                 per_rank_t[d].append(packed[idx])
             else:
                 per_rank[d].append(r.to_wire())
-    got = ctx.comm.exchange_bytes({d: obj_to_bytes({"w": per_rank[d], "seeds": seeds})
+    # a VN's seed only to the ranks of its group (a vn-local helper never
+    # learns another VN's coins)
+    got = ctx.comm.exchange_bytes({d: obj_to_bytes({"w": per_rank[d],
+                                                    "seeds": {v: s for v, s in seeds.items() if d in groups[v]}})
                                    for d in dests if d != ctx.rank})
     msgs = {src: bytes_to_obj(b) for src, b in got.items()}
     wires = {src: m["w"] for src, m in msgs.items()}
     if pool:
         for m in msgs.values():
-            seeds.update(m["seeds"])
+            ctx._pool_seeds[sq.SurveyID].update(m["seeds"])
     tens = {d: t for d, t in zip([d for d in dests if per_rank_t[d]],
                                   nt.cat_rows([per_rank_t[d] for d in dests if per_rank_t[d]]))}
     # the envelopes announced every tensor's size: no size round for the payloads
@@ -190,28 +259,35 @@ def _helper_slice(lists, sq, part) -> list:
     return prq.slice_lists(lists, sq, part)
 
 
+def _pkey(part) -> str:
+    return ",".join(str(int(x)) for x in part)
+
+
 def pool_verify_ranges(ctx, sq, reqs: list, vns: list, comm=None, arrived: float | None = None) -> dict:
-    """Pooled range verification (see ``use_pool``).  Each VN's rank decides
-    that VN's sampling (reference ``rand.Float64() <= Threshold``, from the
-    VN's own coins, or the sharding extension) and draws a per-survey seed;
-    rank k checks slice k/W of the sampled prefix of every list for every VN
-    with coins derived from that VN's seed, and reports its verdicts with
-    the digest of each slice it checked.  Each VN's rank then accepts a
-    helper's slice verdict only when the digest matches its own digest of
-    that slice of the signed payload, and re-checks any other slice itself.
-    ``<vn>_VerifyRange`` (structs_proofs.go:137) runs from ``arrived`` (the
-    VN's inbox: the range fan-out's end on its rank) to that VN's own verdict
-    (after its digest checks and any slice it re-checked).
-    -> {vn_id: {base_key: None (not sampled) | bool}} on every rank."""
+    """Range verification through the verification groups (see
+    ``verification_mode``).  Each VN's rank decides that VN's sampling
+    (reference ``rand.Float64() <= Threshold``, from the VN's own coins, or
+    the sharding extension) and draws a per-survey seed; every rank of VN v's
+    group checks its slice of the sampled prefix of every list with coins
+    derived from v's seed and reports its verdicts with the digest of each
+    slice it checked.  v's rank then accepts a helper's slice verdict only
+    when the digest matches its own digest of that slice of the signed
+    payload, and re-checks any other slice itself.  Groups of one (``own``)
+    need no gather.  ``<vn>_VerifyRange`` (structs_proofs.go:137) runs from
+    ``arrived`` (the VN's inbox: the range fan-out's end on its rank) to that
+    VN's own verdict (after its digest checks and any slice it re-checked).
+    -> {vn_id: {base_key: None (not sampled) | bool}} for the VNs of this rank."""
     comm = comm or ctx.comm
     W, k = comm.world, comm.rank
     rng = [i for i, r in enumerate(reqs) if r.kind == "range" and not r.header_only]
+    groups, gparts = groups_of(ctx, sq)
     # every VN's seed arrived with the fan-out; the helpers check every list a
     # VN may sample (the sharding extension's assignment is public; a random
     # Threshold sample stays the VN's own decision, applied to the verdicts
     # below) -- no control round before the checks
     seeds = getattr(ctx, "_pool_seeds", {}).pop(sq.SurveyID, {})
-    missing = [vn.id for vn in vns if vn.id not in seeds]
+    serve = [vn for vn in vns if k in groups[vn.id]]  # the VNs this rank checks a slice for
+    missing = [vn.id for vn in serve if vn.id not in seeds]
     if missing:
         raise RuntimeError(f"pool: no fan-out seed for {missing} (survey {sq.SurveyID})")
 
@@ -221,48 +297,58 @@ def pool_verify_ranges(ctx, sq, reqs: list, vns: list, comm=None, arrived: float
     vn_idxs = {vn.id: [i for i in rng if may_check(i, vi)] for vi, vn in enumerate(vns)}
     sampled = {vn.id: {reqs[i].base_key(): prq.should_verify(sq, reqs[i], vi, len(vns), ctx.vn_coins(vn.id))
                        for i in rng} for vi, vn in enumerate(vns) if vn.rank == ctx.rank}
-    part_coins = {vn.id: Coins(seeds[vn.id]).derive(("slice", k, W)) for vn in vns}
-    parts = pool_parts(ctx, sq)
     t0 = arrived if arrived is not None else time.perf_counter()
     local_vns = [vn for vn in vns if vn.rank == ctx.rank]
-    # a VN rank's digests of the other ranks' slices of its own payloads run
-    # beside this rank's pool part (their own thread and stream: the part's
-    # latency-bound kernels leave the GPU room), not after the gather
-    exp_f = _expected_async(ctx, sq, reqs, vn_idxs, local_vns, W, parts) \
-        if local_vns and W > 1 else None
-    res, digests = prq.verify_range_pool_part(reqs, vn_idxs, sq, ctx.device, ctx.verifier_cache, parts[k],
-                                              part_coins, async_digests=True)
-    if hasattr(digests, "result"):
-        digests = digests.result()
-    mine = {vn.id: {reqs[i].base_key(): bool(ok) for i, ok in res.get(vn.id, {}).items()} for vn in vns}
-    mydig = {reqs[i].base_key(): d for i, d in digests.items()}
-    gathered = comm.all_gather_object((mine, mydig))
+    helped = [vn for vn in local_vns if len(groups[vn.id]) > 1]
+    # a VN rank's digests of its helpers' slices of its own payloads run beside
+    # this rank's part (their own thread and stream: the part's latency-bound
+    # kernels leave the GPU room), not after the gather
+    exp_f = _expected_async(ctx, sq, reqs, vn_idxs, helped, groups, gparts) if helped else None
+    # this rank's parts: the VNs it serves grouped by the slice it checks for them
+    by_part: dict = {}
+    for vn in serve:
+        by_part.setdefault(tuple(gparts[vn.id][k]), []).append(vn)
+    mine, mydig, futs = {}, {}, []
+    for part, pvns in by_part.items():
+        coins = {vn.id: Coins(seeds[vn.id]).derive(("slice", k, W)) for vn in pvns}
+        res, digests = prq.verify_range_pool_part(reqs, {vn.id: vn_idxs[vn.id] for vn in pvns}, sq, ctx.device,
+                                                  ctx.verifier_cache, part, coins, async_digests=True)
+        for vn in pvns:
+            mine[vn.id] = {reqs[i].base_key(): bool(ok) for i, ok in res.get(vn.id, {}).items()}
+        futs.append((part, digests))
+    for part, digests in futs:
+        if hasattr(digests, "result"):
+            digests = digests.result()
+        mydig[_pkey(part)] = {reqs[i].base_key(): d for i, d in digests.items()}
+    if any(len(g) > 1 for g in groups.values()):
+        gathered = comm.all_gather_object((mine, mydig))
+    else:  # every VN checks alone on its own rank: nothing to gather
+        gathered = {k: (mine, mydig)}
     out = {}
-    if local_vns:
-        trusted = _check_helper_digests(ctx, sq, reqs, vn_idxs, local_vns, gathered, W,
-                                        exp_f.result() if exp_f is not None else None, parts)
-    for vn in vns:
-        if vn.rank != ctx.rank:
-            continue
+    if helped:
+        trusted = _check_helper_digests(ctx, sq, reqs, vn_idxs, helped, gathered, groups, gparts, exp_f.result())
+    for vn in local_vns:
+        g = groups[vn.id]
+        tr = trusted[vn.id] if len(g) > 1 else {}
         verdict = {}
         for key, smp in sampled[vn.id].items():
             if not smp:
                 verdict[key] = None
                 continue
-            verdict[key] = all(gathered[j][0][vn.id].get(key, False) for j in range(W)
-                               if (key, j) in trusted[vn.id])
+            verdict[key] = all(gathered[j][0][vn.id].get(key, False) for j in g
+                               if j == k or (key, j) in tr)
         # slices whose helper digest did not match: this VN checks them itself
         # (only lists this VN sampled: an unsampled one keeps None = code 2,
         # whatever a helper reported for it)
         redo = {j: [i for i in idxs if sampled[vn.id].get(reqs[i].base_key())]
-                for j, idxs in trusted[vn.id].get("redo", {}).items()}
+                for j, idxs in tr.get("redo", {}).items()}
         redo = {j: idxs for j, idxs in redo.items() if idxs}
         if redo:
             with timers.span("rp.verify.pool_redo"):
                 c = ctx.vn_coins(vn.id)
                 for j, idxs in redo.items():
                     r2, _ = prq.verify_range_pool_part(reqs, {vn.id: idxs}, sq, ctx.device, ctx.verifier_cache,
-                                                       parts[j], {vn.id: c})
+                                                       gparts[vn.id][j], {vn.id: c})
                     for i, ok in r2[vn.id].items():
                         key = reqs[i].base_key()
                         verdict[key] = bool(verdict.get(key)) and bool(ok)
@@ -271,15 +357,17 @@ def pool_verify_ranges(ctx, sq, reqs: list, vns: list, comm=None, arrived: float
     return out
 
 
-def _expected_async(ctx, sq, reqs, vn_idxs: dict, local_vns: list, W: int, parts: list):
+def _expected_async(ctx, sq, reqs, vn_idxs: dict, local_vns: list, groups: dict, gparts: dict):
     """``_expected_digests`` as an idle task of this rank's pool part (run
     while its verifier waits for the device, on a HIP stream of its own
     ordered after the caller's, where the payloads were received): no second
     thread contending for the GIL with the part's host work."""
     from ..proofs import range_proof as rp
 
+    def work():
+        return _expected_digests(ctx, sq, reqs, vn_idxs, local_vns, groups, gparts)
     if ctx.device.type != "cuda":
-        return rp.add_idle_task(rp.Deferred(lambda: _expected_digests(ctx, sq, reqs, vn_idxs, local_vns, W, parts)))
+        return rp.add_idle_task(rp.Deferred(work))
     if not hasattr(ctx, "_dig_stream"):
         ctx._dig_stream = torch.cuda.Stream(ctx.device)
     st, cur = ctx._dig_stream, torch.cuda.current_stream(ctx.device)
@@ -287,54 +375,62 @@ def _expected_async(ctx, sq, reqs, vn_idxs: dict, local_vns: list, W: int, parts
 
     def run():
         with torch.cuda.stream(st):
-            return _expected_digests(ctx, sq, reqs, vn_idxs, local_vns, W, parts)
+            return work()
     return rp.add_idle_task(rp.Deferred(run))
 
 
-def _expected_digests(ctx, sq, reqs, vn_idxs: dict, local_vns: list, W: int, parts: list | None = None):
-    """Digests of every other rank's slice of the local VNs' signed payloads
-    -> ({(request, part): digest}, {(request, part) with an empty slice})."""
+def _expected_digests(ctx, sq, reqs, vn_idxs: dict, local_vns: list, groups: dict, gparts: dict):
+    """Digests of the local VNs' helpers' slices of their signed payloads ->
+    ({(request, rank): digest}, {(request, rank) with an empty slice})."""
     me = ctx.rank
-    need = sorted({i for vn in local_vns for i in vn_idxs[vn.id]}) if W > 1 else []
+    want: dict = {}  # (request, rank) -> part
+    for vn in local_vns:
+        for i in vn_idxs[vn.id]:
+            for j in groups[vn.id]:
+                if j != me:
+                    want.setdefault((i, j), gparts[vn.id][j])
     expected: dict = {}
-    empty: set = set()  # (request, part) whose slice is empty: nothing to check there
+    empty: set = set()  # (request, rank) whose slice is empty: nothing to check there
     with timers.span("rp.verify.expected_digests"):
         entries, keys = [], []
-        for i in need:
+        for (i, j), part in sorted(want.items()):
             try:
                 lists = prq._range_lists(reqs[i], ctx.device)
             except Exception:  # noqa: BLE001 -- undecodable: every slice is redone (and fails)
                 continue
-            for j in range(W):
-                if j == me:
-                    continue  # this rank's own part was checked from this very payload
-                sl = prq.slice_lists(lists, sq, parts[j] if parts is not None else (j, W))
-                if not sl:
-                    empty.add((i, j))
-                    continue
-                entries.append(sl)
-                keys.append((i, j))
+            sl = prq.slice_lists(lists, sq, part)
+            if not sl:
+                empty.add((i, j))
+                continue
+            entries.append(sl)
+            keys.append((i, j))
         for key, d in zip(keys, prq.lists_digests(entries)):
             expected[key] = d
     return expected, empty
 
 
-def _check_helper_digests(ctx, sq, reqs, vn_idxs: dict, local_vns: list, gathered: list, W: int,
-                          pre=None, parts: list | None = None) -> dict:
-    """For each local VN: the (base_key, part) pairs whose helper-reported
+def _check_helper_digests(ctx, sq, reqs, vn_idxs: dict, local_vns: list, gathered, groups: dict, gparts: dict,
+                          pre) -> dict:
+    """For each local VN: the (base_key, rank) pairs whose helper-reported
     slice digest equals the digest of that slice of the VN's own signed
-    payload, and the mismatches to redo ({part: [request index]}).
-    ``pre``: the (expected, empty) of ``_expected_digests`` computed earlier."""
+    payload, and the mismatches to redo ({rank: [request index]}).  A helper
+    whose slice of a list is empty (a list shorter than the group) has no
+    verdict on it and is in neither.  ``pre``: the (expected, empty) of
+    ``_expected_digests``."""
     me = ctx.rank
-    expected, empty = pre if pre is not None else _expected_digests(ctx, sq, reqs, vn_idxs, local_vns, W, parts)
+    expected, empty = pre
     out = {}
     for vn in local_vns:
         ok_pairs, redo = set(), {}
         for i in vn_idxs[vn.id]:
             bk = reqs[i].base_key()
-            for j in range(W):
-                if j == me or (i, j) in empty or (expected.get((i, j)) is not None
-                                       and gathered[j][1].get(bk) == expected[(i, j)]):
+            for j in groups[vn.id]:
+                if j == me:
+                    continue
+                got = gathered[j][1].get(_pkey(gparts[vn.id][j]), {}).get(bk)
+                if (i, j) in empty:
+                    continue
+                if expected.get((i, j)) is not None and got == expected[(i, j)]:
                     ok_pairs.add((bk, j))
                 else:
                     redo.setdefault(j, []).append(i)
@@ -349,10 +445,8 @@ def _pool_async(ctx, sq, reqs, vns, comm=None):
     range batches (the GPU's long pole) run while this thread checks the
     short per-CN proofs of each VN.  On a multi-rank node the worker also
     owns the pool's collectives (the main thread issues none meanwhile)."""
-    import concurrent.futures as cf
-
     if not hasattr(ctx, "_pool_exec"):
-        ctx._pool_exec = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="drynx-vn-pool")
+        ctx._pool_exec = streams.executor(ctx.device, 1, "drynx-vn-pool")
     arrived = time.perf_counter()  # the fan-out just delivered the VNs' inboxes
     if ctx.device.type != "cuda":
         return ctx._pool_exec.submit(pool_verify_ranges, ctx, sq, reqs, vns, comm, arrived)
@@ -442,15 +536,15 @@ def range_shape(sq):
 
 
 def early_plane_ok(ctx, sq) -> bool:
-    """The range plane starts before the CN phases when verification is pooled
-    (single operator), the survey has VNs and proofs, and there are range
+    """The range plane starts before the CN phases (whatever the
+    verification mode) when the survey has VNs and proofs, and there are range
     proofs to verify: with ranges (0, 0) the DPs ship commitments only, and
     starting the plane early would just put their signing and fan-out on the
     CN phases' thread instead of beside them."""
     q = sq.Query
     return bool(q.Proofs) and q.RosterVNs is not None and len(q.RosterVNs.list) > 0 \
         and any(r[0] and r[1] for r in (q.Ranges or [])) \
-        and use_pool(ctx) and os.environ.get("DRYNX_RANGE_PLANE", "1") != "0"
+        and os.environ.get("DRYNX_RANGE_PLANE", "1") != "0"
 
 
 LEDGER_PREFETCH = True  # A/B constants (tools/ab_patch.py --no-ledger-prefetch / --pool-priority)
@@ -466,17 +560,14 @@ def proof_collection(ctx, sq, local_requests: list, early: dict | None = None, l
     and check these -- as the reference's VNs verify each proof as it arrives
     (proof_collection_protocol.go:183-305) -- and store one bitmap."""
     vns = [ctx.cluster.by_id(si.id) for si in sq.Query.RosterVNs.list]
-    pool = use_pool(ctx)
     with timers.timed("ProofFanOut"):
-        reqs = fan_out(ctx, sq, local_requests, pool=pool and early is None)
+        # (range lists not already out on the range plane go through the verification groups now)
+        reqs = fan_out(ctx, sq, local_requests, pool=early is None)
     if early is not None:
         reqs = early["reqs"] + reqs
     bitmaps = {}
     with timers.timed("ProofVerification"):
-        if early is not None:
-            pooled = early["pooled"]
-        else:
-            pooled = _pool_async(ctx, sq, reqs, vns) if pool else None
+        pooled = early["pooled"] if early is not None else _pool_async(ctx, sq, reqs, vns)
         local_vns = [vn.id for vn in vns if vn.rank == ctx.rank]
 
         def checks(rs, range_pooled):
@@ -521,7 +612,9 @@ def proof_collection(ctx, sq, local_requests: list, early: dict | None = None, l
     # it resumed from its ledger) and builds the same block itself -- no
     # broadcast round for the block
     root = vns[0]
-    mine = {"bm": bitmaps}
+    # every rank's chain head rides along: all ranks see whether they would
+    # build on the root VN's head before anyone signs a block
+    mine = {"bm": bitmaps, "head": ctx.last_block.Hash if ctx.last_block is not None else None}
     if ctx.rank == root.rank:
         resumed = None
         if ctx.last_block is None:
@@ -529,11 +622,22 @@ def proof_collection(ctx, sq, local_requests: list, early: dict | None = None, l
             # node over a persisted workdir) instead of starting a new genesis
             ctx.last_block = ctx.get_latest_block(root.id)
             resumed = ctx.last_block.to_bytes() if ctx.last_block is not None else None
-        mine["root"] = {"time": time.time(), "prev": resumed}
+        mine["root"] = {"time": time.time(), "prev": resumed,
+                        "head": ctx.last_block.Hash if ctx.last_block is not None else None}
     allbm, rootp = {}, None
-    for d in ctx.comm.all_gather_object(mine):
+    gathered = ctx.comm.all_gather_object(mine)
+    for d in gathered:
         allbm.update(d["bm"])
         rootp = d.get("root", rootp)
+    if rootp["prev"] is None:
+        # no resumed head to adopt: every rank must already hold the root's
+        # head (a rank left behind by a survey that failed on it would build a
+        # block with another hash); decided from the gathered heads, so every
+        # rank raises together instead of hanging in the co-signing round
+        lag = [r for r, d in enumerate(gathered) if d["head"] != rootp["head"]]
+        if lag:
+            raise RuntimeError(f"survey {sq.SurveyID}: rank(s) {lag} hold another chain head than the root VN "
+                               f"({rootp['head']}); refusing to build diverging blocks")
     if hasattr(ctx, "take_proof_starts"):
         # the VNs' verdicts are back on every DP's rank: the reference's
         # <dp>_AllProofs ends here (its proof collection's feedback channel,

@@ -77,6 +77,10 @@ class DrynxNode:
         self.comm = comm or LocalComm(device or ("cuda" if torch.cuda.is_available() else "cpu"))
         self.rank = self.comm.rank
         self.device = torch.device(device) if device is not None else self.comm.device
+        if self.device.type == "cuda":
+            if self.device.index is None:
+                self.device = torch.device("cuda", torch.cuda.current_device())
+            timers.set_device(self.device)
         self.cluster = cluster
         self.key_index = KeyIndex([p.id for p in cluster.parties])
         self.workdir = workdir
@@ -175,7 +179,7 @@ class DrynxNode:
                 for k, ref in zip(mine, self._blobs.put_many(mine, self._host_bytes(items))):
                     refs[k] = ref
             if theirs:  # another VN rank of this node claimed them: references only, no device-to-host copy
-                for k, ref in zip(theirs, self._blobs.put_refs(theirs, [tensors[k].numel() for k in theirs])):
+                for k, ref in zip(theirs, self._blobs.put_refs(theirs)):
                     refs[k] = ref
         for k, idxs in fresh.items():
             for i in idxs:
@@ -223,6 +227,7 @@ class DrynxNode:
         pinned copy on the ledger stream, so the producer only waits for it.
         An item may be a ``ledger_codec.Pending``: the producer builds its
         compact image on the ledger stream and copies that instead."""
+        from ..ledger.store import Compact
         from ..proofs.ledger_codec import Pending
 
         items = list(tensors)
@@ -264,12 +269,14 @@ class DrynxNode:
             out, o, k = [], 0, 0
             for it in items:
                 if isinstance(it, Pending) and it.image is None:
-                    out.append(it.produce(st))
+                    v = it.produce(st)
                 else:
                     v = mv[o: o + sizes[k]]
-                    out.append(it.finish(v) if isinstance(it, Pending) else v)
+                    v = it.finish(v) if isinstance(it, Pending) else v
                     o += sizes[k]
                     k += 1
+                # compact images are tagged as such for the store (never sniffed when read)
+                out.append(Compact(v) if isinstance(it, Pending) and it.compact else v)
             return out
         return produce
 
@@ -475,7 +482,7 @@ class DrynxNode:
             return fut
         attr = f"_cnp_pool{lane}"
         if not hasattr(self, attr):
-            setattr(self, attr, cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix=f"drynx-cn-proofs{lane}"))
+            setattr(self, attr, streams.executor(self.device, 1, f"drynx-cn-proofs{lane}"))
         side = self._side_stream(f"_cnp_streams{lane}", "DRYNX_CNP_PRIORITY", bulk=0, alone=-1)
         # the job's inputs are the work queued so far: an event recorded now and
         # waited for when the job STARTS on the worker -- a wait_stream issued
@@ -510,10 +517,8 @@ class DrynxNode:
         return out
 
     def _submit_client(self, fn, partial: SurveyResult):
-        import concurrent.futures as cf
-
         if not hasattr(self, "_client_pool"):
-            self._client_pool = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="drynx-querier")
+            self._client_pool = streams.executor(self.device, 1, "drynx-querier")
         if self.device.type != "cuda":
             return self._client_pool.submit(fn, partial)
         side = self._side_stream("_client_streams", "DRYNX_CLIENT_PRIORITY", bulk=-1, alone=0)
@@ -640,7 +645,7 @@ class DrynxNode:
         import concurrent.futures as cf
 
         if not hasattr(self, "_pool"):
-            self._pool = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="drynx-proofs")
+            self._pool = streams.executor(self.device, 1, "drynx-proofs")
         if type(self)._range_proofs is not DrynxNode._range_proofs or "_range_proofs" in self.__dict__:
             # a patched (e.g. fault-injecting) prover: run it synchronously
             lst: list = []

@@ -1,4 +1,5 @@
-"""Stream priorities of the framework's HIP streams.
+"""Stream priorities of the framework's HIP streams, and the node's worker
+threads pinned to the rank's device.
 
 ``priority(p)`` is the priority a stream asks for; DRYNX_STREAM_PRIO=0 turns
 every request into the normal priority.  ROCm gives each priority level its
@@ -9,6 +10,7 @@ costs with no overlap inflation)."""
 from __future__ import annotations
 
 import os
+import threading
 
 
 def priority(p: int) -> int:
@@ -28,3 +30,35 @@ def node_process_setup():
     import sys
 
     sys.setswitchinterval(NODE_SWITCH_INTERVAL)
+
+
+_made: list = []  # thread-name prefixes of every executor made here (tests audit the node's workers)
+_tls = threading.local()
+
+
+def executor(device=None, max_workers: int = 1, name: str = "drynx"):
+    """Every worker thread of a node comes from here: a ThreadPoolExecutor
+    whose threads start by making the rank's GPU their current device
+    (``torch.cuda.set_device``), so a worker of rank k never launches or
+    allocates on device 0 by default (one process per GPU: on an 8-GPU node
+    a device-k worker touching device 0 would only show in the 8-GPU run).
+    ``device`` None / CPU: plain threads."""
+    import concurrent.futures as cf
+
+    import torch
+
+    dev = torch.device(device) if device is not None else None
+    init = None
+    if dev is not None and dev.type == "cuda":
+        idx = dev.index if dev.index is not None else torch.cuda.current_device()
+
+        def init():
+            torch.cuda.set_device(idx)
+            _tls.device = idx
+    _made.append(name)
+    return cf.ThreadPoolExecutor(max_workers=max_workers, thread_name_prefix=name, initializer=init)
+
+
+def pinned_device():
+    """The device index this worker thread was pinned to (None: not a pinned worker)."""
+    return getattr(_tls, "device", None)

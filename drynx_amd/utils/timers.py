@@ -92,6 +92,17 @@ def _device_timed() -> bool:
     return torch.cuda.is_available() and torch.cuda.is_initialized()
 
 
+_DEVICE = None  # the rank's GPU (``set_device``); None: the calling thread's current device
+
+
+def set_device(device):
+    """The node's device: phase-end events are recorded on ITS current stream
+    (a phase may end on a worker thread)."""
+    global _DEVICE
+    d = torch.device(device)
+    _DEVICE = d if d.type == "cuda" else None
+
+
 # Phase timers measure WALL time from the host's start of the phase to the
 # completion of the last operation the phase queued on its stream (the
 # reference's StartTimer/EndTimer bracket goroutines that block until their
@@ -148,7 +159,8 @@ class Timer:
             _emit(self.name, int(self.t0 * 1e9), int(t1 * 1e9))
         if self.sync and _device_timed():
             e1 = torch.cuda.Event()
-            e1.record()
+            # on the rank's device explicitly (``set_device``), whatever thread ends the phase
+            e1.record(torch.cuda.current_stream(_DEVICE))
             if not e1.query():  # the phase's device work is still running: the watcher stamps its end
                 with _watch_cv:
                     _watch.append((self.name, self.t0, e1))

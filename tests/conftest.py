@@ -7,6 +7,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
 os.environ.setdefault("DX_NUM_THREADS", "8")
+# every native launch asserts its thread's current device is the tensor's
+# (worker threads are pinned to the rank's GPU: utils/streams.executor)
+os.environ.setdefault("DRYNX_CHECK_DEVICE", "1")
 
 
 def pytest_configure(config):

@@ -2,6 +2,8 @@
 stored as torus (T2) images and rebuilt bit for bit, on the host build here
 and on the GPU in the marked test; a bundle whose GT elements do not round-trip
 falls back to its raw bytes; the store returns the signed bytes either way."""
+import os
+
 import pytest
 import torch
 
@@ -68,13 +70,38 @@ def test_gt_t2_rejects_non_unitary():
 
 
 def test_store_returns_signed_bytes(tmp_path, bundle):
+    """A compact image the writer TAGGED (``ledger.store.Compact``: a rank's
+    blob segment or a node-shared file) reads back as the signed bytes; the
+    same image stored untagged, or any value that merely looks like one, is
+    returned as stored (nothing is decompressed by sniffing)."""
+    from drynx_amd.ledger.store import BlobSegment, Compact, NodeBlobs
+
     stored = bytes(_roundtrip(bundle))
+    signed = bundle.cpu().numpy().tobytes()
     st = Store(str(tmp_path / "db.sqlite"))
-    st.update("s/range", "k", stored)
-    assert st.get("s/range", "k") == bundle.cpu().numpy().tobytes()
-    st.update("s/other", "k", b"RPC2" + b"\0" * 40)  # the magic alone is not the layout
+    seg = BlobSegment(str(tmp_path / "ledger_r0.blobs"))
+    ref_c, ref_r = seg.put_many(["c", "r"], lambda: [Compact(memoryview(stored)), memoryview(stored)])
+    st.update("s/range", "tagged", ref_c)
+    st.update("s/range", "untagged", ref_r)
+    st.update("s/range", "inline", stored)
+    assert st.get("s/range", "tagged") == signed
+    assert st.get("s/range", "untagged") == stored and st.get("s/range", "inline") == stored
+    # node-shared: the claimant writes the compact image, another rank's whole-file reference reads it
+    root = str(tmp_path / "node")
+    w, r = NodeBlobs(root), NodeBlobs(root)
+    assert w.claim(["d"]) == [True] and r.claim(["d"]) == [False]
+    w.put_many(["d"], lambda: [Compact(memoryview(stored))])
+    w.flush()
+    st.update("s/range", "node", r.put_refs(["d"])[0])
+    assert st.get("s/range", "node") == signed
+    st.update("s/other", "k", b"RPC2" + b"\0" * 40)
     assert st.get("s/other", "k") == b"RPC2" + b"\0" * 40
     st.close()
+    seg.close(remove=True)
+    w.close(remove=True)
+    assert os.path.exists(root)  # another user (r) still has the node directory open
+    r.close(remove=True)
+    assert not os.path.exists(root)
 
 
 @pytest.mark.gpu

@@ -63,7 +63,7 @@ def test_node_shared_payloads(tmp_path):
     assert reader.claim(["d1"]) == [False]           # already claimed on the node
     rstore = Store(str(tmp_path / "db_vn1.sqlite"))
     data = np.arange(100000, dtype=np.uint32).view(np.uint8)
-    ref = reader.put_refs(["d1"], [data.nbytes])[0]
+    ref = reader.put_refs(["d1"])[0]
     rstore.update("proofs", "k", ref)               # a reference before the claimant has written anything
     import threading
     import time

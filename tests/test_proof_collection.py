@@ -64,7 +64,6 @@ def test_early_range_plane_only_with_range_proofs(tmp_path, monkeypatch):
     their signing / fan-out stays off the CN phases' thread
     (``early_plane_ok``); the pool itself is used either way."""
     cl, node, sq = _setup(tmp_path)
-    monkeypatch.setattr(pcp, "use_pool", lambda ctx: True)
     assert pcp.early_plane_ok(node, sq)
     client = DrynxClient(node)
     sq0 = make_survey(client, cl, "mean", query_min=0, query_max=10, rows=4, proofs=1, ranges=[0, 0])

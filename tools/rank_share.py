@@ -154,6 +154,9 @@ def main():
                     help="one direction of one xGMI link (GB/s): the fan-out term of the projection")
     ap.add_argument("--passes", type=int, default=2, help="1, or 2: a second pass in the reverse order (min of both)")
     ap.add_argument("--order", default=None, help="comma list: the order the ranks are measured in (default 0..W-1)")
+    ap.add_argument("--vn-mode", default="pool", choices=["pool", "local", "own"],
+                    help="proof_collection.verification_mode of the projected run: pool (every rank for every VN, "
+                         "single operator), local (each VN's own rank + helpers serving only it), own")
     ap.add_argument("--torch-prof", default=None,
                     help="also profile the 1-GPU pooled check of the whole inbox and the proving of every DP "
                          "(torch.profiler on this thread): the GPU time of torch ops per framework frame")
@@ -210,10 +213,38 @@ def main():
     for i, v in enumerate(cl.vns):
         place.setdefault((n_cns + i) % W, []).append(v.id)
     dps_of = {k: [dp.id for i, dp in enumerate(cl.dps) if (n_cns + n_vns + i) % W == k] for k in range(W)}
-    vn_ranks = {(n_cns + i) % W for i in range(n_vns)}
-    # the framework's weighted pool parts for this placement (prq.balanced_parts)
-    parts = prq.balanced_parts(W, [len(dps_of[k]) for k in range(W)],
-                               [sum(1 for i in range(n_vns) if (n_cns + i) % W == k) for k in range(W)])
+    vn_rank_list = [(n_cns + i) % W for i in range(n_vns)]
+    vn_ranks = set(vn_rank_list)
+    vn_ids = [vn.id for vn in cl.vns]
+    # the framework's verification groups and weighted parts for this placement
+    # (proof_collection.verification_groups: the pool, vn-local or own)
+    groups, gparts = pcp.verification_groups(a.vn_mode, W, [len(dps_of[k]) for k in range(W)],
+                                             [vn_rank_list.count(k) for k in range(W)], vn_rank_list)
+    groups, gparts = dict(zip(vn_ids, groups)), dict(zip(vn_ids, gparts))
+
+    def parts_of(k):
+        """{part: [VN ids]} rank k checks (the VNs whose group holds k)."""
+        out = {}
+        for v in vn_ids:
+            if k in groups[v]:
+                out.setdefault(tuple(gparts[v][k]), []).append(v)
+        return out
+
+    def helper_part(k):
+        """The slice part a rank hosting no VN receives (it serves one part)."""
+        ps = list(parts_of(k))
+        return ps[0] if ps else None
+
+    def digest_slices(full, k):
+        """The slices a VN rank k digests: its local VNs' helpers' parts."""
+        want = {}
+        for v, r in zip(vn_ids, vn_rank_list):
+            if r != k:
+                continue
+            for j in groups[v]:
+                if j != k:
+                    want.setdefault(j, gparts[v][j])
+        return [prq.slice_lists(ls, sq, p_) for ls in full for p_ in want.values()]
 
     def helper_reqs(part):
         out = []
@@ -246,12 +277,13 @@ def main():
         reps = int(os.environ.get("RANK_SHARE_TRACE_REPS", "1"))  # > 1: the last one is the steady state
         for k in [int(x) for x in os.environ.get("RANK_SHARE_PARTS", "3,6").split(",") if x]:
             for _ in range(reps):
-                reqs_k = full_reqs() if k in vn_ranks else helper_reqs(parts[k])
+                reqs_k = full_reqs() if k in vn_ranks else helper_reqs(helper_part(k))
                 _sync()
                 time.sleep(1.0)  # an idle gap: a kernel trace shows this part as its own burst (tools/kernel_bursts.py)
                 with timers.span(f"pool_part[{k}]"):
-                    pool_part(reqs_k, {v: list(range(len(rng))) for v in vn_idxs}, sq, dev, cache, parts[k],
-                              {vn.id: Coins() for vn in cl.vns})
+                    for part, pv in parts_of(k).items():
+                        pool_part(reqs_k, {v: list(range(len(rng))) for v in pv}, sq, dev, cache, part,
+                                  {v: Coins() for v in pv})
                 _sync()
         for k in [int(x) for x in os.environ.get("RANK_SHARE_PROVE", "").split(",") if x]:
             # rank k's proving (its DPs' range proofs + signed envelopes), after the pool parts
@@ -266,7 +298,9 @@ def main():
         if os.environ.get("RANK_SHARE_TRACE_ONLY") == "1":
             node.close(remove=True)
             return
-    res = {"world": W, "features": d,
+    res = {"world": W, "features": d, "vn_mode": a.vn_mode,
+           "trust_model": "single-operator-pool" if a.vn_mode == "pool" and W > 1 else "vn-local",
+           "groups": groups,
            "placement": {k: {"parties": place.get(k, []), "dps": dps_of[k]} for k in range(W)},
            "ranks": {}}
     order = [int(x) for x in a.order.split(",")] if a.order else list(range(W))
@@ -276,38 +310,44 @@ def main():
     seq = order + (order[::-1] if a.passes > 1 else [])
     res["passes"] = {}
     for pi, k in enumerate(seq):
-        part = parts[k]
+        mp_ = parts_of(k)
         coins = {vn.id: Coins() for vn in cl.vns}
         is_vn = k in vn_ranks
+
+        def run_parts(reqs_k):
+            for part, pv in mp_.items():
+                pool_part(reqs_k, {v: list(range(len(rng))) for v in pv}, sq, dev, cache, part,
+                          {v: coins[v] for v in pv})
         if is_vn:
             full = [prq._range_lists(reqs[i], dev) for i in rng]
             dst = torch.cuda.Stream(dev) if dev.type == "cuda" else None
+            dig = digest_slices(full, k)
 
             def digests_side():
                 ctx = torch.cuda.stream(dst) if dst is not None else contextlib.nullcontext()
                 with ctx:
-                    prq.lists_digests([prq.slice_lists(ls, sq, parts[j]) for ls in full for j in range(W) if j != k])
+                    if dig:
+                        prq.lists_digests(dig)
                 if dst is not None:
                     dst.synchronize()
 
             def vn_part():
-                # as proof_collection.pool_verify_ranges: the VN's digests of the
-                # other ranks' slices run on their own stream as an idle task of
-                # the part (while its verifier waits for the device)
+                # as proof_collection.pool_verify_ranges: the VN's digests of its
+                # helpers' slices run on their own stream as an idle task of the
+                # part (while its verifier waits for the device)
                 if dst is not None:
                     dst.wait_stream(torch.cuda.current_stream(dev))
                 fut = rp.add_idle_task(rp.Deferred(digests_side))
-                pool_part(full_reqs(), {v: list(range(len(rng))) for v in vn_idxs}, sq, dev, cache, part, coins)
+                run_parts(full_reqs())
                 fut.result()
             t_pool = timed(vn_part, a.reps)
+        elif mp_:
+            t_pool = timed(lambda: run_parts(helper_reqs(helper_part(k))), a.reps)
         else:
-            t_pool = timed(lambda: pool_part(helper_reqs(part), {v: list(range(len(rng)))
-                                                                                  for v in vn_idxs},
-                                                              sq, dev, cache, part, coins), a.reps)
+            t_pool = 0.0
         t_dig = 0.0
-        if is_vn:  # alone, for reference (the pool time above already runs them alongside)
-            t_dig = timed(lambda: prq.lists_digests([prq.slice_lists(ls, sq, parts[j]) for ls in full
-                                                     for j in range(W) if j != k]), a.reps)
+        if is_vn and dig:  # alone, for reference (the pool time above already runs them alongside)
+            t_dig = timed(lambda: prq.lists_digests(dig), a.reps)
         mine = {dp: dp_results[dp] for dp in dps_of[k]}
         t_prove = timed(lambda: node._sign_range(sq, node._prove_range(sq, mine)), a.reps) if mine else 0.0
         rec = {"prove_ms": t_prove, "pool_ms": t_pool, "vn_digest_ms": t_dig, "vn_rank": is_vn, "dps": len(mine)}
@@ -349,7 +389,13 @@ def main():
         for dst in range(W):
             if dst == src:
                 continue
-            nb = full if dst in vn_ranks else prq.range_bundle_pack(prq.slice_lists(lists, sq, parts[dst])).numel() * 4
+            hp = helper_part(dst) if dst not in vn_ranks else None
+            if dst in vn_ranks:
+                nb = full
+            elif hp is not None:
+                nb = prq.range_bundle_pack(prq.slice_lists(lists, sq, hp)).numel() * 4
+            else:
+                continue
             link[(src, dst)] = link.get((src, dst), 0) + nb
     bw = a.xgmi_link_gbs * 1e6  # bytes per ms
     exchange_end = max((res["ranks"][s_]["prove_ms"] + max((b for (s2, _), b in link.items() if s2 == s_),
@@ -359,7 +405,7 @@ def main():
     res["projection_step_ms"] = round(max(serial, exchange_end + pool_max) + ctrl, 2)
     res["projection_terms_ms"] = {"prove_max": prove_max, "xgmi": xgmi, "pool_max": pool_max, "serial": serial,
                                   "ctrl": round(ctrl, 3)}
-    print(json.dumps({"projection_ms": proj, "step_ms": res["projection_step_ms"],
+    print(json.dumps({"vn_mode": a.vn_mode, "projection_ms": proj, "step_ms": res["projection_step_ms"],
                       "terms": res["projection_terms_ms"]}), flush=True)
     if a.json_out:
         json.dump(res, open(a.json_out, "w"), indent=1)
