@@ -78,7 +78,12 @@ QUERY_CONFIGS = {
     "mean": dict(ref_s=2.57, dps=10, records=100_000, d=1, lo=0, hi=3, ranges=(16, 5)),
     "variance": dict(ref_s=2.74, dps=10, records=100_000, d=1, lo=0, hi=3, ranges=(16, 5)),
     "lin_reg": dict(ref_s=15.97, dps=8, records=7_680, d=8, lo=0, hi=199, ranges=(16, 8)),
+    # the reference's MaxOptimized sheet (simul/test_data/graphs/TIFS/maxOpti.py:9-12): max with the
+    # unary encoding over a range of --range values (one ciphertext + one (2, 1) range proof per value
+    # and DP: the simulation's Ranges code 1), 3 CNs, 3 VNs, 10 DPs; totals 5.5 / 28.5 / 246 / 2226 s
+    "max": dict(ref_s=None, dps=10, records=1_000, d=1, lo=0, hi=None, ranges=(2, 1)),
 }
+REFERENCE_MAX_UNARY_S = {1_000: 5.5, 10_000: 28.5, 100_000: 246.0, 1_000_000: 2226.0}  # maxOpti.py:9-12
 
 
 def parse():
@@ -99,6 +104,9 @@ def parse():
     ap.add_argument("--max-iter", type=int, default=450)
     ap.add_argument("--device", default=None)
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--range", dest="value_range", type=int, default=1_000,
+                    help="--query max: values in [0, RANGE) -> RANGE unary outputs per DP (maxOpti rows: "
+                         "1000 / 10000 / 100000 / 1000000)")
     ap.add_argument("--range-mode", type=int, default=0,
                     help="SurveyQuery.RangeProofMode: 0 reference semantics, 1 recomputed challenge + V in G2")
     ap.add_argument("--query", default="lr", choices=["lr", "lr_dro", *QUERY_CONFIGS],
@@ -513,8 +521,12 @@ def _torch_profiler_dump(p, rank):
 
 
 def main_query(args):
-    """BASELINE.json configs 2 and 3: one verifiable integer query per step."""
-    cfg = QUERY_CONFIGS[args.query]
+    """BASELINE.json configs 2 and 3, and the MaxOptimized rows (``--query max
+    --range N``): one verifiable integer query per step."""
+    cfg = dict(QUERY_CONFIGS[args.query])
+    if args.query == "max":
+        cfg["hi"] = args.value_range - 1
+        cfg["ref_s"] = REFERENCE_MAX_UNARY_S.get(args.value_range)
     init_distributed()
     comm = make_comm(args.device)
     _check_world(args, comm)
@@ -526,6 +538,8 @@ def main_query(args):
     offsets = {"cn": 0, "vn": args.cns % world, "dp": (args.cns + args.vns) % world}
     cl, node = local_cluster(args.cns, n_dps, args.vns, comm=comm, device=device,
                              workdir=tempfile.mkdtemp(prefix=f"drynx_bench_r{rank}_"), offsets=offsets)
+    if args.vn_mode:
+        node.pool_policy = args.vn_mode
     rows = cfg["records"] // n_dps
     d = cfg["d"]
     n_in = d + 1 if args.query == "lin_reg" else 1
@@ -535,21 +549,27 @@ def main_query(args):
     u, l = cfg["ranges"]
     client = DrynxClient(node, device=device) if rank == 0 else None
     template = None
+    t_setup = time.perf_counter()
     if rank == 0:
         template = make_survey(client, cl, args.query, query_min=cfg["lo"], query_max=cfg["hi"], d=d, rows=rows,
                                proofs=1, ranges=[u, l], thresholds=[1.0, 1.0, 1.0, 0.0, 1.0], sig_device=device,
                                deterministic_sigs=args.deterministic_sigs)
+    sig_s = time.perf_counter() - t_setup
+    decoded = []
 
     def one_step():
         if rank == 0:
             sq = copy.copy(template)
             sq.SurveyID = new_survey_id()
             _, vals, res = client.send_survey_query(sq)
+            decoded.append(vals[0])
             return res
         return node.run_survey(None)
 
+    t_first = time.perf_counter()
     for _ in range(args.warmup):
         one_step()
+    first_s = (time.perf_counter() - t_first) / max(1, args.warmup) if args.warmup else 0.0
     timers.reset()
     comm.barrier()
     if device.type == "cuda":
@@ -564,23 +584,45 @@ def main_query(args):
     ok = all(b is not None and all(v == 1 for v in b.data_block().Proofs.values()) for b in blocks)
     sec = elapsed / args.steps
     n_out = len(template.Query.Ranges) if rank == 0 else None
+    result_ok = None
+    if args.query == "max":  # the decoded max equals the max over every DP's records
+        mx = comm.all_gather_object(max((int(c.max()) for cols in node.dp_data.values() for c in cols), default=None))
+        want = max(v for v in mx if v is not None)
+        result_ok = rank != 0 or all(int(round(v[0])) == want for v in decoded)
+    allt = comm.all_gather_object(timers.summary())
     if rank == 0:
+        phase = {}
+        for t in allt:
+            for k, v in t.items():
+                phase[k] = max(phase.get(k, 0.0), v["sum"] / args.steps)
         line = {
             "metric": f"end-to-end verifiable {args.query} query latency",
             "value": round(sec, 5),
             "unit": "s per query (whole job)",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1000 * sec, 2),
             "higher_is_better": False, "scaling": "strong",
-            "vs_baseline": round(sec / cfg["ref_s"], 5),
-            "speedup_vs_reference": round(cfg["ref_s"] / sec, 1),
+            "vs_baseline": round(sec / cfg["ref_s"], 5) if cfg["ref_s"] else None,
+            "speedup_vs_reference": round(cfg["ref_s"] / sec, 1) if cfg["ref_s"] else None,
             "dtype": "bn254-exact/int64",
             "data": "synthetic (uniform integer records, random keys and input-validation signatures)",
-            "config": {"model": f"{args.query}" + (f" d={d}" if args.query == "lin_reg" else ""),
+            "config": {"model": f"{args.query}" + (f" d={d}" if args.query == "lin_reg" else "")
+                       + (f" unary encoding over [0, {args.value_range})" if args.query == "max" else ""),
                        "global_batch": rows * n_dps, "seq_len": None,
                        "parallelism": f"{world} ranks: {n_dps} DPs, {args.cns} CNs, {args.vns} VNs",
                        "dps": n_dps, "records_per_dp": rows, "outputs_per_dp": n_out,
-                       "range_proof": {"u": u, "l": l}, "verification": "every VN verifies every proof"},
+                       "range_proof": {"u": u, "l": l, "proofs_per_query": n_dps * n_out,
+                                       "verifications_per_query": n_dps * n_out * args.vns},
+                       "sigs": ("deterministic (InitRangeProofSignatureDeterministic)" if args.deterministic_sigs
+                                else "random (per CN, per column)"),
+                       "verification": "every VN verifies every proof"},
+            "reference_row": ({"sheet": "MaxOptimized", "source": "simul/test_data/graphs/TIFS/maxOpti.py:9-12",
+                               "range": args.value_range, "total_s": cfg["ref_s"]} if args.query == "max" else None),
             "all_proofs_valid": ok,
+            "result_ok": result_ok,
+            "signature_setup_s": round(sig_s, 3),
+            "first_query_s": round(first_s, 3),
+            "phase_s": {k: round(v, 4) for k, v in sorted(phase.items())
+                        if not k[:2] in ("dp", "vn", "cn") or k[2:3] == "0"},
         }
         print(json.dumps(line), flush=True)
         if args.json_out:

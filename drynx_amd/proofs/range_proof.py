@@ -74,16 +74,28 @@ def init_range_proof_signature(u: int, secret: int | None = None, device="cpu") 
 def init_range_proof_signatures(us: list, device="cpu") -> list:
     """Batched InitRangeProofSignature for many (CN, column) keys at once
     (range_proof.go:270-288, simul/drynx_simul.go:292-296): one random secret
-    x per entry of ``us``; y = x*B and every A_k = (x+k)^-1 * B2 in two
-    fixed-base launches instead of one launch per key."""
+    x per entry of ``us`` (ChaCha20 keyed from the OS CSPRNG, expanded on the
+    device), y = x*B and every A_k = (x+k)^-1 * B2 -- the Fr additions and
+    inversions row-wise on the device too -- in two fixed-base launches, so
+    the 3 x 1M keys of a million-value range cost seconds, not minutes of
+    Python big-int inversions.  The secrets never leave the device."""
     n = len(us)
     if n == 0:
         return []
-    xs = [O.random_scalar() for _ in range(n)]
-    y = nt.g1_to_affine(nt.g1_fb_mul(bn.base_table(device), bn.scalars_tensor(xs, device)))
+    dev = torch.device(device)
+    xs = nt.prg_scalars(os.urandom(32), n, dev)  # [n, 8] uniform nonzero Fr
+    y = nt.g1_to_affine(nt.g1_fb_mul(bn.base_table(dev), xs))
     y_bytes = bn.g1_aff_to_bytes(y)
-    inv = [pow((x + k) % O.R, -1, O.R) for x, u in zip(xs, us) for k in range(int(u))]
-    A = bn.g2_aff_to_bytes(nt.g2_fb_mul(bn.base2_table(device), bn.scalars_tensor(inv, device)))
+    u_t = torch.as_tensor([int(u) for u in us], dtype=torch.long)
+    umax = int(u_t.max())
+    ks = bn.scalars_tensor(range(umax), dev)  # [umax, 8]: k = 0 .. umax - 1
+    # row (x_i + k) for every (i, k < u_i), in (i, k) order
+    rows = torch.arange(umax).expand(n, umax) < u_t[:, None]
+    xi = torch.arange(n)[:, None].expand(n, umax)[rows].to(dev)
+    kk = torch.arange(umax)[None, :].expand(n, umax)[rows].to(dev)
+    inv = nt.fr_arith(nt.FR_INV, nt.fr_arith(nt.FR_ADD, xs.index_select(0, xi).contiguous(),
+                                             ks.index_select(0, kk).contiguous()))
+    A = bn.g2_aff_to_bytes(nt.g2_fb_mul(bn.base2_table(dev), inv))
     out, o = [], 0
     for i, u in enumerate(us):
         out.append(PublishSignatureBytes(y_bytes[i].tobytes(), A[o: o + int(u)].tobytes()))
@@ -102,54 +114,96 @@ class SigMaterial:
     Fiat–Shamir hash."""
 
     def __init__(self, sigs, device="cpu"):
+        """Vectorised over every (CN, column) key: one bytes join, one device
+        decode (on-curve checked) of all y, the per-column sums of the y on
+        the device, and numpy deduplication of keys and signature points (a
+        million-value range brings 3 x 1M keys and 6M signature points)."""
         self.device = torch.device(device)
         self.S = len(sigs)
         self.n_cols = len(sigs[0]) if self.S else 0
         self.u = [len(sigs[0][c].Signature) // G2_LEN for c in range(self.n_cols)]
         self.umax = max(self.u) if self.u else 0
-        ys = []
-        A_bytes = np.zeros((self.S, self.n_cols, max(1, self.umax), G2_LEN), dtype=np.uint8)
-        for i in range(self.S):
-            for c in range(self.n_cols):
-                ys.append(O.g1_from_bytes(sigs[i][c].Public))
-                raw = np.frombuffer(sigs[i][c].Signature, dtype=np.uint8).reshape(-1, G2_LEN)
-                A_bytes[i, c, : raw.shape[0]] = raw
-        self.y_pts = ys  # index i*n_cols + c
-        self.y_jac = bn.g1_jac_tensor(ys, device) if ys else None
+        flat_sigs = [s for row in sigs for s in row]  # index i*n_cols + c
+        N = len(flat_sigs)
+        pub = np.frombuffer(b"".join(bytes(s.Public) for s in flat_sigs), dtype=np.uint8)
+        if pub.size != 64 * N:
+            raise ValueError("input-validation keys must be 64-byte G1 points")
+        pub = pub.reshape(N, 64)
+        self._pub = pub
+        y_aff = bn.g1_aff_from_bytes(pub, device, check=True) if N else None  # [N, 16]
+        self.y_jac = nt.g1_from_affine(y_aff) if N else None
+        umax = max(1, self.umax)
+        lens = {len(s.Signature) for s in flat_sigs}
+        if lens == {umax * G2_LEN}:  # every column the same u: one join
+            A_bytes = np.frombuffer(b"".join(bytes(s.Signature) for s in flat_sigs), dtype=np.uint8).reshape(
+                self.S, self.n_cols, umax, G2_LEN)
+        else:
+            A_bytes = np.zeros((self.S, self.n_cols, umax, G2_LEN), dtype=np.uint8)
+            for q, s in enumerate(flat_sigs):
+                raw = np.frombuffer(s.Signature, dtype=np.uint8).reshape(-1, G2_LEN)
+                A_bytes[q // max(1, self.n_cols), q % max(1, self.n_cols), : raw.shape[0]] = raw
         flat = A_bytes.reshape(-1, G2_LEN)
         nz = flat.any(axis=1)
         A = torch.zeros((flat.shape[0], 32), dtype=torch.int32, device=device)
         if nz.any():
-            A[torch.from_numpy(np.nonzero(nz)[0]).to(device)] = bn.g2_aff_from_bytes(flat[nz], device, check=False)
+            if nz.all():
+                A = bn.g2_aff_from_bytes(flat, device, check=False)
+            else:
+                A[torch.from_numpy(np.nonzero(nz)[0]).to(device)] = bn.g2_aff_from_bytes(flat[nz], device, check=False)
         self.A = A  # index (i*n_cols + c)*umax + k
-        self.Ysum_bytes = []
-        for c in range(self.n_cols):
-            acc = None
-            for i in range(self.S):
-                acc = O.g1_add(acc, ys[i * self.n_cols + c])
-            self.Ysum_bytes.append(O.g1_to_bytes(acc))
+        # per-column sum_i y_{i,col} (the Fiat-Shamir hash input), on the device
+        if N:
+            yj = self.y_jac.view(self.S, self.n_cols, -1)
+            acc = yj[0].contiguous()
+            for i in range(1, self.S):
+                acc = nt.g1_add(acc, yj[i].contiguous())
+            self._ysum = bn.g1_aff_to_bytes(nt.g1_to_affine(acc))  # [n_cols, 64]
+        else:
+            self._ysum = np.zeros((0, 64), dtype=np.uint8)
         # prover tables, keyed by the distinct signature point (deduplicated by value)
-        flat_u8 = A_bytes.reshape(-1, G2_LEN)
-        keys = [flat_u8[i].tobytes() for i in range(flat_u8.shape[0])]
-        first = {}
-        canon = []
-        for i, k in enumerate(keys):
-            canon.append(first.setdefault(k, i))
-        self.canon = torch.tensor(canon, dtype=torch.long)  # A index -> first index with the same point
+        _, first, inv = np.unique(np.ascontiguousarray(flat).view(np.dtype((np.void, G2_LEN))).reshape(-1),
+                                  return_index=True, return_inverse=True)
+        self.canon = torch.from_numpy(first[inv.reshape(-1)].astype(np.int64))  # A index -> first equal index
         self._ptab = {}
         # distinct CN keys y_{i,col} (one per CN when the signature sets reuse
         # a key, as InitRangeProofSignatureDeterministic does): comb tables let
         # the verifier's c*y_i be fixed-base multiplications
-        ykeys = [O.g1_to_bytes(y) for y in ys]
-        yfirst: dict = {}
-        first_idx: dict = {}
-        for i, k in enumerate(ykeys):
-            if k not in yfirst:
-                yfirst[k] = len(yfirst)
-                first_idx[k] = i
-        self.y_slot = [yfirst[k] for k in ykeys]
-        self.y_distinct = [ys[first_idx[k]] for k in yfirst]
+        if N:
+            _, yfirst, yinv = np.unique(pub.view(np.dtype((np.void, 64))).reshape(-1), return_index=True,
+                                        return_inverse=True)
+            order = np.argsort(yfirst, kind="stable")  # slots in order of first appearance
+            rank = np.empty_like(order)
+            rank[order] = np.arange(order.size)
+            self.y_slot = rank[yinv.reshape(-1)].tolist()
+            self._y_first = yfirst[order]
+            self._y_aff = y_aff
+        else:
+            self.y_slot, self._y_first, self._y_aff = [], np.zeros(0, dtype=np.int64), None
         self._ytab = {}
+
+    @property
+    def Ysum_bytes(self) -> list:
+        """Per column: the encoding of sum_i y_{i,col} (range_proof.go:350-374)."""
+        if not hasattr(self, "_ysum_list"):
+            self._ysum_list = [r.tobytes() for r in self._ysum]
+        return self._ysum_list
+
+    @property
+    def y_pts(self):
+        """Oracle points of the keys, index i*n_cols + c (decoded on demand)."""
+        pub = self._pub
+
+        class _Lazy:
+            def __getitem__(self, q):
+                return O.g1_from_bytes(pub[q].tobytes())
+
+            def __len__(self):
+                return pub.shape[0]
+        return _Lazy()
+
+    @property
+    def y_distinct(self) -> list:
+        return [O.g1_from_bytes(self._pub[q].tobytes()) for q in self._y_first]
 
     def challenge_words(self, device):
         """(B encoding [16], per-column sum_i y_i encodings [n_cols, 16]) as
@@ -157,7 +211,7 @@ class SigMaterial:
         key = ("cw", str(torch.device(device)))
         if key not in self._ytab:
             b = np.frombuffer(O.g1_to_bytes(O.G1_GEN), dtype="<i4").copy()
-            y = np.frombuffer(b"".join(self.Ysum_bytes), dtype="<i4").reshape(-1, 16).copy()
+            y = np.ascontiguousarray(self._ysum).view("<i4").reshape(-1, 16).copy()
             self._ytab[key] = (torch.from_numpy(b).to(device), torch.from_numpy(y).to(device))
         return self._ytab[key]
 
@@ -169,11 +223,13 @@ class SigMaterial:
         -- so the verifier's c * y_i are fixed-base; 256 keys on the host)."""
         dev = torch.device(device)
         cap = (int(os.environ.get("DRYNX_Y_TABLES_MB", 16384)) << 20) // (8192 * 64) if dev.type == "cuda" else 256
-        if not self.y_distinct or len(self.y_distinct) > cap:
+        nd = len(self._y_first)
+        if not nd or nd > cap:
             return None
         key = str(torch.device(device))
         if key not in self._ytab:
-            aff = bn.g1_aff_tensor(self.y_distinct, device)
+            aff = self._y_aff.index_select(0, torch.from_numpy(self._y_first.astype(np.int64)).to(
+                self._y_aff.device)).to(device).contiguous()
             self._ytab[key] = (nt.g1_fb_table(aff), torch.tensor(self.y_slot, dtype=torch.int32, device=device))
         return self._ytab[key]
 

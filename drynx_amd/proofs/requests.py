@@ -839,7 +839,56 @@ def verify_range_pool_part(reqs: list, vn_idxs: dict, sq, device, cache: Verifie
 _SEG_MAX = 64  # attribution segments per batch (more requests: chunks of requests)
 
 
+def _u_cap() -> int:
+    """Pairing-side U points (verifiers x proofs x servers) per verification
+    batch: a batch's working set is ~17 KB of Miller-loop line coefficients
+    per U plus the G2 joint tables of its V's, so a million-value range
+    (3 x 10M U's per VN) is checked in batches that fit HBM
+    (DRYNX_VERIFY_CHUNK_U; the headline inbox, 186k U's, is one batch)."""
+    return int(os.environ.get("DRYNX_VERIFY_CHUNK_U", 3 << 20))
+
+
+def _item_chunks(live: list, parts: dict, n_vn: int) -> list:
+    """``live`` / ``parts`` cut into batches of at most ``_u_cap`` U points
+    (a list longer than that is split by proof ranges) -> [(live, parts)]."""
+    cap = max(1, _u_cap() // max(1, n_vn))
+    tot = sum(len(r) * r.S for i in live for r in parts[i])
+    if tot <= cap:
+        return [(live, parts)]
+    out, cur, cur_n = [], {}, 0
+    for i in live:
+        for r in parts[i]:
+            per = max(1, r.S)
+            a = 0
+            while a < len(r):
+                take = min(len(r) - a, max(1, (cap - cur_n) // per))
+                cur.setdefault(i, []).append(r if (a, take) == (0, len(r)) else rp.rpl_range(r, a, a + take))
+                cur_n += take * per
+                a += take
+                if cur_n >= cap:
+                    out.append(cur)
+                    cur, cur_n = {}, 0
+    if cur:
+        out.append(cur)
+    return [(list(c), c) for c in out]
+
+
 def _bad_requests(live, parts, sigmat, P, device, mode, coins_list) -> list:
+    """``_bad_requests_batch`` over batches of at most ``_u_cap`` U points
+    (each with fresh weights from every VN's coins); a request is bad for a
+    VN when any of its pieces is."""
+    chunks = _item_chunks(live, parts, len(coins_list))
+    if len(chunks) == 1:
+        return _bad_requests_batch(live, parts, sigmat, P, device, mode, coins_list)
+    bad = [set() for _ in coins_list]
+    for k, (cl, cp) in enumerate(chunks):
+        with timers.span(f"rp.verify.chunk[{k}/{len(chunks)}]"):
+            for b, more in zip(bad, _bad_requests_batch(cl, cp, sigmat, P, device, mode, coins_list)):
+                b |= more
+    return bad
+
+
+def _bad_requests_batch(live, parts, sigmat, P, device, mode, coins_list) -> list:
     """The requests of ``live`` each VN rejects -> [set] per VN.  One batch
     per (u, l, S) group with per-request attribution (rp.verify_range_proof_
     list_multi ``segs``): a passing batch clears everything at once; a
@@ -894,7 +943,7 @@ def _bad_requests(live, parts, sigmat, P, device, mode, coins_list) -> list:
         return [set(int(i) for i in live) for _ in range(n_vn)]
     recheck -= set().union(*bad, *unsure)
     if recheck:  # the decodable requests of a batch that held undecodable ones
-        for b, more in zip(bad, _bad_requests(sorted(recheck), parts, sigmat, P, device, mode, coins_list)):
+        for b, more in zip(bad, _bad_requests_batch(sorted(recheck), parts, sigmat, P, device, mode, coins_list)):
             b |= more
     for k in range(n_vn):
         rest = sorted(unsure[k] - bad[k])

@@ -336,3 +336,27 @@ def test_per_party_timers(env):
         assert rec[f"{vn.id}_VerifyRange"]["n"] >= 1
         assert f"{vn.id}_VerifyKeySwitch" in rec
     assert not node.take_proof_starts(sq.SurveyID)  # consumed at the feedback point
+
+
+def test_range_batches_chunked_by_u_cap(tmp_path, monkeypatch):
+    """Inboxes above DRYNX_VERIFY_CHUNK_U pairing-side points are verified in
+    several batches (a list split across batches by proof ranges): honest
+    lists still pass and a forged one is still blamed exactly."""
+    from drynx_amd.proofs import requests as prq_mod
+    from drynx_amd.utils.faults import FaultPlan
+
+    monkeypatch.setenv("DRYNX_VERIFY_CHUNK_U", "40")  # 2 VNs x 20: lists of 8 proofs x 3 servers split
+    seen = []
+    orig = prq_mod._item_chunks
+    monkeypatch.setattr(prq_mod, "_item_chunks", lambda *a: seen.append(len(orig(*a))) or orig(*a))
+    cl, node = local_cluster(3, 3, 2, device="cpu", workdir=str(tmp_path))
+    client = DrynxClient(node)
+    node.fault_plan = FaultPlan({("dp1", "range"): "corrupt_proof"})
+    sq = make_survey(client, cl, "frequencyCount", query_min=0, query_max=7, rows=4, proofs=1, ranges=[4, 2])
+    _, _, res = client.send_survey_query(sq)
+    codes = res.block.data_block().Proofs
+    by = lambda frag: {v for k, v in codes.items() if frag in k}  # noqa: E731
+    assert max(seen) > 2
+    assert by("/range/dp1/") == {prq.PROOF_FALSE}
+    assert by("/range/dp0/") == by("/range/dp2/") == {prq.PROOF_TRUE}
+    node.close(remove=True)
