@@ -251,6 +251,24 @@ def scalars_from_bytes(b, device="cpu") -> torch.Tensor:
     return nt.fr_arith(nt.FR_REDUCE, t)
 
 
+# ----------------------------------------------------------------------------- shared device caches
+def publish(*objs):
+    """Before a lazily built device object goes into a cache other threads
+    read: wait until its build has landed.  The build (kernels, asynchronous
+    pinned uploads) was queued on the building thread's current stream; a
+    reader on another stream would otherwise launch on the half-built table
+    (no stream orders the two).  One synchronisation per cache entry."""
+    seen = set()
+    for o in objs:
+        ts = [o] if isinstance(o, torch.Tensor) else [v for v in (vars(o).values() if hasattr(o, "__dict__") else o)
+                                                      if isinstance(v, torch.Tensor)]
+        for t in ts:
+            if t.is_cuda and t.device not in seen:
+                seen.add(t.device)
+                torch.cuda.current_stream(t.device).synchronize()
+    return objs[0] if len(objs) == 1 else objs
+
+
 # ----------------------------------------------------------------------------- generator tables
 _tables: dict = {}
 _tlock = threading.Lock()
@@ -276,7 +294,7 @@ def base_table(device="cpu") -> torch.Tensor:
     k = ("B", _dev_key(device))
     with _tlock:
         if k not in _tables:
-            _tables[k] = nt.g1_fb_table(g1_generator_aff(device))
+            _tables[k] = publish(nt.g1_fb_table(g1_generator_aff(device)))
         return _tables[k]
 
 
@@ -284,7 +302,7 @@ def base2_table(device="cpu") -> torch.Tensor:
     k = ("B2", _dev_key(device))
     with _tlock:
         if k not in _tables:
-            _tables[k] = nt.g2_fb_table(g2_generator_aff(device))
+            _tables[k] = publish(nt.g2_fb_table(g2_generator_aff(device)))
         return _tables[k]
 
 

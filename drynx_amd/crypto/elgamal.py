@@ -156,8 +156,12 @@ def pk_table(public_point, device="cpu") -> PublicKeyTable:
     t = _pk_cache.get(key)
     if t is None:
         if len(_pk_cache) > 64:
+            # tables of other keys may still be read by queued kernels of any
+            # stream: the device drains before their memory goes back
+            if torch.cuda.is_available() and torch.cuda.is_initialized():
+                torch.cuda.synchronize()
             _pk_cache.clear()
-        t = _pk_cache[key] = PublicKeyTable(public_point, device)
+        t = _pk_cache[key] = bn.publish(PublicKeyTable(public_point, device))
     return t
 
 
@@ -241,7 +245,7 @@ def decryption_table(bound: int = 10000, device="cpu") -> DecryptionTable:
     key = (int(bound), str(torch.device(device)))
     t = _dt_cache.get(key)
     if t is None:
-        t = _dt_cache[key] = DecryptionTable(bound, device)
+        t = _dt_cache[key] = bn.publish(DecryptionTable(bound, device))
     return t
 
 

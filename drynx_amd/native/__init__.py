@@ -1414,7 +1414,7 @@ def _glv_const(kind: str, device) -> torch.Tensor:
             v = _bn.to_tensor(_bn.ints_to_limbs([_bn.mont(GLV_BETA)]), device)
         else:
             v = _bn.to_tensor(_bn.ints_to_limbs([GLV_LAMBDA]), device)
-        _glv_consts[key] = v.contiguous()
+        _glv_consts[key] = _bn.publish(v.contiguous())
     return _glv_consts[key]
 
 
@@ -1881,6 +1881,59 @@ def multi_exp_grouped_finish(h) -> torch.Tensor:
 # host, so every pass is queued at once behind the sort.
 
 _DPLANS: dict = {}
+_PLAN_LIMIT = 32
+
+
+def _layout_tensors(lay: dict):
+    for k, v in lay.items():
+        if isinstance(v, torch.Tensor):
+            yield v
+        elif k == "passes":
+            for st, ln in v:
+                yield st
+                yield ln
+
+
+def _mark_use(lay: dict, dev):
+    """A cached layout is read by kernels of whatever stream the caller is on;
+    its tensors were allocated on the stream that built it.  Every new user
+    stream is recorded on them (``record_stream``), so when the cache evicts
+    the layout the caching allocator hands its blocks out again only after
+    every such stream has passed its last use -- without this an eviction
+    while another stream's kernels still read the layout let the building
+    stream reuse the memory under them (profiles/r6/graph_fault.md).  A HIP
+    graph being captured keeps the layout itself (``capture_keep``): a
+    captured launch reads it at every replay, long after any eviction."""
+    keep = getattr(_CAPTURE, "keep", None)
+    if keep is not None:
+        keep.append(lay)
+    if dev.type != "cuda":
+        return
+    s = torch.cuda.current_stream(dev)
+    seen = lay.setdefault("_streams", set())
+    if s.stream_id not in seen:
+        seen.add(s.stream_id)
+        for t in _layout_tensors(lay):
+            t.record_stream(s)
+
+
+_CAPTURE = threading.local()
+
+
+class capture_keep:
+    """Inside a HIP graph capture on this thread: collects every cached device
+    object the captured launches read (``_mark_use``) into ``self.items``;
+    the graph must hold them for its lifetime."""
+
+    def __enter__(self):
+        self.prev = getattr(_CAPTURE, "keep", None)
+        self.items = []
+        _CAPTURE.keep = self.items
+        return self
+
+    def __exit__(self, *a):
+        _CAPTURE.keep = self.prev
+        return False
 
 
 def _device_layout(groups: tuple, W: int, c: int, sl: int, dev) -> dict:
@@ -1893,6 +1946,7 @@ def _device_layout(groups: tuple, W: int, c: int, sl: int, dev) -> dict:
     key = (groups, W, c, sl, str(dev))
     lay = _DPLANS.get(key)
     if lay is not None:
+        _mark_use(lay, dev)
         return lay
     D = 1 << c
     nb = len(groups) * W * D
@@ -1928,9 +1982,12 @@ def _device_layout(groups: tuple, W: int, c: int, sl: int, dev) -> dict:
            "first_lane": up(off, np.int64), "multi": up(multi, np.int64),
            "passes": [(up(st, np.int64), up(ln, np.int32)) for st, ln in passes],
            "used_t": up(ubk, np.int64), "unused_t": up(np.flatnonzero(~used), np.int64)}
-    if len(_DPLANS) > 32:  # least recently built first (HIP graphs keep their own references)
+    if dev.type == "cuda":  # uploaded on this stream; readers on others must not see it half-copied
+        torch.cuda.current_stream(dev).synchronize()
+    while len(_DPLANS) > _PLAN_LIMIT:  # least recently built first (see ``_mark_use`` for why that is safe)
         _DPLANS.pop(next(iter(_DPLANS)))
     _DPLANS[key] = lay
+    _mark_use(lay, dev)
     return lay
 
 
@@ -2393,7 +2450,7 @@ def gt_one(device) -> torch.Tensor:
 
         t = _np.zeros((1, 96), dtype=_np.uint32)
         t[0, :8] = _bn.ints_to_limbs([_bn.mont(1)])[0]
-        _gt_one_cache[key] = _bn.to_tensor(t, device)
+        _gt_one_cache[key] = _bn.publish(_bn.to_tensor(t, device))
     return _gt_one_cache[key]
 
 

@@ -10,15 +10,21 @@ Reference: lib/range/range_proof.go
     D 64 B, V 128 B, A 384 B, Commit 128 B).
 
 MI355X design (all lists of proofs are processed as ONE batch on the device):
-  prove : a_ij = FE(ML(-s_j B, V_ij)) * gT^{t_j} with a comb table for
-          gT = e(B, B2) (fused kernel dx_rp_prove_a); D = (sum u^j s_j) B +
+  prove : table-driven -- V = v A_phi from G2 comb / GLS tables of the
+          signature points and a = e(B, A_phi)^{-s v} gT^t from GT tables
+          (``SigMaterial.table_mode``: no pairing per item); without tables
+          (too many distinct points for HBM) a_ij = FE(ML(-s_j B, V_ij)) *
+          gT^{t_j} (fused kernel dx_rp_prove_a).  D = (sum u^j s_j) B +
           (sum m_j) P by two fixed-base mults; all Fr arithmetic on device.
-  verify: D-check folded to c*C + Zr*P + (sum_j Zphi_j u^j)*B per proof, and
-          the l*S pairing equations of every proof in the list combined with
-          random 64-bit weights rho: one Miller loop per (proof, server,
-          digit) + ONE final exponentiation per list (dx_rp_verify_items).
-          The reference's AND over the list (:497-500) makes this exact up
-          to a 2^-64 soundness error.
+  verify: the l*S pairing equations of every proof of the batch combined
+          with each verifier's random GLV weights rho and regrouped by
+          bilinearity (``verify_range_proof_list_multi``, dx_rpmsm.hip):
+          e(B, R) prod_(p,i) e(-c_p y_pi, U_pi) with R one G2 MSM and U_pi
+          the l-digit combinations -- n*S + 1 Miller loops per verifier and
+          one final exponentiation; the prod a^rho side is a GT bucket
+          multi-exponentiation, the D-equations one MSM.  The reference's
+          AND over the list (:497-500) makes this exact up to a 2^-64
+          soundness error; a failing batch is attributed per request.
 
 Extension (documented): ranges may carry a third element ``offset``; the
 proof then shows m + offset in [0, u^l) (signed values such as logistic-
@@ -212,7 +218,7 @@ class SigMaterial:
         if key not in self._ytab:
             b = np.frombuffer(O.g1_to_bytes(O.G1_GEN), dtype="<i4").copy()
             y = np.ascontiguousarray(self._ysum).view("<i4").reshape(-1, 16).copy()
-            self._ytab[key] = (torch.from_numpy(b).to(device), torch.from_numpy(y).to(device))
+            self._ytab[key] = bn.publish(torch.from_numpy(b).to(device), torch.from_numpy(y).to(device))
         return self._ytab[key]
 
     def y_tables(self, device):
@@ -230,7 +236,8 @@ class SigMaterial:
         if key not in self._ytab:
             aff = self._y_aff.index_select(0, torch.from_numpy(self._y_first.astype(np.int64)).to(
                 self._y_aff.device)).to(device).contiguous()
-            self._ytab[key] = (nt.g1_fb_table(aff), torch.tensor(self.y_slot, dtype=torch.int32, device=device))
+            self._ytab[key] = bn.publish(nt.g1_fb_table(aff), torch.tensor(self.y_slot, dtype=torch.int32,
+                                                                             device=device))
         return self._ytab[key]
 
     def attach_shard(self, comm, every_rank_proves: bool):
@@ -375,7 +382,7 @@ class SigMaterial:
                         if b > a:
                             shard.broadcast_into(g2[a * E: b * E], r)
                             shard.broadcast_into(gt[a * E: b * E], r)
-            self._ptab[key] = (g2, gt, slot.to(dev))
+            self._ptab[key] = bn.publish(g2, gt, slot.to(dev))
         return self._ptab[key]
 
     def prover_tables(self, a_idx: torch.Tensor, device, n_items: int | None = None):
@@ -406,6 +413,7 @@ class SigMaterial:
             gt = nt.gt_fb_table(gphi)
             cache["g2"] = g2 if cache["g2"] is None else torch.cat([cache["g2"], g2])
             cache["gt"] = gt if cache["gt"] is None else torch.cat([cache["gt"], gt])
+            bn.publish(cache["g2"], cache["gt"])
             for m in missing:
                 cache["pos"][m] = len(cache["idx"])
                 cache["idx"].append(m)
@@ -421,7 +429,7 @@ def gt_generator_table(device="cpu"):
     key = str(torch.device(device))
     if key not in _gt_cache:
         gT = nt.pairing(bn.g1_generator_aff(device), bn.g2_generator_aff(device))
-        _gt_cache[key] = (gT, nt.gt_fb_table(gT))
+        _gt_cache[key] = bn.publish(gT, nt.gt_fb_table(gT))
     return _gt_cache[key]
 
 
@@ -599,7 +607,7 @@ def _powers(u: int, l: int, device) -> torch.Tensor:
     key = (u, l, str(torch.device(device)))
     t = _pow_cache.get(key)
     if t is None:
-        t = _pow_cache[key] = bn.scalars_tensor([pow(u, j, O.R) for j in range(l)], device)
+        t = _pow_cache[key] = bn.publish(bn.scalars_tensor([pow(u, j, O.R) for j in range(l)], device))
     return t
 
 

@@ -24,6 +24,7 @@ from typing import Any
 import numpy as np
 import torch
 
+from ..crypto import bn254 as bn
 from ..crypto import digest as payload_digest
 from ..query import ivsigs_digest
 from ..utils import timers
@@ -491,8 +492,12 @@ class VerifierCache:
         key = (ivsigs_digest(sigs), len(sigs), len(sigs[0]) if sigs else 0, str(device))
         if key not in self._sig:
             if len(self._sig) > 8:
+                # another set's tables may still be read by queued kernels of
+                # any stream: the device drains before their memory goes back
+                if torch.device(device).type == "cuda":
+                    torch.cuda.synchronize(device)
                 self._sig.clear()
-            self._sig[key] = rp.SigMaterial(sigs, device)
+            self._sig[key] = bn.publish(rp.SigMaterial(sigs, device))
         return self._sig[key]
 
 

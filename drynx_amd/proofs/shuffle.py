@@ -63,7 +63,7 @@ def generators(n: int, device) -> torch.Tensor:
     cur = _gen_cache.get(key)
     if cur is None or cur.shape[0] < n + 1:
         m = max(n + 1, 2 * (cur.shape[0] if cur is not None else 0), 64)
-        _gen_cache[key] = cur = nt.g1_from_affine(nt.hash_to_g1(SEED, 0, m, dev))
+        _gen_cache[key] = cur = bn.publish(nt.g1_from_affine(nt.hash_to_g1(SEED, 0, m, dev)))
     return cur[: n + 1]
 
 

@@ -49,7 +49,7 @@ def executor(device=None, max_workers: int = 1, name: str = "drynx"):
 
     dev = torch.device(device) if device is not None else None
     init = None
-    if dev is not None and dev.type == "cuda":
+    if dev is not None and dev.type == "cuda" and os.environ.get("DRYNX_PIN_WORKERS", "1") != "0":
         idx = dev.index if dev.index is not None else torch.cuda.current_device()
 
         def init():
