@@ -134,7 +134,8 @@ class DistComm(Comm):
         # host memory for gloo (whose all-to-all is CPU only)
         self._stage = self.device if self.backend == "nccl" else torch.device("cpu")
         # control groups of the side planes (created by every rank, in this order)
-        self._planes = {name: _CtrlPlane(self, dist.new_group(backend="gloo")) for name in ("pool",)}
+        # ("pool2": the second stage of a staged range plane, proof_collection.extend_range_plane)
+        self._planes = {name: _CtrlPlane(self, dist.new_group(backend="gloo")) for name in ("pool", "pool2")}
 
     def plane(self, name: str) -> "Comm":
         return self._planes[name]

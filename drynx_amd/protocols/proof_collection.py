@@ -152,7 +152,7 @@ def groups_of(ctx, sq) -> tuple:
     return dict(zip(ids, groups)), dict(zip(ids, parts))
 
 
-def fan_out(ctx, sq, local_requests: list, pool: bool = False) -> list:
+def fan_out(ctx, sq, local_requests: list, pool: bool = False, stage: int = 0) -> list:
     """Every request to the ranks that host a VN; with ``pool`` (the range
     plane: ``verification_groups``), a helper rank gets only ITS slice of
     every range bundle its VN(s) may check (~1/group of the payload) plus the
@@ -178,7 +178,7 @@ def fan_out(ctx, sq, local_requests: list, pool: bool = False) -> list:
         # exchange (no control round of its own): helper k derives that VN's
         # coins for its slice from it
         seeds = {vn.id: ctx.vn_coins(vn.id).seed() for vn in vns if vn.rank == ctx.rank}
-        ctx.__dict__.setdefault("_pool_seeds", {})[sq.SurveyID] = dict(seeds)
+        ctx.__dict__.setdefault("_pool_seeds", {})[(sq.SurveyID, stage)] = dict(seeds)
         if len(ctx._pool_seeds) > 64:
             ctx._pool_seeds.pop(next(iter(ctx._pool_seeds)))
     if W == 1:
@@ -226,7 +226,7 @@ def fan_out(ctx, sq, local_requests: list, pool: bool = False) -> list:
     wires = {src: m["w"] for src, m in msgs.items()}
     if pool:
         for m in msgs.values():
-            ctx._pool_seeds[sq.SurveyID].update(m["seeds"])
+            ctx._pool_seeds[(sq.SurveyID, stage)].update(m["seeds"])
     tens = {d: t for d, t in zip([d for d in dests if per_rank_t[d]],
                                   nt.cat_rows([per_rank_t[d] for d in dests if per_rank_t[d]]))}
     # the envelopes announced every tensor's size: no size round for the payloads
@@ -263,7 +263,8 @@ def _pkey(part) -> str:
     return ",".join(str(int(x)) for x in part)
 
 
-def pool_verify_ranges(ctx, sq, reqs: list, vns: list, comm=None, arrived: float | None = None) -> dict:
+def pool_verify_ranges(ctx, sq, reqs: list, vns: list, comm=None, arrived: float | None = None, stage: int = 0,
+                       record: bool = True, second=None) -> dict:
     """Range verification through the verification groups (see
     ``verification_mode``).  Each VN's rank decides that VN's sampling
     (reference ``rand.Float64() <= Threshold``, from the VN's own coins, or
@@ -276,16 +277,30 @@ def pool_verify_ranges(ctx, sq, reqs: list, vns: list, comm=None, arrived: float
     need no gather.  ``<vn>_VerifyRange`` (structs_proofs.go:137) runs from
     ``arrived`` (the VN's inbox: the range fan-out's end on its rank) to that
     VN's own verdict (after its digest checks and any slice it re-checked).
+    ``second``: a Future of the staged plane's second batch's local part
+    (``_pool_local`` on another worker): both batches' results travel in ONE
+    gather and the verdicts cover both.
     -> {vn_id: {base_key: None (not sampled) | bool}} for the VNs of this rank."""
     comm = comm or ctx.comm
-    W, k = comm.world, comm.rank
+    t0 = arrived if arrived is not None else time.perf_counter()
+    states = [_pool_local(ctx, sq, reqs, vns, comm.rank, comm.world, stage)]
+    if second is not None:
+        with timers.span("rp.verify.pool_second"):
+            states.append(second.result(timeout=float(os.environ.get("DRYNX_STAGE_WAIT_S", "120"))))
+    return _pool_finish(ctx, sq, states, comm, t0, record)
+
+
+def _pool_local(ctx, sq, reqs: list, vns: list, k: int, W: int, stage: int) -> dict:
+    """This rank's share of one batch of a pooled verification: its slices
+    checked for the VNs whose group holds it, their digests, and (a VN's
+    rank) its sampling and the digests of its helpers' slices (queued)."""
     rng = [i for i, r in enumerate(reqs) if r.kind == "range" and not r.header_only]
     groups, gparts = groups_of(ctx, sq)
     # every VN's seed arrived with the fan-out; the helpers check every list a
     # VN may sample (the sharding extension's assignment is public; a random
     # Threshold sample stays the VN's own decision, applied to the verdicts
     # below) -- no control round before the checks
-    seeds = getattr(ctx, "_pool_seeds", {}).pop(sq.SurveyID, {})
+    seeds = getattr(ctx, "_pool_seeds", {}).pop((sq.SurveyID, stage), {})
     serve = [vn for vn in vns if k in groups[vn.id]]  # the VNs this rank checks a slice for
     missing = [vn.id for vn in serve if vn.id not in seeds]
     if missing:
@@ -297,7 +312,6 @@ def pool_verify_ranges(ctx, sq, reqs: list, vns: list, comm=None, arrived: float
     vn_idxs = {vn.id: [i for i in rng if may_check(i, vi)] for vi, vn in enumerate(vns)}
     sampled = {vn.id: {reqs[i].base_key(): prq.should_verify(sq, reqs[i], vi, len(vns), ctx.vn_coins(vn.id))
                        for i in rng} for vi, vn in enumerate(vns) if vn.rank == ctx.rank}
-    t0 = arrived if arrived is not None else time.perf_counter()
     local_vns = [vn for vn in vns if vn.rank == ctx.rank]
     helped = [vn for vn in local_vns if len(groups[vn.id]) > 1]
     # a VN rank's digests of its helpers' slices of its own payloads run beside
@@ -320,40 +334,57 @@ def pool_verify_ranges(ctx, sq, reqs: list, vns: list, comm=None, arrived: float
         if hasattr(digests, "result"):
             digests = digests.result()
         mydig[_pkey(part)] = {reqs[i].base_key(): d for i, d in digests.items()}
+    return {"reqs": reqs, "vn_idxs": vn_idxs, "sampled": sampled, "helped": helped, "exp_f": exp_f,
+            "mine": mine, "mydig": mydig, "groups": groups, "gparts": gparts, "local_vns": local_vns}
+
+
+def _pool_finish(ctx, sq, states: list, comm, t0: float, record: bool) -> dict:
+    """One gather of every batch's (verdicts, slice digests), then each local
+    VN's verdicts: helper verdicts bound to its own digests of their slices,
+    mismatching slices re-checked, unsampled lists left None."""
+    k = comm.rank
+    groups = states[0]["groups"]
+    payload = [(s["mine"], s["mydig"]) for s in states]
     if any(len(g) > 1 for g in groups.values()):
-        gathered = comm.all_gather_object((mine, mydig))
+        gathered = comm.all_gather_object(payload)
     else:  # every VN checks alone on its own rank: nothing to gather
-        gathered = {k: (mine, mydig)}
-    out = {}
-    if helped:
-        trusted = _check_helper_digests(ctx, sq, reqs, vn_idxs, helped, gathered, groups, gparts, exp_f.result())
-    for vn in local_vns:
-        g = groups[vn.id]
-        tr = trusted[vn.id] if len(g) > 1 else {}
-        verdict = {}
-        for key, smp in sampled[vn.id].items():
-            if not smp:
-                verdict[key] = None
-                continue
-            verdict[key] = all(gathered[j][0][vn.id].get(key, False) for j in g
-                               if j == k or (key, j) in tr)
-        # slices whose helper digest did not match: this VN checks them itself
-        # (only lists this VN sampled: an unsampled one keeps None = code 2,
-        # whatever a helper reported for it)
-        redo = {j: [i for i in idxs if sampled[vn.id].get(reqs[i].base_key())]
-                for j, idxs in tr.get("redo", {}).items()}
-        redo = {j: idxs for j, idxs in redo.items() if idxs}
-        if redo:
-            with timers.span("rp.verify.pool_redo"):
-                c = ctx.vn_coins(vn.id)
-                for j, idxs in redo.items():
-                    r2, _ = prq.verify_range_pool_part(reqs, {vn.id: idxs}, sq, ctx.device, ctx.verifier_cache,
-                                                       gparts[vn.id][j], {vn.id: c})
-                    for i, ok in r2[vn.id].items():
-                        key = reqs[i].base_key()
-                        verdict[key] = bool(verdict.get(key)) and bool(ok)
-        out[vn.id] = verdict
-        timers.record(f"{vn.id}_VerifyRange", time.perf_counter() - t0)
+        gathered = {k: payload}
+    out: dict = {}
+    for si, st in enumerate(states):
+        reqs, vn_idxs, sampled, gparts = st["reqs"], st["vn_idxs"], st["sampled"], st["gparts"]
+        got = {j: gathered[j][si] for j in (gathered if isinstance(gathered, dict) else range(len(gathered)))}
+        trusted = {}
+        if st["helped"]:
+            trusted = _check_helper_digests(ctx, sq, reqs, vn_idxs, st["helped"], got, groups, gparts,
+                                            st["exp_f"].result())
+        for vn in st["local_vns"]:
+            g = groups[vn.id]
+            tr = trusted[vn.id] if len(g) > 1 else {}
+            verdict = {}
+            for key, smp in sampled[vn.id].items():
+                if not smp:
+                    verdict[key] = None
+                    continue
+                verdict[key] = all(got[j][0][vn.id].get(key, False) for j in g if j == k or (key, j) in tr)
+            # slices whose helper digest did not match: this VN checks them itself
+            # (only lists this VN sampled: an unsampled one keeps None = code 2,
+            # whatever a helper reported for it)
+            redo = {j: [i for i in idxs if sampled[vn.id].get(reqs[i].base_key())]
+                    for j, idxs in tr.get("redo", {}).items()}
+            redo = {j: idxs for j, idxs in redo.items() if idxs}
+            if redo:
+                with timers.span("rp.verify.pool_redo"):
+                    c = ctx.vn_coins(vn.id)
+                    for j, idxs in redo.items():
+                        r2, _ = prq.verify_range_pool_part(reqs, {vn.id: idxs}, sq, ctx.device, ctx.verifier_cache,
+                                                           gparts[vn.id][j], {vn.id: c})
+                        for i, ok in r2[vn.id].items():
+                            key = reqs[i].base_key()
+                            verdict[key] = bool(verdict.get(key)) and bool(ok)
+            out.setdefault(vn.id, {}).update(verdict)
+    if record:
+        for vn in states[0]["local_vns"]:
+            timers.record(f"{vn.id}_VerifyRange", time.perf_counter() - t0)
     return out
 
 
@@ -368,9 +399,12 @@ def _expected_async(ctx, sq, reqs, vn_idxs: dict, local_vns: list, groups: dict,
         return _expected_digests(ctx, sq, reqs, vn_idxs, local_vns, groups, gparts)
     if ctx.device.type != "cuda":
         return rp.add_idle_task(rp.Deferred(work))
-    if not hasattr(ctx, "_dig_stream"):
-        ctx._dig_stream = torch.cuda.Stream(ctx.device)
-    st, cur = ctx._dig_stream, torch.cuda.current_stream(ctx.device)
+    # one digest stream per pool thread (a staged range plane runs two)
+    dstreams = ctx.__dict__.setdefault("_dig_streams", {})
+    tid = __import__("threading").get_ident()
+    if tid not in dstreams:
+        dstreams[tid] = torch.cuda.Stream(ctx.device)
+    st, cur = dstreams[tid], torch.cuda.current_stream(ctx.device)
     st.wait_stream(cur)
 
     def run():
@@ -440,16 +474,17 @@ def _check_helper_digests(ctx, sq, reqs, vn_idxs: dict, local_vns: list, gathere
     return out
 
 
-def _pool_async(ctx, sq, reqs, vns, comm=None):
+def _pool_async(ctx, sq, reqs, vns, comm=None, second=None):
     """pool_verify_ranges on a worker thread with its own HIP stream: the
     range batches (the GPU's long pole) run while this thread checks the
     short per-CN proofs of each VN.  On a multi-rank node the worker also
-    owns the pool's collectives (the main thread issues none meanwhile)."""
+    owns the pool's collectives (the main thread issues none meanwhile).
+    ``second``: see ``pool_verify_ranges`` (a staged range plane)."""
     if not hasattr(ctx, "_pool_exec"):
         ctx._pool_exec = streams.executor(ctx.device, 1, "drynx-vn-pool")
     arrived = time.perf_counter()  # the fan-out just delivered the VNs' inboxes
     if ctx.device.type != "cuda":
-        return ctx._pool_exec.submit(pool_verify_ranges, ctx, sq, reqs, vns, comm, arrived)
+        return ctx._pool_exec.submit(pool_verify_ranges, ctx, sq, reqs, vns, comm, arrived, 0, True, second)
     if not hasattr(ctx, "_pool_stream"):
         ctx._pool_stream = torch.cuda.Stream(ctx.device, priority=streams.priority(POOL_PRIORITY))
     side, main = ctx._pool_stream, torch.cuda.current_stream(ctx.device)
@@ -457,11 +492,36 @@ def _pool_async(ctx, sq, reqs, vns, comm=None):
 
     def run():
         with torch.cuda.stream(side):
-            out = pool_verify_ranges(ctx, sq, reqs, vns, comm, arrived)
+            out = pool_verify_ranges(ctx, sq, reqs, vns, comm, arrived, 0, True, second)
         side.synchronize()
         return out
 
     return ctx._pool_exec.submit(run)
+
+
+def _pool_local_async(ctx, sq, reqs, vns, stage: int):
+    """``_pool_local`` of a staged plane's later batch on a second worker and
+    HIP stream (no collectives: its results go out in the first batch's
+    gather) -> Future of its state."""
+    if not hasattr(ctx, "_pool_exec2"):
+        ctx._pool_exec2 = streams.executor(ctx.device, 1, "drynx-vn-pool2")
+    k, W = ctx.comm.rank, ctx.comm.world
+    if ctx.device.type != "cuda":
+        return ctx._pool_exec2.submit(_pool_local, ctx, sq, reqs, vns, k, W, stage)
+    if not hasattr(ctx, "_pool_stream2"):
+        ctx._pool_stream2 = torch.cuda.Stream(ctx.device, priority=streams.priority(POOL_PRIORITY))
+    side, main = ctx._pool_stream2, torch.cuda.current_stream(ctx.device)
+    side.wait_stream(main)
+
+    def run():
+        with torch.cuda.stream(side):
+            st = _pool_local(ctx, sq, reqs, vns, k, W, stage)
+            if st["exp_f"] is not None:  # the helper digests are queued on this thread: compute them here
+                st["exp_f"].result()
+        side.synchronize()
+        return st
+
+    return ctx._pool_exec2.submit(run)
 
 
 def verify_and_store(ctx, sq, vn, vn_index: int, n_vns: int, requests: list, range_pooled=None) -> dict:
@@ -501,17 +561,28 @@ def store_verdicts(ctx, sq, vn, requests: list, pending) -> dict:
     return bitmap
 
 
-def start_range_plane(ctx, sq, range_requests: list) -> dict:
+def start_range_plane(ctx, sq, range_requests: list, staged: bool = False) -> dict:
     """The range-proof plane, started as soon as this rank's range proofs are
     signed (the reference streams them to the VNs while the CNs aggregate,
     data_collection_protocol.go:278-348): their fan-out on the data plane
     (main thread: every RCCL collective stays on one thread), then the pooled
     verification on a worker with its own HIP stream and its own control
-    group (``Comm.plane("pool")``), overlapping the CN phases."""
+    group (``Comm.plane("pool")``), overlapping the CN phases.  ``staged``:
+    a second batch follows (``extend_range_plane``); the first batch's worker
+    waits for that batch's local part and gathers both at once."""
+    import concurrent.futures as cf
+
     vns = [ctx.cluster.by_id(si.id) for si in sq.Query.RosterVNs.list]
     with timers.timed("RangeFanOut"):
         reqs = fan_out(ctx, sq, range_requests, pool=True)
-    out = {"reqs": reqs, "pooled": _pool_async(ctx, sq, reqs, vns, ctx.comm.plane("pool"))}
+    second = cf.Future() if staged else None
+    out = {"reqs": reqs, "pooled": _pool_async(ctx, sq, reqs, vns, ctx.comm.plane("pool"), second),
+           "second_state": second}
+    _prefetch_range(ctx, sq, reqs, vns)
+    return out
+
+
+def _prefetch_range(ctx, sq, reqs, vns):
     if any(vn.rank == ctx.rank for vn in vns) and hasattr(ctx, "ledger_values"):
         # the stored payloads' device-to-host copy starts now, under the pooled
         # verification, instead of at the verdicts (store_verdicts finds them
@@ -519,7 +590,46 @@ def start_range_plane(ctx, sq, range_requests: list) -> dict:
         # (received ones: a digest here would wait for the exchange) go then
         with timers.span("ledger.prefetch"):
             ctx.ledger_values([r for r in reqs if r.kind == "range" and r.data_digest], range_shape(sq))
-    return out
+
+
+def range_stages(ctx, sq) -> int:
+    """How many DPs of each rank prove in the range plane's FIRST batch, or 0
+    for one batch.  With DPs spread unevenly over the ranks (10 DPs on 8
+    GPUs: two ranks prove two), a single fan-out waits for the slowest
+    prover and every pool part starts late; staged, the first exchange
+    carries every rank's first min(DPs per rank) DPs, the pool parts start on
+    it, and the rest follows in a second exchange whose batch verifies
+    concurrently (the reference streams each DP's proofs as they are made,
+    data_collection_protocol.go:278-348).  A function of the placement:
+    identical on every rank.  DRYNX_RANGE_STAGES=0 keeps one batch."""
+    W = ctx.comm.world
+    if W <= 1 or os.environ.get("DRYNX_RANGE_STAGES", "1") == "0":
+        return 0
+    dps, _, _ = _placement(ctx, sq)
+    lo, hi = min(dps), max(dps)
+    return lo if 0 < lo < hi else 0
+
+
+def extend_range_plane(ctx, sq, early: dict, range_requests: list) -> dict:
+    """The second batch of a staged range plane (``range_stages``): its
+    fan-out (collective: every rank calls it, with or without requests of
+    its own), then its local part on a second worker and stream, concurrent
+    with the first batch's; ``early`` then holds both batches' requests."""
+    vns = [ctx.cluster.by_id(si.id) for si in sq.Query.RosterVNs.list]
+    with timers.timed("RangeFanOut2"):
+        reqs = fan_out(ctx, sq, range_requests, pool=True, stage=1)
+    fut = _pool_local_async(ctx, sq, reqs, vns, 1)
+    ph = early["second_state"]
+
+    def relay(f):
+        e = f.exception()
+        if e is not None:
+            ph.set_exception(e)
+        else:
+            ph.set_result(f.result())
+    fut.add_done_callback(relay)
+    _prefetch_range(ctx, sq, reqs, vns)
+    return {**early, "reqs": early["reqs"] + reqs, "second_state": None}
 
 
 def range_shape(sq):

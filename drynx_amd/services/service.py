@@ -337,7 +337,22 @@ class DrynxNode:
         # asynchronously, data_collection_protocol.go:278-348): proving is queued
         # on the GPU now, envelope marshalling + signing runs on a worker thread
         # while the CN phases below proceed
-        range_future = self._range_proofs_async(sq, dp_results) if q.Proofs else None
+        range_future = range_future2 = None
+        if q.Proofs:
+            # staged range plane (pcp.range_stages): the first min(DPs per
+            # rank) DPs of every rank fan out first, the rest in a second batch
+            m = pcp.range_stages(self, sq) if pcp.early_plane_ok(self, sq) else 0
+            if m:
+                items = list(dp_results.items())
+                range_future = self._range_proofs_async(sq, dict(items[:m]), staged=True)
+                range_future2 = self._range_proofs_async(sq, dict(items[m:]), staged=True) if items[m:] else None
+                if range_future2 is None:  # no second-stage DP here: the rank still joins that exchange
+                    import concurrent.futures as cf
+
+                    range_future2 = cf.Future()
+                    range_future2.set_result([])
+            else:
+                range_future = self._range_proofs_async(sq, dp_results)
         want = dcp.expected_n_out(sq)
         if dp_results:  # (a width that does not fit ``want`` aborted the route on every rank)
             n_out = len(next(iter(dp_results.values()))["cv"]) // n_groups
@@ -350,11 +365,17 @@ class DrynxNode:
             # the range-proof plane starts now, beside the CN phases
             with timers.span("range.plane.start"):
                 rreqs = range_future.result()
-                if hasattr(self, "_prove_stream"):
-                    torch.cuda.current_stream(self.device).wait_stream(self._prove_stream)
+                # the signed payloads are complete (a staged batch's signing
+                # waited for its own proving only: the prove stream may still
+                # run the second batch, which the exchange must not wait for)
+                src = "_sign_stream" if range_future2 is not None else "_prove_stream"
+                if hasattr(self, src):
+                    torch.cuda.current_stream(self.device).wait_stream(getattr(self, src))
                 if self.fault_plan:
                     self.fault_plan.apply(rreqs, lambda pid: self.cluster.by_id(pid).keypair.secret)
-                early = pcp.start_range_plane(self, sq, rreqs)
+                early = pcp.start_range_plane(self, sq, rreqs, staged=range_future2 is not None)
+                if range_future2 is not None:
+                    early["second"] = range_future2
             range_future = None
         # range proofs on the GPU during this query's CN phases and querier (``_side_stream``)
         self._range_active = bool(early is not None or range_future is not None) and \
@@ -424,6 +445,15 @@ class DrynxNode:
             return out
 
         block = None
+        if early is not None and "second" in early:
+            # the staged range plane's second batch (every rank: a collective)
+            with timers.span("range.plane.extend"):
+                rreqs2 = early.pop("second").result()
+                if hasattr(self, "_sign_stream"):
+                    torch.cuda.current_stream(self.device).wait_stream(self._sign_stream)
+                if self.fault_plan:
+                    self.fault_plan.apply(rreqs2, secret_of)
+                early = pcp.extend_range_plane(self, sq, early, rreqs2)
         if q.Proofs and q.RosterVNs is not None and len(q.RosterVNs.list):
             block = pcp.proof_collection(self, sq, proofs, early, late)
         elif late_f is not None:
@@ -641,7 +671,13 @@ class DrynxNode:
         secrets = [self.cluster.by_id(dp_id).keypair.secret for dp_id, _ in items]
         return prq.new_range_requests(items, sq.SurveyID, secrets, self.device)
 
-    def _range_proofs_async(self, sq, dp_results: dict):
+    def _range_proofs_async(self, sq, dp_results: dict, staged: bool = False):
+        """Prove the range proofs of ``dp_results`` on the prove stream and sign
+        them on the proof worker -> Future of the signed requests.
+        ``staged``: one of several batches queued back to back on the prove
+        stream; its signing then waits for ITS proving only (an event) and
+        runs on a stream of its own, so the first batch's envelopes do not
+        wait for the second batch's kernels."""
         import concurrent.futures as cf
 
         if not hasattr(self, "_pool"):
@@ -671,6 +707,22 @@ class DrynxNode:
         side.wait_stream(main)  # the DP ciphertexts / randomness are ready
         with torch.cuda.stream(side):
             proved = self._prove_range(sq, dp_results)
+        if staged:
+            done = torch.cuda.Event()
+            done.record(side)
+            if not hasattr(self, "_sign_stream"):
+                self._sign_stream = torch.cuda.Stream(self.device)
+            sst = self._sign_stream
+
+            def sign_staged():
+                sst.wait_event(done)
+                with torch.cuda.stream(sst):
+                    reqs = self._sign_range(sq, proved)
+                sst.synchronize()
+                self._record_all_proofs(sq, reqs, t0)
+                return reqs
+
+            return self._pool.submit(sign_staged)
 
         def sign():
             with torch.cuda.stream(side):

@@ -61,9 +61,9 @@ def _worker(rank, world, port, outdir, mode, op="frequencyCount", lie=True):
     seen = {}
     orig_fan = pcp.fan_out
 
-    def spy(ctx, sq, reqs, pool=False):
-        out = orig_fan(ctx, sq, reqs, pool)
-        seen.update(getattr(ctx, "_pool_seeds", {}).get(sq.SurveyID, {}))
+    def spy(ctx, sq, reqs, pool=False, stage=0):
+        out = orig_fan(ctx, sq, reqs, pool, stage)
+        seen.update(getattr(ctx, "_pool_seeds", {}).get((sq.SurveyID, stage), {}))
         return out
     pcp.fan_out = spy
     out = {"bad": bad, "groups": groups}

@@ -77,7 +77,9 @@ def pool_part(*a):
     from drynx_amd.protocols import proof_collection as pc
     from drynx_amd.utils import streams
 
-    key = (str(dev), pc.POOL_PRIORITY)
+    import threading
+
+    key = (str(dev), pc.POOL_PRIORITY, threading.get_ident())  # one stream per pool thread (a staged plane: two)
     if key not in _PSTREAM:
         _PSTREAM[key] = torch.cuda.Stream(dev, priority=streams.priority(pc.POOL_PRIORITY))
     st = _PSTREAM[key]
@@ -154,6 +156,9 @@ def main():
                     help="one direction of one xGMI link (GB/s): the fan-out term of the projection")
     ap.add_argument("--passes", type=int, default=2, help="1, or 2: a second pass in the reverse order (min of both)")
     ap.add_argument("--order", default=None, help="comma list: the order the ranks are measured in (default 0..W-1)")
+    ap.add_argument("--single-stage", action="store_true",
+                    help="project ONE range fan-out after every rank's proving (DRYNX_RANGE_STAGES=0) instead of "
+                         "the staged plane (proof_collection.range_stages)")
     ap.add_argument("--vn-mode", default="pool", choices=["pool", "local", "own"],
                     help="proof_collection.verification_mode of the projected run: pool (every rank for every VN, "
                          "single operator), local (each VN's own rank + helpers serving only it), own")
@@ -186,9 +191,9 @@ def main():
         cap["dp_results"], cap["sq"] = dp_results, sq
         return orig_async(self, sq, dp_results)
 
-    def cap_plane(ctx, sq, reqs):
+    def cap_plane(ctx, sq, reqs, **kw):
         cap["reqs"] = list(reqs)
-        return orig_plane(ctx, sq, reqs)
+        return orig_plane(ctx, sq, reqs, **kw)
 
     DrynxNode._range_proofs_async, pcp.start_range_plane = cap_async, cap_plane
     for _ in range(2):  # the first query builds the prover tables
@@ -308,54 +313,124 @@ def main():
     # times the min of its two: the rank measured last read ~2 ms slow in
     # either order (profiles/r5/order), a drift of the process, not of the rank
     seq = order + (order[::-1] if a.passes > 1 else [])
+    # the staged range plane (proof_collection.range_stages): every rank's first
+    # m DPs fan out first, the rest (the ranks proving more DPs) in a second
+    # exchange whose pool batch runs beside the first
+    counts = [len(dps_of[k]) for k in range(W)]
+    m = min(counts) if (not a.single_stage and 0 < min(counts) < max(counts)) else 0
+    first = {dp for k in range(W) for dp in (dps_of[k][:m] if m else dps_of[k])}
+    sel_a = [j for j, i in enumerate(rng) if reqs[i].sender_id in first]
+    sel_b = [j for j, i in enumerate(rng) if reqs[i].sender_id not in first]
+    res["stages"] = {"first_dps_per_rank": m or None, "first_lists": len(sel_a), "second_lists": len(sel_b)}
+
+    def sub(rs, sel):
+        return [rs[j] for j in sel]
+
+    # 1. proving: every rank's whole proving and (staged) its first batch
+    prove = {}
+    for k in seq:
+        mine = {dp: dp_results[dp] for dp in dps_of[k]}
+        t_all = timed(lambda: node._sign_range(sq, node._prove_range(sq, mine)), a.reps) if mine else 0.0
+        mine_a = {dp: dp_results[dp] for dp in (dps_of[k][:m] if m else dps_of[k])}
+        t_a = t_all if len(mine_a) == len(mine) else \
+            timed(lambda: node._sign_range(sq, node._prove_range(sq, mine_a)), a.reps)
+        prev = prove.get(k)
+        prove[k] = (t_a, t_all) if prev is None else (min(prev[0], t_a), min(prev[1], t_all))
+    # 2. the exchanges over xGMI: every rank's payloads to each peer over that
+    # peer's link (full bundles to VN ranks, the helper's slice to the others);
+    # each batch's parts start when its last link has delivered
+    dp_rank = {dp: k for k, ids in dps_of.items() for dp in ids}
+    link = [{}, {}]
+    for j, i in enumerate(rng):
+        r = reqs[i]
+        src = dp_rank.get(r.sender_id)
+        if src is None:
+            continue
+        full = r.tensor.numel() * r.tensor.element_size() if r.tensor is not None else len(r.data)
+        lists = prq._range_lists(r, dev)
+        st = 0 if r.sender_id in first else 1
+        for dst in range(W):
+            if dst == src:
+                continue
+            hp = helper_part(dst) if dst not in vn_ranks else None
+            if dst in vn_ranks:
+                nb = full
+            elif hp is not None:
+                nb = prq.range_bundle_pack(prq.slice_lists(lists, sq, hp)).numel() * 4
+            else:
+                continue
+            link[st][(src, dst)] = link[st].get((src, dst), 0) + nb
+    bw = a.xgmi_link_gbs * 1e6  # bytes per ms
+
+    def exch_end(st, t):
+        return max(t[s_] + max((b_ for (s2, _), b_ in link[st].items() if s2 == s_), default=0) / bw
+                   for s_ in range(W))
+    end_a = exch_end(0, {k: prove[k][0] for k in range(W)})
+    end_b = exch_end(1, {k: prove[k][1] for k in range(W)}) if sel_b else end_a
+    delay = max(0.0, end_b - end_a)  # the second batch's parts start this much after the first's
+    # 3. every rank's pool share: the first batch's part, and (staged) the
+    # second batch's on a second thread and stream, started ``delay`` later
     res["passes"] = {}
+    import concurrent.futures as cf
+
+    ex2 = cf.ThreadPoolExecutor(max_workers=1)
     for pi, k in enumerate(seq):
         mp_ = parts_of(k)
         coins = {vn.id: Coins() for vn in cl.vns}
         is_vn = k in vn_ranks
 
-        def run_parts(reqs_k):
+        def run_parts(reqs_k, sel):
+            idx = list(range(len(sel)))
             for part, pv in mp_.items():
-                pool_part(reqs_k, {v: list(range(len(rng))) for v in pv}, sq, dev, cache, part,
-                          {v: coins[v] for v in pv})
-        if is_vn:
-            full = [prq._range_lists(reqs[i], dev) for i in rng]
-            dst = torch.cuda.Stream(dev) if dev.type == "cuda" else None
-            dig = digest_slices(full, k)
+                pool_part(reqs_k, {v: idx for v in pv}, sq, dev, cache, part, {v: coins[v] for v in pv})
+        full = [prq._range_lists(reqs[i], dev) for i in rng] if is_vn else None
+        dig = digest_slices(full, k) if is_vn else []
 
-            def digests_side():
-                ctx = torch.cuda.stream(dst) if dst is not None else contextlib.nullcontext()
-                with ctx:
-                    if dig:
-                        prq.lists_digests(dig)
-                if dst is not None:
-                    dst.synchronize()
+        def batch(sel):
+            if not sel or not mp_:
+                return
+            if is_vn:
+                dst = torch.cuda.Stream(dev) if dev.type == "cuda" else None
+                dg = digest_slices(sub(full, sel), k)
 
-            def vn_part():
-                # as proof_collection.pool_verify_ranges: the VN's digests of its
-                # helpers' slices run on their own stream as an idle task of the
-                # part (while its verifier waits for the device)
+                def digests_side():
+                    ctx = torch.cuda.stream(dst) if dst is not None else contextlib.nullcontext()
+                    with ctx:
+                        if dg:
+                            prq.lists_digests(dg)
+                    if dst is not None:
+                        dst.synchronize()
+                # as proof_collection: the VN's digests of its helpers' slices run on
+                # their own stream as an idle task of the part
                 if dst is not None:
                     dst.wait_stream(torch.cuda.current_stream(dev))
                 fut = rp.add_idle_task(rp.Deferred(digests_side))
-                run_parts(full_reqs())
+                run_parts(sub(full_reqs(), sel), sel)
                 fut.result()
-            t_pool = timed(vn_part, a.reps)
-        elif mp_:
-            t_pool = timed(lambda: run_parts(helper_reqs(helper_part(k))), a.reps)
-        else:
-            t_pool = 0.0
-        t_dig = 0.0
-        if is_vn and dig:  # alone, for reference (the pool time above already runs them alongside)
-            t_dig = timed(lambda: prq.lists_digests(dig), a.reps)
-        mine = {dp: dp_results[dp] for dp in dps_of[k]}
-        t_prove = timed(lambda: node._sign_range(sq, node._prove_range(sq, mine)), a.reps) if mine else 0.0
-        rec = {"prove_ms": t_prove, "pool_ms": t_pool, "vn_digest_ms": t_dig, "vn_rank": is_vn, "dps": len(mine)}
+            else:
+                run_parts(sub(helper_reqs(helper_part(k)), sel), sel)
+            _sync()
+
+        def both():
+            if sel_b and mp_:
+                def late():
+                    time.sleep(delay / 1e3)
+                    batch(sel_b)
+                f = ex2.submit(late)
+                batch(sel_a)
+                f.result()
+            else:
+                batch(sel_a)
+        t_pool = timed(both, a.reps) if mp_ else 0.0
+        t_dig = timed(lambda: prq.lists_digests(dig), a.reps) if (is_vn and dig) else 0.0
+        rec = {"prove_ms": prove[k][1], "prove_first_ms": prove[k][0], "pool_ms": t_pool, "vn_digest_ms": t_dig,
+               "vn_rank": is_vn, "dps": len(dps_of[k])}
         res["passes"].setdefault(k, []).append(rec)
         prev = res["ranks"].get(k)
         res["ranks"][k] = rec if prev is None else {**rec, **{f: min(prev[f], rec[f]) for f in
-                                                              ("prove_ms", "pool_ms", "vn_digest_ms")}}
+                                                              ("pool_ms", "vn_digest_ms")}}
         print(json.dumps({"rank": k, "pass": 1 + (pi >= len(order)), **rec}), flush=True)
+    ex2.shutdown()
     if a.serial_json:
         s = json.load(open(a.serial_json))
         res["serial_ms"] = s["ms_per_step"]
@@ -369,42 +444,18 @@ def main():
         res["ctrl_source"] = a.ctrl_json
     proj = {}
     for k, v in res["ranks"].items():
-        rng_path = v["prove_ms"] + v["pool_ms"]  # a VN rank's pool_ms includes its overlapped digests
-        proj[k] = round(max(serial if k == 0 else 0.0, rng_path) + ctrl, 2)
+        # each rank's range path: its first batch's parts start at that exchange's end
+        # (a VN rank's pool_ms includes its overlapped digests)
+        proj[k] = round(max(serial if k == 0 else 0.0, end_a + v["pool_ms"]) + ctrl, 2)
     res["projection_ms"] = proj
-    prove_max = max(v["prove_ms"] for v in res["ranks"].values())
+    prove_max = max(v[1] for v in prove.values())
     pool_max = max(v["pool_ms"] for v in res["ranks"].values())
-    # the range fan-out over xGMI: every rank's payloads to each peer over that
-    # peer's link (full bundles to VN ranks, the helper's slice to the others);
-    # the pool parts start when the last link has delivered
-    dp_rank = {dp: k for k, ids in dps_of.items() for dp in ids}
-    link = {}
-    for i in rng:
-        r = reqs[i]
-        src = dp_rank.get(r.sender_id)
-        if src is None:
-            continue
-        full = r.tensor.numel() * r.tensor.element_size() if r.tensor is not None else len(r.data)
-        lists = prq._range_lists(r, dev)
-        for dst in range(W):
-            if dst == src:
-                continue
-            hp = helper_part(dst) if dst not in vn_ranks else None
-            if dst in vn_ranks:
-                nb = full
-            elif hp is not None:
-                nb = prq.range_bundle_pack(prq.slice_lists(lists, sq, hp)).numel() * 4
-            else:
-                continue
-            link[(src, dst)] = link.get((src, dst), 0) + nb
-    bw = a.xgmi_link_gbs * 1e6  # bytes per ms
-    exchange_end = max((res["ranks"][s_]["prove_ms"] + max((b for (s2, _), b in link.items() if s2 == s_),
-                                                          default=0) / bw) for s_ in res["ranks"])
-    xgmi = round(exchange_end - prove_max, 3)
-    res["xgmi_link_bytes_max"] = max(link.values(), default=0)
-    res["projection_step_ms"] = round(max(serial, exchange_end + pool_max) + ctrl, 2)
-    res["projection_terms_ms"] = {"prove_max": prove_max, "xgmi": xgmi, "pool_max": pool_max, "serial": serial,
-                                  "ctrl": round(ctrl, 3)}
+    xgmi = round(end_a - max(v[0] for v in prove.values()), 3)
+    res["xgmi_link_bytes_max"] = max([b_ for lk in link for b_ in lk.values()], default=0)
+    res["projection_step_ms"] = round(max(serial, end_a + pool_max) + ctrl, 2)
+    res["projection_terms_ms"] = {"prove_max": prove_max, "first_exchange_end": round(end_a, 3),
+                                  "second_exchange_delay": round(delay, 3), "xgmi": xgmi, "pool_max": pool_max,
+                                  "serial": serial, "ctrl": round(ctrl, 3)}
     print(json.dumps({"vn_mode": a.vn_mode, "projection_ms": proj, "step_ms": res["projection_step_ms"],
                       "terms": res["projection_terms_ms"]}), flush=True)
     if a.json_out:
