@@ -43,10 +43,16 @@ DX_HD G2J lam_jac(const G2J &q) {  // [lambda] Q = -psi^2(Q) = (TWX2 x, y) (TWX2
 // version of this file): the kernels here make no calls at all.
 constexpr int kWG = 64;
 
-// T[it*15 + da + 4 db - 1] = affine(da V_it + db [lambda] V_it).  The Jacobian
-// (X, Y) of every entry is parked in the output slot itself, the Z values and
-// prefix products in the thread's frame; one inversion per V (Montgomery's
-// trick) converts all 15 in place.
+// T[it*15 + da + 4 db - 1] = affine(da V_it + db [lambda] V_it).  2V and 3V
+// come from ONE inversion (Jacobian, Montgomery's trick over their two Z);
+// the six single-axis entries (da V, db [lambda] V: [lambda] = x * TWX2) are
+// then written at once, and the nine mixed entries da V + db [lambda] V are
+// AFFINE additions sharing a second inversion: d = x_b - x_a per entry, the
+// prefix products parked in the x of each entry's own output slot (read back
+// in the reverse pass), the operand points re-read from their slots -- no
+// per-entry arrays in the thread's frame (the previous Jacobian version kept
+// 15 Z values and prefix products there: 3,360 B of scratch per lane,
+// profiles/r5/kernel_resources.txt) and ~1/3 of its field products.
 DX_HD void joint_table_one(const uint32_t *V_aff, uint32_t *T_aff, int64_t it) {
   G2A *T = reinterpret_cast<G2A *>(T_aff) + it * kT;
   const G2A v = at<G2A>(V_aff, it);
@@ -54,31 +60,45 @@ DX_HD void joint_table_one(const uint32_t *V_aff, uint32_t *T_aff, int64_t it) {
     for (int e = 0; e < kT; e++) T[e] = G2A::inf();
     return;
   }
-  Fp2 z[kT], pre[kT];
-  G2J P[4];
-  P[1] = G2J::from_aff(v);
-  P[2] = jdbl(P[1]);
-  P[3] = jadd_mixed(P[2], v);
+  const Fp tw = Fp::from_limbs(Frob::TWX2[0]);
+  {
+    const G2J P2 = jdbl(G2J::from_aff(v));
+    const G2J P3 = jadd_mixed(P2, v);
+    const Fp2 ii = inv(mul(P2.z, P3.z));  // 2V, 3V != infinity (r is prime, > 3)
+    const Fp2 z2i = mul(ii, P3.z), z3i = mul(ii, P2.z);
+    const Fp2 z2i2 = sqr(z2i), z3i2 = sqr(z3i);
+    const G2A A2{mul(P2.x, z2i2), mul(mul(P2.y, z2i2), z2i)};
+    const G2A A3{mul(P3.x, z3i2), mul(mul(P3.y, z3i2), z3i)};
+    T[0] = v;                                 // (1, 0)
+    T[1] = A2;                                // (2, 0)
+    T[2] = A3;                                // (3, 0)
+    T[3] = G2A{mul_fp(v.x, tw), v.y};         // (0, 1)
+    T[7] = G2A{mul_fp(A2.x, tw), A2.y};       // (0, 2)
+    T[11] = G2A{mul_fp(A3.x, tw), A3.y};      // (0, 3)
+  }
+  // mixed entries e = da + 4 db - 1, da, db in 1..3: forward prefix products
+  // of d_e = x(db [lambda] V) - x(da V) (nonzero: da V != +-db [lambda] V)
   Fp2 acc = Fp2::one();
-  for (int db = 0; db < 4; db++) {
-    const G2J Lb = db ? lam_jac(P[db]) : G2J::inf();
-    for (int da = 0; da < 4; da++) {
+  for (int db = 1; db < 4; db++) {
+    for (int da = 1; da < 4; da++) {
       const int e = da + 4 * db - 1;
-      if (e < 0) continue;
-      const G2J q = da == 0 ? Lb : (db == 0 ? P[da] : jadd(P[da], Lb));
-      T[e] = G2A{q.x, q.y};
-      z[e] = q.z;
-      pre[e] = acc;
-      acc = mul(acc, q.z);
+      const Fp2 d = sub(T[4 * db - 1].x, T[da - 1].x);
+      T[e].x = acc;  // parked: the prefix product before this entry
+      acc = mul(acc, d);
     }
   }
-  Fp2 inv_all = inv(acc);  // da + db lambda != 0 mod r for da, db < 4: no entry is infinity
-  for (int e = kT - 1; e >= 0; e--) {
-    const Fp2 zi = mul(inv_all, pre[e]);
-    inv_all = mul(inv_all, z[e]);
-    const Fp2 zi2 = sqr(zi);
-    const G2A raw = T[e];
-    T[e] = G2A{mul(raw.x, zi2), mul(mul(raw.y, zi2), zi)};
+  Fp2 iv = inv(acc);
+  for (int db = 3; db >= 1; db--) {
+    for (int da = 3; da >= 1; da--) {
+      const int e = da + 4 * db - 1;
+      const G2A a = T[da - 1], b = T[4 * db - 1];
+      const Fp2 d = sub(b.x, a.x);
+      const Fp2 di = mul(iv, T[e].x);  // 1 / d_e
+      iv = mul(iv, d);
+      const Fp2 lm = mul(sub(b.y, a.y), di);
+      const Fp2 x3 = sub(sub(sqr(lm), a.x), b.x);
+      T[e] = G2A{x3, sub(mul(lm, sub(a.x, x3)), a.y)};
+    }
   }
 }
 
