@@ -601,9 +601,13 @@ def range_stages(ctx, sq) -> int:
     it, and the rest follows in a second exchange whose batch verifies
     concurrently (the reference streams each DP's proofs as they are made,
     data_collection_protocol.go:278-348).  A function of the placement:
-    identical on every rank.  DRYNX_RANGE_STAGES=0 keeps one batch."""
+    identical on every rank.  Opt-in (DRYNX_RANGE_STAGES=1): measured at
+    W = 8 on one GPU the second batch beside the first lengthens every part
+    from ~30 to ~39-40 ms (its kernels and host work contend with the
+    first's), which outweighs starting ~5 ms earlier (projection 51.7 vs
+    50.0 ms, profiles/r6/staged/)."""
     W = ctx.comm.world
-    if W <= 1 or os.environ.get("DRYNX_RANGE_STAGES", "1") == "0":
+    if W <= 1 or os.environ.get("DRYNX_RANGE_STAGES", "0") != "1":
         return 0
     dps, _, _ = _placement(ctx, sq)
     lo, hi = min(dps), max(dps)

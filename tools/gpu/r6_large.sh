@@ -14,6 +14,7 @@ if [ "${R6_LARGE:-small}" = small ]; then
   step max10k 300 python -u bench.py --query max --range 10000 --steps 2 --warmup 1 --json-out $O/max_10k.json
   step max100k 500 python -u bench.py --query max --range 100000 --steps 1 --warmup 1 --json-out $O/max_100k.json
   step dro100k 300 python -u bench.py --query lr_dro --dro 100000 --steps 2 --warmup 1 --json-out $O/lrdro_100k.json
+  step sweeps 500 python -u tools/bench_scaling.py 3 servers,vns,threshold
 else
   step max1m 900 python -u bench.py --query max --range 1000000 --steps 1 --warmup 1 --json-out $O/max_1m.json
   step dro1m 600 python -u bench.py --query lr_dro --dro 1000000 --steps 1 --warmup 1 --json-out $O/lrdro_1m.json

@@ -156,9 +156,9 @@ def main():
                     help="one direction of one xGMI link (GB/s): the fan-out term of the projection")
     ap.add_argument("--passes", type=int, default=2, help="1, or 2: a second pass in the reverse order (min of both)")
     ap.add_argument("--order", default=None, help="comma list: the order the ranks are measured in (default 0..W-1)")
-    ap.add_argument("--single-stage", action="store_true",
-                    help="project ONE range fan-out after every rank's proving (DRYNX_RANGE_STAGES=0) instead of "
-                         "the staged plane (proof_collection.range_stages)")
+    ap.add_argument("--staged", action="store_true", default=os.environ.get("DRYNX_RANGE_STAGES") == "1",
+                    help="project the staged range plane (DRYNX_RANGE_STAGES=1, proof_collection.range_stages) "
+                         "instead of ONE fan-out after every rank's proving (the default)")
     ap.add_argument("--vn-mode", default="pool", choices=["pool", "local", "own"],
                     help="proof_collection.verification_mode of the projected run: pool (every rank for every VN, "
                          "single operator), local (each VN's own rank + helpers serving only it), own")
@@ -317,7 +317,7 @@ def main():
     # m DPs fan out first, the rest (the ranks proving more DPs) in a second
     # exchange whose pool batch runs beside the first
     counts = [len(dps_of[k]) for k in range(W)]
-    m = min(counts) if (not a.single_stage and 0 < min(counts) < max(counts)) else 0
+    m = min(counts) if (a.staged and 0 < min(counts) < max(counts)) else 0
     first = {dp for k in range(W) for dp in (dps_of[k][:m] if m else dps_of[k])}
     sel_a = [j for j, i in enumerate(rng) if reqs[i].sender_id in first]
     sel_b = [j for j, i in enumerate(rng) if reqs[i].sender_id not in first]
