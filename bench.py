@@ -24,7 +24,12 @@ value  = range-proof verifications per second of end-to-end query time
 ms_per_step = end-to-end latency of one verifiable query (max over ranks).
 scaling = strong: the query is fixed; N GPUs share it (DPs round robin over the
          ranks, CNs and VNs on distinct ranks, every VN's range checks pooled
-         over all ranks).
+         over all ranks by default).  The JSON's ``config.trust_model`` says
+         what a VN's verdict depended on in the run: ``single-operator-pool``
+         (helper ranks serve every VN, their slice verdicts bound to the VN's
+         own digests of the bytes they checked) or ``vn-local`` (only ranks
+         assigned to that VN: ``--vn-mode local``, or the VN's own rank:
+         ``--vn-mode own``; one GPU: every VN on its own coins).
 vs_baseline = value / 315.6, the reference's verifications per second of
          end-to-end time in that run (20,700 x 3 / 196.77 s).
 
