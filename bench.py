@@ -76,6 +76,8 @@ from drynx_amd.utils import timers  # noqa: E402
 
 REFERENCE_LR_SPECTF_S = 196.77  # AllResults.xlsx LogRegr row 7
 REFERENCE_DIFFPRI_10K_S = 82.0  # AllResults.xlsx DiifPri row 6: query with a 10k-entry noise list
+# the reference's DiffPri sheet by noise-list size (simul/test_data/graphs/TIFS/diffPri.py:9-12): totals
+REFERENCE_DIFFPRI_S = {0: 2.3, 10_000: 81.9, 100_000: 657.0, 1_000_000: 5872.0}
 DRO_LAP_SCALE, DRO_LIMIT = 2.0, 50.0  # noise list parameters of the config-4 line
 REFERENCE_VERIFICATIONS_PER_S = 10 * 2070 * 3 / REFERENCE_LR_SPECTF_S  # 10 DPs x 2070 proofs x 3 VNs
 # AllOps totals (AllResults.xlsx rows 6, 7, 16) and this bench's shape for them
@@ -380,6 +382,10 @@ def main():
                                "proof of shuffle, added to the aggregate before key switching (the reference's "
                                "Obfuscation protocol is only legal for bit operations, structs.go:450-462)",
                 "noise_list": {"size": args.dro, "lap_scale": DRO_LAP_SCALE, "limit": DRO_LIMIT},
+                "reference_row": ({"sheet": "DiffPri", "source": "simul/test_data/graphs/TIFS/diffPri.py:9-12",
+                                   "noise_list": args.dro, "total_s": REFERENCE_DIFFPRI_S[args.dro],
+                                   "speedup": round(REFERENCE_DIFFPRI_S[args.dro] / (ms / 1000.0), 1)}
+                                  if args.dro in REFERENCE_DIFFPRI_S else None),
             }
         line = {
             "metric": "end-to-end query latency + range-proof verifications/sec, logreg on 1e6 records",

@@ -71,3 +71,22 @@ def test_early_range_plane_only_with_range_proofs(tmp_path, monkeypatch):
     monkeypatch.setenv("DRYNX_RANGE_PLANE", "0")
     assert not pcp.early_plane_ok(node, sq)
     node.close(remove=True)
+
+
+def test_commitment_only_lists_are_not_decoded(tmp_path, monkeypatch):
+    """With every query range (0, 0) the verification is true whatever the
+    list holds (range_proof.go:508-510): the VN neither decodes nor checks the
+    commitment-only bundles (the serial path's rp.verify.unpack_many)."""
+    cl, node, sq = _setup(tmp_path)
+    client = DrynxClient(node)
+    sq0 = make_survey(client, cl, "mean", query_min=0, query_max=10, rows=4, proofs=1, ranges=[0, 0])
+    calls = []
+    monkeypatch.setattr(prq, "range_bundle_unpack_many", lambda ts: calls.append(len(ts)) or [])
+    monkeypatch.setattr(prq, "range_bundle_unpack", lambda t: calls.append(1))
+    req = prq.ProofRequest("range", sq0.SurveyID, cl.dps[0].id, "", b"\x00" * 64, b"")
+    base, parts = prq._range_parts([req, req], [0, 1], sq0, "cpu", None)
+    assert base == {0: True, 1: True} and parts == {0: [], 1: []} and not calls
+    # a query with range proofs still decodes (and rejects the garbage)
+    base, _ = prq._range_parts([req], [0], sq, "cpu", None)
+    assert base == {0: False}
+    node.close(remove=True)
