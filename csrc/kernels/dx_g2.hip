@@ -86,45 +86,8 @@ int dx_g2_mul(int on_gpu, void *stream, const uint32_t *pts_aff, const uint32_t 
 
 }  // extern "C"
 
-namespace {
-// psi on Jacobian coordinates: (X, Y, Z) -> (conj(X) twx, conj(Y) twy, conj(Z)).
-DX_HD G2J psi_jac(const G2J &q) {
-  return {mul(conj(q.x), Fp2::from_limbs(Frob::TWX1)), mul(conj(q.y), Fp2::from_limbs(Frob::TWY1)), conj(q.z)};
-}
-}  // namespace
-
 extern "C" {
-// G2 membership of a twist point (range-proof V_ij): on the curve and
-//   [u+1] Q + psi([u] Q) + psi^2([u] Q) == psi^3([2u] Q)
-// (the BN-curve test of Dai-Lin-Zhao-Zhou 2022: one 63-bit ladder [u] Q instead
-// of the 127-bit [6u^2] Q of psi(Q) == [6u^2] Q).  Exact: the cofactor 2p - r is
-// squarefree (10069 * 5864401 * 1875725156269 * p54), psi acts on each cyclic
-// prime-order part as a scalar, and the test's endomorphism is non-zero on each
-// (tests/test_range_hardening.py checks a point of every torsion order).
-int dx_g2_subgroup(int on_gpu, void *stream, const uint32_t *aff, uint8_t *out, int64_t n) {
-  auto op = [=] __host__ __device__(int64_t i) {
-    const G2A q = at<G2A>(aff, i);
-    if (!on_curve(q)) {
-      out[i] = 0;
-      return;
-    }
-    if (q.is_inf()) {
-      out[i] = 1;
-      return;
-    }
-    G2J uq = G2J::from_aff(q);  // top bit of u (bit 62)
-    for (int b = 61; b >= 0; --b) {
-      uq = jdbl(uq);
-      if ((BN_U >> b) & 1ull) uq = jadd_mixed(uq, q);
-    }
-    const G2J p1 = psi_jac(uq);
-    const G2J lhs = jadd(jadd(jadd_mixed(uq, q), p1), psi_jac(p1));
-    const G2J rhs = psi_jac(psi_jac(psi_jac(jdbl(uq))));
-    out[i] = jeq(lhs, rhs) ? 1 : 0;
-  };
-  return run(on_gpu, stream, n, op, true, "g2_subgroup");
-}
-
+// dx_g2_subgroup: csrc/kernels/dx_check_inl.hip (force-inlined, spill-free)
 int dx_g2_on_curve(int on_gpu, void *stream, const uint32_t *aff, uint8_t *out, int64_t n) {
   auto op = [=] __host__ __device__(int64_t i) { out[i] = on_curve(at<G2A>(aff, i)) ? 1 : 0; };
   return run(on_gpu, stream, n, op, false, "g2_on_curve");

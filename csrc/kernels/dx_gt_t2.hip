@@ -13,9 +13,11 @@
 // The ledger must give back exactly what was signed, so an element is only
 // compressed when the round trip is exact: canonical limbs, unitary, h != 0
 // (``ok`` = 0 otherwise, and the caller stores that list raw).  Both
-// directions take one inversion per chunk of kChunk elements (Montgomery's
-// simultaneous inversion), so a query's ~10^6 elements cost a few hundred
-// Fp multiplications each.  Host and device builds (run()).
+// directions take one inversion per chunk of up to kChunk elements
+// (Montgomery's simultaneous inversion; t2_chunk), so an element costs a few
+// hundred Fp multiplications.  Host and device builds (run()); the tower
+// functions are force-inlined into this unit's kernels (no call frames).
+#define DX_NI __host__ __device__ __forceinline__
 #include "common.h"
 
 namespace {
@@ -27,52 +29,55 @@ DX_HD bool fp_canonical(const uint32_t *w) {
   return br != 0;
 }
 
-// c_i = (1 + g_i) / h_i for a chunk of elements [i0, i1); ok_i as above
+// c_i = (1 + g_i) / h_i for a chunk of elements [i0, i1); ok_i as above.
+// The prefix products of Montgomery's trick are parked in each element's own
+// output slot c_i (an Fp6, the size of the output) and read back by the
+// reverse pass: no per-chunk arrays in the thread's frame (the array version
+// kept 8 Fp6 prefixes there, 3,552 B of scratch per lane).
 DX_HD void compress_chunk(const uint32_t *a, uint32_t *c, uint8_t *ok, int64_t i0, int64_t i1) {
-  Fp6 pre[kChunk];
   Fp6 acc = Fp6::one();
-  bool good[kChunk];
+  uint32_t good = 0;
   for (int64_t i = i0; i < i1; i++) {
-    const int j = (int)(i - i0);
     const uint32_t *w = a + 96 * i;
     bool g = true;
     for (int k = 0; k < 12; k++) g = g && fp_canonical(w + 8 * k);
     const Fp12 f = at<Fp12>(a, i);
     g = g && !(f.c1 == Fp6::zero()) && sub(sqr(f.c0), mul_v(sqr(f.c1))) == Fp6::one();
-    good[j] = g;
-    pre[j] = acc;
-    if (g) acc = mul(acc, f.c1);
+    at<Fp6>(c, i) = acc;
+    if (g) {
+      good |= 1u << (i - i0);
+      acc = mul(acc, f.c1);
+    }
   }
   Fp6 inv_all = inv(acc);
   for (int64_t i = i1 - 1; i >= i0; i--) {
-    const int j = (int)(i - i0);
-    ok[i] = good[j] ? 1 : 0;
-    if (!good[j]) {
+    const bool g = (good >> (i - i0)) & 1u;
+    ok[i] = g ? 1 : 0;
+    if (!g) {
       at<Fp6>(c, i) = Fp6::zero();
       continue;
     }
     const Fp12 f = at<Fp12>(a, i);
-    const Fp6 hi = mul(inv_all, pre[j]);
+    const Fp6 hi = mul(inv_all, at<Fp6>(c, i));
     inv_all = mul(inv_all, f.c1);
     at<Fp6>(c, i) = mul(add(Fp6::one(), f.c0), hi);
   }
 }
 
-// f_i = ((c^2 + v) + 2c w) / (c^2 - v)
+// f_i = ((c^2 + v) + 2c w) / (c^2 - v); prefixes parked in the w half of a_i
 DX_HD void decompress_chunk(const uint32_t *c, uint32_t *a, int64_t i0, int64_t i1) {
-  Fp6 pre[kChunk];
   Fp6 acc = Fp6::one();
   const Fp6 v = {Fp2::zero(), Fp2::one(), Fp2::zero()};
   for (int64_t i = i0; i < i1; i++) {
     const Fp6 x = at<Fp6>(c, i);
-    pre[i - i0] = acc;
+    at<Fp12>(a, i).c1 = acc;
     acc = mul(acc, sub(sqr(x), v));
   }
   Fp6 inv_all = inv(acc);
   for (int64_t i = i1 - 1; i >= i0; i--) {
     const Fp6 x = at<Fp6>(c, i);
     const Fp6 x2 = sqr(x);
-    const Fp6 di = mul(inv_all, pre[i - i0]);
+    const Fp6 di = mul(inv_all, at<Fp12>(a, i).c1);
     inv_all = mul(inv_all, sub(x2, v));
     at<Fp12>(a, i) = Fp12{mul(add(x2, v), di), mul(add(x, x), di)};
   }
@@ -164,11 +169,24 @@ int dx_g2_x_decompress(int on_gpu, void *stream, const uint32_t *xi, const uint3
 }
 
 
+// Elements per simultaneous inversion: up to kChunk, but no more than keeps
+// >= 2 waves per SIMD busy (1,024 SIMDs x 64 lanes x 2).  A ledger payload is
+// one DP's ~10^5 GT elements: 8 per lane left 12k lanes -- a fifth of the
+// SIMDs, each lane running 8 elements' products back to back (1.37 ms per
+// payload, serialized); one per lane spreads them over the chip and pays one
+// Fp6 inversion each.  The host path keeps kChunk (few threads).
+inline int64_t t2_chunk(int on_gpu, int64_t n) {
+  if (!on_gpu) return kChunk;
+  const int64_t c = n / (1024 * 64 * 2);
+  return c < 1 ? 1 : (c > kChunk ? kChunk : c);
+}
+
 // a [n, 96] GT elements (Montgomery limbs) -> c [n, 48], ok [n] (1: c round-trips to a)
 int dx_gt_t2_compress(int on_gpu, void *stream, const uint32_t *a, uint32_t *c, uint8_t *ok, int64_t n) {
-  const int64_t chunks = (n + kChunk - 1) / kChunk;
+  const int64_t k = t2_chunk(on_gpu, n);
+  const int64_t chunks = (n + k - 1) / k;
   auto op = [=] __host__ __device__(int64_t t) {
-    const int64_t i0 = t * kChunk, i1 = i0 + kChunk < n ? i0 + kChunk : n;
+    const int64_t i0 = t * k, i1 = i0 + k < n ? i0 + k : n;
     compress_chunk(a, c, ok, i0, i1);
   };
   return run(on_gpu, stream, chunks, op, true, "gt_t2_compress");
@@ -176,9 +194,10 @@ int dx_gt_t2_compress(int on_gpu, void *stream, const uint32_t *a, uint32_t *c, 
 
 // c [n, 48] -> a [n, 96]
 int dx_gt_t2_decompress(int on_gpu, void *stream, const uint32_t *c, uint32_t *a, int64_t n) {
-  const int64_t chunks = (n + kChunk - 1) / kChunk;
+  const int64_t k = t2_chunk(on_gpu, n);
+  const int64_t chunks = (n + k - 1) / k;
   auto op = [=] __host__ __device__(int64_t t) {
-    const int64_t i0 = t * kChunk, i1 = i0 + kChunk < n ? i0 + kChunk : n;
+    const int64_t i0 = t * k, i1 = i0 + k < n ? i0 + k : n;
     decompress_chunk(c, a, i0, i1);
   };
   return run(on_gpu, stream, chunks, op, true, "gt_t2_decompress");

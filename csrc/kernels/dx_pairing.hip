@@ -115,19 +115,7 @@ int dx_gt_fb4_pow(int on_gpu, void *stream, const uint32_t *tables, const int32_
   return run(on_gpu, stream, n, op, true, "gt_fb4_pow");
 }
 
-// GT-side validity of prover-supplied Fp12 values (range-proof a_ij): membership
-// of the cyclotomic subgroup G_Phi12 (order Phi12(p) = p^4 - p^2 + 1 = r h),
-// x^(p^4) x == x^(p^2): three Frobenius maps and one product.  The prime-order
-// part is then enforced by the batch equation plus one random combination
-// checked in GT (range_proof.py).
-int dx_gt_cyclotomic(int on_gpu, void *stream, const uint32_t *a, uint8_t *out, int64_t n) {
-  auto op = [=] __host__ __device__(int64_t i) {
-    const Fp12 x = at<Fp12>(a, i);
-    const Fp12 x2 = frob<2>(x);
-    out[i] = (mul(frob<2>(x2), x) == x2 && !(x.c0 == Fp6::zero() && x.c1 == Fp6::zero())) ? 1 : 0;
-  };
-  return run(on_gpu, stream, n, op, true, "gt_cyclotomic");
-}
+// dx_gt_cyclotomic (a_ij in the cyclotomic subgroup): csrc/kernels/dx_check_inl.hip
 
 // Exact membership of the prime-order GT for elements of the cyclotomic
 // subgroup: p = 6u^2 (mod r), so x^r = 1 iff x^p == x^(6u^2).  x^p is ONE

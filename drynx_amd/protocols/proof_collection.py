@@ -696,20 +696,34 @@ def proof_collection(ctx, sq, local_requests: list, early: dict | None = None, l
         def prefetch(rs):
             # the stored payloads' host copy and blob write run under their
             # verification instead of after the verdicts (store_verdicts finds
-            # them in the rank's blob segment); payloads whose digest is known
-            if LEDGER_PREFETCH and local_vns and hasattr(ctx, "ledger_values"):
-                with timers.span("ledger.prefetch"):
-                    ctx.ledger_values([r for r in rs if r.kind != "shuffle" and r.data_digest
-                                       and r.tensor is not None], range_shape(sq))
+            # them in the rank's blob segment); payloads whose digest is known.
+            # On a worker of its own: the main thread goes on to the checks
+            # (the late key-switch proofs' prefetch sat on the serial path)
+            if not (LEDGER_PREFETCH and local_vns and hasattr(ctx, "ledger_values")):
+                return None
+            sel = [r for r in rs if r.kind != "shuffle" and r.data_digest and r.tensor is not None]
+            if not sel:
+                return None
+            ex = getattr(ctx, "_prefetch_exec", None)
+            if ex is None:
+                ex = ctx._prefetch_exec = streams.executor(ctx.device, 1, "drynx-ledger-prefetch")
 
-        prefetch(reqs)
+            def run():
+                with timers.span("ledger.prefetch"):
+                    ctx.ledger_values(sel, range_shape(sq))
+            return ex.submit(run)
+
+        pfs = [prefetch(reqs)]
         pending = checks(reqs, pooled)
         reqs2, pending2 = [], {}
         if late is not None:
             with timers.timed("ProofFanOut"):
                 reqs2 = fan_out(ctx, sq, late(), pool=False)
-            prefetch(reqs2)
+            pfs.append(prefetch(reqs2))
             pending2 = checks(reqs2, None)
+        for f in pfs:  # store_verdicts reads the blob segment the prefetch fills
+            if f is not None:
+                f.result()
         for vn in vns:
             if vn.id in pending:
                 codes = pending[vn.id]()
