@@ -280,17 +280,63 @@ __global__ void __launch_bounds__(kWG) DX_OCC u_joint_kernel(const uint32_t *T, 
   DX_TID();
   if (i < n) u_joint_one(T, ab, U, n_groups, L, pad, pos, i);
 }
+__global__ void __launch_bounds__(kWG) DX_OCC u_joint_reduce_kernel(const uint32_t *P, uint32_t *U, int64_t n_groups,
+                                                                   int sp, int64_t pad, const int64_t *pos,
+                                                                   int64_t n) {
+  DX_TID();
+  if (i < n) u_joint_reduce_one(P, U, n_groups, sp, pad, pos, i);
+}
 __global__ void __launch_bounds__(kWG) DX_OCC u_joint_part_kernel(const uint32_t *T, const uint32_t *ab,
                                                                  uint32_t *P, int64_t n_groups, int L, int sp,
                                                                  int64_t n) {
   DX_TID();
   if (i < n) u_joint_part_one(T, ab, P, n_groups, L, sp, i);
 }
-__global__ void __launch_bounds__(kWG) DX_OCC u_joint_reduce_kernel(const uint32_t *P, uint32_t *U, int64_t n_groups,
-                                                                   int sp, int64_t pad, const int64_t *pos,
-                                                                   int64_t n) {
+// The split combination with its reduction in the same workgroup: the sp
+// lanes of a (v, q) are adjacent (sp | 64), add their partials pairwise
+// through LDS (log2 sp rounds) and the first normalises -- no Jacobian
+// partials through HBM and no second, one-lane-per-(v, q) launch (a pool
+// part's ~23k (v, q) filled a third of the SIMDs there, 2.4 ms of the U chain,
+// profiles/r6/prof/timeline_part6.txt).  Every lane reaches every barrier.
+__global__ void __launch_bounds__(kWG) DX_OCC u_joint_fused_kernel(const uint32_t *T, const uint32_t *ab, uint32_t *U,
+                                                                  int64_t n_groups, int L, int sp, int64_t pad,
+                                                                  const int64_t *pos, int64_t n) {
+  __shared__ G2J red[kWG];
   DX_TID();
-  if (i < n) u_joint_reduce_one(P, U, n_groups, sp, pad, pos, i);
+  const bool live = i < n * sp;
+  G2J acc = G2J::inf();
+  if (live) {
+    const int part = (int)(i % sp);
+    const int64_t vq = i / sp;
+    const int64_t v = vq / n_groups, q = vq % n_groups;
+    const int64_t m = n_groups * L;
+    const int per = (L + sp - 1) / sp;
+    const int j0 = part * per, j1 = j0 + per < L ? j0 + per : L;
+    const G2A *Tq = reinterpret_cast<const G2A *>(T) + q * L * kT;
+    const uint32_t *w = ab + 2 * (v * m + q * L);
+    for (int win = 15; win >= 0; win--) {
+      if (win != 15) {
+        acc = jdbl(acc);
+        acc = jdbl(acc);
+      }
+      for (int j = j0; j < j1; j++) {
+        const uint32_t e = ((w[2 * j] >> (2 * win)) & 3u) + 4u * ((w[2 * j + 1] >> (2 * win)) & 3u);
+        if (e) acc = jadd_mixed(acc, Tq[j * kT + e - 1]);
+      }
+    }
+  }
+  const int part = (int)(threadIdx.x % sp);
+  for (int st = 1; st < sp; st <<= 1) {
+    if (part % (2 * st) == st) red[threadIdx.x] = acc;
+    __syncthreads();
+    if (part % (2 * st) == 0) acc = jadd(acc, red[threadIdx.x + st]);
+    __syncthreads();
+  }
+  if (live && part == 0) {
+    const int64_t vq = i / sp;
+    const int64_t v = vq / n_groups, q = vq % n_groups;
+    at<G2A>(U, pos ? pos[vq] : v * pad + q) = to_affine(acc);
+  }
 }
 __global__ void __launch_bounds__(kWG) DX_OCC slice_sum_kernel(const uint32_t *src, const int32_t *idx,
                                                               const int64_t *start, const int32_t *len,
@@ -374,6 +420,11 @@ int dx_rp_u_joint_split(int on_gpu, void *stream, const uint32_t *T_aff, const u
     host_for_each(n * sp, [=](int64_t t) { u_joint_part_one(T_aff, ab, tmp, n_groups, L, sp, t); });
     host_for_each(n, [=](int64_t t) { u_joint_reduce_one(tmp, U_aff, n_groups, sp, pad, pos, t); });
     return 0;
+  }
+  if (kWG % sp == 0) {
+    hipLaunchKernelGGL(u_joint_fused_kernel, grid_of(n * sp), dim3(kWG), 0, (hipStream_t)stream, T_aff, ab, U_aff,
+                       n_groups, L, sp, pad, pos, n);
+    return check_hip(hipGetLastError(), "rp_u_joint_fused");
   }
   hipLaunchKernelGGL(u_joint_part_kernel, grid_of(n * sp), dim3(kWG), 0, (hipStream_t)stream, T_aff, ab, tmp,
                      n_groups, L, sp, n * sp);

@@ -83,6 +83,31 @@ def test_u_joint_combinations(device):
     assert torch.equal(out2.index_select(0, pos), want)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("L", [16, 5])
+def test_u_joint_split_matches_host(L):
+    """Pool-slice sizes split each (v, q) over 4 lanes reduced through LDS in
+    the same workgroup (u_joint_fused_kernel): many workgroups, groups of
+    lanes whose digit ranges are uneven or empty (L = 5), against the host
+    path (separate partials + reduction)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    G, nq = 3, 50
+    rnd = random.Random(11)
+    base = _g2_points(7, 4)
+    pts = [base[rnd.randrange(7)] for _ in range(nq * L)]  # repeated points: doubling cases in the sums
+    V = bn.g2_aff_tensor(pts, "cpu")
+    ab = torch.tensor([[rnd.getrandbits(32), rnd.getrandbits(32)] for _ in range(G * nq * L)],
+                      dtype=torch.int64).to(torch.int32)
+    pad = nq + 3
+    outs = []
+    for dev in ("cpu", "cuda"):
+        out = torch.zeros((G * pad, 32), dtype=torch.int32, device=dev)
+        nt.rp_u_joint(nt.g2_joint_table(V.to(dev)), ab.to(dev), nq, G, L, out, pad)
+        outs.append(out.cpu())
+    assert torch.equal(outs[0], outs[1])
+
+
 @pytest.mark.parametrize("device", DEVICES)
 @pytest.mark.parametrize("c", [13, 4])
 def test_g2_msm_grouped(device, c):
