@@ -1286,15 +1286,12 @@ def _msm_queue(Y, V, ab_all, G: int, n: int, S: int, L: int, vstream=None, segs:
             table = nt.g2_joint_table(V)
     out = {"G": G}
     if dev.type == "cuda":
-        # DRYNX_UFOLD=coop: the three-lane fold at every size (A/B of the
-        # one-lane K-item accumulation the large batches use by default)
-        force_coop = os.environ.get("DRYNX_UFOLD", "auto") == "coop"
         if nseg == 1:
-            K = 1 if force_coop else fold_k(G * (nq + 1))
+            K = fold_k(G * (nq + 1))
             rows = 64 * K
             pad = -(-(nq + 1) // rows) * rows
         else:
-            K = 1 if force_coop else fold_k(G * nq)
+            K = fold_k(G * nq)
             rows = 64 * K
             ac = -(-cq // rows) * rows                              # segments start whole workgroups
             segbase = np.cumsum(ac) - ac
@@ -1303,7 +1300,8 @@ def _msm_queue(Y, V, ab_all, G: int, n: int, S: int, L: int, vstream=None, segs:
         # a small batch (a pool slice) folds on three lanes per item over the
         # raw line coefficients and affine points (-Y); a large one keeps the
         # one-lane accumulation over normalised lines and (x/y, 1/y) points
-        coop = K == 1 and (force_coop or G * pad <= _COOP_MAX_ITEMS)
+        # (the three-lane fold at the 1-GPU size: no faster, profiles/r6/ab/)
+        coop = K == 1 and G * pad <= _COOP_MAX_ITEMS
         Uall = torch.zeros((G * pad, 32), dtype=torch.int32, device=dev)
         UV = torch.zeros((period, 16), dtype=torch.int32, device=dev)
         pos = None
