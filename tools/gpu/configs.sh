@@ -1,7 +1,7 @@
 #!/bin/bash
-# BASELINE configs 2-4 and the 6-CN headline on the final tree.
+# BASELINE configs 2-4 and the 6-CN headline on a tree.
 set -o pipefail
-O=gpurun_out/r5cfg; mkdir -p $O
+O=gpurun_out/${CFG_OUT:-configs}; mkdir -p $O
 export HSA_ENABLE_IPC_MODE_LEGACY=0 TMPDIR=/tmp
 step() { local name=$1; shift; timeout -k 10 "$@" > $O/$name.log 2>&1; local rc=$?; tail -1 $O/$name.log | cut -c1-200; if [ $rc -ne 0 ]; then tail -30 $O/$name.log; exit $rc; fi; }
 step mean 300 python -u bench.py --query mean --steps 5 --warmup 2 --json-out $O/mean.json
