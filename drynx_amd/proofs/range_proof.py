@@ -954,22 +954,11 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
             else:
                 chk = ch_ok                    # a wrong challenge fails its own segment (attributed below)
     tabB = bn.base_table(device)
-    # --- shared, weight-free inputs
-    _sp = timers.span("rp.verify.inputs")
-    _sp.__enter__()
-    Cp = r.commit.C                                                    # C' = C + offset*B
-    if any(r.offset):
-        Cp = nt.g1_add(Cp, nt.g1_fb_mul_i64(tabB, bn.h2d(torch.tensor(r.offset, dtype=torch.int64), device)))
-    z = nt.fr_dot_rows(r.zphi, _powers(u, l, device), n, b_periodic=True)   # sum_j Zphi_j u^j
-    cols_t = bn.h2d(torch.tensor(r.cols, dtype=torch.long), device)
-    y_idx = (torch.arange(S, device=device).view(1, S) * sigmat.n_cols + cols_t.view(n, 1)).reshape(-1)
-    ytabs = sigmat.y_tables(device)
-    if ytabs is not None:                                              # c * y_i as fixed-base mults
-        Y = nt.g1_fb_mul_idx(ytabs[0], ytabs[1].index_select(0, y_idx).contiguous(), _rep(r.challenge, S))
-    else:
-        Y = nt.g1_mul(sigmat.y_jac.to(device).index_select(0, y_idx).contiguous(), _rep(r.challenge, S))  # [n*S]
-    _sp.__exit__(None, None, None)
-    # --- per-VN weights (each from its own coins): every VN's bucket plans in ONE host sync each
+    # --- per-VN weights (each from its own coins): every VN's bucket plans in
+    # ONE host sync each.  Drawn before the weight-free inputs: on a GPU the U
+    # combinations (queue stream) and the R MSM (aux stream) need only these
+    # and the joint tables, so both chains start before the host has issued
+    # the inputs' small launches (c y_i, sum Zphi u^j, C')
     G, m = n_vn, n * S * l
     cl = list(coins) if coins is not None else [None] * G
     cl += [None] * (G - len(cl))
@@ -1000,6 +989,7 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
     # one bad payload costs no second pass: the batch verdict IS the verdict
     # of the decodable segments
     masked = segs is not None
+    vm = None
     if masked:
         if ev_valid is not None:
             torch.cuda.current_stream(device).wait_event(ev_valid)
@@ -1010,8 +1000,6 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
         ab_all = (ab_all.view(G, m, 2) * mi).view(G * m, 2)
         rho_all = (rho_all.view(G, m, 8) * mi).view(G * m, 8)
         gam_all = (gam_all.view(G, m, 8) * mi).view(G * m, 8)
-        Y = Y.clone()
-        Y[:, 16:] *= vm.repeat_interleave(S).view(-1, 1)                # Z = 0: -c y_i at infinity
     _sw.__exit__(None, None, None)
     vns = [{"rho": rho_all[v * m:(v + 1) * m], "ab": ab_all[v * m:(v + 1) * m]} for v in range(G)]
     timers.count("rp.verify.items", G * m)
@@ -1019,33 +1007,69 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
     # windows by cost (nt.me_window): 16 bits for a 1-GPU inbox, 11 for a pool
     # slice; the host keeps bytes (fewer buckets for its serial products)
     wc_ = nt.me_window(me_groups) if device.type == "cuda" else (5, 8)
-    if not ddirect:
-        dpts = torch.cat([Cp.contiguous(), r.D.contiguous()]).repeat(G, 1)
-        wc = nt.fr_arith(nt.FR_MUL, w_all, r.challenge)
-        dsc = torch.stack([wc.view(G, n, 8), w_all.view(G, n, 8)], 1).reshape(-1, 8).contiguous()
     aux = _aux_stream(device) if device.type == "cuda" else None
     meta = (G, m, S, l, gb, tuple(wc_), _r_window(m, G))
-    # GPU: the U side first, on this stream (its chain of Miller-loop kernels
-    # is the critical path of a small batch), then the R MSM, the
-    # multi-exponentiation and the D-check on the aux stream.  (Launching the R
-    # MSM first measured neutral on the pool parts and +2.5 ms on the 1-GPU
-    # query: the two chains only slow each other down on the shared CUs.)
     ev_u = ev_r = None
     if aux is not None:
-        ready = torch.cuda.Event()
-        ready.record(torch.cuda.current_stream(device))
+        # the R MSM needs only V, Zphi and the weights: queued on the aux stream now
+        ready_w = torch.cuda.Event()
+        ready_w.record(torch.cuda.current_stream(device))
+        aux.wait_event(ready_w)
+        with timers.span("rp.verify.passes"), torch.cuda.stream(aux):
+            S_R, hR = _pass_r(r.V, r.zphi, rho_all, meta)
+            ev_r = torch.cuda.Event()                                   # the R MSM is queued
+            ev_r.record(aux)
+    # --- shared, weight-free inputs: the fold's points c y_i (on a GPU issued
+    # by _msm_queue after the U combinations, on the U stream), and C' and
+    # sum_j Zphi_j u^j for the D-check and the exponent sums (on the aux
+    # stream, before the multi-exponentiation: nothing there waits for the U side)
+    inp = {}
+
+    def _inputs():
+        with timers.span("rp.verify.inputs"):
+            cols_t = bn.h2d(torch.tensor(r.cols, dtype=torch.long), device)
+            y_idx = (torch.arange(S, device=device).view(1, S) * sigmat.n_cols + cols_t.view(n, 1)).reshape(-1)
+            ytabs = sigmat.y_tables(device)
+            if ytabs is not None:                                              # c * y_i as fixed-base mults
+                Y = nt.g1_fb_mul_idx(ytabs[0], ytabs[1].index_select(0, y_idx).contiguous(), _rep(r.challenge, S))
+            else:
+                Y = nt.g1_mul(sigmat.y_jac.to(device).index_select(0, y_idx).contiguous(),
+                              _rep(r.challenge, S))                             # [n*S]
+            if vm is not None:
+                Y = Y.clone()
+                Y[:, 16:] *= vm.repeat_interleave(S).view(-1, 1)                # Z = 0: -c y_i at infinity
+        inp["Y"] = Y
+        return Y
+
+    def _zcp():
+        Cp = r.commit.C                                                        # C' = C + offset*B
+        if any(r.offset):
+            Cp = nt.g1_add(Cp, nt.g1_fb_mul_i64(tabB, bn.h2d(torch.tensor(r.offset, dtype=torch.int64), device)))
+        return Cp, nt.fr_dot_rows(r.zphi, _powers(u, l, device), n, b_periodic=True)   # sum_j Zphi_j u^j
+
+    # GPU: the U side on this stream (its chain of Miller-loop kernels is the
+    # critical path of a small batch), the R MSM (above), the
+    # multi-exponentiation and the D-check on the aux stream.  (Launching the R
+    # MSM before the U side measured neutral on the pool parts and +2.5 ms on
+    # the 1-GPU query: the two chains only slow each other down on the shared
+    # CUs; here both are queued before the inputs.)
+    if aux is not None:
         with timers.span("rp.verify.msm_queue"):
-            msq = _msm_queue(Y, r.V, ab_all, G, n, S, l, vstream, segs, table)
+            msq = _msm_queue(_inputs, r.V, ab_all, G, n, S, l, vstream, segs, table)
             for v, uok in zip(vns, msq["u_ok"]):
                 v["u_ok"] = uok
         ev_u = torch.cuda.Event()                                       # the U side's fold is queued
         ev_u.record(torch.cuda.current_stream(device))
-        aux.wait_event(ready)
+    else:
+        _inputs()
     with timers.span("rp.verify.passes"), (torch.cuda.stream(aux) if aux is not None else _nullctx()):
-        S_R, hR = _pass_r(r.V, r.zphi, rho_all, meta)
-        if aux is not None:
-            ev_r = torch.cuda.Event()                                   # the R MSM is queued
-            ev_r.record(aux)
+        Cp, z = _zcp()
+        if not ddirect:
+            dpts = torch.cat([Cp.contiguous(), r.D.contiguous()]).repeat(G, 1)
+            wc = nt.fr_arith(nt.FR_MUL, w_all, r.challenge)
+            dsc = torch.stack([wc.view(G, n, 8), w_all.view(G, n, 8)], 1).reshape(-1, 8).contiguous()
+        if aux is None:
+            S_R, hR = _pass_r(r.V, r.zphi, rho_all, meta)
         A2, mexp, e_all, dfull = _pass_me(r.A, ab_all, gam_all, rho_all, r.zv, w_all, r.zr, z, meta)
         with timers.span("rp.run.D"):
             if ddirect:
@@ -1060,7 +1084,7 @@ def verify_range_proof_list_multi(r: RangeProofList, sigmat: SigMaterial, P_poin
             else:
                 dcheck = nt.g1_msm_device(dpts, dsc, n, ((n, 254),) * (2 * G))     # group = row // n
     if aux is None:  # host: the U side after the passes
-        msq = _msm_queue(Y, r.V, ab_all, G, n, S, l, None, segs)
+        msq = _msm_queue(inp["Y"], r.V, ab_all, G, n, S, l, None, segs)
         for v, uok in zip(vns, msq["u_ok"]):
             v["u_ok"] = uok
     useg = fR = None
@@ -1275,7 +1299,8 @@ def _msm_queue(Y, V, ab_all, G: int, n: int, S: int, L: int, vstream=None, segs:
     workgroup) that the normalised fold kernels pair with uv(-Y_q) -> per-
     workgroup partial products ("fb"), reduced per (VN, segment) by
     ``_seg_products``; host: per-item Miller loops over the same pairs.
-    "u_seg": [G, n_segments] exact G2 membership of every segment's U's."""
+    "u_seg": [G, n_segments] exact G2 membership of every segment's U's.
+    ``Y`` may be a callable returning it (issued after the U combinations)."""
     dev = V.device
     nq = n * S
     nseg = len(segs) if segs else 1
@@ -1312,21 +1337,6 @@ def _msm_queue(Y, V, ab_all, G: int, n: int, S: int, L: int, vstream=None, segs:
             qseg = np.repeat(np.arange(nseg), cq)
             qpos = segbase[qseg] + np.arange(nq) - qoff[:-1][qseg]
             pos = _h2d((np.arange(G).reshape(G, 1) * pad + qpos.reshape(1, nq)).reshape(-1).astype(np.int64), dev)
-        # the points of the fold (affine -Y_q, or uv(-Y_q) for the normalised
-        # lines) in place before the U combinations
-        if coop:  # affine -Y_q, the same for every VN
-            negY = nt.g1_to_affine(nt.g1_add(bn.g1_infinity_jac(nq, dev), Y.contiguous(), subtract=True))
-        elif nseg > 1:  # uv(-Y_q) is the same for every VN: computed once, copied per VN below
-            UVd = torch.zeros((nq + 1, 16), dtype=torch.int32, device=dev)
-            nt.rp_msm_uv(Y, UVd, nq, 1, nq + 1)
-            negY = UVd[:nq]
-        if nseg == 1:
-            if coop:
-                UV[: G * pad].view(G, pad, 16)[:, :nq] = negY
-            else:
-                nt.rp_msm_uv(Y, UV, nq, G, pad)
-        else:
-            UV.index_copy_(0, pos, negY.repeat(G, 1))
         with timers.span("rp.u.joint"):
             nt.rp_u_joint(table, ab_all, nq, G, L, Uall, pad, pos)
         # G2 membership of every U (exact test), on the validation stream beside the fold
@@ -1344,6 +1354,24 @@ def _msm_queue(Y, V, ab_all, G: int, n: int, S: int, L: int, vstream=None, segs:
         Uall.record_stream(vs)
         if pos is not None:
             pos.record_stream(vs)
+        # the points of the fold (affine -Y_q, or uv(-Y_q) for the normalised
+        # lines), after the U combinations are queued (``Y`` may be the
+        # callable that issues their inputs)
+        if callable(Y):
+            Y = Y()
+        if coop:  # affine -Y_q, the same for every VN
+            negY = nt.g1_to_affine(nt.g1_add(bn.g1_infinity_jac(nq, dev), Y.contiguous(), subtract=True))
+        elif nseg > 1:  # uv(-Y_q) is the same for every VN: computed once, copied per VN below
+            UVd = torch.zeros((nq + 1, 16), dtype=torch.int32, device=dev)
+            nt.rp_msm_uv(Y, UVd, nq, 1, nq + 1)
+            negY = UVd[:nq]
+        if nseg == 1:
+            if coop:
+                UV[: G * pad].view(G, pad, 16)[:, :nq] = negY
+            else:
+                nt.rp_msm_uv(Y, UV, nq, G, pad)
+        else:
+            UV.index_copy_(0, pos, negY.repeat(G, 1))
         with timers.span("rp.u.fold"):
             if coop:
                 out["fb"] = nt.rp_fold_accum_coop_raw(nt.rp_fold_coeffs(Uall), UV, Uall, period, 1)
@@ -1353,6 +1381,8 @@ def _msm_queue(Y, V, ab_all, G: int, n: int, S: int, L: int, vstream=None, segs:
         out["sb"] = [0] if nseg == 1 else (segbase // rows).tolist()
         out["nb"] = [pad // rows] if nseg == 1 else (ac // rows).tolist()
     else:
+        if callable(Y):
+            Y = Y()
         Uall = torch.zeros((G * nq, 32), dtype=torch.int32, device=dev)
         nt.rp_u_joint(table, ab_all, nq, G, L, Uall, nq)
         out["u_seg"] = _seg_all(nt.g2_subgroup(Uall).view(G, nq).bool(), cq, dev)
