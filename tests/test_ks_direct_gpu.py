@@ -39,3 +39,16 @@ def test_ks_direct_multi_and_blame(gpu_device):
                                 p.T1.cpu(), p.T2.cpu(), p.T3, p.c, p.za.cpu(), p.zb) for p in proofs]
     assert sigma.key_switch_batch_verification(cpu, 1.0, coins=Coins(os.urandom(32))) == [True, False, True]
     torch.cuda.synchronize()
+
+
+def test_ks_multi_fs_failure_reruns_live(gpu_device):
+    """The grouped MSM is queued over every proof while the transcript checks
+    run on a worker; a proof failing its Fiat-Shamir check is dropped and the
+    MSM runs again over the live ones (the others stay accepted)."""
+    from drynx_amd.crypto import oracle as O
+
+    proofs = _proofs(gpu_device)
+    proofs[2].c = (proofs[2].c + 1) % O.R
+    res = sigma.key_switch_batch_verification_multi(proofs, 1.0, [Coins(os.urandom(32)) for _ in range(3)])
+    assert res == [[True, True, False]] * 3
+    torch.cuda.synchronize()
