@@ -1236,12 +1236,38 @@ class _nullctx:
         return False
 
 
+_SHAPE_INDEX: dict = {}
+_SHAPE_INDEX_MAX = 16
+
+
+def _shape_index(key, device, fn, n: int) -> torch.Tensor:
+    """``fn(arange(n))`` -- an index that depends on the batch shape only
+    (item -> Zphi row, multi-exponentiation entry -> group) -- built once per
+    shape and device: a query's ~9M-entry arange and its elementwise glue ran
+    on every verification pass (profiles/r6/cost/span_kernels.txt).
+    Published (ready on every stream) when built; every reading stream is
+    recorded on it and the cache drains the device before it drops entries,
+    as the plan layouts and the key and signature caches do."""
+    k = (key, str(torch.device(device)))
+    t = _SHAPE_INDEX.get(k)
+    if t is None:
+        if len(_SHAPE_INDEX) >= _SHAPE_INDEX_MAX:
+            if torch.device(device).type == "cuda":
+                torch.cuda.synchronize(device)
+            _SHAPE_INDEX.clear()
+        t = _SHAPE_INDEX[k] = bn.publish(fn(torch.arange(n, device=device)).contiguous())
+    if t.is_cuda:
+        t.record_stream(torch.cuda.current_stream(t.device))  # a later drop waits for this reader
+    return t
+
+
 def _pass_r(V, zphi, rho, meta):
     """R = sum_it (rho_it Zphi_(p, j)) V_it per VN: the G2 Pippenger MSM with a
     device plan, queued on the current stream (no host sync) -> (S_R, hR)."""
     G, m, S, l, gb, wc, cR = meta
-    it = torch.arange(m, device=V.device)
-    s_r = nt.fr_arith(nt.FR_MUL, rho, zphi.index_select(0, (it // (S * l)) * l + it % l).contiguous())
+    zi = _shape_index(("zphi", m, S, l), V.device,
+                      lambda it: (it // (S * l)) * l + it % l, m)        # item -> its Zphi row
+    s_r = nt.fr_arith(nt.FR_MUL, rho, zphi.index_select(0, zi).contiguous())
     with timers.span("rp.run.R"):
         return nt.g2_msm_device(V, s_r, m, ((m, 254),) * G, c=cR)
 
@@ -1262,8 +1288,9 @@ def _pass_me(A, ab, gam, rho, zv, w, zr, z, meta):
     kr[:, :m, 0] = abv[:, :, 0]
     kr[:, m:, 0] = abv[:, :, 1]
     k[2 * G * m:] = gam
-    e = torch.arange(3 * G * m, device=dev)                          # entry -> group, elementwise only
-    mgrp = torch.where(e < 2 * G * m, e // (2 * m), G + (e - 2 * G * m) // m).to(torch.int32)
+    mgrp = _shape_index(("mgrp", G, m), dev,                         # entry -> group
+                        lambda e: torch.where(e < 2 * G * m, e // (2 * m), G + (e - 2 * G * m) // m).to(torch.int32),
+                        3 * G * m)
     with timers.span("rp.run.ME"):
         mexp = nt.multi_exp_device(A2, k, mgrp, ((2 * m, 32),) * G + ((m, gb),) * G, wc[0], wc[1],
                                    item_split=(2 * G * m, m))

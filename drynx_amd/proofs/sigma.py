@@ -657,30 +657,13 @@ def key_switch_batch_verification_multi(proofs: list, threshold: float, coins_li
     n_vn = len(coins_list)
     if not proofs:
         return [[] for _ in range(n_vn)]
-    every = [(i, pr, _first(pr.K.shape[0], threshold)) for i, pr in enumerate(proofs)]
-    every = [x for x in every if x[2] > 0]
-    pre = None
-    if every and proofs[0].K.device.type == "cuda":
-        # the transcript checks (digest launches + one copy, then host work)
-        # on a worker while this thread queues the grouped MSM over every
-        # proof -- the usual outcome; a proof failing its Fiat-Shamir check
-        # sends the MSM round again over the live ones below
-        fut = _fs_pool(proofs[0].K.device).submit(
-            lambda: _ks_fs_ok(proofs, n_vn) if n_vn > 1 else [_ks_fs_ok(proofs)])
-        with timers.span("ks.verify.msm_multi"):
-            pre = _ks_combined(every, n_vn, coins_list)
-        oks = fut.result()
-    else:
-        oks = _ks_fs_ok(proofs, n_vn) if n_vn > 1 else [_ks_fs_ok(proofs)]
+    oks = _ks_fs_ok(proofs, n_vn) if n_vn > 1 else [_ks_fs_ok(proofs)]
     lives = [[(i, pr, _first(pr.K.shape[0], threshold)) for i, pr in enumerate(proofs) if ok[i]] for ok in oks]
     lives = [[x for x in lv if x[2] > 0] for lv in lives]
     out = [list(ok) for ok in oks]
     if all(lv == lives[0] for lv in lives) and lives[0]:
-        if pre is not None and [x[0] for x in lives[0]] == [x[0] for x in every]:
-            verdicts = pre
-        else:
-            with timers.span("ks.verify.msm_multi"):
-                verdicts = _ks_combined(lives[0], n_vn, coins_list)
+        with timers.span("ks.verify.msm_multi"):
+            verdicts = _ks_combined(lives[0], n_vn, coins_list)
     else:
         verdicts = [(_ks_combined(lv, 1, [c])[0] if lv else True) for lv, c in zip(lives, coins_list)]
     for v in range(n_vn):
@@ -688,20 +671,6 @@ def key_switch_batch_verification_multi(proofs: list, threshold: float, coins_li
             for idx, pr, k in lives[v]:
                 out[v][idx] = _ks_combined([(idx, pr, k)], 1, [coins_list[v]])[0]
     return out
-
-
-_FS_POOLS: dict = {}
-
-
-def _fs_pool(device):
-    """One worker per device for the key-switch transcript checks (pinned to
-    the device: utils.streams.executor)."""
-    from ..utils import streams
-
-    key = str(device)
-    if key not in _FS_POOLS:
-        _FS_POOLS[key] = streams.executor(device, 1, "drynx-ks-fs")
-    return _FS_POOLS[key]
 
 
 def _ks_combined(live, n_vn: int = 1, coins=None):

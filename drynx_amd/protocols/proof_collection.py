@@ -686,17 +686,10 @@ def proof_collection(ctx, sq, local_requests: list, early: dict | None = None, l
 
         def checks(rs, range_pooled):
             if len(local_vns) > 1:  # co-hosted VNs: their signature checks in one host batch
-                # the envelopes' Schnorr checks (host batch, the GIL released in
-                # the native call) on a worker beside the grouped key-switch
-                # check: independent verdicts, both needed before the bitmaps
-                ex = getattr(ctx, "_sigcheck_exec", None)
-                if ex is None:
-                    ex = ctx._sigcheck_exec = streams.executor(ctx.device, 1, "drynx-sigcheck")
-                sf = ex.submit(prq.prewarm_signatures, rs, sq, local_vns, ctx.verifier_cache)
+                prq.prewarm_signatures(rs, sq, local_vns, ctx.verifier_cache)
                 with timers.span("verify.keyswitch.multi"):  # one grouped key-switch MSM for all of them
                     prq.prewarm_keyswitch(rs, sq, local_vns, ctx.device, ctx.verifier_cache,
                                           {v: ctx.vn_coins(v) for v in local_vns})
-                sf.result()
             return {vn.id: check_requests(ctx, sq, vn, idx, len(vns), rs, range_pooled)
                     for idx, vn in enumerate(vns) if vn.rank == ctx.rank}
 
