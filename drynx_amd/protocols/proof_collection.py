@@ -662,7 +662,7 @@ def early_plane_ok(ctx, sq) -> bool:
 
 
 LEDGER_PREFETCH = True  # A/B constants (tools/ab_patch.py --no-ledger-prefetch / --pool-priority)
-POOL_PRIORITY = 0
+POOL_PRIORITY = -1  # the U chain ahead of validation and ledger kernels (profiles/r6/pool_prio/)
 
 
 def proof_collection(ctx, sq, local_requests: list, early: dict | None = None, late=None):
