@@ -6,7 +6,7 @@ O=gpurun_out/${R6_OUT:-r6abtree}; mkdir -p $O
 export HSA_ENABLE_IPC_MODE_LEGACY=0 TMPDIR=/tmp
 R=$(pwd)
 step() { local name=$1; shift; timeout -k 10 "$@" > $R/$O/$name.log 2>&1; local rc=$?; tail -1 $R/$O/$name.log | cut -c1-160; if [ $rc -ne 0 ]; then tail -40 $R/$O/$name.log; exit $rc; fi; }
-step tests 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_rpmsm.py tests/test_range_hardening.py tests/test_gpu.py
+step tests 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_rpmsm.py tests/test_range_hardening.py tests/test_gpu.py tests/test_ledger_codec.py
 step new1 300 python -u bench.py --steps 10 --warmup 3 --json-out $O/new1.json
 (cd ab_base && step old1 300 python -u bench.py --steps 10 --warmup 3 --json-out $R/$O/old1.json) || exit 1
 step new2 300 python -u bench.py --steps 10 --warmup 3 --json-out $O/new2.json
