@@ -327,11 +327,6 @@ class DrynxNode:
         t_exec = timers.start_timer("JustExecution")
         if self.net is not None:
             self._net_dissemination(sq)
-        noise = cnp.dro_phase(self, sq, proofs)
-        if self.net is not None and noise is not None:
-            cns = [si.id for si in sq.RosterServers.list]
-            nb = int(sq.Query.DiffP.NoiseListSize) * 3 * CT_BYTES
-            self.net.step("dro", [(a, b, nb) for a, b in zip(cns, cns[1:] + cns[:1])], hops=flow_hops("dro", len(cns)))
         cn_sums, cn_inputs, dp_results = dcp.data_collection(self, sq)
         # range proofs start right after encoding (the reference fires them
         # asynchronously, data_collection_protocol.go:278-348): proving is queued
@@ -353,6 +348,16 @@ class DrynxNode:
                     range_future2.set_result([])
             else:
                 range_future = self._range_proofs_async(sq, dp_results)
+        # DRO noise shuffle: after the DPs' encoding and with their range
+        # proofs already queued, so its shuffles and shuffle proofs run beside
+        # the proving instead of before it (the reference runs the DRO phase in
+        # its own goroutine beside data collection and waits for it only before
+        # key switching, services/service.go:341-352, 733-736)
+        noise = cnp.dro_phase(self, sq, proofs)
+        if self.net is not None and noise is not None:
+            cns = [si.id for si in sq.RosterServers.list]
+            nb = int(sq.Query.DiffP.NoiseListSize) * 3 * CT_BYTES
+            self.net.step("dro", [(a, b, nb) for a, b in zip(cns, cns[1:] + cns[:1])], hops=flow_hops("dro", len(cns)))
         want = dcp.expected_n_out(sq)
         if dp_results:  # (a width that does not fit ``want`` aborted the route on every rank)
             n_out = len(next(iter(dp_results.values()))["cv"]) // n_groups

@@ -1,0 +1,12 @@
+#!/bin/bash
+# Same-box A/B of BASELINE config 4 (--query lr_dro, 10k noise list): working tree vs the ab_base/ snapshot.
+set -o pipefail
+O=gpurun_out/${R6_OUT:-r6abdro}; mkdir -p $O
+export HSA_ENABLE_IPC_MODE_LEGACY=0 TMPDIR=/tmp
+R=$(pwd)
+step() { local name=$1; shift; timeout -k 10 "$@" > $R/$O/$name.log 2>&1; local rc=$?; tail -1 $R/$O/$name.log | cut -c1-160; if [ $rc -ne 0 ]; then tail -40 $R/$O/$name.log; exit $rc; fi; }
+step tests 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu.py
+for k in 1 2; do
+  step new$k 300 python -u bench.py --query lr_dro ${DRO_ARGS:-} --steps 5 --warmup 2 --json-out $O/new$k.json
+  (cd ab_base && step old$k 300 python -u bench.py --query lr_dro ${DRO_ARGS:-} --steps 5 --warmup 2 --json-out $R/$O/old$k.json) || exit 1
+done
