@@ -20,6 +20,12 @@ def _free_port():
     return p
 
 
+def _diffp():
+    from drynx_amd.query import QueryDiffP
+
+    return QueryDiffP(LapMean=0.0, LapScale=1.0, NoiseListSize=40, Quanta=1.0, Scale=1.0, Limit=5.0)
+
+
 def _worker(rank, world, port, outdir):
     import json
 
@@ -36,7 +42,9 @@ def _worker(rank, world, port, outdir):
     cl, node = local_cluster(3, 4, 2, comm=comm, device="cpu", workdir=os.path.join(outdir, f"r{rank}"))
     out = {}
     for op, kw in [("sum", {}), ("variance", {}), ("frequencyCount", {}), ("sum", {"proofs": 1, "ranges": [16, 3]}),
-                   ("max", {"proofs": 1, "ranges": [2, 1], "obfuscation": True})]:
+                   ("max", {"proofs": 1, "ranges": [2, 1], "obfuscation": True}),
+                   # DRO noise list shuffled by CNs on both ranks, beside the range proving
+                   ("sum", {"proofs": 1, "ranges": [16, 3], "diffp": _diffp()})]:
         if rank == 0:
             client = DrynxClient(node)
             sq = make_survey(client, cl, op, query_min=0, query_max=4, rows=6, **kw)
@@ -62,7 +70,7 @@ def test_two_rank_gloo_surveys():
     o1 = json.load(open(os.path.join(outdir, "out1.json")))
     for k in o0:
         assert o0[k]["block"] == o1[k]["block"]
-    assert o0["sum3"]["codes"] == [1] and o0["max4"]["codes"] == [1]
+    assert o0["sum3"]["codes"] == [1] and o0["max4"]["codes"] == [1] and o0["sum5"]["codes"] == [1]
     assert o0["max4"]["vals"][0] <= 4.0
 
 
