@@ -651,10 +651,12 @@ def sampled_bounds(sq, n: int, part=None) -> tuple:
 # discount (a discount only lengthened the other parts: profiles/r5/it15,
 # pool(share) ~ 13 ms + 122 ms x share); a VN rank's part also carries the
 # digests of the other slices (a side stream: +2.2 ms of its part at equal
-# shares, profiles/r5/it16).  Refitted in round 6: at 0.14 the VN ranks'
-# parts still ended ~1.5 ms after the others' (29.9-31.0 vs 29.1-29.7 ms,
-# profiles/r6/final/), i.e. ~3.7 ms of extra work -> 0.22
-_POOL_DP_W, _POOL_VN_W = 0.0, 0.22
+# shares, profiles/r5/it16).  Round 6: 0.22 while the pool stream ran at
+# normal priority (the VN ranks' parts ended ~1.5 ms after the others',
+# profiles/r6/final/rank_share_w8_vnw014.json); with the pool stream at high
+# priority the digests cost less of the part and 0.14 balances again (same-box
+# A/B: projection 45.0-45.4 vs 45.8-46.2 ms at 0.22, profiles/r6/vnw_ab/)
+_POOL_DP_W, _POOL_VN_W = 0.0, 0.14
 
 
 def rank_weights(dps: list, vns: list) -> list:
